@@ -1,0 +1,194 @@
+/*
+ * kraken_hip.h -- C ABI of the MI355X-native blob-metainfo hot path.
+ *
+ * The drop-in boundary.  Plain pointers and sizes only (no torch types); all
+ * entry points are re-entrant and return KRK_OK (0) or a negative KRK_E*
+ * code, with a thread-local message from krk_last_error().  The Go wrappers
+ *  bind these through cgo and re-create the reference's exact
+ * error strings.  Each entry point names the reference interface it replaces.
+ *
+ * Device work runs on the calling thread's current device (krk_set_device);
+ * "stream" arguments are hipStream_t passed as void* (NULL = the library's
+ * own per-device stream).  *_dev entry points take device pointers and do no
+ * host<->device copies of bulk data; the host entry points stage through
+ * library-owned hipHostMalloc buffers with double-buffered hipMemcpyAsync.
+ */
+#ifndef KRAKEN_HIP_H
+#define KRAKEN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KRK_OK 0
+#define KRK_EINVAL (-1)    /* bad argument; e.g. "piece length must be positive" */
+#define KRK_EHIP (-2)      /* HIP runtime error (message has the hip error string) */
+#define KRK_ENOMEM (-3)    /* host or device allocation failed */
+#define KRK_ENODEV (-4)    /* no MI355X (gfx950) device visible */
+#define KRK_ERANGE (-5)    /* output capacity too small */
+#define KRK_EHEX (-6)      /* invalid hex key (hrw.Score returns NaN, rendezvous.go:154-157) */
+
+/* ---------------------------------------------------------------- runtime */
+const char* krk_version(void);
+const char* krk_last_error(void);            /* thread-local, never NULL */
+int krk_device_count(int* n);                /* gfx950 devices visible */
+int krk_set_device(int dev);                 /* per calling thread */
+int krk_synchronize(void);                   /* drain the library's streams on the current device */
+
+/* ------------------------------------------------- CRC-32/IEEE piece sums
+ * Replaces core.calcPieceSums (core/metainfo.go:158-179), the loop inside
+ * core.NewMetaInfo (core/metainfo.go:55-79); PieceHash() = crc32.NewIEEE()
+ * (core/piece_hash.go:22-24).  Pieces are [i*P, min((i+1)*P, L)), ceil(L/P)
+ * sums, none for L == 0, no empty trailing piece. */
+
+typedef struct krk_blob {
+    const uint8_t* data;     /* device pointer (any alignment; 16 B is the fast path) */
+    uint64_t length;         /* bytes */
+    int64_t piece_length;    /* > 0, else KRK_EINVAL "piece length must be positive" */
+    uint64_t sums_offset;    /* index of this blob's first sum in the sums array */
+} krk_blob;
+
+/* Number of piece sums for a blob: ceil(length / piece_length). */
+uint64_t krk_num_pieces(uint64_t length, int64_t piece_length);
+
+/* Device-resident batch: sums_dev (device, uint32) receives every blob's sums
+ * at blobs[i].sums_offset.  Asynchronous on `stream`. */
+int krk_piece_sums_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev, void* stream);
+
+/* Host batch (end-to-end): blobs[i].data are HOST pointers; sums_host receives
+ * the sums.  Streams bytes through pinned staging, overlapping H2D with the
+ * kernel.  Synchronous.  This is the batch form of Generator.Generate's
+ * NewMetaInfo call (lib/metainfogen/generator.go:41-58). */
+int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host);
+
+/* Streaming form for NewMetaInfo(d, io.Reader, P): the cgo shim copies each
+ * Read() chunk in with _update; CRC state is carried across chunk and piece
+ * boundaries on the device.  _end returns the io.CopyN-loop results. */
+typedef struct krk_piece_stream krk_piece_stream;
+int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out);
+int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* host_buf, uint64_t n);
+int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap,
+                         uint64_t* n_sums, uint64_t* length);
+void krk_piece_stream_free(krk_piece_stream* s);
+
+/* crc32.Update(crc, IEEETable, p) for one buffer (hash.Hash32 Write path used
+ * by agentstorage.Torrent.writePiece, lib/torrent/storage/agentstorage/torrent.go:175-199).
+ * data is a HOST pointer. */
+int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
+
+/* Batch piece verification (the same kernel in verify mode): ok_out[i] = 1 iff
+ * piece i of the blob matches expected[i].  data is a device pointer. */
+int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host,
+                          uint8_t* ok_out_host, void* stream);
+
+/* ----------------------------------------------------- SHA-256 (Digester)
+ * Replaces core.Digester (core/digester.go:28-72): crypto.SHA256 over the whole
+ * blob.  One Merkle-Damgard stream per lane, many blobs per launch. */
+
+/* Device-resident batch: data_dev[i] (device pointers, array itself on host),
+ * lengths[i]; digests_dev receives n*32 bytes (device). Asynchronous. */
+int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n,
+                   uint8_t* digests_dev, void* stream);
+
+/* Host batch: HOST data pointers; digests_host n*32 bytes.  Synchronous. */
+int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
+                    uint8_t* digests_host);
+
+/* Streaming Digester: _write may be called any number of times (io.Copy chunks);
+ * _sum does not reset (Digester.Digest(), digester.go:41-48) so writing may
+ * continue afterwards.  Concurrent digesters share launches. */
+typedef struct krk_digester krk_digester;
+int krk_digester_new(krk_digester** out);
+int krk_digester_write(krk_digester* d, const uint8_t* host_buf, uint64_t n);
+int krk_digester_sum(krk_digester* d, uint8_t out32[32]);
+void krk_digester_free(krk_digester* d);
+
+/* ----------------------------------------- metainfo + digest (batch)
+ * Both products for every blob in one call: the Digester SHA-256 of
+ * uploader.verify (origin/blobserver/uploader.go:74-94) and the piece sums of
+ * Generate (lib/metainfogen/generator.go:41-58).  The SHA and CRC kernels run
+ * concurrently on two internal streams joined back into `stream`.  Device
+ * pointers; asynchronous. */
+int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev,
+                            uint8_t* digests_dev, void* stream);
+
+/* ---------------------------------------------------- InfoHash (host CPU)
+ * info.Hash() (core/metainfo.go:37-44): SHA-1 over the bencoded
+ * info{PieceLength, PieceSums, Name, Length}.  bencode_out may be NULL. */
+int krk_info_hash(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
+                  const char* name, uint64_t name_len, int64_t length, uint8_t out20[20]);
+int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
+                     const char* name, uint64_t name_len, int64_t length,
+                     uint8_t* out, uint64_t cap, uint64_t* written);
+
+/* pieceLengthConfig.get (lib/metainfogen/config.go:71-80); thresholds ascending. */
+int64_t krk_piece_length_for_size(const int64_t* thresholds, const int64_t* lengths,
+                                  uint32_t n, int64_t size);
+
+/* -------------------------------------------------------- HRW placement
+ * Replaces hrw.RendezvousHash.GetOrderedNodes / RendezvousHashNode.Score
+ * (lib/hrw/rendezvous.go:151-217) with murmur3.New64 + UInt64ToFloat64
+ * (rendezvous.go:39,99-118), and hashring.ring.Locations (lib/hashring/ring.go:96-118).
+ * Keys are hex strings (hex-decoded, then key||label is hashed).  Order is
+ * descending score; exact ties go to the lower node index (the reference's
+ * tie order is unspecified: Go map order, ring.go:151). */
+
+typedef struct krk_nodes {
+    const char* labels;          /* concatenated label bytes */
+    const uint64_t* label_off;   /* n_nodes + 1 offsets into labels */
+    const int64_t* weights;      /* n_nodes (ring nodes use 100, ring.go:28) */
+    uint32_t n_nodes;
+} krk_nodes;
+
+/* keys: concatenated hex strings with key_off (n_keys+1).  order_out:
+ * n_keys * n_out node indices (-1 padded when n_out > n_nodes); scores_out
+ * (nullable): n_keys * n_nodes, in node order.  Returns KRK_EHEX if any key is
+ * not valid hex (its row is then filled from NaN scores: node order). */
+int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys,
+                    const krk_nodes* nodes, uint32_t n_out, int32_t* order_out,
+                    double* scores_out);
+
+/* ring.Locations for raw 32-byte sha256 digests (ShardID = first 2 bytes).
+ * healthy: n_nodes flags.  locs_out: n * max(1, max_replica) node indices
+ * (-1 padded); counts_out: n entries. */
+int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* nodes,
+                       const uint8_t* healthy, int32_t max_replica,
+                       int32_t* locs_out, uint8_t* counts_out);
+/* Device-resident form (digests/locs/counts are device pointers). */
+int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                           const uint8_t* healthy, int32_t max_replica,
+                           int32_t* locs_dev, uint8_t* counts_dev, void* stream);
+
+/* ----------------------------------------------------- synthetic blobs
+ * Fills a device buffer with bytes [offset, offset+n) of synthetic blob
+ * blob_idx (splitmix64 counter stream, variant 0 = uniform bytes, 1 = alnum;
+ * spec in DESIGN.md).  Benchmark/test data generator. */
+int krk_synth_fill_dev(uint8_t* dst_dev, uint64_t blob_idx, uint64_t offset, uint64_t n,
+                       int variant, void* stream);
+
+/* ------------------------------------------------ device memory helpers
+ * For callers (benchmarks, cgo) that do not own a device allocator. */
+int krk_dev_alloc(uint64_t bytes, void** out);
+int krk_dev_free(void* p);
+int krk_memcpy_h2d(void* dst_dev, const void* src_host, uint64_t n);
+int krk_memcpy_d2h(void* dst_host, const void* src_dev, uint64_t n);
+int krk_stream_create(void** out);
+int krk_stream_destroy(void* s);
+int krk_stream_sync(void* s);
+
+/* Kernel timing: when enabled, every kernel launch is bracketed by hipEvents
+ * recorded on the stream the kernel runs on; krk_kernel_stats returns the
+ * number of launches and their summed device time (ms) since the last reset
+ * for kernel name "crc32_pieces", "sha256_multi", "hrw_shard_table",
+ * "hrw_gather" or "synth_fill" (timed launches are synchronised lazily). */
+int krk_set_timing(int on);
+int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms);
+int krk_reset_kernel_stats(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KRAKEN_HIP_H */

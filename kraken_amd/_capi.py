@@ -1,0 +1,108 @@
+"""ctypes binding of libkraken_hip.so (include/kraken_hip.h).
+
+This is the Python-side FFI stub over the C ABI -- the same role the cgo stubs in
+INTEGRATION.md play for the reference's Go code.  There is no fallback: if the
+HIP library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkraken_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip.h")
+
+KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX = 0, -1, -2, -3, -4, -5, -6
+
+
+class KrakenError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class krk_blob(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("length", C.c_uint64), ("piece_length", C.c_int64),
+                ("sums_offset", C.c_uint64)]
+
+
+class krk_nodes(C.Structure):
+    _fields_ = [("labels", C.c_char_p), ("label_off", C.POINTER(C.c_uint64)),
+                ("weights", C.POINTER(C.c_int64)), ("n_nodes", C.c_uint32)]
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = C.CDLL(LIB_PATH)
+    vp, u8p, u32p, u64p, i32p, i64p, f64p = (C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint32),
+                                              C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
+                                              C.POINTER(C.c_int64), C.POINTER(C.c_double))
+    blobp, nodesp = C.POINTER(krk_blob), C.POINTER(krk_nodes)
+    i = C.c_int
+    sig = {
+        "krk_version": (C.c_char_p, []),
+        "krk_last_error": (C.c_char_p, []),
+        "krk_device_count": (i, [C.POINTER(C.c_int)]),
+        "krk_set_device": (i, [i]),
+        "krk_synchronize": (i, []),
+        "krk_num_pieces": (C.c_uint64, [C.c_uint64, C.c_int64]),
+        "krk_piece_sums_dev": (i, [blobp, C.c_uint64, vp, vp]),
+        "krk_piece_sums_host": (i, [blobp, C.c_uint64, u32p]),
+        "krk_piece_stream_begin": (i, [C.c_int64, C.POINTER(vp)]),
+        "krk_piece_stream_update": (i, [vp, vp, C.c_uint64]),
+        "krk_piece_stream_end": (i, [vp, u32p, C.c_uint64, u64p, u64p]),
+        "krk_piece_stream_free": (None, [vp]),
+        "krk_crc32_update": (i, [C.c_uint32, vp, C.c_uint64, u32p]),
+        "krk_verify_pieces_dev": (i, [blobp, u32p, u8p, vp]),
+        "krk_sha256_dev": (i, [C.POINTER(vp), u64p, C.c_uint64, vp, vp]),
+        "krk_sha256_host": (i, [C.POINTER(vp), u64p, C.c_uint64, u8p]),
+        "krk_digester_new": (i, [C.POINTER(vp)]),
+        "krk_digester_write": (i, [vp, vp, C.c_uint64]),
+        "krk_digester_sum": (i, [vp, u8p]),
+        "krk_digester_free": (None, [vp]),
+        "krk_metainfo_digest_dev": (i, [blobp, C.c_uint64, vp, vp, vp]),
+        "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),
+        "krk_bencode_info": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p,
+                                 C.c_uint64, u64p]),
+        "krk_piece_length_for_size": (C.c_int64, [i64p, i64p, C.c_uint32, C.c_int64]),
+        "krk_hrw_ordered": (i, [C.c_char_p, u64p, C.c_uint64, nodesp, C.c_uint32, i32p, f64p]),
+        "krk_ring_locations": (i, [u8p, C.c_uint64, nodesp, u8p, C.c_int32, i32p, u8p]),
+        "krk_ring_locations_dev": (i, [vp, C.c_uint64, nodesp, u8p, C.c_int32, vp, vp, vp]),
+        "krk_synth_fill_dev": (i, [vp, C.c_uint64, C.c_uint64, C.c_uint64, i, vp]),
+        "krk_dev_alloc": (i, [C.c_uint64, C.POINTER(vp)]),
+        "krk_dev_free": (i, [vp]),
+        "krk_memcpy_h2d": (i, [vp, vp, C.c_uint64]),
+        "krk_memcpy_d2h": (i, [vp, vp, C.c_uint64]),
+        "krk_stream_create": (i, [C.POINTER(vp)]),
+        "krk_stream_destroy": (i, [vp]),
+        "krk_stream_sync": (i, [vp]),
+        "krk_set_timing": (i, [i]),
+        "krk_kernel_stats": (i, [C.c_char_p, u64p, f64p]),
+        "krk_reset_kernel_stats": (i, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    lib._krk_sigs = sig  # for tests: the bound surface
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int) -> int:
+    if rc != KRK_OK:
+        raise KrakenError(rc, lib.krk_last_error().decode(errors="replace"))
+    return rc
+
+
+def declared_symbols() -> list[str]:
+    """Every krk_* function declared in include/kraken_hip.h."""
+    import re
+    src = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(krk_[a-z0-9_]+)\s*\(", src)))

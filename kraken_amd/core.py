@@ -1,0 +1,363 @@
+"""Host-side mirror of the reference's `core` package over the C ABI.
+
+Names, argument meaning and error strings follow the Go API so callers (and the
+parity tests) read like the reference:
+
+* ``PieceHash``           core/piece_hash.go:21-24
+* ``NewMetaInfo``         core/metainfo.go:53-79 (+ calcPieceSums :157-179)
+* ``MetaInfo`` accessors  core/metainfo.go:81-155
+* ``Digester``            core/digester.go:28-72
+* ``Digest``              core/digest.go:51-161
+* ``InfoHash``            core/infohash.go:25-60
+
+All bulk arithmetic (piece CRCs, SHA-256) runs in libkraken_hip on the GPU; the
+O(pieces) bencode + SHA-1 InfoHash runs in the same library's host code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import io
+import json
+import re
+
+import numpy as np
+
+from ._capi import KrakenError, check, krk_blob, lib
+
+SHA256 = "sha256"
+DigestEmptyTar = "sha256:e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+_COPY_BUF = 32 * 1024  # io.Copy's buffer: the Go reader granularity
+
+_HEX = re.compile(r"^[0-9a-fA-F]*$")
+
+
+# ---------------------------------------------------------------- Digest
+
+def ValidateSHA256(s: str) -> None:
+    """core/digest.go:152-161."""
+    if len(s) != 64:
+        raise ValueError(f"expected 64 characters, got {len(s)} from {s!r}")
+    if not _HEX.match(s):
+        raise ValueError("hex: invalid byte")
+
+
+class Digest:
+    __slots__ = ("_algo", "_hex", "_raw")
+
+    def __init__(self, algo: str = "", hex_: str = "", raw: str = ""):
+        self._algo, self._hex, self._raw = algo, hex_, raw
+
+    def Algo(self) -> str:
+        return self._algo
+
+    def Hex(self) -> str:
+        return self._hex
+
+    def String(self) -> str:
+        return self._raw
+
+    __str__ = String
+
+    def ShardID(self) -> str:
+        """core/digest.go:148-150: the first 4 hex characters."""
+        return self._hex[:4]
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, Digest) and (self._algo, self._hex, self._raw) == (
+            other._algo, other._hex, other._raw)
+
+    def __hash__(self) -> int:
+        return hash(self._raw)
+
+    def __repr__(self) -> str:
+        return f"Digest({self._raw!r})"
+
+
+def NewSHA256DigestFromHex(hex_: str) -> Digest:
+    """core/digest.go:59-68."""
+    try:
+        ValidateSHA256(hex_)
+    except ValueError as e:
+        raise ValueError(f"invalid sha256: {e}") from None
+    return Digest(SHA256, hex_, f"{SHA256}:{hex_}")
+
+
+def ParseSHA256Digest(raw: str) -> Digest:
+    """core/digest.go:72-93."""
+    if raw == "":
+        raise ValueError("invalid digest: empty")
+    parts = raw.split(":")
+    if len(parts) != 2:
+        raise ValueError("invalid digest: expected '<algo>:<hex>'")
+    if parts[0] != SHA256:
+        raise ValueError("invalid digest algo: expected sha256")
+    try:
+        ValidateSHA256(parts[1])
+    except ValueError as e:
+        raise ValueError(f"invalid sha256: {e}") from None
+    return Digest(parts[0], parts[1], raw)
+
+
+class Digester:
+    """core.Digester: streaming SHA-256 on the GPU (one Merkle-Damgard stream per
+    lane).  Digest() does not reset, exactly like hash.Hash.Sum."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        check(lib.krk_digester_new(C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.krk_digester_free(h)
+            self._h = None
+
+    def _write(self, p) -> int:
+        b = _as_bytes(p)
+        if b.nbytes:
+            check(lib.krk_digester_write(self._h, b.ctypes.data, b.nbytes))
+        return b.nbytes
+
+    def Digest(self) -> Digest:
+        out = (C.c_uint8 * 32)()
+        check(lib.krk_digester_sum(self._h, out))
+        return NewSHA256DigestFromHex(bytes(out).hex())
+
+    def FromReader(self, rd) -> Digest:
+        while True:
+            chunk = rd.read(_COPY_BUF)
+            if not chunk:
+                break
+            self._write(chunk)
+        return self.Digest()
+
+    def FromBytes(self, p) -> Digest:
+        self._write(p)
+        return self.Digest()
+
+    def Tee(self, r):
+        return _TeeReader(r, self)
+
+
+def NewDigester() -> Digester:
+    return Digester()
+
+
+class _TeeReader(io.RawIOBase):
+    def __init__(self, r, d: Digester):
+        self._r, self._d = r, d
+
+    def readable(self):
+        return True
+
+    def read(self, n=-1):
+        b = self._r.read(n)
+        if b:
+            self._d._write(b)
+        return b
+
+    def readinto(self, buf):
+        b = self.read(len(buf))
+        buf[: len(b)] = b
+        return len(b)
+
+
+# ---------------------------------------------------------------- InfoHash
+
+class InfoHash(bytes):
+    def Hex(self) -> str:
+        return self.hex()
+
+    def Bytes(self) -> bytes:
+        return bytes(self)
+
+    def String(self) -> str:
+        return self.hex()
+
+
+def NewInfoHashFromHex(s: str) -> InfoHash:
+    """core/infohash.go:29-40."""
+    if len(s) != 40:
+        raise ValueError(f"invalid hash: expected 40 characters, got {len(s)}")
+    try:
+        return InfoHash(bytes.fromhex(s))
+    except ValueError as e:
+        raise ValueError(f"invalid hex: {e}") from None
+
+
+def _info_hash(piece_length: int, sums: np.ndarray, name: str, length: int) -> InfoHash:
+    s = np.ascontiguousarray(sums, dtype=np.uint32)
+    out = (C.c_uint8 * 20)()
+    nb = name.encode()
+    sp = s.ctypes.data_as(C.POINTER(C.c_uint32)) if s.size else None
+    check(lib.krk_info_hash(piece_length, sp, s.size, nb, len(nb), length, out))
+    return InfoHash(bytes(out))
+
+
+# ---------------------------------------------------------------- MetaInfo
+
+class MetaInfo:
+    """core.MetaInfo (core/metainfo.go:46-155)."""
+
+    def __init__(self, piece_length: int, piece_sums: np.ndarray | None, name: str, length: int,
+                 digest: Digest, info_hash: InfoHash):
+        self._pl = int(piece_length)
+        self._sums = None if piece_sums is None else np.asarray(piece_sums, dtype=np.uint32)
+        self._name = name
+        self._len = int(length)
+        self._digest = digest
+        self._ih = info_hash
+
+    def InfoHash(self) -> InfoHash:
+        return self._ih
+
+    def Digest(self) -> Digest:
+        return self._digest
+
+    def Length(self) -> int:
+        return self._len
+
+    def NumPieces(self) -> int:
+        return 0 if self._sums is None else int(self._sums.size)
+
+    def PieceLength(self) -> int:
+        return self._pl
+
+    def GetPieceLength(self, i: int) -> int:
+        """core/metainfo.go:108-118."""
+        n = self.NumPieces()
+        if i < 0 or i >= n:
+            return 0
+        if i == n - 1:
+            return self._len - self._pl * i
+        return self._pl
+
+    def GetPieceSum(self, i: int) -> int:
+        return int(self._sums[i])
+
+    def PieceSums(self) -> np.ndarray:
+        return np.zeros(0, dtype=np.uint32) if self._sums is None else self._sums
+
+    def Serialize(self) -> bytes:
+        """core/metainfo.go:131-134: json of {"Info": info} (field order as declared)."""
+        sums = None if self._sums is None else [int(x) for x in self._sums]
+        obj = {"Info": {"PieceLength": self._pl, "PieceSums": sums, "Name": self._name,
+                        "Length": self._len}}
+        return json.dumps(obj, separators=(",", ":")).encode()
+
+
+def DeserializeMetaInfo(data: bytes) -> MetaInfo:
+    """core/metainfo.go:136-155."""
+    try:
+        j = json.loads(data)
+        info = j["Info"]
+    except (ValueError, KeyError, TypeError) as e:
+        raise ValueError(f"json: {e}") from None
+    sums = info.get("PieceSums")
+    arr = None if sums is None else np.asarray(sums, dtype=np.uint32)
+    ih = _info_hash(int(info["PieceLength"]), arr if arr is not None else np.zeros(0, np.uint32),
+                    info["Name"], int(info["Length"]))
+    try:
+        d = NewSHA256DigestFromHex(info["Name"])
+    except ValueError as e:
+        raise ValueError(f"parse name: {e}") from None
+    return MetaInfo(int(info["PieceLength"]), arr, info["Name"], int(info["Length"]), d, ih)
+
+
+def _as_bytes(p) -> np.ndarray:
+    if isinstance(p, np.ndarray):
+        return np.ascontiguousarray(p).view(np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(p).cast("B"), dtype=np.uint8)
+
+
+def _reader(blob):
+    if isinstance(blob, (bytes, bytearray, memoryview, np.ndarray)):
+        return io.BytesIO(_as_bytes(blob).tobytes())
+    return blob
+
+
+def calcPieceSums(blob, piece_length: int):
+    """core.calcPieceSums (core/metainfo.go:157-179) on the GPU: the reader is
+    copied through the C ABI's streaming piece API in io.Copy-sized chunks; CRC
+    state crosses chunk and piece boundaries on the device."""
+    if piece_length <= 0:
+        raise ValueError("piece length must be positive")
+    rd = _reader(blob)
+    h = C.c_void_p()
+    check(lib.krk_piece_stream_begin(piece_length, C.byref(h)))
+    try:
+        while True:
+            try:
+                chunk = rd.read(_COPY_BUF)
+            except Exception as e:  # io error -> "read blob: %s"
+                raise IOError(f"read blob: {e}") from None
+            if not chunk:
+                break
+            b = _as_bytes(chunk)
+            check(lib.krk_piece_stream_update(h, b.ctypes.data, b.nbytes))
+        n = C.c_uint64()
+        ln = C.c_uint64()
+        check(lib.krk_piece_stream_end(h, None, 0, C.byref(n), C.byref(ln)))
+        sums = np.zeros(max(n.value, 1), dtype=np.uint32)
+        check(lib.krk_piece_stream_end(h, sums.ctypes.data_as(C.POINTER(C.c_uint32)), n.value,
+                                       C.byref(n), C.byref(ln)))
+        return ln.value, (sums[: n.value] if n.value else None)
+    finally:
+        lib.krk_piece_stream_free(h)
+
+
+def NewMetaInfo(d: Digest, blob, piece_length: int) -> MetaInfo:
+    """core.NewMetaInfo (core/metainfo.go:53-79).  Assumes d is the valid digest."""
+    length, sums = calcPieceSums(blob, piece_length)
+    ih = _info_hash(piece_length, sums if sums is not None else np.zeros(0, np.uint32), d.Hex(), length)
+    return MetaInfo(piece_length, sums, d.Hex(), length, d, ih)
+
+
+class _PieceHash32:
+    """hash.Hash32 returned by PieceHash(): crc32.NewIEEE semantics; Sum32 runs the
+    GPU kernel over the bytes written since the last Sum32 (state carried)."""
+
+    def __init__(self):
+        self._crc = 0
+        self._pending: list[bytes] = []
+
+    def Write(self, p) -> int:
+        b = bytes(_as_bytes(p))
+        self._pending.append(b)
+        return len(b)
+
+    def _fold(self):
+        if self._pending:
+            buf = np.frombuffer(b"".join(self._pending), dtype=np.uint8)
+            self._pending = []
+            out = C.c_uint32()
+            check(lib.krk_crc32_update(self._crc, buf.ctypes.data if buf.size else None, buf.size,
+                                       C.byref(out)))
+            self._crc = out.value
+
+    def Sum32(self) -> int:
+        self._fold()
+        return self._crc
+
+    def Sum(self, b: bytes = b"") -> bytes:
+        return bytes(b) + self.Sum32().to_bytes(4, "big")
+
+    def Reset(self):
+        self._crc, self._pending = 0, []
+
+    def Size(self) -> int:
+        return 4
+
+    def BlockSize(self) -> int:
+        return 1
+
+
+def PieceHash() -> _PieceHash32:
+    return _PieceHash32()
+
+
+__all__ = ["Digest", "Digester", "NewDigester", "NewSHA256DigestFromHex", "ParseSHA256Digest",
+           "ValidateSHA256", "InfoHash", "NewInfoHashFromHex", "MetaInfo", "NewMetaInfo",
+           "DeserializeMetaInfo", "PieceHash", "calcPieceSums", "DigestEmptyTar", "KrakenError",
+           "krk_blob"]

@@ -1,0 +1,99 @@
+// kernels.hpp -- device work descriptors and kernel launchers (implemented in *.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace krk {
+
+// ---------------------------------------------------------------- CRC pieces
+// One work item = a contiguous byte run inside ONE piece, processed by one wave.
+// Its raw CRC is shifted to the piece end (mul = x^(8*(piece_end - item_end))) and
+// XOR-ed into sums[out]; the piece's first item also carries the init/xorout term
+// xr = shift(~0, piece_len) ^ ~0.  XOR is order-free, so items of one piece may run
+// on any wave, XCD or launch.
+struct alignas(16) CrcItem {
+    uint64_t ptr;   // device address of the run
+    uint32_t len;   // bytes, 1 .. kItemBytes
+    uint32_t out;   // index into sums[]
+    uint32_t mul;
+    uint32_t xr;
+    uint32_t pad[2];
+};
+static_assert(sizeof(CrcItem) == 32, "CrcItem layout");
+
+constexpr uint32_t kSeg = 64;                // bytes per lane per wave step
+constexpr uint32_t kStep = 64 * kSeg;        // bytes per wave step (4 KiB)
+constexpr uint32_t kGap = kStep - kSeg;      // zero-gap between a lane's segments
+constexpr uint32_t kItemBytes = 256 * 1024;  // max bytes per work item
+
+// Global constant table layout (uint32 words).
+constexpr int kTabT = 0;        // T0..T3 slicing tables, 1024 words
+constexpr int kTabG = 1024;     // G0..G3 shift-by-kGap tables, 1024 words
+constexpr int kTabLaneMul = 2048;  // 64 words: x^(8*(63-l)*kSeg)
+constexpr int kTabX8Pow = 2112;    // 64 words: x^(8*2^k)
+constexpr int kTabWords = 2176;
+
+struct CrcLaunchCfg {
+    int cus;           // compute units
+    int variant;       // 0 = R16 (2 blocks/CU), 1 = R32 (1 block/CU)
+};
+
+hipError_t launch_crc_items(const CrcItem* items, uint32_t n_items, const uint32_t* tabs,
+                            uint32_t* sums, const CrcLaunchCfg& cfg, hipStream_t s);
+
+// Piece verification: ok[i] = (sums[i] == expected[i]).
+hipError_t launch_crc_verify(const uint32_t* sums, const uint32_t* expected, uint8_t* ok,
+                             uint32_t n, hipStream_t s);
+
+// ---------------------------------------------------------------- SHA-256
+// One job = one Merkle-Damgard stream, run by one lane.  Processes len bytes
+// starting from midstate h (or from out_state + 8*out when kShaFromState); if
+// kShaFinal, pads with total = prefix + len bytes and writes the big-endian digest
+// to out_digest + 32*out, else writes the midstate (len must then be a multiple of
+// 64) to out_state + 8*out.
+constexpr uint32_t kShaFinal = 1;
+constexpr uint32_t kShaFromState = 2;
+struct alignas(16) ShaJob {
+    uint64_t ptr;
+    uint64_t len;
+    uint64_t prefix;   // bytes absorbed before this job (for the length field)
+    uint32_t out;
+    uint32_t flags;
+    uint32_t h[8];
+};
+static_assert(sizeof(ShaJob) == 64, "ShaJob layout");
+
+hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
+                         uint32_t* out_state, hipStream_t s);
+
+// ---------------------------------------------------------------- HRW
+// Scores for (key, node) pairs and the per-key descending order.
+struct HrwArgs {
+    const uint8_t* keys;      // decoded key bytes
+    const uint64_t* key_off;  // n_keys + 1
+    uint64_t n_keys;
+    const uint8_t* labels;
+    const uint64_t* label_off;  // n_nodes + 1
+    const int64_t* weights;
+    uint32_t n_nodes;
+    uint32_t n_out;
+    const uint8_t* key_bad;   // n_keys flags: invalid hex -> NaN scores
+    int32_t* order;           // n_keys * n_out
+    double* scores;           // nullable: n_keys * n_nodes
+};
+hipError_t launch_hrw_order(const HrwArgs& a, hipStream_t s);
+
+// Locations filter over full orders (n_out == n_nodes rows).
+hipError_t launch_ring_filter(const int32_t* order, uint64_t n_rows, uint32_t n_nodes,
+                              const uint8_t* healthy, int32_t max_replica, uint32_t row_out,
+                              int32_t* locs, uint8_t* counts, hipStream_t s);
+// Per-digest gather from the 65,536-row shard table.
+hipError_t launch_shard_gather(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
+                               const uint8_t* table_counts, uint32_t row_out, int32_t* locs,
+                               uint8_t* counts, hipStream_t s);
+
+// ---------------------------------------------------------------- synthetic data
+hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n,
+                             int variant, hipStream_t s);
+
+}  // namespace krk

@@ -1,0 +1,1201 @@
+// runtime.cpp -- the C ABI (include/kraken_hip.h): device contexts, work
+// descriptor builders, pinned staging pipelines and kernel launches.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kraken_hip.h"
+#include "crc_math.hpp"
+#include "kernels.hpp"
+
+namespace krk {
+
+// ------------------------------------------------------------------ errors
+thread_local std::string t_err;
+thread_local int t_dev = 0;
+
+void set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    (void)code;
+    t_err = buf;
+}
+
+#define KRK_HIP(expr)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            set_error(KRK_EHIP, "%s: %s", #expr, hipGetErrorString(e_));              \
+            return KRK_EHIP;                                                          \
+        }                                                                             \
+    } while (0)
+
+#define KRK_CHECK(cond, code, ...)        \
+    do {                                  \
+        if (!(cond)) {                    \
+            set_error(code, __VA_ARGS__); \
+            return code;                  \
+        }                                 \
+    } while (0)
+
+// ------------------------------------------------------------------ timing
+enum Kern { K_CRC, K_SHA, K_HRW, K_FILTER, K_GATHER, K_SYNTH, K_N };
+static const char* kKernNames[K_N] = {"crc32_pieces", "sha256_multi", "hrw_order",
+                                      "ring_filter",  "hrw_gather",   "synth_fill"};
+static std::atomic<bool> g_timing{false};
+struct Pending {
+    hipEvent_t a, b;
+    int k, dev;
+};
+static std::mutex g_tmu;
+static std::vector<Pending> g_pending;
+static double g_ms[K_N];
+static uint64_t g_cnt[K_N];
+
+template <class F>
+static hipError_t timed(int k, hipStream_t s, F&& f) {
+    if (!g_timing.load(std::memory_order_relaxed)) return f();
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, s);
+    hipError_t e = f();
+    hipEventRecord(b, s);
+    std::lock_guard<std::mutex> g(g_tmu);
+    g_pending.push_back({a, b, k, t_dev});
+    return e;
+}
+
+static void drain_timing() {
+    std::lock_guard<std::mutex> g(g_tmu);
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (auto& p : g_pending) {
+        hipSetDevice(p.dev);
+        hipEventSynchronize(p.b);
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            g_ms[p.k] += ms;
+            g_cnt[p.k] += 1;
+        }
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    g_pending.clear();
+    hipSetDevice(cur);
+}
+
+// ------------------------------------------------------------------ device
+struct PinnedSlot {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool busy = false;
+};
+
+struct Device {
+    int id = 0;
+    int cus = 0;
+    hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
+    uint32_t* d_tabs = nullptr;
+    int crc_variant = 0;
+    std::mutex mu;
+    PinnedSlot slots[8];
+    unsigned next_slot = 0;
+};
+
+static std::mutex g_dmu;
+static std::vector<std::unique_ptr<Device>> g_devs;
+static X8Pow g_x8;
+static std::once_flag g_x8_once;
+
+static const X8Pow& x8() {
+    std::call_once(g_x8_once, [] { g_x8 = make_x8pow(); });
+    return g_x8;
+}
+
+static int init_device(Device& D, int id) {
+    D.id = id;
+    KRK_HIP(hipSetDevice(id));
+    hipDeviceProp_t prop;
+    KRK_HIP(hipGetDeviceProperties(&prop, id));
+    KRK_CHECK(strncmp(prop.gcnArchName, "gfx950", 6) == 0, KRK_ENODEV,
+              "device %d is %s, this build targets gfx950 (MI355X)", id, prop.gcnArchName);
+    D.cus = prop.multiProcessorCount;
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_main, hipStreamNonBlocking));
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
+    std::vector<uint32_t> tabs(kTabWords);
+    make_slice_tables(tabs.data() + kTabT);
+    const X8Pow& xp = x8();
+    make_shift_tables(tabs.data() + kTabG, x8n(kGap, xp.v));
+    for (int l = 0; l < 64; ++l) tabs[kTabLaneMul + l] = x8n(uint64_t(63 - l) * kSeg, xp.v);
+    for (int k = 0; k < 64; ++k) tabs[kTabX8Pow + k] = xp.v[k];
+    KRK_HIP(hipMalloc(&D.d_tabs, kTabWords * 4));
+    KRK_HIP(hipMemcpy(D.d_tabs, tabs.data(), kTabWords * 4, hipMemcpyHostToDevice));
+    const char* v = getenv("KRK_CRC_VARIANT");
+    D.crc_variant = v ? atoi(v) : 0;
+    return KRK_OK;
+}
+
+static Device* device(int* rc) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error(KRK_ENODEV, "no HIP device visible");
+        *rc = KRK_ENODEV;
+        return nullptr;
+    }
+    if (t_dev < 0 || t_dev >= n) {
+        set_error(KRK_ENODEV, "device %d out of range (%d visible)", t_dev, n);
+        *rc = KRK_ENODEV;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_dmu);
+    if ((int)g_devs.size() < n) g_devs.resize(n);
+    if (!g_devs[t_dev]) {
+        auto D = std::make_unique<Device>();
+        int r = init_device(*D, t_dev);
+        if (r != KRK_OK) {
+            *rc = r;
+            return nullptr;
+        }
+        g_devs[t_dev] = std::move(D);
+    }
+    if (hipSetDevice(t_dev) != hipSuccess) {
+        set_error(KRK_EHIP, "hipSetDevice(%d) failed", t_dev);
+        *rc = KRK_EHIP;
+        return nullptr;
+    }
+    *rc = KRK_OK;
+    return g_devs[t_dev].get();
+}
+
+#define KRK_DEVICE(D)         \
+    int rc_ = KRK_OK;         \
+    Device* D = device(&rc_); \
+    if (!D) return rc_;
+
+static hipStream_t pick(Device* D, void* s) { return s ? static_cast<hipStream_t>(s) : D->s_main; }
+
+// Stage `n` host bytes through a pinned slot into a fresh stream-ordered device
+// allocation (freed with hipFreeAsync by the caller).
+static int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_t s) {
+    *d_out = nullptr;
+    if (!n) return KRK_OK;
+    KRK_HIP(hipMallocAsync(d_out, n, s));
+    std::lock_guard<std::mutex> g(D->mu);
+    PinnedSlot& P = D->slots[D->next_slot++ % 8];
+    if (P.busy) {
+        KRK_HIP(hipEventSynchronize(P.ev));
+        P.busy = false;
+    }
+    if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
+    if (P.cap < n) {
+        if (P.p) hipHostFree(P.p);
+        P.cap = std::max<size_t>(n, 1 << 20);
+        KRK_HIP(hipHostMalloc(&P.p, P.cap, hipHostMallocDefault));
+    }
+    memcpy(P.p, src, n);
+    KRK_HIP(hipMemcpyAsync(*d_out, P.p, n, hipMemcpyHostToDevice, s));
+    KRK_HIP(hipEventRecord(P.ev, s));
+    P.busy = true;
+    return KRK_OK;
+}
+
+// ------------------------------------------------------------------ CRC items
+// Items for bytes [a, b) of one blob (length L, pieces of P bytes), where blob byte
+// `a` lives at device address `base`.  `seed` is the register the IEEE CRC starts
+// from (~crc of crc32.Update; ~0 for PieceHash()).
+struct ItemBuilder {
+    std::unordered_map<uint64_t, uint32_t> cache;
+    struct Pattern {
+        std::vector<CrcItem> items;  // for one full piece starting at offset 0
+    };
+    std::unordered_map<uint64_t, Pattern> full;
+
+    uint32_t X(uint64_t n) {
+        if (n == 0) return kOne;
+        auto it = cache.find(n);
+        if (it != cache.end()) return it->second;
+        const uint32_t v = x8n(n, x8().v);
+        cache.emplace(n, v);
+        return v;
+    }
+
+    void piece(std::vector<CrcItem>& out, uint64_t ptr_of_ps, uint64_t ps, uint64_t pe, uint64_t s,
+               uint64_t e, uint32_t out_idx, uint32_t seed) {
+        // Items start at multiples of kItemBytes from the piece start (or at s).
+        for (uint64_t q = s; q < e;) {
+            const uint64_t next = std::min(e, ps + ((q - ps) / kItemBytes + 1) * kItemBytes);
+            CrcItem it{};
+            it.ptr = ptr_of_ps + (q - ps);
+            it.len = (uint32_t)(next - q);
+            it.out = out_idx;
+            it.mul = X(pe - next);
+            it.xr = (q == ps) ? (gf2_mulmod(seed, X(pe - ps)) ^ 0xFFFFFFFFu) : 0u;
+            out.push_back(it);
+            q = next;
+        }
+    }
+
+    void add(std::vector<CrcItem>& out, uint64_t base, uint64_t a, uint64_t b, uint64_t L, uint64_t P,
+             uint64_t sums_off, uint32_t seed = 0xFFFFFFFFu) {
+        if (a >= b) return;
+        for (uint64_t pi = a / P; pi * P < b; ++pi) {
+            const uint64_t ps = pi * P, pe = std::min(ps + P, L);
+            const uint64_t s = std::max(a, ps), e = std::min(b, pe);
+            const uint64_t ptr_ps = base + ps - a;  // may point before base; only offsets >= s used
+            if (s == ps && e == pe && pe - ps == P && seed == 0xFFFFFFFFu) {
+                auto it = full.find(P);
+                if (it == full.end()) {
+                    Pattern pat;
+                    piece(pat.items, 0, 0, P, 0, P, 0, seed);
+                    it = full.emplace(P, std::move(pat)).first;
+                }
+                for (const CrcItem& t : it->second.items) {
+                    CrcItem c = t;
+                    c.ptr += ptr_ps;
+                    c.out = (uint32_t)(sums_off + pi);
+                    out.push_back(c);
+                }
+            } else {
+                piece(out, ptr_ps, ps, pe, s, e, (uint32_t)(sums_off + pi), seed);
+            }
+        }
+    }
+};
+
+static int validate_blobs(const krk_blob* blobs, uint64_t n) {
+    KRK_CHECK(n == 0 || blobs, KRK_EINVAL, "blobs is NULL");
+    for (uint64_t i = 0; i < n; ++i) {
+        KRK_CHECK(blobs[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
+        KRK_CHECK(blobs[i].length == 0 || blobs[i].data, KRK_EINVAL, "blob %llu: data is NULL",
+                  (unsigned long long)i);
+        const uint64_t np = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
+        KRK_CHECK(blobs[i].sums_offset + np <= 0xFFFFFFFFull, KRK_EINVAL,
+                  "sums index exceeds 2^32 in one call");
+    }
+    return KRK_OK;
+}
+
+// Zero the sums span [lo, hi) that the blobs cover.
+static void sums_span(const krk_blob* blobs, uint64_t n, uint64_t* lo, uint64_t* hi) {
+    *lo = UINT64_MAX;
+    *hi = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t np = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
+        if (!np) continue;
+        *lo = std::min(*lo, blobs[i].sums_offset);
+        *hi = std::max(*hi, blobs[i].sums_offset + np);
+    }
+    if (*lo > *hi) *lo = *hi = 0;
+}
+
+static int run_items(Device* D, const std::vector<CrcItem>& items, uint32_t* sums_dev, hipStream_t s) {
+    if (items.empty()) return KRK_OK;
+    void* d_items = nullptr;
+    int r = upload(D, items.data(), items.size() * sizeof(CrcItem), &d_items, s);
+    if (r) return r;
+    CrcLaunchCfg cfg{D->cus, D->crc_variant};
+    hipError_t e = timed(K_CRC, s, [&] {
+        return launch_crc_items(static_cast<const CrcItem*>(d_items), (uint32_t)items.size(), D->d_tabs,
+                                sums_dev, cfg, s);
+    });
+    hipFreeAsync(d_items, s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+static int piece_sums_dev(Device* D, const krk_blob* blobs, uint64_t n, uint32_t* sums_dev, hipStream_t s) {
+    int r = validate_blobs(blobs, n);
+    if (r) return r;
+    uint64_t lo, hi;
+    sums_span(blobs, n, &lo, &hi);
+    if (hi == lo) return KRK_OK;
+    KRK_CHECK(sums_dev, KRK_EINVAL, "sums_dev is NULL");
+    KRK_HIP(hipMemsetAsync(sums_dev + lo, 0, (hi - lo) * 4, s));
+    ItemBuilder B;
+    std::vector<CrcItem> items;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += blobs[i].length;
+    items.reserve(total / kItemBytes + 2 * n + 16);
+    for (uint64_t i = 0; i < n; ++i)
+        B.add(items, reinterpret_cast<uint64_t>(blobs[i].data), 0, blobs[i].length, blobs[i].length,
+              (uint64_t)blobs[i].piece_length, blobs[i].sums_offset);
+    return run_items(D, items, sums_dev, s);
+}
+
+// ------------------------------------------------------------------ SHA jobs
+static const uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+static int run_jobs(Device* D, std::vector<ShaJob>& jobs, uint8_t* digests_dev, uint32_t* state_dev,
+                    hipStream_t s) {
+    if (jobs.empty()) return KRK_OK;
+    // Longest streams first: lanes of one wave then carry similar lengths.
+    std::stable_sort(jobs.begin(), jobs.end(), [](const ShaJob& a, const ShaJob& b) { return a.len > b.len; });
+    void* d_jobs = nullptr;
+    int r = upload(D, jobs.data(), jobs.size() * sizeof(ShaJob), &d_jobs, s);
+    if (r) return r;
+    hipError_t e = timed(K_SHA, s, [&] {
+        return launch_sha256(static_cast<const ShaJob*>(d_jobs), (uint32_t)jobs.size(), digests_dev,
+                             state_dev, s);
+    });
+    hipFreeAsync(d_jobs, s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+static ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
+    ShaJob j{};
+    j.ptr = reinterpret_cast<uint64_t>(p);
+    j.len = len;
+    j.prefix = 0;
+    j.out = out;
+    j.flags = kShaFinal;
+    memcpy(j.h, kIV, sizeof kIV);
+    return j;
+}
+
+// ------------------------------------------------------------------ host staging pipeline
+// Two pinned host windows and two device windows; window k is refilled only after
+// the kernel that consumed it (event) has finished.
+struct Window {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t copied = nullptr, consumed = nullptr;
+    bool inflight = false;
+};
+
+struct Pipeline {
+    Window w[2];
+    ~Pipeline() {
+        for (auto& x : w) {
+            if (x.inflight) hipEventSynchronize(x.consumed);
+            if (x.host) hipHostFree(x.host);
+            if (x.dev) hipFree(x.dev);
+            if (x.copied) hipEventDestroy(x.copied);
+            if (x.consumed) hipEventDestroy(x.consumed);
+        }
+    }
+    int init(size_t cap) {
+        for (auto& x : w) {
+            x.cap = cap;
+            KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&x.host), cap, hipHostMallocDefault));
+            KRK_HIP(hipMalloc(reinterpret_cast<void**>(&x.dev), cap));
+            KRK_HIP(hipEventCreateWithFlags(&x.copied, hipEventDisableTiming));
+            KRK_HIP(hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming));
+        }
+        return KRK_OK;
+    }
+    int acquire(int k) {
+        if (w[k].inflight) {
+            KRK_HIP(hipEventSynchronize(w[k].consumed));
+            w[k].inflight = false;
+        }
+        return KRK_OK;
+    }
+};
+
+static size_t window_bytes() {
+    const char* v = getenv("KRK_WINDOW_MB");
+    size_t mb = v ? strtoull(v, nullptr, 10) : 256;
+    if (mb < 1) mb = 1;
+    return mb << 20;
+}
+
+}  // namespace krk
+
+using namespace krk;
+
+// ======================================================================= C ABI
+extern "C" {
+
+const char* krk_version(void) { return "kraken_amd 0.1 (gfx950)"; }
+const char* krk_last_error(void) { return t_err.c_str(); }
+
+int krk_device_count(int* n) {
+    KRK_CHECK(n, KRK_EINVAL, "n is NULL");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    int good = 0;
+    for (int i = 0; i < c; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
+    }
+    *n = good;
+    return KRK_OK;
+}
+
+int krk_set_device(int dev) {
+    t_dev = dev;
+    KRK_DEVICE(D);
+    (void)D;
+    return KRK_OK;
+}
+
+int krk_synchronize(void) {
+    KRK_DEVICE(D);
+    KRK_HIP(hipStreamSynchronize(D->s_main));
+    KRK_HIP(hipStreamSynchronize(D->s_a));
+    KRK_HIP(hipStreamSynchronize(D->s_b));
+    return KRK_OK;
+}
+
+uint64_t krk_num_pieces(uint64_t length, int64_t piece_length) {
+    if (piece_length <= 0) return 0;
+    return (length + (uint64_t)piece_length - 1) / (uint64_t)piece_length;
+}
+
+int krk_piece_sums_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev, void* stream) {
+    KRK_DEVICE(D);
+    return piece_sums_dev(D, blobs, n_blobs, sums_dev, pick(D, stream));
+}
+
+int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n, uint8_t* digests_dev,
+                   void* stream) {
+    KRK_DEVICE(D);
+    if (!n) return KRK_OK;
+    KRK_CHECK(data_dev && lengths && digests_dev, KRK_EINVAL, "sha256_dev: null argument");
+    std::vector<ShaJob> jobs(n);
+    for (uint64_t i = 0; i < n; ++i) jobs[i] = full_job(data_dev[i], lengths[i], (uint32_t)i);
+    return run_jobs(D, jobs, digests_dev, nullptr, pick(D, stream));
+}
+
+int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev, uint8_t* digests_dev,
+                            void* stream) {
+    KRK_DEVICE(D);
+    int r = validate_blobs(blobs, n_blobs);
+    if (r) return r;
+    if (!n_blobs) return KRK_OK;
+    KRK_CHECK(digests_dev, KRK_EINVAL, "digests_dev is NULL");
+    hipStream_t s = pick(D, stream);
+    hipEvent_t fork, j1, j2;
+    KRK_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    KRK_HIP(hipEventCreateWithFlags(&j1, hipEventDisableTiming));
+    KRK_HIP(hipEventCreateWithFlags(&j2, hipEventDisableTiming));
+    KRK_HIP(hipEventRecord(fork, s));
+    KRK_HIP(hipStreamWaitEvent(D->s_a, fork, 0));
+    KRK_HIP(hipStreamWaitEvent(D->s_b, fork, 0));
+    // SHA first: it is the long pole; the CRC kernel fills the rest of the chip.
+    std::vector<ShaJob> jobs(n_blobs);
+    for (uint64_t i = 0; i < n_blobs; ++i) jobs[i] = full_job(blobs[i].data, blobs[i].length, (uint32_t)i);
+    r = run_jobs(D, jobs, digests_dev, nullptr, D->s_a);
+    if (!r) r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
+    hipEventRecord(j1, D->s_a);
+    hipEventRecord(j2, D->s_b);
+    hipStreamWaitEvent(s, j1, 0);
+    hipStreamWaitEvent(s, j2, 0);
+    hipEventDestroy(fork);
+    hipEventDestroy(j1);
+    hipEventDestroy(j2);
+    return r;
+}
+
+int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
+    KRK_DEVICE(D);
+    int r = validate_blobs(blobs, n_blobs);
+    if (r) return r;
+    uint64_t lo, hi;
+    sums_span(blobs, n_blobs, &lo, &hi);
+    if (hi == lo) return KRK_OK;
+    KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
+    uint32_t* d_sums = nullptr;
+    KRK_HIP(hipMalloc(&d_sums, hi * 4));
+    KRK_HIP(hipMemset(d_sums, 0, hi * 4));
+    Pipeline pl;
+    const size_t W = window_bytes();
+    r = pl.init(W);
+    hipStream_t cp = D->s_a, ks = D->s_b;
+    ItemBuilder B;
+    int k = 0;
+    uint64_t bi = 0, boff = 0;
+    while (!r && bi < n_blobs) {
+        r = pl.acquire(k);
+        if (r) break;
+        Window& w = pl.w[k];
+        size_t fill = 0;
+        std::vector<CrcItem> items;
+        while (bi < n_blobs && fill < W) {
+            const krk_blob& b = blobs[bi];
+            const uint64_t take = std::min<uint64_t>(b.length - boff, W - fill);
+            if (take) {
+                memcpy(w.host + fill, b.data + boff, take);
+                B.add(items, reinterpret_cast<uint64_t>(w.dev + fill), boff, boff + take, b.length,
+                      (uint64_t)b.piece_length, b.sums_offset);
+            }
+            fill += take;
+            boff += take;
+            // keep 16-byte alignment of every run inside the window
+            fill = (fill + 15) & ~size_t(15);
+            if (boff >= b.length) { ++bi; boff = 0; }
+        }
+        if (hipMemcpyAsync(w.dev, w.host, std::min(fill, W), hipMemcpyHostToDevice, cp) != hipSuccess ||
+            hipEventRecord(w.copied, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
+            set_error(KRK_EHIP, "piece_sums_host: staging copy failed");
+            r = KRK_EHIP;
+            break;
+        }
+        r = run_items(D, items, d_sums, ks);
+        if (r) break;
+        hipEventRecord(w.consumed, ks);
+        w.inflight = true;
+        hipStreamWaitEvent(cp, w.consumed, 0);
+        k ^= 1;
+    }
+    if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "sums copy-out failed");
+        r = KRK_EHIP;
+    }
+    hipFree(d_sums);
+    return r;
+}
+
+int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n, uint8_t* digests_host) {
+    KRK_DEVICE(D);
+    if (!n) return KRK_OK;
+    KRK_CHECK(data_host && lengths && digests_host, KRK_EINVAL, "sha256_host: null argument");
+    const size_t W = window_bytes();
+    // Per-stream chunk per round: the window split over the streams (multiple of 64).
+    uint64_t C = (W / n) & ~uint64_t(63);
+    if (C < 64) C = 64;
+    const size_t cap = std::max<size_t>(W, C * n + 16 * n);
+    Pipeline pl;
+    int r = pl.init(cap);
+    if (r) return r;
+    uint8_t* d_dig = nullptr;
+    uint32_t* d_state = nullptr;
+    KRK_HIP(hipMalloc(&d_dig, n * 32));
+    KRK_HIP(hipMalloc(&d_state, n * 32));
+    std::vector<uint64_t> off(n, 0);
+    std::vector<char> done(n, 0);
+    hipStream_t cp = D->s_a, ks = D->s_b;
+    uint64_t remaining = n;
+    int k = 0;
+    while (!r && remaining) {
+        r = pl.acquire(k);
+        if (r) break;
+        Window& w = pl.w[k];
+        std::vector<ShaJob> jobs;
+        size_t fill = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (done[i]) continue;
+            const uint64_t left = lengths[i] - off[i];
+            const bool fin = left <= C;
+            const uint64_t take = fin ? left : C;
+            if (take) memcpy(w.host + fill, data_host[i] + off[i], take);
+            ShaJob j{};
+            j.ptr = reinterpret_cast<uint64_t>(w.dev + fill);
+            j.len = take;
+            j.prefix = off[i];
+            j.out = (uint32_t)i;
+            j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
+            memcpy(j.h, kIV, sizeof kIV);
+            jobs.push_back(j);
+            off[i] += take;
+            fill += (take + 15) & ~uint64_t(15);
+            if (fin) { done[i] = 1; --remaining; }
+        }
+        if (hipMemcpyAsync(w.dev, w.host, fill, hipMemcpyHostToDevice, cp) != hipSuccess ||
+            hipEventRecord(w.copied, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
+            set_error(KRK_EHIP, "sha256_host: staging copy failed");
+            r = KRK_EHIP;
+            break;
+        }
+        r = run_jobs(D, jobs, d_dig, d_state, ks);
+        if (r) break;
+        hipEventRecord(w.consumed, ks);
+        w.inflight = true;
+        hipStreamWaitEvent(cp, w.consumed, 0);
+        k ^= 1;
+    }
+    if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "digest copy-out failed");
+        r = KRK_EHIP;
+    }
+    hipFree(d_dig);
+    hipFree(d_state);
+    return r;
+}
+
+// ---------------------------------------------------------------- piece stream
+struct krk_piece_stream {
+    Device* D = nullptr;
+    uint64_t P = 0;
+    size_t W = 0;
+    Pipeline pl;
+    int cur = 0;
+    size_t fill = 0;
+    uint64_t flushed = 0;  // bytes already handed to the device
+    uint32_t* d_sums = nullptr;
+    uint64_t sums_cap = 0;
+    ItemBuilder B;
+    int err = KRK_OK;
+};
+
+static int stream_grow_sums(krk_piece_stream* s, uint64_t need) {
+    if (need <= s->sums_cap) return KRK_OK;
+    uint64_t cap = std::max<uint64_t>(need, s->sums_cap * 2 + 1024);
+    uint32_t* n = nullptr;
+    KRK_HIP(hipMallocAsync(&n, cap * 4, s->D->s_b));
+    KRK_HIP(hipMemsetAsync(n, 0, cap * 4, s->D->s_b));
+    if (s->d_sums) {
+        KRK_HIP(hipMemcpyAsync(n, s->d_sums, s->sums_cap * 4, hipMemcpyDeviceToDevice, s->D->s_b));
+        KRK_HIP(hipFreeAsync(s->d_sums, s->D->s_b));
+    }
+    s->d_sums = n;
+    s->sums_cap = cap;
+    return KRK_OK;
+}
+
+static int stream_flush(krk_piece_stream* s, bool final) {
+    Window& w = s->pl.w[s->cur];
+    const uint64_t a = s->flushed, b = s->flushed + s->fill;
+    const uint64_t L = b;  // non-final flushes hold whole pieces only, so L = b is exact for them
+    if (s->fill) {
+        int r = stream_grow_sums(s, krk_num_pieces(b, (int64_t)s->P));
+        if (r) return r;
+        std::vector<CrcItem> items;
+        s->B.add(items, reinterpret_cast<uint64_t>(w.dev), a, b, L, s->P, 0);
+        KRK_HIP(hipMemcpyAsync(w.dev, w.host, s->fill, hipMemcpyHostToDevice, s->D->s_a));
+        KRK_HIP(hipEventRecord(w.copied, s->D->s_a));
+        KRK_HIP(hipStreamWaitEvent(s->D->s_b, w.copied, 0));
+        r = run_items(s->D, items, s->d_sums, s->D->s_b);
+        if (r) return r;
+        KRK_HIP(hipEventRecord(w.consumed, s->D->s_b));
+        KRK_HIP(hipStreamWaitEvent(s->D->s_a, w.consumed, 0));
+        w.inflight = true;
+    }
+    s->flushed = b;
+    s->fill = 0;
+    (void)final;
+    s->cur ^= 1;
+    return s->pl.acquire(s->cur);
+}
+
+int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_CHECK(piece_length > 0, KRK_EINVAL, "piece length must be positive");
+    KRK_DEVICE(D);
+    auto* s = new krk_piece_stream();
+    s->D = D;
+    s->P = (uint64_t)piece_length;
+    const uint64_t target = 64ull << 20;
+    s->W = (size_t)(s->P * std::max<uint64_t>(1, target / s->P));
+    int r = s->pl.init(s->W);
+    if (r) { delete s; return r; }
+    *out = s;
+    return KRK_OK;
+}
+
+int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
+    KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
+    if (s->err) return s->err;
+    KRK_CHECK(n == 0 || buf, KRK_EINVAL, "buffer is NULL");
+    KRK_HIP(hipSetDevice(s->D->id));
+    while (n) {
+        const size_t take = std::min<uint64_t>(n, s->W - s->fill);
+        memcpy(s->pl.w[s->cur].host + s->fill, buf, take);
+        s->fill += take;
+        buf += take;
+        n -= take;
+        if (s->fill == s->W) {
+            int r = stream_flush(s, false);
+            if (r) return s->err = r;
+        }
+    }
+    return KRK_OK;
+}
+
+int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, uint64_t* n_sums,
+                         uint64_t* length) {
+    KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
+    if (s->err) return s->err;
+    KRK_HIP(hipSetDevice(s->D->id));
+    int r = stream_flush(s, true);
+    if (r) return r;
+    KRK_HIP(hipStreamSynchronize(s->D->s_b));
+    const uint64_t np = krk_num_pieces(s->flushed, (int64_t)s->P);
+    if (n_sums) *n_sums = np;
+    if (length) *length = s->flushed;
+    KRK_CHECK(np <= cap || !sums_out, KRK_ERANGE, "sums capacity %llu < %llu pieces", (unsigned long long)cap,
+              (unsigned long long)np);
+    if (sums_out && np) KRK_HIP(hipMemcpy(sums_out, s->d_sums, np * 4, hipMemcpyDeviceToHost));
+    return KRK_OK;
+}
+
+void krk_piece_stream_free(krk_piece_stream* s) {
+    if (!s) return;
+    hipSetDevice(s->D->id);
+    hipStreamSynchronize(s->D->s_b);
+    if (s->d_sums) hipFree(s->d_sums);
+    delete s;
+}
+
+int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    if (n == 0) { *out = crc; return KRK_OK; }
+    KRK_CHECK(data, KRK_EINVAL, "data is NULL");
+    KRK_DEVICE(D);
+    hipStream_t s = D->s_main;
+    uint8_t* d_buf = nullptr;
+    uint32_t* d_sum = nullptr;
+    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_buf), n + 4, s));
+    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_sum), 4, s));
+    KRK_HIP(hipMemcpyAsync(d_buf, data, n, hipMemcpyHostToDevice, s));
+    KRK_HIP(hipMemsetAsync(d_sum, 0, 4, s));
+    ItemBuilder B;
+    std::vector<CrcItem> items;
+    // crc32.Update(crc, IEEETable, p) = ~raw(~crc, p): one piece seeded with ~crc.
+    B.add(items, reinterpret_cast<uint64_t>(d_buf), 0, n, n, n, 0, ~crc);
+    int r = run_items(D, items, d_sum, s);
+    if (!r && hipMemcpyAsync(out, d_sum, 4, hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    hipFreeAsync(d_buf, s);
+    hipFreeAsync(d_sum, s);
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
+    return r;
+}
+
+int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, uint8_t* ok_out_host, void* stream) {
+    KRK_CHECK(blob && expected_host && ok_out_host, KRK_EINVAL, "verify: null argument");
+    KRK_DEVICE(D);
+    hipStream_t s = pick(D, stream);
+    krk_blob b = *blob;
+    b.sums_offset = 0;
+    const uint64_t np = krk_num_pieces(b.length, b.piece_length);
+    int r = validate_blobs(&b, 1);
+    if (r || !np) return r;
+    uint32_t* d_sums = nullptr;
+    uint8_t* d_ok = nullptr;
+    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_sums), np * 4, s));
+    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ok), np, s));
+    r = piece_sums_dev(D, &b, 1, d_sums, s);
+    void* d_exp = nullptr;
+    if (!r) r = upload(D, expected_host, np * 4, &d_exp, s);
+    if (!r) {
+        hipError_t e = launch_crc_verify(d_sums, static_cast<const uint32_t*>(d_exp), d_ok, (uint32_t)np, s);
+        if (e != hipSuccess) { set_error(KRK_EHIP, "verify launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+    }
+    if (!r && hipMemcpyAsync(ok_out_host, d_ok, np, hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    hipFreeAsync(d_sums, s);
+    hipFreeAsync(d_ok, s);
+    if (d_exp) hipFreeAsync(d_exp, s);
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "verify sync"); r = KRK_EHIP; }
+    return r;
+}
+
+// ---------------------------------------------------------------- digester
+struct krk_digester {
+    Device* D = nullptr;
+    Pipeline pl;
+    size_t W = 0;
+    int cur = 0;
+    size_t fill = 0;
+    uint64_t absorbed = 0;  // bytes folded into the device midstate
+    uint32_t* d_state = nullptr;
+    uint8_t* d_dig = nullptr;
+};
+
+static int digester_flush_blocks(krk_digester* d) {
+    // Fold the whole-block prefix of the pending bytes into the midstate.
+    const size_t nb = d->fill & ~size_t(63);
+    if (!nb) return KRK_OK;
+    Window& w = d->pl.w[d->cur];
+    hipStream_t s = d->D->s_b;
+    KRK_HIP(hipMemcpyAsync(w.dev, w.host, nb, hipMemcpyHostToDevice, s));
+    std::vector<ShaJob> jobs(1);
+    ShaJob& j = jobs[0];
+    j = ShaJob{};
+    j.ptr = reinterpret_cast<uint64_t>(w.dev);
+    j.len = nb;
+    j.prefix = d->absorbed;
+    j.out = 0;
+    j.flags = d->absorbed ? kShaFromState : 0;
+    memcpy(j.h, kIV, sizeof kIV);
+    int r = run_jobs(d->D, jobs, d->d_dig, d->d_state, s);
+    if (r) return r;
+    KRK_HIP(hipEventRecord(w.consumed, s));
+    w.inflight = true;
+    d->absorbed += nb;
+    const size_t rest = d->fill - nb;
+    const int nxt = d->cur ^ 1;
+    r = d->pl.acquire(nxt);
+    if (r) return r;
+    if (rest) memcpy(d->pl.w[nxt].host, w.host + nb, rest);
+    d->fill = rest;
+    d->cur = nxt;
+    return KRK_OK;
+}
+
+int krk_digester_new(krk_digester** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    auto* d = new krk_digester();
+    d->D = D;
+    d->W = 16u << 20;
+    int r = d->pl.init(d->W + 64);
+    if (!r && hipMalloc(&d->d_state, 32) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && hipMalloc(&d->d_dig, 32) != hipSuccess) r = KRK_ENOMEM;
+    if (r) { delete d; set_error(r, "digester allocation failed"); return r; }
+    *out = d;
+    return KRK_OK;
+}
+
+int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
+    KRK_CHECK(d, KRK_EINVAL, "digester is NULL");
+    KRK_CHECK(n == 0 || buf, KRK_EINVAL, "buffer is NULL");
+    KRK_HIP(hipSetDevice(d->D->id));
+    while (n) {
+        const size_t take = std::min<uint64_t>(n, d->W - d->fill);
+        memcpy(d->pl.w[d->cur].host + d->fill, buf, take);
+        d->fill += take;
+        buf += take;
+        n -= take;
+        if (d->fill == d->W) {
+            int r = digester_flush_blocks(d);
+            if (r) return r;
+        }
+    }
+    return KRK_OK;
+}
+
+int krk_digester_sum(krk_digester* d, uint8_t out32[32]) {
+    KRK_CHECK(d && out32, KRK_EINVAL, "digester_sum: null argument");
+    KRK_HIP(hipSetDevice(d->D->id));
+    int r = digester_flush_blocks(d);
+    if (r) return r;
+    // Final job over the (< 64 B) pending tail from the midstate; the midstate is
+    // left untouched, so writing may continue (Digest() does not reset).
+    Window& w = d->pl.w[d->cur];
+    hipStream_t s = d->D->s_b;
+    if (d->fill) KRK_HIP(hipMemcpyAsync(w.dev, w.host, d->fill, hipMemcpyHostToDevice, s));
+    std::vector<ShaJob> jobs(1);
+    ShaJob& j = jobs[0];
+    j = ShaJob{};
+    j.ptr = reinterpret_cast<uint64_t>(w.dev);
+    j.len = d->fill;
+    j.prefix = d->absorbed;
+    j.out = 0;
+    j.flags = kShaFinal | (d->absorbed ? kShaFromState : 0);
+    memcpy(j.h, kIV, sizeof kIV);
+    r = run_jobs(d->D, jobs, d->d_dig, d->d_state, s);
+    if (r) return r;
+    KRK_HIP(hipMemcpyAsync(out32, d->d_dig, 32, hipMemcpyDeviceToHost, s));
+    KRK_HIP(hipStreamSynchronize(s));
+    return KRK_OK;
+}
+
+void krk_digester_free(krk_digester* d) {
+    if (!d) return;
+    hipSetDevice(d->D->id);
+    hipStreamSynchronize(d->D->s_b);
+    hipFree(d->d_state);
+    hipFree(d->d_dig);
+    delete d;
+}
+
+// ---------------------------------------------------------------- HRW
+static int hexv(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+
+struct DevNodes {
+    void* labels = nullptr;
+    void* off = nullptr;
+    void* w = nullptr;
+};
+
+static int upload_nodes(Device* D, const krk_nodes* nodes, DevNodes& dn, hipStream_t s) {
+    KRK_CHECK(nodes && nodes->n_nodes > 0 && nodes->label_off && nodes->weights, KRK_EINVAL,
+              "nodes: empty or null");
+    KRK_CHECK(nodes->n_nodes <= 4096, KRK_EINVAL, "more than 4096 nodes");
+    const uint64_t lb = nodes->label_off[nodes->n_nodes];
+    int r = KRK_OK;
+    if (lb) r = upload(D, nodes->labels, lb, &dn.labels, s);
+    if (!r) r = upload(D, nodes->label_off, (nodes->n_nodes + 1) * 8, &dn.off, s);
+    if (!r) r = upload(D, nodes->weights, nodes->n_nodes * 8, &dn.w, s);
+    return r;
+}
+
+static void free_nodes(DevNodes& dn, hipStream_t s) {
+    if (dn.labels) hipFreeAsync(dn.labels, s);
+    if (dn.off) hipFreeAsync(dn.off, s);
+    if (dn.w) hipFreeAsync(dn.w, s);
+}
+
+// Order + Locations table for the given decoded keys; result rows on the device.
+static int hrw_table(Device* D, const std::vector<uint8_t>& kb, const std::vector<uint64_t>& koff,
+                     const std::vector<uint8_t>& bad, const krk_nodes* nodes, const uint8_t* healthy,
+                     int32_t max_replica, uint32_t row_out, int32_t** d_locs, uint8_t** d_counts,
+                     hipStream_t s) {
+    const uint64_t nk = koff.size() - 1;
+    const uint32_t N = nodes->n_nodes;
+    DevNodes dn;
+    int r = upload_nodes(D, nodes, dn, s);
+    void *d_kb = nullptr, *d_koff = nullptr, *d_bad = nullptr, *d_h = nullptr;
+    int32_t* d_order = nullptr;
+    if (!r) r = upload(D, kb.data(), kb.size(), &d_kb, s);
+    if (!r) r = upload(D, koff.data(), koff.size() * 8, &d_koff, s);
+    if (!r) r = upload(D, bad.data(), bad.size(), &d_bad, s);
+    if (!r) r = upload(D, healthy, N, &d_h, s);
+    if (!r && hipMallocAsync(reinterpret_cast<void**>(&d_order), nk * N * 4, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && hipMallocAsync(reinterpret_cast<void**>(d_locs), nk * row_out * 4, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && hipMallocAsync(reinterpret_cast<void**>(d_counts), nk, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r) {
+        HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), nk,
+                  static_cast<const uint8_t*>(dn.labels), static_cast<const uint64_t*>(dn.off),
+                  static_cast<const int64_t*>(dn.w), N, N, static_cast<const uint8_t*>(d_bad), d_order, nullptr};
+        hipError_t e = timed(K_HRW, s, [&] { return launch_hrw_order(a, s); });
+        if (e == hipSuccess)
+            e = timed(K_FILTER, s, [&] {
+                return launch_ring_filter(d_order, nk, N, static_cast<const uint8_t*>(d_h), max_replica, row_out,
+                                          *d_locs, *d_counts, s);
+            });
+        if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+    }
+    free_nodes(dn, s);
+    for (void* p : {d_kb, d_koff, d_bad, d_h, static_cast<void*>(d_order)})
+        if (p) hipFreeAsync(p, s);
+    return r;
+}
+
+int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, const krk_nodes* nodes,
+                    uint32_t n_out, int32_t* order_out, double* scores_out) {
+    if (!n_keys) return KRK_OK;
+    KRK_CHECK(keys && key_off && order_out, KRK_EINVAL, "hrw_ordered: null argument");
+    KRK_DEVICE(D);
+    hipStream_t s = D->s_main;
+    // hex.DecodeString per key (rendezvous.go:154-157).
+    std::vector<uint8_t> kb;
+    std::vector<uint64_t> koff(n_keys + 1, 0);
+    std::vector<uint8_t> bad(n_keys, 0);
+    bool any_bad = false;
+    for (uint64_t i = 0; i < n_keys; ++i) {
+        const char* k = keys + key_off[i];
+        const uint64_t len = key_off[i + 1] - key_off[i];
+        koff[i] = kb.size();
+        bool ok = (len % 2) == 0;
+        for (uint64_t q = 0; ok && q + 1 < len; q += 2) {
+            const int a = hexv(k[q]), b = hexv(k[q + 1]);
+            if (a < 0 || b < 0) { ok = false; break; }
+            kb.push_back((uint8_t)(a << 4 | b));
+        }
+        if (!ok) { kb.resize(koff[i]); bad[i] = 1; any_bad = true; }
+    }
+    koff[n_keys] = kb.size();
+    if (kb.empty()) kb.push_back(0);
+    DevNodes dn;
+    int r = upload_nodes(D, nodes, dn, s);
+    const uint32_t N = nodes ? nodes->n_nodes : 0;
+    void *d_kb = nullptr, *d_koff = nullptr, *d_bad = nullptr;
+    int32_t* d_order = nullptr;
+    double* d_sc = nullptr;
+    if (!r) r = upload(D, kb.data(), kb.size(), &d_kb, s);
+    if (!r) r = upload(D, koff.data(), koff.size() * 8, &d_koff, s);
+    if (!r) r = upload(D, bad.data(), bad.size(), &d_bad, s);
+    if (!r && hipMallocAsync(reinterpret_cast<void**>(&d_order), n_keys * n_out * 4 + 4, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && scores_out && hipMallocAsync(reinterpret_cast<void**>(&d_sc), n_keys * N * 8, s) != hipSuccess)
+        r = KRK_ENOMEM;
+    if (!r) {
+        HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), n_keys,
+                  static_cast<const uint8_t*>(dn.labels), static_cast<const uint64_t*>(dn.off),
+                  static_cast<const int64_t*>(dn.w), N, n_out, static_cast<const uint8_t*>(d_bad), d_order, d_sc};
+        hipError_t e = n_out ? timed(K_HRW, s, [&] { return launch_hrw_order(a, s); }) : hipSuccess;
+        if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+    }
+    if (!r && n_out && hipMemcpyAsync(order_out, d_order, n_keys * n_out * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        r = KRK_EHIP;
+    if (!r && scores_out && hipMemcpyAsync(scores_out, d_sc, n_keys * N * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+        r = KRK_EHIP;
+    free_nodes(dn, s);
+    for (void* p : {d_kb, d_koff, d_bad, static_cast<void*>(d_order), static_cast<void*>(d_sc)})
+        if (p) hipFreeAsync(p, s);
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "hrw sync"); r = KRK_EHIP; }
+    if (!r && any_bad) {
+        set_error(KRK_EHEX, "invalid hex key: Score is NaN");
+        return KRK_EHEX;
+    }
+    return r;
+}
+
+static void shard_keys(std::vector<uint8_t>& kb, std::vector<uint64_t>& koff, const std::vector<uint32_t>& shards) {
+    kb.resize(shards.size() * 2);
+    koff.resize(shards.size() + 1);
+    for (size_t i = 0; i < shards.size(); ++i) {
+        kb[2 * i] = (uint8_t)(shards[i] >> 8);
+        kb[2 * i + 1] = (uint8_t)shards[i];
+        koff[i] = 2 * i;
+    }
+    koff[shards.size()] = kb.size();
+}
+
+int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* nodes, const uint8_t* healthy,
+                       int32_t max_replica, int32_t* locs_out, uint8_t* counts_out) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(digests32 && healthy && locs_out && counts_out, KRK_EINVAL, "ring_locations: null argument");
+    KRK_DEVICE(D);
+    hipStream_t s = D->s_main;
+    const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
+    // Only the shards present: Locations depends on d only through ShardID.
+    std::vector<int32_t> row_of(65536, -1);
+    std::vector<uint32_t> shards;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t sh = (uint32_t)digests32[32 * i] << 8 | digests32[32 * i + 1];
+        if (row_of[sh] < 0) { row_of[sh] = (int32_t)shards.size(); shards.push_back(sh); }
+    }
+    std::vector<uint8_t> kb, bad(shards.size(), 0);
+    std::vector<uint64_t> koff;
+    shard_keys(kb, koff, shards);
+    int32_t* d_locs = nullptr;
+    uint8_t* d_counts = nullptr;
+    int r = hrw_table(D, kb, koff, bad, nodes, healthy, max_replica, row_out, &d_locs, &d_counts, s);
+    std::vector<int32_t> tl(shards.size() * row_out);
+    std::vector<uint8_t> tc(shards.size());
+    if (!r && hipMemcpyAsync(tl.data(), d_locs, tl.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    if (!r && hipMemcpyAsync(tc.data(), d_counts, tc.size(), hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    if (d_locs) hipFreeAsync(d_locs, s);
+    if (d_counts) hipFreeAsync(d_counts, s);
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "ring sync"); r = KRK_EHIP; }
+    if (r) return r;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int32_t row = row_of[(uint32_t)digests32[32 * i] << 8 | digests32[32 * i + 1]];
+        memcpy(locs_out + i * row_out, tl.data() + (uint64_t)row * row_out, row_out * 4);
+        counts_out[i] = tc[row];
+    }
+    return KRK_OK;
+}
+
+int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                           const uint8_t* healthy, int32_t max_replica, int32_t* locs_dev, uint8_t* counts_dev,
+                           void* stream) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(digests32_dev && healthy && locs_dev && counts_dev, KRK_EINVAL, "ring_locations_dev: null argument");
+    KRK_DEVICE(D);
+    hipStream_t s = pick(D, stream);
+    const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
+    std::vector<uint32_t> shards(65536);
+    std::iota(shards.begin(), shards.end(), 0u);
+    std::vector<uint8_t> kb, bad(65536, 0);
+    std::vector<uint64_t> koff;
+    shard_keys(kb, koff, shards);
+    int32_t* d_tl = nullptr;
+    uint8_t* d_tc = nullptr;
+    int r = hrw_table(D, kb, koff, bad, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, s);
+    if (!r) {
+        hipError_t e = timed(K_GATHER, s, [&] {
+            return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
+        });
+        if (e != hipSuccess) { set_error(KRK_EHIP, "gather launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+    }
+    if (d_tl) hipFreeAsync(d_tl, s);
+    if (d_tc) hipFreeAsync(d_tc, s);
+    return r;
+}
+
+// ---------------------------------------------------------------- synthetic data
+int krk_synth_fill_dev(uint8_t* dst_dev, uint64_t blob_idx, uint64_t offset, uint64_t n, int variant, void* stream) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(dst_dev, KRK_EINVAL, "dst is NULL");
+    KRK_DEVICE(D);
+    hipStream_t s = pick(D, stream);
+    const uint64_t GAMMA = 0x9E3779B97F4A7C15ULL;
+    auto mix = [](uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    };
+    const uint64_t seed = mix((0x4B52414B454EULL ^ blob_idx) + GAMMA);
+    hipError_t e = timed(K_SYNTH, s, [&] { return launch_synth_fill(dst_dev, seed, offset, n, variant, s); });
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+// ---------------------------------------------------------------- memory helpers
+int krk_dev_alloc(uint64_t bytes, void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+    KRK_CHECK(e == hipSuccess, KRK_ENOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+    return KRK_OK;
+}
+int krk_dev_free(void* p) {
+    KRK_HIP(hipFree(p));
+    return KRK_OK;
+}
+int krk_memcpy_h2d(void* dst, const void* src, uint64_t n) {
+    KRK_DEVICE(D);
+    (void)D;
+    KRK_HIP(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+    return KRK_OK;
+}
+int krk_memcpy_d2h(void* dst, const void* src, uint64_t n) {
+    KRK_DEVICE(D);
+    (void)D;
+    KRK_HIP(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+    return KRK_OK;
+}
+int krk_stream_create(void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    hipStream_t s;
+    KRK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = s;
+    return KRK_OK;
+}
+int krk_stream_destroy(void* s) {
+    KRK_HIP(hipStreamDestroy(static_cast<hipStream_t>(s)));
+    return KRK_OK;
+}
+int krk_stream_sync(void* s) {
+    KRK_DEVICE(D);
+    KRK_HIP(hipStreamSynchronize(pick(D, s)));
+    return KRK_OK;
+}
+
+int krk_set_timing(int on) {
+    g_timing.store(on != 0);
+    return KRK_OK;
+}
+int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms) {
+    KRK_CHECK(kernel, KRK_EINVAL, "kernel is NULL");
+    drain_timing();
+    std::lock_guard<std::mutex> g(g_tmu);
+    for (int k = 0; k < K_N; ++k)
+        if (strcmp(kernel, kKernNames[k]) == 0) {
+            if (launches) *launches = g_cnt[k];
+            if (total_ms) *total_ms = g_ms[k];
+            return KRK_OK;
+        }
+    set_error(KRK_EINVAL, "unknown kernel '%s'", kernel);
+    return KRK_EINVAL;
+}
+int krk_reset_kernel_stats(void) {
+    drain_timing();
+    std::lock_guard<std::mutex> g(g_tmu);
+    for (int k = 0; k < K_N; ++k) { g_ms[k] = 0; g_cnt[k] = 0; }
+    return KRK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+// synth_fill.hip -- device generator for the benchmark's synthetic blobs.
+// Spec (shared with oracle/oracle.c orc_synth_fill): word j of blob i is
+// mix64(seed_i + (j+1)*GAMMA) in little-endian byte order, seed_i =
+// mix64((0x4B52414B454E ^ i) + GAMMA); variant 1 maps every byte b to
+// "a-zA-Z0-9"[b % 62] (the randutil.Text alphabet, utils/randutil/randutil.go:37).
+#include "kernels.hpp"
+#include "device_util.hpp"
+
+namespace krk {
+
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ULL;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t alnum8(uint64_t w) {
+    const char* A = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";
+    uint64_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) r |= (uint64_t)(uint8_t)A[((w >> (8 * b)) & 0xFF) % 62] << (8 * b);
+    return r;
+}
+
+// Fast path: dst 16-byte aligned and offset 8-byte aligned -> one uint4 (2 words)
+// per thread per iteration.
+__global__ void synth_fill_words(uint4* dst, uint64_t seed, uint64_t word0, uint64_t npairs,
+                                 int variant) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += stride) {
+        const uint64_t j = word0 + 2 * i;
+        uint64_t a = mix64(seed + (j + 1) * kGamma), b = mix64(seed + (j + 2) * kGamma);
+        if (variant) { a = alnum8(a); b = alnum8(b); }
+        dst[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+}
+
+__global__ void synth_fill_bytes(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n, int variant) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t pos = offset + i;
+        uint64_t w = mix64(seed + ((pos >> 3) + 1) * kGamma);
+        if (variant) w = alnum8(w);
+        dst[i] = (uint8_t)(w >> (8 * (pos & 7)));
+    }
+}
+
+hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n, int variant,
+                             hipStream_t s) {
+    if (!n) return hipSuccess;
+    uint64_t head = 0;
+    if ((offset & 7) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const uint64_t npairs = n / 16;
+        if (npairs) {
+            const uint64_t blocks = (npairs + 255) / 256;
+            hipLaunchKernelGGL(synth_fill_words, dim3((uint32_t)(blocks < 8192 ? blocks : 8192)), dim3(256),
+                               0, s, reinterpret_cast<uint4*>(dst), seed, offset >> 3, npairs, variant);
+        }
+        head = npairs * 16;
+    }
+    if (head < n) {
+        const uint64_t rest = n - head;
+        const uint64_t blocks = (rest + 255) / 256;
+        hipLaunchKernelGGL(synth_fill_bytes, dim3((uint32_t)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s,
+                           dst + head, seed, offset + head, rest, variant);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace krk

@@ -1,0 +1,167 @@
+"""Device-resident batch helpers over the C ABI (used by bench.py and the GPU
+parity tests): an HBM arena of synthetic blobs and the batch calls on it."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._capi import check, krk_blob, krk_nodes, lib
+
+ALIGN = 256  # every blob starts 256-byte aligned in the arena
+
+
+class DeviceBuffer:
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib.krk_dev_alloc(max(int(nbytes), 1), C.byref(p)))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    def free(self):
+        if self.ptr:
+            lib.krk_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def to_host(self, dtype=np.uint8, count: int | None = None, offset: int = 0) -> np.ndarray:
+        it = np.dtype(dtype).itemsize
+        n = (self.nbytes - offset) // it if count is None else count
+        out = np.empty(n, dtype=dtype)
+        if n:
+            check(lib.krk_memcpy_d2h(out.ctypes.data, self.ptr + offset, n * it))
+        return out
+
+    def from_host(self, a: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(a)
+        if a.nbytes:
+            check(lib.krk_memcpy_h2d(self.ptr + offset, a.ctypes.data, a.nbytes))
+
+
+def device_count() -> int:
+    n = C.c_int()
+    check(lib.krk_device_count(C.byref(n)))
+    return n.value
+
+
+def set_device(d: int):
+    check(lib.krk_set_device(d))
+
+
+def synchronize():
+    check(lib.krk_synchronize())
+
+
+class BlobArena:
+    """Blobs laid out back to back in one HBM allocation (each 256 B aligned)."""
+
+    def __init__(self, lengths, piece_length, blob_ids=None, variant: int = 0, fill: bool = True,
+                 misalign: int = 0):
+        self.lengths = np.asarray(lengths, dtype=np.uint64)
+        n = len(self.lengths)
+        pls = np.broadcast_to(np.asarray(piece_length, dtype=np.int64), (n,))
+        self.piece_lengths = np.array(pls, dtype=np.int64)
+        self.blob_ids = np.arange(n, dtype=np.uint64) if blob_ids is None else np.asarray(blob_ids, np.uint64)
+        self.offsets = np.zeros(n, dtype=np.uint64)
+        o = 0
+        for i, L in enumerate(self.lengths):
+            self.offsets[i] = o + misalign  # misalign > 0 exercises the unaligned path
+            o += (int(L) + misalign + ALIGN - 1) // ALIGN * ALIGN
+        self.nbytes = max(o, 1)
+        self.buf = DeviceBuffer(self.nbytes)
+        self.n_pieces = np.array([lib.krk_num_pieces(int(L), int(p)) for L, p in
+                                  zip(self.lengths, self.piece_lengths)], dtype=np.uint64)
+        self.sums_off = np.zeros(n, dtype=np.uint64)
+        if n:
+            self.sums_off[1:] = np.cumsum(self.n_pieces)[:-1]
+        self.total_pieces = int(self.n_pieces.sum())
+        if fill:
+            for i in range(n):
+                self.fill(i, variant)
+            synchronize()
+
+    def fill(self, i: int, variant: int = 0):
+        check(lib.krk_synth_fill_dev(self.buf.ptr + int(self.offsets[i]), int(self.blob_ids[i]), 0,
+                                     int(self.lengths[i]), variant, None))
+
+    def put(self, i: int, data: np.ndarray):
+        self.buf.from_host(np.asarray(data, dtype=np.uint8), int(self.offsets[i]))
+
+    def blob_structs(self):
+        n = len(self.lengths)
+        arr = (krk_blob * max(n, 1))()
+        for i in range(n):
+            arr[i] = krk_blob(self.buf.ptr + int(self.offsets[i]), int(self.lengths[i]),
+                              int(self.piece_lengths[i]), int(self.sums_off[i]))
+        return arr
+
+    def data_ptrs(self):
+        n = len(self.lengths)
+        ptrs = (C.c_void_p * max(n, 1))(*[self.buf.ptr + int(o) for o in self.offsets])
+        lens = np.ascontiguousarray(self.lengths, dtype=np.uint64)
+        return ptrs, lens
+
+
+class BatchOutputs:
+    def __init__(self, arena: BlobArena):
+        self.sums = DeviceBuffer(max(arena.total_pieces, 1) * 4)
+        self.digests = DeviceBuffer(max(len(arena.lengths), 1) * 32)
+
+
+def piece_sums(arena: BlobArena, out: BatchOutputs, stream=None):
+    check(lib.krk_piece_sums_dev(arena.blob_structs(), len(arena.lengths), out.sums.ptr, stream))
+
+
+def sha256(arena: BlobArena, out: BatchOutputs, stream=None):
+    ptrs, lens = arena.data_ptrs()
+    check(lib.krk_sha256_dev(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), len(arena.lengths),
+                             out.digests.ptr, stream))
+
+
+def metainfo_digest(arena: BlobArena, out: BatchOutputs, stream=None):
+    check(lib.krk_metainfo_digest_dev(arena.blob_structs(), len(arena.lengths), out.sums.ptr,
+                                      out.digests.ptr, stream))
+
+
+def nodes_struct(labels, weights):
+    enc = [s.encode() for s in labels]
+    blob = b"".join(enc)
+    off = np.zeros(len(enc) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(e) for e in enc])
+    w = np.ascontiguousarray(weights, dtype=np.int64)
+    s = krk_nodes(blob, off.ctypes.data_as(C.POINTER(C.c_uint64)), w.ctypes.data_as(C.POINTER(C.c_int64)),
+                  len(labels))
+    return s, (blob, off, w)  # keep the backing arrays alive
+
+
+def ring_locations_dev(digests_dev: DeviceBuffer, n: int, labels, healthy, max_replica: int,
+                       locs_dev: DeviceBuffer, counts_dev: DeviceBuffer, stream=None):
+    s, keep = nodes_struct(labels, [100] * len(labels))
+    h = np.ascontiguousarray(healthy, dtype=np.uint8)
+    check(lib.krk_ring_locations_dev(digests_dev.ptr, n, C.byref(s), h.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                      max_replica, locs_dev.ptr, counts_dev.ptr, stream))
+    del keep
+
+
+class KernelTimer:
+    """hipEvent-based per-kernel device time (recorded on each kernel's stream)."""
+
+    def __enter__(self):
+        check(lib.krk_set_timing(1))
+        check(lib.krk_reset_kernel_stats())
+        return self
+
+    def __exit__(self, *a):
+        check(lib.krk_set_timing(0))
+
+    @staticmethod
+    def stats(kernel: str):
+        n = C.c_uint64()
+        ms = C.c_double()
+        check(lib.krk_kernel_stats(kernel.encode(), C.byref(n), C.byref(ms)))
+        return n.value, ms.value

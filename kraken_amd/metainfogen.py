@@ -1,0 +1,127 @@
+"""Host-side mirror of lib/metainfogen over the C ABI.
+
+* ``newPieceLengthConfig`` / ``pieceLengthConfig.get``: lib/metainfogen/config.go:48-80
+* ``Generator.Generate``: lib/metainfogen/generator.go:40-58 (stat -> piece length
+  -> NewMetaInfo over the cache file -> persist the _torrentmeta sidecar)
+* ``Generator.GenerateBatch``: the batch form used for whole-CAS regeneration
+  (SURVEY.md §8(f) row 2): one GPU pass over many cache files.
+
+The CAS store itself (lib/store) is out of scope; ``DirCAS`` is a minimal
+stand-in exposing the three calls Generate makes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import core
+from ._capi import check, krk_blob, lib
+
+
+class pieceLengthConfig:
+    def __init__(self, ranges):
+        self.ranges = ranges  # sorted [(fileSize, pieceLength)]
+
+    def get(self, file_size: int) -> int:
+        t = np.ascontiguousarray([a for a, _ in self.ranges], dtype=np.int64)
+        l = np.ascontiguousarray([b for _, b in self.ranges], dtype=np.int64)
+        return lib.krk_piece_length_for_size(t.ctypes.data_as(C.POINTER(C.c_int64)),
+                                              l.ctypes.data_as(C.POINTER(C.c_int64)), len(t), file_size)
+
+
+def newPieceLengthConfig(piece_length_by_file_size: dict) -> pieceLengthConfig:
+    if not piece_length_by_file_size:
+        raise ValueError("no piece lengths configured")
+    return pieceLengthConfig(sorted((int(a), int(b)) for a, b in piece_length_by_file_size.items()))
+
+
+class DirCAS:
+    """Minimal content-addressed cache: <root>/<hex>/data and <hex>/_torrentmeta
+    (cf. lib/store/base/file_entry.go:175-189)."""
+
+    def __init__(self, root: str):
+        self.root = root
+
+    def _dir(self, hex_: str) -> str:
+        return os.path.join(self.root, hex_)
+
+    def GetCacheFileStat(self, hex_: str) -> os.stat_result:
+        return os.stat(os.path.join(self._dir(hex_), "data"))
+
+    def GetCacheFileReader(self, hex_: str):
+        return open(os.path.join(self._dir(hex_), "data"), "rb")
+
+    def SetCacheFileMetadata(self, hex_: str, mi: core.MetaInfo) -> bool:
+        p = os.path.join(self._dir(hex_), "_torrentmeta")
+        b = mi.Serialize()
+        if os.path.exists(p) and open(p, "rb").read() == b:
+            return False
+        with open(p, "wb") as f:
+            f.write(b)
+        return True
+
+    def WriteCacheFile(self, data: bytes) -> core.Digest:
+        d = core.NewDigester().FromBytes(data)
+        os.makedirs(self._dir(d.Hex()), exist_ok=True)
+        with open(os.path.join(self._dir(d.Hex()), "data"), "wb") as f:
+            f.write(data)
+        return d
+
+
+class Generator:
+    def __init__(self, config: dict, cas):
+        try:
+            self.pieceLengthConfig = newPieceLengthConfig(config)
+        except ValueError as e:
+            raise ValueError(f"piece length config: {e}") from None
+        self.cas = cas
+
+    def Generate(self, d: core.Digest) -> None:
+        try:
+            info = self.cas.GetCacheFileStat(d.Hex())
+        except OSError as e:
+            raise IOError(f"cache stat: {e}") from None
+        try:
+            f = self.cas.GetCacheFileReader(d.Hex())
+        except OSError as e:
+            raise IOError(f"get cache file: {e}") from None
+        with f:
+            pl = self.pieceLengthConfig.get(info.st_size)
+            try:
+                mi = core.NewMetaInfo(d, f, pl)
+            except (ValueError, IOError) as e:
+                raise IOError(f"create metainfo: {e}") from None
+        try:
+            self.cas.SetCacheFileMetadata(d.Hex(), mi)
+        except OSError as e:
+            raise IOError(f"set metainfo: {e}") from None
+
+    def GenerateBatch(self, digests) -> list[core.MetaInfo]:
+        """Generate for many cache files in one pipelined GPU pass."""
+        datas, blobs, off = [], [], 0
+        for d in digests:
+            with self.cas.GetCacheFileReader(d.Hex()) as f:
+                b = np.frombuffer(f.read(), dtype=np.uint8)
+            pl = self.pieceLengthConfig.get(b.size)
+            datas.append((d, b, pl, off))
+            off += int(lib.krk_num_pieces(b.size, pl))
+        arr = (krk_blob * max(len(datas), 1))()
+        for i, (d, b, pl, o) in enumerate(datas):
+            arr[i] = krk_blob(b.ctypes.data if b.size else None, b.size, pl, o)
+        sums = np.zeros(max(off, 1), dtype=np.uint32)
+        check(lib.krk_piece_sums_host(arr, len(datas), sums.ctypes.data_as(C.POINTER(C.c_uint32))))
+        out = []
+        for d, b, pl, o in datas:
+            n = int(lib.krk_num_pieces(b.size, pl))
+            s = sums[o:o + n].copy() if n else None
+            ih = core._info_hash(pl, s if s is not None else np.zeros(0, np.uint32), d.Hex(), b.size)
+            mi = core.MetaInfo(pl, s, d.Hex(), b.size, d, ih)
+            self.cas.SetCacheFileMetadata(d.Hex(), mi)
+            out.append(mi)
+        return out
+
+
+def New(config: dict, cas) -> Generator:
+    return Generator(config, cas)

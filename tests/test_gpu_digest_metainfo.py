@@ -1,0 +1,174 @@
+"""GPU parity: SHA-256 digests (core.Digester, core/digester.go:28-72) and
+NewMetaInfo / InfoHash (core/metainfo.go:53-79) through the C ABI vs hashlib and
+the CPU oracle, bit-exact.  KATs from core/digester_test.go:27-28 and
+core/metainfo_test.go:61-76."""
+import ctypes as C
+import hashlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+from kraken_amd import core
+from kraken_amd import device as D
+from kraken_amd._capi import check, lib
+
+pytestmark = pytest.mark.gpu
+
+SHA_LENS = list(range(0, 130)) + [183, 184, 191, 192, 255, 256, 1000, 4096, 65535, 65536, 1 << 20, (1 << 20) + 55]
+
+
+def test_digester_kat(gpu):
+    d = core.NewDigester()
+    assert d.FromBytes(b"test").Hex() == "9f86d081884c7d659a2feaa0c55ad015a3bf4f1b2b0b822cd15d6c15b0f00a08"
+    assert core.NewDigester().Digest().String() == core.DigestEmptyTar
+
+
+def test_digester_reader_and_tee(gpu):
+    data = os.urandom(300000)
+    assert core.NewDigester().FromReader(io.BytesIO(data)).Hex() == hashlib.sha256(data).hexdigest()
+    d = core.NewDigester()
+    r = d.Tee(io.BytesIO(data))
+    w = io.BytesIO()
+    while True:
+        b = r.read(32768)
+        if not b:
+            break
+        w.write(b)
+    assert w.getvalue() == data
+    assert d.Digest().Hex() == hashlib.sha256(data).hexdigest()
+
+
+def test_digester_no_reset(gpu):
+    """Digest() does not reset; FromBytes twice hashes the concatenation."""
+    d = core.NewDigester()
+    a, b = os.urandom(100), os.urandom(70000)
+    assert d.FromBytes(a).Hex() == hashlib.sha256(a).hexdigest()
+    assert d.FromBytes(b).Hex() == hashlib.sha256(a + b).hexdigest()
+    assert d.Digest().Hex() == hashlib.sha256(a + b).hexdigest()
+
+
+def test_digester_large_chunked(gpu):
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, size=40 << 20, dtype=np.uint8).tobytes()
+    d = core.NewDigester()
+    pos = 0
+    for n in rng.integers(1, 3 << 20, size=100):
+        d._write(data[pos:pos + int(n)])
+        pos += int(n)
+        if pos >= len(data):
+            break
+    d._write(data[pos:])
+    assert d.Digest().Hex() == hashlib.sha256(data).hexdigest()
+
+
+def test_sha256_dev_batch_lengths(gpu, orc):
+    arena = D.BlobArena(SHA_LENS, 4096, blob_ids=range(len(SHA_LENS)))
+    out = D.BatchOutputs(arena)
+    D.sha256(arena, out)
+    D.synchronize()
+    got = out.digests.to_host(np.uint8, 32 * len(SHA_LENS)).reshape(-1, 32)
+    for i, L in enumerate(SHA_LENS):
+        ref = hashlib.sha256(orc.synth(i, L).tobytes()).digest()
+        assert bytes(got[i]) == ref, L
+
+
+@pytest.mark.parametrize("misalign", [1, 4, 8])
+def test_sha256_dev_unaligned(gpu, orc, misalign):
+    lens = [0, 55, 56, 64, 65, 1000, 100003]
+    arena = D.BlobArena(lens, 4096, blob_ids=range(20, 27), misalign=misalign)
+    out = D.BatchOutputs(arena)
+    D.sha256(arena, out)
+    D.synchronize()
+    got = out.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+    for i, L in enumerate(lens):
+        assert bytes(got[i]) == hashlib.sha256(orc.synth(20 + i, L).tobytes()).digest(), L
+
+
+def test_sha256_host_batch_windowed(gpu):
+    rng = np.random.default_rng(11)
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in (0, 1, 64, 1000, 3 << 20, 5 << 20 + 3)]
+    ptrs = (C.c_void_p * len(datas))(*[d.ctypes.data if d.size else None for d in datas])
+    lens = np.array([d.size for d in datas], dtype=np.uint64)
+    out = np.zeros((len(datas), 32), dtype=np.uint8)
+    os.environ["KRK_WINDOW_MB"] = "1"
+    try:
+        check(lib.krk_sha256_host(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), len(datas),
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    finally:
+        del os.environ["KRK_WINDOW_MB"]
+    for i, d in enumerate(datas):
+        assert bytes(out[i]) == hashlib.sha256(d.tobytes()).digest(), i
+
+
+def test_metainfo_digest_batch(gpu, orc):
+    """Both products in one call (the two passes of uploader.verify + Generate)."""
+    lens = [0, 1, 1000, 4 << 20, (4 << 20) + 1, 9_999_999]
+    arena = D.BlobArena(lens, 4 << 20, blob_ids=range(200, 206))
+    out = D.BatchOutputs(arena)
+    D.metainfo_digest(arena, out)
+    D.synchronize()
+    sums = out.sums.to_host(np.uint32, arena.total_pieces)
+    dg = out.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+    for i, L in enumerate(lens):
+        data = orc.synth(200 + i, L)
+        assert bytes(dg[i]) == orc.sha256(data)
+        ref = orc.calc_piece_sums(data, 4 << 20)[1]
+        o = int(arena.sums_off[i])
+        assert np.array_equal(sums[o:o + len(ref)], ref)
+
+
+@pytest.mark.parametrize("size,pl", [(10, 3), (8, 2), (256, 8), (236, 4194304), (0, 4), (1 << 20, 4096),
+                                     ((64 << 20) + 5, 4 << 20), (100_000, 100_000)])
+def test_new_metainfo_matches_oracle(gpu, orc, size, pl):
+    """NewMetaInfo over a reader (core/fixtures.go SizedBlobFixture shape)."""
+    data = orc.synth(size, size, variant=1).tobytes()
+    d = core.NewSHA256DigestFromHex(hashlib.sha256(data).hexdigest())
+    mi = core.NewMetaInfo(d, io.BytesIO(data), pl)
+    length, ref = orc.calc_piece_sums(data, pl)
+    assert mi.Length() == length == size
+    assert np.array_equal(mi.PieceSums(), ref)
+    assert bytes(mi.InfoHash()) == orc.info_hash(pl, ref, d.Hex(), size)
+    for i in range(-1, mi.NumPieces() + 1):
+        assert mi.GetPieceLength(i) == orc.get_piece_length(size, pl, len(ref), i)
+
+
+def test_metainfo_get_piece_length_table(gpu):
+    """core/metainfo_test.go:25-46."""
+    cases = [(10, 3, 0, 3), (10, 3, 3, 1), (8, 2, 3, 2), (10, 3, 1, 3), (10, 3, 4, 0), (10, 3, -1, 0)]
+    for size, pl, i, want in cases:
+        data = os.urandom(size)
+        mi = core.NewMetaInfo(core.NewDigester().FromBytes(data), data, pl)
+        assert mi.GetPieceLength(i) == want
+
+
+def test_metainfo_serialization_roundtrip(gpu):
+    data = os.urandom(256)
+    d = core.NewDigester().FromBytes(data)
+    mi = core.NewMetaInfo(d, data, 8)
+    back = core.DeserializeMetaInfo(mi.Serialize())
+    assert back.Digest() == d and back.InfoHash() == mi.InfoHash()
+
+
+def test_new_metainfo_bad_piece_length(gpu):
+    with pytest.raises(ValueError, match="piece length must be positive"):
+        core.NewMetaInfo(core.NewDigester().FromBytes(b"x"), b"x", 0)
+
+
+def test_generator_generate_and_batch(gpu, orc, tmp_path):
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path))
+    blobs = [os.urandom(n) for n in (0, 17, 3 << 20, (5 << 20) + 1)]
+    ds = [cas.WriteCacheFile(b) for b in blobs]
+    g = metainfogen.New({0: 1 << 20, 4 << 20: 4 << 20}, cas)
+    for d, b in zip(ds, blobs):
+        g.Generate(d)
+        mi = core.DeserializeMetaInfo(open(tmp_path / d.Hex() / "_torrentmeta", "rb").read())
+        pl = 1 << 20 if len(b) < 4 << 20 else 4 << 20
+        ref = orc.calc_piece_sums(b, pl)[1]
+        assert bytes(mi.InfoHash()) == orc.info_hash(pl, ref, d.Hex(), len(b))
+    mis = g.GenerateBatch(ds)
+    for mi, d, b in zip(mis, ds, blobs):
+        pl = mi.PieceLength()
+        assert bytes(mi.InfoHash()) == orc.info_hash(pl, orc.calc_piece_sums(b, pl)[1], d.Hex(), len(b))

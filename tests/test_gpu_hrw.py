@@ -1,0 +1,127 @@
+"""GPU parity: lib/hrw scores/orders and hashring Locations through the C ABI vs
+the CPU oracle.  Scores must match bit for bit (fp64, Go math.Log restated, no
+FMA).  Distribution properties follow lib/hrw/rendezvous_test.go:100-274."""
+import os
+
+import numpy as np
+import pytest
+
+from kraken_amd import hashring, hrw
+from kraken_amd import device as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(rng, n, nbytes):
+    return [rng.bytes(nbytes).hex() for _ in range(n)]
+
+
+@pytest.mark.parametrize("n_nodes", [1, 3, 5, 16, 64])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_scores_and_orders_match_oracle(gpu, orc, n_nodes, weighted):
+    rng = np.random.default_rng(n_nodes * 2 + weighted)
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(n_nodes)]
+    weights = [[100, 200, 400, 800][i % 4] if weighted else 100 for i in range(n_nodes)]
+    rh = hrw.NewRendezvousHash()
+    for l, w in zip(labels, weights):
+        rh.AddNode(l, w)
+    keys = _keys(rng, 300, 2) + _keys(rng, 100, 1) + _keys(rng, 100, 32) + _keys(rng, 50, 64)
+    order = rh.GetOrderedNodesBatch(keys, n_nodes)
+    scores = rh.Scores(keys)
+    for i, k in enumerate(keys):
+        ref_o, ref_s = orc.hrw_ordered(k, labels, weights, with_scores=True)
+        assert order[i].tolist() == ref_o, k
+        assert scores[i].tobytes() == np.asarray(ref_s, dtype=np.float64).tobytes(), k
+
+
+def test_survey_sanity_vector(gpu):
+    """dummy-origin-master0{1,2,3}-zone2:80, weight 100."""
+    rh = hrw.NewRendezvousHash()
+    for i in (1, 2, 3):
+        rh.AddNode(f"dummy-origin-master0{i}-zone2:80", 100)
+    lab = lambda k: [n.Label[-9:-8] for n in rh.GetOrderedNodes(k, 3)]
+    assert lab("e3b0") == ["3", "2", "1"]
+    assert lab("0000") == ["1", "3", "2"]
+    assert lab("ffff") == ["1", "3", "2"]
+
+
+def test_get_ordered_nodes_n_and_invalid_hex(gpu):
+    rh = hrw.NewRendezvousHash()
+    for i, w in enumerate([100, 200, 400, 800]):
+        rh.AddNode(str(i), w)
+    assert len(rh.GetOrderedNodes("abcd", 2)) == 2
+    assert len(rh.GetOrderedNodes("abcd", 10)) == 4
+    assert np.isnan(rh.Nodes[0].Score("zz"))  # rendezvous.go:154-157
+    assert [n.Label for n in rh.GetOrderedNodes("xyz", 4)] == ["0", "1", "2", "3"]
+
+
+def test_key_distribution_weighted(gpu):
+    """rendezvous_test.go:145-148: keys split ~ weights 100/200/400/800 (+-0.1)."""
+    rh = hrw.NewRendezvousHash()
+    ws = [100, 200, 400, 800]
+    for i, w in enumerate(ws):
+        rh.AddNode(str(i), w)
+    rng = np.random.default_rng(0)
+    keys = _keys(rng, 20000, 64)
+    first = rh.GetOrderedNodesBatch(keys, 1)[:, 0]
+    frac = np.bincount(first, minlength=4) / len(keys)
+    assert np.all(np.abs(frac - np.array(ws) / 1500.0) < 0.1 * np.array(ws) / 1500.0 + 0.01), frac
+
+
+def test_add_remove_node_stability(gpu):
+    """rendezvous_test.go:150-193: removing a node only moves its own keys."""
+    rh = hrw.NewRendezvousHash()
+    for i, w in enumerate([100, 200, 400, 800]):
+        rh.AddNode(str(i), w)
+    rng = np.random.default_rng(9)
+    keys = _keys(rng, 5000, 32)
+    before = [rh.Nodes[j].Label for j in rh.GetOrderedNodesBatch(keys, 1)[:, 0]]
+    rh.RemoveNode("1")
+    after = [rh.Nodes[j].Label for j in rh.GetOrderedNodesBatch(keys, 1)[:, 0]]
+    for b, a in zip(before, after):
+        if b != "1":
+            assert a == b
+
+
+@pytest.mark.parametrize("n_nodes,max_replica", [(3, 3), (5, 2), (16, 3), (64, 2), (4, 0), (4, 10)])
+def test_ring_locations_match_oracle(gpu, orc, n_nodes, max_replica):
+    rng = np.random.default_rng(n_nodes + 31 * max_replica)
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(n_nodes)]
+    for healthy in (np.ones(n_nodes, np.uint8), (rng.random(n_nodes) < 0.75).astype(np.uint8),
+                    np.zeros(n_nodes, np.uint8)):
+        ring = hashring.Ring(labels, [l for l, h in zip(labels, healthy) if h], max_replica)
+        digests = rng.integers(0, 256, size=(2000, 32), dtype=np.uint8)
+        locs, counts = ring.LocationsBatch(digests)
+        for i in range(len(digests)):
+            key = bytes(digests[i, :2]).hex()
+            order = orc.hrw_ordered(key, labels, [100] * n_nodes)
+            ref = orc.ring_locations(order, healthy, max_replica)
+            assert locs[i, : counts[i]].tolist() == ref, (i, key)
+
+
+def test_ring_locations_dev_full_table(gpu, orc):
+    """Device-resident 65,536-shard table + gather (config C5 path) vs oracle."""
+    n_nodes, max_replica = 16, 3
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(n_nodes)]
+    rng = np.random.default_rng(77)
+    healthy = (rng.random(n_nodes) < 0.75).astype(np.uint8)
+    n = 50000
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    lbuf = D.DeviceBuffer(n * max_replica * 4)
+    cbuf = D.DeviceBuffer(n)
+    D.ring_locations_dev(dbuf, n, labels, healthy, max_replica, lbuf, cbuf)
+    D.synchronize()
+    locs = lbuf.to_host(np.int32, n * max_replica).reshape(n, max_replica)
+    counts = cbuf.to_host(np.uint8, n)
+    cache = {}
+    for i in range(0, n, 7):
+        key = bytes(digests[i, :2]).hex()
+        if key not in cache:
+            cache[key] = orc.ring_locations(orc.hrw_ordered(key, labels, [100] * n_nodes), healthy, max_replica)
+        assert locs[i, : counts[i]].tolist() == cache[key]
+    ring = hashring.Ring(labels, [l for l, h in zip(labels, healthy) if h], max_replica)
+    from kraken_amd import core
+    d = core.NewSHA256DigestFromHex(bytes(digests[0]).hex())
+    assert ring.Locations(d) == [labels[j] for j in locs[0, : counts[0]]]

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One gpurun session: GPU parity tests, then the perf probe; stops at the first
+# crash/timeout (exit codes other than 0/1 from a step).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name" >&2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >&2
+  tail -5 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    probe0) step probe_v0 300 python tools/probe_perf.py --variant 0 ;;
+    probe1) step probe_v1 300 python tools/probe_perf.py --variant 1 --sha none ;;
+    bench) step bench 900 python bench.py ;;
+  esac
+done
