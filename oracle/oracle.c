@@ -618,6 +618,7 @@ typedef struct {
     uint8_t* digests;
     uint32_t* sums;
     const uint64_t* sums_off;
+    uint64_t n_jobs;  /* n * repeats: job q processes blob q % n */
     volatile uint64_t next;
     pthread_barrier_t bar;
     double t0, t1;
@@ -672,9 +673,9 @@ static void* bl_worker(void* arg) {
     bl_job* J = (bl_job*)arg;
     pthread_barrier_wait(&J->bar);
     for (;;) {
-        uint64_t b = __atomic_fetch_add(&J->next, 1, __ATOMIC_RELAXED);
-        if (b >= J->n) break;
-        bl_blob(J, b);
+        uint64_t q = __atomic_fetch_add(&J->next, 1, __ATOMIC_RELAXED);
+        if (q >= J->n_jobs) break;
+        bl_blob(J, q % J->n);
     }
     pthread_barrier_wait(&J->bar);
     return NULL;
@@ -688,9 +689,10 @@ static void* fill_worker(void* a) {
 }
 
 double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
-                        int64_t piece_len, int n_threads, int fast,
+                        int64_t piece_len, int n_threads, int fast, uint64_t repeats,
                         uint8_t* digests_out, uint32_t* sums_out, const uint64_t* sums_off) {
     if (n_threads < 1) n_threads = 1;
+    if (repeats < 1) repeats = 1;
     bl_job J;
     memset(&J, 0, sizeof J);
     J.bufs = (uint8_t**)calloc(n_blobs, sizeof(uint8_t*));
@@ -708,6 +710,7 @@ double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint6
     }
     J.lengths = lengths; J.n = n_blobs; J.piece_len = piece_len; J.fast = fast;
     J.digests = digests_out; J.sums = sums_out; J.sums_off = sums_off; J.next = 0;
+    J.n_jobs = n_blobs * repeats;
     pthread_barrier_init(&J.bar, NULL, (unsigned)n_threads + 1);
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)n_threads);
     for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, bl_worker, &J);

@@ -1,0 +1,72 @@
+"""Host-side logic of the mirror API (no GPU): digest parsing/validation, InfoHash
+hex, MetaInfo JSON, metainfogen config -- with the reference's error strings."""
+import numpy as np
+import pytest
+
+from kraken_amd import core, metainfogen
+
+
+def test_digest_parse_and_validate():
+    h = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+    d = core.NewSHA256DigestFromHex(h)
+    assert d.String() == core.DigestEmptyTar and d.Algo() == "sha256" and d.ShardID() == "e3b0"
+    assert core.ParseSHA256Digest(core.DigestEmptyTar) == d
+    with pytest.raises(ValueError, match="invalid sha256: expected 64 characters"):
+        core.NewSHA256DigestFromHex("abc")
+    with pytest.raises(ValueError, match="invalid sha256: hex"):
+        core.NewSHA256DigestFromHex("z" * 64)
+    with pytest.raises(ValueError, match="invalid digest: empty"):
+        core.ParseSHA256Digest("")
+    with pytest.raises(ValueError, match="expected '<algo>:<hex>'"):
+        core.ParseSHA256Digest("sha256")
+    with pytest.raises(ValueError, match="invalid digest algo"):
+        core.ParseSHA256Digest("md5:" + h)
+
+
+def test_infohash_hex():
+    ih = core.NewInfoHashFromHex("85b978c4377625b3963df406d0dd3a1da5a7d9c3")
+    assert ih.Hex() == "85b978c4377625b3963df406d0dd3a1da5a7d9c3"
+    with pytest.raises(ValueError, match="expected 40 characters"):
+        core.NewInfoHashFromHex("00")
+
+
+def test_metainfo_backwards_compatibility_kat():
+    """core/metainfo_test.go:61-76 (production agent metainfo -> same info hash)."""
+    raw = (b'{"Info":{"PieceLength":4194304,"PieceSums":[2131691452],"Name":'
+           b'"289314c356bc2a19802c3e31505506db30ea81a0bcaea4ec3e079524c8ac3cf5","Length":236},'
+           b'"Announce":"","AnnounceList":null,"CreationDate":0,"Comment":"","CreatedBy":""}')
+    mi = core.DeserializeMetaInfo(raw)
+    assert mi.InfoHash() == core.NewInfoHashFromHex("85b978c4377625b3963df406d0dd3a1da5a7d9c3")
+    assert mi.NumPieces() == 1 and mi.GetPieceLength(0) == 236 and mi.GetPieceLength(1) == 0
+    back = core.DeserializeMetaInfo(mi.Serialize())
+    assert back.InfoHash() == mi.InfoHash()
+
+
+def test_metainfo_serialization_limit():
+    """core/metainfo_test.go:78-120: 100 GB / 2 MB pieces stays under 512 MB of JSON."""
+    n = (100 << 30) // (2 << 20)
+    sums = np.random.default_rng(0).integers(0, 2 ** 32, size=n, dtype=np.uint64).astype(np.uint32)
+    mi = core.MetaInfo(2 << 20, sums, "6422b52513a39399598494bdb7471211890cd13c271fb5c11c5ba6538ed7578c",
+                       100 << 30, None, None)
+    assert len(mi.Serialize()) < 512 << 20
+
+
+def test_deserialize_errors():
+    with pytest.raises(ValueError, match="json"):
+        core.DeserializeMetaInfo(b"{")
+    with pytest.raises(ValueError, match="parse name"):
+        core.DeserializeMetaInfo(b'{"Info":{"PieceLength":1,"PieceSums":[],"Name":"x","Length":0}}')
+
+
+def test_piece_length_config():
+    """lib/metainfogen/config_test.go:23-38."""
+    c = metainfogen.newPieceLengthConfig({0: 1 << 20, 2 << 30: 4 << 20, 4 << 30: 8 << 20})
+    assert c.get(1 << 30) == 1 << 20
+    assert c.get(2 << 30) == 4 << 20
+    assert c.get(3 << 30) == 4 << 20
+    assert c.get(4 << 30) == 8 << 20
+    assert c.get(8 << 30) == 8 << 20
+    with pytest.raises(ValueError, match="no piece lengths configured"):
+        metainfogen.newPieceLengthConfig({})
+    with pytest.raises(ValueError, match="piece length config: no piece lengths configured"):
+        metainfogen.New({}, None)
