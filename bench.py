@@ -46,10 +46,27 @@ def _env_int(k, d):
         return d
 
 
+def host_cores() -> int:
+    """CPUs this process may actually use: the affinity mask capped by the cgroup
+    CPU quota and by OMP_NUM_THREADS (GPU boxes expose the whole machine in the
+    mask but grant a 16-CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return n
+
+
 def cpu_baseline(n_bytes_blob, piece, target_s, want_check):
     from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
     O.build()
-    threads = len(os.sched_getaffinity(0))
+    threads = host_cores()
     m = 2 * threads
     ids = list(range(m))
     lens = [n_bytes_blob] * m
@@ -62,7 +79,7 @@ def cpu_baseline(n_bytes_blob, piece, target_s, want_check):
     info = {"value": round(gbps, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": (f"{m} x {n_bytes_blob >> 20} MiB synthetic blobs x {reps} passes ({t:.1f} s): "
                        "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL), 32 KiB chunks, one blob per "
-                       f"thread, {threads} threads (all host cores visible), oracle/oracle.c"),
+                       f"thread, {threads} threads (the host CPU share of this GPU), oracle/oracle.c"),
             "seconds": round(t, 2), "have_shani": bool(O.lib().orc_have_shani()),
             "have_clmul": bool(O.lib().orc_have_clmul())}
     return info, dg, sums

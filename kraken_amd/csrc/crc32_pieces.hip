@@ -62,17 +62,20 @@ __device__ __forceinline__ uint32_t step64(uint32_t c, const u32x4& v0, const u3
     return seg16(c, v3, T);
 }
 
-// Bytes [p, p+n) into register c, n <= kSeg; p is 4-byte aligned when aligned4.
+// Bytes [p, p+n) into register c, n <= kSeg, any alignment (see load_bytes64).
 template <int R>
-__device__ __forceinline__ uint32_t seg_tail(uint32_t c, uint64_t p, uint32_t n, bool aligned4,
-                                             const Tab<R>& T) {
-    uint32_t i = 0;
-    if (aligned4) {
-        gptr<uint32_t> w = as_global<uint32_t>(p);
-        for (; i + 4 <= n; i += 4) c = T.word(c ^ w[i / 4]);
+__device__ __forceinline__ uint32_t seg_tail(uint32_t c, uint64_t p, uint32_t n, const Tab<R>& T) {
+    uint32_t w[16];
+    load_bytes64(p, n, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int keep = (int)n - 4 * j;
+        if (keep >= 4) {
+            c = T.word(c ^ w[j]);
+        } else if (keep > 0) {
+            for (int b = 0; b < keep; ++b) c = T.byte(c, (w[j] >> (8 * b)) & 0xFF);
+        }
     }
-    gptr<uint8_t> b = as_global<uint8_t>(p);
-    for (; i < n; ++i) c = T.byte(c, b[i]);
     return c;
 }
 
@@ -133,19 +136,19 @@ crc_items_kernel(const CrcItem* __restrict__ items, uint32_t n_items,
             if (ts < len) {
                 const uint32_t nb = min(kSeg, len - ts);
                 c = gap_shift<RG>(c, G);
-                c = seg_tail(c, base + ts, nb, true, T);
+                c = seg_tail(c, base + ts, nb, T);
                 end = ts + nb;
             }
         } else {
             // Unaligned run (odd piece lengths, caller-provided pointers): same lane
-            // structure, byte loads.
+            // structure, aligned-dword loads re-assembled in registers.
             const uint32_t nsteps = (len + kStep - 1) / kStep;
             for (uint32_t s = 0; s < nsteps; ++s) {
                 const uint32_t ss = s * kStep + lane * kSeg;
                 if (ss < len) {
                     const uint32_t nb = min(kSeg, len - ss);
                     c = gap_shift<RG>(c, G);
-                    c = seg_tail(c, base + ss, nb, false, T);
+                    c = seg_tail(c, base + ss, nb, T);
                     end = ss + nb;
                 }
             }

@@ -21,4 +21,26 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// Bytes [a, a+n) (n <= 64, any alignment) as 16 little-endian words, zero padded
+// past n.  Only dword-ALIGNED loads are issued, and only for dwords holding at
+// least one requested byte, so nothing outside the run's pages is touched and no
+// misaligned access is ever formed (the byte-wise form lets the compiler fuse
+// odd-address 16-bit loads); the words are re-assembled with v_alignbit.
+__device__ __forceinline__ void load_bytes64(uint64_t a, uint32_t n, uint32_t out[16]) {
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    const uint32_t nd = n ? (uint32_t)(((a + n - 1) >> 2) - (a >> 2) + 1) : 0;  // <= 17
+    gptr<uint32_t> d = as_global<uint32_t>(a & ~uint64_t(3));
+    uint32_t raw[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) raw[k] = (uint32_t)k < nd ? d[k] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint32_t w = __builtin_amdgcn_alignbit(raw[j + 1], raw[j], sh);
+        const int keep = (int)n - 4 * j;  // bytes of word j inside the run
+        if (keep <= 0) w = 0;
+        else if (keep < 4) w &= (1u << (8 * keep)) - 1;
+        out[j] = w;
+    }
+}
+
 }  // namespace krk

@@ -766,7 +766,8 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
     // crc32.Update(crc, IEEETable, p) = ~raw(~crc, p): one piece seeded with ~crc.
     B.add(items, reinterpret_cast<uint64_t>(d_buf), 0, n, n, n, 0, ~crc);
     int r = run_items(D, items, d_sum, s);
-    if (!r && hipMemcpyAsync(out, d_sum, 4, hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(out, d_sum, 4, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
     hipFreeAsync(d_buf, s);
     hipFreeAsync(d_sum, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
@@ -793,7 +794,8 @@ int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, u
         hipError_t e = launch_crc_verify(d_sums, static_cast<const uint32_t*>(d_exp), d_ok, (uint32_t)np, s);
         if (e != hipSuccess) { set_error(KRK_EHIP, "verify launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
-    if (!r && hipMemcpyAsync(ok_out_host, d_ok, np, hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "verify sync"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(ok_out_host, d_ok, np, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
     hipFreeAsync(d_sums, s);
     hipFreeAsync(d_ok, s);
     if (d_exp) hipFreeAsync(d_exp, s);
@@ -897,8 +899,8 @@ int krk_digester_sum(krk_digester* d, uint8_t out32[32]) {
     memcpy(j.h, kIV, sizeof kIV);
     r = run_jobs(d->D, jobs, d->d_dig, d->d_state, s);
     if (r) return r;
-    KRK_HIP(hipMemcpyAsync(out32, d->d_dig, 32, hipMemcpyDeviceToHost, s));
     KRK_HIP(hipStreamSynchronize(s));
+    KRK_HIP(hipMemcpy(out32, d->d_dig, 32, hipMemcpyDeviceToHost));
     return KRK_OK;
 }
 
@@ -1023,9 +1025,11 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
         hipError_t e = n_out ? timed(K_HRW, s, [&] { return launch_hrw_order(a, s); }) : hipSuccess;
         if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
-    if (!r && n_out && hipMemcpyAsync(order_out, d_order, n_keys * n_out * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+    // Copy-out: drain the stream, then blocking copies into the caller's (pageable) memory.
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "hrw sync"); r = KRK_EHIP; }
+    if (!r && n_out && hipMemcpy(order_out, d_order, n_keys * n_out * 4, hipMemcpyDeviceToHost) != hipSuccess)
         r = KRK_EHIP;
-    if (!r && scores_out && hipMemcpyAsync(scores_out, d_sc, n_keys * N * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (!r && scores_out && hipMemcpy(scores_out, d_sc, n_keys * N * 8, hipMemcpyDeviceToHost) != hipSuccess)
         r = KRK_EHIP;
     free_nodes(dn, s);
     for (void* p : {d_kb, d_koff, d_bad, static_cast<void*>(d_order), static_cast<void*>(d_sc)})
@@ -1071,8 +1075,9 @@ int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* no
     int r = hrw_table(D, kb, koff, bad, nodes, healthy, max_replica, row_out, &d_locs, &d_counts, s);
     std::vector<int32_t> tl(shards.size() * row_out);
     std::vector<uint8_t> tc(shards.size());
-    if (!r && hipMemcpyAsync(tl.data(), d_locs, tl.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
-    if (!r && hipMemcpyAsync(tc.data(), d_counts, tc.size(), hipMemcpyDeviceToHost, s) != hipSuccess) r = KRK_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "ring sync"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(tl.data(), d_locs, tl.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
+    if (!r && hipMemcpy(tc.data(), d_counts, tc.size(), hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
     if (d_locs) hipFreeAsync(d_locs, s);
     if (d_counts) hipFreeAsync(d_counts, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "ring sync"); r = KRK_EHIP; }

@@ -19,6 +19,10 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     probe0) step probe_v0 300 python tools/probe_perf.py --variant 0 ;;
     probe1) step probe_v1 300 python tools/probe_perf.py --variant 1 --sha none ;;
+    shaA) step probe_sha0 300 python tools/probe_perf.py --sha-variant 0 --crc-gb 1 --sha 1024:8,16384:1 ;;
+    shaB) step probe_sha1 300 python tools/probe_perf.py --sha-variant 1 --crc-gb 1 --sha 64:8,1024:8,16384:1 ;;
+    c2split) step probe_c2 300 python tools/probe_perf.py --c2 ;;
+    benchsmall) step bench_small 300 python bench.py --workload small --cpu-seconds 3 ;;
     bench) step bench 900 python bench.py ;;
   esac
 done

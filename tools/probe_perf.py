@@ -33,6 +33,23 @@ def crc(nbytes_gb: float, blob_mb: int, piece: int, reps: int):
             "kernel_ms": ms / max(k, 1), "kernel_GBps": total / (ms / max(k, 1) / 1e3) / 1e9}
 
 
+def crc_concurrent(n: int, mb: int, piece: int):
+    """C2-sized arena: CRC alone, SHA alone, then both via metainfo_digest."""
+    arena = D.BlobArena([mb << 20] * n, piece)
+    out = D.BatchOutputs(arena)
+    res = {"what": "c2_split", "blobs": n, "mb": mb}
+    for name, fn in (("crc_alone", D.piece_sums), ("sha_alone", D.sha256), ("both", D.metainfo_digest)):
+        with D.KernelTimer():
+            t0 = time.perf_counter()
+            fn(arena, out)
+            D.synchronize()
+            t1 = time.perf_counter()
+            k1, ms1 = D.KernelTimer.stats("crc32_pieces")
+            k2, ms2 = D.KernelTimer.stats("sha256_multi")
+        res[name] = {"wall_ms": round((t1 - t0) * 1e3, 2), "crc_ms": round(ms1, 3), "sha_ms": round(ms2, 2)}
+    return res
+
+
 def sha(streams: int, mb: int):
     arena = D.BlobArena([mb << 20] * streams, 1 << 20)
     out = D.BatchOutputs(arena)
@@ -52,10 +69,16 @@ if __name__ == "__main__":
     ap.add_argument("--crc-gb", type=float, default=16)
     ap.add_argument("--sha", default="64:8,1024:8,4096:4,16384:1")
     ap.add_argument("--variant", default="0")
+    ap.add_argument("--sha-variant", default="1")
+    ap.add_argument("--c2", action="store_true")
     a = ap.parse_args()
     os.environ["KRK_CRC_VARIANT"] = a.variant
+    os.environ["KRK_SHA_VARIANT"] = a.sha_variant
     D.set_device(0)
     res = []
+    if a.c2:
+        print(json.dumps(crc_concurrent(1000, 100, 4 << 20)), flush=True)
+        sys.exit(0)
     res.append(crc(a.crc_gb, 100, 4 << 20, 3))
     print(json.dumps(res[-1]), flush=True)
     res.append(crc(4, 256, 256 << 10, 3))
