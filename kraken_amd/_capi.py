@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libkraken_hip.so")
+LIB_PATH = os.environ.get("KRK_LIB_PATH") or os.path.join(_HERE, "lib", "libkraken_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip.h")
 
 KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX = 0, -1, -2, -3, -4, -5, -6

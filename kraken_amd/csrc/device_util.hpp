@@ -26,13 +26,31 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // least one requested byte, so nothing outside the run's pages is touched and no
 // misaligned access is ever formed (the byte-wise form lets the compiler fuse
 // odd-address 16-bit loads); the words are re-assembled with v_alignbit.
-__device__ __forceinline__ void load_bytes64(uint64_t a, uint32_t n, uint32_t out[16]) {
+// KRK_BOUNDS_CHECK (debug builds only): every global access is checked against
+// the caller's legitimate byte range [lo, hi); violations are printed and skipped.
+#ifdef KRK_BOUNDS_CHECK
+__device__ __forceinline__ bool krk_in_range(uint64_t addr, uint32_t size, uint64_t lo, uint64_t hi,
+                                             int site) {
+    if (addr >= lo && addr + size <= hi) return true;
+    printf("KRK_BOUNDS site=%d addr=0x%llx size=%u lo=0x%llx hi=0x%llx block=%u thread=%u\n", site,
+           (unsigned long long)addr, size, (unsigned long long)lo, (unsigned long long)hi, blockIdx.x,
+           threadIdx.x);
+    return false;
+}
+#define KRK_GUARD(addr, size, lo, hi, site) krk_in_range((addr), (size), (lo), (hi), (site))
+#else
+#define KRK_GUARD(addr, size, lo, hi, site) true
+#endif
+
+__device__ __forceinline__ void load_bytes64(uint64_t a, uint32_t n, uint32_t out[16], uint64_t lo = 0,
+                                             uint64_t hi = ~0ull) {
     const uint32_t sh = (uint32_t)(a & 3) * 8;
     const uint32_t nd = n ? (uint32_t)(((a + n - 1) >> 2) - (a >> 2) + 1) : 0;  // <= 17
     gptr<uint32_t> d = as_global<uint32_t>(a & ~uint64_t(3));
     uint32_t raw[17];
 #pragma unroll
-    for (int k = 0; k < 17; ++k) raw[k] = (uint32_t)k < nd ? d[k] : 0u;
+    for (int k = 0; k < 17; ++k)
+        raw[k] = ((uint32_t)k < nd && KRK_GUARD((a & ~uint64_t(3)) + 4 * k, 4, lo, hi, 1)) ? d[k] : 0u;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         uint32_t w = __builtin_amdgcn_alignbit(raw[j + 1], raw[j], sh);

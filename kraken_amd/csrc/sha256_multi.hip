@@ -58,17 +58,18 @@ __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) {
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
-__device__ __forceinline__ void load_block(uint64_t p, bool al16, uint32_t w[16]) {
+__device__ __forceinline__ void load_block(uint64_t p, bool al16, uint32_t w[16], uint64_t lo = 0,
+                                           uint64_t hi = ~0ull) {
     if (al16) {
         gptr<u32x4> q = as_global<u32x4>(p);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const u32x4 v = q[k];
+            const u32x4 v = KRK_GUARD(p + 16 * k, 16, lo, hi, 2) ? q[k] : u32x4{0, 0, 0, 0};
             w[4 * k + 0] = bswap(v.x); w[4 * k + 1] = bswap(v.y);
             w[4 * k + 2] = bswap(v.z); w[4 * k + 3] = bswap(v.w);
         }
     } else {
-        load_bytes64(p, 64, w);
+        load_bytes64(p, 64, w, lo, hi);
 #pragma unroll
         for (int k = 0; k < 16; ++k) w[k] = bswap(w[k]);
     }
@@ -82,6 +83,7 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
     const ShaJob job = jobs[j];
     const uint64_t p = job.ptr;
     const bool al16 = (job.ptr & 15) == 0;
+    const uint64_t lo = p & ~uint64_t(3), hi = (p + job.len + 3) & ~uint64_t(3);
     uint32_t h[8];
     if (job.flags & kShaFromState) {
 #pragma unroll
@@ -93,16 +95,16 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
 
     const uint64_t nblk = job.len / 64;
     uint32_t w0[16], w1[16], w2[16];
-    if (nblk > 0) load_block(p, al16, w0);
-    if (nblk > 1) load_block(p + 64, al16, w1);
+    if (nblk > 0) load_block(p, al16, w0, lo, hi);
+    if (nblk > 1) load_block(p + 64, al16, w1, lo, hi);
     uint64_t i = 0;
     // Three register sets rotate so that two blocks are always in flight.
     for (; i + 3 <= nblk; i += 3) {
-        load_block(p + (i + 2) * 64, al16, w2);
+        load_block(p + (i + 2) * 64, al16, w2, lo, hi);
         compress(h, w0);
-        if (i + 3 < nblk) load_block(p + (i + 3) * 64, al16, w0);
+        if (i + 3 < nblk) load_block(p + (i + 3) * 64, al16, w0, lo, hi);
         compress(h, w1);
-        if (i + 4 < nblk) load_block(p + (i + 4) * 64, al16, w1);
+        if (i + 4 < nblk) load_block(p + (i + 4) * 64, al16, w1, lo, hi);
         compress(h, w2);
     }
     if (i < nblk) { compress(h, w0); ++i; }
@@ -112,7 +114,7 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
         // Tail (< 64 bytes) + 0x80 + zeros + 64-bit big-endian bit length.
         const uint32_t rem = (uint32_t)(job.len - nblk * 64);
         uint32_t w[16];
-        load_bytes64(p + nblk * 64, rem, w);
+        load_bytes64(p + nblk * 64, rem, w, lo, hi);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             w[k] = bswap(w[k]);
@@ -128,7 +130,9 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
         w[15] = (uint32_t)bits;
         compress(h, w);
         uint8_t* o = out_digest + 32 * (uint64_t)job.out;
-        if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+        if (!KRK_GUARD(reinterpret_cast<uint64_t>(o), 32, reinterpret_cast<uint64_t>(out_digest),
+                       reinterpret_cast<uint64_t>(out_digest) + 32ull * n_jobs, 3)) {
+        } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
             reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
             reinterpret_cast<uint4*>(o)[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
         } else {
@@ -168,10 +172,11 @@ __device__ __forceinline__ uint32_t job_blocks(const ShaJob& job) {
 __device__ __forceinline__ void produce(const ShaJob& job, uint32_t b, uint32_t lane, uint32_t* lds) {
     constexpr uint32_t K[64] = {KRK_K256};
     const uint64_t p = job.ptr;
+    const uint64_t lo = p & ~uint64_t(3), hi = (p + job.len + 3) & ~uint64_t(3);
     const uint32_t nblk = (uint32_t)(job.len / 64);
     uint32_t w[16];
     if (b < nblk) {
-        load_block(p + (uint64_t)b * 64, (p & 15) == 0, w);
+        load_block(p + (uint64_t)b * 64, (p & 15) == 0, w, lo, hi);
     } else {
 #pragma unroll
         for (int k = 0; k < 16; ++k) w[k] = 0;
@@ -179,7 +184,7 @@ __device__ __forceinline__ void produce(const ShaJob& job, uint32_t b, uint32_t 
             const uint32_t rem = (uint32_t)(job.len & 63);
             const uint64_t bits = (job.prefix + job.len) * 8;
             if (b == nblk) {
-                load_bytes64(p + (uint64_t)nblk * 64, rem, w);
+                load_bytes64(p + (uint64_t)nblk * 64, rem, w, lo, hi);
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
                     w[k] = bswap(w[k]);
@@ -280,7 +285,9 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         if (live) {
             if (job.flags & kShaFinal) {
                 uint8_t* o = out_digest + 32 * (uint64_t)job.out;
-                if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+                if (!KRK_GUARD(reinterpret_cast<uint64_t>(o), 32, reinterpret_cast<uint64_t>(out_digest),
+                               reinterpret_cast<uint64_t>(out_digest) + 32ull * n_jobs, 4)) {
+                } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
                     reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
                     reinterpret_cast<uint4*>(o)[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
                 } else {

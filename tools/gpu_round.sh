@@ -3,7 +3,9 @@
 # crash/timeout (exit codes other than 0/1 from a step).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-step() {  # step <name> <timeout> <cmd...>
+export TMPDIR=/tmp
+R=$PWD
+step() {  # step <name> <timeout> <cmd...>  (env assignments before "step" are exported to it)
   local name=$1 t=$2; shift 2
   echo "=== $name" >&2
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
@@ -16,6 +18,9 @@ step() {  # step <name> <timeout> <cmd...>
 for s in "$@"; do
   case $s in
     test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    dbg) step dbg_unaligned 300 env KRK_LIB_PATH=kraken_amd/lib/debug/libkraken_hip.so python -m pytest tests/test_gpu_digest_metainfo.py -k "unaligned or lengths" -v -s -p no:cacheprovider ;;
+    hrw) step pytest_hrw 600 python -m pytest tests/test_gpu_hrw.py -x -q -p no:cacheprovider ;;
+    pieces) step pytest_pieces 600 python -m pytest tests/test_gpu_pieces.py -x -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     probe0) step probe_v0 300 python tools/probe_perf.py --variant 0 ;;
     probe1) step probe_v1 300 python tools/probe_perf.py --variant 1 --sha none ;;
@@ -24,5 +29,8 @@ for s in "$@"; do
     c2split) step probe_c2 300 python tools/probe_perf.py --c2 ;;
     benchsmall) step bench_small 300 python bench.py --workload small --cpu-seconds 3 ;;
     bench) step bench 900 python bench.py ;;
+    prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
   esac
 done
