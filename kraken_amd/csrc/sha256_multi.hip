@@ -130,9 +130,7 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
         w[15] = (uint32_t)bits;
         compress(h, w);
         uint8_t* o = out_digest + 32 * (uint64_t)job.out;
-        if (!KRK_GUARD(reinterpret_cast<uint64_t>(o), 32, reinterpret_cast<uint64_t>(out_digest),
-                       reinterpret_cast<uint64_t>(out_digest) + 32ull * n_jobs, 3)) {
-        } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+        if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
             reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
             reinterpret_cast<uint4*>(o)[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
         } else {
@@ -285,9 +283,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         if (live) {
             if (job.flags & kShaFinal) {
                 uint8_t* o = out_digest + 32 * (uint64_t)job.out;
-                if (!KRK_GUARD(reinterpret_cast<uint64_t>(o), 32, reinterpret_cast<uint64_t>(out_digest),
-                               reinterpret_cast<uint64_t>(out_digest) + 32ull * n_jobs, 4)) {
-                } else if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+                if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
                     reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
                     reinterpret_cast<uint4*>(o)[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
                 } else {

@@ -79,6 +79,9 @@ def test_sha256_dev_unaligned(gpu, orc, misalign):
     lens = [0, 55, 56, 64, 65, 1000, 100003]
     arena = D.BlobArena(lens, 4096, blob_ids=range(20, 27), misalign=misalign)
     out = D.BatchOutputs(arena)
+    if os.environ.get("KRK_TEST_VERBOSE"):
+        print(f"arena=0x{arena.buf.ptr:x}+{arena.nbytes} digests=0x{out.digests.ptr:x} "
+              f"offsets={arena.offsets.tolist()}", flush=True)
     D.sha256(arena, out)
     D.synchronize()
     got = out.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)

@@ -19,6 +19,9 @@ for s in "$@"; do
   case $s in
     test) step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     dbg) step dbg_unaligned 300 env KRK_LIB_PATH=kraken_amd/lib/debug/libkraken_hip.so python -m pytest tests/test_gpu_digest_metainfo.py -k "unaligned or lengths" -v -s -p no:cacheprovider ;;
+    dbgall) step dbg_digest_all 600 env KRK_LIB_PATH=kraken_amd/lib/debug/libkraken_hip.so python -m pytest tests/test_gpu_digest_metainfo.py -v -s -x -p no:cacheprovider ;;
+    serial) step serial_digest 600 env AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 AMD_LOG_LEVEL=1 python -m pytest tests/test_gpu_digest_metainfo.py -v -s -x -p no:cacheprovider ;;
+    serial4) step serial_unaligned 300 env KRK_TEST_VERBOSE=1 AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 AMD_LOG_LEVEL=4 python -m pytest tests/test_gpu_digest_metainfo.py -k unaligned -v -s -x -p no:cacheprovider ;;
     hrw) step pytest_hrw 600 python -m pytest tests/test_gpu_hrw.py -x -q -p no:cacheprovider ;;
     pieces) step pytest_pieces 600 python -m pytest tests/test_gpu_pieces.py -x -q -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
