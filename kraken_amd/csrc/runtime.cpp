@@ -107,7 +107,62 @@ struct PinnedSlot {
     bool busy = false;
 };
 
+// Stream-ordered device scratch.  Blocks are power-of-two sized and stay with the
+// device context; a released block carries an event recorded on the releasing
+// stream and its next user's stream waits on that event, so reuse is ordered on
+// the device with no host stall and no allocator work per call.
+struct DevCache {
+    struct Blk {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    std::mutex mu;
+    std::unordered_map<void*, Blk> live;
+    std::unordered_multimap<size_t, Blk> idle;
+
+    hipError_t alloc(void** out, size_t n, hipStream_t s) {
+        size_t cap = 256;
+        while (cap < n) cap <<= 1;
+        Blk b;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = idle.find(cap);
+            if (it != idle.end()) {
+                b = it->second;
+                idle.erase(it);
+            }
+        }
+        hipError_t e = hipSuccess;
+        if (b.p) {
+            if (b.pending) e = hipStreamWaitEvent(s, b.ev, 0);
+        } else {
+            e = hipMalloc(&b.p, cap);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+            b.cap = cap;
+        }
+        if (e != hipSuccess) return e;
+        std::lock_guard<std::mutex> g(mu);
+        live[b.p] = b;
+        *out = b.p;
+        return hipSuccess;
+    }
+    void release(void* p, hipStream_t s) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        auto it = live.find(p);
+        if (it == live.end()) return;
+        Blk b = it->second;
+        live.erase(it);
+        b.pending = hipEventRecord(b.ev, s) == hipSuccess;
+        if (!b.pending) hipStreamSynchronize(s);
+        idle.emplace(b.cap, b);
+    }
+};
+
 struct Device {
+    DevCache cache;
     int id = 0;
     int cus = 0;
     hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
@@ -117,6 +172,15 @@ struct Device {
     PinnedSlot slots[8];
     unsigned next_slot = 0;
 };
+
+template <class T>
+static hipError_t scratch_alloc(Device* D, T** p, size_t n, hipStream_t s) {
+    void* v = nullptr;
+    hipError_t e = D->cache.alloc(&v, n, s);
+    *p = static_cast<T*>(v);
+    return e;
+}
+static void scratch_free(Device* D, void* p, hipStream_t s) { D->cache.release(p, s); }
 
 static std::mutex g_dmu;
 static std::vector<std::unique_ptr<Device>> g_devs;
@@ -192,11 +256,11 @@ static Device* device(int* rc) {
 static hipStream_t pick(Device* D, void* s) { return s ? static_cast<hipStream_t>(s) : D->s_main; }
 
 // Stage `n` host bytes through a pinned slot into a fresh stream-ordered device
-// allocation (freed with hipFreeAsync by the caller).
+// scratch block (released with scratch_free by the caller).
 static int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_t s) {
     *d_out = nullptr;
     if (!n) return KRK_OK;
-    KRK_HIP(hipMallocAsync(d_out, n, s));
+    KRK_HIP(scratch_alloc(D, d_out, n, s));
     std::lock_guard<std::mutex> g(D->mu);
     PinnedSlot& P = D->slots[D->next_slot++ % 8];
     if (P.busy) {
@@ -315,7 +379,7 @@ static int run_items(Device* D, const std::vector<CrcItem>& items, uint32_t* sum
         return launch_crc_items(static_cast<const CrcItem*>(d_items), (uint32_t)items.size(), D->d_tabs,
                                 sums_dev, cfg, s);
     });
-    hipFreeAsync(d_items, s);
+    scratch_free(D, d_items, s);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
     return KRK_OK;
 }
@@ -355,7 +419,7 @@ static int run_jobs(Device* D, std::vector<ShaJob>& jobs, uint8_t* digests_dev, 
         return launch_sha256(static_cast<const ShaJob*>(d_jobs), (uint32_t)jobs.size(), digests_dev,
                              state_dev, s);
     });
-    hipFreeAsync(d_jobs, s);
+    scratch_free(D, d_jobs, s);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", hipGetErrorString(e));
     return KRK_OK;
 }
@@ -654,11 +718,11 @@ static int stream_grow_sums(krk_piece_stream* s, uint64_t need) {
     if (need <= s->sums_cap) return KRK_OK;
     uint64_t cap = std::max<uint64_t>(need, s->sums_cap * 2 + 1024);
     uint32_t* n = nullptr;
-    KRK_HIP(hipMallocAsync(&n, cap * 4, s->D->s_b));
+    KRK_HIP(scratch_alloc(s->D, &n, cap * 4, s->D->s_b));
     KRK_HIP(hipMemsetAsync(n, 0, cap * 4, s->D->s_b));
     if (s->d_sums) {
         KRK_HIP(hipMemcpyAsync(n, s->d_sums, s->sums_cap * 4, hipMemcpyDeviceToDevice, s->D->s_b));
-        KRK_HIP(hipFreeAsync(s->d_sums, s->D->s_b));
+        scratch_free(s->D, s->d_sums, s->D->s_b);
     }
     s->d_sums = n;
     s->sums_cap = cap;
@@ -745,7 +809,7 @@ void krk_piece_stream_free(krk_piece_stream* s) {
     if (!s) return;
     hipSetDevice(s->D->id);
     hipStreamSynchronize(s->D->s_b);
-    if (s->d_sums) hipFree(s->d_sums);
+    scratch_free(s->D, s->d_sums, s->D->s_b);
     delete s;
 }
 
@@ -757,8 +821,8 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
     hipStream_t s = D->s_main;
     uint8_t* d_buf = nullptr;
     uint32_t* d_sum = nullptr;
-    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_buf), n + 4, s));
-    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_sum), 4, s));
+    KRK_HIP(scratch_alloc(D, reinterpret_cast<void**>(&d_buf), n + 4, s));
+    KRK_HIP(scratch_alloc(D, reinterpret_cast<void**>(&d_sum), 4, s));
     KRK_HIP(hipMemcpyAsync(d_buf, data, n, hipMemcpyHostToDevice, s));
     KRK_HIP(hipMemsetAsync(d_sum, 0, 4, s));
     ItemBuilder B;
@@ -768,8 +832,8 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
     int r = run_items(D, items, d_sum, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
     if (!r && hipMemcpy(out, d_sum, 4, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
-    hipFreeAsync(d_buf, s);
-    hipFreeAsync(d_sum, s);
+    scratch_free(D, d_buf, s);
+    scratch_free(D, d_sum, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
     return r;
 }
@@ -785,8 +849,8 @@ int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, u
     if (r || !np) return r;
     uint32_t* d_sums = nullptr;
     uint8_t* d_ok = nullptr;
-    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_sums), np * 4, s));
-    KRK_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ok), np, s));
+    KRK_HIP(scratch_alloc(D, reinterpret_cast<void**>(&d_sums), np * 4, s));
+    KRK_HIP(scratch_alloc(D, reinterpret_cast<void**>(&d_ok), np, s));
     r = piece_sums_dev(D, &b, 1, d_sums, s);
     void* d_exp = nullptr;
     if (!r) r = upload(D, expected_host, np * 4, &d_exp, s);
@@ -796,9 +860,9 @@ int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, u
     }
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "verify sync"); r = KRK_EHIP; }
     if (!r && hipMemcpy(ok_out_host, d_ok, np, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
-    hipFreeAsync(d_sums, s);
-    hipFreeAsync(d_ok, s);
-    if (d_exp) hipFreeAsync(d_exp, s);
+    scratch_free(D, d_sums, s);
+    scratch_free(D, d_ok, s);
+    if (d_exp) scratch_free(D, d_exp, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "verify sync"); r = KRK_EHIP; }
     return r;
 }
@@ -939,10 +1003,10 @@ static int upload_nodes(Device* D, const krk_nodes* nodes, DevNodes& dn, hipStre
     return r;
 }
 
-static void free_nodes(DevNodes& dn, hipStream_t s) {
-    if (dn.labels) hipFreeAsync(dn.labels, s);
-    if (dn.off) hipFreeAsync(dn.off, s);
-    if (dn.w) hipFreeAsync(dn.w, s);
+static void free_nodes(Device* D, DevNodes& dn, hipStream_t s) {
+    if (dn.labels) scratch_free(D, dn.labels, s);
+    if (dn.off) scratch_free(D, dn.off, s);
+    if (dn.w) scratch_free(D, dn.w, s);
 }
 
 // Order + Locations table for the given decoded keys; result rows on the device.
@@ -960,9 +1024,9 @@ static int hrw_table(Device* D, const std::vector<uint8_t>& kb, const std::vecto
     if (!r) r = upload(D, koff.data(), koff.size() * 8, &d_koff, s);
     if (!r) r = upload(D, bad.data(), bad.size(), &d_bad, s);
     if (!r) r = upload(D, healthy, N, &d_h, s);
-    if (!r && hipMallocAsync(reinterpret_cast<void**>(&d_order), nk * N * 4, s) != hipSuccess) r = KRK_ENOMEM;
-    if (!r && hipMallocAsync(reinterpret_cast<void**>(d_locs), nk * row_out * 4, s) != hipSuccess) r = KRK_ENOMEM;
-    if (!r && hipMallocAsync(reinterpret_cast<void**>(d_counts), nk, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && scratch_alloc(D, reinterpret_cast<void**>(&d_order), nk * N * 4, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && scratch_alloc(D, reinterpret_cast<void**>(d_locs), nk * row_out * 4, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && scratch_alloc(D, reinterpret_cast<void**>(d_counts), nk, s) != hipSuccess) r = KRK_ENOMEM;
     if (!r) {
         HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), nk,
                   static_cast<const uint8_t*>(dn.labels), static_cast<const uint64_t*>(dn.off),
@@ -975,9 +1039,9 @@ static int hrw_table(Device* D, const std::vector<uint8_t>& kb, const std::vecto
             });
         if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
-    free_nodes(dn, s);
+    free_nodes(D, dn, s);
     for (void* p : {d_kb, d_koff, d_bad, d_h, static_cast<void*>(d_order)})
-        if (p) hipFreeAsync(p, s);
+        if (p) scratch_free(D, p, s);
     return r;
 }
 
@@ -1015,8 +1079,8 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
     if (!r) r = upload(D, kb.data(), kb.size(), &d_kb, s);
     if (!r) r = upload(D, koff.data(), koff.size() * 8, &d_koff, s);
     if (!r) r = upload(D, bad.data(), bad.size(), &d_bad, s);
-    if (!r && hipMallocAsync(reinterpret_cast<void**>(&d_order), n_keys * n_out * 4 + 4, s) != hipSuccess) r = KRK_ENOMEM;
-    if (!r && scores_out && hipMallocAsync(reinterpret_cast<void**>(&d_sc), n_keys * N * 8, s) != hipSuccess)
+    if (!r && scratch_alloc(D, reinterpret_cast<void**>(&d_order), n_keys * n_out * 4 + 4, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r && scores_out && scratch_alloc(D, reinterpret_cast<void**>(&d_sc), n_keys * N * 8, s) != hipSuccess)
         r = KRK_ENOMEM;
     if (!r) {
         HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), n_keys,
@@ -1031,9 +1095,9 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
         r = KRK_EHIP;
     if (!r && scores_out && hipMemcpy(scores_out, d_sc, n_keys * N * 8, hipMemcpyDeviceToHost) != hipSuccess)
         r = KRK_EHIP;
-    free_nodes(dn, s);
+    free_nodes(D, dn, s);
     for (void* p : {d_kb, d_koff, d_bad, static_cast<void*>(d_order), static_cast<void*>(d_sc)})
-        if (p) hipFreeAsync(p, s);
+        if (p) scratch_free(D, p, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "hrw sync"); r = KRK_EHIP; }
     if (!r && any_bad) {
         set_error(KRK_EHEX, "invalid hex key: Score is NaN");
@@ -1078,8 +1142,8 @@ int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* no
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "ring sync"); r = KRK_EHIP; }
     if (!r && hipMemcpy(tl.data(), d_locs, tl.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
     if (!r && hipMemcpy(tc.data(), d_counts, tc.size(), hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
-    if (d_locs) hipFreeAsync(d_locs, s);
-    if (d_counts) hipFreeAsync(d_counts, s);
+    if (d_locs) scratch_free(D, d_locs, s);
+    if (d_counts) scratch_free(D, d_counts, s);
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "ring sync"); r = KRK_EHIP; }
     if (r) return r;
     for (uint64_t i = 0; i < n; ++i) {
@@ -1112,8 +1176,8 @@ int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_n
         });
         if (e != hipSuccess) { set_error(KRK_EHIP, "gather launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
-    if (d_tl) hipFreeAsync(d_tl, s);
-    if (d_tc) hipFreeAsync(d_tc, s);
+    if (d_tl) scratch_free(D, d_tl, s);
+    if (d_tc) scratch_free(D, d_tc, s);
     return r;
 }
 

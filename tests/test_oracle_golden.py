@@ -31,6 +31,16 @@ def test_reference_kats(orc):
         assert orc.murmur3_h1(s.encode()) == int(h, 16)
 
 
+def test_survey_sanity_vector(orc):
+    """labels dummy-origin-master0{1,2,3}-zone2:80, weight 100."""
+    labels = [f"dummy-origin-master0{i}-zone2:80" for i in (1, 2, 3)]
+    h1 = [orc.murmur3_h1(bytes.fromhex("e3b0") + l.encode()) for l in labels]
+    assert h1 == [0x826B41F830434FBC, 0xBB8FB798DBB4FA8A, 0x85319F9780C10BFC]
+    assert orc.hrw_ordered("e3b0", labels, [100] * 3) == [2, 1, 0]
+    assert orc.hrw_ordered("0000", labels, [100] * 3) == [0, 2, 1]
+    assert orc.hrw_ordered("ffff", labels, [100] * 3) == [0, 2, 1]
+
+
 def test_rehash_property(orc):
     """lib/hrw/rendezvous_test.go:59-98: 2^53..2^63 have zero low 53 bits -> 0.0
     without a hasher, non-zero (finite log) after the one-time rehash."""

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One gpurun session: GPU parity tests, then the perf probe; stops at the first
-# crash/timeout (exit codes other than 0/1 from a step).
+# crash/timeout (exit codes other than 0/1 from a step) or GPU fault in its log.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -13,6 +13,9 @@ step() {  # step <name> <timeout> <cmd...>  (env assignments before "step" are e
   echo "=== $name rc=$rc" >&2
   tail -5 "gpurun_out/$name.log" >&2
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
+  if grep -qiE "memory fault|illegal memory access|memory access fault|device not stable" "gpurun_out/$name.log"; then
+    echo "stopping after $name (GPU fault in log)" >&2; exit 3
+  fi
   return 0
 }
 for s in "$@"; do
