@@ -167,32 +167,78 @@ __device__ __forceinline__ uint32_t job_blocks(const ShaJob& job) {
     return nblk + (((uint32_t)(job.len & 63) >= 56) ? 2u : 1u);
 }
 
-__device__ __forceinline__ void produce(const ShaJob& job, uint32_t b, uint32_t lane, uint32_t* lds) {
+// Bytes of block b that lie inside the run (64 for full blocks, the tail for
+// b == len/64, 0 past the data).
+__device__ __forceinline__ uint32_t block_bytes(const ShaJob& job, uint32_t b) {
+    const uint64_t off = (uint64_t)b * 64;
+    return off < job.len ? (uint32_t)min<uint64_t>(64, job.len - off) : 0u;
+}
+
+// Issue the loads of block b into raw[]: the five 16-byte-aligned chunks from
+// (block start & ~15), as five dwordx4 that every lane always issues (no branch,
+// so the compiler's vmcnt accounting stays exact and the loads stay in flight
+// across the schedule work of the blocks in between).  An aligned chunk that
+// holds a byte of the run lies in a page holding that byte, so it is always
+// mapped; chunks past the last one holding a byte of the block re-read that
+// chunk, and lanes with no bytes read the always-valid `safe` chunk.
+constexpr int kRaw = 5;  // chunks
+
+__device__ __forceinline__ void fetch(const ShaJob& job, uint32_t b, u32x4 raw[kRaw], uint64_t safe) {
+    const uint64_t a = job.ptr + (uint64_t)b * 64;
+    const uint32_t n = block_bytes(job, b);
+    const uint64_t base = n ? (a & ~uint64_t(15)) : safe;
+    const uint32_t cmax = n ? (uint32_t)(((a + n - 1) >> 4) - (a >> 4)) : 0u;  // <= 4
+    const uint64_t lo = job.ptr & ~uint64_t(15), hi = (job.ptr + job.len + 15) & ~uint64_t(15);
+    gptr<u32x4> q = as_global<u32x4>(base);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const uint32_t cc = min((uint32_t)c, cmax);
+        raw[c] = (!n || KRK_GUARD(base + 16 * cc, 16, lo, hi, 1)) ? q[cc] : u32x4{0, 0, 0, 0};
+    }
+}
+
+// Block b's 16 big-endian message words from raw[] (+ the 0x80 terminator and the
+// bit length on the final blocks), expanded to KW[r] = W[r] + K[r] in ring slot b % kSlots.
+__device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4 rawc[kRaw], uint32_t lane,
+                                      uint32_t* lds) {
     constexpr uint32_t K[64] = {KRK_K256};
-    const uint64_t p = job.ptr;
-    const uint64_t lo = p & ~uint64_t(3), hi = (p + job.len + 3) & ~uint64_t(3);
-    const uint32_t nblk = (uint32_t)(job.len / 64);
+    const uint32_t n = block_bytes(job, b);
+    uint32_t raw[4 * kRaw];
+#pragma unroll
+    for (int c = 0; c < kRaw; ++c) {
+        raw[4 * c + 0] = rawc[c].x; raw[4 * c + 1] = rawc[c].y; raw[4 * c + 2] = rawc[c].z; raw[4 * c + 3] = rawc[c].w;
+    }
     uint32_t w[16];
-    if (b < nblk) {
-        load_block(p + (uint64_t)b * 64, (p & 15) == 0, w, lo, hi);
+    // Wave-uniform split: every live lane on a 16-byte aligned run inside a full block.
+    if (__all((n == 64 && (job.ptr & 15) == 0) || b >= job_blocks(job))) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = bswap(raw[j]);
     } else {
+        // Dword q of the first chunk starts the block; bytes shift by sh within it.
+        const uint32_t qd = (uint32_t)(job.ptr >> 2) & 3, sh = (uint32_t)(job.ptr & 3) * 8;
+        // Value muxes (v_bfi), not selects of addresses: a selected index would
+        // leave these arrays in scratch.
+        const uint32_t m1 = 0u - (qd & 1), m2 = 0u - ((qd >> 1) & 1);
+        uint32_t t[19], u[17];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = 0;
-        if (job.flags & kShaFinal) {
-            const uint32_t rem = (uint32_t)(job.len & 63);
+        for (int j = 0; j < 19; ++j) t[j] = (raw[j + 1] & m1) | (raw[j] & ~m1);
+#pragma unroll
+        for (int j = 0; j < 17; ++j) u[j] = (t[j + 2] & m2) | (t[j] & ~m2);
+        const bool fin = (job.flags & kShaFinal) != 0;
+        const uint32_t nblk = (uint32_t)(job.len / 64);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            uint32_t x = __builtin_amdgcn_alignbit(u[j + 1], u[j], sh);
+            const int keep = (int)n - 4 * j;
+            if (keep <= 0) x = 0;
+            else if (keep < 4) x &= (1u << (8 * keep)) - 1;
+            w[j] = bswap(x);
+            if (fin && b == nblk && j == (int)(n >> 2)) w[j] |= 0x80u << (24 - 8 * (n & 3));
+        }
+        if (fin && b == job_blocks(job) - 1) {
             const uint64_t bits = (job.prefix + job.len) * 8;
-            if (b == nblk) {
-                load_bytes64(p + (uint64_t)nblk * 64, rem, w, lo, hi);
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    w[k] = bswap(w[k]);
-                    if (k == (int)(rem >> 2)) w[k] |= 0x80u << (24 - 8 * (rem & 3));
-                }
-            }
-            if (b == job_blocks(job) - 1) {
-                w[14] = (uint32_t)(bits >> 32);
-                w[15] = (uint32_t)bits;
-            }
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
         }
     }
     const int slot = (int)(b % kSlots);
@@ -216,6 +262,18 @@ __device__ __forceinline__ void produce(const ShaJob& job, uint32_t b, uint32_t 
         }
         *reinterpret_cast<u32x4*>(lds + kw_index(slot, q, lane)) = u32x4{kw[0], kw[1], kw[2], kw[3]};
     }
+}
+
+// One producer step (b is wave-uniform): wait for the consumer to free a slot
+// (from block kDepth on), start the loads of block b + 2 (always issued, so no
+// branch sits between a load and its use), then build block b from registers.
+__device__ __forceinline__ void produce_step(const ShaJob& job, uint32_t b, uint32_t nb, uint32_t lane,
+                                             uint32_t* lds, const u32x4 use[kRaw], u32x4 next[kRaw],
+                                             uint64_t safe) {
+    const bool act = b < nb;
+    if (act && b >= (uint32_t)kDepth) __syncthreads();
+    fetch(job, b + 2, next, safe);
+    if (act) build(job, b, use, lane, lds);
 }
 
 __device__ __forceinline__ void rounds(uint32_t h[8], const uint32_t* lds, int slot, uint32_t lane) {
@@ -254,12 +312,20 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     nb = __builtin_amdgcn_readfirstlane(nb);
 
     if (producer) {
-        const uint32_t pre = nb < (uint32_t)kDepth ? nb : (uint32_t)kDepth;
-        for (uint32_t b = 0; b < pre; ++b) produce(job, b, lane, ring);
-        for (uint32_t i = 0; i < nb; ++i) {
-            __syncthreads();
-            if (i + kDepth < nb) produce(job, i + kDepth, lane, ring);
+        // Blocks are built kDepth ahead of the consumer; their loads are issued two
+        // blocks before that, into a 3-deep register rotation (R0, R1, R2).
+        u32x4 R0[kRaw], R1[kRaw], R2[kRaw];
+        const uint64_t safe = reinterpret_cast<uint64_t>(jobs);
+        fetch(job, 0, R0, safe);
+        fetch(job, 1, R1, safe);
+        for (uint32_t b = 0; b < nb; b += 3) {
+            produce_step(job, b, nb, lane, ring, R0, R2, safe);
+            produce_step(job, b + 1, nb, lane, ring, R1, R0, safe);
+            produce_step(job, b + 2, nb, lane, ring, R2, R1, safe);
         }
+        // The consumer passes nb barriers; the loop above took max(0, nb - kDepth).
+        const uint32_t tail = nb < (uint32_t)kDepth ? nb : (uint32_t)kDepth;
+        for (uint32_t i = 0; i < tail; ++i) __syncthreads();
     } else {
         uint32_t h[8];
         if (live && (job.flags & kShaFromState)) {
