@@ -85,6 +85,37 @@ def cpu_baseline(n_bytes_blob, piece, target_s, want_check):
     return info, dg, sums
 
 
+def end_to_end(D, arena, n, Le, P, out, dist):
+    """End-to-end leg (reported beside `value`, never as it): the same blobs' first
+    Le bytes in pageable host memory, through krk_metainfo_digest_host (pinned
+    windows, one PCIe pass feeding both kernels), results back on the host."""
+    import ctypes as C
+    datas = [np.empty(Le, dtype=np.uint8) for _ in range(n)]
+    for i, d in enumerate(datas):  # the device blobs' prefixes (device-generated content)
+        D.check(D.lib.krk_memcpy_d2h(d.ctypes.data_as(C.c_void_p), arena.buf.ptr + int(arena.offsets[i]), Le))
+    D.metainfo_digest_host(datas[:2], P)  # warm the staging windows
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    sums, dg = D.metainfo_digest_host(datas, P)
+    t1 = time.perf_counter()
+    el = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    world = dist.get_world_size() if dist is not None else 1
+    # piece sums of the prefixes must equal the device-resident run's first pieces
+    dev_sums = out.sums.to_host(np.uint32, arena.total_pieces)
+    k = Le // P
+    ok = all(np.array_equal(sums[i][:k], dev_sums[int(arena.sums_off[i]):int(arena.sums_off[i]) + k])
+             for i in range(n)) if k else None
+    return {"value": round(world * n * Le / el / 1e9, 3), "unit": "GB/s", "blobs_per_gpu": n, "blob_bytes": Le,
+            "seconds": round(el, 3), "source": "pageable host memory (numpy), copied into pinned windows",
+            "bound": "PCIe H2D / SHA per-stream rate", "sums_match_device_run": ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +126,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers, PCIe) leg")
+    ap.add_argument("--e2e-mb", type=int, default=16, help="bytes per blob for the end-to-end leg (MiB)")
     a = ap.parse_args()
 
     rank, world, local = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1), _env_int("LOCAL_RANK", 0)
@@ -184,6 +217,8 @@ def main():
            "roofline": roofline, "roofline_crc": crc_roof,
            "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)},
                        "sha256_multi": {"launches": sha_n, "avg_ms": round(sha_avg, 3)}}}
+    if not a.no_e2e:
+        res["end_to_end"] = end_to_end(D, arena, n, min(a.e2e_mb << 20, L), P, out, dist)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cb, dg, sums = cpu_baseline(L, P, a.cpu_seconds, True)
         m = len(dg)

@@ -115,6 +115,15 @@ void krk_digester_free(krk_digester* d);
 int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev,
                             uint8_t* digests_dev, void* stream);
 
+/* End-to-end form: blobs[i].data are HOST pointers (pageable or pinned).  Every
+ * byte crosses PCIe once: the library copies the caller's bytes into its own
+ * pinned windows (several host threads), uploads each window once and runs
+ * both kernels on it (SHA-256 chained from per-blob midstates, CRC by byte
+ * range), double-buffered against the next window's copy.  sums_host indexed
+ * by blobs[i].sums_offset; digests_host n_blobs*32 bytes.  Synchronous. */
+int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host,
+                             uint8_t* digests_host);
+
 /* ---------------------------------------------------- InfoHash (host CPU)
  * info.Hash() (core/metainfo.go:37-44): SHA-1 over the bencoded
  * info{PieceLength, PieceSums, Name, Length}.  bencode_out may be NULL. */

@@ -65,6 +65,7 @@ def _load() -> C.CDLL:
         "krk_digester_sum": (i, [vp, u8p]),
         "krk_digester_free": (None, [vp]),
         "krk_metainfo_digest_dev": (i, [blobp, C.c_uint64, vp, vp, vp]),
+        "krk_metainfo_digest_host": (i, [blobp, C.c_uint64, u32p, u8p]),
         "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),
         "krk_bencode_info": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p,
                                  C.c_uint64, u64p]),

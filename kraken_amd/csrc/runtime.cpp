@@ -12,6 +12,7 @@
 #include <mutex>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -483,6 +484,45 @@ static size_t window_bytes() {
     return mb << 20;
 }
 
+// Host -> pinned staging copies of one window, split over a few threads (one
+// host thread's memcpy is well below the PCIe rate).  KRK_COPY_THREADS overrides.
+struct CopyTask {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+
+static unsigned copy_threads() {
+    const char* v = getenv("KRK_COPY_THREADS");
+    if (v) return std::max(1u, (unsigned)strtoul(v, nullptr, 10));
+    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+static void par_copy(const std::vector<CopyTask>& tasks) {
+    size_t total = 0;
+    for (const auto& t : tasks) total += t.n;
+    const unsigned T = copy_threads();
+    if (T == 1 || total < (8u << 20)) {
+        for (const auto& t : tasks) memcpy(t.dst, t.src, t.n);
+        return;
+    }
+    // Cut the concatenated byte range into T equal spans.
+    auto run = [&](size_t lo, size_t hi) {
+        size_t pos = 0;
+        for (const auto& t : tasks) {
+            const size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
+            if (a < b) memcpy(t.dst + (a - pos), t.src + (a - pos), b - a);
+            pos += t.n;
+            if (pos >= hi) break;
+        }
+    };
+    std::vector<std::thread> th;
+    const size_t span = (total + T - 1) / T;
+    for (unsigned i = 1; i < T; ++i) th.emplace_back(run, i * span, std::min(total, (i + 1) * span));
+    run(0, std::min(total, span));
+    for (auto& t : th) t.join();
+}
+
 }  // namespace krk
 
 using namespace krk;
@@ -696,6 +736,111 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     }
     hipFree(d_dig);
     hipFree(d_state);
+    return r;
+}
+
+int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {
+    KRK_DEVICE(D);
+    int r = validate_blobs(blobs, n);
+    if (r) return r;
+    if (!n) return KRK_OK;
+    KRK_CHECK(digests_host, KRK_EINVAL, "digests_host is NULL");
+    uint64_t lo, hi;
+    sums_span(blobs, n, &lo, &hi);
+    KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
+    const size_t W = window_bytes();
+    // Every unfinished blob contributes up to C bytes per window, so the SHA
+    // streams all advance together (multiple of 64: only final chunks are partial).
+    uint64_t C = (W / n) & ~uint64_t(63);
+    if (C < 64) C = 64;
+    const size_t cap = std::max<size_t>(W, C * n + 16 * n);
+    Pipeline pl;
+    r = pl.init(cap);
+    if (r) return r;
+    uint8_t* d_dig = nullptr;
+    uint32_t *d_state = nullptr, *d_sums = nullptr;
+    KRK_HIP(hipMalloc(&d_dig, n * 32));
+    KRK_HIP(hipMalloc(&d_state, n * 32));
+    KRK_HIP(hipMalloc(&d_sums, std::max<uint64_t>(hi, 1) * 4));
+    KRK_HIP(hipMemset(d_sums, 0, std::max<uint64_t>(hi, 1) * 4));
+    std::vector<uint64_t> off(n, 0);
+    std::vector<char> done(n, 0);
+    hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
+    hipEvent_t sha_done, crc_done;
+    KRK_HIP(hipEventCreateWithFlags(&sha_done, hipEventDisableTiming));
+    KRK_HIP(hipEventCreateWithFlags(&crc_done, hipEventDisableTiming));
+    ItemBuilder B;
+    uint64_t remaining = n;
+    int k = 0;
+    while (!r && remaining) {
+        r = pl.acquire(k);
+        if (r) break;
+        Window& w = pl.w[k];
+        std::vector<ShaJob> jobs;
+        std::vector<CrcItem> items;
+        std::vector<CopyTask> copies;
+        size_t fill = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (done[i]) continue;
+            const krk_blob& b = blobs[i];
+            const uint64_t left = b.length - off[i];
+            const bool fin = left <= C;
+            const uint64_t take = fin ? left : C;
+            const uint64_t dev = reinterpret_cast<uint64_t>(w.dev + fill);
+            if (take) {
+                copies.push_back({w.host + fill, b.data + off[i], take});
+                B.add(items, dev, off[i], off[i] + take, b.length, (uint64_t)b.piece_length, b.sums_offset);
+            }
+            ShaJob j{};
+            j.ptr = dev;
+            j.len = take;
+            j.prefix = off[i];
+            j.out = (uint32_t)i;
+            j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
+            memcpy(j.h, kIV, sizeof kIV);
+            jobs.push_back(j);
+            off[i] += take;
+            fill += (take + 15) & ~uint64_t(15);
+            if (fin) { done[i] = 1; --remaining; }
+        }
+        par_copy(copies);
+        if (hipMemcpyAsync(w.dev, w.host, fill, hipMemcpyHostToDevice, cp) != hipSuccess ||
+            hipEventRecord(w.copied, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
+            hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess) {
+            set_error(KRK_EHIP, "metainfo_digest_host: staging copy failed");
+            r = KRK_EHIP;
+            break;
+        }
+        r = run_jobs(D, jobs, d_dig, d_state, ks);
+        if (!r) r = run_items(D, items, d_sums, kc);
+        if (r) break;
+        // the window is free again once both kernels have read it
+        hipEventRecord(sha_done, ks);
+        hipEventRecord(crc_done, kc);
+        hipStreamWaitEvent(cp, sha_done, 0);
+        hipStreamWaitEvent(cp, crc_done, 0);
+        hipEventRecord(w.consumed, cp);
+        w.inflight = true;
+        k ^= 1;
+    }
+    if (!r && (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(kc) != hipSuccess ||
+               hipStreamSynchronize(cp) != hipSuccess)) {
+        set_error(KRK_EHIP, "sync failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "digest copy-out failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hi > lo && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "sums copy-out failed");
+        r = KRK_EHIP;
+    }
+    hipEventDestroy(sha_done);
+    hipEventDestroy(crc_done);
+    hipFree(d_dig);
+    hipFree(d_state);
+    hipFree(d_sums);
     return r;
 }
 

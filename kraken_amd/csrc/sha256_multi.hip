@@ -189,6 +189,8 @@ __device__ __forceinline__ void fetch(const ShaJob& job, uint32_t b, u32x4 raw[k
     const uint64_t base = n ? (a & ~uint64_t(15)) : safe;
     const uint32_t cmax = n ? (uint32_t)(((a + n - 1) >> 4) - (a >> 4)) : 0u;  // <= 4
     const uint64_t lo = job.ptr & ~uint64_t(15), hi = (job.ptr + job.len + 15) & ~uint64_t(15);
+    (void)lo;
+    (void)hi;
     gptr<u32x4> q = as_global<u32x4>(base);
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
@@ -276,24 +278,87 @@ __device__ __forceinline__ void produce_step(const ShaJob& job, uint32_t b, uint
     if (act) build(job, b, use, lane, lds);
 }
 
-__device__ __forceinline__ void rounds(uint32_t h[8], const uint32_t* lds, int slot, uint32_t lane) {
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+// Four SHA-256 rounds as one fixed 56-instruction sequence.  The compiler's
+// scheduler does not model the gfx950 dependent-issue latency and places most
+// results right before their consumer; here every result is consumed at least
+// one instruction after it is produced, so a lone wave keeps issuing one VALU op
+// per slot (and the hazard recognizer pads once per four rounds, not per round).
+// hk = h + KW[r] enters precomputed; each round forms the next one's
+// (g + KW[r+1]) in its own shadow.  Round operands: state A..G, HK, next KW,
+// outputs NE (new e), NA (new a), NH (next hk); S1 lands in r6, S0 in q2.
+#define KRK_SHA_ROUND(A, B, C, D, E, F, G, HK, KWN, NE, NA, NH)                  \
+    "v_alignbit_b32 %[r6], %[" #E "], %[" #E "], 6\n\t"                        \
+    "v_alignbit_b32 %[r11], %[" #E "], %[" #E "], 11\n\t"                      \
+    "v_alignbit_b32 %[r25], %[" #E "], %[" #E "], 25\n\t"                      \
+    "v_bitop3_b32 %[ch], %[" #E "], %[" #F "], %[" #G "] bitop3:0xca\n\t"     \
+    "v_bitop3_b32 %[r6], %[r6], %[r11], %[r25] bitop3:0x96\n\t"                \
+    "v_alignbit_b32 %[q2], %[" #A "], %[" #A "], 2\n\t"                        \
+    "v_add3_u32 %[t1], %[" #HK "], %[r6], %[ch]\n\t"                           \
+    "v_alignbit_b32 %[q13], %[" #A "], %[" #A "], 13\n\t"                      \
+    "v_add_u32_e32 %[" #NE "], %[" #D "], %[t1]\n\t"                           \
+    "v_alignbit_b32 %[q22], %[" #A "], %[" #A "], 22\n\t"                      \
+    "v_bitop3_b32 %[mj], %[" #A "], %[" #B "], %[" #C "] bitop3:0xe8\n\t"     \
+    "v_bitop3_b32 %[q2], %[q2], %[q13], %[q22] bitop3:0x96\n\t"                \
+    "v_add_u32_e32 %[" #NH "], %[" #G "], %[" #KWN "]\n\t"                     \
+    "v_add3_u32 %[" #NA "], %[t1], %[q2], %[mj]\n\t"
+
+// Rounds r..r+3: (a..g, hk) in, KW[r+1..r+4] in (0 past the block), state after
+// round r+3 out.  The h entering round r+3 is e1 (returned for the final add).
+__device__ __forceinline__ void sha_quad(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
+                                         uint32_t& f, uint32_t& g, uint32_t& hk, uint32_t k1, uint32_t k2,
+                                         uint32_t k3, uint32_t k4, uint32_t& h_last) {
+    uint32_t r6, r11, r25, ch, q2, t1, q13, q22, mj;
+    uint32_t e1, e2, e3, e4, a1, a2, a3, a4, h1, h2, h3, h4;
+    asm volatile(KRK_SHA_ROUND(a, b, c, d, e, f, g, hk, k1, e1, a1, h1)
+                 KRK_SHA_ROUND(a1, a, b, c, e1, e, f, h1, k2, e2, a2, h2)
+                 KRK_SHA_ROUND(a2, a1, a, b, e2, e1, e, h2, k3, e3, a3, h3)
+                 KRK_SHA_ROUND(a3, a2, a1, a, e3, e2, e1, h3, k4, e4, a4, h4)
+                 : [r6] "=&v"(r6), [r11] "=&v"(r11), [r25] "=&v"(r25), [ch] "=&v"(ch), [q2] "=&v"(q2),
+                   [t1] "=&v"(t1), [q13] "=&v"(q13), [q22] "=&v"(q22), [mj] "=&v"(mj), [e1] "=&v"(e1),
+                   [e2] "=&v"(e2), [e3] "=&v"(e3), [e4] "=&v"(e4), [a1] "=&v"(a1), [a2] "=&v"(a2),
+                   [a3] "=&v"(a3), [a4] "=&v"(a4), [h1] "=&v"(h1), [h2] "=&v"(h2), [h3] "=&v"(h3),
+                   [h4] "=&v"(h4)
+                 : [a] "v"(a), [b] "v"(b), [c] "v"(c), [d] "v"(d), [e] "v"(e), [f] "v"(f), [g] "v"(g),
+                   [hk] "v"(hk), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3), [k4] "v"(k4));
+    h_last = e1;
+    a = a4; b = a3; c = a2; d = a1;
+    e = e4; f = e3; g = e2;
+    hk = h4;
+}
+#undef KRK_SHA_ROUND
+
+// The 64 rounds of one block; quads 0 and 1 of its KW arrive already loaded
+// (read before the barrier that opens the block), the rest are read two quads ahead.
+__device__ __forceinline__ void rounds(uint32_t h[8], const uint32_t* lds, int slot, uint32_t lane,
+                                       const u32x4& k0, const u32x4& k1) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6];
+    uint32_t hk = h[7] + k0[0], hl = 0;
+    u32x4 kw = k0, nkw = k1, nnkw = k1;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        const u32x4 kw = *reinterpret_cast<const u32x4*>(lds + kw_index(slot, q, lane));
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-            const uint32_t ch = (e & f) ^ (~e & g);
-            const uint32_t t1 = hh + S1 + ch + kw[t];
-            const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-            const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
-            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
-        }
+        // quad q+2 is read while quads q and q+1 are consumed (one quad of slack)
+        if (q + 2 < 16) nnkw = *reinterpret_cast<const u32x4*>(lds + kw_index(slot, q + 2, lane));
+        sha_quad(a, b, c, d, e, f, g, hk, kw[1], kw[2], kw[3], q + 1 < 16 ? nkw[0] : 0u, hl);
+        kw = nkw;
+        nkw = nnkw;
     }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hl;
 }
 
+__device__ __forceinline__ u32x4 kw_quad(const uint32_t* lds, int slot, int q, uint32_t lane) {
+    return *reinterpret_cast<const u32x4*>(lds + kw_index(slot, q, lane));
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// kTiming (diagnostic variant 2 only, wrong digests): the producer idles and the
+// consumer runs its rounds on whatever the ring holds with no barriers -- the
+// consumer's issue-bound time per block, to price the producer/consumer sync.
+template <bool kTiming>
 __global__ void __launch_bounds__(128)
 sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __restrict__ out_digest,
                  uint32_t* __restrict__ out_state) {
@@ -311,6 +376,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off, 64));
     nb = __builtin_amdgcn_readfirstlane(nb);
 
+    if (producer && kTiming) return;
     if (producer) {
         // Blocks are built kDepth ahead of the consumer; their loads are issued two
         // blocks before that, into a 3-deep register rotation (R0, R1, R2).
@@ -335,13 +401,36 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
 #pragma unroll
             for (int k = 0; k < 8; ++k) h[k] = job.h[k];
         }
+        // The rounds are the long pole: win VALU issue arbitration should the
+        // producer share this wave's SIMD.
+        __builtin_amdgcn_s_setprio(3);
+        // Blocks every live lane still needs (wave-uniform): no per-lane masking there.
+        const uint32_t common = wave_min(live ? mine : ~0u);
+        u32x4 k0{}, k1{};
         for (uint32_t i = 0; i < nb; ++i) {
-            __syncthreads();
+            // The consumer writes no LDS, so its barrier needs no release fence (no
+            // lgkmcnt drain): the quads prefetched below stay in flight across it.
+            // Block i+1 is complete once this barrier has passed (the producer runs
+            // kDepth-1 >= 1 blocks ahead of it), and its slot is not rewritten
+            // before the barrier after next.
+            if (!kTiming) __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (i == 0) {
+                k0 = kw_quad(ring, 0, 0, lane);
+                k1 = kw_quad(ring, 0, 1, lane);
+            }
             uint32_t x[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) x[k] = h[k];
-            rounds(x, ring, (int)(i % kSlots), lane);
-            if (i < mine) {
+            rounds(x, ring, (int)(i % kSlots), lane, k0, k1);
+            if (i + 1 < nb) {
+                k0 = kw_quad(ring, (int)((i + 1) % kSlots), 0, lane);
+                k1 = kw_quad(ring, (int)((i + 1) % kSlots), 1, lane);
+            }
+            if (i < common) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) h[k] = x[k];
+            } else if (i < mine) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) h[k] = x[k];
             }
@@ -376,11 +465,13 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;
     const uint32_t grid = (n_jobs + 63) / 64;
-    if (sha_variant() == 1) {
+    const int v = sha_variant();
+    if (v == 1 || v == 2) {
         constexpr size_t lds = size_t(kSlots) * kSlotWords * 4;  // 64 KiB
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&sha256_ws_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(sha256_ws_kernel, dim3(grid), dim3(128), lds, s, jobs, n_jobs, out_digest, out_state);
+        auto* k = v == 1 ? &sha256_ws_kernel<false> : &sha256_ws_kernel<true>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(128), lds, s, jobs, n_jobs, out_digest, out_state);
     } else {
         hipLaunchKernelGGL(sha256_multi_kernel, dim3(grid), dim3(64), 0, s, jobs, n_jobs, out_digest, out_state);
     }

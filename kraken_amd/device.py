@@ -128,6 +128,24 @@ def metainfo_digest(arena: BlobArena, out: BatchOutputs, stream=None):
                                       out.digests.ptr, stream))
 
 
+def metainfo_digest_host(datas, piece_lengths):
+    """End-to-end batch over HOST buffers (numpy uint8 arrays, pageable or
+    pinned): one PCIe pass feeds both kernels.  Returns (sums per blob, digests)."""
+    n = len(datas)
+    pls = np.broadcast_to(np.asarray(piece_lengths, dtype=np.int64), (n,))
+    counts = [int(lib.krk_num_pieces(int(d.size), int(p))) for d, p in zip(datas, pls)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(counts) if n else []
+    arr = (krk_blob * max(n, 1))()
+    for i, d in enumerate(datas):
+        arr[i] = krk_blob(d.ctypes.data if d.size else None, int(d.size), int(pls[i]), int(offs[i]))
+    sums = np.zeros(max(int(offs[-1]), 1), dtype=np.uint32)
+    dg = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    check(lib.krk_metainfo_digest_host(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       dg.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return [sums[int(offs[i]):int(offs[i + 1])] for i in range(n)], dg[:n]
+
+
 def nodes_struct(labels, weights):
     enc = [s.encode() for s in labels]
     blob = b"".join(enc)

@@ -175,3 +175,22 @@ def test_generator_generate_and_batch(gpu, orc, tmp_path):
     for mi, d, b in zip(mis, ds, blobs):
         pl = mi.PieceLength()
         assert bytes(mi.InfoHash()) == orc.info_hash(pl, orc.calc_piece_sums(b, pl)[1], d.Hex(), len(b))
+
+
+@pytest.mark.parametrize("window_mb", [1, 256])
+def test_metainfo_digest_host_end_to_end(gpu, orc, window_mb):
+    """krk_metainfo_digest_host: host buffers, one PCIe pass feeding both kernels,
+    several windows per blob at 1 MiB (midstate chaining + CRC across windows)."""
+    rng = np.random.default_rng(window_mb)
+    lens = [0, 1, 63, 64, 65, 4095, 1 << 20, (3 << 20) + 17, 5_000_001]
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in lens]
+    pls = [4096, 3, 64, 64, 10, 4096, 1 << 18, 1 << 20, 4 << 20]
+    os.environ["KRK_WINDOW_MB"] = str(window_mb)
+    try:
+        sums, dg = D.metainfo_digest_host(datas, pls)
+    finally:
+        del os.environ["KRK_WINDOW_MB"]
+    for i, d in enumerate(datas):
+        assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), lens[i]
+        ref = orc.calc_piece_sums(d, pls[i])[1]
+        assert np.array_equal(sums[i], ref), lens[i]

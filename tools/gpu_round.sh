@@ -32,11 +32,16 @@ for s in "$@"; do
     probe1) step probe_v1 300 python tools/probe_perf.py --variant 1 --sha none ;;
     shaA) step probe_sha0 300 python tools/probe_perf.py --sha-variant 0 --crc-gb 1 --sha 1024:8,16384:1 ;;
     shaB) step probe_sha1 300 python tools/probe_perf.py --sha-variant 1 --crc-gb 1 --sha 64:8,1024:8,16384:1 ;;
+    pmcsha) step pmc_sha_a 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES --output-format csv -d $R/gpurun_out/pmc_sha_a -- python3 $R/tools/probe_perf.py --crc-gb 0 --sha 1024:8 &&
+            step pmc_sha_b 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU --output-format csv -d $R/gpurun_out/pmc_sha_b -- python3 $R/tools/probe_perf.py --crc-gb 0 --sha 1024:8 &&
+            step pmc_sha_c 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $R/gpurun_out/pmc_sha_c -- python3 $R/tools/probe_perf.py --crc-gb 0 --sha 1024:8 ;;
+    micro) step micro_banks 120 tools/micro/vgpr_banks ;;
+    shaD) step probe_sha_diag 300 python tools/probe_perf.py --sha-variant 2 --crc-gb 0 --sha 64:8,1024:8 ;;
     c2split) step probe_c2 300 python tools/probe_perf.py --c2 ;;
     benchsmall) step bench_small 300 python bench.py --workload small --cpu-seconds 3 ;;
     bench) step bench 900 python bench.py ;;
-    prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
-    pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e ;;
+    pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e ;;
+    pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e ;;
   esac
 done
