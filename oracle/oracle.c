@@ -615,6 +615,7 @@ typedef struct {
     uint64_t n;
     int64_t piece_len;
     int fast;
+    int passes; /* bit 0: SHA-256 pass, bit 1: CRC piece pass */
     uint8_t* digests;
     uint32_t* sums;
     const uint64_t* sums_off;
@@ -636,7 +637,9 @@ static void bl_blob(bl_job* J, uint64_t b) {
     const uint64_t CH = 32768; /* io.Copy's 32 KiB buffer */
     uint8_t dg[32];
     /* pass 1: SHA-256 (uploader.verify / CAStore.WriteCacheFile) */
-    if (J->fast && orc_have_shani()) {
+    if (!(J->passes & 1)) {
+        memset(dg, 0, sizeof dg);
+    } else if (J->fast && orc_have_shani()) {
         /* SHA-NI block function over whole 32 KiB chunks (chunks are multiples of 64 B) */
         orc_sha256_ctx c;
         orc_sha256_init(&c);
@@ -653,6 +656,7 @@ static void bl_blob(bl_job* J, uint64_t b) {
     }
     if (J->digests) memcpy(J->digests + 32 * b, dg, 32);
     /* pass 2: CRC piece sums (Generate -> NewMetaInfo -> calcPieceSums) */
+    if (!(J->passes & 2)) return;
     uint64_t P = (uint64_t)J->piece_len, k = 0, off = 0;
     for (;;) {
         uint64_t n = L - off < P ? L - off : P;
@@ -689,7 +693,7 @@ static void* fill_worker(void* a) {
 }
 
 double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
-                        int64_t piece_len, int n_threads, int fast, uint64_t repeats,
+                        int64_t piece_len, int n_threads, int fast, int passes, uint64_t repeats,
                         uint8_t* digests_out, uint32_t* sums_out, const uint64_t* sums_off) {
     if (n_threads < 1) n_threads = 1;
     if (repeats < 1) repeats = 1;
@@ -709,6 +713,7 @@ double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint6
         for (uint64_t i = 0; i < m; i++) pthread_join(th[i], NULL);
     }
     J.lengths = lengths; J.n = n_blobs; J.piece_len = piece_len; J.fast = fast;
+    J.passes = passes ? passes : 3;
     J.digests = digests_out; J.sums = sums_out; J.sums_off = sums_off; J.next = 0;
     J.n_jobs = n_blobs * repeats;
     pthread_barrier_init(&J.bar, NULL, (unsigned)n_threads + 1);

@@ -92,9 +92,10 @@ void orc_synth_fill(uint64_t blob_idx, uint64_t off, uint8_t* out, uint64_t n, i
  * For each of n_blobs synthetic blobs (generated untimed): SHA-256 pass
  * (uploader.go:74-94) then CRC piece pass (metainfo.go:158-179), both streamed
  * in 32 KiB chunks; the job list visits every blob `repeats` times (bounded RAM,
- * longer sample).  Returns seconds of the timed section; outputs optional. */
+ * longer sample).  passes: bit 0 SHA-256 pass, bit 1 CRC pass (0 = both).
+ * Returns seconds of the timed section; outputs optional. */
 double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
-                        int64_t piece_len, int n_threads, int fast, uint64_t repeats,
+                        int64_t piece_len, int n_threads, int fast, int passes, uint64_t repeats,
                         uint8_t* digests_out, uint32_t* sums_out, const uint64_t* sums_off);
 /* HRW baseline: GetOrderedNodes + Locations per digest on n_threads. */
 double orc_baseline_hrw(const uint8_t* digests, uint64_t n, const char* labels,

@@ -52,7 +52,7 @@ def _load() -> C.CDLL:
         "orc_piece_length_for_size": (C.c_int64, [i64p, i64p, C.c_uint32, C.c_int64]),
         "orc_blob_seed": (C.c_uint64, [C.c_uint64]),
         "orc_synth_fill": (None, [C.c_uint64, C.c_uint64, u8p, C.c_uint64, C.c_int]),
-        "orc_baseline_run": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
+        "orc_baseline_run": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_uint64, u8p, u32p, u64p]),
         "orc_baseline_hrw": (C.c_double, [u8p, C.c_uint64, C.c_char_p, u64p, C.c_uint32, u8p,
                                           C.c_int32, C.c_int, i32p, u8p]),
@@ -231,7 +231,7 @@ def synth(blob_idx: int, length: int, offset: int = 0, variant: int = 0) -> np.n
 # ---- CPU baseline -----------------------------------------------------------
 
 def baseline_run(blob_idx, lengths, piece_length: int, threads: int, fast: bool = True,
-                 want_outputs: bool = False, repeats: int = 1):
+                 want_outputs: bool = False, repeats: int = 1, passes: int = 3):
     """Times the reference's two-pass structure (SHA pass, then CRC piece pass),
     one blob per worker thread.  Returns (seconds, digests|None, sums|None)."""
     bi = np.ascontiguousarray(np.asarray(blob_idx, dtype=np.uint64))
@@ -246,7 +246,7 @@ def baseline_run(blob_idx, lengths, piece_length: int, threads: int, fast: bool 
         sums = np.zeros(max(int(off[-1]), 1), dtype=np.uint32)
         dp, sp, op = _ptr(dg, C.c_uint8), _ptr(sums, C.c_uint32), _ptr(off, C.c_uint64)
     t = lib().orc_baseline_run(_ptr(bi, C.c_uint64), _ptr(ln, C.c_uint64), len(bi), piece_length,
-                               threads, 1 if fast else 0, repeats, dp, sp, op)
+                               threads, 1 if fast else 0, passes, repeats, dp, sp, op)
     return t, dg, (sums, off) if want_outputs else None
 
 
