@@ -1,24 +1,34 @@
 #!/usr/bin/env python
 """bench.py -- metainfo+digest GB/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "C2"): 1,000 synthetic 100 MiB blobs, 4 MiB
-pieces, resident in HBM.  One step = the hot path over the batch: the piece
-CRC-32 of every piece (core.calcPieceSums) and the whole-blob SHA-256 of every
-blob (core.Digester), both through the C ABI (krk_metainfo_digest_dev: the SHA
-and CRC kernels run concurrently on two streams), with the 25,000 sums and the
-1,000 digests copied back to the host inside the step.
+Default workload (BASELINE.json configs[1], "C2"): 1,000 synthetic 100 MiB
+blobs, 4 MiB pieces, resident in HBM.  One step = the hot path over the batch:
+the piece CRC-32 of every piece (core.calcPieceSums) and the whole-blob SHA-256
+of every blob (core.Digester), both through the C ABI (krk_metainfo_digest_dev:
+the SHA and CRC kernels run concurrently on two streams), with the 25,000 sums
+and the 1,000 digests copied back to the host inside the step.
+
+Other configs of BASELINE.json (--workload): c1 (one 1 GiB blob), c3 (this
+rank's LPT shard of 20k blobs of 100 MiB-1 GiB, streamed through HBM in
+windows with krk_metainfo_digest_chunks_dev; the synthetic window generation
+runs on its own stream, overlapped, inside the timed region), c4 (one 20 GiB
+blob, 256 KiB pieces, piece sums only), c5 (1M-digest hashring placement,
+digests/s) and c5regen (1,000 blobs of log-uniform sizes with the metainfogen
+piece-length ranges).
 
 Multi-GPU: one process per GPU (torch.distributed.run); the path shards by blob
-with no data-path collective (weak scaling: every rank runs its own 1,000 blobs,
-blob ids offset by rank).  A gloo barrier brackets the timed region, the time is
-the max over ranks, and value = bytes processed by all ranks / that time.
+with no data-path collective (C2 is weak scaling: every rank runs its own 1,000
+blobs, ids offset by rank; C3 is a fixed total split by LPT).  A gloo barrier
+brackets the timed region, the time is the max over ranks, and value = units
+processed by all ranks / that time.
 
-cpu_baseline (rank 0, N=1): the CPU restatement of the reference's two-pass path
-(oracle/, SHA-NI + PCLMUL variants) on all host cores of this box, one blob per
-thread, on a bounded sample of the same synthetic blobs.
+cpu_baseline (rank 0, N=1): the CPU restatement of the reference's path
+(oracle/: the two-pass SHA-NI + PCLMUL run, or the HRW ring placement) on the
+host cores of this box, on a bounded sample of the same synthetic inputs.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -30,12 +40,29 @@ import numpy as np  # noqa: E402
 
 METRIC = "metainfo+digest GB/s (device-resident & end-to-end) at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+GAMMA = 0x9E3779B97F4A7C15
+M64 = (1 << 64) - 1
+
+# Per-stream SHA-256 issue ceiling (Kernels): the consumer wave alone,
+# running a block's 64 rounds with no producer and no barrier (diagnostic kernel
+# variant 2), sustains 36.9 MB/s per stream (profiles/r01/sha_consumer_only_diag.jsonl)
+# -- the rounds' own issue time, 12 VOP3 + 2 VOP2 per round at ~5 / ~4 cycles each
+# for a lone wave (profiles/r01/micro_vgpr_issue_cost.txt), 2.39 GHz under load
+# (profiles/r01/sha_pmc_1024x8MB.json).
+SHA_STREAM_CEILING_MBPS = 36.9
+SHA_MODEL_MBPS = 2.39e9 * 64 / (64 * (12 * 5 + 2 * 4) + 33) / 1e6  # ~34.9, the cycle-count model
 
 WORKLOADS = {
-    # name: (n_blobs, blob_bytes, piece_length, description)
-    "c2": (1000, 100 << 20, 4 << 20, "C2: 1000 x 100 MiB blobs, 4 MiB pieces, piece CRC-32 + SHA-256 per blob"),
-    "c1": (1, 1 << 30, 4 << 20, "C1: 1 x 1 GiB blob, 4 MiB pieces"),
-    "small": (64, 16 << 20, 4 << 20, "dev: 64 x 16 MiB blobs, 4 MiB pieces"),
+    "c2": dict(kind="metainfo", desc="C2: 1000 x 100 MiB blobs, 4 MiB pieces, piece CRC-32 + SHA-256 per blob"),
+    "c1": dict(kind="metainfo", desc="C1: 1 x 1 GiB blob, 4 MiB pieces (one SHA-256 stream)"),
+    "small": dict(kind="metainfo", desc="dev: 64 x 16 MiB blobs, 4 MiB pieces"),
+    "c5regen": dict(kind="metainfo", desc="C5 regen: 1000 blobs, log-uniform sizes in [0, 1 GiB), piece lengths "
+                                          "from {0:1MB, 2GB:4MB, 4GB:8MB}"),
+    "c4": dict(kind="pieces", desc="C4: one 20 GiB blob per GPU, 256 KiB pieces (81,920), piece sums only"),
+    "c3": dict(kind="chunked", desc="C3: 20k blobs of 100 MiB + (rng mod 968,884,225) B, 4 MiB pieces, "
+                                    "LPT-sharded by blob, streamed through HBM in windows"),
+    "c5": dict(kind="hrw", desc="C5: 1M seeded 32-B digests -> hashring.Locations (ShardID key), "
+                                "16 origins weight 100, MaxReplica 3, all healthy"),
 }
 
 
@@ -44,6 +71,12 @@ def _env_int(k, d):
         return int(os.environ.get(k, d))
     except ValueError:
         return d
+
+
+def mix64(z: int) -> int:
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
 
 
 def host_cores() -> int:
@@ -63,29 +96,192 @@ def host_cores() -> int:
     return n
 
 
-def cpu_baseline(n_bytes_blob, piece, target_s, want_check):
+# ----------------------------------------------------------------- workloads
+def c3_lengths(n_total=20000):
+    """L_i = 104,857,600 + (rng_i mod 968,884,225), rng_i = mix64(0xC3 + i*gamma)."""
+    return [104_857_600 + mix64((0xC3 + i * GAMMA) & M64) % 968_884_225 for i in range(n_total)]
+
+
+def c5regen_lengths(n=1000):
+    """Log-uniform in [0, 2^30): L = floor(2^(30*u)) - 1, u from a seeded stream."""
+    out = []
+    for i in range(n):
+        u = (mix64((0xC5 + i * GAMMA) & M64) >> 11) / float(1 << 53)
+        out.append(int(math.floor(2.0 ** (30.0 * u))) - 1)
+    return out
+
+
+def workload_blobs(name, rank, world, nblobs_override):
+    """(blob ids, lengths, piece length) this rank processes."""
+    if name == "c2":
+        n = nblobs_override or 1000
+        return [rank * n + i for i in range(n)], [100 << 20] * n, 4 << 20
+    if name == "c1":
+        return [rank], [1 << 30], 4 << 20
+    if name == "small":
+        n = nblobs_override or 64
+        return [rank * n + i for i in range(n)], [16 << 20] * n, 4 << 20
+    if name == "c4":
+        return [rank], [20 << 30], 256 << 10
+    if name == "c5regen":
+        from kraken_amd import metainfogen
+        lens = c5regen_lengths(nblobs_override or 1000)
+        cfg = metainfogen.newPieceLengthConfig({0: 1 << 20, 2 << 30: 4 << 20, 4 << 30: 8 << 20})
+        pls = {cfg.get(L) for L in lens}
+        assert len(pls) == 1, pls  # every C5 regen blob is < 2 GB -> 1 MiB pieces
+        ids = [(1 << 40) + rank * len(lens) + i for i in range(len(lens))]
+        return ids, lens, pls.pop()
+    if name == "c3":
+        from kraken_amd.shard import lpt_shard
+        lens = c3_lengths(nblobs_override or 20000)
+        mine = lpt_shard(lens, world)[rank]
+        return [(2 << 40) + i for i in mine], [lens[i] for i in mine], 4 << 20
+    raise ValueError(name)
+
+
+# -------------------------------------------------------------- CPU baseline
+def cpu_baseline_metainfo(lens_sample, ids_sample, piece, target_s, passes=3):
     from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
     O.build()
     threads = host_cores()
-    m = 2 * threads
-    ids = list(range(m))
-    lens = [n_bytes_blob] * m
-    # calibration pass (also yields outputs for the cross-check)
-    t1, dg, sums = O.baseline_run(ids, lens, piece, threads, fast=True, want_outputs=want_check)
-    per_pass = max(t1, 1e-3)
-    reps = max(1, int(round(target_s / per_pass)))
-    t, _, _ = O.baseline_run(ids, lens, piece, threads, fast=True, repeats=reps)
-    gbps = m * reps * n_bytes_blob / t / 1e9
-    info = {"value": round(gbps, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": (f"{m} x {n_bytes_blob >> 20} MiB synthetic blobs x {reps} passes ({t:.1f} s): "
-                       "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL), 32 KiB chunks, one blob per "
-                       f"thread, {threads} threads (the host CPU share of this GPU), oracle/oracle.c"),
+    t1, dg, sums = O.baseline_run(ids_sample, lens_sample, piece, threads, fast=True, want_outputs=True,
+                                  passes=passes)
+    reps = max(1, int(round(target_s / max(t1, 1e-3))))
+    t, _, _ = O.baseline_run(ids_sample, lens_sample, piece, threads, fast=True, repeats=reps, passes=passes)
+    total = sum(lens_sample) * reps
+    what = {3: "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL)", 2: "CRC-32 piece pass (PCLMUL) only",
+            1: "SHA-256 pass (SHA-NI) only"}[passes]
+    info = {"value": round(total / t / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": (f"{len(lens_sample)} synthetic blobs ({sum(lens_sample) / 2**20:.0f} MiB) x {reps} passes "
+                       f"({t:.1f} s): {what}, 32 KiB chunks, one blob per thread, {threads} threads (the host "
+                       "CPU share of this GPU), oracle/oracle.c"),
             "seconds": round(t, 2), "have_shani": bool(O.lib().orc_have_shani()),
             "have_clmul": bool(O.lib().orc_have_clmul())}
     return info, dg, sums
 
 
-def end_to_end(D, arena, n, Le, P, out, dist):
+def cpu_baseline_hrw(digests, labels, healthy, max_replica, target_s):
+    from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
+    O.build()
+    threads = host_cores()
+    m = min(len(digests), 100_000)
+    t1, locs, counts = O.baseline_hrw(digests[:m], labels, healthy, max_replica, threads)
+    reps = max(1, int(round(target_s / max(t1, 1e-3))))
+    t = 0.0
+    for _ in range(reps):
+        t += O.baseline_hrw(digests[:m], labels, healthy, max_replica, threads)[0]
+    return ({"value": round(m * reps / t, 1), "unit": "digests/s", "cores": threads, "kind": "port",
+             "sample": f"{m} digests x {reps} passes ({t:.1f} s): GetOrderedNodes(ShardID) + Locations filter "
+                       f"per digest, {threads} threads, oracle/oracle.c"}, locs, counts)
+
+
+# ------------------------------------------------------------------ runners
+class Timer:
+    def __init__(self, D, dist):
+        self.D, self.dist = D, dist
+
+    def barrier(self):
+        self.D.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def roofline_obj(kernel, gbps, avg_ms, bytes_launch, traffic):
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(gbps / HBM_PEAK_GBPS, 5), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
+            "algorithmic_bytes_per_launch": bytes_launch}
+
+
+def load_traffic(path, workload, n):
+    try:
+        pm = json.load(open(path))
+        if pm.get("workload") == workload and pm.get("blobs") == n:
+            return pm.get("bytes_per_launch", {})
+    except (ValueError, OSError):
+        pass
+    return {}
+
+
+def run_metainfo(a, D, T, rank, world, res):
+    ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
+    n = len(lens)
+    arena = D.BlobArena(lens, P, blob_ids=ids)
+    out = D.BatchOutputs(arena)
+    sums_h = np.empty(max(arena.total_pieces, 1), dtype=np.uint32)
+    dg_h = np.empty(max(n, 1) * 32, dtype=np.uint8)
+
+    def step():
+        D.metainfo_digest(arena, out)
+        D.synchronize()
+        sums_h[:] = out.sums.to_host(np.uint32, sums_h.size)
+        dg_h[:] = out.digests.to_host(np.uint8, dg_h.size)
+
+    for _ in range(a.warmup):
+        step()
+    T.barrier()
+    with D.KernelTimer():
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        T.barrier()
+        t1 = time.perf_counter()
+        crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
+        sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
+    elapsed = T.max_over_ranks(t1 - t0)
+    bytes_rank = int(sum(lens))
+    value = world * bytes_rank * a.steps / elapsed / 1e9
+    crc_avg, sha_avg = crc_ms / max(crc_n, 1), sha_ms / max(sha_n, 1)
+    crc_gbps = bytes_rank / (crc_avg / 1e3) / 1e9 if crc_n else 0.0
+    sha_gbps = bytes_rank / (sha_avg / 1e3) / 1e9 if sha_n else 0.0
+    traffic = load_traffic(a.pmc_json, a.workload, n)
+    dominant = "sha256_multi" if sha_avg >= crc_avg else "crc32_pieces"
+    roof = roofline_obj(dominant, sha_gbps if dominant == "sha256_multi" else crc_gbps,
+                        sha_avg if dominant == "sha256_multi" else crc_avg, bytes_rank, traffic.get(dominant))
+    if dominant == "sha256_multi":
+        per_stream = max(lens) / (sha_avg / 1e3) / 1e6
+        roof["note"] = ("SHA-256 is one sequential Merkle-Damgard chain per blob (one lane each): this kernel is "
+                        "bound by per-stream VALU issue, not HBM; issue_bound compares the longest stream's rate "
+                        "with the per-stream issue ceiling (DESIGN.md)")
+        roof["issue_bound"] = {"achieved_per_stream_MBps": round(per_stream, 2),
+                               "ceiling_per_stream_MBps": round(SHA_STREAM_CEILING_MBPS, 2),
+                               "frac": round(per_stream / SHA_STREAM_CEILING_MBPS, 4), "streams": n,
+                               "ceiling_source": "rounds-only diagnostic kernel (variant 2), same hardware",
+                               "model_per_stream_MBps": round(SHA_MODEL_MBPS, 2)}
+    res.update({"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "steps": a.steps,
+                "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "weak", "dtype": "u8",
+                "data": "synthetic (device-generated splitmix64 blobs, spec in DESIGN.md)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "blobs_per_gpu": n,
+                           "bytes_per_gpu": bytes_rank, "piece_length": P, "mode": "device-resident",
+                           "parallelism": f"blob-sharded x{world}, no collective"},
+                "roofline": roof,
+                "roofline_crc": roofline_obj("crc32_pieces", crc_gbps, crc_avg, bytes_rank,
+                                             traffic.get("crc32_pieces")),
+                "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)},
+                            "sha256_multi": {"launches": sha_n, "avg_ms": round(sha_avg, 3)}}})
+    if a.workload == "c2" and not a.no_e2e:
+        res["end_to_end"] = end_to_end(D, T, arena, n, min(a.e2e_mb << 20, lens[0]), P, out, world)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        m = min(n, 2 * host_cores())  # bounded sample: the first blobs of this workload
+        cb, dg, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds)
+        ok = all(bytes(dg[k]) == bytes(dg_h[32 * k:32 * k + 32]) for k in range(m))
+        s, off = sums
+        for k in range(m):
+            o, cnt = int(arena.sums_off[k]), int(off[k + 1] - off[k])
+            ok = ok and np.array_equal(s[int(off[k]):int(off[k + 1])], sums_h[o:o + cnt])
+        cb["outputs_match_gpu"] = bool(ok)
+        res["cpu_baseline"] = cb
+
+
+def end_to_end(D, T, arena, n, Le, P, out, world):
     """End-to-end leg (reported beside `value`, never as it): the same blobs' first
     Le bytes in pageable host memory, through krk_metainfo_digest_host (pinned
     windows, one PCIe pass feeding both kernels), results back on the host."""
@@ -94,26 +290,201 @@ def end_to_end(D, arena, n, Le, P, out, dist):
     for i, d in enumerate(datas):  # the device blobs' prefixes (device-generated content)
         D.check(D.lib.krk_memcpy_d2h(d.ctypes.data_as(C.c_void_p), arena.buf.ptr + int(arena.offsets[i]), Le))
     D.metainfo_digest_host(datas[:2], P)  # warm the staging windows
-    if dist is not None:
-        dist.barrier()
+    T.barrier()
     t0 = time.perf_counter()
     sums, dg = D.metainfo_digest_host(datas, P)
-    t1 = time.perf_counter()
-    el = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    world = dist.get_world_size() if dist is not None else 1
-    # piece sums of the prefixes must equal the device-resident run's first pieces
+    el = T.max_over_ranks(time.perf_counter() - t0)
     dev_sums = out.sums.to_host(np.uint32, arena.total_pieces)
     k = Le // P
     ok = all(np.array_equal(sums[i][:k], dev_sums[int(arena.sums_off[i]):int(arena.sums_off[i]) + k])
              for i in range(n)) if k else None
     return {"value": round(world * n * Le / el / 1e9, 3), "unit": "GB/s", "blobs_per_gpu": n, "blob_bytes": Le,
             "seconds": round(el, 3), "source": "pageable host memory (numpy), copied into pinned windows",
-            "bound": "PCIe H2D / SHA per-stream rate", "sums_match_device_run": ok}
+            "bound": "PCIe H2D / host staging copy / SHA per-stream rate", "sums_match_device_run": ok}
+
+
+def run_pieces(a, D, T, rank, world, res):
+    ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
+    arena = D.BlobArena(lens, P, blob_ids=ids)
+    out = D.BatchOutputs(arena)
+    sums_h = np.empty(max(arena.total_pieces, 1), dtype=np.uint32)
+
+    def step():
+        D.piece_sums(arena, out)
+        D.synchronize()
+        sums_h[:] = out.sums.to_host(np.uint32, sums_h.size)
+
+    for _ in range(a.warmup):
+        step()
+    T.barrier()
+    with D.KernelTimer():
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        T.barrier()
+        t1 = time.perf_counter()
+        crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
+    elapsed = T.max_over_ranks(t1 - t0)
+    bytes_rank = int(sum(lens))
+    crc_avg = crc_ms / max(crc_n, 1)
+    crc_gbps = bytes_rank / (crc_avg / 1e3) / 1e9
+    res.update({"metric": "piece-sum (NewMetaInfo CRC-32) GB/s",
+                "value": round(world * bytes_rank * a.steps / elapsed / 1e9, 3), "unit": "GB/s",
+                "steps": a.steps, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "weak", "dtype": "u8", "data": "synthetic (device-generated splitmix64 blobs)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "bytes_per_gpu": bytes_rank,
+                           "piece_length": P, "pieces_per_gpu": arena.total_pieces, "mode": "device-resident"},
+                "roofline": roofline_obj("crc32_pieces", crc_gbps, crc_avg, bytes_rank,
+                                         load_traffic(a.pmc_json, a.workload, len(lens)).get("crc32_pieces")),
+                "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)}}})
+    # InfoHash over the 81,920 sums stays on the host (bencode + SHA-1, core/metainfo.go:37-44)
+    from kraken_amd import core
+    t0 = time.perf_counter()
+    core._info_hash(P, sums_h[:arena.total_pieces], "0" * 64, lens[0])
+    res["info_hash_host_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        m = 2 * host_cores()
+        cb, _, sums = cpu_baseline_metainfo([256 << 20] * m, [ids[0]] * m, P, a.cpu_seconds, passes=2)
+        s, off = sums
+        cnt = int(off[1] - off[0])
+        cb["outputs_match_gpu"] = bool(np.array_equal(s[:cnt], sums_h[:cnt]))
+        cb["sample"] += " (sample blobs: 256 MiB prefixes of the same synthetic blob)"
+        res["cpu_baseline"] = cb
+
+
+def run_chunked(a, D, T, rank, world, res):
+    """C3: every blob of this rank's LPT shard advances by one chunk per window; the
+    next window's bytes are generated on the device (own stream) while the
+    current window's kernels run."""
+    import ctypes as C
+    ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
+    n = len(lens)
+    W = a.window_gib << 30
+    bufs = [D.DeviceBuffer(W + 16 * n), D.DeviceBuffer(W + 16 * n)]
+    cb = D.ChunkedBatch(lens, P)
+    gen_s, run_s = C.c_void_p(), C.c_void_p()
+    D.check(D.lib.krk_stream_create(C.byref(gen_s)))
+    D.check(D.lib.krk_stream_create(C.byref(run_s)))
+
+    wins, pos, live = [], [0] * n, list(range(n))
+    while live:  # every live blob advances by the same 64-multiple chunk per window
+        c = max(64, (W // len(live)) // 64 * 64)
+        w, nxt = [], []
+        for i in live:
+            take = min(c, lens[i] - pos[i])
+            w.append((i, pos[i], take))
+            pos[i] += take
+            if pos[i] < lens[i]:
+                nxt.append(i)
+        wins.append(w)
+        live = nxt
+
+    def items_of(k):
+        buf, out, off = bufs[k & 1], [], 0
+        for (i, o, ln) in wins[k]:
+            out.append((i, buf.ptr + off, o, ln))
+            off += (ln + 15) // 16 * 16
+        return out
+
+    def gen(items):
+        D.synth_fill_chunks([(ids[i], p, o, ln) for (i, p, o, ln) in items], stream=gen_s)
+        D.check(D.lib.krk_stream_sync(gen_s))
+
+    T.barrier()
+    with D.KernelTimer():
+        t0 = time.perf_counter()
+        cur = items_of(0)
+        gen(cur)
+        for k in range(len(wins)):
+            D.check(D.lib.krk_stream_sync(run_s))  # window k-1 done: its buffer may be refilled
+            cb.step(cur, stream=run_s)
+            if k + 1 < len(wins):
+                cur = items_of(k + 1)
+                gen(cur)
+        D.check(D.lib.krk_stream_sync(run_s))
+        T.barrier()
+        t1 = time.perf_counter()
+        sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
+        crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
+        gen_n, gen_ms = D.KernelTimer.stats("synth_fill")
+    elapsed = T.max_over_ranks(t1 - t0)
+    bytes_rank = int(sum(lens))
+    total_bytes = int(sum(c3_lengths(a.blobs or 20000)))
+    res.update({"metric": "metainfo+digest GB/s (C3, device-generated windows)",
+                "value": round(total_bytes / elapsed / 1e9, 3), "unit": "GB/s", "steps": 1,
+                "ms_per_step": round(elapsed * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+                "dtype": "u8", "data": "synthetic (generated on the device per window, inside the timed region)",
+                "config": {"workload": WORKLOADS["c3"]["desc"], "blobs_total": a.blobs or 20000,
+                           "blobs_this_rank": n, "bytes_this_rank": bytes_rank, "bytes_total": total_bytes,
+                           "windows": len(wins), "window_bytes": W, "piece_length": P,
+                           "longest_blob": max(lens), "parallelism": f"LPT blob shard x{world}, no collective"},
+                "kernels": {"sha256_multi": {"launches": sha_n, "total_ms": round(sha_ms, 1)},
+                            "crc32_pieces": {"launches": crc_n, "total_ms": round(crc_ms, 1)},
+                            "synth_fill": {"launches": gen_n, "total_ms": round(gen_ms, 1)}},
+                "note": "bounded below by the longest blob's sequential SHA-256 chain (longest_blob / per-stream "
+                        "rate) at any GPU count"})
+    if rank == 0:  # spot-check three blobs against the one-shot device path
+        pick = sorted({0, n // 2, n - 1})
+        dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
+        sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
+        del bufs[:]
+        arena = D.BlobArena([lens[i] for i in pick], P, blob_ids=[ids[i] for i in pick])
+        out = D.BatchOutputs(arena)
+        D.metainfo_digest(arena, out)
+        D.synchronize()
+        ref = out.digests.to_host(np.uint8, 32 * len(pick)).reshape(-1, 32)
+        rs = out.sums.to_host(np.uint32, arena.total_pieces)
+        ok = all(bytes(dg[i]) == bytes(ref[k]) for k, i in enumerate(pick))
+        for k, i in enumerate(pick):
+            o, ro, cnt = int(cb.sums_off[i]), int(arena.sums_off[k]), int(arena.n_pieces[k])
+            ok = ok and np.array_equal(sums[o:o + cnt], rs[ro:ro + cnt])
+        res["spot_check_matches_one_shot"] = bool(ok)
+    D.lib.krk_stream_destroy(gen_s)
+    D.lib.krk_stream_destroy(run_s)
+
+
+def run_hrw(a, D, T, rank, world, res):
+    n = a.blobs or 1_000_000
+    N, R = a.nodes, 3
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(N)]
+    healthy = np.ones(N, dtype=np.uint8)
+    rng = np.random.default_rng(0xC5 + rank)
+    dig = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(dig.reshape(-1))
+    locs = D.DeviceBuffer(n * R * 4)
+    counts = D.DeviceBuffer(n)
+    locs_h = np.empty((n, R), dtype=np.int32)
+
+    def step():
+        D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts)
+        D.synchronize()
+        locs_h[:] = locs.to_host(np.int32, n * R).reshape(n, R)
+
+    for _ in range(a.warmup):
+        step()
+    T.barrier()
+    with D.KernelTimer():
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        T.barrier()
+        t1 = time.perf_counter()
+        hn, hms = D.KernelTimer.stats("hrw_order")
+        gn, gms = D.KernelTimer.stats("hrw_gather")
+    elapsed = T.max_over_ranks(t1 - t0)
+    res.update({"metric": "hashring placement digests/s (C5)", "value": round(world * n * a.steps / elapsed, 1),
+                "unit": "digests/s", "steps": a.steps, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "weak", "dtype": "u64+f64",
+                "data": "synthetic (seeded random 32-byte digests)",
+                "config": {"workload": WORKLOADS["c5"]["desc"], "digests_per_gpu": n, "nodes": N,
+                           "max_replica": R, "mode": "device-resident (65,536-shard table + gather)"},
+                "kernels": {"hrw_order": {"launches": hn, "avg_ms": round(hms / max(hn, 1), 3)},
+                            "hrw_gather": {"launches": gn, "avg_ms": round(gms / max(gn, 1), 3)}}})
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cbl, cl, cc = cpu_baseline_hrw(dig, labels, healthy, R, a.cpu_seconds)
+        cbl["outputs_match_gpu"] = bool(np.array_equal(cl, locs_h[:cl.shape[0]]))
+        res["cpu_baseline"] = cbl
 
 
 def main():
@@ -122,7 +493,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--blobs", type=int, default=0, help="override the blob count")
+    ap.add_argument("--blobs", type=int, default=0, help="override the blob (or digest) count")
+    ap.add_argument("--nodes", type=int, default=16, help="C5: origins in the ring")
+    ap.add_argument("--window-gib", type=int, default=48, help="C3: device window size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -140,96 +513,17 @@ def main():
     from kraken_amd import device as D
 
     D.set_device(local)
-    n, L, P, desc = WORKLOADS[a.workload]
-    if a.blobs:
-        n = a.blobs
-    ids = [rank * n + i for i in range(n)]
-    arena = D.BlobArena([L] * n, P, blob_ids=ids)
-    out = D.BatchOutputs(arena)
-    sums_h = np.empty(max(arena.total_pieces, 1), dtype=np.uint32)
-    dg_h = np.empty(max(n, 1) * 32, dtype=np.uint8)
-
-    def step():
-        D.metainfo_digest(arena, out)
-        D.synchronize()
-        sums_h[:] = out.sums.to_host(np.uint32, sums_h.size)
-        dg_h[:] = out.digests.to_host(np.uint8, dg_h.size)
-
-    def barrier():
-        D.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    for _ in range(a.warmup):
-        step()
-    barrier()
-    with D.KernelTimer():
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            step()
-        barrier()
-        t1 = time.perf_counter()
-        crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
-        sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    bytes_rank = n * L
-    value = world * bytes_rank * a.steps / elapsed / 1e9
-    crc_avg = crc_ms / max(crc_n, 1)
-    sha_avg = sha_ms / max(sha_n, 1)
-    crc_gbps = bytes_rank / (crc_avg / 1e3) / 1e9 if crc_n else 0.0
-    sha_gbps = bytes_rank / (sha_avg / 1e3) / 1e9 if sha_n else 0.0
-    traffic = {}
-    if os.path.exists(a.pmc_json):
-        try:
-            pm = json.load(open(a.pmc_json))
-            if pm.get("workload") == a.workload and pm.get("blobs") == n:
-                traffic = pm.get("bytes_per_launch", {})
-        except (ValueError, OSError):
-            traffic = {}
-    dominant = "sha256_multi" if sha_avg >= crc_avg else "crc32_pieces"
-    dom_gbps = sha_gbps if dominant == "sha256_multi" else crc_gbps
-    dom_avg = sha_avg if dominant == "sha256_multi" else crc_avg
-    roofline = {"kernel": dominant, "bound": "hbm", "achieved": round(dom_gbps, 2), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 5),
-                "traffic": traffic.get(dominant), "avg_launch_ms": round(dom_avg, 3),
-                "algorithmic_bytes_per_launch": bytes_rank}
-    if dominant == "sha256_multi":
-        # one Merkle-Damgard stream per lane: the chain is latency/issue bound per stream
-        roofline["note"] = ("SHA-256 is sequential per blob: the ceiling is n_blobs x per-stream rate, "
-                            "not HBM; see per_stream_MBps")
-        roofline["per_stream_MBps"] = round(L / (sha_avg / 1e3) / 1e6, 2)
-    crc_roof = {"kernel": "crc32_pieces", "bound": "hbm", "achieved": round(crc_gbps, 2), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(crc_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic.get("crc32_pieces"),
-                "avg_launch_ms": round(crc_avg, 3), "algorithmic_bytes_per_launch": bytes_rank}
-
-    res = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-           "data": "synthetic (device-generated splitmix64 blobs, spec in DESIGN.md)",
-           "config": {"workload": desc, "blobs_per_gpu": n, "blob_bytes": L, "piece_length": P,
-                      "mode": "device-resident", "parallelism": f"blob-sharded x{world}, no collective"},
-           "roofline": roofline, "roofline_crc": crc_roof,
-           "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)},
-                       "sha256_multi": {"launches": sha_n, "avg_ms": round(sha_avg, 3)}}}
-    if not a.no_e2e:
-        res["end_to_end"] = end_to_end(D, arena, n, min(a.e2e_mb << 20, L), P, out, dist)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cb, dg, sums = cpu_baseline(L, P, a.cpu_seconds, True)
-        m = len(dg)
-        ok = bool(np.array_equal(dg.reshape(-1), dg_h[: m * 32])) if m <= n else None
-        if ok and sums is not None:
-            s, off = sums
-            ok = bool(np.array_equal(s[: int(off[min(m, n)])], sums_h[: int(off[min(m, n)])]))
-        cb["outputs_match_gpu"] = ok
-        res["cpu_baseline"] = cb
+    T = Timer(D, dist)
+    res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
+    kind = WORKLOADS[a.workload]["kind"]
+    {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw}[kind](
+        a, D, T, rank, world, res)
+    order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config"]
+    line = {k: res[k] for k in order if k in res}
+    line.update({k: v for k, v in res.items() if k not in line})
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

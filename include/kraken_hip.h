@@ -115,6 +115,27 @@ void krk_digester_free(krk_digester* d);
 int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev,
                             uint8_t* digests_dev, void* stream);
 
+/* Chunked (streaming) form on device data: each call advances every listed blob
+ * by one chunk -- SHA-256 from the blob's midstate in state_dev (8 words per
+ * blob slot, written back), CRC-32 of the chunk's byte range XOR-accumulated
+ * into its pieces' sums (sums_dev must be zero before a blob's first chunk).
+ * A blob's chunks are submitted in order, one per call; every chunk but the
+ * last is a multiple of 64 bytes; the chunk that reaches blob_length writes
+ * the digest to digests_dev[32*blob].  This is the multi-blob Digester.Write +
+ * calcPieceSums step that end-to-end and larger-than-HBM batches (C3) run
+ * window by window.  Asynchronous on `stream`. */
+typedef struct krk_chunk {
+    const uint8_t* data;     /* device pointer to the chunk's bytes */
+    uint64_t offset;         /* chunk's first byte inside its blob */
+    uint64_t length;         /* chunk bytes */
+    uint64_t blob_length;    /* total blob length */
+    int64_t piece_length;    /* > 0 */
+    uint64_t sums_offset;    /* blob's first piece-sum slot */
+    uint64_t blob;           /* blob slot for state_dev / digests_dev */
+} krk_chunk;
+int krk_metainfo_digest_chunks_dev(const krk_chunk* chunks, uint64_t n_chunks, uint32_t* state_dev,
+                                   uint32_t* sums_dev, uint8_t* digests_dev, void* stream);
+
 /* End-to-end form: blobs[i].data are HOST pointers (pageable or pinned).  Every
  * byte crosses PCIe once: the library copies the caller's bytes into its own
  * pinned windows (several host threads), uploads each window once and runs
@@ -177,6 +198,10 @@ int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_n
  * spec in DESIGN.md).  Benchmark/test data generator. */
 int krk_synth_fill_dev(uint8_t* dst_dev, uint64_t blob_idx, uint64_t offset, uint64_t n,
                        int variant, void* stream);
+/* Batched form for window generation: chunk i fills chunks[i].data (device)
+ * with bytes [offset, offset+length) of synthetic blob chunks[i].blob (the
+ * other krk_chunk fields are ignored).  One launch. */
+int krk_synth_fill_chunks_dev(const krk_chunk* chunks, uint64_t n, int variant, void* stream);
 
 /* ------------------------------------------------ device memory helpers
  * For callers (benchmarks, cgo) that do not own a device allocator. */

@@ -27,6 +27,12 @@ class krk_blob(C.Structure):
                 ("sums_offset", C.c_uint64)]
 
 
+class krk_chunk(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offset", C.c_uint64), ("length", C.c_uint64),
+                ("blob_length", C.c_uint64), ("piece_length", C.c_int64), ("sums_offset", C.c_uint64),
+                ("blob", C.c_uint64)]
+
+
 class krk_nodes(C.Structure):
     _fields_ = [("labels", C.c_char_p), ("label_off", C.POINTER(C.c_uint64)),
                 ("weights", C.POINTER(C.c_int64)), ("n_nodes", C.c_uint32)]
@@ -66,6 +72,7 @@ def _load() -> C.CDLL:
         "krk_digester_free": (None, [vp]),
         "krk_metainfo_digest_dev": (i, [blobp, C.c_uint64, vp, vp, vp]),
         "krk_metainfo_digest_host": (i, [blobp, C.c_uint64, u32p, u8p]),
+        "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),
         "krk_bencode_info": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p,
                                  C.c_uint64, u64p]),
@@ -74,6 +81,7 @@ def _load() -> C.CDLL:
         "krk_ring_locations": (i, [u8p, C.c_uint64, nodesp, u8p, C.c_int32, i32p, u8p]),
         "krk_ring_locations_dev": (i, [vp, C.c_uint64, nodesp, u8p, C.c_int32, vp, vp, vp]),
         "krk_synth_fill_dev": (i, [vp, C.c_uint64, C.c_uint64, C.c_uint64, i, vp]),
+        "krk_synth_fill_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, i, vp]),
         "krk_dev_alloc": (i, [C.c_uint64, C.POINTER(vp)]),
         "krk_dev_free": (i, [vp]),
         "krk_memcpy_h2d": (i, [vp, vp, C.c_uint64]),

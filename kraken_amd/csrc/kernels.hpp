@@ -93,6 +93,14 @@ hipError_t launch_shard_gather(const uint8_t* digests32, uint64_t n, const int32
                                uint8_t* counts, hipStream_t s);
 
 // ---------------------------------------------------------------- synthetic data
+// One synthetic chunk: bytes [offset, offset + n) of the blob whose stream seed is `seed`.
+struct SynthChunk {
+    uint8_t* dst;
+    uint64_t seed;
+    uint64_t offset;
+    uint64_t n;
+};
+hipError_t launch_synth_fill_chunks(const SynthChunk* chunks, uint32_t n_chunks, int variant, hipStream_t s);
 hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n,
                              int variant, hipStream_t s);
 

@@ -739,6 +739,76 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     return r;
 }
 
+static int validate_chunks(const krk_chunk* c, uint64_t n) {
+    KRK_CHECK(n == 0 || c, KRK_EINVAL, "chunks is NULL");
+    std::unordered_map<uint64_t, uint64_t> seen;
+    seen.reserve(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        KRK_CHECK(seen.emplace(c[i].blob, i).second, KRK_EINVAL, "blob slot %llu appears twice in one call",
+                  (unsigned long long)c[i].blob);
+        KRK_CHECK(c[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
+        KRK_CHECK(c[i].length == 0 || c[i].data, KRK_EINVAL, "chunk %llu: data is NULL", (unsigned long long)i);
+        KRK_CHECK(c[i].offset + c[i].length <= c[i].blob_length, KRK_ERANGE, "chunk %llu runs past its blob",
+                  (unsigned long long)i);
+        KRK_CHECK(c[i].offset % 64 == 0, KRK_EINVAL, "chunk %llu: offset is not a multiple of 64",
+                  (unsigned long long)i);
+        KRK_CHECK(c[i].length % 64 == 0 || c[i].offset + c[i].length == c[i].blob_length, KRK_EINVAL,
+                  "chunk %llu: only a blob's last chunk may be a partial block", (unsigned long long)i);
+        KRK_CHECK(c[i].blob <= 0xFFFFFFFFull, KRK_EINVAL, "blob slot exceeds 2^32");
+        KRK_CHECK(c[i].sums_offset + krk_num_pieces(c[i].blob_length, c[i].piece_length) <= 0xFFFFFFFFull,
+                  KRK_EINVAL, "sums index exceeds 2^32 in one call");
+    }
+    return KRK_OK;
+}
+
+// One window step over device chunks: SHA jobs on D->s_a, CRC items on D->s_b,
+// both forked from and joined back into s.
+static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
+                       uint8_t* digests_dev, hipStream_t s, ItemBuilder& B) {
+    std::vector<ShaJob> jobs(n);
+    std::vector<CrcItem> items;
+    for (uint64_t i = 0; i < n; ++i) {
+        ShaJob& j = jobs[i];
+        j = ShaJob{};
+        j.ptr = reinterpret_cast<uint64_t>(c[i].data);
+        j.len = c[i].length;
+        j.prefix = c[i].offset;
+        j.out = (uint32_t)c[i].blob;
+        j.flags = (c[i].offset + c[i].length == c[i].blob_length ? kShaFinal : 0) | (c[i].offset ? kShaFromState : 0);
+        memcpy(j.h, kIV, sizeof kIV);
+        if (c[i].length)
+            B.add(items, j.ptr, c[i].offset, c[i].offset + c[i].length, c[i].blob_length,
+                  (uint64_t)c[i].piece_length, c[i].sums_offset);
+    }
+    hipEvent_t fork, j1, j2;
+    KRK_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    KRK_HIP(hipEventCreateWithFlags(&j1, hipEventDisableTiming));
+    KRK_HIP(hipEventCreateWithFlags(&j2, hipEventDisableTiming));
+    KRK_HIP(hipEventRecord(fork, s));
+    KRK_HIP(hipStreamWaitEvent(D->s_a, fork, 0));
+    KRK_HIP(hipStreamWaitEvent(D->s_b, fork, 0));
+    int r = run_jobs(D, jobs, digests_dev, state_dev, D->s_a);
+    if (!r) r = run_items(D, items, sums_dev, D->s_b);
+    hipEventRecord(j1, D->s_a);
+    hipEventRecord(j2, D->s_b);
+    hipStreamWaitEvent(s, j1, 0);
+    hipStreamWaitEvent(s, j2, 0);
+    hipEventDestroy(fork);
+    hipEventDestroy(j1);
+    hipEventDestroy(j2);
+    return r;
+}
+
+int krk_metainfo_digest_chunks_dev(const krk_chunk* chunks, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
+                                   uint8_t* digests_dev, void* stream) {
+    KRK_DEVICE(D);
+    int r = validate_chunks(chunks, n);
+    if (r || !n) return r;
+    KRK_CHECK(state_dev && sums_dev && digests_dev, KRK_EINVAL, "chunks_dev: null output");
+    ItemBuilder B;
+    return chunks_step(D, chunks, n, state_dev, sums_dev, digests_dev, pick(D, stream), B);
+}
+
 int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {
     KRK_DEVICE(D);
     int r = validate_blobs(blobs, n);
@@ -1340,6 +1410,38 @@ int krk_synth_fill_dev(uint8_t* dst_dev, uint64_t blob_idx, uint64_t offset, uin
     };
     const uint64_t seed = mix((0x4B52414B454EULL ^ blob_idx) + GAMMA);
     hipError_t e = timed(K_SYNTH, s, [&] { return launch_synth_fill(dst_dev, seed, offset, n, variant, s); });
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+int krk_synth_fill_chunks_dev(const krk_chunk* chunks, uint64_t n, int variant, void* stream) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(chunks, KRK_EINVAL, "chunks is NULL");
+    KRK_CHECK(n <= 0xFFFFFFFFull / 16, KRK_EINVAL, "too many chunks");
+    KRK_DEVICE(D);
+    hipStream_t s = pick(D, stream);
+    const uint64_t GAMMA = 0x9E3779B97F4A7C15ULL;
+    auto mix = [](uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    };
+    std::vector<SynthChunk> sc;
+    sc.reserve(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (!chunks[i].length) continue;
+        KRK_CHECK(chunks[i].data, KRK_EINVAL, "chunk %llu: data is NULL", (unsigned long long)i);
+        sc.push_back({const_cast<uint8_t*>(chunks[i].data), mix((0x4B52414B454EULL ^ chunks[i].blob) + GAMMA),
+                      chunks[i].offset, chunks[i].length});
+    }
+    if (sc.empty()) return KRK_OK;
+    void* d_sc = nullptr;
+    int r = upload(D, sc.data(), sc.size() * sizeof(SynthChunk), &d_sc, s);
+    if (r) return r;
+    hipError_t e = timed(K_SYNTH, s, [&] {
+        return launch_synth_fill_chunks(static_cast<const SynthChunk*>(d_sc), (uint32_t)sc.size(), variant, s);
+    });
+    scratch_free(D, d_sc, s);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", hipGetErrorString(e));
     return KRK_OK;
 }

@@ -47,6 +47,45 @@ __global__ void synth_fill_bytes(uint8_t* dst, uint64_t seed, uint64_t offset, u
     }
 }
 
+// Many chunks in one launch (window generation for chunked batches): a fixed
+// number of workgroups per chunk, each striding over its share of the chunk's
+// 16-byte pairs (dst 16-aligned and offset 8-aligned) or bytes otherwise.
+constexpr uint32_t kSynthBlocksPerChunk = 16;
+
+__global__ void __launch_bounds__(256) synth_fill_chunks(const SynthChunk* __restrict__ chunks, uint32_t n_chunks,
+                                                         int variant) {
+    const uint32_t c = blockIdx.x / kSynthBlocksPerChunk, part = blockIdx.x % kSynthBlocksPerChunk;
+    if (c >= n_chunks) return;
+    const SynthChunk k = chunks[c];
+    const uint64_t stride = (uint64_t)kSynthBlocksPerChunk * blockDim.x;
+    const uint64_t t0 = (uint64_t)part * blockDim.x + threadIdx.x;
+    uint64_t head = 0;
+    if ((k.offset & 7) == 0 && (reinterpret_cast<uintptr_t>(k.dst) & 15) == 0) {
+        const uint64_t npairs = k.n / 16, word0 = k.offset >> 3;
+        uint4* d = reinterpret_cast<uint4*>(k.dst);
+        for (uint64_t i = t0; i < npairs; i += stride) {
+            const uint64_t j = word0 + 2 * i;
+            uint64_t a = mix64(k.seed + (j + 1) * kGamma), b = mix64(k.seed + (j + 2) * kGamma);
+            if (variant) { a = alnum8(a); b = alnum8(b); }
+            d[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+        }
+        head = npairs * 16;
+    }
+    for (uint64_t i = head + t0; i < k.n; i += stride) {
+        const uint64_t pos = k.offset + i;
+        uint64_t w = mix64(k.seed + ((pos >> 3) + 1) * kGamma);
+        if (variant) w = alnum8(w);
+        k.dst[i] = (uint8_t)(w >> (8 * (pos & 7)));
+    }
+}
+
+hipError_t launch_synth_fill_chunks(const SynthChunk* chunks, uint32_t n_chunks, int variant, hipStream_t s) {
+    if (!n_chunks) return hipSuccess;
+    hipLaunchKernelGGL(synth_fill_chunks, dim3(n_chunks * kSynthBlocksPerChunk), dim3(256), 0, s, chunks, n_chunks,
+                       variant);
+    return hipGetLastError();
+}
+
 hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n, int variant,
                              hipStream_t s) {
     if (!n) return hipSuccess;

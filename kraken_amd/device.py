@@ -6,7 +6,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._capi import check, krk_blob, krk_nodes, lib
+from ._capi import check, krk_blob, krk_chunk, krk_nodes, lib
 
 ALIGN = 256  # every blob starts 256-byte aligned in the arena
 
@@ -36,6 +36,9 @@ class DeviceBuffer:
         if n:
             check(lib.krk_memcpy_d2h(out.ctypes.data, self.ptr + offset, n * it))
         return out
+
+    def zero(self):
+        self.from_host(np.zeros(self.nbytes, dtype=np.uint8))
 
     def from_host(self, a: np.ndarray, offset: int = 0):
         a = np.ascontiguousarray(a)
@@ -144,6 +147,44 @@ def metainfo_digest_host(datas, piece_lengths):
     check(lib.krk_metainfo_digest_host(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)),
                                        dg.ctypes.data_as(C.POINTER(C.c_uint8))))
     return [sums[int(offs[i]):int(offs[i + 1])] for i in range(n)], dg[:n]
+
+
+class ChunkedBatch:
+    """Window-by-window metainfo+digest over device chunks (krk_metainfo_digest_chunks_dev):
+    per-blob SHA midstates and XOR-accumulated piece sums live on the device between steps."""
+
+    def __init__(self, lengths, piece_lengths):
+        self.lengths = np.asarray(lengths, dtype=np.uint64)
+        n = len(self.lengths)
+        self.piece_lengths = np.array(np.broadcast_to(np.asarray(piece_lengths, dtype=np.int64), (n,)))
+        self.n_pieces = np.array([lib.krk_num_pieces(int(L), int(p)) for L, p in
+                                  zip(self.lengths, self.piece_lengths)], dtype=np.uint64)
+        self.sums_off = np.zeros(n, dtype=np.uint64)
+        if n:
+            self.sums_off[1:] = np.cumsum(self.n_pieces)[:-1]
+        self.total_pieces = int(self.n_pieces.sum())
+        self.state = DeviceBuffer(max(n, 1) * 32)
+        self.sums = DeviceBuffer(max(self.total_pieces, 1) * 4)
+        self.sums.zero()
+        self.digests = DeviceBuffer(max(n, 1) * 32)
+
+    def step(self, items, stream=None):
+        """items: [(blob index, device address of the chunk, offset, length)]."""
+        arr = (krk_chunk * max(len(items), 1))()
+        for k, (i, ptr, off, ln) in enumerate(items):
+            arr[k] = krk_chunk(ptr, int(off), int(ln), int(self.lengths[i]), int(self.piece_lengths[i]),
+                               int(self.sums_off[i]), int(i))
+        check(lib.krk_metainfo_digest_chunks_dev(arr, len(items), self.state.ptr, self.sums.ptr,
+                                                 self.digests.ptr, stream))
+
+
+def synth_fill_chunks(items, variant: int = 0, stream=None):
+    """items: [(blob id, device address, offset, length)] -> bytes [offset, offset+length)
+    of each synthetic blob written at its address, one launch."""
+    arr = (krk_chunk * max(len(items), 1))()
+    for k, (b, ptr, off, ln) in enumerate(items):
+        arr[k] = krk_chunk(ptr, int(off), int(ln), 0, 1, 0, int(b))
+    check(lib.krk_synth_fill_chunks_dev(arr, len(items), variant, stream))
 
 
 def nodes_struct(labels, weights):

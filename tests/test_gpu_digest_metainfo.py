@@ -194,3 +194,55 @@ def test_metainfo_digest_host_end_to_end(gpu, orc, window_mb):
         assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), lens[i]
         ref = orc.calc_piece_sums(d, pls[i])[1]
         assert np.array_equal(sums[i], ref), lens[i]
+
+
+def test_metainfo_digest_chunks_dev(gpu, orc):
+    """krk_metainfo_digest_chunks_dev: blobs advanced by uneven 64-multiple chunks
+    over several calls (blobs finishing at different calls) == one-shot results."""
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 64, 200, 4096, 70_000, 1 << 20, (1 << 20) + 3]
+    pls = [8, 3, 64, 7, 1000, 4096, 1 << 18, 100_000]
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in lens]
+    buf = D.DeviceBuffer(sum(lens) + 16 * len(lens))
+    base, off = [], 0
+    for d in datas:
+        base.append(off)
+        buf.from_host(d, off)
+        off += (d.size + 15) // 16 * 16
+    cb = D.ChunkedBatch(lens, pls)
+    pos = [0] * len(lens)
+    started = [False] * len(lens)
+    while not all(started[i] and pos[i] >= lens[i] for i in range(len(lens))):
+        items = []
+        for i, L in enumerate(lens):
+            if started[i] and pos[i] >= L:
+                continue
+            step = int(rng.integers(1, 5000)) * 64
+            take = min(step, L - pos[i])
+            items.append((i, buf.ptr + base[i] + pos[i], pos[i], take))
+            pos[i] += take
+            started[i] = True
+        cb.step(items)
+    D.synchronize()
+    dg = cb.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+    sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
+    for i, d in enumerate(datas):
+        assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), lens[i]
+        ref = orc.calc_piece_sums(d, pls[i])[1]
+        o = int(cb.sums_off[i])
+        assert np.array_equal(sums[o:o + len(ref)], ref), lens[i]
+
+
+def test_synth_fill_chunks_matches_spec(gpu, orc):
+    """Batched window generator == the synthetic-blob spec (oracle/oracle.c orc_synth_fill)."""
+    specs = [(3, 0, 100), (3, 100, 1 << 16), (9, 64, 4097), (11, 7, 33), (12, 1 << 20, 1_000_003)]
+    buf = D.DeviceBuffer(sum(n + 16 for _, _, n in specs))
+    items, off = [], 0
+    for b, o, n in specs:
+        items.append((b, buf.ptr + off, o, n))
+        off += (n + 15) // 16 * 16
+    D.synth_fill_chunks(items)
+    D.synchronize()
+    for (b, o, n), (_, ptr, _, _) in zip(specs, items):
+        got = buf.to_host(np.uint8, n, ptr - buf.ptr)
+        assert np.array_equal(got, orc.synth(b, n, offset=o)), (b, o, n)

@@ -40,6 +40,11 @@ for s in "$@"; do
     c2split) step probe_c2 300 python tools/probe_perf.py --c2 ;;
     benchsmall) step bench_small 300 python bench.py --workload small --cpu-seconds 3 ;;
     bench) step bench 900 python bench.py ;;
+    bc1) step bench_c1 600 python bench.py --workload c1 --steps 1 --warmup 1 ;;
+    bc3) step bench_c3 900 python bench.py --workload c3 ;;
+    bc4) step bench_c4 600 python bench.py --workload c4 ;;
+    bc5) step bench_c5 600 python bench.py --workload c5 ;;
+    bc5r) step bench_c5regen 900 python bench.py --workload c5regen --steps 1 --warmup 1 ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e ;;
     pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e ;;
     pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e ;;
