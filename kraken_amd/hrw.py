@@ -106,4 +106,43 @@ def NewRendezvousHash() -> RendezvousHash:
     return RendezvousHash()
 
 
-__all__ = ["RendezvousHash", "RendezvousHashNode", "NewRendezvousHash", "KrakenError"]
+def UInt64ToFloat64(bytes_uint: bytes, max_value: bytes = b"\xff" * 8, rehash=None) -> float:
+    """rendezvous.go:99-118 on the host (the device path computes the same in
+    hrw_place.hip): the low 53 bits of the big-endian value, re-hashed once by
+    `rehash(bytes) -> 8 bytes` when they are all zero, divided by 2^53."""
+    ones53 = int.from_bytes(max_value[:8], "big") >> 11
+    val = int.from_bytes(bytes_uint[:8], "big") & ones53
+    if val == 0 and rehash is not None:
+        val = int.from_bytes(rehash(bytes_uint)[:8], "big") & ones53
+    return float(val) / float(1 << 53)
+
+
+def _round_prec(v: int, prec: int) -> int:
+    """Round a non-negative integer to `prec` significant bits, ties to even
+    (big.Float.SetPrec's default rounding mode)."""
+    extra = v.bit_length() - prec
+    if extra <= 0:
+        return v
+    q, r = divmod(v, 1 << extra)
+    half = 1 << (extra - 1)
+    if r > half or (r == half and q & 1):
+        q += 1
+    return q << extra
+
+
+def BigIntToFloat64(bytes_uint: bytes, max_value: bytes, hasher=None) -> float:
+    """rendezvous.go:120-146 (test-only in the reference; no ring uses it):
+    big.Float(hash) rounded to 53 bits, divided by big.Float(max) into a
+    53-bit result (round to nearest even), returned as float64."""
+    del hasher  # unused by the reference too
+    h = _round_prec(int.from_bytes(bytes_uint, "big"), 53)
+    m = int.from_bytes(max_value, "big")
+    if m == 0:
+        raise ZeroDivisionError("BigIntToFloat64: zero max value")
+    # Python's int / int true division is correctly rounded to the nearest double
+    # (53-bit significand, ties to even) -- big.Float.Quo at prec 53 + Float64().
+    return h / m
+
+
+__all__ = ["RendezvousHash", "RendezvousHashNode", "NewRendezvousHash", "UInt64ToFloat64", "BigIntToFloat64",
+           "KrakenError"]

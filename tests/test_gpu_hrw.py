@@ -125,3 +125,26 @@ def test_ring_locations_dev_full_table(gpu, orc):
     from kraken_amd import core
     d = core.NewSHA256DigestFromHex(bytes(digests[0]).hex())
     assert ring.Locations(d) == [labels[j] for j in locs[0, : counts[0]]]
+
+
+def test_cas_volume_placement(gpu, orc, tmp_path):
+    """lib/store/ca_store.go:137-171: weighted HRW over volumes for subdirs "%02X"."""
+    from kraken_amd import castore
+    vols = []
+    for i, w in enumerate((100, 200, 400, 800)):
+        p = tmp_path / f"vol{i}"
+        p.mkdir()
+        vols.append(castore.Volume(str(p), w))
+    m = castore.volume_subdirs(vols)
+    labels, weights = [v.Location for v in vols], [v.Weight for v in vols]
+    for sub, loc in m.items():
+        assert loc == labels[orc.hrw_ordered(sub, labels, weights)[0]], sub
+    d = tmp_path / "cas"
+    d.mkdir()
+    castore.initCASVolumes(str(d), vols)
+    for sub, loc in m.items():
+        assert os.readlink(d / sub) == os.path.join(loc, "cas", sub)
+        assert (d / sub).is_dir()
+    castore.initCASVolumes(str(d), vols)  # idempotent
+    with pytest.raises(OSError, match="verify volume"):
+        castore.initCASVolumes(str(d), [castore.Volume(str(tmp_path / "missing"), 100)])

@@ -70,3 +70,49 @@ def test_piece_length_config():
         metainfogen.newPieceLengthConfig({})
     with pytest.raises(ValueError, match="piece length config: no piece lengths configured"):
         metainfogen.New({}, None)
+
+
+def test_score_function_float_precision():
+    """lib/hrw/rendezvous_test.go:30-57 (TestScoreFunctionFloatPrecision)."""
+    import math
+    from kraken_amd import hrw
+    for idx, bl in enumerate((8, 16, 32)):
+        for si, f in enumerate((hrw.BigIntToFloat64, hrw.UInt64ToFloat64)):
+            if idx > 0 and si > 0:
+                continue
+            v = f(b"\x00" * (bl - 1) + b"\x01", b"\xff" * bl, None)
+            assert v != 0.0 and math.isfinite(math.log(v))
+
+
+def test_bigint_to_float64_rounding():
+    """BigIntToFloat64 = round53(round53(h) / max): exact cases and correct rounding."""
+    from fractions import Fraction
+    from kraken_amd import hrw
+    M8 = b"\xff" * 8
+    assert hrw.BigIntToFloat64((1 << 63).to_bytes(8, "big"), M8) == 0.5
+    assert hrw.BigIntToFloat64(b"\xff" * 8, M8) == 1.0
+    assert hrw.BigIntToFloat64(b"\x00" * 8, M8) == 0.0
+    rng = np.random.default_rng(7)
+    for bl in (8, 16, 32):
+        M = (1 << (8 * bl)) - 1
+        for _ in range(200):
+            h = int.from_bytes(rng.bytes(bl), "big")
+            got = hrw.BigIntToFloat64(h.to_bytes(bl, "big"), M.to_bytes(bl, "big"))
+            h53 = hrw._round_prec(h, 53)
+            assert h53.bit_length() <= max(53, h.bit_length() + 1)
+            exact = Fraction(h53, M)
+            # nearest double: no double strictly closer than `got`
+            lo, hi = np.nextafter(got, 0.0), np.nextafter(got, 2.0)
+            assert abs(Fraction(got) - exact) <= abs(Fraction(float(lo)) - exact)
+            assert abs(Fraction(got) - exact) <= abs(Fraction(float(hi)) - exact)
+
+
+def test_uint64_to_float64_host_matches_oracle(orc):
+    """rendezvous.go:99-118: host helper == oracle restatement, incl. the rehash rule."""
+    from kraken_amd import hrw
+    rh = lambda b: orc.murmur3_h1(b).to_bytes(8, "big")
+    vals = [1, 2, (1 << 53) - 1, 1 << 53, 1 << 60, (1 << 64) - 1, 0x123456789ABCDEF0] + [1 << k for k in range(53, 64)]
+    for v in vals:
+        b = v.to_bytes(8, "big")
+        assert hrw.UInt64ToFloat64(b, rehash=rh) == orc.uint64_to_float64(v, rehash=True), hex(v)
+        assert hrw.UInt64ToFloat64(b) == orc.uint64_to_float64(v, rehash=False), hex(v)
