@@ -143,7 +143,8 @@ def workload_blobs(name, rank, world, nblobs_override):
 def cpu_baseline_metainfo(lens_sample, ids_sample, piece, target_s, passes=3):
     from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
     O.build()
-    threads = host_cores()
+    # one blob per worker, as the reference (one goroutine per blob): C1's single blob is one core
+    threads = min(host_cores(), len(lens_sample))
     t1, dg, sums = O.baseline_run(ids_sample, lens_sample, piece, threads, fast=True, want_outputs=True,
                                   passes=passes)
     reps = max(1, int(round(target_s / max(t1, 1e-3))))

@@ -62,6 +62,13 @@ class DirCAS:
             f.write(b)
         return True
 
+    def WriteCacheFileAs(self, d: core.Digest, data) -> core.Digest:
+        """Commit already-verified bytes under their digest."""
+        os.makedirs(self._dir(d.Hex()), exist_ok=True)
+        with open(os.path.join(self._dir(d.Hex()), "data"), "wb") as f:
+            f.write(memoryview(data))
+        return d
+
     def WriteCacheFile(self, data: bytes) -> core.Digest:
         d = core.NewDigester().FromBytes(data)
         os.makedirs(self._dir(d.Hex()), exist_ok=True)
@@ -118,6 +125,35 @@ class Generator:
             s = sums[o:o + n].copy() if n else None
             ih = core._info_hash(pl, s if s is not None else np.zeros(0, np.uint32), d.Hex(), b.size)
             mi = core.MetaInfo(pl, s, d.Hex(), b.size, d, ih)
+            self.cas.SetCacheFileMetadata(d.Hex(), mi)
+            out.append(mi)
+        return out
+
+
+    def VerifyAndGenerateBatch(self, uploads):
+        """Fused upload verification + metainfo generation.
+
+        The reference reads every uploaded blob twice: uploader.verify digests it
+        (origin/blobserver/uploader.go:74-94, error "computed digest %s doesn't
+        match parameter %s") and Generate later re-reads the committed cache file
+        for the piece sums (generator.go:41-58).  Here one host->device pass over
+        each blob (krk_metainfo_digest_host) yields both.  uploads: [(core.Digest
+        expected, bytes-like data)].  Verified blobs are committed to the CAS with
+        their _torrentmeta; returns [MetaInfo | ValueError] in input order."""
+        from . import device as D
+        datas = [np.frombuffer(memoryview(b), dtype=np.uint8) for _, b in uploads]
+        pls = [self.pieceLengthConfig.get(int(x.size)) for x in datas]
+        sums, dg = D.metainfo_digest_host(datas, pls)
+        out = []
+        for (want, _), x, pl, s, g in zip(uploads, datas, pls, sums, dg):
+            got = core.NewSHA256DigestFromHex(bytes(g).hex())
+            if got != want:
+                out.append(ValueError(f"computed digest {got.String()} doesn't match parameter {want.String()}"))
+                continue
+            d = self.cas.WriteCacheFileAs(want, x)
+            s = s.copy() if s.size else None
+            ih = core._info_hash(pl, s if s is not None else np.zeros(0, np.uint32), d.Hex(), int(x.size))
+            mi = core.MetaInfo(pl, s, d.Hex(), int(x.size), d, ih)
             self.cas.SetCacheFileMetadata(d.Hex(), mi)
             out.append(mi)
         return out

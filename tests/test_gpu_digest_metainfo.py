@@ -246,3 +246,25 @@ def test_synth_fill_chunks_matches_spec(gpu, orc):
     for (b, o, n), (_, ptr, _, _) in zip(specs, items):
         got = buf.to_host(np.uint8, n, ptr - buf.ptr)
         assert np.array_equal(got, orc.synth(b, n, offset=o)), (b, o, n)
+
+
+def test_verify_and_generate_batch(gpu, orc, tmp_path):
+    """Fused upload verify + Generate (one PCIe pass): a corrupted upload is rejected
+    with the reference's message, the others are committed with byte-identical
+    _torrentmeta to the two-pass path."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path))
+    g = metainfogen.New({0: 1 << 20, 4 << 20: 4 << 20}, cas)
+    blobs = [os.urandom(n) for n in (0, 5, 1 << 20, (4 << 20) + 7, 3_000_001)]
+    want = [core.NewSHA256DigestFromHex(hashlib.sha256(b).hexdigest()) for b in blobs]
+    bad = bytearray(blobs[3])
+    bad[12345] ^= 1
+    ups = list(zip(want, blobs)) + [(want[3], bytes(bad))]
+    res = g.VerifyAndGenerateBatch(ups)
+    assert isinstance(res[-1], ValueError) and "doesn't match parameter" in str(res[-1])
+    for mi, d, b in zip(res[:-1], want, blobs):
+        pl = 1 << 20 if len(b) < 4 << 20 else 4 << 20
+        assert bytes(mi.InfoHash()) == orc.info_hash(pl, orc.calc_piece_sums(b, pl)[1], d.Hex(), len(b))
+        two_pass = core.NewMetaInfo(d, b, pl)
+        assert open(tmp_path / d.Hex() / "_torrentmeta", "rb").read() == two_pass.Serialize()
+        assert open(tmp_path / d.Hex() / "data", "rb").read() == b
