@@ -349,6 +349,119 @@ __device__ __forceinline__ u32x4 kw_quad(const uint32_t* lds, int slot, int q, u
     return *reinterpret_cast<const u32x4*>(lds + kw_index(slot, q, lane));
 }
 
+// ---------------------------------------------------------------------------
+// Two lanes per stream.  One lane runs the rounds of a stream at one VALU op per
+// ~4.4 cycles (a lone wave cannot issue faster), so when a batch has fewer
+// streams than the chip has SIMDs the per-stream chain is the bound, and spending
+// two lanes on one stream buys a shorter chain.  The A lane keeps the a-history
+// (a, b, c, d) and the E lane the e-history (e, f, g, h) of the same stream; both
+// run ONE instruction stream with per-lane operands, the A lane one round behind
+// the E lane (in instruction-round n the E lane runs round n, the A lane n-1):
+//   S = rotr(x0, r1) ^ rotr(x0, r2) ^ rotr(x0, r3)   A: Sigma0(a)      E: Sigma1(e)
+//   k = x0 ^ (x1 & mA) ^ ~mA                         A: a ^ b          E: ~e
+//   F = k ? x2 : x1                                  A: Maj(a, b, c)   E: Ch(e, f, g)
+//   P                                                A: e[n] - d[n-1]  E: d[n] + h + KW[n]
+//   x0' = S + F + P                                  A: a[n]           E: e[n+1]
+// The A lane's T1 = e[n] - d[n-1] is the E lane's result of the previous
+// instruction-round and the E lane's d[n] = a[n-3] is three rounds old, so both
+// cross-lane reads (DPP) are off the recurrence, which is three VALU ops deep
+// (rotate, xor3, add3).  Ten ops a round: 7 VOP3, 1 VOP2, 2 DPP
+// (tools/micro/sha2lane.hip prices the variants; the un-skewed form with the
+// combine DPP on the chain measured 56 cycles a round, one lane 63).
+//
+// Lane layout (DPP rows of 16 lanes, banks of 4): stream s of the wave's 32 has its
+// A lane in bank 0 or 2 and its E lane four lanes up (bank 1 or 3), so row_shl:4
+// reads the E partner and row_shr:4 the A partner; bank_mask confines each DPP
+// write to one side.
+__device__ __forceinline__ uint32_t two_lane_stream(uint32_t lane) {
+    return (lane >> 4) * 8 + ((lane >> 3) & 1) * 4 + (lane & 3);
+}
+__device__ __forceinline__ bool two_lane_is_e(uint32_t lane) { return (lane >> 2) & 1; }
+
+// One instruction-round; the new x0 overwrites x3 (dead once P is formed) -- or
+// NX for the block's last instruction-round, whose E half is discarded.
+#define KRK_SHA2_ROUND(X0, X1, X2, X3, NX, KW)                                          \
+    "v_add_u32_e32 %[y], %[" #X3 "], %[" #KW "]\n\t"                                   \
+    "v_add_u32_dpp %[p], %[" #X2 "], %[y] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"     \
+    "v_alignbit_b32 %[t1], %[" #X0 "], %[" #X0 "], %[r1]\n\t"                          \
+    "v_alignbit_b32 %[t2], %[" #X0 "], %[" #X0 "], %[r2]\n\t"                          \
+    "v_alignbit_b32 %[t3], %[" #X0 "], %[" #X0 "], %[r3]\n\t"                          \
+    "v_sub_u32_dpp %[p], %[" #X0 "], %[" #X3 "] row_shl:4 row_mask:0xf bank_mask:0x5\n\t" \
+    "v_bitop3_b32 %[k], %[" #X0 "], %[" #X1 "], %[ma] bitop3:0x2d\n\t"                 \
+    "v_bitop3_b32 %[t1], %[t1], %[t2], %[t3] bitop3:0x96\n\t"                          \
+    "v_bitop3_b32 %[k], %[k], %[" #X2 "], %[" #X1 "] bitop3:0xca\n\t"                  \
+    "v_add3_u32 %[" #NX "], %[t1], %[k], %[p]\n\t"
+
+struct TwoLaneConst {
+    uint32_t r1, r2, r3, ma;
+};
+
+#define KRK_SHA2_OPERANDS                                                                             \
+    : [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [k] "=&v"(k), [y] "=&v"(y), [p] "=&v"(p),        \
+      [R0] "+v"(R0), [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
+
+// Instruction-rounds 4q..4q+3 (KW[4q..4q+3] for the E lanes).  History registers
+// rotate: in instruction-round n, x0 = R[n%4], x3 = R[(n+1)%4].
+__device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3,
+                                          const TwoLaneConst& c, const u32x4& kw) {
+    uint32_t t1, t2, t3, k, y, p;
+    asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, R1, w0)
+                 KRK_SHA2_ROUND(R1, R0, R3, R2, R2, w1)
+                 KRK_SHA2_ROUND(R2, R1, R0, R3, R3, w2)
+                 KRK_SHA2_ROUND(R3, R2, R1, R0, R0, w3)
+                 KRK_SHA2_OPERANDS
+                 : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w0] "v"(kw[0]),
+                   [w1] "v"(kw[1]), [w2] "v"(kw[2]), [w3] "v"(kw[3]));
+}
+
+// The 64 rounds of one block on a lane pair: 65 instruction-rounds (the A lane
+// idles in the first, the E lane in the last).  h[] = this lane's half of the
+// state (A: H0..H3, E: H4..H7), fed forward at the end.  Quads 0 and 1 of the
+// block's KW arrive already loaded, the rest are read two quads ahead.
+__device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int slot, uint32_t lane,
+                                        const TwoLaneConst& c, bool is_e, const u32x4& k0, const u32x4& k1) {
+    // Instruction-round 0: E runs round 0 on (e, f, g, h); A "runs round -1" on
+    // (b, c, d) and its result is replaced by a.
+    uint32_t R0 = is_e ? h[0] : h[1], R3 = is_e ? h[1] : h[2], R2 = is_e ? h[2] : h[3], R1 = h[3];
+    {
+        uint32_t t1, t2, t3, k, y, p;
+        asm volatile("s_nop 1\n\t" KRK_SHA2_ROUND(R0, R3, R2, R1, R1, w0)
+                     KRK_SHA2_OPERANDS
+                     : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w0] "v"(k0[0]));
+    }
+    R1 = is_e ? R1 : h[0];
+    {
+        uint32_t t1, t2, t3, k, y, p;
+        // s_nop 1: the DPP reads of R1 in the next two rounds follow its VALU write.
+        asm volatile("s_nop 1\n\t" KRK_SHA2_ROUND(R1, R0, R3, R2, R2, w1)
+                     KRK_SHA2_ROUND(R2, R1, R0, R3, R3, w2)
+                     KRK_SHA2_ROUND(R3, R2, R1, R0, R0, w3)
+                     KRK_SHA2_OPERANDS
+                     : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w1] "v"(k0[1]),
+                       [w2] "v"(k0[2]), [w3] "v"(k0[3]));
+    }
+    u32x4 nkw = k1, nnkw = k1;
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+        if (q + 1 < 16) nnkw = *reinterpret_cast<const u32x4*>(lds + kw_index(slot, q + 1, lane));
+        sha2_quad(R0, R1, R2, R3, c, nkw);
+        nkw = nnkw;
+    }
+    // Instruction-round 64: A runs round 63 into T; E's state is already final.
+    uint32_t T;
+    {
+        uint32_t t1, t2, t3, k, y, p;
+        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, T, w0)
+                     KRK_SHA2_OPERANDS, [T] "=&v"(T)
+                     : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w0] "v"(0u));
+    }
+    h[0] += is_e ? R0 : T;
+    h[1] += is_e ? R3 : R0;
+    h[2] += is_e ? R2 : R3;
+    h[3] += is_e ? R1 : R2;
+}
+#undef KRK_SHA2_OPERANDS
+
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
@@ -358,14 +471,17 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // kTiming (diagnostic variant 2 only, wrong digests): the producer idles and the
 // consumer runs its rounds on whatever the ring holds with no barriers -- the
 // consumer's issue-bound time per block, to price the producer/consumer sync.
-template <bool kTiming>
+// kTwo: two lanes per stream (32 streams per workgroup, rounds2); the producer
+// is unchanged -- both lanes of a stream build the same schedule into their own
+// LDS column.
+template <bool kTiming, bool kTwo>
 __global__ void __launch_bounds__(128)
 sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __restrict__ out_digest,
                  uint32_t* __restrict__ out_state) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ring[];
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = threadIdx.x < 64;
-    const uint32_t j = blockIdx.x * 64 + lane;
+    const uint32_t j = kTwo ? blockIdx.x * 32 + two_lane_stream(lane) : blockIdx.x * 64 + lane;
     const bool live = j < n_jobs;
     ShaJob job{};
     if (live) job = jobs[j];
@@ -392,6 +508,54 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         // The consumer passes nb barriers; the loop above took max(0, nb - kDepth).
         const uint32_t tail = nb < (uint32_t)kDepth ? nb : (uint32_t)kDepth;
         for (uint32_t i = 0; i < tail; ++i) __syncthreads();
+    } else if (kTwo) {
+        const bool is_e = two_lane_is_e(lane);
+        const uint32_t half = is_e ? 4u : 0u;
+        const TwoLaneConst c{is_e ? 6u : 2u, is_e ? 11u : 13u, is_e ? 25u : 22u, is_e ? 0u : ~0u};
+        uint32_t h[4];
+        if (live && (job.flags & kShaFromState)) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[k] = out_state[8 * (uint64_t)job.out + half + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[k] = is_e ? job.h[4 + k] : job.h[k];  // no dynamic index: keeps job out of scratch
+        }
+        __builtin_amdgcn_s_setprio(3);
+        u32x4 k0{}, k1{};
+        for (uint32_t i = 0; i < nb; ++i) {
+            if (!kTiming) __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (i == 0) {
+                k0 = kw_quad(ring, 0, 0, lane);
+                k1 = kw_quad(ring, 0, 1, lane);
+            }
+            uint32_t x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = h[k];
+            rounds2(x, ring, (int)(i % kSlots), lane, c, is_e, k0, k1);
+            if (i + 1 < nb) {
+                k0 = kw_quad(ring, (int)((i + 1) % kSlots), 0, lane);
+                k1 = kw_quad(ring, (int)((i + 1) % kSlots), 1, lane);
+            }
+            if (i < mine) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) h[k] = x[k];
+            }
+        }
+        if (live) {
+            if (job.flags & kShaFinal) {
+                uint8_t* o = out_digest + 32 * (uint64_t)job.out + 4 * half;
+                if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+                    reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+                } else {
+                    for (int k = 0; k < 16; ++k) o[k] = (uint8_t)(h[k >> 2] >> (24 - 8 * (k & 3)));
+                }
+            } else {
+                uint32_t* o = out_state + 8 * (uint64_t)job.out + half;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] = h[k];
+            }
+        }
     } else {
         uint32_t h[8];
         if (live && (job.flags & kShaFromState)) {
@@ -453,27 +617,53 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     }
 }
 
+// KRK_SHA_VARIANT: 0 = one lane does loads + schedule + rounds; 1 = wave-specialised,
+// one lane per stream; 2 = its rounds-only timing diagnostic (wrong digests);
+// 3 = wave-specialised, two lanes per stream; 4 = its timing diagnostic.
+// Default (-1): two lanes while the batch leaves SIMDs idle, else one.
+// Read at every launch (a getenv is cheap next to any SHA launch), so tests can
+// cover each variant in one process.
 static int sha_variant() {
-    static int v = [] {
-        const char* e = getenv("KRK_SHA_VARIANT");
-        return e ? atoi(e) : 1;
+    const char* e = getenv("KRK_SHA_VARIANT");
+    return e ? atoi(e) : -1;
+}
+
+// Streams up to which two lanes per stream win: one two-lane workgroup per CU.
+// Measured (tools/probe_perf.py): 4,096 streams 190 GB/s two-lane vs 147 one-lane;
+// 16,384 streams 448 vs 586 (two-lane workgroups then share SIMDs).
+static uint32_t two_lane_max_streams() {
+    static uint32_t n = [] {
+        const char* e = getenv("KRK_SHA_TWO_LANE_MAX");
+        if (e) return (uint32_t)strtoul(e, nullptr, 10);
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            hipDeviceProp_t p;
+            if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
+        }
+        return (uint32_t)cus * 32u;
     }();
-    return v;
+    return n;
 }
 
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;
-    const uint32_t grid = (n_jobs + 63) / 64;
-    const int v = sha_variant();
-    if (v == 1 || v == 2) {
+    int v = sha_variant();
+    if (v < 0) v = n_jobs <= two_lane_max_streams() ? 3 : 1;
+    if (v >= 1 && v <= 4) {
         constexpr size_t lds = size_t(kSlots) * kSlotWords * 4;  // 64 KiB
-        auto* k = v == 1 ? &sha256_ws_kernel<false> : &sha256_ws_kernel<true>;
+        const bool two = v >= 3;
+        auto* k = v == 1 ? &sha256_ws_kernel<false, false>
+                : v == 2 ? &sha256_ws_kernel<true, false>
+                : v == 3 ? &sha256_ws_kernel<false, true>
+                         : &sha256_ws_kernel<true, true>;
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-        hipLaunchKernelGGL(k, dim3(grid), dim3(128), lds, s, jobs, n_jobs, out_digest, out_state);
+        const uint32_t per = two ? 32u : 64u;
+        hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128), lds, s, jobs, n_jobs, out_digest, out_state);
     } else {
-        hipLaunchKernelGGL(sha256_multi_kernel, dim3(grid), dim3(64), 0, s, jobs, n_jobs, out_digest, out_state);
+        hipLaunchKernelGGL(sha256_multi_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, s, jobs, n_jobs, out_digest,
+                           out_state);
     }
     return hipGetLastError();
 }

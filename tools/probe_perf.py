@@ -69,7 +69,7 @@ if __name__ == "__main__":
     ap.add_argument("--crc-gb", type=float, default=16)
     ap.add_argument("--sha", default="64:8,1024:8,4096:4,16384:1")
     ap.add_argument("--variant", default="0")
-    ap.add_argument("--sha-variant", default="1")
+    ap.add_argument("--sha-variant", default="-1")
     ap.add_argument("--c2", action="store_true")
     a = ap.parse_args()
     os.environ["KRK_CRC_VARIANT"] = a.variant
