@@ -149,10 +149,11 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
 // the message schedule into KW[r] = W[r] + K[r] in an LDS ring; wave 1 (consumer)
 // only runs the 64 rounds (no VMEM, no schedule: ~14 VALU ops per round).  The
 // two waves sit on different SIMDs, so the consumer keeps its full issue rate.
-// One s_barrier per block; the producer runs kDepth blocks ahead in a kSlots
-// ring (kDepth <= kSlots - 1 keeps every slot's reuse behind its last read).
+// One s_barrier per block; the producer fills a ring of kSlots slots (one lane,
+// 4 slots) or kSlots2 slots (two lanes per stream, where each producer step
+// builds two blocks), see produce_step.
 constexpr int kSlots = 4;
-constexpr int kDepth = 3;
+constexpr int kSlots2 = 6;
 constexpr int kSlotWords = 64 * 64;  // 64 rounds x 64 lanes
 
 // LDS image of one slot: [round/4][lane][4] words -> a lane's 4 consecutive KW
@@ -200,7 +201,9 @@ __device__ __forceinline__ void fetch(const ShaJob& job, uint32_t b, u32x4 raw[k
 }
 
 // Block b's 16 big-endian message words from raw[] (+ the 0x80 terminator and the
-// bit length on the final blocks), expanded to KW[r] = W[r] + K[r] in ring slot b % kSlots.
+// bit length on the final blocks), expanded to KW[r] = W[r] + K[r] in ring slot b % kNs,
+// LDS column `lane`.
+template <int kNs>
 __device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4 rawc[kRaw], uint32_t lane,
                                       uint32_t* lds) {
     constexpr uint32_t K[64] = {KRK_K256};
@@ -243,7 +246,7 @@ __device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4
             w[15] = (uint32_t)bits;
         }
     }
-    const int slot = (int)(b % kSlots);
+    const uint32_t slot = b % kNs;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         uint32_t kw[4];
@@ -266,16 +269,36 @@ __device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4
     }
 }
 
-// One producer step (b is wave-uniform): wait for the consumer to free a slot
-// (from block kDepth on), start the loads of block b + 2 (always issued, so no
-// branch sits between a load and its use), then build block b from registers.
-__device__ __forceinline__ void produce_step(const ShaJob& job, uint32_t b, uint32_t nb, uint32_t lane,
-                                             uint32_t* lds, const u32x4 use[kRaw], u32x4 next[kRaw],
-                                             uint64_t safe) {
+// One producer step over blocks b .. b + kStep - 1 (b wave-uniform); this lane
+// builds block ob (one lane per stream: ob = b; two lanes: the A lane b, the E
+// lane b + 1, both into the E lane's column `col`).  The consumer passes one
+// barrier per step (kStep blocks), the producer one per step too, so a step has
+// a whole consumer step of time (two blocks with two lanes: a producer step takes
+// 1.4 us, a consumer block 1.26).  Slot reuse: step m lands on the slots of step
+// m - kNs/kStep, free once the consumer has started step m - kNs/kStep + 1, i.e.
+// passed barrier m - kNs/kStep + 1; the producer reaches barrier j only after
+// building step j + kNs/kStep - 1, and the consumer needs steps j and j + 1 (its
+// prefetch of the next block's first quads) after barrier j.  The loads of this
+// lane's block two steps ahead are issued here (always, so no branch sits between
+// a load and its use), then block ob is built from registers.
+template <int kNs, int kStep, bool kNoLoad = false>
+__device__ __forceinline__ void produce_step(const ShaJob& job, uint32_t b, uint32_t ob, uint32_t nb,
+                                             uint32_t col, uint32_t* lds, const u32x4 use[kRaw],
+                                             u32x4 next[kRaw], uint64_t safe, uint32_t& passed) {
     const bool act = b < nb;
-    if (act && b >= (uint32_t)kDepth) __syncthreads();
-    fetch(job, b + 2, next, safe);
-    if (act) build(job, b, use, lane, lds);
+    if (act) {
+        while (passed + kNs / kStep < b / kStep + 2) {
+            __syncthreads();
+            ++passed;
+        }
+    }
+    if (kNoLoad) {
+#pragma unroll
+        for (int c = 0; c < kRaw; ++c) next[c] = u32x4{b, col, (uint32_t)c, b ^ col};
+    } else {
+        fetch(job, ob + 2 * kStep, next, safe);
+    }
+    if (act) build<kNs>(job, ob, use, col, lds);
 }
 
 // Four SHA-256 rounds as one fixed 56-instruction sequence.  The compiler's
@@ -355,112 +378,135 @@ __device__ __forceinline__ u32x4 kw_quad(const uint32_t* lds, int slot, int q, u
 // streams than the chip has SIMDs the per-stream chain is the bound, and spending
 // two lanes on one stream buys a shorter chain.  The A lane keeps the a-history
 // (a, b, c, d) and the E lane the e-history (e, f, g, h) of the same stream; both
-// run ONE instruction stream with per-lane operands, the A lane one round behind
-// the E lane (in instruction-round n the E lane runs round n, the A lane n-1):
-//   S = rotr(x0, r1) ^ rotr(x0, r2) ^ rotr(x0, r3)   A: Sigma0(a)      E: Sigma1(e)
-//   k = x0 ^ (x1 & mA) ^ ~mA                         A: a ^ b          E: ~e
-//   F = k ? x2 : x1                                  A: Maj(a, b, c)   E: Ch(e, f, g)
-//   P                                                A: e[n] - d[n-1]  E: d[n] + h + KW[n]
-//   x0' = S + F + P                                  A: a[n]           E: e[n+1]
-// The A lane's T1 = e[n] - d[n-1] is the E lane's result of the previous
-// instruction-round and the E lane's d[n] = a[n-3] is three rounds old, so both
-// cross-lane reads (DPP) are off the recurrence, which is three VALU ops deep
-// (rotate, xor3, add3).  Ten ops a round: 7 VOP3, 1 VOP2, 2 DPP
-// (tools/micro/sha2lane.hip prices the variants; the un-skewed form with the
-// combine DPP on the chain measured 56 cycles a round, one lane 63).
+// run ONE instruction stream with per-lane operands, the A lane two rounds behind
+// the E lane (in instruction-round n the E lane runs round n, the A lane n-2):
+//   S = rotr(x0, r1) ^ rotr(x0, r2) ^ rotr(x0, r3)   A: Sigma0(a)        E: Sigma1(e)
+//   k = x0 ^ (x1 & mA) ^ ~mA                         A: a ^ b            E: ~e
+//   F = k ? x2 : x1                                  A: Maj(a, b, c)     E: Ch(e, f, g)
+//   z = (x3 ^ mA) + W                                A: -d  (W = 1)      E: h + KW[n]
+//   P = partner's x1 + z                             A: e[n-1] - d       E: a[n-3] + h + KW[n]
+//   x0' = S + F + P                                  A: a[n-1]           E: e[n+1]
+// With the two-round skew the A lane's T1 (= e[n-1] - d) and the E lane's d
+// (= a[n-3]) both sit in the partner's x1, so ONE unmasked DPP add (row_mirror)
+// serves both lanes, and it reads a register written two rounds earlier: the
+// recurrence is three VALU ops deep (rotate, xor3, add3) and a round is nine ops
+// (7 VOP3, 1 DPP, 1 xad).  tools/micro/sha2lane.hip prices the variants.
 //
-// Lane layout (DPP rows of 16 lanes, banks of 4): stream s of the wave's 32 has its
-// A lane in bank 0 or 2 and its E lane four lanes up (bank 1 or 3), so row_shl:4
-// reads the E partner and row_shr:4 the A partner; bank_mask confines each DPP
-// write to one side.
+// Lane layout: in each DPP row of 16 lanes, stream s's A lane is lane s and its E
+// lane lane 15 - s (row_mirror pairs them); 8 streams a row, 32 a wave.  W comes
+// from the LDS ring like KW: the E lanes' columns hold KW, the A lanes' columns
+// are filled with 1 once at kernel start and never written again.
+__device__ __forceinline__ bool two_lane_is_e(uint32_t lane) { return (lane >> 3) & 1; }
 __device__ __forceinline__ uint32_t two_lane_stream(uint32_t lane) {
-    return (lane >> 4) * 8 + ((lane >> 3) & 1) * 4 + (lane & 3);
+    return (lane >> 4) * 8 + (two_lane_is_e(lane) ? 7 - (lane & 7) : (lane & 7));
 }
-__device__ __forceinline__ bool two_lane_is_e(uint32_t lane) { return (lane >> 2) & 1; }
 
-// One instruction-round; the new x0 overwrites x3 (dead once P is formed) -- or
-// NX for the block's last instruction-round, whose E half is discarded.
-#define KRK_SHA2_ROUND(X0, X1, X2, X3, NX, KW)                                          \
-    "v_add_u32_e32 %[y], %[" #X3 "], %[" #KW "]\n\t"                                   \
-    "v_add_u32_dpp %[p], %[" #X2 "], %[y] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"     \
+// One instruction-round; the new x0 overwrites x3 (dead once P is formed) or NX.
+// z for the NEXT round is formed here (its x3 is this round's x2) so that no DPP
+// reads a result of the instruction right before it (that costs ~8 cycles; see
+// tools/micro/sha2lane.hip: 38 cycles a round this way, 47 with z formed in-round).
+#define KRK_SHA2_ROUND(X0, X1, X2, NX, WN)                                              \
+    "v_add_u32_dpp %[p], %[" #X1 "], %[z] row_mirror row_mask:0xf bank_mask:0xf\n\t"    \
     "v_alignbit_b32 %[t1], %[" #X0 "], %[" #X0 "], %[r1]\n\t"                          \
     "v_alignbit_b32 %[t2], %[" #X0 "], %[" #X0 "], %[r2]\n\t"                          \
     "v_alignbit_b32 %[t3], %[" #X0 "], %[" #X0 "], %[r3]\n\t"                          \
-    "v_sub_u32_dpp %[p], %[" #X0 "], %[" #X3 "] row_shl:4 row_mask:0xf bank_mask:0x5\n\t" \
     "v_bitop3_b32 %[k], %[" #X0 "], %[" #X1 "], %[ma] bitop3:0x2d\n\t"                 \
     "v_bitop3_b32 %[t1], %[t1], %[t2], %[t3] bitop3:0x96\n\t"                          \
     "v_bitop3_b32 %[k], %[k], %[" #X2 "], %[" #X1 "] bitop3:0xca\n\t"                  \
+    "v_xad_u32 %[z], %[" #X2 "], %[ma], %[" #WN "]\n\t"                                \
     "v_add3_u32 %[" #NX "], %[t1], %[k], %[p]\n\t"
 
 struct TwoLaneConst {
-    uint32_t r1, r2, r3, ma;
+    uint32_t r1, r2, r3, ma, one_a;
 };
 
 #define KRK_SHA2_OPERANDS                                                                             \
-    : [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [k] "=&v"(k), [y] "=&v"(y), [p] "=&v"(p),        \
+    : [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [k] "=&v"(k), [p] "=&v"(p), [z] "+v"(z),        \
       [R0] "+v"(R0), [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
+#define KRK_SHA2_CONSTS [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma)
 
-// Instruction-rounds 4q..4q+3 (KW[4q..4q+3] for the E lanes).  History registers
-// rotate: in instruction-round n, x0 = R[n%4], x3 = R[(n+1)%4].
-__device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3,
-                                          const TwoLaneConst& c, const u32x4& kw) {
-    uint32_t t1, t2, t3, k, y, p;
-    asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, R1, w0)
-                 KRK_SHA2_ROUND(R1, R0, R3, R2, R2, w1)
-                 KRK_SHA2_ROUND(R2, R1, R0, R3, R3, w2)
-                 KRK_SHA2_ROUND(R3, R2, R1, R0, R0, w3)
+// Instruction-rounds 4q..4q+3; W of rounds 4q+1..4q+4 (for the z's).  History
+// registers rotate: in instruction-round n, x0 = R[n%4], x3 = R[(n+1)%4].
+__device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                          const TwoLaneConst& c, uint32_t w1, uint32_t w2, uint32_t w3,
+                                          uint32_t w4) {
+    uint32_t t1, t2, t3, k, p;
+    asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
+                 KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                 KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                 KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
                  KRK_SHA2_OPERANDS
-                 : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w0] "v"(kw[0]),
-                   [w1] "v"(kw[1]), [w2] "v"(kw[2]), [w3] "v"(kw[3]));
+                 : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
 }
 
-// The 64 rounds of one block on a lane pair: 65 instruction-rounds (the A lane
-// idles in the first, the E lane in the last).  h[] = this lane's half of the
-// state (A: H0..H3, E: H4..H7), fed forward at the end.  Quads 0 and 1 of the
-// block's KW arrive already loaded, the rest are read two quads ahead.
-__device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int slot, uint32_t lane,
-                                        const TwoLaneConst& c, bool is_e, const u32x4& k0, const u32x4& k1) {
-    // Instruction-round 0: E runs round 0 on (e, f, g, h); A "runs round -1" on
-    // (b, c, d) and its result is replaced by a.
-    uint32_t R0 = is_e ? h[0] : h[1], R3 = is_e ? h[1] : h[2], R2 = is_e ? h[2] : h[3], R1 = h[3];
+// The 64 rounds of one block on a lane pair: 66 instruction-rounds (the A lane
+// idles in the first two, the E lane in the last two).  h[] = this lane's half of
+// the state (A: H0..H3, E: H4..H7), fed forward at the end.  W is read from LDS
+// slot cslot (the E lanes: the block's ring slot; the A lanes: the all-1 slot);
+// quads 0 and 1 arrive already loaded, the rest are read two quads ahead, and
+// quads 0 and 1 of the next block (slot ncslot) during the last quads, into k0/k1.
+__device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int cslot, int ncslot,
+                                        uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4& k0, u32x4& k1) {
+    // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
+    // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
+    // its own starts, so A starts at (H2, H3) and its two results are replaced by
+    // H1 and H0.
+    uint32_t R0 = is_e ? h[0] : h[2], R3 = is_e ? h[1] : h[3], R2 = h[2], R1 = h[3], z;
+    u32x4 cur = k1, nkw = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, 2, lane)), nnkw = nkw;
     {
-        uint32_t t1, t2, t3, k, y, p;
-        asm volatile("s_nop 1\n\t" KRK_SHA2_ROUND(R0, R3, R2, R1, R1, w0)
+        uint32_t t1, t2, t3, k, p;
+        // s_nop 0 + the xad: two wait states before the DPP read of R3.
+        asm volatile("s_nop 0\n\t"
+                     "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
+                     KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
                      KRK_SHA2_OPERANDS
-                     : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w0] "v"(k0[0]));
+                     : KRK_SHA2_CONSTS, [w0] "v"(k0[0]), [w1] "v"(k0[1]));
     }
-    R1 = is_e ? R1 : h[0];
+    R1 = is_e ? R1 : h[1];
     {
-        uint32_t t1, t2, t3, k, y, p;
-        // s_nop 1: the DPP reads of R1 in the next two rounds follow its VALU write.
-        asm volatile("s_nop 1\n\t" KRK_SHA2_ROUND(R1, R0, R3, R2, R2, w1)
-                     KRK_SHA2_ROUND(R2, R1, R0, R3, R3, w2)
-                     KRK_SHA2_ROUND(R3, R2, R1, R0, R0, w3)
+        uint32_t t1, t2, t3, k, p;
+        asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
                      KRK_SHA2_OPERANDS
-                     : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w1] "v"(k0[1]),
-                       [w2] "v"(k0[2]), [w3] "v"(k0[3]));
+                     : KRK_SHA2_CONSTS, [w2] "v"(k0[2]));
     }
-    u32x4 nkw = k1, nnkw = k1;
+    R2 = is_e ? R2 : h[0];
+    {
+        uint32_t t1, t2, t3, k, p;
+        asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w3] "v"(k0[3]), [w4] "v"(k1[0]));
+    }
 #pragma unroll
     for (int q = 1; q < 16; ++q) {
-        if (q + 1 < 16) nnkw = *reinterpret_cast<const u32x4*>(lds + kw_index(slot, q + 1, lane));
-        sha2_quad(R0, R1, R2, R3, c, nkw);
+        // quad q+1's first W feeds this quad's last z, so reads run two quads ahead
+        if (q + 2 < 16) nnkw = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, q + 2, lane));
+        // The next block's first two quads, read unconditionally (a slot is always
+        // mapped LDS; past the last block the values go unused) so that no branch
+        // sinks them to the end of the block, where their latency would be exposed.
+        if (q == 14) k0 = *reinterpret_cast<const u32x4*>(lds + kw_index(ncslot, 0, lane));
+        if (q == 15) k1 = *reinterpret_cast<const u32x4*>(lds + kw_index(ncslot, 1, lane));
+        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? nkw[0] : c.one_a);
+        cur = nkw;
         nkw = nnkw;
     }
-    // Instruction-round 64: A runs round 63 into T; E's state is already final.
-    uint32_t T;
+    // Instruction-rounds 64, 65: A runs rounds 62, 63 into T1, T2 (W = 1 on A lanes);
+    // the E lanes' registers keep their final state.
+    uint32_t T1, T2;
     {
-        uint32_t t1, t2, t3, k, y, p;
-        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, T, w0)
-                     KRK_SHA2_OPERANDS, [T] "=&v"(T)
-                     : [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma), [w0] "v"(0u));
+        uint32_t t1, t2, t3, k, p;
+        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
+                     KRK_SHA2_ROUND(T1, R0, R3, T2, w)
+                     KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
+                     : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
     }
-    h[0] += is_e ? R0 : T;
-    h[1] += is_e ? R3 : R0;
-    h[2] += is_e ? R2 : R3;
-    h[3] += is_e ? R1 : R2;
+    h[0] += is_e ? R0 : T2;
+    h[1] += is_e ? R3 : T1;
+    h[2] += is_e ? R2 : R0;
+    h[3] += is_e ? R1 : R3;
 }
 #undef KRK_SHA2_OPERANDS
+#undef KRK_SHA2_CONSTS
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
@@ -474,11 +520,21 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // kTwo: two lanes per stream (32 streams per workgroup, rounds2); the producer
 // is unchanged -- both lanes of a stream build the same schedule into their own
 // LDS column.
-template <bool kTiming, bool kTwo>
+// kTiming 2 (diagnostic variants 5/6, wrong digests): the consumer exits at once and
+// the producer runs alone (its barriers then count only itself) -- the producer's
+// time per block.
+//
+// kTwo: the producer's A and E lanes of a stream build two different blocks per
+// step (even and odd), so the producer's 64 lanes all do distinct work: built one
+// block a step, it (47.6 MB/s a stream) could not keep up with the two-lane
+// consumer (50 MB/s a stream).
+template <int kTiming, bool kTwo>
 __global__ void __launch_bounds__(128)
 sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __restrict__ out_digest,
                  uint32_t* __restrict__ out_state) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ring[];
+    constexpr int kNs = kTwo ? kSlots2 : kSlots;
+    constexpr int kStep = kTwo ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = threadIdx.x < 64;
     const uint32_t j = kTwo ? blockIdx.x * 32 + two_lane_stream(lane) : blockIdx.x * 64 + lane;
@@ -492,26 +548,40 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off, 64));
     nb = __builtin_amdgcn_readfirstlane(nb);
 
-    if (producer && kTiming) return;
+    if (producer && kTiming == 1) return;
+    if (!producer && kTiming >= 2) return;
     if (producer) {
-        // Blocks are built kDepth ahead of the consumer; their loads are issued two
-        // blocks before that, into a 3-deep register rotation (R0, R1, R2).
+        // Two lanes per stream: the A lanes read W from the extra slot kNs, all 1s
+        // (rounds2).
+        if (kTwo) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                *reinterpret_cast<u32x4*>(ring + kw_index(kNs, q, lane)) = u32x4{1u, 1u, 1u, 1u};
+        }
+        // Loads are issued two steps ahead into a 3-deep register rotation (R0, R1, R2).
         u32x4 R0[kRaw], R1[kRaw], R2[kRaw];
         const uint64_t safe = reinterpret_cast<uint64_t>(jobs);
-        fetch(job, 0, R0, safe);
-        fetch(job, 1, R1, safe);
-        for (uint32_t b = 0; b < nb; b += 3) {
-            produce_step(job, b, nb, lane, ring, R0, R2, safe);
-            produce_step(job, b + 1, nb, lane, ring, R1, R0, safe);
-            produce_step(job, b + 2, nb, lane, ring, R2, R1, safe);
+        const uint32_t par = kTwo && two_lane_is_e(lane) ? 1u : 0u;  // E lanes: odd blocks
+        const uint32_t col = kTwo && !par ? (lane ^ 15u) : lane;      // the E lane's column
+        uint32_t passed = 0;
+        fetch(job, par, R0, safe);
+        fetch(job, par + kStep, R1, safe);
+        for (uint32_t b = 0; b < nb; b += 3 * kStep) {
+            produce_step<kNs, kStep, kTiming == 3>(job, b, b + par, nb, col, ring, R0, R2, safe, passed);
+            produce_step<kNs, kStep, kTiming == 3>(job, b + kStep, b + kStep + par, nb, col, ring, R1, R0, safe,
+                                                   passed);
+            produce_step<kNs, kStep, kTiming == 3>(job, b + 2 * kStep, b + 2 * kStep + par, nb, col, ring, R2, R1,
+                                                   safe, passed);
         }
-        // The consumer passes nb barriers; the loop above took max(0, nb - kDepth).
-        const uint32_t tail = nb < (uint32_t)kDepth ? nb : (uint32_t)kDepth;
-        for (uint32_t i = 0; i < tail; ++i) __syncthreads();
+        // The consumer passes one barrier per step.
+        while (passed < (nb + kStep - 1) / kStep) {
+            __syncthreads();
+            ++passed;
+        }
     } else if (kTwo) {
         const bool is_e = two_lane_is_e(lane);
         const uint32_t half = is_e ? 4u : 0u;
-        const TwoLaneConst c{is_e ? 6u : 2u, is_e ? 11u : 13u, is_e ? 25u : 22u, is_e ? 0u : ~0u};
+        const TwoLaneConst c{is_e ? 6u : 2u, is_e ? 11u : 13u, is_e ? 25u : 22u, is_e ? 0u : ~0u, is_e ? 0u : 1u};
         uint32_t h[4];
         if (live && (job.flags & kShaFromState)) {
 #pragma unroll
@@ -522,26 +592,30 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         }
         __builtin_amdgcn_s_setprio(3);
         u32x4 k0{}, k1{};
+#ifdef KRK_SHA_CYCLES  // diagnostic build (make cycles): consumer cycles per block
+        const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
+#endif
         for (uint32_t i = 0; i < nb; ++i) {
-            if (!kTiming) __builtin_amdgcn_s_barrier();
+            if (kTiming == 0 && i % kStep == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (i == 0) {
-                k0 = kw_quad(ring, 0, 0, lane);
-                k1 = kw_quad(ring, 0, 1, lane);
+                k0 = kw_quad(ring, is_e ? 0 : kNs, 0, lane);
+                k1 = kw_quad(ring, is_e ? 0 : kNs, 1, lane);
             }
             uint32_t x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = h[k];
-            rounds2(x, ring, (int)(i % kSlots), lane, c, is_e, k0, k1);
-            if (i + 1 < nb) {
-                k0 = kw_quad(ring, (int)((i + 1) % kSlots), 0, lane);
-                k1 = kw_quad(ring, (int)((i + 1) % kSlots), 1, lane);
-            }
+            rounds2(x, ring, is_e ? (int)(i % kNs) : kNs, is_e ? (int)((i + 1) % kNs) : kNs, lane, c, is_e, k0, k1);
             if (i < mine) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) h[k] = x[k];
             }
         }
+#ifdef KRK_SHA_CYCLES
+        if (blockIdx.x == 0 && lane == 0 && nb)
+            printf("KRK_SHA_CYCLES timing=%d two=1 blocks=%u cycles/block=%.1f\n", kTiming, nb,
+                   (double)(__builtin_amdgcn_s_memtime() - cyc0) / nb);
+#endif
         if (live) {
             if (job.flags & kShaFinal) {
                 uint8_t* o = out_digest + 32 * (uint64_t)job.out + 4 * half;
@@ -577,7 +651,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             // Block i+1 is complete once this barrier has passed (the producer runs
             // kDepth-1 >= 1 blocks ahead of it), and its slot is not rewritten
             // before the barrier after next.
-            if (!kTiming) __builtin_amdgcn_s_barrier();
+            if (kTiming == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (i == 0) {
                 k0 = kw_quad(ring, 0, 0, lane);
@@ -619,7 +693,9 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
 
 // KRK_SHA_VARIANT: 0 = one lane does loads + schedule + rounds; 1 = wave-specialised,
 // one lane per stream; 2 = its rounds-only timing diagnostic (wrong digests);
-// 3 = wave-specialised, two lanes per stream; 4 = its timing diagnostic.
+// 3 = wave-specialised, two lanes per stream; 4 = its timing diagnostic;
+// 5/6 = producer-only timing diagnostics (one/two lanes); 7 = producer-only with
+// no global loads (two lanes).
 // Default (-1): two lanes while the batch leaves SIMDs idle, else one.
 // Read at every launch (a getenv is cheap next to any SHA launch), so tests can
 // cover each variant in one process.
@@ -650,13 +726,17 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
     if (!n_jobs) return hipSuccess;
     int v = sha_variant();
     if (v < 0) v = n_jobs <= two_lane_max_streams() ? 3 : 1;
-    if (v >= 1 && v <= 4) {
-        constexpr size_t lds = size_t(kSlots) * kSlotWords * 4;  // 64 KiB
-        const bool two = v >= 3;
-        auto* k = v == 1 ? &sha256_ws_kernel<false, false>
-                : v == 2 ? &sha256_ws_kernel<true, false>
-                : v == 3 ? &sha256_ws_kernel<false, true>
-                         : &sha256_ws_kernel<true, true>;
+    if (v >= 1 && v <= 7) {
+        // 1/3: production (one/two lanes); 2/4: consumer only; 5/6: producer only
+        const bool two = v == 3 || v == 4 || v >= 6;
+        const size_t lds = size_t(two ? kSlots2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB; 112 KiB (6 slots + all-1)
+        auto* k = v == 1 ? &sha256_ws_kernel<0, false>
+                : v == 2 ? &sha256_ws_kernel<1, false>
+                : v == 3 ? &sha256_ws_kernel<0, true>
+                : v == 4 ? &sha256_ws_kernel<1, true>
+                : v == 5 ? &sha256_ws_kernel<2, false>
+                : v == 6 ? &sha256_ws_kernel<2, true>
+                         : &sha256_ws_kernel<3, true>;
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         const uint32_t per = two ? 32u : 64u;

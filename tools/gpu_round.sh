@@ -37,9 +37,15 @@ for s in "$@"; do
             step pmc_sha_c 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $R/gpurun_out/pmc_sha_c -- python3 $R/tools/probe_perf.py --crc-gb 0 --sha 1024:8 ;;
     micro) step micro_banks 120 tools/micro/vgpr_banks ;;
     micro2) step micro_sha2lane 120 tools/micro/sha2lane ;;
+    hwid) step micro_hwid 120 tools/micro/hwid ;;
+    cyc) step sha_cycles 300 env KRK_LIB_PATH=kraken_amd/lib/cycles/libkraken_hip.so python tools/probe_perf.py --sha-variant 4 --crc-gb 0 --sha 64:8 &&
+         step sha_cycles_real 300 env KRK_LIB_PATH=kraken_amd/lib/cycles/libkraken_hip.so python tools/probe_perf.py --sha-variant 3 --crc-gb 0 --sha 64:8 ;;
     sha2) step probe_sha2 300 python tools/probe_perf.py --sha-variant 3 --crc-gb 0 --sha 64:8,1000:8,4096:4,16384:2 &&
           step probe_sha2t 300 python tools/probe_perf.py --sha-variant 4 --crc-gb 0 --sha 64:8,1000:8 &&
           step probe_sha1b 300 python tools/probe_perf.py --sha-variant 1 --crc-gb 0 --sha 4096:4,16384:2 ;;
+    shaP) step probe_shaP 300 python tools/probe_perf.py --sha-variant 6 --crc-gb 0 --sha 64:8,1000:8 &&
+          step probe_shaPn 300 python tools/probe_perf.py --sha-variant 7 --crc-gb 0 --sha 64:8,1000:8 &&
+          step probe_shaP1 300 python tools/probe_perf.py --sha-variant 5 --crc-gb 0 --sha 64:8,1000:8 ;;
     test1) step pytest_gpu_v1 900 env KRK_SHA_VARIANT=1 python -m pytest tests/test_gpu_digest_metainfo.py -x -q -p no:cacheprovider ;;
     shaD) step probe_sha_diag 300 python tools/probe_perf.py --sha-variant 2 --crc-gb 0 --sha 64:8,1024:8 ;;
     c2split) step probe_c2 300 python tools/probe_perf.py --c2 ;;

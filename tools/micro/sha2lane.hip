@@ -19,8 +19,12 @@ __global__ void dpp_semantics(unsigned* out) {
                  "v_add_u32_dpp %1, %2, %3 row_shr:4 row_mask:0xf bank_mask:0xa\n\ts_nop 1"
                  : "+v"(a), "+v"(b)
                  : "v"(lane), "v"(0u));
+    unsigned m = 3000u;
+    asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 row_mirror row_mask:0xf bank_mask:0xf\n\ts_nop 1"
+                 : "=&v"(m) : "v"(lane), "v"(0u));
     out[lane] = a;
     out[64 + lane] = b;
+    out[128 + lane] = m;
 }
 
 template <int K>
@@ -162,9 +166,48 @@ __global__ void rounds(unsigned long long* out, unsigned* sink) {
     "v_add3_u32 %[" #X3 "], %[t1], %[k], %[p]\n\t"
 #define Q6 R6(R0, R3, R2, R1) R6(R1, R0, R3, R2) R6(R2, R1, R0, R3) R6(R3, R2, R1, R0)
 
+// variant 7: skew-2 lanes, one unmasked row_mirror DPP per round (production)
+#define R7(X0, X1, X2, X3)                                                               \
+    "v_xad_u32 %[y], %[" #X3 "], %[ma], %[kw]\n\t"                                     \
+    "v_add_u32_dpp %[p], %[" #X1 "], %[y] row_mirror row_mask:0xf bank_mask:0xf\n\t"   \
+    "v_alignbit_b32 %[t1], %[" #X0 "], %[" #X0 "], %[r1]\n\t"                          \
+    "v_alignbit_b32 %[t2], %[" #X0 "], %[" #X0 "], %[r2]\n\t"                          \
+    "v_alignbit_b32 %[t3], %[" #X0 "], %[" #X0 "], %[r3]\n\t"                          \
+    "v_bitop3_b32 %[k], %[" #X0 "], %[" #X1 "], %[ma] bitop3:0x2d\n\t"                 \
+    "v_bitop3_b32 %[t1], %[t1], %[t2], %[t3] bitop3:0x96\n\t"                          \
+    "v_bitop3_b32 %[k], %[k], %[" #X2 "], %[" #X1 "] bitop3:0xca\n\t"                  \
+    "v_add3_u32 %[" #X3 "], %[t1], %[k], %[p]\n\t"
+#define Q7 R7(R0, R3, R2, R1) R7(R1, R0, R3, R2) R7(R2, R1, R0, R3) R7(R3, R2, R1, R0)
+
+// variant 8: skew-2, z for the next round formed at the end of this one (no xad -> DPP back-to-back)
+#define R8(X0, X1, X2, X3)                                                               \
+    "v_add_u32_dpp %[p], %[" #X1 "], %[y] row_mirror row_mask:0xf bank_mask:0xf\n\t"   \
+    "v_alignbit_b32 %[t1], %[" #X0 "], %[" #X0 "], %[r1]\n\t"                          \
+    "v_alignbit_b32 %[t2], %[" #X0 "], %[" #X0 "], %[r2]\n\t"                          \
+    "v_alignbit_b32 %[t3], %[" #X0 "], %[" #X0 "], %[r3]\n\t"                          \
+    "v_bitop3_b32 %[k], %[" #X0 "], %[" #X1 "], %[ma] bitop3:0x2d\n\t"                 \
+    "v_bitop3_b32 %[t1], %[t1], %[t2], %[t3] bitop3:0x96\n\t"                          \
+    "v_bitop3_b32 %[k], %[k], %[" #X2 "], %[" #X1 "] bitop3:0xca\n\t"                  \
+    "v_xad_u32 %[y], %[" #X2 "], %[ma], %[kw]\n\t"                                     \
+    "v_add3_u32 %[" #X3 "], %[t1], %[k], %[p]\n\t"
+#define Q8 R8(R0, R3, R2, R1) R8(R1, R0, R3, R2) R8(R2, R1, R0, R3) R8(R3, R2, R1, R0)
+// variant 9: as 7 with a VOP2 add in place of the xad (timing only: is it VOP3 -> DPP?)
+#define R9(X0, X1, X2, X3)                                                               \
+    "v_add_u32_e32 %[y], %[" #X3 "], %[kw]\n\t"                                         \
+    "v_add_u32_dpp %[p], %[" #X1 "], %[y] row_mirror row_mask:0xf bank_mask:0xf\n\t"   \
+    "v_alignbit_b32 %[t1], %[" #X0 "], %[" #X0 "], %[r1]\n\t"                          \
+    "v_alignbit_b32 %[t2], %[" #X0 "], %[" #X0 "], %[r2]\n\t"                          \
+    "v_alignbit_b32 %[t3], %[" #X0 "], %[" #X0 "], %[r3]\n\t"                          \
+    "v_bitop3_b32 %[k], %[" #X0 "], %[" #X1 "], %[ma] bitop3:0x2d\n\t"                 \
+    "v_bitop3_b32 %[t1], %[t1], %[t2], %[t3] bitop3:0x96\n\t"                          \
+    "v_bitop3_b32 %[k], %[k], %[" #X2 "], %[" #X1 "] bitop3:0xca\n\t"                  \
+    "v_add3_u32 %[" #X3 "], %[t1], %[k], %[p]\n\t"
+#define Q9 R9(R0, R3, R2, R1) R9(R1, R0, R3, R2) R9(R2, R1, R0, R3) R9(R3, R2, R1, R0)
+
 template <int K>
 __global__ void quads(unsigned long long* out, unsigned* sink) {
-    unsigned long long t0, t1;
+    unsigned long long t0, t1, rt0, rt1;
+    rt0 = __builtin_amdgcn_s_memrealtime();
     const unsigned l = threadIdx.x;
     unsigned R0 = l, R1 = 2 * l, R2v = 3 * l, R3 = 5 * l, C0 = 1, C1 = 1, C2 = 1, C3 = 1, p = 7, kw = 19;
     unsigned a, b, c, k;
@@ -181,29 +224,48 @@ __global__ void quads(unsigned long long* out, unsigned* sink) {
     if (K == 4) QUAD_ASM(Q4);
     if (K == 5) QUAD_ASM(Q5);
     unsigned y;
+#define QY(Q) asm volatile(REP16(Q)                                                                 \
+                     : [t1] "=&v"(a), [t2] "=&v"(b), [t3] "=&v"(c), [k] "=&v"(k), [y] "+v"(y), [R0] "+v"(R0), \
+                       [R1] "+v"(R1), [R2] "+v"(R2v), [R3] "+v"(R3), [p] "+v"(p)                               \
+                     : [r1] "v"(r1), [r2] "v"(r2), [r3] "v"(r3), [ma] "v"(ma), [kw] "v"(kw))
+    y = 3;
+    if (K == 8)
+        for (int it = 0; it < 256; ++it) QY(Q8);
+    if (K == 9) QY(Q9);
+    if (K == 7)
+        asm volatile(REP16(Q7)
+                     : [t1] "=&v"(a), [t2] "=&v"(b), [t3] "=&v"(c), [k] "=&v"(k), [y] "=&v"(y), [R0] "+v"(R0),
+                       [R1] "+v"(R1), [R2] "+v"(R2v), [R3] "+v"(R3), [p] "+v"(p)
+                     : [r1] "v"(r1), [r2] "v"(r2), [r3] "v"(r3), [ma] "v"(ma), [kw] "v"(kw));
     if (K == 6)
         asm volatile(REP16(Q6)
                      : [t1] "=&v"(a), [t2] "=&v"(b), [t3] "=&v"(c), [k] "=&v"(k), [y] "=&v"(y), [R0] "+v"(R0),
                        [R1] "+v"(R1), [R2] "+v"(R2v), [R3] "+v"(R3), [p] "+v"(p)
                      : [r1] "v"(r1), [r2] "v"(r2), [r3] "v"(r3), [ma] "v"(ma), [kw] "v"(kw));
     t1 = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) out[0] = t1 - t0;
+    rt1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = rt1 - rt0;
+    }
     sink[l] = R0 + R1 + R2v + R3 + C0 + C1 + C2 + C3 + p;
 }
 
 int main() {
     unsigned long long* d;
     unsigned *sink, *sem;
-    hipMalloc(&d, 8);
+    hipMalloc(&d, 16);
     hipMalloc(&sink, 256 * 4);
-    hipMalloc(&sem, 128 * 4);
+    hipMalloc(&sem, 192 * 4);
     hipLaunchKernelGGL(dpp_semantics, 1, 64, 0, 0, sem);
-    unsigned hs[128];
+    unsigned hs[192];
     hipMemcpy(hs, sem, sizeof hs, hipMemcpyDeviceToHost);
     printf("row_shl:4 bank_mask:0x5 (lane: value)  ");
     for (int i = 0; i < 32; ++i) printf("%d:%u ", i, hs[i]);
     printf("\nrow_shr:4 bank_mask:0xa (lane: value)  ");
     for (int i = 0; i < 32; ++i) printf("%d:%u ", i, hs[64 + i]);
+    printf("\nrow_mirror (lane: value)  ");
+    for (int i = 0; i < 32; ++i) printf("%d:%u ", i, hs[128 + i]);
     printf("\n");
     for (int rep = 0; rep < 2; ++rep) {
         const char* names[] = {"v_add_u32_dpp", "v_xad_u32", "v_add3_u32"};
@@ -222,15 +284,22 @@ int main() {
             hipMemcpy(&c, d, 8, hipMemcpyDeviceToHost);
             if (rep) printf("%-24s %.2f cycles/round\n", k ? "two-lane round (10 ops)" : "one-lane round (14 ops)", c / 64.0);
         }
-        for (int k = 2; k < 7; ++k) {
+        for (int k = 2; k < 10; ++k) {
             if (k == 2) hipLaunchKernelGGL(quads<2>, 1, 64, 0, 0, d, sink);
             if (k == 3) hipLaunchKernelGGL(quads<3>, 1, 64, 0, 0, d, sink);
             if (k == 4) hipLaunchKernelGGL(quads<4>, 1, 64, 0, 0, d, sink);
             if (k == 5) hipLaunchKernelGGL(quads<5>, 1, 64, 0, 0, d, sink);
             if (k == 6) hipLaunchKernelGGL(quads<6>, 1, 64, 0, 0, d, sink);
+            if (k == 7) hipLaunchKernelGGL(quads<7>, 1, 64, 0, 0, d, sink);
+            if (k == 8) hipLaunchKernelGGL(quads<8>, 1, 64, 0, 0, d, sink);
+            if (k == 9) hipLaunchKernelGGL(quads<9>, 1, 64, 0, 0, d, sink);
             unsigned long long c = 0;
             hipMemcpy(&c, d, 8, hipMemcpyDeviceToHost);
-            const char* nm[] = {"", "", "dep quads, production", "dep quads, xad after DPP", "dep quads, nop after DPP", "dep quads, plain V add", "dep quads, skewed lanes"};
+            unsigned long long rt = 0;
+            hipMemcpy(&rt, d + 1, 8, hipMemcpyDeviceToHost);
+            if (k == 8) c /= 256;
+            if (rep && k == 8) printf("clock during quads<8>: %.3f GHz (s_memtime %llu cycles / s_memrealtime %llu x 10 ns)\n", c * 256 / (rt * 10.0), c * 256, rt);
+            const char* nm[] = {"", "", "dep quads, production", "dep quads, xad after DPP", "dep quads, nop after DPP", "dep quads, plain V add", "dep quads, skewed lanes", "dep quads, skew-2 mirror", "skew-2, z a round early", "skew-2, VOP2 z (timing)"};
             if (rep) printf("%-28s %.2f cycles/round\n", nm[k], c / 64.0);
         }
     }
