@@ -421,7 +421,7 @@ struct TwoLaneConst {
 };
 
 #define KRK_SHA2_OPERANDS                                                                             \
-    : [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [k] "=&v"(k), [p] "=&v"(p), [z] "+v"(z),        \
+    : [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [k] "=&v"(kk), [p] "=&v"(p), [z] "+v"(z),       \
       [R0] "+v"(R0), [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
 #define KRK_SHA2_CONSTS [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma)
 
@@ -430,7 +430,7 @@ struct TwoLaneConst {
 __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
                                           const TwoLaneConst& c, uint32_t w1, uint32_t w2, uint32_t w3,
                                           uint32_t w4) {
-    uint32_t t1, t2, t3, k, p;
+    uint32_t t1, t2, t3, kk, p;
     asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
                  KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
                  KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
@@ -442,59 +442,72 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 // The 64 rounds of one block on a lane pair: 66 instruction-rounds (the A lane
 // idles in the first two, the E lane in the last two).  h[] = this lane's half of
 // the state (A: H0..H3, E: H4..H7), fed forward at the end.  W is read from LDS
-// slot cslot (the E lanes: the block's ring slot; the A lanes: the all-1 slot);
-// quads 0 and 1 arrive already loaded, the rest are read two quads ahead, and
-// quads 0 and 1 of the next block (slot ncslot) during the last quads, into k0/k1.
+// slot cslot (the E lanes: the block's ring slot; the A lanes: the all-1 slot).
+// Quads 0..2 arrive already loaded in k[]; the rest are read three quads ahead
+// (quad q+1's first W feeds quad q's last z, so a read issued one quad before its
+// use would stall: ~230 cycles a block), and quads 0..2 of the next block (slot
+// ncslot) are read into k[] during the last quads.
 __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int cslot, int ncslot,
-                                        uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4& k0, u32x4& k1) {
+                                        uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[3]) {
     // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
     // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
     // its own starts, so A starts at (H2, H3) and its two results are replaced by
     // H1 and H0.
     uint32_t R0 = is_e ? h[0] : h[2], R3 = is_e ? h[1] : h[3], R2 = h[2], R1 = h[3], z;
-    u32x4 cur = k1, nkw = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, 2, lane)), nnkw = nkw;
+    // W ring: quad q lives in wq[q % 4]
+    u32x4 wq[4];
+    wq[1] = k[1];
+    wq[2] = k[2];
+#ifdef KRK_SHA_NOLDS  // diagnostic: W from registers (wrong digests) -- prices the LDS reads
+    wq[3] = u32x4{3u, lane, (uint32_t)cslot, 7u};
+#else
+    wq[3] = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, 3, lane));
+#endif
     {
-        uint32_t t1, t2, t3, k, p;
+        uint32_t t1, t2, t3, kk, p;
         // s_nop 0 + the xad: two wait states before the DPP read of R3.
         asm volatile("s_nop 0\n\t"
                      "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
                      KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
                      KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w0] "v"(k0[0]), [w1] "v"(k0[1]));
+                     : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
     }
     R1 = is_e ? R1 : h[1];
     {
-        uint32_t t1, t2, t3, k, p;
+        uint32_t t1, t2, t3, kk, p;
         asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
                      KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w2] "v"(k0[2]));
+                     : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
     }
     R2 = is_e ? R2 : h[0];
     {
-        uint32_t t1, t2, t3, k, p;
+        uint32_t t1, t2, t3, kk, p;
         asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
                      KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
                      KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w3] "v"(k0[3]), [w4] "v"(k1[0]));
+                     : KRK_SHA2_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
     }
 #pragma unroll
     for (int q = 1; q < 16; ++q) {
-        // quad q+1's first W feeds this quad's last z, so reads run two quads ahead
-        if (q + 2 < 16) nnkw = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, q + 2, lane));
-        // The next block's first two quads, read unconditionally (a slot is always
+        if (q + 3 < 16) {
+#ifdef KRK_SHA_NOLDS
+            wq[(q + 3) & 3] = u32x4{(uint32_t)q, lane, (uint32_t)cslot, 7u};
+#else
+            wq[(q + 3) & 3] = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, q + 3, lane));
+#endif
+        }
+        // The next block's first three quads, read unconditionally (a slot is always
         // mapped LDS; past the last block the values go unused) so that no branch
         // sinks them to the end of the block, where their latency would be exposed.
-        if (q == 14) k0 = *reinterpret_cast<const u32x4*>(lds + kw_index(ncslot, 0, lane));
-        if (q == 15) k1 = *reinterpret_cast<const u32x4*>(lds + kw_index(ncslot, 1, lane));
-        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? nkw[0] : c.one_a);
-        cur = nkw;
-        nkw = nnkw;
+        if (q >= 13) k[q - 13] = *reinterpret_cast<const u32x4*>(lds + kw_index(ncslot, q - 13, lane));
+        const u32x4& cur = wq[q & 3];
+        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) & 3][0] : c.one_a);
     }
     // Instruction-rounds 64, 65: A runs rounds 62, 63 into T1, T2 (W = 1 on A lanes);
     // the E lanes' registers keep their final state.
     uint32_t T1, T2;
     {
-        uint32_t t1, t2, t3, k, p;
+        uint32_t t1, t2, t3, kk, p;
         asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
                      KRK_SHA2_ROUND(T1, R0, R3, T2, w)
                      KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
@@ -591,21 +604,35 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             for (int k = 0; k < 4; ++k) h[k] = is_e ? job.h[4 + k] : job.h[k];  // no dynamic index: keeps job out of scratch
         }
         __builtin_amdgcn_s_setprio(3);
-        u32x4 k0{}, k1{};
+        u32x4 kq[3] = {};
 #ifdef KRK_SHA_CYCLES  // diagnostic build (make cycles): consumer cycles per block
         const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef KRK_SHA_CYCLES
+        uint64_t cyc_bar = 0, cyc_rounds = 0;
+#endif
         for (uint32_t i = 0; i < nb; ++i) {
+#ifdef KRK_SHA_CYCLES
+            const uint64_t cb0 = __builtin_amdgcn_s_memtime();
+#endif
             if (kTiming == 0 && i % kStep == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (i == 0) {
-                k0 = kw_quad(ring, is_e ? 0 : kNs, 0, lane);
-                k1 = kw_quad(ring, is_e ? 0 : kNs, 1, lane);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) kq[q] = kw_quad(ring, is_e ? 0 : kNs, q, lane);
             }
             uint32_t x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = h[k];
-            rounds2(x, ring, is_e ? (int)(i % kNs) : kNs, is_e ? (int)((i + 1) % kNs) : kNs, lane, c, is_e, k0, k1);
+#ifdef KRK_SHA_CYCLES
+            const uint64_t cb1 = __builtin_amdgcn_s_memtime();
+#endif
+            rounds2(x, ring, is_e ? (int)(i % kNs) : kNs, is_e ? (int)((i + 1) % kNs) : kNs, lane, c, is_e, kq);
+#ifdef KRK_SHA_CYCLES
+            const uint64_t cb2 = __builtin_amdgcn_s_memtime();
+            cyc_bar += cb1 - cb0;
+            cyc_rounds += cb2 - cb1;
+#endif
             if (i < mine) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) h[k] = x[k];
@@ -613,8 +640,9 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         }
 #ifdef KRK_SHA_CYCLES
         if (blockIdx.x == 0 && lane == 0 && nb)
-            printf("KRK_SHA_CYCLES timing=%d two=1 blocks=%u cycles/block=%.1f\n", kTiming, nb,
-                   (double)(__builtin_amdgcn_s_memtime() - cyc0) / nb);
+            printf("KRK_SHA_CYCLES timing=%d two=1 blocks=%u cycles/block=%.1f barrier+setup=%.1f rounds2=%.1f\n",
+                   kTiming, nb, (double)(__builtin_amdgcn_s_memtime() - cyc0) / nb, (double)cyc_bar / nb,
+                   (double)cyc_rounds / nb);
 #endif
         if (live) {
             if (job.flags & kShaFinal) {

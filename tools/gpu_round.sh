@@ -38,6 +38,8 @@ for s in "$@"; do
     micro) step micro_banks 120 tools/micro/vgpr_banks ;;
     micro2) step micro_sha2lane 120 tools/micro/sha2lane ;;
     hwid) step micro_hwid 120 tools/micro/hwid ;;
+    vop) step micro_vopcost 120 tools/micro/vopcost ;;
+    regrot) step micro_regrot 120 tools/micro/regrot ;;
     cyc) step sha_cycles 300 env KRK_LIB_PATH=kraken_amd/lib/cycles/libkraken_hip.so python tools/probe_perf.py --sha-variant 4 --crc-gb 0 --sha 64:8 &&
          step sha_cycles_real 300 env KRK_LIB_PATH=kraken_amd/lib/cycles/libkraken_hip.so python tools/probe_perf.py --sha-variant 3 --crc-gb 0 --sha 64:8 ;;
     sha2) step probe_sha2 300 python tools/probe_perf.py --sha-variant 3 --crc-gb 0 --sha 64:8,1000:8,4096:4,16384:2 &&
