@@ -222,6 +222,12 @@ int krk_set_timing(int on);
 int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms);
 int krk_reset_kernel_stats(void);
 
+/* SHA-256 launch plan: lanes per stream (1 or 2) the library uses for a batch of
+ * n_streams streams on the current device (two lanes while the batch leaves SIMDs
+ * idle: fewer than one two-lane workgroup per CU).  Diagnostic; bench.py prices
+ * the per-stream issue ceiling of that plan. */
+int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,8 @@ static_assert(sizeof(ShaJob) == 64, "ShaJob layout");
 
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s);
+// Lanes per stream launch_sha256 uses for a batch of n_jobs streams (1 or 2).
+int sha_lanes_for(uint32_t n_jobs);
 
 // ---------------------------------------------------------------- HRW
 // Scores for (key, node) pairs and the per-key descending order.

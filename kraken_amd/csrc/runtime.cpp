@@ -1507,6 +1507,14 @@ int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms) {
     set_error(KRK_EINVAL, "unknown kernel '%s'", kernel);
     return KRK_EINVAL;
 }
+int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes) {
+    KRK_CHECK(lanes, KRK_EINVAL, "lanes is NULL");
+    KRK_CHECK(n_streams <= 0xffffffffull, KRK_ERANGE, "too many streams");
+    KRK_DEVICE(D);
+    (void)D;
+    *lanes = sha_lanes_for((uint32_t)n_streams);
+    return KRK_OK;
+}
 int krk_reset_kernel_stats(void) {
     drain_timing();
     std::lock_guard<std::mutex> g(g_tmu);

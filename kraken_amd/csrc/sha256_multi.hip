@@ -749,6 +749,12 @@ static uint32_t two_lane_max_streams() {
     return n;
 }
 
+int sha_lanes_for(uint32_t n_jobs) {
+    const int v = sha_variant();
+    if (v < 0) return n_jobs <= two_lane_max_streams() ? 2 : 1;
+    return (v == 3 || v == 4 || v >= 6) ? 2 : 1;
+}
+
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;

@@ -60,6 +60,13 @@ def synchronize():
     check(lib.krk_synchronize())
 
 
+def sha_lanes_per_stream(n_streams: int) -> int:
+    """Lanes per SHA-256 stream the library uses for a batch of n_streams (1 or 2)."""
+    v = C.c_int(0)
+    check(lib.krk_sha_lanes_per_stream(n_streams, C.byref(v)))
+    return v.value
+
+
 class BlobArena:
     """Blobs laid out back to back in one HBM allocation (each 256 B aligned)."""
 
