@@ -1,14 +1,24 @@
 // crc32_pieces.hip -- piece CRC-32/IEEE for gfx950 (core.calcPieceSums,
 // core/metainfo.go:158-179; PieceHash = crc32.NewIEEE, core/piece_hash.go:22-24).
 //
-// Layout of the work: one wave per CrcItem (<= 256 KiB inside one piece).  A wave
-// step covers 4 KiB: lane l owns the 64-byte segment [step*4096 + 64l, +64) and
-// loads it as 4 x 16-byte global loads (a wave step reads one contiguous 4 KiB).
-// Each lane runs slicing-by-4 over its own bytes; between two of its segments the
-// lane's virtual stream holds 4032 zero bytes, applied as one shift-by-4032 table
-// step (4 lookups per 64 bytes).  At the end every lane shifts its register to the
-// item end (one GF(2) multiply by a per-lane constant), the wave XOR-reduces, and
-// lane 0 shifts to the piece end and atomically XORs into sums[piece].
+// Work: one wave per work item, a run of <= 256 KiB inside one piece.  One launch
+// takes items from two sources (CrcWork): runs of whole pieces, expanded here on
+// the device (a whole piece's items and constants depend only on the piece
+// length), and explicit CrcItems built on the host (partial pieces, stream
+// windows, seeded crc32.Update calls).
+//
+// Two lane layouts (CrcLaunchCfg.variant):
+//  * strided (0, 1): a wave step covers 4 KiB; lane l owns the 64-byte segment
+//    [step*4096 + 64l, +64), loaded as 4 x 16 B; one CRC chain per lane, and the
+//    lane's virtual stream holds 4032 zero bytes between two of its segments.
+//  * coalesced (2, 3): each 1 KiB quarter k of a step is ONE fully coalesced wave
+//    load (lane l: bytes [1024k + 16l, +16)); lane l runs four independent chains,
+//    one per quarter (ILP 4 on the LDS lookups), 4080 zero bytes apart.
+// Each chain runs slicing-by-4 (1 LDS lookup per byte); a zero gap is one
+// 4-lookup shift-table step.  At the end every chain is shifted to the item end
+// (GF(2) multiply by a per-lane constant), the wave XOR-reduces, and lane 0 shifts
+// to the piece end and atomically XORs into sums[piece].  XOR is order-free, so
+// the items of one piece may run on any wave, XCD or launch.
 //
 // Tables live in LDS, replicated R times and interleaved (word (t*256+e)*R + r) so
 // lane l reads replica l % R: with R = 32 the 32 lanes of a ds_read_b32 half-wave
@@ -51,6 +61,22 @@ __device__ __forceinline__ uint32_t seg16(uint32_t c, const u32x4& v, const Tab<
     return c;
 }
 
+// Up to 4 little-endian words holding n valid bytes (n <= 16) into register c.
+template <int R, int NW>
+__device__ __forceinline__ uint32_t feed_words(uint32_t c, const uint32_t* w, uint32_t n, const Tab<R>& T) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        const int keep = (int)n - 4 * j;
+        if (keep >= 4) {
+            c = T.word(c ^ w[j]);
+        } else if (keep > 0) {
+            for (int b = 0; b < keep; ++b) c = T.byte(c, (w[j] >> (8 * b)) & 0xFF);
+        }
+    }
+    return c;
+}
+
+// ------------------------------------------------------------ strided layout
 // One wave step for this lane: skip the 4032-byte gap, then its 64 own bytes.
 template <int R, int RG>
 __device__ __forceinline__ uint32_t step64(uint32_t c, const u32x4& v0, const u32x4& v1, const u32x4& v2,
@@ -62,32 +88,166 @@ __device__ __forceinline__ uint32_t step64(uint32_t c, const u32x4& v0, const u3
     return seg16(c, v3, T);
 }
 
-// Bytes [p, p+n) into register c, n <= kSeg, any alignment (see load_bytes64).
-template <int R>
-__device__ __forceinline__ uint32_t seg_tail(uint32_t c, uint64_t p, uint32_t n, const Tab<R>& T) {
-    uint32_t w[16];
-    load_bytes64(p, n, w);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int keep = (int)n - 4 * j;
-        if (keep >= 4) {
-            c = T.word(c ^ w[j]);
-        } else if (keep > 0) {
-            for (int b = 0; b < keep; ++b) c = T.byte(c, (w[j] >> (8 * b)) & 0xFF);
+// This lane's share of bytes [base, base+len), shifted to the item end.
+template <int R, int RG>
+__device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const Tab<R>& T,
+                                                     const uint32_t* G, uint32_t lane_mul,
+                                                     const uint32_t* x8pow) {
+    uint32_t c = 0;
+    uint32_t end = 0;  // end offset (in item) of this lane's last processed byte + 1
+    const uint32_t nfull = len / kStep;
+    if ((base & 15) == 0) {
+        if (nfull > 0) {
+            // Two register sets in ping-pong: the next step's 4 x 16 B are in
+            // flight while the current step's lookups run.
+            gptr<u32x4> p = as_global<u32x4>(base + lane * kSeg);
+            constexpr uint32_t S = kStep / 16;
+            u32x4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            u32x4 b0, b1, b2, b3;
+            uint32_t s = 0;
+            for (; s + 2 <= nfull; s += 2) {
+                gptr<u32x4> q = p + (s + 1) * S;
+                b0 = q[0]; b1 = q[1]; b2 = q[2]; b3 = q[3];
+                c = step64<R, RG>(c, a0, a1, a2, a3, T, G);
+                if (s + 2 < nfull) {
+                    q = p + (s + 2) * S;
+                    a0 = q[0]; a1 = q[1]; a2 = q[2]; a3 = q[3];
+                }
+                c = step64<R, RG>(c, b0, b1, b2, b3, T, G);
+            }
+            if (s < nfull) c = step64<R, RG>(c, a0, a1, a2, a3, T, G);
+            end = (nfull - 1) * kStep + (lane + 1) * kSeg;
+        }
+        const uint32_t ts = nfull * kStep + lane * kSeg;
+        if (ts < len) {
+            const uint32_t nb = min(kSeg, len - ts);
+            uint32_t w[16];
+            load_bytes64(base + ts, nb, w);
+            c = feed_words<R, 16>(gap_shift<RG>(c, G), w, nb, T);
+            end = ts + nb;
+        }
+    } else {
+        // Unaligned run (odd piece lengths, caller-provided pointers): same lane
+        // structure, aligned-dword loads re-assembled in registers.
+        const uint32_t nsteps = (len + kStep - 1) / kStep;
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            const uint32_t ss = s * kStep + lane * kSeg;
+            if (ss < len) {
+                const uint32_t nb = min(kSeg, len - ss);
+                uint32_t w[16];
+                load_bytes64(base + ss, nb, w);
+                c = feed_words<R, 16>(gap_shift<RG>(c, G), w, nb, T);
+                end = ss + nb;
+            }
         }
     }
-    return c;
+    const uint32_t d = len - end;
+    uint32_t m = lane_mul;
+    if (d != (63 - lane) * kSeg) m = x8n(d, x8pow);
+    return end ? gf2_mulmod(c, m) : 0u;
 }
 
-template <int R, int RG, int BLOCK>
+// ---------------------------------------------------------- coalesced layout
+template <int R, int RG>
+__device__ __forceinline__ void step_coal(uint32_t c[4], const u32x4 v[4], const Tab<R>& T, const uint32_t* G) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = seg16(gap_shift<RG>(c[k], G), v[k], T);
+}
+
+template <int R, int RG>
+__device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, uint32_t lane, const Tab<R>& T,
+                                                  const uint32_t* G, const uint32_t lm[4], const uint32_t* x8pow) {
+    uint32_t c[4] = {0u, 0u, 0u, 0u};
+    uint32_t end[4] = {0u, 0u, 0u, 0u};
+    const uint32_t nfull = len / kStep;
+    uint32_t s0 = 0;  // first step left to the generic loop below
+    if ((base & 15) == 0 && nfull > 0) {
+        gptr<u32x4> p = as_global<u32x4>(base + lane * 16);
+        constexpr uint32_t S = kStep / 16;
+        u32x4 a[4], b[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = p[64 * k];
+        uint32_t s = 0;
+        for (; s + 2 <= nfull; s += 2) {
+            gptr<u32x4> q = p + (s + 1) * S;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[k] = q[64 * k];
+            step_coal<R, RG>(c, a, T, G);
+            if (s + 2 < nfull) {
+                q = p + (s + 2) * S;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a[k] = q[64 * k];
+            }
+            step_coal<R, RG>(c, b, T, G);
+        }
+        if (s < nfull) step_coal<R, RG>(c, a, T, G);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) end[k] = (nfull - 1) * kStep + 1024 * k + 16 * lane + 16;
+        s0 = nfull;
+    }
+    // The partial last step, or every step of an unaligned run.
+    const uint32_t nsteps = (len + kStep - 1) / kStep;
+    for (uint32_t s = s0; s < nsteps; ++s) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t ss = s * kStep + 1024 * k + 16 * lane;
+            if (ss < len) {
+                const uint32_t nb = min(16u, len - ss);
+                uint32_t w[4];
+                load_bytes16(base + ss, nb, w);
+                c[k] = feed_words<R, 4>(gap_shift<RG>(c[k], G), w, nb, T);
+                end[k] = ss + nb;
+            }
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (end[k]) {
+            const uint32_t d = len - end[k];
+            const uint32_t m = d == kGapC - 1024 * k - 16 * lane ? lm[k] : x8n(d, x8pow);
+            acc ^= gf2_mulmod(c[k], m);
+        }
+    }
+    return acc;
+}
+
+// --------------------------------------------------------------- item source
+struct ItemRef {
+    uint64_t ptr;
+    uint32_t len, out, mul, xr;
+};
+
+// Item `it` (wave-uniform) of the launch.
+__device__ __forceinline__ ItemRef fetch_item(const CrcWork& w, uint32_t it) {
+    if (it >= w.run_items) {
+        const CrcItem ci = w.items[it - w.run_items];
+        return {ci.ptr, ci.len, ci.out, ci.mul, ci.xr};
+    }
+    uint32_t lo = 0, hi = w.n_runs;  // last run with item_base <= it
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (w.runs[mid].item_base <= it) lo = mid;
+        else hi = mid;
+    }
+    const CrcRun r = w.runs[lo];
+    const uint32_t j = it - r.item_base;
+    const uint32_t pc = j / r.ipp, jj = j - pc * r.ipp;
+    const uint64_t q = uint64_t(jj) * kItemBytes;
+    const uint64_t nx = min(q + kItemBytes, r.plen);
+    return {r.ptr + uint64_t(pc) * r.plen + q, (uint32_t)(nx - q), r.out + pc, w.consts[r.cpat + jj],
+            jj == 0 ? w.consts[r.cpat + r.ipp] : 0u};
+}
+
+template <int R, int RG, int BLOCK, bool COAL>
 __global__ void __launch_bounds__(BLOCK)
-crc_items_kernel(const CrcItem* __restrict__ items, uint32_t n_items,
-                 const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
+crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr int TW = 1024 * R;
     constexpr int GW = 1024 * RG;
+    constexpr int GT = COAL ? kTabGC : kTabG;
     for (int i = threadIdx.x; i < TW; i += BLOCK) lds[i] = tabs[kTabT + i / R];
-    for (int i = threadIdx.x; i < GW; i += BLOCK) lds[TW + i] = tabs[kTabG + i / RG];
+    for (int i = threadIdx.x; i < GW; i += BLOCK) lds[TW + i] = tabs[GT + i / RG];
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63;
@@ -95,70 +255,20 @@ crc_items_kernel(const CrcItem* __restrict__ items, uint32_t n_items,
     T.lo = lds + (lane % R);
     T.hi = lds + 2 * 256 * R + (lane % R);
     const uint32_t* G = lds + TW + (lane % RG);
-    const uint32_t lane_mul = tabs[kTabLaneMul + lane];
     const uint32_t* x8pow = tabs + kTabX8Pow;
+    uint32_t lm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lm[k] = COAL ? tabs[kTabLaneMulC + 64 * k + lane] : tabs[kTabLaneMul + lane];
 
     constexpr uint32_t WPB = BLOCK / 64;
     const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + threadIdx.x / 64);
     const uint32_t n_waves = gridDim.x * WPB;
+    const uint32_t n_items = w.run_items + w.n_items;
 
     for (uint32_t it = wave0; it < n_items; it += n_waves) {
-        const CrcItem ci = items[it];
-        const uint64_t base = ci.ptr;
-        const uint32_t len = ci.len;
-        uint32_t c = 0;
-        uint32_t end = 0;  // end offset (in item) of this lane's last processed byte + 1
-        const uint32_t nfull = len / kStep;
-
-        if ((ci.ptr & 15) == 0) {
-            if (nfull > 0) {
-                // Two register sets in ping-pong: the next step's 4 x 16 B are in
-                // flight while the current step's lookups run.
-                gptr<u32x4> p = as_global<u32x4>(base + lane * kSeg);
-                constexpr uint32_t S = kStep / 16;
-                u32x4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-                u32x4 b0, b1, b2, b3;
-                uint32_t s = 0;
-                for (; s + 2 <= nfull; s += 2) {
-                    gptr<u32x4> q = p + (s + 1) * S;
-                    b0 = q[0]; b1 = q[1]; b2 = q[2]; b3 = q[3];
-                    c = step64<R, RG>(c, a0, a1, a2, a3, T, G);
-                    if (s + 2 < nfull) {
-                        q = p + (s + 2) * S;
-                        a0 = q[0]; a1 = q[1]; a2 = q[2]; a3 = q[3];
-                    }
-                    c = step64<R, RG>(c, b0, b1, b2, b3, T, G);
-                }
-                if (s < nfull) c = step64<R, RG>(c, a0, a1, a2, a3, T, G);
-                end = (nfull - 1) * kStep + (lane + 1) * kSeg;
-            }
-            const uint32_t ts = nfull * kStep + lane * kSeg;
-            if (ts < len) {
-                const uint32_t nb = min(kSeg, len - ts);
-                c = gap_shift<RG>(c, G);
-                c = seg_tail(c, base + ts, nb, T);
-                end = ts + nb;
-            }
-        } else {
-            // Unaligned run (odd piece lengths, caller-provided pointers): same lane
-            // structure, aligned-dword loads re-assembled in registers.
-            const uint32_t nsteps = (len + kStep - 1) / kStep;
-            for (uint32_t s = 0; s < nsteps; ++s) {
-                const uint32_t ss = s * kStep + lane * kSeg;
-                if (ss < len) {
-                    const uint32_t nb = min(kSeg, len - ss);
-                    c = gap_shift<RG>(c, G);
-                    c = seg_tail(c, base + ss, nb, T);
-                    end = ss + nb;
-                }
-            }
-        }
-
-        // Shift this lane's register to the item end.
-        const uint32_t d = len - end;
-        uint32_t m = lane_mul;
-        if (d != (63 - lane) * kSeg) m = x8n(d, x8pow);
-        c = end ? gf2_mulmod(c, m) : 0u;
+        const ItemRef ci = fetch_item(w, it);
+        uint32_t c = COAL ? lane_crc_coal<R, RG>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
+                          : lane_crc_strided<R, RG>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
         // Wave XOR-reduction.
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c ^= __shfl_xor(c, off, 64);
@@ -169,34 +279,40 @@ crc_items_kernel(const CrcItem* __restrict__ items, uint32_t n_items,
     }
 }
 
-template <int R, int RG, int BLOCK>
-static hipError_t launch_variant(const CrcItem* items, uint32_t n_items, const uint32_t* tabs,
-                                 uint32_t* sums, int cus, int blocks_per_cu, hipStream_t s) {
+template <int R, int RG, int BLOCK, bool COAL>
+static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
+                                 int blocks_per_cu, hipStream_t s) {
     constexpr size_t lds = size_t(1024) * (R + RG) * 4;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const uint32_t wpb = BLOCK / 64;
-    uint64_t want = (uint64_t(n_items) + wpb - 1) / wpb;
+    const uint64_t n_items = uint64_t(w.run_items) + w.n_items;
+    uint64_t want = (n_items + wpb - 1) / wpb;
     uint64_t cap = uint64_t(cus) * blocks_per_cu;
     uint32_t grid = (uint32_t)(want < cap ? want : cap);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK>), dim3(grid), dim3(BLOCK), lds, s, items,
-                       n_items, tabs, sums);
+    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
     return hipGetLastError();
 }
 
-hipError_t launch_crc_items(const CrcItem* items, uint32_t n_items, const uint32_t* tabs,
-                            uint32_t* sums, const CrcLaunchCfg& cfg, hipStream_t s) {
-    if (n_items == 0) return hipSuccess;
-    if (cfg.variant == 1)  // 144 KiB LDS: one 1024-thread block per CU
-        return launch_variant<32, 4, 1024>(items, n_items, tabs, sums, cfg.cus, 1, s);
-    // 80 KiB LDS: two 512-thread blocks per CU
-    return launch_variant<16, 4, 512>(items, n_items, tabs, sums, cfg.cus, 2, s);
+hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, const CrcLaunchCfg& cfg,
+                            hipStream_t s) {
+    if (uint64_t(w.run_items) + w.n_items == 0) return hipSuccess;
+    switch (cfg.variant) {
+        case 1:  // 144 KiB LDS: one 1024-thread block per CU
+            return launch_variant<32, 4, 1024, false>(w, tabs, sums, cfg.cus, 1, s);
+        case 2:  // coalesced, 80 KiB LDS: two 512-thread blocks per CU
+            return launch_variant<16, 4, 512, true>(w, tabs, sums, cfg.cus, 2, s);
+        case 3:  // coalesced, 144 KiB LDS: one 1024-thread block per CU
+            return launch_variant<32, 4, 1024, true>(w, tabs, sums, cfg.cus, 1, s);
+        default:  // strided, 80 KiB LDS: two 512-thread blocks per CU
+            return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
+    }
 }
 
 __global__ void crc_verify_kernel(const uint32_t* sums, const uint32_t* expected, uint8_t* ok,

@@ -61,4 +61,25 @@ __device__ __forceinline__ void load_bytes64(uint64_t a, uint32_t n, uint32_t ou
     }
 }
 
+// Bytes [a, a+n) (n <= 16, any alignment) as 4 little-endian words, zero padded;
+// the 16-byte form of load_bytes64 (at most 5 aligned dword loads).
+__device__ __forceinline__ void load_bytes16(uint64_t a, uint32_t n, uint32_t out[4], uint64_t lo = 0,
+                                             uint64_t hi = ~0ull) {
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    const uint32_t nd = n ? (uint32_t)(((a + n - 1) >> 2) - (a >> 2) + 1) : 0;  // <= 5
+    gptr<uint32_t> d = as_global<uint32_t>(a & ~uint64_t(3));
+    uint32_t raw[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        raw[k] = ((uint32_t)k < nd && KRK_GUARD((a & ~uint64_t(3)) + 4 * k, 4, lo, hi, 3)) ? d[k] : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t w = __builtin_amdgcn_alignbit(raw[j + 1], raw[j], sh);
+        const int keep = (int)n - 4 * j;
+        if (keep <= 0) w = 0;
+        else if (keep < 4) w &= (1u << (8 * keep)) - 1;
+        out[j] = w;
+    }
+}
+
 }  // namespace krk

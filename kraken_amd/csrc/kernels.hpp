@@ -31,15 +31,50 @@ constexpr int kTabT = 0;        // T0..T3 slicing tables, 1024 words
 constexpr int kTabG = 1024;     // G0..G3 shift-by-kGap tables, 1024 words
 constexpr int kTabLaneMul = 2048;  // 64 words: x^(8*(63-l)*kSeg)
 constexpr int kTabX8Pow = 2112;    // 64 words: x^(8*2^k)
-constexpr int kTabWords = 2176;
+// Coalesced layout (variants 2, 3): wave step = 4 KiB loaded as four fully coalesced
+// 1 KiB wave-instructions; lane l owns chain k = bytes [1024k + 16l, +16) of every
+// step, so a chain's segments are kGapC = 4080 zero bytes apart.
+constexpr uint32_t kGapC = kStep - 16;
+constexpr int kTabGC = 2176;       // G0..G3 shift-by-kGapC tables, 1024 words
+constexpr int kTabLaneMulC = 3200; // 256 words [k*64 + l]: x^(8*(kGapC - 1024k - 16l))
+constexpr int kTabWords = 3456;
+
+// A run of consecutive WHOLE pieces of one blob, expanded into work items on the
+// device: a whole piece's items and their constants depend only on the piece
+// length, so the host writes one run per blob range instead of one item per
+// 256 KiB (C4: 81,920 items -> 1 run).  consts[cpat + j] is item j's piece-end
+// shift, consts[cpat + ipp] the piece's init/xor-out term.
+struct alignas(16) CrcRun {
+    uint64_t ptr;        // device address of the run's first piece
+    uint64_t plen;       // piece length
+    uint32_t n_pieces;
+    uint32_t out;        // sums index of the first piece
+    uint32_t item_base;  // index of the run's first item in the launch
+    uint32_t ipp;        // items per piece = ceil(plen / kItemBytes)
+    uint32_t cpat;
+    uint32_t pad[3];
+};
+static_assert(sizeof(CrcRun) == 48, "CrcRun layout");
+
+// One CRC launch: items [0, run_items) come from the runs, [run_items,
+// run_items + n_items) from the explicit item array.
+struct CrcWork {
+    const CrcRun* runs;
+    const CrcItem* items;
+    const uint32_t* consts;
+    uint32_t n_runs;
+    uint32_t run_items;
+    uint32_t n_items;
+    uint32_t pad;
+};
 
 struct CrcLaunchCfg {
     int cus;           // compute units
-    int variant;       // 0 = R16 (2 blocks/CU), 1 = R32 (1 block/CU)
+    int variant;       // 0 = R16 (2 blocks/CU), 1 = R32 (1 block/CU); 2/3 = the same, coalesced 4-chain layout
 };
 
-hipError_t launch_crc_items(const CrcItem* items, uint32_t n_items, const uint32_t* tabs,
-                            uint32_t* sums, const CrcLaunchCfg& cfg, hipStream_t s);
+hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, const CrcLaunchCfg& cfg,
+                            hipStream_t s);
 
 // Piece verification: ok[i] = (sums[i] == expected[i]).
 hipError_t launch_crc_verify(const uint32_t* sums, const uint32_t* expected, uint8_t* ok,

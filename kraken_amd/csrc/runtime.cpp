@@ -210,6 +210,10 @@ static int init_device(Device& D, int id) {
     make_shift_tables(tabs.data() + kTabG, x8n(kGap, xp.v));
     for (int l = 0; l < 64; ++l) tabs[kTabLaneMul + l] = x8n(uint64_t(63 - l) * kSeg, xp.v);
     for (int k = 0; k < 64; ++k) tabs[kTabX8Pow + k] = xp.v[k];
+    make_shift_tables(tabs.data() + kTabGC, x8n(kGapC, xp.v));
+    for (int k = 0; k < 4; ++k)
+        for (int l = 0; l < 64; ++l)
+            tabs[kTabLaneMulC + k * 64 + l] = x8n(uint64_t(kGapC) - 1024 * k - 16 * l, xp.v);
     KRK_HIP(hipMalloc(&D.d_tabs, kTabWords * 4));
     KRK_HIP(hipMemcpy(D.d_tabs, tabs.data(), kTabWords * 4, hipMemcpyHostToDevice));
     const char* v = getenv("KRK_CRC_VARIANT");
@@ -282,15 +286,22 @@ static int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_
 }
 
 // ------------------------------------------------------------------ CRC items
+// The work of one CRC launch: runs of whole pieces (expanded into items on the
+// device) plus explicit items for partial pieces and seeded CRCs.
+struct CrcBatch {
+    std::vector<CrcRun> runs;
+    std::vector<CrcItem> items;
+    std::vector<uint32_t> consts;
+    std::unordered_map<uint64_t, uint32_t> pat;  // piece length -> consts index of its pattern
+    uint64_t run_items = 0;
+    bool empty() const { return runs.empty() && items.empty(); }
+};
+
 // Items for bytes [a, b) of one blob (length L, pieces of P bytes), where blob byte
 // `a` lives at device address `base`.  `seed` is the register the IEEE CRC starts
 // from (~crc of crc32.Update; ~0 for PieceHash()).
 struct ItemBuilder {
     std::unordered_map<uint64_t, uint32_t> cache;
-    struct Pattern {
-        std::vector<CrcItem> items;  // for one full piece starting at offset 0
-    };
-    std::unordered_map<uint64_t, Pattern> full;
 
     uint32_t X(uint64_t n) {
         if (n == 0) return kOne;
@@ -317,29 +328,54 @@ struct ItemBuilder {
         }
     }
 
-    void add(std::vector<CrcItem>& out, uint64_t base, uint64_t a, uint64_t b, uint64_t L, uint64_t P,
-             uint64_t sums_off, uint32_t seed = 0xFFFFFFFFu) {
+    // consts index of the whole-piece pattern for piece length P (item muls, then xr).
+    uint32_t pattern(CrcBatch& B, uint64_t P) {
+        auto it = B.pat.find(P);
+        if (it != B.pat.end()) return it->second;
+        const uint32_t at = (uint32_t)B.consts.size();
+        for (uint64_t q = 0; q < P; q += kItemBytes) B.consts.push_back(X(P - std::min(q + kItemBytes, P)));
+        B.consts.push_back(gf2_mulmod(0xFFFFFFFFu, X(P)) ^ 0xFFFFFFFFu);
+        B.pat.emplace(P, at);
+        return at;
+    }
+
+    // Whole pieces [f0, f1) of a blob whose piece f0 starts at device address ptr.
+    void run(CrcBatch& B, uint64_t ptr, uint64_t f0, uint64_t f1, uint64_t P, uint64_t sums_off) {
+        const uint64_t ipp = (P + kItemBytes - 1) / kItemBytes;
+        const uint32_t cpat = pattern(B, P);
+        for (uint64_t f = f0; f < f1;) {  // a run's item count stays below 2^31
+            const uint64_t n = std::min<uint64_t>(f1 - f, std::max<uint64_t>(1, (1ull << 31) / ipp));
+            CrcRun r{};
+            r.ptr = ptr + (f - f0) * P;
+            r.plen = P;
+            r.n_pieces = (uint32_t)n;
+            r.out = (uint32_t)(sums_off + f);
+            r.item_base = (uint32_t)B.run_items;
+            r.ipp = (uint32_t)ipp;
+            r.cpat = cpat;
+            B.runs.push_back(r);
+            B.run_items += n * ipp;
+            f += n;
+        }
+    }
+
+    void add(CrcBatch& B, uint64_t base, uint64_t a, uint64_t b, uint64_t L, uint64_t P, uint64_t sums_off,
+             uint32_t seed = 0xFFFFFFFFu) {
         if (a >= b) return;
-        for (uint64_t pi = a / P; pi * P < b; ++pi) {
+        const uint64_t pa = a / P, pb = (b - 1) / P;  // pieces touched, inclusive
+        // Whole pieces [f0, f1): inside [a, b), full length, unseeded -> one run.
+        uint64_t f0 = (a + P - 1) / P, f1 = std::min(b, L) / P;
+        if (seed != 0xFFFFFFFFu || f1 <= f0) f0 = f1 = pb + 1;
+        for (uint64_t pi = pa; pi <= pb; ++pi) {
+            if (pi == f0) {
+                run(B, base + f0 * P - a, f0, f1, P, sums_off);
+                pi = f1 - 1;
+                continue;
+            }
             const uint64_t ps = pi * P, pe = std::min(ps + P, L);
             const uint64_t s = std::max(a, ps), e = std::min(b, pe);
             const uint64_t ptr_ps = base + ps - a;  // may point before base; only offsets >= s used
-            if (s == ps && e == pe && pe - ps == P && seed == 0xFFFFFFFFu) {
-                auto it = full.find(P);
-                if (it == full.end()) {
-                    Pattern pat;
-                    piece(pat.items, 0, 0, P, 0, P, 0, seed);
-                    it = full.emplace(P, std::move(pat)).first;
-                }
-                for (const CrcItem& t : it->second.items) {
-                    CrcItem c = t;
-                    c.ptr += ptr_ps;
-                    c.out = (uint32_t)(sums_off + pi);
-                    out.push_back(c);
-                }
-            } else {
-                piece(out, ptr_ps, ps, pe, s, e, (uint32_t)(sums_off + pi), seed);
-            }
+            piece(B.items, ptr_ps, ps, pe, s, e, (uint32_t)(sums_off + pi), seed);
         }
     }
 };
@@ -370,17 +406,30 @@ static void sums_span(const krk_blob* blobs, uint64_t n, uint64_t* lo, uint64_t*
     if (*lo > *hi) *lo = *hi = 0;
 }
 
-static int run_items(Device* D, const std::vector<CrcItem>& items, uint32_t* sums_dev, hipStream_t s) {
-    if (items.empty()) return KRK_OK;
-    void* d_items = nullptr;
-    int r = upload(D, items.data(), items.size() * sizeof(CrcItem), &d_items, s);
+static int run_items(Device* D, const CrcBatch& B, uint32_t* sums_dev, hipStream_t s) {
+    if (B.empty()) return KRK_OK;
+    KRK_CHECK(B.run_items + B.items.size() < (1ull << 32), KRK_EINVAL, "more than 2^32 CRC work items in one call");
+    // One upload: [runs][items][consts], each part 16-byte aligned.
+    const size_t nr = B.runs.size() * sizeof(CrcRun), ni = B.items.size() * sizeof(CrcItem);
+    const size_t nc = B.consts.size() * 4;
+    std::vector<uint8_t> pack(nr + ni + nc);
+    if (nr) memcpy(pack.data(), B.runs.data(), nr);
+    if (ni) memcpy(pack.data() + nr, B.items.data(), ni);
+    if (nc) memcpy(pack.data() + nr + ni, B.consts.data(), nc);
+    void* d_pack = nullptr;
+    int r = upload(D, pack.data(), pack.size(), &d_pack, s);
     if (r) return r;
+    const uint8_t* dp = static_cast<const uint8_t*>(d_pack);
+    CrcWork w{};
+    w.runs = reinterpret_cast<const CrcRun*>(dp);
+    w.items = reinterpret_cast<const CrcItem*>(dp + nr);
+    w.consts = reinterpret_cast<const uint32_t*>(dp + nr + ni);
+    w.n_runs = (uint32_t)B.runs.size();
+    w.run_items = (uint32_t)B.run_items;
+    w.n_items = (uint32_t)B.items.size();
     CrcLaunchCfg cfg{D->cus, D->crc_variant};
-    hipError_t e = timed(K_CRC, s, [&] {
-        return launch_crc_items(static_cast<const CrcItem*>(d_items), (uint32_t)items.size(), D->d_tabs,
-                                sums_dev, cfg, s);
-    });
-    scratch_free(D, d_items, s);
+    hipError_t e = timed(K_CRC, s, [&] { return launch_crc_items(w, D->d_tabs, sums_dev, cfg, s); });
+    scratch_free(D, d_pack, s);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
     return KRK_OK;
 }
@@ -394,10 +443,7 @@ static int piece_sums_dev(Device* D, const krk_blob* blobs, uint64_t n, uint32_t
     KRK_CHECK(sums_dev, KRK_EINVAL, "sums_dev is NULL");
     KRK_HIP(hipMemsetAsync(sums_dev + lo, 0, (hi - lo) * 4, s));
     ItemBuilder B;
-    std::vector<CrcItem> items;
-    uint64_t total = 0;
-    for (uint64_t i = 0; i < n; ++i) total += blobs[i].length;
-    items.reserve(total / kItemBytes + 2 * n + 16);
+    CrcBatch items;
     for (uint64_t i = 0; i < n; ++i)
         B.add(items, reinterpret_cast<uint64_t>(blobs[i].data), 0, blobs[i].length, blobs[i].length,
               (uint64_t)blobs[i].piece_length, blobs[i].sums_offset);
@@ -634,7 +680,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         if (r) break;
         Window& w = pl.w[k];
         size_t fill = 0;
-        std::vector<CrcItem> items;
+        CrcBatch items;
         while (bi < n_blobs && fill < W) {
             const krk_blob& b = blobs[bi];
             const uint64_t take = std::min<uint64_t>(b.length - boff, W - fill);
@@ -766,7 +812,7 @@ static int validate_chunks(const krk_chunk* c, uint64_t n) {
 static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
                        uint8_t* digests_dev, hipStream_t s, ItemBuilder& B) {
     std::vector<ShaJob> jobs(n);
-    std::vector<CrcItem> items;
+    CrcBatch items;
     for (uint64_t i = 0; i < n; ++i) {
         ShaJob& j = jobs[i];
         j = ShaJob{};
@@ -847,7 +893,7 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         if (r) break;
         Window& w = pl.w[k];
         std::vector<ShaJob> jobs;
-        std::vector<CrcItem> items;
+        CrcBatch items;
         std::vector<CopyTask> copies;
         size_t fill = 0;
         for (uint64_t i = 0; i < n; ++i) {
@@ -951,7 +997,7 @@ static int stream_flush(krk_piece_stream* s, bool final) {
     if (s->fill) {
         int r = stream_grow_sums(s, krk_num_pieces(b, (int64_t)s->P));
         if (r) return r;
-        std::vector<CrcItem> items;
+        CrcBatch items;
         s->B.add(items, reinterpret_cast<uint64_t>(w.dev), a, b, L, s->P, 0);
         KRK_HIP(hipMemcpyAsync(w.dev, w.host, s->fill, hipMemcpyHostToDevice, s->D->s_a));
         KRK_HIP(hipEventRecord(w.copied, s->D->s_a));
@@ -1041,7 +1087,7 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
     KRK_HIP(hipMemcpyAsync(d_buf, data, n, hipMemcpyHostToDevice, s));
     KRK_HIP(hipMemsetAsync(d_sum, 0, 4, s));
     ItemBuilder B;
-    std::vector<CrcItem> items;
+    CrcBatch items;
     // crc32.Update(crc, IEEETable, p) = ~raw(~crc, p): one piece seeded with ~crc.
     B.add(items, reinterpret_cast<uint64_t>(d_buf), 0, n, n, n, 0, ~crc);
     int r = run_items(D, items, d_sum, s);
