@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -162,8 +163,16 @@ struct DevCache {
     }
 };
 
+struct Pipeline;
+
 struct Device {
     DevCache cache;
+    // Staging windows of the host paths, kept across calls (pinning 2 x 256 MiB
+    // costs ~0.2 s, a third of a 16 GB end-to-end batch).  Leaked at exit like the
+    // other device resources: freeing pinned memory during static destruction can
+    // race the HIP runtime's own teardown.
+    Pipeline* staging = nullptr;
+    std::mutex staging_mu;
     int id = 0;
     int cus = 0;
     hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
@@ -489,19 +498,31 @@ struct Window {
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
-    hipEvent_t copied = nullptr, consumed = nullptr;
-    bool inflight = false;
+    hipEvent_t copied = nullptr;    // the H2D out of `host` has finished: host buffer reusable
+    hipEvent_t consumed = nullptr;  // single-stream users: all work reading `dev` has finished
+    hipEvent_t done[2] = {nullptr, nullptr};  // kernels reading `dev`, one event per kernel stream
+    bool inflight = false, copying = false;
+    bool done_pending[2] = {false, false};
 };
 
+// Two pinned host windows and two device windows.  The host side of window k is
+// refilled once its H2D is done; the H2D into its device side waits (on the copy
+// stream only) for the kernels that read the previous contents, so the upload of
+// window k+1 overlaps the kernels of window k.
 struct Pipeline {
     Window w[2];
     ~Pipeline() {
         for (auto& x : w) {
             if (x.inflight) hipEventSynchronize(x.consumed);
+            if (x.copying) hipEventSynchronize(x.copied);
+            for (int i = 0; i < 2; ++i)
+                if (x.done_pending[i]) hipEventSynchronize(x.done[i]);
             if (x.host) hipHostFree(x.host);
             if (x.dev) hipFree(x.dev);
             if (x.copied) hipEventDestroy(x.copied);
             if (x.consumed) hipEventDestroy(x.consumed);
+            for (auto e : x.done)
+                if (e) hipEventDestroy(e);
         }
     }
     int init(size_t cap) {
@@ -511,23 +532,90 @@ struct Pipeline {
             KRK_HIP(hipMalloc(reinterpret_cast<void**>(&x.dev), cap));
             KRK_HIP(hipEventCreateWithFlags(&x.copied, hipEventDisableTiming));
             KRK_HIP(hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming));
+            for (auto& e : x.done) KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         return KRK_OK;
     }
+    // Host side of window k is free for refilling.
     int acquire(int k) {
         if (w[k].inflight) {
             KRK_HIP(hipEventSynchronize(w[k].consumed));
             w[k].inflight = false;
         }
+        if (w[k].copying) {
+            KRK_HIP(hipEventSynchronize(w[k].copied));
+            w[k].copying = false;
+        }
         return KRK_OK;
+    }
+    // Upload n bytes of window k on cp, after the kernels that read its last contents.
+    hipError_t h2d(int k, size_t n, hipStream_t cp) {
+        Window& x = w[k];
+        for (int i = 0; i < 2; ++i)
+            if (x.done_pending[i]) {
+                hipError_t e = hipStreamWaitEvent(cp, x.done[i], 0);
+                if (e != hipSuccess) return e;
+                x.done_pending[i] = false;
+            }
+        hipError_t e = hipMemcpyAsync(x.dev, x.host, n, hipMemcpyHostToDevice, cp);
+        if (e == hipSuccess) e = hipEventRecord(x.copied, cp);
+        if (e == hipSuccess) x.copying = true;
+        return e;
+    }
+    // Kernel stream ks (slot 0 or 1) has enqueued everything that reads window k.
+    hipError_t release(int k, int slot, hipStream_t ks) {
+        hipError_t e = hipEventRecord(w[k].done[slot], ks);
+        if (e == hipSuccess) w[k].done_pending[slot] = true;
+        return e;
     }
 };
 
+// KRK_TRACE=1: host-side phase times of the windowed host paths, to stderr.
+static bool trace_on() {
+    static const bool on = getenv("KRK_TRACE") && atoi(getenv("KRK_TRACE")) > 0;
+    return on;
+}
+static double wall_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static size_t window_bytes() {
     const char* v = getenv("KRK_WINDOW_MB");
-    size_t mb = v ? strtoull(v, nullptr, 10) : 256;
+    size_t mb = v ? strtoull(v, nullptr, 10) : 512;
     if (mb < 1) mb = 1;
     return mb << 20;
+}
+
+// The device's persistent staging windows (grown to at least `cap`) for one host-path
+// call; a concurrent second caller gets private windows instead of waiting.
+struct StagingLease {
+    Device* D = nullptr;
+    Pipeline* p = nullptr;
+    std::unique_ptr<Pipeline> own;
+    bool locked = false;
+    ~StagingLease() {
+        if (locked) D->staging_mu.unlock();
+    }
+};
+
+static int lease_staging(Device* D, size_t cap, StagingLease& L) {
+    L.D = D;
+    if (D->staging_mu.try_lock()) {
+        L.locked = true;
+        if (!D->staging || D->staging->w[0].cap < cap) {
+            delete D->staging;  // its destructor drains the old windows' events
+            D->staging = nullptr;
+            auto p = std::make_unique<Pipeline>();
+            int r = p->init(cap);
+            if (r) return r;
+            D->staging = p.release();
+        }
+        L.p = D->staging;
+        return KRK_OK;
+    }
+    L.own = std::make_unique<Pipeline>();
+    L.p = L.own.get();
+    return L.own->init(cap);
 }
 
 // Host -> pinned staging copies of one window, split over a few threads (one
@@ -668,9 +756,14 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     uint32_t* d_sums = nullptr;
     KRK_HIP(hipMalloc(&d_sums, hi * 4));
     KRK_HIP(hipMemset(d_sums, 0, hi * 4));
-    Pipeline pl;
     const size_t W = window_bytes();
-    r = pl.init(W);
+    StagingLease lease;
+    r = lease_staging(D, W, lease);
+    if (r) {
+        hipFree(d_sums);
+        return r;
+    }
+    Pipeline& pl = *lease.p;
     hipStream_t cp = D->s_a, ks = D->s_b;
     ItemBuilder B;
     int k = 0;
@@ -695,17 +788,14 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
             fill = (fill + 15) & ~size_t(15);
             if (boff >= b.length) { ++bi; boff = 0; }
         }
-        if (hipMemcpyAsync(w.dev, w.host, std::min(fill, W), hipMemcpyHostToDevice, cp) != hipSuccess ||
-            hipEventRecord(w.copied, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
+        if (pl.h2d(k, std::min(fill, W), cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "piece_sums_host: staging copy failed");
             r = KRK_EHIP;
             break;
         }
         r = run_items(D, items, d_sums, ks);
         if (r) break;
-        hipEventRecord(w.consumed, ks);
-        w.inflight = true;
-        hipStreamWaitEvent(cp, w.consumed, 0);
+        pl.release(k, 0, ks);
         k ^= 1;
     }
     if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
@@ -726,9 +816,10 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     uint64_t C = (W / n) & ~uint64_t(63);
     if (C < 64) C = 64;
     const size_t cap = std::max<size_t>(W, C * n + 16 * n);
-    Pipeline pl;
-    int r = pl.init(cap);
+    StagingLease lease;
+    int r = lease_staging(D, cap, lease);
     if (r) return r;
+    Pipeline& pl = *lease.p;
     uint8_t* d_dig = nullptr;
     uint32_t* d_state = nullptr;
     KRK_HIP(hipMalloc(&d_dig, n * 32));
@@ -762,17 +853,14 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
             fill += (take + 15) & ~uint64_t(15);
             if (fin) { done[i] = 1; --remaining; }
         }
-        if (hipMemcpyAsync(w.dev, w.host, fill, hipMemcpyHostToDevice, cp) != hipSuccess ||
-            hipEventRecord(w.copied, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
+        if (pl.h2d(k, fill, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "sha256_host: staging copy failed");
             r = KRK_EHIP;
             break;
         }
         r = run_jobs(D, jobs, d_dig, d_state, ks);
         if (r) break;
-        hipEventRecord(w.consumed, ks);
-        w.inflight = true;
-        hipStreamWaitEvent(cp, w.consumed, 0);
+        pl.release(k, 0, ks);
         k ^= 1;
     }
     if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
@@ -870,9 +958,10 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     uint64_t C = (W / n) & ~uint64_t(63);
     if (C < 64) C = 64;
     const size_t cap = std::max<size_t>(W, C * n + 16 * n);
-    Pipeline pl;
-    r = pl.init(cap);
+    StagingLease lease;
+    r = lease_staging(D, cap, lease);
     if (r) return r;
+    Pipeline& pl = *lease.p;
     uint8_t* d_dig = nullptr;
     uint32_t *d_state = nullptr, *d_sums = nullptr;
     KRK_HIP(hipMalloc(&d_dig, n * 32));
@@ -882,15 +971,17 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     std::vector<uint64_t> off(n, 0);
     std::vector<char> done(n, 0);
     hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
-    hipEvent_t sha_done, crc_done;
-    KRK_HIP(hipEventCreateWithFlags(&sha_done, hipEventDisableTiming));
-    KRK_HIP(hipEventCreateWithFlags(&crc_done, hipEventDisableTiming));
     ItemBuilder B;
     uint64_t remaining = n;
     int k = 0;
+    double t_acq = 0, t_build = 0, t_copy = 0, t_enq = 0, t0 = wall_s();
+    int n_win = 0;
     while (!r && remaining) {
+        double ta = wall_s();
         r = pl.acquire(k);
         if (r) break;
+        double tb = wall_s();
+        t_acq += tb - ta;
         Window& w = pl.w[k];
         std::vector<ShaJob> jobs;
         CrcBatch items;
@@ -919,9 +1010,13 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
             fill += (take + 15) & ~uint64_t(15);
             if (fin) { done[i] = 1; --remaining; }
         }
+        double tc = wall_s();
+        t_build += tc - tb;
         par_copy(copies);
-        if (hipMemcpyAsync(w.dev, w.host, fill, hipMemcpyHostToDevice, cp) != hipSuccess ||
-            hipEventRecord(w.copied, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
+        double td = wall_s();
+        t_copy += td - tc;
+        ++n_win;
+        if (pl.h2d(k, fill, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
             hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "metainfo_digest_host: staging copy failed");
             r = KRK_EHIP;
@@ -930,20 +1025,23 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         r = run_jobs(D, jobs, d_dig, d_state, ks);
         if (!r) r = run_items(D, items, d_sums, kc);
         if (r) break;
-        // the window is free again once both kernels have read it
-        hipEventRecord(sha_done, ks);
-        hipEventRecord(crc_done, kc);
-        hipStreamWaitEvent(cp, sha_done, 0);
-        hipStreamWaitEvent(cp, crc_done, 0);
-        hipEventRecord(w.consumed, cp);
-        w.inflight = true;
+        // the device window is free again once both kernels have read it
+        pl.release(k, 0, ks);
+        pl.release(k, 1, kc);
+        t_enq += wall_s() - td;
         k ^= 1;
     }
+    const double t_loop = wall_s() - t0;
     if (!r && (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(kc) != hipSuccess ||
                hipStreamSynchronize(cp) != hipSuccess)) {
         set_error(KRK_EHIP, "sync failed");
         r = KRK_EHIP;
     }
+    if (trace_on())
+        fprintf(stderr,
+                "krk_trace metainfo_digest_host: windows=%d W=%zu C=%llu loop=%.3fs acquire=%.3fs build=%.3fs "
+                "copy=%.3fs enqueue=%.3fs drain=%.3fs\n",
+                n_win, W, (unsigned long long)C, t_loop, t_acq, t_build, t_copy, t_enq, wall_s() - t0 - t_loop);
     if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
         set_error(KRK_EHIP, "digest copy-out failed");
         r = KRK_EHIP;
@@ -952,8 +1050,6 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;
     }
-    hipEventDestroy(sha_done);
-    hipEventDestroy(crc_done);
     hipFree(d_dig);
     hipFree(d_state);
     hipFree(d_sums);
@@ -999,14 +1095,11 @@ static int stream_flush(krk_piece_stream* s, bool final) {
         if (r) return r;
         CrcBatch items;
         s->B.add(items, reinterpret_cast<uint64_t>(w.dev), a, b, L, s->P, 0);
-        KRK_HIP(hipMemcpyAsync(w.dev, w.host, s->fill, hipMemcpyHostToDevice, s->D->s_a));
-        KRK_HIP(hipEventRecord(w.copied, s->D->s_a));
+        KRK_HIP(s->pl.h2d(s->cur, s->fill, s->D->s_a));
         KRK_HIP(hipStreamWaitEvent(s->D->s_b, w.copied, 0));
         r = run_items(s->D, items, s->d_sums, s->D->s_b);
         if (r) return r;
-        KRK_HIP(hipEventRecord(w.consumed, s->D->s_b));
-        KRK_HIP(hipStreamWaitEvent(s->D->s_a, w.consumed, 0));
-        w.inflight = true;
+        KRK_HIP(s->pl.release(s->cur, 0, s->D->s_b));
     }
     s->flushed = b;
     s->fill = 0;
