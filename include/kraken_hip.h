@@ -84,6 +84,15 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
 int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host,
                           uint8_t* ok_out_host, void* stream);
 
+/* Batched agent piece verification over HOST buffers: ok_out[i] = 1 iff
+ * crc32(data[i][0:lengths[i]]) == expected[i] -- the h.Sum32() != GetPieceSum(pi)
+ * check of agentstorage.Torrent.writePiece (lib/torrent/storage/agentstorage/
+ * torrent.go:174-199, error "invalid piece sum"), for many received pieces (any
+ * torrents, any lengths) in one pinned, pipelined GPU pass instead of one
+ * hash.Hash32 per piece.  Synchronous. */
+int krk_verify_pieces_host(const uint8_t* const* data, const uint64_t* lengths, const uint32_t* expected,
+                           uint64_t n, uint8_t* ok_out);
+
 /* ----------------------------------------------------- SHA-256 (Digester)
  * Replaces core.Digester (core/digester.go:28-72): crypto.SHA256 over the whole
  * blob.  One Merkle-Damgard stream per lane, many blobs per launch. */

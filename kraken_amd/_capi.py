@@ -64,6 +64,7 @@ def _load() -> C.CDLL:
         "krk_piece_stream_free": (None, [vp]),
         "krk_crc32_update": (i, [C.c_uint32, vp, C.c_uint64, u32p]),
         "krk_verify_pieces_dev": (i, [blobp, u32p, u8p, vp]),
+        "krk_verify_pieces_host": (i, [C.POINTER(vp), u64p, u32p, C.c_uint64, u8p]),
         "krk_sha256_dev": (i, [C.POINTER(vp), u64p, C.c_uint64, vp, vp]),
         "krk_sha256_host": (i, [C.POINTER(vp), u64p, C.c_uint64, u8p]),
         "krk_digester_new": (i, [C.POINTER(vp)]),

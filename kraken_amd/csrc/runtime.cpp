@@ -1221,6 +1221,21 @@ int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, u
     return r;
 }
 
+int krk_verify_pieces_host(const uint8_t* const* data, const uint64_t* lengths, const uint32_t* expected,
+                           uint64_t n, uint8_t* ok_out) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(data && lengths && expected && ok_out, KRK_EINVAL, "verify_pieces_host: null argument");
+    // Each piece is a one-piece blob; an empty piece sums to 0 (crc32 of nothing).
+    std::vector<krk_blob> blobs(n);
+    for (uint64_t i = 0; i < n; ++i)
+        blobs[i] = krk_blob{data[i], lengths[i], (int64_t)std::max<uint64_t>(lengths[i], 1), i};
+    std::vector<uint32_t> sums(n, 0);
+    int r = krk_piece_sums_host(blobs.data(), n, sums.data());
+    if (r) return r;
+    for (uint64_t i = 0; i < n; ++i) ok_out[i] = sums[i] == expected[i];
+    return KRK_OK;
+}
+
 // ---------------------------------------------------------------- digester
 struct krk_digester {
     Device* D = nullptr;

@@ -1,0 +1,64 @@
+"""GPU parity: batched agent piece verification (agentstorage.Torrent.writePiece,
+lib/torrent/storage/agentstorage/torrent.go:174-220) through krk_verify_pieces_host,
+against zlib.crc32 (= Go hash/crc32 IEEE) and the reference's error strings."""
+import io
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from kraken_amd import agentstorage, core
+
+pytestmark = pytest.mark.gpu
+
+
+def test_verify_pieces_matches_crc32(gpu):
+    rng = np.random.default_rng(11)
+    lens = [0, 1, 2, 3, 4, 15, 16, 17, 63, 64, 65, 4095, 4096, 4097, 262143, 262144, 262145,
+            (1 << 20) + 1, 4 << 20, (4 << 20) - 3]
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    expected = [zlib.crc32(d) for d in datas]
+    assert agentstorage.verify_pieces(datas, expected).all()
+    # one flipped bit / one wrong sum per piece -> every check fails
+    bad = [bytes([d[0] ^ 1]) + d[1:] if d else d for d in datas]
+    ok = agentstorage.verify_pieces(bad, expected)
+    assert ok.tolist() == [len(d) == 0 for d in datas]
+    ok = agentstorage.verify_pieces(datas, [e ^ 0x80000000 for e in expected])
+    assert not ok.any()
+
+
+def test_verify_many_small_pieces_one_call(gpu):
+    rng = np.random.default_rng(12)
+    datas = [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 5000, 3000)]
+    expected = np.array([zlib.crc32(d) for d in datas], dtype=np.uint32)
+    flip = rng.choice(len(datas), 100, replace=False)
+    expected[flip] ^= 1
+    ok = agentstorage.verify_pieces(datas, expected)
+    want = np.ones(len(datas), dtype=bool)
+    want[flip] = False
+    assert np.array_equal(ok, want)
+
+
+def test_torrent_write_pieces(gpu, tmp_path):
+    rng = np.random.default_rng(13)
+    blob = rng.integers(0, 256, size=10 * 65536 + 1234, dtype=np.uint8).tobytes()
+    P = 65536
+    d = core.NewDigester().FromBytes(blob)
+    mi = core.NewMetaInfo(d, io.BytesIO(blob), P)
+    t = agentstorage.Torrent(mi, str(tmp_path / "download"))
+    pieces = {pi: blob[pi * P:pi * P + mi.GetPieceLength(pi)] for pi in range(mi.NumPieces())}
+    corrupt = dict(pieces)
+    corrupt[3] = b"\x00" + pieces[3][1:]
+    first = {pi: corrupt[pi] for pi in (7, 3, 10, 0)}
+    res = t.WritePieces(first)
+    assert res[7] is None and res[10] is None and res[0] is None
+    assert str(res[3]) == "invalid piece sum"
+    with pytest.raises(ValueError, match="invalid piece length: expected 65536, got 3"):
+        t.WritePiece(b"abc", 5)
+    with pytest.raises(agentstorage.ErrPieceComplete):
+        t.WritePiece(pieces[7], 7)
+    rest = {pi: pieces[pi] for pi in range(mi.NumPieces()) if not t.complete[pi]}
+    assert all(e is None for e in t.WritePieces(rest).values())
+    assert t.Complete()
+    assert open(tmp_path / "download", "rb").read() == blob
