@@ -37,15 +37,32 @@ def newPieceLengthConfig(piece_length_by_file_size: dict) -> pieceLengthConfig:
     return pieceLengthConfig(sorted((int(a), int(b)) for a, b in piece_length_by_file_size.items()))
 
 
+DefaultShardIDLength = 2  # lib/store/base/const.go:16-18
+
+
 class DirCAS:
-    """Minimal content-addressed cache: <root>/<hex>/data and <hex>/_torrentmeta
-    (cf. lib/store/base/file_entry.go:175-189)."""
+    """Minimal content-addressed cache directory in the reference's layout:
+    <root>/<hex[0:2]>/<hex[2:4]>/<hex>/data with the _torrentmeta sidecar beside it
+    (casFileEntryFactory.GetRelativePath, lib/store/base/file_entry.go:176-189;
+    getMetadataPath :468-469)."""
 
     def __init__(self, root: str):
         self.root = root
 
     def _dir(self, hex_: str) -> str:
-        return os.path.join(self.root, hex_)
+        shards = [hex_[2 * i:2 * i + 2] for i in range(min(DefaultShardIDLength, len(hex_) // 2))]
+        return os.path.join(self.root, *shards, hex_)
+
+    def ListNames(self) -> list[str]:
+        """Every cached blob name, walking the shard directories (file_entry.go ListNames)."""
+        out = []
+        for dirpath, dirnames, filenames in os.walk(self.root):
+            rel = os.path.relpath(dirpath, self.root)
+            depth = 0 if rel == "." else rel.count(os.sep) + 1
+            if depth == DefaultShardIDLength + 1 and "data" in filenames:
+                out.append(os.path.basename(dirpath))
+                dirnames[:] = []
+        return sorted(out)
 
     def GetCacheFileStat(self, hex_: str) -> os.stat_result:
         return os.stat(os.path.join(self._dir(hex_), "data"))
@@ -105,6 +122,24 @@ class Generator:
         except OSError as e:
             raise IOError(f"set metainfo: {e}") from None
 
+    def RegenerateAll(self, batch_bytes: int = 8 << 30) -> dict:
+        """Whole-CAS regeneration: every cached blob's
+        _torrentmeta rewritten from GPU piece sums in batches of ~batch_bytes
+        (each batch one pinned, pipelined pass), byte-identical to what
+        Generate writes.  Returns counts of blobs seen / sidecars changed."""
+        names = self.cas.ListNames()
+        seen = changed = 0
+        batch, size = [], 0
+        for i, name in enumerate(names):
+            batch.append(core.NewSHA256DigestFromHex(name))
+            size += self.cas.GetCacheFileStat(name).st_size
+            if size >= batch_bytes or i == len(names) - 1:
+                self.GenerateBatch(batch)
+                changed += self._last_changed
+                seen += len(batch)
+                batch, size = [], 0
+        return {"blobs": seen, "changed": changed}
+
     def GenerateBatch(self, digests) -> list[core.MetaInfo]:
         """Generate for many cache files in one pipelined GPU pass."""
         datas, blobs, off = [], [], 0
@@ -120,12 +155,13 @@ class Generator:
         sums = np.zeros(max(off, 1), dtype=np.uint32)
         check(lib.krk_piece_sums_host(arr, len(datas), sums.ctypes.data_as(C.POINTER(C.c_uint32))))
         out = []
+        self._last_changed = 0
         for d, b, pl, o in datas:
             n = int(lib.krk_num_pieces(b.size, pl))
             s = sums[o:o + n].copy() if n else None
             ih = core._info_hash(pl, s if s is not None else np.zeros(0, np.uint32), d.Hex(), b.size)
             mi = core.MetaInfo(pl, s, d.Hex(), b.size, d, ih)
-            self.cas.SetCacheFileMetadata(d.Hex(), mi)
+            self._last_changed += bool(self.cas.SetCacheFileMetadata(d.Hex(), mi))
             out.append(mi)
         return out
 
@@ -161,3 +197,35 @@ class Generator:
 
 def New(config: dict, cas) -> Generator:
     return Generator(config, cas)
+
+
+def _parse_config(text: str) -> dict:
+    """"0:4194304,2147483648:8388608" -> {0: 4194304, 2147483648: 8388608}."""
+    out = {}
+    for part in text.split(","):
+        a, b = part.split(":")
+        out[int(a)] = int(b)
+    return out
+
+
+def main(argv=None) -> int:
+    """python -m kraken_amd.metainfogen <cache dir> [--piece-lengths 0:4194304]:
+    regenerate every _torrentmeta of a CAS cache directory on the GPU."""
+    import argparse
+    import json
+    ap = argparse.ArgumentParser(description=main.__doc__)
+    ap.add_argument("cache_dir")
+    ap.add_argument("--piece-lengths", default="0:4194304",
+                    help="size:pieceLength ranges (config/origin/base.yaml:24-26 default: 0:4MB)")
+    ap.add_argument("--batch-gib", type=int, default=8)
+    ap.add_argument("--device", type=int, default=0)
+    a = ap.parse_args(argv)
+    from . import device
+    device.set_device(a.device)
+    g = New(_parse_config(a.piece_lengths), DirCAS(a.cache_dir))
+    print(json.dumps(g.RegenerateAll(a.batch_gib << 30)))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

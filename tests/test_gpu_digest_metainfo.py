@@ -167,7 +167,7 @@ def test_generator_generate_and_batch(gpu, orc, tmp_path):
     g = metainfogen.New({0: 1 << 20, 4 << 20: 4 << 20}, cas)
     for d, b in zip(ds, blobs):
         g.Generate(d)
-        mi = core.DeserializeMetaInfo(open(tmp_path / d.Hex() / "_torrentmeta", "rb").read())
+        mi = core.DeserializeMetaInfo(open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read())
         pl = 1 << 20 if len(b) < 4 << 20 else 4 << 20
         ref = orc.calc_piece_sums(b, pl)[1]
         assert bytes(mi.InfoHash()) == orc.info_hash(pl, ref, d.Hex(), len(b))
@@ -266,5 +266,43 @@ def test_verify_and_generate_batch(gpu, orc, tmp_path):
         pl = 1 << 20 if len(b) < 4 << 20 else 4 << 20
         assert bytes(mi.InfoHash()) == orc.info_hash(pl, orc.calc_piece_sums(b, pl)[1], d.Hex(), len(b))
         two_pass = core.NewMetaInfo(d, b, pl)
-        assert open(tmp_path / d.Hex() / "_torrentmeta", "rb").read() == two_pass.Serialize()
-        assert open(tmp_path / d.Hex() / "data", "rb").read() == b
+        assert open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read() == two_pass.Serialize()
+        assert open(os.path.join(cas._dir(d.Hex()), "data"), "rb").read() == b
+
+
+def _go_json(pl, sums, name, length):
+    """encoding/json of metaInfoJSON{info} (core/metainfo.go:125-134), written out
+    independently of core.MetaInfo.Serialize: declared field order, compact, nil
+    slice -> null."""
+    ps = "null" if sums is None else "[" + ",".join(str(int(x)) for x in sums) + "]"
+    return ('{"Info":{"PieceLength":%d,"PieceSums":%s,"Name":"%s","Length":%d}}' % (pl, ps, name, length)).encode()
+
+
+def test_regenerate_all_cas_sidecars(gpu, orc, tmp_path):
+    """Whole-CAS _torrentmeta regeneration in the reference's
+    shard layout, byte-identical sidecars, only changed ones rewritten."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path))
+    rng = np.random.default_rng(21)
+    lens = [0, 1, 4095, 65536, 1 << 20, (1 << 20) + 3, (3 << 20) + 7, 9 << 20]
+    blobs = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    ds = [cas.WriteCacheFile(b) for b in blobs]
+    for d in ds:  # <hex[0:2]>/<hex[2:4]>/<hex>/data (lib/store/base/file_entry.go:176-189)
+        h = d.Hex()
+        assert os.path.exists(tmp_path / h[:2] / h[2:4] / h / "data")
+    assert cas.ListNames() == sorted(d.Hex() for d in ds)
+    cfg = {0: 1 << 20, 8 << 20: 4 << 20}
+    g = metainfogen.New(cfg, cas)
+    assert g.RegenerateAll(batch_bytes=4 << 20) == {"blobs": len(ds), "changed": len(ds)}
+    for d, b in zip(ds, blobs):
+        pl = 1 << 20 if len(b) < 8 << 20 else 4 << 20
+        ref = orc.calc_piece_sums(b, pl)[1] if len(b) else None
+        got = open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read()
+        assert got == _go_json(pl, ref, d.Hex(), len(b))
+    assert g.RegenerateAll() == {"blobs": len(ds), "changed": 0}
+    # CLI over the same directory with another piece-length table rewrites everything
+    assert metainfogen.main([str(tmp_path), "--piece-lengths", "0:65536"]) == 0
+    for d, b in zip(ds, blobs):
+        ref = orc.calc_piece_sums(b, 65536)[1] if len(b) else None
+        got = open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read()
+        assert got == _go_json(65536, ref, d.Hex(), len(b))

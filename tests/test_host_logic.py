@@ -1,5 +1,6 @@
 """Host-side logic of the mirror API (no GPU): digest parsing/validation, InfoHash
 hex, MetaInfo JSON, metainfogen config -- with the reference's error strings."""
+import os
 import numpy as np
 import pytest
 
@@ -116,3 +117,18 @@ def test_uint64_to_float64_host_matches_oracle(orc):
         b = v.to_bytes(8, "big")
         assert hrw.UInt64ToFloat64(b, rehash=rh) == orc.uint64_to_float64(v, rehash=True), hex(v)
         assert hrw.UInt64ToFloat64(b) == orc.uint64_to_float64(v, rehash=False), hex(v)
+
+
+def test_dircas_layout_and_list_names(tmp_path):
+    """DirCAS follows casFileEntryFactory.GetRelativePath (lib/store/base/file_entry.go:176-189)."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path))
+    name = "07123e1f482356c415f684407a3b8723e10b2cbbc0b8fcd6282c49d37c9c1abc"  # the reference's example
+    assert cas._dir(name) == str(tmp_path / "07" / "12" / name)
+    names = [name, "ff" * 32, "00ab" + "1" * 60]
+    for n in names:
+        os.makedirs(cas._dir(n))
+        open(os.path.join(cas._dir(n), "data"), "wb").close()
+    os.makedirs(tmp_path / "07" / "12" / "stray")  # no data file: not a blob
+    assert cas.ListNames() == sorted(names)
+    assert metainfogen._parse_config("0:4194304,2147483648:8388608") == {0: 4194304, 2147483648: 8388608}
