@@ -71,6 +71,7 @@ if __name__ == "__main__":
     ap.add_argument("--variant", default="0")
     ap.add_argument("--sha-variant", default="-1")
     ap.add_argument("--c2", action="store_true")
+    ap.add_argument("--crc-spec", default="", help="gb:blob_mb:piece_kb,... custom CRC shapes")
     a = ap.parse_args()
     os.environ["KRK_CRC_VARIANT"] = a.variant
     os.environ["KRK_SHA_VARIANT"] = a.sha_variant
@@ -78,6 +79,11 @@ if __name__ == "__main__":
     res = []
     if a.c2:
         print(json.dumps(crc_concurrent(1000, 100, 4 << 20)), flush=True)
+        sys.exit(0)
+    if a.crc_spec:
+        for spec in a.crc_spec.split(","):
+            gb, mb, pk = spec.split(":")
+            print(json.dumps(crc(float(gb), int(mb), int(pk) << 10, 3)), flush=True)
         sys.exit(0)
     if a.crc_gb > 0:
         res.append(crc(a.crc_gb, 100, 4 << 20, 3))
