@@ -1,0 +1,65 @@
+"""Re-entrancy of the C ABI (SURVEY.md §8(b) "Threading": HTTP handlers, the
+blobrefresh worker pool and P2P dispatch call NewMetaInfo / Digester /
+PieceHash / Locations from many goroutines at once).  Eight host threads call
+the host-buffer entry points concurrently (ctypes drops the GIL for the call);
+every result must equal the single-threaded reference."""
+import hashlib
+import io
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from kraken_amd import agentstorage, core, hrw
+from kraken_amd import device as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _work(seed: int):
+    D.set_device(0)  # per calling thread (krk_set_device)
+    rng = np.random.default_rng(seed)
+    out = []
+    # Digester streaming writes
+    data = rng.integers(0, 256, int(rng.integers(1, 3 << 20)), dtype=np.uint8).tobytes()
+    d = core.NewDigester()
+    for i in range(0, len(data), 700_001):
+        d._write(data[i:i + 700_001])
+    out.append(d.Digest().Hex() == hashlib.sha256(data).hexdigest())
+    # NewMetaInfo over a reader (piece stream) vs zlib per piece
+    P = int(rng.choice([3, 4096, 65536, 1 << 20]))
+    small = data[:200_000]
+    mi = core.NewMetaInfo(core.NewDigester().FromBytes(small), io.BytesIO(small), P)
+    ref = [zlib.crc32(small[i:i + P]) for i in range(0, len(small), P)]
+    out.append(mi.PieceSums().tolist() == ref)
+    # PieceHash
+    h = core.PieceHash()
+    h.Write(data[:12345])
+    out.append(h.Sum32() == zlib.crc32(data[:12345]))
+    # batched host metainfo + digest
+    blobs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(0, 1 << 20, 6)]
+    sums, dg = D.metainfo_digest_host(blobs, 1 << 18)
+    for b, s, g in zip(blobs, sums, dg):
+        out.append(bytes(g) == hashlib.sha256(b.tobytes()).digest())
+        out.append(s.tolist() == [zlib.crc32(b[i:i + (1 << 18)].tobytes()) for i in range(0, b.size, 1 << 18)])
+    # agent piece verification
+    pieces = [data[i:i + 5000] for i in range(0, 50_000, 5000)]
+    out.append(bool(agentstorage.verify_pieces(pieces, [zlib.crc32(p) for p in pieces]).all()))
+    # HRW ordering
+    rh = hrw.NewRendezvousHash()
+    for k in range(5):
+        rh.AddNode(f"origin-{k:03d}.kraken.test:15002", 100)
+    keys = [rng.bytes(2).hex() for _ in range(50)]
+    out.append([o.tolist() for o in rh.GetOrderedNodesBatch(keys, 5)])
+    return out
+
+
+def test_concurrent_callers_match_serial(gpu):
+    serial = [_work(s) for s in range(8)]
+    for r in serial:
+        assert all(x is True for x in r[:-1])
+    with ThreadPoolExecutor(8) as ex:
+        for rounds in range(2):
+            par = list(ex.map(_work, range(8)))
+            assert par == serial

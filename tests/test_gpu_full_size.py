@@ -1,0 +1,108 @@
+"""GPU parity at BASELINE.json's full sizes, where the oracle cannot recompute
+everything in seconds: sampled oracle checks plus size-independent properties.
+
+* C2 (configs[1]: 1,000 x 100 MiB, 4 MiB pieces, 105 GB in HBM): sampled blobs
+  against hashlib / the oracle, and decomposition invariance over ALL blobs --
+  the chunked path (SHA-256 from per-blob midstates, CRC items cut at chunk edges
+  that split pieces) must give the same 1,000 digests and 25,000 sums as the
+  one-shot path (two different work decompositions of the same bytes).
+* C4 (configs[3]: one 20 GiB blob, 256 KiB pieces): sampled pieces against the
+  oracle (content regenerated at the piece's offset), and CRC linearity -- the
+  81,920 piece sums combined with crc(A||B) = shift(crc(A), |B|) ^ crc(B) equal the
+  GPU's CRC of the whole blob computed as ONE piece (81,920 work items XOR-reduced
+  into a single sum).
+"""
+import hashlib
+import zlib
+
+import numpy as np
+import pytest
+
+from kraken_amd import device as D
+
+pytestmark = pytest.mark.gpu
+
+POLY = 0xEDB88320
+ONE = 0x80000000  # the polynomial 1, bit-reflected (crc_math.hpp)
+
+
+def _mulmod(a: int, b: int) -> int:
+    p = 0
+    for i in range(31, -1, -1):
+        if (a >> i) & 1:
+            p ^= b
+        b = (b >> 1) ^ (POLY if b & 1 else 0)
+    return p
+
+
+def _x8n(n: int) -> int:
+    p, sq = ONE, ONE >> 8  # x^0, x^8
+    while n:
+        if n & 1:
+            p = _mulmod(p, sq)
+        sq = _mulmod(sq, sq)
+        n >>= 1
+    return p
+
+
+def _combine(crcs, piece: int) -> int:
+    """CRC of the concatenation of equal-length pieces from their CRCs
+    (multiplication by the fixed x^(8*piece) through four byte tables)."""
+    x = _x8n(piece)
+    T = [[_mulmod(b << (8 * k), x) for b in range(256)] for k in range(4)]
+    c = 0
+    for s in crcs:
+        c = T[0][c & 255] ^ T[1][(c >> 8) & 255] ^ T[2][(c >> 16) & 255] ^ T[3][c >> 24] ^ int(s)
+    return c
+
+
+def test_crc_combine_helper_matches_zlib():
+    rng = np.random.default_rng(1)
+    parts = [rng.integers(0, 256, 1000, dtype=np.uint8).tobytes() for _ in range(5)]
+    assert _combine([zlib.crc32(p) for p in parts], 1000) == zlib.crc32(b"".join(parts))
+
+
+def test_c2_full_size_decomposition_invariance(gpu, orc):
+    n, L, P = 1000, 100 << 20, 4 << 20
+    arena = D.BlobArena([L] * n, P)  # blob i = synthetic blob i, generated on the device
+    out = D.BatchOutputs(arena)
+    D.metainfo_digest(arena, out)
+    D.synchronize()
+    sums = out.sums.to_host(np.uint32, arena.total_pieces)
+    dg = out.digests.to_host(np.uint8, 32 * n).reshape(n, 32)
+    assert arena.total_pieces == 25_000
+    for i in (0, 517, 999):
+        data = orc.synth(i, L)
+        assert bytes(dg[i]) == hashlib.sha256(data).digest(), i
+        o = int(arena.sums_off[i])
+        assert np.array_equal(sums[o:o + 25], orc.calc_piece_sums(data, P)[1]), i
+    cb = D.ChunkedBatch([L] * n, P)
+    chunk = 3 * P + 64 * 1001  # a multiple of 64 that cuts pieces at varying offsets
+    pos = 0
+    while pos < L:
+        take = min(chunk, L - pos)
+        cb.step([(i, arena.buf.ptr + int(arena.offsets[i]) + pos, pos, take) for i in range(n)])
+        pos += take
+    D.synchronize()
+    assert np.array_equal(cb.sums.to_host(np.uint32, arena.total_pieces), sums)
+    assert np.array_equal(cb.digests.to_host(np.uint8, 32 * n).reshape(n, 32), dg)
+
+
+def test_c4_full_size_sampled_and_linear(gpu, orc):
+    L, P = 20 << 30, 256 << 10
+    arena = D.BlobArena([L], P, blob_ids=[0])
+    out = D.BatchOutputs(arena)
+    D.piece_sums(arena, out)
+    D.synchronize()
+    n = L // P
+    sums = out.sums.to_host(np.uint32, n)
+    rng = np.random.default_rng(4)
+    for pi in [0, 1, n // 2, n - 1] + rng.choice(n, 12, replace=False).tolist():
+        assert int(sums[pi]) == orc.crc32_clmul(orc.synth(0, P, offset=pi * P)), pi
+    # the same 20 GiB as ONE piece
+    from kraken_amd._capi import check, krk_blob, lib
+    one = (krk_blob * 1)(krk_blob(arena.buf.ptr + int(arena.offsets[0]), L, L, 0))
+    s1 = D.DeviceBuffer(4)
+    check(lib.krk_piece_sums_dev(one, 1, s1.ptr, None))
+    D.synchronize()
+    assert int(s1.to_host(np.uint32, 1)[0]) == _combine(sums, P)
