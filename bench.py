@@ -237,14 +237,15 @@ def run_metainfo(a, D, T, rank, world, res):
     n = len(lens)
     arena = D.BlobArena(lens, P, blob_ids=ids)
     out = D.BatchOutputs(arena)
-    sums_h = np.empty(max(arena.total_pieces, 1), dtype=np.uint32)
-    dg_h = np.empty(max(n, 1) * 32, dtype=np.uint8)
+    pin_s = D.PinnedArray((max(arena.total_pieces, 1),), np.uint32)  # results gathered to pinned host memory
+    pin_d = D.PinnedArray((max(n, 1) * 32,), np.uint8)
+    sums_h, dg_h = pin_s.a, pin_d.a
 
     def step():
         D.metainfo_digest(arena, out)
         D.synchronize()
-        sums_h[:] = out.sums.to_host(np.uint32, sums_h.size)
-        dg_h[:] = out.digests.to_host(np.uint8, dg_h.size)
+        pin_s.fill_from(out.sums)
+        pin_d.fill_from(out.digests)
 
     for _ in range(a.warmup):
         step()
@@ -332,12 +333,13 @@ def run_pieces(a, D, T, rank, world, res):
     ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
     arena = D.BlobArena(lens, P, blob_ids=ids)
     out = D.BatchOutputs(arena)
-    sums_h = np.empty(max(arena.total_pieces, 1), dtype=np.uint32)
+    pin_s = D.PinnedArray((max(arena.total_pieces, 1),), np.uint32)  # results gathered to pinned host memory
+    sums_h = pin_s.a
 
     def step():
         D.piece_sums(arena, out)
         D.synchronize()
-        sums_h[:] = out.sums.to_host(np.uint32, sums_h.size)
+        pin_s.fill_from(out.sums)
 
     for _ in range(a.warmup):
         step()
@@ -479,12 +481,13 @@ def run_hrw(a, D, T, rank, world, res):
     dbuf.from_host(dig.reshape(-1))
     locs = D.DeviceBuffer(n * R * 4)
     counts = D.DeviceBuffer(n)
-    locs_h = np.empty((n, R), dtype=np.int32)
+    pin = D.PinnedArray((n, R), np.int32)  # owner lists gathered to pinned host memory
+    locs_h = pin.a
 
     def step():
         D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts)
         D.synchronize()
-        locs_h[:] = locs.to_host(np.int32, n * R).reshape(n, R)
+        pin.fill_from(locs)
 
     for _ in range(a.warmup):
         step()
@@ -510,6 +513,51 @@ def run_hrw(a, D, T, rank, world, res):
         cbl, cl, cc = cpu_baseline_hrw(dig, labels, healthy, R, a.cpu_seconds)
         cbl["outputs_match_gpu"] = bool(np.array_equal(cl, locs_h[:cl.shape[0]]))
         res["cpu_baseline"] = cbl
+    if rank == 0 and world == 1 and not a.no_sweep:
+        res["sweep"] = hrw_sweep(D, dbuf, dig, n, a.steps)
+
+
+def hrw_sweep(D, dbuf, dig, n, steps):
+    """SURVEY.md 8(d) C5 grid: N in {3, 5, 16, 64} origins x MaxReplica in {2, 3} x
+    healthy = all / a seeded 75 % subset, plus the weighted variant (100/200/400/800).
+    Each point: digests/s over `steps` timed calls, and its first 2,048 digests
+    checked against the oracle's GetOrderedNodes + Locations filter."""
+    from oracle import oracle as O  # the checker (test infrastructure)
+    O.build()
+    points = [(N, R, hf, False) for N in (3, 5, 16, 64) for R in (2, 3) for hf in (1.0, 0.75)]
+    points += [(16, 3, 1.0, True), (64, 3, 0.75, True)]
+    out = []
+    for N, R, hf, weighted in points:
+        labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(N)]
+        weights = [[100, 200, 400, 800][i % 4] if weighted else 100 for i in range(N)]
+        healthy = np.ones(N, dtype=np.uint8)
+        if hf < 1.0:
+            rng = np.random.default_rng(0x75 + N)
+            healthy[rng.choice(N, N - int(round(N * hf)), replace=False)] = 0
+        locs = D.DeviceBuffer(n * R * 4)
+        counts = D.DeviceBuffer(n)
+        pin = D.PinnedArray((n, R), np.int32)
+        D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts, weights=weights)
+        D.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):  # same step as the headline C5 line: results gathered to host
+            D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts, weights=weights)
+            D.synchronize()
+            pin.fill_from(locs)
+        el = time.perf_counter() - t0
+        got = pin.a
+        cnt = counts.to_host(np.uint8, n)
+        ok, memo = True, {}
+        for i in range(2048):
+            key = bytes(dig[i, :2]).hex()
+            if key not in memo:
+                order = O.hrw_ordered(key, labels, weights)
+                memo[key] = O.ring_locations(order, healthy, R)
+            want = list(memo[key])
+            ok = ok and int(cnt[i]) == len(want) and got[i, :len(want)].tolist() == want
+        out.append({"nodes": N, "max_replica": R, "healthy": int(healthy.sum()), "weighted": weighted,
+                    "digests_per_s": round(n * steps / el, 1), "oracle_match_first_2048": bool(ok)})
+    return out
 
 
 def main():
@@ -527,6 +575,7 @@ def main():
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the live SHA issue-ceiling run (profiler passes: keeps its launches out of the trace)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers, PCIe) leg")
+    ap.add_argument("--no-sweep", action="store_true", help="C5: skip the N x MaxReplica x healthy grid")
     ap.add_argument("--e2e-mb", type=int, default=16, help="bytes per blob for the end-to-end leg (MiB)")
     a = ap.parse_args()
 

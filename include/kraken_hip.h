@@ -216,6 +216,11 @@ int krk_synth_fill_chunks_dev(const krk_chunk* chunks, uint64_t n, int variant, 
  * For callers (benchmarks, cgo) that do not own a device allocator. */
 int krk_dev_alloc(uint64_t bytes, void** out);
 int krk_dev_free(void* p);
+/* Pinned (page-locked) host memory: what a cgo caller reads files / receives
+ * pieces into so that the host entry points DMA it without a staging copy, and
+ * where device results are gathered at full PCIe rate. */
+int krk_host_alloc(uint64_t bytes, void** out);
+int krk_host_free(void* p);
 int krk_memcpy_h2d(void* dst_dev, const void* src_host, uint64_t n);
 int krk_memcpy_d2h(void* dst_host, const void* src_dev, uint64_t n);
 int krk_stream_create(void** out);

@@ -173,6 +173,13 @@ struct Device {
     // race the HIP runtime's own teardown.
     Pipeline* staging = nullptr;
     std::mutex staging_mu;
+    // The 65,536 ShardID keys (2 bytes each) of the Locations shard table, uploaded
+    // once: constant input of every krk_ring_locations_dev call.
+    uint8_t* shard_kb = nullptr;
+    uint64_t* shard_koff = nullptr;
+    uint8_t* shard_bad = nullptr;
+    std::once_flag shard_once;
+    int shard_rc = 0;
     int id = 0;
     int cus = 0;
     hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
@@ -1378,20 +1385,16 @@ static void free_nodes(Device* D, DevNodes& dn, hipStream_t s) {
     if (dn.w) scratch_free(D, dn.w, s);
 }
 
-// Order + Locations table for the given decoded keys; result rows on the device.
-static int hrw_table(Device* D, const std::vector<uint8_t>& kb, const std::vector<uint64_t>& koff,
-                     const std::vector<uint8_t>& bad, const krk_nodes* nodes, const uint8_t* healthy,
-                     int32_t max_replica, uint32_t row_out, int32_t** d_locs, uint8_t** d_counts,
-                     hipStream_t s) {
-    const uint64_t nk = koff.size() - 1;
+// Order + Locations table for nk decoded keys already on the device; result rows
+// on the device.
+static int hrw_table_dev(Device* D, const void* d_kb, const void* d_koff, const void* d_bad, uint64_t nk,
+                         const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica, uint32_t row_out,
+                         int32_t** d_locs, uint8_t** d_counts, hipStream_t s) {
     const uint32_t N = nodes->n_nodes;
     DevNodes dn;
     int r = upload_nodes(D, nodes, dn, s);
-    void *d_kb = nullptr, *d_koff = nullptr, *d_bad = nullptr, *d_h = nullptr;
+    void* d_h = nullptr;
     int32_t* d_order = nullptr;
-    if (!r) r = upload(D, kb.data(), kb.size(), &d_kb, s);
-    if (!r) r = upload(D, koff.data(), koff.size() * 8, &d_koff, s);
-    if (!r) r = upload(D, bad.data(), bad.size(), &d_bad, s);
     if (!r) r = upload(D, healthy, N, &d_h, s);
     if (!r && scratch_alloc(D, reinterpret_cast<void**>(&d_order), nk * N * 4, s) != hipSuccess) r = KRK_ENOMEM;
     if (!r && scratch_alloc(D, reinterpret_cast<void**>(d_locs), nk * row_out * 4, s) != hipSuccess) r = KRK_ENOMEM;
@@ -1409,7 +1412,23 @@ static int hrw_table(Device* D, const std::vector<uint8_t>& kb, const std::vecto
         if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
     free_nodes(D, dn, s);
-    for (void* p : {d_kb, d_koff, d_bad, d_h, static_cast<void*>(d_order)})
+    for (void* p : {d_h, static_cast<void*>(d_order)})
+        if (p) scratch_free(D, p, s);
+    return r;
+}
+
+// The same for keys given on the host.
+static int hrw_table(Device* D, const std::vector<uint8_t>& kb, const std::vector<uint64_t>& koff,
+                     const std::vector<uint8_t>& bad, const krk_nodes* nodes, const uint8_t* healthy,
+                     int32_t max_replica, uint32_t row_out, int32_t** d_locs, uint8_t** d_counts,
+                     hipStream_t s) {
+    void *d_kb = nullptr, *d_koff = nullptr, *d_bad = nullptr;
+    int r = upload(D, kb.data(), kb.size(), &d_kb, s);
+    if (!r) r = upload(D, koff.data(), koff.size() * 8, &d_koff, s);
+    if (!r) r = upload(D, bad.data(), bad.size(), &d_bad, s);
+    if (!r) r = hrw_table_dev(D, d_kb, d_koff, d_bad, koff.size() - 1, nodes, healthy, max_replica, row_out,
+                              d_locs, d_counts, s);
+    for (void* p : {d_kb, d_koff, d_bad})
         if (p) scratch_free(D, p, s);
     return r;
 }
@@ -1531,14 +1550,24 @@ int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_n
     KRK_DEVICE(D);
     hipStream_t s = pick(D, stream);
     const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
-    std::vector<uint32_t> shards(65536);
-    std::iota(shards.begin(), shards.end(), 0u);
-    std::vector<uint8_t> kb, bad(65536, 0);
-    std::vector<uint64_t> koff;
-    shard_keys(kb, koff, shards);
+    std::call_once(D->shard_once, [D] {
+        std::vector<uint32_t> shards(65536);
+        std::iota(shards.begin(), shards.end(), 0u);
+        std::vector<uint8_t> kb, bad(65536, 0);
+        std::vector<uint64_t> koff;
+        shard_keys(kb, koff, shards);
+        if (hipMalloc(&D->shard_kb, kb.size()) != hipSuccess || hipMalloc(&D->shard_koff, koff.size() * 8) != hipSuccess ||
+            hipMalloc(&D->shard_bad, bad.size()) != hipSuccess ||
+            hipMemcpy(D->shard_kb, kb.data(), kb.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(D->shard_koff, koff.data(), koff.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(D->shard_bad, bad.data(), bad.size(), hipMemcpyHostToDevice) != hipSuccess)
+            D->shard_rc = KRK_ENOMEM;
+    });
+    KRK_CHECK(D->shard_rc == KRK_OK, D->shard_rc, "shard key table allocation failed");
     int32_t* d_tl = nullptr;
     uint8_t* d_tc = nullptr;
-    int r = hrw_table(D, kb, koff, bad, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, s);
+    int r = hrw_table_dev(D, D->shard_kb, D->shard_koff, D->shard_bad, 65536, nodes, healthy, max_replica, row_out,
+                          &d_tl, &d_tc, s);
     if (!r) {
         hipError_t e = timed(K_GATHER, s, [&] {
             return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
@@ -1611,6 +1640,19 @@ int krk_dev_alloc(uint64_t bytes, void** out) {
 }
 int krk_dev_free(void* p) {
     KRK_HIP(hipFree(p));
+    return KRK_OK;
+}
+int krk_host_alloc(uint64_t bytes, void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    KRK_CHECK(e == hipSuccess, KRK_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
+              hipGetErrorString(e));
+    return KRK_OK;
+}
+int krk_host_free(void* p) {
+    KRK_HIP(hipHostFree(p));
     return KRK_OK;
 }
 int krk_memcpy_h2d(void* dst, const void* src, uint64_t n) {

@@ -46,6 +46,32 @@ class DeviceBuffer:
             check(lib.krk_memcpy_h2d(self.ptr + offset, a.ctypes.data, a.nbytes))
 
 
+class PinnedArray:
+    """A numpy view of library-allocated pinned host memory (krk_host_alloc):
+    device results land here at PCIe rate instead of through a pageable bounce."""
+
+    def __init__(self, shape, dtype):
+        self.array_nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = C.c_void_p()
+        check(lib.krk_host_alloc(max(self.array_nbytes, 1), C.byref(p)))
+        self.ptr = p.value
+        buf = (C.c_uint8 * max(self.array_nbytes, 1)).from_address(self.ptr)
+        self.a = np.frombuffer(buf, dtype=np.uint8, count=self.array_nbytes).view(dtype).reshape(shape)
+
+    def fill_from(self, dev: "DeviceBuffer", offset: int = 0):
+        if self.array_nbytes:
+            check(lib.krk_memcpy_d2h(self.ptr, dev.ptr + offset, self.array_nbytes))
+        return self.a
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib.krk_host_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
 def device_count() -> int:
     n = C.c_int()
     check(lib.krk_device_count(C.byref(n)))
@@ -206,8 +232,10 @@ def nodes_struct(labels, weights):
 
 
 def ring_locations_dev(digests_dev: DeviceBuffer, n: int, labels, healthy, max_replica: int,
-                       locs_dev: DeviceBuffer, counts_dev: DeviceBuffer, stream=None):
-    s, keep = nodes_struct(labels, [100] * len(labels))
+                       locs_dev: DeviceBuffer, counts_dev: DeviceBuffer, stream=None, weights=None):
+    """ring.Locations for n device-resident digests; weights default to the ring's 100
+    (lib/hashring/ring.go:28)."""
+    s, keep = nodes_struct(labels, [100] * len(labels) if weights is None else weights)
     h = np.ascontiguousarray(healthy, dtype=np.uint8)
     check(lib.krk_ring_locations_dev(digests_dev.ptr, n, C.byref(s), h.ctypes.data_as(C.POINTER(C.c_uint8)),
                                       max_replica, locs_dev.ptr, counts_dev.ptr, stream))
