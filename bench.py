@@ -223,6 +223,10 @@ def roofline_obj(kernel, gbps, avg_ms, bytes_launch, traffic):
 
 
 def load_traffic(path, workload, n):
+    """Per-launch HBM bytes from the PMC passes: profiles/pmc_traffic.json (C2) or
+    profiles/pmc_traffic_<workload>.json (tools/pmc_traffic.py)."""
+    if workload != "c2" and os.path.basename(path) == "pmc_traffic.json":
+        path = os.path.join(os.path.dirname(path), f"pmc_traffic_{workload}.json")
     try:
         pm = json.load(open(path))
         if pm.get("workload") == workload and pm.get("blobs") == n:
