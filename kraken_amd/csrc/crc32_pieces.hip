@@ -23,6 +23,8 @@
 // Tables live in LDS, replicated R times and interleaved (word (t*256+e)*R + r) so
 // lane l reads replica l % R: with R = 32 the 32 lanes of a ds_read_b32 half-wave
 // hit 32 distinct banks (conflict-free); R = 16 allows at most 2-way.
+#include <mutex>
+
 #include "kernels.hpp"
 #include "crc_math.hpp"
 #include "device_util.hpp"
@@ -283,13 +285,13 @@ template <int R, int RG, int BLOCK, bool COAL>
 static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
                                  int blocks_per_cu, hipStream_t s) {
     constexpr size_t lds = size_t(1024) * (R + RG) * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    if (attr_err != hipSuccess) return attr_err;
     const uint32_t wpb = BLOCK / 64;
     const uint64_t n_items = uint64_t(w.run_items) + w.n_items;
     uint64_t want = (n_items + wpb - 1) / wpb;
