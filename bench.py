@@ -592,7 +592,8 @@ def main():
 
     from kraken_amd import device as D
 
-    D.set_device(local)
+    # one process per GPU; modulo the visible count so a multi-rank rehearsal can share one GPU
+    D.set_device(local % max(1, D.device_count()))
     T = Timer(D, dist)
     res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
     kind = WORKLOADS[a.workload]["kind"]
