@@ -48,14 +48,49 @@ struct Tab {
     }
 };
 
+// Byte-addressable table layout (variants 7, 8): entry e of slicing table k,
+// replica r = lane % RP, at LDS byte e*256 + (k % TPR)*RP*4 + r*4 + (k / TPR)*65536,
+// TPR = 64 / RP tables per 256-byte row.  A lookup address is then ONE v_perm_b32
+// (byte e -> bits 8-15, the lane's replica offset -> bits 0-7, the region bit from
+// the selector) and the table's place in the row rides in the ds_read offset field,
+// instead of extract + shift + add.  RP = 32 (128 KiB): bank = (address / 4) mod 32
+// = r, the 32 lanes of a ds_read_b32 half-wave never conflict.  RP = 16 (64 KiB):
+// lanes l and l + 16 share a bank (2-way), but two workgroups fit a CU.
+typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
+
+template <int RP>
+struct TabP {
+    static constexpr int TPR = 64 / RP;
+    uint32_t loff;  // (1 << 16) | (lane % RP) * 4: byte 0 = replica offset, byte 2 = region 1
+    // The tables start at LDS byte 0 (the kernel's only LDS is its dynamic array; checked
+    // at kernel start), so the perm result is the ds_read address as it stands.
+    __device__ __forceinline__ uint32_t at(uint32_t a, int off) const { return *(lds_u32p)(size_t)(a + off); }
+    // byte0 <- loff.byte0, byte1 <- x.byte J, byte2 <- REGION ? loff.byte2 : 0, byte3 <- 0
+    template <int J, int REGION>
+    __device__ __forceinline__ uint32_t addr(uint32_t x) const {
+        constexpr uint32_t sel = 0x0C000000u | ((REGION ? 0x02u : 0x0Cu) << 16) | ((4u + J) << 8);
+        return __builtin_amdgcn_perm(x, loff, sel);
+    }
+    // table k looked up with byte J of x
+    template <int J, int K>
+    __device__ __forceinline__ uint32_t t(uint32_t x) const {
+        return at(addr<J, (K / TPR)>(x), (K % TPR) * RP * 4);
+    }
+    // T3[byte 0] ^ T2[byte 1] ^ T1[byte 2] ^ T0[byte 3]
+    __device__ __forceinline__ uint32_t word(uint32_t c) const {
+        return xor3(t<0, 3>(c), t<1, 2>(c), t<2, 1>(c)) ^ t<3, 0>(c);
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t c, uint32_t b) const { return t<0, 0>(c ^ b) ^ (c >> 8); }
+};
+
 template <int RG>
 __device__ __forceinline__ uint32_t gap_shift(uint32_t c, const uint32_t* G) {
     return xor3(G[(0 * 256 + (c & 0xFF)) * RG], G[(1 * 256 + ((c >> 8) & 0xFF)) * RG],
                 G[(2 * 256 + ((c >> 16) & 0xFF)) * RG]) ^ G[(3 * 256 + (c >> 24)) * RG];
 }
 
-template <int R>
-__device__ __forceinline__ uint32_t seg16(uint32_t c, const u32x4& v, const Tab<R>& T) {
+template <class TT>
+__device__ __forceinline__ uint32_t seg16(uint32_t c, const u32x4& v, const TT& T) {
     c = T.word(c ^ v.x);
     c = T.word(c ^ v.y);
     c = T.word(c ^ v.z);
@@ -64,8 +99,8 @@ __device__ __forceinline__ uint32_t seg16(uint32_t c, const u32x4& v, const Tab<
 }
 
 // Up to 4 little-endian words holding n valid bytes (n <= 16) into register c.
-template <int R, int NW>
-__device__ __forceinline__ uint32_t feed_words(uint32_t c, const uint32_t* w, uint32_t n, const Tab<R>& T) {
+template <class TT, int NW>
+__device__ __forceinline__ uint32_t feed_words(uint32_t c, const uint32_t* w, uint32_t n, const TT& T) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
         const int keep = (int)n - 4 * j;
@@ -80,9 +115,12 @@ __device__ __forceinline__ uint32_t feed_words(uint32_t c, const uint32_t* w, ui
 
 // ------------------------------------------------------------ strided layout
 // One wave step for this lane: skip the 4032-byte gap, then its 64 own bytes.
-template <int R, int RG>
+template <class TT, int RG, bool LOADONLY = false>
 __device__ __forceinline__ uint32_t step64(uint32_t c, const u32x4& v0, const u32x4& v1, const u32x4& v2,
-                                           const u32x4& v3, const Tab<R>& T, const uint32_t* G) {
+                                           const u32x4& v3, const TT& T, const uint32_t* G) {
+    if (LOADONLY)  // timing diagnostic (variant 4): the loads without the table work
+        return c ^ xor3(v0.x ^ v0.y ^ v0.z ^ v0.w, v1.x ^ v1.y ^ v1.z ^ v1.w, v2.x ^ v2.y ^ v2.z ^ v2.w) ^ v3.x ^
+               v3.y ^ v3.z ^ v3.w;
     c = gap_shift<RG>(c, G);
     c = seg16(c, v0, T);
     c = seg16(c, v1, T);
@@ -91,8 +129,8 @@ __device__ __forceinline__ uint32_t step64(uint32_t c, const u32x4& v0, const u3
 }
 
 // This lane's share of bytes [base, base+len), shifted to the item end.
-template <int R, int RG>
-__device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const Tab<R>& T,
+template <class TT, int RG, bool LOADONLY = false>
+__device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                      const uint32_t* G, uint32_t lane_mul,
                                                      const uint32_t* x8pow) {
     uint32_t c = 0;
@@ -110,14 +148,14 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
             for (; s + 2 <= nfull; s += 2) {
                 gptr<u32x4> q = p + (s + 1) * S;
                 b0 = q[0]; b1 = q[1]; b2 = q[2]; b3 = q[3];
-                c = step64<R, RG>(c, a0, a1, a2, a3, T, G);
+                c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
                 if (s + 2 < nfull) {
                     q = p + (s + 2) * S;
                     a0 = q[0]; a1 = q[1]; a2 = q[2]; a3 = q[3];
                 }
-                c = step64<R, RG>(c, b0, b1, b2, b3, T, G);
+                c = step64<TT, RG, LOADONLY>(c, b0, b1, b2, b3, T, G);
             }
-            if (s < nfull) c = step64<R, RG>(c, a0, a1, a2, a3, T, G);
+            if (s < nfull) c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
             end = (nfull - 1) * kStep + (lane + 1) * kSeg;
         }
         const uint32_t ts = nfull * kStep + lane * kSeg;
@@ -125,7 +163,7 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
             const uint32_t nb = min(kSeg, len - ts);
             uint32_t w[16];
             load_bytes64(base + ts, nb, w);
-            c = feed_words<R, 16>(gap_shift<RG>(c, G), w, nb, T);
+            c = feed_words<TT, 16>(gap_shift<RG>(c, G), w, nb, T);
             end = ts + nb;
         }
     } else {
@@ -138,7 +176,7 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
                 const uint32_t nb = min(kSeg, len - ss);
                 uint32_t w[16];
                 load_bytes64(base + ss, nb, w);
-                c = feed_words<R, 16>(gap_shift<RG>(c, G), w, nb, T);
+                c = feed_words<TT, 16>(gap_shift<RG>(c, G), w, nb, T);
                 end = ss + nb;
             }
         }
@@ -150,14 +188,14 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
 }
 
 // ---------------------------------------------------------- coalesced layout
-template <int R, int RG>
-__device__ __forceinline__ void step_coal(uint32_t c[4], const u32x4 v[4], const Tab<R>& T, const uint32_t* G) {
+template <class TT, int RG>
+__device__ __forceinline__ void step_coal(uint32_t c[4], const u32x4 v[4], const TT& T, const uint32_t* G) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) c[k] = seg16(gap_shift<RG>(c[k], G), v[k], T);
 }
 
-template <int R, int RG>
-__device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, uint32_t lane, const Tab<R>& T,
+template <class TT, int RG>
+__device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                   const uint32_t* G, const uint32_t lm[4], const uint32_t* x8pow) {
     uint32_t c[4] = {0u, 0u, 0u, 0u};
     uint32_t end[4] = {0u, 0u, 0u, 0u};
@@ -174,15 +212,15 @@ __device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, u
             gptr<u32x4> q = p + (s + 1) * S;
 #pragma unroll
             for (int k = 0; k < 4; ++k) b[k] = q[64 * k];
-            step_coal<R, RG>(c, a, T, G);
+            step_coal<TT, RG>(c, a, T, G);
             if (s + 2 < nfull) {
                 q = p + (s + 2) * S;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) a[k] = q[64 * k];
             }
-            step_coal<R, RG>(c, b, T, G);
+            step_coal<TT, RG>(c, b, T, G);
         }
-        if (s < nfull) step_coal<R, RG>(c, a, T, G);
+        if (s < nfull) step_coal<TT, RG>(c, a, T, G);
 #pragma unroll
         for (int k = 0; k < 4; ++k) end[k] = (nfull - 1) * kStep + 1024 * k + 16 * lane + 16;
         s0 = nfull;
@@ -197,7 +235,7 @@ __device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, u
                 const uint32_t nb = min(16u, len - ss);
                 uint32_t w[4];
                 load_bytes16(base + ss, nb, w);
-                c[k] = feed_words<R, 4>(gap_shift<RG>(c[k], G), w, nb, T);
+                c[k] = feed_words<TT, 4>(gap_shift<RG>(c[k], G), w, nb, T);
                 end[k] = ss + nb;
             }
         }
@@ -241,36 +279,15 @@ __device__ __forceinline__ ItemRef fetch_item(const CrcWork& w, uint32_t it) {
             jj == 0 ? w.consts[r.cpat + r.ipp] : 0u};
 }
 
-template <int R, int RG, int BLOCK, bool COAL>
-__global__ void __launch_bounds__(BLOCK)
-crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr int TW = 1024 * R;
-    constexpr int GW = 1024 * RG;
-    constexpr int GT = COAL ? kTabGC : kTabG;
-    for (int i = threadIdx.x; i < TW; i += BLOCK) lds[i] = tabs[kTabT + i / R];
-    for (int i = threadIdx.x; i < GW; i += BLOCK) lds[TW + i] = tabs[GT + i / RG];
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63;
-    Tab<R> T;
-    T.lo = lds + (lane % R);
-    T.hi = lds + 2 * 256 * R + (lane % R);
-    const uint32_t* G = lds + TW + (lane % RG);
-    const uint32_t* x8pow = tabs + kTabX8Pow;
-    uint32_t lm[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lm[k] = COAL ? tabs[kTabLaneMulC + 64 * k + lane] : tabs[kTabLaneMul + lane];
-
-    constexpr uint32_t WPB = BLOCK / 64;
-    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + threadIdx.x / 64);
-    const uint32_t n_waves = gridDim.x * WPB;
+template <class TT, int RG, bool COAL, bool LOADONLY>
+__device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const uint32_t* G, const uint32_t lm[4],
+                                          const uint32_t* x8pow, uint32_t lane, uint32_t wave0, uint32_t n_waves,
+                                          uint32_t* sums) {
     const uint32_t n_items = w.run_items + w.n_items;
-
     for (uint32_t it = wave0; it < n_items; it += n_waves) {
         const ItemRef ci = fetch_item(w, it);
-        uint32_t c = COAL ? lane_crc_coal<R, RG>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
-                          : lane_crc_strided<R, RG>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
+        uint32_t c = COAL ? lane_crc_coal<TT, RG>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
+                          : lane_crc_strided<TT, RG, LOADONLY>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
         // Wave XOR-reduction.
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c ^= __shfl_xor(c, off, 64);
@@ -281,14 +298,55 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
     }
 }
 
-template <int R, int RG, int BLOCK, bool COAL>
+template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0>
+__global__ void __launch_bounds__(BLOCK)
+crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr int TW = 1024 * (PERM ? PERM : R);
+    constexpr int GW = 1024 * RG;
+    constexpr int GT = COAL ? kTabGC : kTabG;
+    if constexpr (PERM != 0) {
+        for (int i = threadIdx.x; i < TW; i += BLOCK) {  // 16384 words (64 KiB) per region
+            const int region = i >> 14, e = (i & 16383) >> 6, kk = (i & 63) / PERM;
+            lds[i] = tabs[kTabT + (region * (64 / PERM) + kk) * 256 + e];
+        }
+    } else {
+        for (int i = threadIdx.x; i < TW; i += BLOCK) lds[i] = tabs[kTabT + i / R];
+    }
+    for (int i = threadIdx.x; i < GW; i += BLOCK) lds[TW + i] = tabs[GT + i / RG];
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t* G = lds + TW + (lane % RG);
+    const uint32_t* x8pow = tabs + kTabX8Pow;
+    uint32_t lm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lm[k] = COAL ? tabs[kTabLaneMulC + 64 * k + lane] : tabs[kTabLaneMul + lane];
+
+    constexpr uint32_t WPB = BLOCK / 64;
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WPB + threadIdx.x / 64);
+    const uint32_t n_waves = gridDim.x * WPB;
+    if constexpr (PERM != 0) {
+        if ((uint32_t)(size_t)(lds_u32p)lds != 0) __builtin_trap();
+        TabP<PERM> T;
+        T.loff = (1u << 16) | ((lane % PERM) << 2);
+        item_loop<TabP<PERM>, RG, COAL, LOADONLY>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+    } else {
+        Tab<R> T;
+        T.lo = lds + (lane % R);
+        T.hi = lds + 2 * 256 * R + (lane % R);
+        item_loop<Tab<R>, RG, COAL, LOADONLY>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+    }
+}
+
+template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0>
 static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
                                  int blocks_per_cu, hipStream_t s) {
-    constexpr size_t lds = size_t(1024) * (R + RG) * 4;
+    constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4;
     static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL>),
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (attr_err != hipSuccess) return attr_err;
@@ -298,7 +356,7 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
     uint64_t cap = uint64_t(cus) * blocks_per_cu;
     uint32_t grid = (uint32_t)(want < cap ? want : cap);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
+    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
     return hipGetLastError();
 }
 
@@ -312,6 +370,16 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
             return launch_variant<16, 4, 512, true>(w, tabs, sums, cfg.cus, 2, s);
         case 3:  // coalesced, 144 KiB LDS: one 1024-thread block per CU
             return launch_variant<32, 4, 1024, true>(w, tabs, sums, cfg.cus, 1, s);
+        case 4:  // timing diagnostic: variant 0's loads and occupancy without the lookups (wrong sums)
+            return launch_variant<16, 4, 512, false, true>(w, tabs, sums, cfg.cus, 2, s);
+        case 5:  // strided, 80 KiB LDS per 1024-thread block, two per CU: 32 waves/CU
+            return launch_variant<16, 4, 1024, false>(w, tabs, sums, cfg.cus, 2, s);
+        case 6:  // strided, R8 tables (40 KiB), four 512-thread blocks per CU: 32 waves/CU
+            return launch_variant<8, 2, 512, false>(w, tabs, sums, cfg.cus, 4, s);
+        case 7:  // strided, byte-addressable tables (v_perm addresses, 144 KiB), one 1024-thread block per CU
+            return launch_variant<32, 4, 1024, false, false, 32>(w, tabs, sums, cfg.cus, 1, s);
+        case 8:  // as 7 with 16 replicas (80 KiB): two 1024-thread blocks per CU
+            return launch_variant<16, 4, 1024, false, false, 16>(w, tabs, sums, cfg.cus, 2, s);
         default:  // strided, 80 KiB LDS: two 512-thread blocks per CU
             return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
     }

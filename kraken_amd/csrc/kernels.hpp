@@ -70,7 +70,7 @@ struct CrcWork {
 
 struct CrcLaunchCfg {
     int cus;           // compute units
-    int variant;       // 0 = R16 (2 blocks/CU), 1 = R32 (1 block/CU); 2/3 = the same, coalesced 4-chain layout
+    int variant;       // crc32_pieces.hip launch_crc_items; default 7 (byte-addressable tables)
 };
 
 hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, const CrcLaunchCfg& cfg,

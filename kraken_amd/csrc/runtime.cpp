@@ -233,7 +233,7 @@ static int init_device(Device& D, int id) {
     KRK_HIP(hipMalloc(&D.d_tabs, kTabWords * 4));
     KRK_HIP(hipMemcpy(D.d_tabs, tabs.data(), kTabWords * 4, hipMemcpyHostToDevice));
     const char* v = getenv("KRK_CRC_VARIANT");
-    D.crc_variant = v ? atoi(v) : 0;
+    D.crc_variant = v ? atoi(v) : 7;  // byte-addressable tables (crc32_pieces.hip)
     return KRK_OK;
 }
 
