@@ -20,9 +20,12 @@
 // to the piece end and atomically XORs into sums[piece].  XOR is order-free, so
 // the items of one piece may run on any wave, XCD or launch.
 //
-// Tables live in LDS, replicated R times and interleaved (word (t*256+e)*R + r) so
-// lane l reads replica l % R: with R = 32 the 32 lanes of a ds_read_b32 half-wave
-// hit 32 distinct banks (conflict-free); R = 16 allows at most 2-way.
+// Tables live in LDS, replicated so that the lanes of a ds_read_b32 half-wave hit
+// distinct banks.  Default (variant 7): the byte-addressable layout of TabP, where a
+// lookup address is one v_perm_b32.  Variants 0-6: replicated R times and interleaved
+// (word (t*256+e)*R + r, lane l reads replica l % R: R = 32 conflict-free, R = 16 at
+// most 2-way), addresses formed by extract + shift + add.  DESIGN.md §4.1 has the
+// measurements of every variant.
 #include <mutex>
 
 #include "kernels.hpp"
