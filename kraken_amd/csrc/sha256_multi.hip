@@ -153,13 +153,26 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
 // 4 slots) or kSlots2 slots (two lanes per stream, where each producer step
 // builds two blocks), see produce_step.
 constexpr int kSlots = 4;
-constexpr int kSlots2 = 6;
+constexpr int kSlots2 = 6;           // two lanes: block positions in the ring ...
+constexpr int kRing2 = kSlots2 / 2;  // ... in 3 slots, two blocks per slot (A / E columns)
 constexpr int kSlotWords = 64 * 64;  // 64 rounds x 64 lanes
 
 // LDS image of one slot: [round/4][lane][4] words -> a lane's 4 consecutive KW
 // are one conflict-free ds_read_b128 / ds_write_b128 across the wave.
 __device__ __forceinline__ uint32_t kw_index(int slot, int quad, uint32_t lane) {
     return (uint32_t)slot * kSlotWords + ((uint32_t)quad * 64 + lane) * 4;
+}
+// Word offset of quad 0 of one column of a slot; quad q is 256 words further.
+__device__ __forceinline__ uint32_t kw_base(uint32_t slot, uint32_t col) { return slot * kSlotWords + col * 4; }
+
+// Two lanes per stream: block b lives in slot (b / 2) % kRing2, the even block in
+// the A lanes' columns and the odd block in the E lanes' (each producer lane writes
+// its own column).  Every consumer lane reads column lane ^ 15 for even blocks
+// (the E lanes their partner's, the A lanes the all-1 slot's) and its own column
+// for odd blocks: a bijection within each 16-lane row, so the ds_read_b128 stays
+// conflict-free.  3 slots + the all-1 slot = 64 KiB: two workgroups fit a CU.
+__device__ __forceinline__ uint32_t kw2_base(uint32_t b, bool is_e, uint32_t lane) {
+    return kw_base(is_e ? (b >> 1) % kRing2 : kRing2, (b & 1) ? lane : (lane ^ 15u));
 }
 
 __device__ __forceinline__ uint32_t job_blocks(const ShaJob& job) {
@@ -204,7 +217,7 @@ __device__ __forceinline__ void fetch(const ShaJob& job, uint32_t b, u32x4 raw[k
 // bit length on the final blocks), expanded to KW[r] = W[r] + K[r] in ring slot b % kNs,
 // LDS column `lane`.
 template <int kNs>
-__device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4 rawc[kRaw], uint32_t lane,
+__device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4 rawc[kRaw], uint32_t base,
                                       uint32_t* lds) {
     constexpr uint32_t K[64] = {KRK_K256};
     const uint32_t n = block_bytes(job, b);
@@ -246,7 +259,6 @@ __device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4
             w[15] = (uint32_t)bits;
         }
     }
-    const uint32_t slot = b % kNs;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         uint32_t kw[4];
@@ -265,7 +277,7 @@ __device__ __forceinline__ void build(const ShaJob& job, uint32_t b, const u32x4
             }
             kw[t] = wi + K[i];
         }
-        *reinterpret_cast<u32x4*>(lds + kw_index(slot, q, lane)) = u32x4{kw[0], kw[1], kw[2], kw[3]};
+        *reinterpret_cast<u32x4*>(lds + base + 256 * q) = u32x4{kw[0], kw[1], kw[2], kw[3]};
     }
 }
 
@@ -298,7 +310,9 @@ __device__ __forceinline__ void produce_step(const ShaJob& job, uint32_t b, uint
     } else {
         fetch(job, ob + 2 * kStep, next, safe);
     }
-    if (act) build<kNs>(job, ob, use, col, lds);
+    // one lane per stream: block ob in slot ob % kNs; two: slot (ob / 2) % kRing2
+    const uint32_t base = kStep == 2 ? kw_base((ob >> 1) % (kNs / 2), col) : kw_base(ob % kNs, col);
+    if (act) build<kNs>(job, ob, use, base, lds);
 }
 
 // Four SHA-256 rounds as one fixed 56-instruction sequence.  The compiler's
@@ -447,7 +461,7 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 // (quad q+1's first W feeds quad q's last z, so a read issued one quad before its
 // use would stall: ~230 cycles a block), and quads 0..2 of the next block (slot
 // ncslot) are read into k[] during the last quads.
-__device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int cslot, int ncslot,
+__device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
                                         uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[3]) {
     // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
     // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
@@ -459,9 +473,9 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int 
     wq[1] = k[1];
     wq[2] = k[2];
 #ifdef KRK_SHA_NOLDS  // diagnostic: W from registers (wrong digests) -- prices the LDS reads
-    wq[3] = u32x4{3u, lane, (uint32_t)cslot, 7u};
+    wq[3] = u32x4{3u, lane, cbase, 7u};
 #else
-    wq[3] = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, 3, lane));
+    wq[3] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * 3);
 #endif
     {
         uint32_t t1, t2, t3, kk, p;
@@ -491,15 +505,15 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, int 
     for (int q = 1; q < 16; ++q) {
         if (q + 3 < 16) {
 #ifdef KRK_SHA_NOLDS
-            wq[(q + 3) & 3] = u32x4{(uint32_t)q, lane, (uint32_t)cslot, 7u};
+            wq[(q + 3) & 3] = u32x4{(uint32_t)q, lane, cbase, 7u};
 #else
-            wq[(q + 3) & 3] = *reinterpret_cast<const u32x4*>(lds + kw_index(cslot, q + 3, lane));
+            wq[(q + 3) & 3] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + 3));
 #endif
         }
         // The next block's first three quads, read unconditionally (a slot is always
         // mapped LDS; past the last block the values go unused) so that no branch
         // sinks them to the end of the block, where their latency would be exposed.
-        if (q >= 13) k[q - 13] = *reinterpret_cast<const u32x4*>(lds + kw_index(ncslot, q - 13, lane));
+        if (q >= 13) k[q - 13] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - 13));
         const u32x4& cur = wq[q & 3];
         sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) & 3][0] : c.one_a);
     }
@@ -564,18 +578,18 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     if (producer && kTiming == 1) return;
     if (!producer && kTiming >= 2) return;
     if (producer) {
-        // Two lanes per stream: the A lanes read W from the extra slot kNs, all 1s
+        // Two lanes per stream: the A lanes read W from the extra slot kRing2, all 1s
         // (rounds2).
         if (kTwo) {
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                *reinterpret_cast<u32x4*>(ring + kw_index(kNs, q, lane)) = u32x4{1u, 1u, 1u, 1u};
+                *reinterpret_cast<u32x4*>(ring + kw_index(kRing2, q, lane)) = u32x4{1u, 1u, 1u, 1u};
         }
         // Loads are issued two steps ahead into a 3-deep register rotation (R0, R1, R2).
         u32x4 R0[kRaw], R1[kRaw], R2[kRaw];
         const uint64_t safe = reinterpret_cast<uint64_t>(jobs);
         const uint32_t par = kTwo && two_lane_is_e(lane) ? 1u : 0u;  // E lanes: odd blocks
-        const uint32_t col = kTwo && !par ? (lane ^ 15u) : lane;      // the E lane's column
+        const uint32_t col = lane;                                    // each lane writes its own column
         uint32_t passed = 0;
         fetch(job, par, R0, safe);
         fetch(job, par + kStep, R1, safe);
@@ -619,7 +633,8 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             asm volatile("" ::: "memory");
             if (i == 0) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q) kq[q] = kw_quad(ring, is_e ? 0 : kNs, q, lane);
+                for (int q = 0; q < 3; ++q)
+                    kq[q] = *reinterpret_cast<const u32x4*>(ring + kw2_base(0, is_e, lane) + 256 * q);
             }
             uint32_t x[4];
 #pragma unroll
@@ -627,7 +642,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb1 = __builtin_amdgcn_s_memtime();
 #endif
-            rounds2(x, ring, is_e ? (int)(i % kNs) : kNs, is_e ? (int)((i + 1) % kNs) : kNs, lane, c, is_e, kq);
+            rounds2(x, ring, kw2_base(i, is_e, lane), kw2_base(i + 1, is_e, lane), lane, c, is_e, kq);
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb2 = __builtin_amdgcn_s_memtime();
             cyc_bar += cb1 - cb0;
@@ -732,9 +747,11 @@ static int sha_variant() {
     return e ? atoi(e) : -1;
 }
 
-// Streams up to which two lanes per stream win: one two-lane workgroup per CU.
-// Measured (tools/probe_perf.py): 4,096 streams 190 GB/s two-lane vs 147 one-lane;
-// 16,384 streams 448 vs 586 (two-lane workgroups then share SIMDs).
+// Streams up to which two lanes per stream win: two two-lane workgroups (64 KiB of
+// LDS each) per CU.  Measured (tools/probe_perf.py, profiles/r01/sha_compact_ring.jsonl):
+// 8,192 streams 47.9 MB/s a stream two-lane vs 35.9 one-lane; 16,384 streams 37.3 vs
+// 35.5 (two workgroups then share a CU's SIMDs).  Beyond that the two-lane grid would
+// run in waves of workgroups.
 static uint32_t two_lane_max_streams() {
     static uint32_t n = [] {
         const char* e = getenv("KRK_SHA_TWO_LANE_MAX");
@@ -744,7 +761,7 @@ static uint32_t two_lane_max_streams() {
             hipDeviceProp_t p;
             if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
         }
-        return (uint32_t)cus * 32u;
+        return (uint32_t)cus * 64u;
     }();
     return n;
 }
@@ -763,7 +780,7 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
     if (v >= 1 && v <= 7) {
         // 1/3: production (one/two lanes); 2/4: consumer only; 5/6: producer only
         const bool two = v == 3 || v == 4 || v >= 6;
-        const size_t lds = size_t(two ? kSlots2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB; 112 KiB (6 slots + all-1)
+        const size_t lds = size_t(two ? kRing2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB either way
         auto* k = v == 1 ? &sha256_ws_kernel<0, false>
                 : v == 2 ? &sha256_ws_kernel<1, false>
                 : v == 3 ? &sha256_ws_kernel<0, true>
