@@ -397,28 +397,27 @@ def run_chunked(a, D, T, rank, world, res):
     D.check(D.lib.krk_stream_create(C.byref(gen_s)))
     D.check(D.lib.krk_stream_create(C.byref(run_s)))
 
-    wins, pos, live = [], [0] * n, list(range(n))
-    while live:  # every live blob advances by the same 64-multiple chunk per window
-        c = max(64, (W // len(live)) // 64 * 64)
-        w, nxt = [], []
-        for i in live:
-            take = min(c, lens[i] - pos[i])
-            w.append((i, pos[i], take))
-            pos[i] += take
-            if pos[i] < lens[i]:
-                nxt.append(i)
-        wins.append(w)
-        live = nxt
+    # Window plan: every live blob advances by the same 64-multiple chunk per window.
+    L = np.asarray(lens, dtype=np.uint64)
+    ids_a = np.asarray(ids, dtype=np.uint64)
+    wins, pos, live = [], np.zeros(n, dtype=np.uint64), np.arange(n)
+    while live.size:
+        c = max(64, (W // live.size) // 64 * 64)
+        take = np.minimum(np.uint64(c), L[live] - pos[live])
+        wins.append((live, pos[live].copy(), take))
+        pos[live] += take
+        live = live[pos[live] < L[live]]
 
     def items_of(k):
-        buf, out, off = bufs[k & 1], [], 0
-        for (i, o, ln) in wins[k]:
-            out.append((i, buf.ptr + off, o, ln))
-            off += (ln + 15) // 16 * 16
-        return out
+        blobs, offs, take = wins[k]
+        dev = np.zeros(take.size, dtype=np.uint64)  # 16-byte aligned chunk addresses in the window
+        dev[1:] = np.cumsum((take + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]
+        dev += np.uint64(bufs[k & 1].ptr)
+        return blobs, dev, offs, take
 
     def gen(items):
-        D.synth_fill_chunks([(ids[i], p, o, ln) for (i, p, o, ln) in items], stream=gen_s)
+        blobs, dev, offs, take = items
+        D.synth_fill_chunk_arrays(ids_a[blobs], dev, offs, take, stream=gen_s)
         D.check(D.lib.krk_stream_sync(gen_s))
 
     T.barrier()
@@ -428,7 +427,7 @@ def run_chunked(a, D, T, rank, world, res):
         gen(cur)
         for k in range(len(wins)):
             D.check(D.lib.krk_stream_sync(run_s))  # window k-1 done: its buffer may be refilled
-            cb.step(cur, stream=run_s)
+            cb.step_arrays(cur[0], cur[1], cur[2], cur[3], stream=run_s)
             if k + 1 < len(wins):
                 cur = items_of(k + 1)
                 gen(cur)

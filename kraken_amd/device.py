@@ -201,6 +201,13 @@ class ChunkedBatch:
         self.sums.zero()
         self.digests = DeviceBuffer(max(n, 1) * 32)
 
+    def step_arrays(self, blob_idx, ptrs, offsets, lengths, stream=None):
+        """step() from numpy arrays (one window of thousands of chunks, no Python loop)."""
+        arr = chunk_array(ptrs, offsets, lengths, self.lengths[blob_idx], self.piece_lengths[blob_idx],
+                          self.sums_off[blob_idx], blob_idx)
+        check(lib.krk_metainfo_digest_chunks_dev(arr.ctypes.data_as(C.POINTER(krk_chunk)), len(arr), self.state.ptr,
+                                                 self.sums.ptr, self.digests.ptr, stream))
+
     def step(self, items, stream=None):
         """items: [(blob index, device address of the chunk, offset, length)]."""
         arr = (krk_chunk * max(len(items), 1))()
@@ -209,6 +216,28 @@ class ChunkedBatch:
                                int(self.sums_off[i]), int(i))
         check(lib.krk_metainfo_digest_chunks_dev(arr, len(items), self.state.ptr, self.sums.ptr,
                                                  self.digests.ptr, stream))
+
+
+KRK_CHUNK_DTYPE = np.dtype([("data", "<u8"), ("offset", "<u8"), ("length", "<u8"), ("blob_length", "<u8"),
+                            ("piece_length", "<i8"), ("sums_offset", "<u8"), ("blob", "<u8")])
+assert KRK_CHUNK_DTYPE.itemsize == C.sizeof(krk_chunk)
+
+
+def chunk_array(ptrs, offsets, lengths, blob_lengths, piece_lengths, sums_offsets, blobs) -> np.ndarray:
+    """A krk_chunk[] built column-wise with numpy."""
+    n = len(ptrs)
+    arr = np.zeros(max(n, 1), dtype=KRK_CHUNK_DTYPE)[:n]
+    arr["data"], arr["offset"], arr["length"] = ptrs, offsets, lengths
+    arr["blob_length"], arr["piece_length"] = blob_lengths, piece_lengths
+    arr["sums_offset"], arr["blob"] = sums_offsets, blobs
+    return arr
+
+
+def synth_fill_chunk_arrays(blob_ids, ptrs, offsets, lengths, variant: int = 0, stream=None):
+    """synth_fill_chunks from numpy arrays."""
+    n = len(ptrs)
+    arr = chunk_array(ptrs, offsets, lengths, 0, 1, 0, blob_ids)
+    check(lib.krk_synth_fill_chunks_dev(arr.ctypes.data_as(C.POINTER(krk_chunk)), n, variant, stream))
 
 
 def synth_fill_chunks(items, variant: int = 0, stream=None):
