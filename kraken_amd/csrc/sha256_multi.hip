@@ -555,22 +555,40 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // step (even and odd), so the producer's 64 lanes all do distinct work: built one
 // block a step, it (47.6 MB/s a stream) could not keep up with the two-lane
 // consumer (50 MB/s a stream).
-template <int kTiming, bool kTwo>
-__global__ void __launch_bounds__(128)
+//
+// kGroups = 2: two producer/consumer pairs in one 4-wave workgroup, each with its own
+// ring (128 KiB): the hardware puts the four waves of a workgroup on the four SIMDs
+// of one CU, where two 2-wave workgroups sharing a CU also share SIMDs (47.9 vs 37.3
+// MB/s a stream with two lanes).  The pairs share the workgroup barrier, so both run
+// the workgroup's largest block count (jobs arrive sorted by length).
+template <int kTiming, bool kTwo, int kGroups = 1>
+__global__ void __launch_bounds__(128 * kGroups)
 sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __restrict__ out_digest,
                  uint32_t* __restrict__ out_state) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t ring[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t ring_all[];
     constexpr int kNs = kTwo ? kSlots2 : kSlots;
     constexpr int kStep = kTwo ? 2 : 1;
+    constexpr uint32_t kPer = kTwo ? 32u : 64u;  // streams per producer/consumer pair
+    constexpr uint32_t kRingWords = uint32_t(kTwo ? kRing2 + 1 : kSlots) * kSlotWords;
     const uint32_t lane = threadIdx.x & 63;
-    const bool producer = threadIdx.x < 64;
-    const uint32_t j = kTwo ? blockIdx.x * 32 + two_lane_stream(lane) : blockIdx.x * 64 + lane;
+    const uint32_t wave = threadIdx.x >> 6;
+    const bool producer = wave < (uint32_t)kGroups;
+    const uint32_t grp = wave % kGroups;
+    uint32_t* ring = ring_all + grp * kRingWords;
+    const uint32_t sbase = blockIdx.x * kPer * kGroups;
+    const uint32_t me = kTwo ? two_lane_stream(lane) : lane;
+    const uint32_t j = sbase + grp * kPer + me;
     const bool live = j < n_jobs;
     ShaJob job{};
     if (live) job = jobs[j];
     const uint32_t mine = live ? job_blocks(job) : 0u;
-    // wave-uniform block count (both waves see the same 64 jobs)
-    uint32_t nb = mine;
+    // workgroup-uniform block count (every wave passes the same barriers)
+    uint32_t nb = 0;
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const uint32_t jj = sbase + g * kPer + me;
+        if (jj < n_jobs) nb = max(nb, g == (int)grp ? mine : job_blocks(jobs[jj]));
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off, 64));
     nb = __builtin_amdgcn_readfirstlane(nb);
@@ -739,7 +757,8 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
 // 3 = wave-specialised, two lanes per stream; 4 = its timing diagnostic;
 // 5/6 = producer-only timing diagnostics (one/two lanes); 7 = producer-only with
 // no global loads (two lanes).
-// Default (-1): two lanes while the batch leaves SIMDs idle, else one.
+// 8/9 = 1/3 with two producer/consumer pairs per workgroup.
+// Default (-1): auto_variant (two lanes while the batch leaves SIMDs idle, else one).
 // Read at every launch (a getenv is cheap next to any SHA launch), so tests can
 // cover each variant in one process.
 static int sha_variant() {
@@ -752,46 +771,66 @@ static int sha_variant() {
 // 8,192 streams 47.9 MB/s a stream two-lane vs 35.9 one-lane; 16,384 streams 37.3 vs
 // 35.5 (two workgroups then share a CU's SIMDs).  Beyond that the two-lane grid would
 // run in waves of workgroups.
-static uint32_t two_lane_max_streams() {
+static uint32_t device_cus() {
     static uint32_t n = [] {
-        const char* e = getenv("KRK_SHA_TWO_LANE_MAX");
-        if (e) return (uint32_t)strtoul(e, nullptr, 10);
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) {
             hipDeviceProp_t p;
             if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
         }
-        return (uint32_t)cus * 64u;
+        return (uint32_t)cus;
+    }();
+    return n;
+}
+static uint32_t two_lane_max_streams() {
+    static uint32_t n = [] {
+        const char* e = getenv("KRK_SHA_TWO_LANE_MAX");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : device_cus() * 64u;
     }();
     return n;
 }
 
+// Automatic plan: two lanes, one pair per workgroup (a workgroup per CU) up to
+// 32 x CUs streams; two lanes, two pairs per workgroup up to 64 x CUs; one lane, two
+// pairs per workgroup beyond.
+static int auto_variant(uint32_t n_jobs) {
+    if (n_jobs <= device_cus() * 32u && n_jobs <= two_lane_max_streams()) return 3;
+    return n_jobs <= two_lane_max_streams() ? 9 : 8;
+}
+
+static bool variant_two_lanes(int v) { return v == 3 || v == 4 || v == 6 || v == 7 || v == 9; }
+
 int sha_lanes_for(uint32_t n_jobs) {
-    const int v = sha_variant();
-    if (v < 0) return n_jobs <= two_lane_max_streams() ? 2 : 1;
-    return (v == 3 || v == 4 || v >= 6) ? 2 : 1;
+    int v = sha_variant();
+    if (v < 0) v = auto_variant(n_jobs);
+    return variant_two_lanes(v) ? 2 : 1;
 }
 
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;
     int v = sha_variant();
-    if (v < 0) v = n_jobs <= two_lane_max_streams() ? 3 : 1;
-    if (v >= 1 && v <= 7) {
-        // 1/3: production (one/two lanes); 2/4: consumer only; 5/6: producer only
-        const bool two = v == 3 || v == 4 || v >= 6;
-        const size_t lds = size_t(two ? kRing2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB either way
+    if (v < 0) v = auto_variant(n_jobs);
+    if (v >= 1 && v <= 9) {
+        // 1/3: production (one/two lanes); 2/4: consumer only; 5/6/7: producer only;
+        // 8/9: production, two producer/consumer pairs per workgroup (one/two lanes)
+        const bool two = variant_two_lanes(v);
+        const int groups = v >= 8 ? 2 : 1;
+        const size_t lds = size_t(groups) * size_t(two ? kRing2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB a pair
         auto* k = v == 1 ? &sha256_ws_kernel<0, false>
                 : v == 2 ? &sha256_ws_kernel<1, false>
                 : v == 3 ? &sha256_ws_kernel<0, true>
                 : v == 4 ? &sha256_ws_kernel<1, true>
                 : v == 5 ? &sha256_ws_kernel<2, false>
                 : v == 6 ? &sha256_ws_kernel<2, true>
-                         : &sha256_ws_kernel<3, true>;
+                : v == 7 ? &sha256_ws_kernel<3, true>
+                : v == 8 ? &sha256_ws_kernel<0, false, 2>
+                         : &sha256_ws_kernel<0, true, 2>;
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-        const uint32_t per = two ? 32u : 64u;
-        hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128), lds, s, jobs, n_jobs, out_digest, out_state);
+        const uint32_t per = (two ? 32u : 64u) * groups;
+        hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * groups), lds, s, jobs, n_jobs, out_digest,
+                           out_state);
     } else {
         hipLaunchKernelGGL(sha256_multi_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, s, jobs, n_jobs, out_digest,
                            out_state);

@@ -306,3 +306,35 @@ def test_regenerate_all_cas_sidecars(gpu, orc, tmp_path):
         ref = orc.calc_piece_sums(b, 65536)[1] if len(b) else None
         got = open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read()
         assert got == _go_json(65536, ref, d.Hex(), len(b))
+
+
+@pytest.mark.parametrize("variant", ["1", "3", "8", "9"])
+def test_sha_launch_plans_bit_exact(gpu, orc, variant, monkeypatch):
+    """Every production SHA-256 plan (one / two lanes per stream; one / two
+    producer-consumer pairs per workgroup) on a batch of mixed lengths and
+    alignments, one-shot and from midstates (chunked), against hashlib."""
+    monkeypatch.setenv("KRK_SHA_VARIANT", variant)
+    rng = np.random.default_rng(int(variant))
+    lens = [int(x) for x in rng.integers(0, 300_000, 300)] + [0, 1, 55, 56, 63, 64, 65, 119, 120, 128]
+    arena = D.BlobArena(lens, 1 << 16, blob_ids=range(900, 900 + len(lens)), misalign=int(variant) % 3)
+    out = D.BatchOutputs(arena)
+    D.sha256(arena, out)
+    D.synchronize()
+    dg = out.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+    for i, L in enumerate(lens):
+        assert bytes(dg[i]) == hashlib.sha256(orc.synth(900 + i, L).tobytes()).digest(), (variant, i, L)
+    # chunked: midstates carried in HBM across three calls
+    cb = D.ChunkedBatch(lens, 1 << 16)
+    pos = [0] * len(lens)
+    for step in range(3):
+        items = []
+        for i, L in enumerate(lens):
+            if pos[i] == L and (L or step):
+                continue  # finished in an earlier call
+            take = L - pos[i] if step == 2 else min(L - pos[i], 64 * int(rng.integers(0, 1500)))
+            items.append((i, arena.buf.ptr + int(arena.offsets[i]) + pos[i], pos[i], take))
+            pos[i] += take
+        cb.step(items)
+    D.synchronize()
+    cdg = cb.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+    assert np.array_equal(cdg, dg), variant
