@@ -594,7 +594,8 @@ static size_t window_bytes() {
 }
 
 // The device's persistent staging windows (grown to at least `cap`) for one host-path
-// call; a concurrent second caller gets private windows instead of waiting.
+// call; a concurrent second caller, or a call wanting windows above 1 GiB, gets
+// private windows (freed when the call returns) instead.
 struct StagingLease {
     Device* D = nullptr;
     Pipeline* p = nullptr;
@@ -607,7 +608,8 @@ struct StagingLease {
 
 static int lease_staging(Device* D, size_t cap, StagingLease& L) {
     L.D = D;
-    if (D->staging_mu.try_lock()) {
+    constexpr size_t kKeepMax = size_t(1) << 30;  // windows kept across calls: at most 2 x 1 GiB pinned
+    if (cap <= kKeepMax && D->staging_mu.try_lock()) {
         L.locked = true;
         if (!D->staging || D->staging->w[0].cap < cap) {
             delete D->staging;  // its destructor drains the old windows' events
