@@ -4,10 +4,16 @@
 // (lib/metainfogen/config.go:71-80).
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
+#include <utility>
 #include <vector>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 #include "../../include/kraken_hip.h"
 
@@ -16,14 +22,13 @@ void set_error(int code, const char* fmt, ...);
 
 namespace {
 
-struct Sha1 {
-    uint32_t h[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
-    uint8_t buf[64];
-    uint64_t n = 0;
-    uint32_t nb = 0;
-
-    static uint32_t rol(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
-    void block(const uint8_t* p) {
+// ------------------------------------------------------------------- SHA-1
+// FIPS 180-4 SHA-1 over whole 64-byte blocks; the x86 SHA extensions when the CPU
+// has them (sha1rnds4: four rounds per instruction), the portable compressor
+// otherwise.  InfoHash is host work by design (O(pieces)).
+static void sha1_blocks_portable(uint32_t h[5], const uint8_t* p, size_t nblocks) {
+    auto rol = [](uint32_t x, int k) { return (x << k) | (x >> (32 - k)); };
+    for (; nblocks; --nblocks, p += 64) {
         uint32_t w[80];
         for (int i = 0; i < 16; ++i)
             w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
@@ -40,49 +45,144 @@ struct Sha1 {
         }
         h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
     }
-    void write(const void* data, size_t len) {
-        const uint8_t* p = static_cast<const uint8_t*>(data);
-        n += len;
-        while (len) {
-            const uint32_t take = (uint32_t)(len < 64 - nb ? len : 64 - nb);
-            memcpy(buf + nb, p, take);
-            nb += take; p += take; len -= take;
-            if (nb == 64) { block(buf); nb = 0; }
-        }
+}
+
+#if defined(__x86_64__)
+// Quad-round q (rounds 4q..4q+3) of the SHA-NI schedule: message words rotate
+// through M[0..3]; E alternates between the two E registers.
+template <int Q>
+__attribute__((target("sha,sse4.1"))) static inline void sha1_quad(__m128i& abcd, __m128i& e0, __m128i& e1,
+                                                                    __m128i M[4]) {
+    __m128i& ein = (Q & 1) ? e1 : e0;   // E feeding this quad's rounds
+    __m128i& eout = (Q & 1) ? e0 : e1;  // receives ABCD for the next quad's E
+    if (Q == 0) ein = _mm_add_epi32(ein, M[0]);
+    else ein = _mm_sha1nexte_epu32(ein, M[Q & 3]);
+    eout = abcd;
+    if (Q >= 3 && Q <= 18) M[(Q + 1) & 3] = _mm_sha1msg2_epu32(M[(Q + 1) & 3], M[Q & 3]);
+    abcd = _mm_sha1rnds4_epu32(abcd, ein, Q / 5);
+    if (Q >= 1 && Q <= 16) M[(Q + 3) & 3] = _mm_sha1msg1_epu32(M[(Q + 3) & 3], M[Q & 3]);
+    if (Q >= 2 && Q <= 17) M[(Q + 2) & 3] = _mm_xor_si128(M[(Q + 2) & 3], M[Q & 3]);
+}
+
+template <int... Q>
+__attribute__((target("sha,sse4.1"))) static inline void sha1_quads(__m128i& abcd, __m128i& e0, __m128i& e1,
+                                                                     __m128i M[4], const uint8_t* p,
+                                                                     std::integer_sequence<int, Q...>) {
+    const __m128i bswap = _mm_set_epi64x(0x0001020304050607ULL, 0x08090a0b0c0d0e0fULL);
+    for (int k = 0; k < 4; ++k)
+        M[k] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * k)), bswap);
+    (sha1_quad<Q>(abcd, e0, e1, M), ...);
+}
+
+__attribute__((target("sha,sse4.1"))) static void sha1_blocks_ni(uint32_t h[5], const uint8_t* p,
+                                                                  size_t nblocks) {
+    __m128i abcd = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h)), 0x1B);
+    __m128i e0 = _mm_set_epi32((int)h[4], 0, 0, 0), e1;
+    __m128i M[4];
+    for (; nblocks; --nblocks, p += 64) {
+        const __m128i abcd_save = abcd, e0_save = e0;
+        sha1_quads(abcd, e0, e1, M, p, std::make_integer_sequence<int, 20>{});
+        e0 = _mm_sha1nexte_epu32(e0, e0_save);
+        abcd = _mm_add_epi32(abcd, abcd_save);
     }
-    void sum(uint8_t out[20]) {
-        const uint64_t bits = n * 8;
-        const uint8_t pad = 0x80, zero = 0;
-        write(&pad, 1);
-        while (nb != 56) write(&zero, 1);
-        uint8_t lb[8];
-        for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
-        write(lb, 8);
-        for (int i = 0; i < 5; ++i)
-            for (int k = 0; k < 4; ++k) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h), _mm_shuffle_epi32(abcd, 0x1B));
+    h[4] = (uint32_t)_mm_extract_epi32(e0, 3);
+}
+
+static bool have_sha_ni() {
+    static const bool ok = __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+    return ok;
+}
+#endif
+
+// KRK_SHA1_PORTABLE=1 forces the portable compressor (tests compare both).
+static void sha1_blocks(uint32_t h[5], const uint8_t* p, size_t nblocks) {
+#if defined(__x86_64__)
+    static const bool portable = getenv("KRK_SHA1_PORTABLE") && atoi(getenv("KRK_SHA1_PORTABLE")) > 0;
+    if (!portable && have_sha_ni()) return sha1_blocks_ni(h, p, nblocks);
+#endif
+    sha1_blocks_portable(h, p, nblocks);
+}
+
+// SHA-1 of a whole buffer.
+static void sha1(const uint8_t* p, size_t n, uint8_t out[20]) {
+    uint32_t h[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
+    sha1_blocks(h, p, n / 64);
+    uint8_t tail[128] = {};
+    const size_t r = n % 64;
+    memcpy(tail, p + n - r, r);
+    tail[r] = 0x80;
+    const size_t tl = r < 56 ? 64 : 128;
+    const uint64_t bits = (uint64_t)n * 8;
+    for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    sha1_blocks(h, tail, tl / 64);
+    for (int i = 0; i < 5; ++i)
+        for (int k = 0; k < 4; ++k) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
+}
+
+// --------------------------------------------------------------- bencode
+// Decimal digits of v at the END of buf[0..20); returns the first digit's index.
+static int put_u64(char* buf, uint64_t v) {
+    static const char d2[] =
+        "0001020304050607080910111213141516171819202122232425262728293031323334353637383940414243444546474849"
+        "5051525354555657585960616263646566676869707172737475767778798081828384858687888990919293949596979899";
+    int i = 20;
+    while (v >= 100) {
+        const uint64_t q = v / 100;
+        const int r = (int)(v - q * 100);
+        buf[--i] = d2[2 * r + 1];
+        buf[--i] = d2[2 * r];
+        v = q;
     }
-};
+    if (v >= 10) {
+        buf[--i] = d2[2 * v + 1];
+        buf[--i] = d2[2 * v];
+    } else {
+        buf[--i] = (char)('0' + v);
+    }
+    return i;
+}
+
+static void put_i64(std::string& out, int64_t v) {
+    char b[21];
+    if (v < 0) {
+        out.push_back('-');
+        const int i = put_u64(b, (uint64_t)0 - (uint64_t)v);
+        out.append(b + i, 20 - i);
+    } else {
+        const int i = put_u64(b, (uint64_t)v);
+        out.append(b + i, 20 - i);
+    }
+}
 
 // jackpal/bencode-go encoding of core.info (struct -> dict, keys in sorted order:
-// Length, Name, PieceLength, PieceSums; []uint32 -> list of ints).
-template <class Sink>
-void bencode_info(Sink& out, int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
+// Length, Name, PieceLength, PieceSums; []uint32 -> list of ints), as one buffer.
+void bencode_info(std::string& out, int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
                   const char* name, uint64_t name_len, int64_t length) {
-    char b[48];
-    int k;
-    out("d6:Lengthi", 10);
-    k = snprintf(b, sizeof b, "%lld", (long long)length); out(b, k);
-    out("e4:Name", 7);
-    k = snprintf(b, sizeof b, "%llu:", (unsigned long long)name_len); out(b, k);
-    out(name, name_len);
-    out("11:PieceLengthi", 15);
-    k = snprintf(b, sizeof b, "%lld", (long long)piece_length); out(b, k);
-    out("e9:PieceSumsl", 13);
-    for (uint64_t i = 0; i < n_sums; ++i) {
-        k = snprintf(b, sizeof b, "i%ue", sums[i]);
-        out(b, k);
+    out.clear();
+    out.reserve(96 + name_len + 12 * n_sums);
+    out.append("d6:Lengthi");
+    put_i64(out, length);
+    out.append("e4:Name");
+    put_i64(out, (int64_t)name_len);
+    out.push_back(':');
+    out.append(name, name_len);
+    out.append("11:PieceLengthi");
+    put_i64(out, piece_length);
+    out.append("e9:PieceSumsl");
+    const size_t at = out.size();
+    out.resize(at + 12 * n_sums);  // "i" + <= 10 digits + "e"
+    char* w = &out[at];
+    char b[21];
+    for (uint64_t k = 0; k < n_sums; ++k) {
+        const int i = put_u64(b, sums[k]);
+        *w++ = 'i';
+        memcpy(w, b + i, 20 - i);
+        w += 20 - i;
+        *w++ = 'e';
     }
-    out("ee", 2);
+    out.resize((size_t)(w - out.data()));
+    out.append("ee");
 }
 
 }  // namespace
@@ -96,21 +196,18 @@ int krk_info_hash(int64_t piece_length, const uint32_t* sums, uint64_t n_sums, c
         krk::set_error(KRK_EINVAL, "info_hash: null argument");
         return KRK_EINVAL;
     }
-    krk::Sha1 h;
-    auto sink = [&](const char* p, uint64_t n) { h.write(p, n); };
-    krk::bencode_info(sink, piece_length, sums, n_sums, name, name_len, length);
-    h.sum(out20);
+    std::string b;
+    krk::bencode_info(b, piece_length, sums, n_sums, name, name_len, length);
+    krk::sha1(reinterpret_cast<const uint8_t*>(b.data()), b.size(), out20);
     return KRK_OK;
 }
 
 int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums, const char* name,
                      uint64_t name_len, int64_t length, uint8_t* out, uint64_t cap, uint64_t* written) {
-    uint64_t pos = 0;
-    auto sink = [&](const char* p, uint64_t n) {
-        if (out && pos + n <= cap) memcpy(out + pos, p, n);
-        pos += n;
-    };
-    krk::bencode_info(sink, piece_length, sums, n_sums, name, name_len, length);
+    std::string b;
+    krk::bencode_info(b, piece_length, sums, n_sums, name, name_len, length);
+    const uint64_t pos = b.size();
+    if (out && pos <= cap) memcpy(out, b.data(), pos);
     if (written) *written = pos;
     if (out && pos > cap) {
         krk::set_error(KRK_ERANGE, "bencode: need %llu bytes, have %llu", (unsigned long long)pos,

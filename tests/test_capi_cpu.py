@@ -85,3 +85,61 @@ def test_device_entry_points_fail_loudly_without_gpu():
     out = C.c_uint32()
     assert lib.krk_crc32_update(0, b"abc", 3, C.byref(out)) == KRK_ENODEV
     assert b"no HIP device" in lib.krk_last_error()
+
+
+def _ih(P, sums, name, L):
+    out = (C.c_uint8 * 20)()
+    s = np.ascontiguousarray(sums, dtype=np.uint32)
+    check(lib.krk_info_hash(P, s.ctypes.data_as(C.POINTER(C.c_uint32)) if s.size else None, s.size,
+                            name.encode(), len(name.encode()), L, out))
+    return bytes(out)
+
+
+def test_info_hash_reference_kat():
+    """core/metainfo_test.go:61-76 through the C ABI (host bencode + SHA-1)."""
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    k = gold["kat"]["info_hash"]
+    assert _ih(k["piece_length"], k["piece_sums"], k["name"], k["length"]).hex() == k["expected"]
+
+
+def test_info_hash_every_tail_length(orc):
+    """Every bencode length residue mod 64 (the SHA-1 tail and two-block padding cases),
+    large and negative integers, against the oracle's independent SHA-1 + bencode."""
+    rng = np.random.default_rng(9)
+    for n in list(range(0, 140)) + [999, 4096, 81920]:
+        sums = rng.integers(0, 2 ** 32, size=n, dtype=np.uint64).astype(np.uint32)
+        name = rng.bytes(int(rng.integers(0, 40))).hex()
+        L = int(rng.integers(-(1 << 62), 1 << 62))
+        P = int(rng.integers(1, 1 << 40))
+        assert _ih(P, sums, name, L) == orc.info_hash(P, sums, name, L), n
+
+
+_IH_SCRIPT = """
+import sys, ctypes as C
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from kraken_amd._capi import lib
+rng = np.random.default_rng(3)
+out = []
+for n in range(0, 300, 7):
+    s = rng.integers(0, 2 ** 32, size=n, dtype=np.uint64).astype(np.uint32)
+    o = (C.c_uint8 * 20)()
+    lib.krk_info_hash(12345, s.ctypes.data_as(C.POINTER(C.c_uint32)) if n else None, n, b"ab", 2, n, o)
+    out.append(bytes(o).hex())
+print(" ".join(out))
+"""
+
+
+def test_info_hash_sha_ni_matches_portable_sha1(tmp_path):
+    """The SHA-NI compressor (when this CPU has it) and the portable one agree."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "ih.py"
+    f.write_text(_IH_SCRIPT)
+    runs = [subprocess.run([sys.executable, str(f), root], capture_output=True, text=True,
+                           env={**os.environ, "KRK_SHA1_PORTABLE": v}) for v in ("0", "1")]
+    assert all(r.returncode == 0 for r in runs), [r.stderr for r in runs]
+    assert runs[0].stdout == runs[1].stdout and len(runs[0].stdout.split()) == 43
