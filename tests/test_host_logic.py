@@ -132,3 +132,22 @@ def test_dircas_layout_and_list_names(tmp_path):
     os.makedirs(tmp_path / "07" / "12" / "stray")  # no data file: not a blob
     assert cas.ListNames() == sorted(names)
     assert metainfogen._parse_config("0:4194304,2147483648:8388608") == {0: 4194304, 2147483648: 8388608}
+
+
+def test_generate_error_wrapping(tmp_path):
+    """lib/metainfogen/generator.go:41-58 error prefixes, on the paths that fail before
+    any device work: a missing cache file and an unreadable one."""
+    cas = metainfogen.DirCAS(str(tmp_path))
+    g = metainfogen.New({0: 1 << 20}, cas)
+    d = core.NewSHA256DigestFromHex("ab" * 32)
+    with pytest.raises(IOError, match=r"^cache stat: "):
+        g.Generate(d)
+
+    class Unreadable(metainfogen.DirCAS):
+        def GetCacheFileReader(self, hex_):
+            raise OSError("permission denied")
+
+    os.makedirs(cas._dir(d.Hex()))
+    open(os.path.join(cas._dir(d.Hex()), "data"), "wb").close()
+    with pytest.raises(IOError, match=r"^get cache file: permission denied"):
+        metainfogen.New({0: 1 << 20}, Unreadable(str(tmp_path))).Generate(d)
