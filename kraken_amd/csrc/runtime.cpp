@@ -783,11 +783,12 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         Window& w = pl.w[k];
         size_t fill = 0;
         CrcBatch items;
+        std::vector<CopyTask> copies;
         while (bi < n_blobs && fill < W) {
             const krk_blob& b = blobs[bi];
             const uint64_t take = std::min<uint64_t>(b.length - boff, W - fill);
             if (take) {
-                memcpy(w.host + fill, b.data + boff, take);
+                copies.push_back({w.host + fill, b.data + boff, take});
                 B.add(items, reinterpret_cast<uint64_t>(w.dev + fill), boff, boff + take, b.length,
                       (uint64_t)b.piece_length, b.sums_offset);
             }
@@ -797,6 +798,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
             fill = (fill + 15) & ~size_t(15);
             if (boff >= b.length) { ++bi; boff = 0; }
         }
+        par_copy(copies);
         if (pl.h2d(k, std::min(fill, W), cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "piece_sums_host: staging copy failed");
             r = KRK_EHIP;
