@@ -77,8 +77,11 @@ WORKLOADS = {
     "c2": dict(kind="metainfo", desc="C2: 1000 x 100 MiB blobs, 4 MiB pieces, piece CRC-32 + SHA-256 per blob"),
     "c1": dict(kind="metainfo", desc="C1: 1 x 1 GiB blob, 4 MiB pieces (one SHA-256 stream)"),
     "small": dict(kind="metainfo", desc="dev: 64 x 16 MiB blobs, 4 MiB pieces"),
-    "c5regen": dict(kind="metainfo", desc="C5 regen: 1000 blobs, log-uniform sizes in [0, 1 GiB), piece lengths "
-                                          "from {0:1MB, 2GB:4MB, 4GB:8MB}"),
+    "c5regen": dict(kind="regen", desc="C5 regen: Generator.Generate over 1000 blobs (piece sums + InfoHash, no "
+                                       "digest: core/metainfo.go:53-55), log-uniform sizes in [0, 1 GiB), piece "
+                                       "lengths from {0:1MB, 2GB:4MB, 4GB:8MB}"),
+    "c5regen_digest": dict(kind="metainfo", desc="C5 regen blobs with the upload digest as well (metainfo + "
+                                                 "SHA-256 per blob)"),
     "c4": dict(kind="pieces", desc="C4: one 20 GiB blob per GPU, 256 KiB pieces (81,920), piece sums only"),
     "c3": dict(kind="chunked", desc="C3: 20k blobs of 100 MiB + (rng mod 968,884,225) B, 4 MiB pieces, "
                                     "LPT-sharded by blob, streamed through HBM in windows"),
@@ -144,7 +147,7 @@ def workload_blobs(name, rank, world, nblobs_override):
         return [rank * n + i for i in range(n)], [16 << 20] * n, 4 << 20
     if name == "c4":
         return [rank], [20 << 30], 256 << 10
-    if name == "c5regen":
+    if name in ("c5regen", "c5regen_digest"):
         from kraken_amd import metainfogen
         lens = c5regen_lengths(nblobs_override or 1000)
         cfg = metainfogen.newPieceLengthConfig({0: 1 << 20, 2 << 30: 4 << 20, 4 << 30: 8 << 20})
@@ -308,6 +311,67 @@ def run_metainfo(a, D, T, rank, world, res):
             o, cnt = int(arena.sums_off[k]), int(off[k + 1] - off[k])
             ok = ok and np.array_equal(s[int(off[k]):int(off[k + 1])], sums_h[o:o + cnt])
         cb["outputs_match_gpu"] = bool(ok)
+        res["cpu_baseline"] = cb
+
+
+def run_regen(a, D, T, rank, world, res):
+    """C5 regen = Generator.Generate over a batch (lib/metainfogen/generator.go:41-58):
+    NewMetaInfo per blob = piece sums on the GPU + InfoHash (bencode + SHA-1) on the
+    host, batched; Generate computes no digest (core/metainfo.go:53-55 assumes it)."""
+    from kraken_amd import core
+    ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
+    n = len(lens)
+    arena = D.BlobArena(lens, P, blob_ids=ids)
+    out = D.BatchOutputs(arena)
+    pin_s = D.PinnedArray((max(arena.total_pieces, 1),), np.uint32)
+    names = [f"{mix64(int(i)):016x}" * 4 for i in ids]  # the blobs' digest names (Generate takes them as given)
+    ihs = []
+
+    def step():
+        D.piece_sums(arena, out)
+        D.synchronize()
+        pin_s.fill_from(out.sums)
+        ihs[:] = core._info_hash_batch([P] * n, pin_s.a, arena.sums_off, arena.n_pieces, names, lens)
+
+    for _ in range(a.warmup):
+        step()
+    T.barrier()
+    with D.KernelTimer():
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        T.barrier()
+        t1 = time.perf_counter()
+        crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
+    elapsed = T.max_over_ranks(t1 - t0)
+    bytes_rank = int(sum(lens))
+    crc_avg = crc_ms / max(crc_n, 1)
+    res.update({"metric": "metainfo regen GB/s (C5: Generator.Generate = piece sums + InfoHash per blob)",
+                "value": round(world * bytes_rank * a.steps / elapsed / 1e9, 3), "unit": "GB/s", "steps": a.steps,
+                "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+                "dtype": "u8", "data": "synthetic (device-generated splitmix64 blobs)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "blobs_per_gpu": n, "bytes_per_gpu": bytes_rank,
+                           "piece_length": P, "pieces_per_gpu": arena.total_pieces, "mode": "device-resident"},
+                "roofline": roofline_obj("crc32_pieces", bytes_rank / (crc_avg / 1e3) / 1e9, crc_avg, bytes_rank, None),
+                "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)}}})
+    # spot-check the InfoHashes of the first blobs against the oracle's independent bencode + SHA-1
+    if rank == 0:
+        from oracle import oracle as O  # the checker (test infrastructure)
+        O.build()
+        ok = True
+        for k in range(min(n, 8)):
+            o, c = int(arena.sums_off[k]), int(arena.n_pieces[k])
+            ok = ok and bytes(ihs[k]) == O.info_hash(P, pin_s.a[o:o + c], names[k], lens[k])
+        res["info_hash_matches_oracle"] = bool(ok)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        m = min(n, 2 * host_cores())
+        cb, _, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds, passes=2)
+        s_, off = sums
+        ok = all(np.array_equal(s_[int(off[k]):int(off[k + 1])],
+                                pin_s.a[int(arena.sums_off[k]):int(arena.sums_off[k]) + int(off[k + 1] - off[k])])
+                 for k in range(m))
+        cb["outputs_match_gpu"] = bool(ok)
+        cb["sample"] += " (the CPU side times the CRC pass only; its InfoHash is not counted)"
         res["cpu_baseline"] = cb
 
 
@@ -596,7 +660,7 @@ def main():
     T = Timer(D, dist)
     res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
     kind = WORKLOADS[a.workload]["kind"]
-    {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw}[kind](
+    {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen}[kind](
         a, D, T, rank, world, res)
     order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
              "vs_baseline", "dtype", "data", "config"]

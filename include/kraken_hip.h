@@ -159,6 +159,13 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* 
  * info{PieceLength, PieceSums, Name, Length}.  bencode_out may be NULL. */
 int krk_info_hash(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
                   const char* name, uint64_t name_len, int64_t length, uint8_t out20[20]);
+/* Batch form for many blobs (Generator.Generate over a batch, whole-CAS regen):
+ * blob i has piece_lengths[i], sums[sums_off[i] .. sums_off[i] + n_sums[i]), name
+ * names[name_off[i] .. name_off[i+1]), length lengths[i]; out20 receives 20*n bytes.
+ * Spread over host threads.  names may be NULL when every name is empty. */
+int krk_info_hash_batch(const int64_t* piece_lengths, const uint32_t* sums, const uint64_t* sums_off,
+                        const uint64_t* n_sums, const char* names, const uint64_t* name_off,
+                        const int64_t* lengths, uint64_t n, uint8_t* out20);
 int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
                      const char* name, uint64_t name_len, int64_t length,
                      uint8_t* out, uint64_t cap, uint64_t* written);

@@ -75,6 +75,8 @@ def _load() -> C.CDLL:
         "krk_metainfo_digest_host": (i, [blobp, C.c_uint64, u32p, u8p]),
         "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),
+        "krk_info_hash_batch": (i, [C.POINTER(C.c_int64), u32p, u64p, u64p, C.c_char_p, u64p, C.POINTER(C.c_int64),
+                                    C.c_uint64, u8p]),
         "krk_bencode_info": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p,
                                  C.c_uint64, u64p]),
         "krk_piece_length_for_size": (C.c_int64, [i64p, i64p, C.c_uint32, C.c_int64]),

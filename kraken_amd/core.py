@@ -195,6 +195,29 @@ def _info_hash(piece_length: int, sums: np.ndarray, name: str, length: int) -> I
     return InfoHash(bytes(out))
 
 
+def _info_hash_batch(piece_lengths, sums: np.ndarray, sums_off, n_sums, names, lengths) -> list:
+    """InfoHashes of many blobs in one call (krk_info_hash_batch, host threads):
+    blob i's sums are sums[sums_off[i] : sums_off[i] + n_sums[i]]."""
+    n = len(names)
+    if not n:
+        return []
+    enc = [x.encode() for x in names]
+    noff = np.zeros(n + 1, dtype=np.uint64)
+    noff[1:] = np.cumsum([len(e) for e in enc])
+    pl = np.ascontiguousarray(piece_lengths, dtype=np.int64)
+    so = np.ascontiguousarray(sums_off, dtype=np.uint64)
+    ns = np.ascontiguousarray(n_sums, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.int64)
+    s = np.ascontiguousarray(sums, dtype=np.uint32)
+    out = np.zeros(20 * n, dtype=np.uint8)
+    check(lib.krk_info_hash_batch(pl.ctypes.data_as(C.POINTER(C.c_int64)),
+                                  s.ctypes.data_as(C.POINTER(C.c_uint32)) if s.size else None,
+                                  so.ctypes.data_as(C.POINTER(C.c_uint64)), ns.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                  b"".join(enc) or None, noff.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                  ln.ctypes.data_as(C.POINTER(C.c_int64)), n, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return [InfoHash(bytes(out[20 * i:20 * i + 20])) for i in range(n)]
+
+
 # ---------------------------------------------------------------- MetaInfo
 
 class MetaInfo:

@@ -7,7 +7,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -199,6 +201,41 @@ int krk_info_hash(int64_t piece_length, const uint32_t* sums, uint64_t n_sums, c
     std::string b;
     krk::bencode_info(b, piece_length, sums, n_sums, name, name_len, length);
     krk::sha1(reinterpret_cast<const uint8_t*>(b.data()), b.size(), out20);
+    return KRK_OK;
+}
+
+int krk_info_hash_batch(const int64_t* piece_lengths, const uint32_t* sums, const uint64_t* sums_off,
+                        const uint64_t* n_sums, const char* names, const uint64_t* name_off,
+                        const int64_t* lengths, uint64_t n, uint8_t* out20) {
+    if (!n) return KRK_OK;
+    if (!piece_lengths || !sums_off || !n_sums || !name_off || !lengths || !out20 || (name_off[n] && !names)) {
+        krk::set_error(KRK_EINVAL, "info_hash_batch: null argument");
+        return KRK_EINVAL;
+    }
+    for (uint64_t i = 0; i < n; ++i)
+        if (n_sums[i] && !sums) {
+            krk::set_error(KRK_EINVAL, "info_hash_batch: null sums");
+            return KRK_EINVAL;
+        }
+    auto work = [&](uint64_t lo, uint64_t hi) {
+        std::string b;
+        for (uint64_t i = lo; i < hi; ++i) {
+            krk::bencode_info(b, piece_lengths[i], n_sums[i] ? sums + sums_off[i] : nullptr, n_sums[i],
+                              names ? names + name_off[i] : "", name_off[i + 1] - name_off[i], lengths[i]);
+            krk::sha1(reinterpret_cast<const uint8_t*>(b.data()), b.size(), out20 + 20 * i);
+        }
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const uint64_t T = std::min<uint64_t>({n, 16, hw ? hw : 1});
+    if (T <= 1 || n < 64) {
+        work(0, n);
+        return KRK_OK;
+    }
+    std::vector<std::thread> th;
+    const uint64_t span = (n + T - 1) / T;
+    for (uint64_t t = 1; t < T; ++t) th.emplace_back(work, t * span, std::min(n, (t + 1) * span));
+    work(0, std::min(n, span));
+    for (auto& x : th) x.join();
     return KRK_OK;
 }
 

@@ -156,10 +156,11 @@ class Generator:
         check(lib.krk_piece_sums_host(arr, len(datas), sums.ctypes.data_as(C.POINTER(C.c_uint32))))
         out = []
         self._last_changed = 0
-        for d, b, pl, o in datas:
-            n = int(lib.krk_num_pieces(b.size, pl))
+        counts = [int(lib.krk_num_pieces(b.size, pl)) for _, b, pl, _ in datas]
+        ihs = core._info_hash_batch([pl for _, _, pl, _ in datas], sums, [o for *_, o in datas], counts,
+                                    [d.Hex() for d, *_ in datas], [b.size for _, b, _, _ in datas])
+        for (d, b, pl, o), n, ih in zip(datas, counts, ihs):
             s = sums[o:o + n].copy() if n else None
-            ih = core._info_hash(pl, s if s is not None else np.zeros(0, np.uint32), d.Hex(), b.size)
             mi = core.MetaInfo(pl, s, d.Hex(), b.size, d, ih)
             self._last_changed += bool(self.cas.SetCacheFileMetadata(d.Hex(), mi))
             out.append(mi)

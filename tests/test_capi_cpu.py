@@ -143,3 +143,20 @@ def test_info_hash_sha_ni_matches_portable_sha1(tmp_path):
                            env={**os.environ, "KRK_SHA1_PORTABLE": v}) for v in ("0", "1")]
     assert all(r.returncode == 0 for r in runs), [r.stderr for r in runs]
     assert runs[0].stdout == runs[1].stdout and len(runs[0].stdout.split()) == 43
+
+
+def test_info_hash_batch_matches_single(orc):
+    from kraken_amd import core
+    rng = np.random.default_rng(17)
+    n = 300
+    ns = rng.integers(0, 50, n)
+    ns[::7] = 0
+    sums = rng.integers(0, 2 ** 32, size=int(ns.sum()), dtype=np.uint64).astype(np.uint32)
+    off = np.concatenate(([0], np.cumsum(ns)[:-1]))
+    names = [rng.bytes(32).hex() if i % 5 else "" for i in range(n)]
+    pls = rng.integers(1, 1 << 30, n)
+    lens = rng.integers(0, 1 << 40, n)
+    got = core._info_hash_batch(pls, sums, off, ns, names, lens)
+    for i in range(n):
+        s = sums[off[i]:off[i] + ns[i]]
+        assert bytes(got[i]) == orc.info_hash(int(pls[i]), s, names[i], int(lens[i])), i
