@@ -132,7 +132,15 @@ __device__ __forceinline__ uint32_t step64(uint32_t c, const u32x4& v0, const u3
 }
 
 // This lane's share of bytes [base, base+len), shifted to the item end.
-template <class TT, int RG, bool LOADONLY = false>
+// One 16-byte load; NT marks it nontemporal (global_load ... nt: the bytes are read
+// once, so they need not displace anything in L2 / MALL).
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(gptr<u32x4> p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <class TT, int RG, bool LOADONLY = false, bool NT = false>
 __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                      const uint32_t* G, uint32_t lane_mul,
                                                      const uint32_t* x8pow) {
@@ -145,16 +153,16 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
             // flight while the current step's lookups run.
             gptr<u32x4> p = as_global<u32x4>(base + lane * kSeg);
             constexpr uint32_t S = kStep / 16;
-            u32x4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+            u32x4 a0 = ld16<NT>(p), a1 = ld16<NT>(p + 1), a2 = ld16<NT>(p + 2), a3 = ld16<NT>(p + 3);
             u32x4 b0, b1, b2, b3;
             uint32_t s = 0;
             for (; s + 2 <= nfull; s += 2) {
                 gptr<u32x4> q = p + (s + 1) * S;
-                b0 = q[0]; b1 = q[1]; b2 = q[2]; b3 = q[3];
+                b0 = ld16<NT>(q); b1 = ld16<NT>(q + 1); b2 = ld16<NT>(q + 2); b3 = ld16<NT>(q + 3);
                 c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
                 if (s + 2 < nfull) {
                     q = p + (s + 2) * S;
-                    a0 = q[0]; a1 = q[1]; a2 = q[2]; a3 = q[3];
+                    a0 = ld16<NT>(q); a1 = ld16<NT>(q + 1); a2 = ld16<NT>(q + 2); a3 = ld16<NT>(q + 3);
                 }
                 c = step64<TT, RG, LOADONLY>(c, b0, b1, b2, b3, T, G);
             }
@@ -282,7 +290,7 @@ __device__ __forceinline__ ItemRef fetch_item(const CrcWork& w, uint32_t it) {
             jj == 0 ? w.consts[r.cpat + r.ipp] : 0u};
 }
 
-template <class TT, int RG, bool COAL, bool LOADONLY>
+template <class TT, int RG, bool COAL, bool LOADONLY, bool NT>
 __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const uint32_t* G, const uint32_t lm[4],
                                           const uint32_t* x8pow, uint32_t lane, uint32_t wave0, uint32_t n_waves,
                                           uint32_t* sums) {
@@ -290,7 +298,7 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
     for (uint32_t it = wave0; it < n_items; it += n_waves) {
         const ItemRef ci = fetch_item(w, it);
         uint32_t c = COAL ? lane_crc_coal<TT, RG>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
-                          : lane_crc_strided<TT, RG, LOADONLY>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
+                          : lane_crc_strided<TT, RG, LOADONLY, NT>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
         // Wave XOR-reduction.
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c ^= __shfl_xor(c, off, 64);
@@ -301,7 +309,7 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
     }
 }
 
-template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0>
+template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false>
 __global__ void __launch_bounds__(BLOCK)
 crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -333,23 +341,23 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
         if ((uint32_t)(size_t)(lds_u32p)lds != 0) __builtin_trap();
         TabP<PERM> T;
         T.loff = (1u << 16) | ((lane % PERM) << 2);
-        item_loop<TabP<PERM>, RG, COAL, LOADONLY>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
     } else {
         Tab<R> T;
         T.lo = lds + (lane % R);
         T.hi = lds + 2 * 256 * R + (lane % R);
-        item_loop<Tab<R>, RG, COAL, LOADONLY>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+        item_loop<Tab<R>, RG, COAL, LOADONLY, NT>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
     }
 }
 
-template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0>
+template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false>
 static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
                                  int blocks_per_cu, hipStream_t s) {
     constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4;
     static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM>),
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (attr_err != hipSuccess) return attr_err;
@@ -359,7 +367,7 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
     uint64_t cap = uint64_t(cus) * blocks_per_cu;
     uint32_t grid = (uint32_t)(want < cap ? want : cap);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
+    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
     return hipGetLastError();
 }
 
@@ -383,6 +391,12 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
             return launch_variant<32, 4, 1024, false, false, 32>(w, tabs, sums, cfg.cus, 1, s);
         case 8:  // as 7 with 16 replicas (80 KiB): two 1024-thread blocks per CU
             return launch_variant<16, 4, 1024, false, false, 16>(w, tabs, sums, cfg.cus, 2, s);
+        case 9:  // as 7 with nontemporal data loads
+            return launch_variant<32, 4, 1024, false, false, 32, true>(w, tabs, sums, cfg.cus, 1, s);
+        case 10:  // timing diagnostic: variant 9's loads and occupancy without the lookups (wrong sums)
+            return launch_variant<32, 4, 1024, false, true, 32, true>(w, tabs, sums, cfg.cus, 1, s);
+        case 11:  // timing diagnostic: variant 7's loads and occupancy without the lookups (wrong sums)
+            return launch_variant<32, 4, 1024, false, true, 32, false>(w, tabs, sums, cfg.cus, 1, s);
         default:  // strided, 80 KiB LDS: two 512-thread blocks per CU
             return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
     }
