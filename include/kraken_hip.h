@@ -30,6 +30,7 @@ extern "C" {
 #define KRK_ENODEV (-4)    /* no MI355X (gfx950) device visible */
 #define KRK_ERANGE (-5)    /* output capacity too small */
 #define KRK_EHEX (-6)      /* invalid hex key (hrw.Score returns NaN, rendezvous.go:154-157) */
+#define KRK_EIO (-7)       /* file open/read failed (message has the path and errno text) */
 
 /* ---------------------------------------------------------------- runtime */
 const char* krk_version(void);
@@ -63,6 +64,22 @@ int krk_piece_sums_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_d
  * kernel.  Synchronous.  This is the batch form of Generator.Generate's
  * NewMetaInfo call (lib/metainfogen/generator.go:41-58). */
 int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host);
+
+/* Piece sums of cache FILES: the batch form of Generator.Generate reading the
+ * CAS cache file itself (lib/metainfogen/generator.go:41-58: GetCacheFileReader
+ * -> NewMetaInfo).  Each file's bytes are read (pread on a pool of host
+ * threads, or O_DIRECT when KRK_FILE_DIRECT=1 and the filesystem allows it)
+ * straight into the pinned staging windows -- no pageable copy -- and the
+ * windows feed the CRC kernel as in krk_piece_sums_host.  length is the size
+ * the caller stat-ed (Generate picks the piece length from it); a file shorter
+ * than that is KRK_EIO "read blob: <path>: unexpected EOF".  Synchronous. */
+typedef struct krk_file_blob {
+    const char* path;
+    uint64_t length;
+    int64_t piece_length;    /* > 0 */
+    uint64_t sums_offset;
+} krk_file_blob;
+int krk_piece_sums_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host);
 
 /* Streaming form for NewMetaInfo(d, io.Reader, P): the cgo shim copies each
  * Read() chunk in with _update; CRC state is carried across chunk and piece

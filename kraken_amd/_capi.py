@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KRK_LIB_PATH") or os.path.join(_HERE, "lib", "libkraken_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip.h")
 
-KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX = 0, -1, -2, -3, -4, -5, -6
+KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX, KRK_EIO = 0, -1, -2, -3, -4, -5, -6, -7
 
 
 class KrakenError(RuntimeError):
@@ -24,6 +24,11 @@ class KrakenError(RuntimeError):
 
 class krk_blob(C.Structure):
     _fields_ = [("data", C.c_void_p), ("length", C.c_uint64), ("piece_length", C.c_int64),
+                ("sums_offset", C.c_uint64)]
+
+
+class krk_file_blob(C.Structure):
+    _fields_ = [("path", C.c_char_p), ("length", C.c_uint64), ("piece_length", C.c_int64),
                 ("sums_offset", C.c_uint64)]
 
 
@@ -58,6 +63,7 @@ def _load() -> C.CDLL:
         "krk_num_pieces": (C.c_uint64, [C.c_uint64, C.c_int64]),
         "krk_piece_sums_dev": (i, [blobp, C.c_uint64, vp, vp]),
         "krk_piece_sums_host": (i, [blobp, C.c_uint64, u32p]),
+        "krk_piece_sums_files": (i, [C.POINTER(krk_file_blob), C.c_uint64, u32p]),
         "krk_piece_stream_begin": (i, [C.c_int64, C.POINTER(vp)]),
         "krk_piece_stream_update": (i, [vp, vp, C.c_uint64]),
         "krk_piece_stream_end": (i, [vp, u32p, C.c_uint64, u64p, u64p]),

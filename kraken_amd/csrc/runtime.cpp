@@ -1,7 +1,10 @@
 // runtime.cpp -- the C ABI (include/kraken_hip.h): device contexts, work
 // descriptor builders, pinned staging pipelines and kernel launches.
+#include <errno.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <unistd.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -666,6 +669,60 @@ static void par_copy(const std::vector<CopyTask>& tasks) {
     for (auto& t : th) t.join();
 }
 
+// File -> pinned window reads of one window, split over the copy threads at
+// 1 MiB-aligned spans (O_DIRECT needs block-aligned offsets and lengths; every
+// task starts 4 KiB-aligned in both the file and the window).
+struct ReadTask {
+    int fd;
+    uint64_t off;   // file offset
+    uint8_t* dst;
+    size_t n;       // bytes wanted (O_DIRECT reads round the last block up)
+    size_t blob;    // index into the caller's files (for the error message)
+};
+
+// Returns -1 on success, else the index of the failed task; err = its errno (0 = EOF).
+static long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) {
+    // Spans are cut in a stream of the tasks laid end to end, each padded to 4 KiB
+    // when direct, so every span boundary falls on a block boundary of its task.
+    auto padded = [direct](size_t n) { return direct ? (n + 4095) & ~size_t(4095) : n; };
+    size_t total = 0;
+    for (const auto& t : tasks) total += padded(t.n);
+    std::atomic<long> bad{-1};
+    std::atomic<int> bad_errno{0};
+    auto run = [&](size_t lo, size_t hi) {
+        size_t pos = 0;
+        for (size_t i = 0; i < tasks.size() && pos < hi; pos += padded(tasks[i].n), ++i) {
+            const ReadTask& t = tasks[i];
+            size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
+            if (a >= b) continue;
+            a -= pos;
+            b -= pos;
+            while (a < b) {
+                size_t want = b - a;
+                if (direct) want = (want + 4095) & ~size_t(4095);
+                const ssize_t got = pread(t.fd, t.dst + a, want, (off_t)(t.off + a));
+                if (got < 0 && errno == EINTR) continue;
+                if (got <= 0) {
+                    long expect = -1;
+                    bad.compare_exchange_strong(expect, (long)i);
+                    bad_errno.store(got < 0 ? errno : 0);
+                    return;
+                }
+                a += (size_t)got;
+            }
+        }
+    };
+    const unsigned T = (total < (8u << 20)) ? 1 : copy_threads();
+    constexpr size_t kAlign = size_t(1) << 20;
+    const size_t span = std::max(kAlign, ((total + T - 1) / T + kAlign - 1) & ~(kAlign - 1));
+    std::vector<std::thread> th;
+    for (size_t lo = span; lo < total; lo += span) th.emplace_back(run, lo, std::min(total, lo + span));
+    run(0, std::min(total, span));
+    for (auto& t : th) t.join();
+    *err = bad_errno.load();
+    return bad.load();
+}
+
 }  // namespace krk
 
 using namespace krk;
@@ -810,6 +867,117 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         k ^= 1;
     }
     if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "sums copy-out failed");
+        r = KRK_EHIP;
+    }
+    hipFree(d_sums);
+    return r;
+}
+
+int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_host) {
+    KRK_DEVICE(D);
+    if (!n) return KRK_OK;
+    KRK_CHECK(files, KRK_EINVAL, "files is NULL");
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        KRK_CHECK(files[i].path, KRK_EINVAL, "file %llu: path is NULL", (unsigned long long)i);
+        KRK_CHECK(files[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
+        const uint64_t np = krk_num_pieces(files[i].length, files[i].piece_length);
+        if (np) {
+            lo = std::min(lo, files[i].sums_offset);
+            hi = std::max(hi, files[i].sums_offset + np);
+        }
+    }
+    if (hi == 0) return KRK_OK;
+    KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
+    const bool want_direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
+    uint32_t* d_sums = nullptr;
+    KRK_HIP(hipMalloc(&d_sums, hi * 4));
+    KRK_HIP(hipMemset(d_sums, 0, hi * 4));
+    const size_t W = window_bytes();  // a multiple of 1 MiB
+    StagingLease lease;
+    int r = lease_staging(D, W, lease);
+    Pipeline* pl = lease.p;
+    hipStream_t cp = D->s_a, ks = D->s_b;
+    ItemBuilder B;
+    std::vector<int> fds(n, -1);
+    std::vector<char> direct(n, 0);
+    auto open_file = [&](uint64_t i) -> int {
+        if (fds[i] >= 0) return KRK_OK;
+        int fd = -1;
+        if (want_direct) {
+            fd = open(files[i].path, O_RDONLY | O_DIRECT | O_CLOEXEC);
+            direct[i] = fd >= 0;
+        }
+        if (fd < 0) fd = open(files[i].path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+            set_error(KRK_EIO, "open %s: %s", files[i].path, strerror(errno));
+            return KRK_EIO;
+        }
+        fds[i] = fd;
+        return KRK_OK;
+    };
+    int k = 0;
+    uint64_t bi = 0, boff = 0;
+    while (!r && bi < n) {
+        r = pl->acquire(k);
+        if (r) break;
+        Window& w = pl->w[k];
+        size_t fill = 0;
+        CrcBatch items;
+        std::vector<ReadTask> plain, odirect;
+        std::vector<uint64_t> finished;
+        while (bi < n && fill < W) {
+            const krk_file_blob& f = files[bi];
+            const uint64_t take = std::min<uint64_t>(f.length - boff, W - fill);
+            if (take) {
+                r = open_file(bi);
+                if (r) break;
+                (direct[bi] ? odirect : plain).push_back({fds[bi], boff, w.host + fill, (size_t)take, (size_t)bi});
+                B.add(items, reinterpret_cast<uint64_t>(w.dev + fill), boff, boff + take, f.length,
+                      (uint64_t)f.piece_length, f.sums_offset);
+            }
+            fill += take;
+            boff += take;
+            fill = (fill + 4095) & ~size_t(4095);  // every file starts page-aligned in the window
+            if (boff >= f.length) {
+                finished.push_back(bi);
+                ++bi;
+                boff = 0;
+            }
+        }
+        if (r) break;
+        for (int pass = 0; pass < 2 && !r; ++pass) {
+            const auto& tasks = pass ? odirect : plain;
+            if (tasks.empty()) continue;
+            int e = 0;
+            const long bad = par_read(tasks, pass == 1, &e);
+            if (bad >= 0) {
+                const char* path = files[tasks[bad].blob].path;
+                if (e) set_error(KRK_EIO, "read blob: %s: %s", path, strerror(e));
+                else set_error(KRK_EIO, "read blob: %s: unexpected EOF", path);
+                r = KRK_EIO;
+            }
+        }
+        for (uint64_t i : finished) {
+            if (fds[i] >= 0) close(fds[i]);
+            fds[i] = -1;
+        }
+        if (r) break;
+        if (pl->h2d(k, std::min(fill, W), cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
+            set_error(KRK_EHIP, "piece_sums_files: staging copy failed");
+            r = KRK_EHIP;
+            break;
+        }
+        r = run_items(D, items, d_sums, ks);
+        if (r) break;
+        pl->release(k, 0, ks);
+        k ^= 1;
+    }
+    for (int fd : fds)
+        if (fd >= 0) close(fd);
+    if (hipStreamSynchronize(ks) != hipSuccess && !r) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
     if (!r && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;

@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 from . import core
-from ._capi import check, krk_blob, lib
+from ._capi import KRK_EIO, check, krk_blob, krk_file_blob, lib
 
 
 class pieceLengthConfig:
@@ -69,6 +69,11 @@ class DirCAS:
 
     def GetCacheFileReader(self, hex_: str):
         return open(os.path.join(self._dir(hex_), "data"), "rb")
+
+    def GetCacheFilePath(self, hex_: str) -> str:
+        """The cache file's path (base FileOp.GetFilePath): lets GenerateBatch read
+        the file natively into pinned staging instead of through a reader."""
+        return os.path.join(self._dir(hex_), "data")
 
     def SetCacheFileMetadata(self, hex_: str, mi: core.MetaInfo) -> bool:
         p = os.path.join(self._dir(hex_), "_torrentmeta")
@@ -141,31 +146,63 @@ class Generator:
         return {"blobs": seen, "changed": changed}
 
     def GenerateBatch(self, digests) -> list[core.MetaInfo]:
-        """Generate for many cache files in one pipelined GPU pass."""
-        datas, blobs, off = [], [], 0
-        for d in digests:
-            with self.cas.GetCacheFileReader(d.Hex()) as f:
-                b = np.frombuffer(f.read(), dtype=np.uint8)
-            pl = self.pieceLengthConfig.get(b.size)
-            datas.append((d, b, pl, off))
-            off += int(lib.krk_num_pieces(b.size, pl))
-        arr = (krk_blob * max(len(datas), 1))()
-        for i, (d, b, pl, o) in enumerate(datas):
-            arr[i] = krk_blob(b.ctypes.data if b.size else None, b.size, pl, o)
-        sums = np.zeros(max(off, 1), dtype=np.uint32)
-        check(lib.krk_piece_sums_host(arr, len(datas), sums.ctypes.data_as(C.POINTER(C.c_uint32))))
+        """Generate for many cache files in one pipelined GPU pass.  When the CAS
+        exposes file paths (DirCAS.GetCacheFilePath) the files are read by the
+        library's host threads straight into pinned staging windows
+        (krk_piece_sums_files); otherwise through GetCacheFileReader into host
+        memory (krk_piece_sums_host).  Errors carry Generate's prefixes
+        (generator.go:41-58)."""
+        if hasattr(self.cas, "GetCacheFilePath"):
+            metas, off = [], 0
+            for d in digests:
+                try:
+                    size = self.cas.GetCacheFileStat(d.Hex()).st_size
+                except OSError as e:
+                    raise IOError(f"cache stat: {e}") from None
+                pl = self.pieceLengthConfig.get(size)
+                metas.append((d, size, pl, off))
+                off += int(lib.krk_num_pieces(size, pl))
+            paths = [os.fsencode(self.cas.GetCacheFilePath(d.Hex())) for d, *_ in metas]
+            arr = (krk_file_blob * max(len(metas), 1))()
+            for i, ((d, size, pl, o), path) in enumerate(zip(metas, paths)):
+                arr[i] = krk_file_blob(path, size, pl, o)
+            sums = np.zeros(max(off, 1), dtype=np.uint32)
+            rc = lib.krk_piece_sums_files(arr, len(metas), sums.ctypes.data_as(C.POINTER(C.c_uint32)))
+            if rc == KRK_EIO:
+                raise IOError(f"create metainfo: {lib.krk_last_error().decode()}")
+            check(rc)
+        else:
+            datas, metas, off = [], [], 0
+            for d in digests:
+                try:
+                    f = self.cas.GetCacheFileReader(d.Hex())
+                except OSError as e:
+                    raise IOError(f"get cache file: {e}") from None
+                with f:
+                    b = np.frombuffer(f.read(), dtype=np.uint8)
+                pl = self.pieceLengthConfig.get(b.size)
+                datas.append(b)
+                metas.append((d, b.size, pl, off))
+                off += int(lib.krk_num_pieces(b.size, pl))
+            arr = (krk_blob * max(len(metas), 1))()
+            for i, (b, (d, size, pl, o)) in enumerate(zip(datas, metas)):
+                arr[i] = krk_blob(b.ctypes.data if b.size else None, size, pl, o)
+            sums = np.zeros(max(off, 1), dtype=np.uint32)
+            check(lib.krk_piece_sums_host(arr, len(metas), sums.ctypes.data_as(C.POINTER(C.c_uint32))))
         out = []
         self._last_changed = 0
-        counts = [int(lib.krk_num_pieces(b.size, pl)) for _, b, pl, _ in datas]
-        ihs = core._info_hash_batch([pl for _, _, pl, _ in datas], sums, [o for *_, o in datas], counts,
-                                    [d.Hex() for d, *_ in datas], [b.size for _, b, _, _ in datas])
-        for (d, b, pl, o), n, ih in zip(datas, counts, ihs):
-            s = sums[o:o + n].copy() if n else None
-            mi = core.MetaInfo(pl, s, d.Hex(), b.size, d, ih)
-            self._last_changed += bool(self.cas.SetCacheFileMetadata(d.Hex(), mi))
+        counts = [int(lib.krk_num_pieces(size, pl)) for _, size, pl, _ in metas]
+        ihs = core._info_hash_batch([pl for _, _, pl, _ in metas], sums, [o for *_, o in metas], counts,
+                                    [d.Hex() for d, *_ in metas], [size for _, size, _, _ in metas])
+        for (d, size, pl, o), n, ih in zip(metas, counts, ihs):
+            s_ = sums[o:o + n].copy() if n else None
+            mi = core.MetaInfo(pl, s_, d.Hex(), size, d, ih)
+            try:
+                self._last_changed += bool(self.cas.SetCacheFileMetadata(d.Hex(), mi))
+            except OSError as e:
+                raise IOError(f"set metainfo: {e}") from None
             out.append(mi)
         return out
-
 
     def VerifyAndGenerateBatch(self, uploads):
         """Fused upload verification + metainfo generation.
@@ -188,11 +225,21 @@ class Generator:
                 out.append(ValueError(f"computed digest {got.String()} doesn't match parameter {want.String()}"))
                 continue
             d = self.cas.WriteCacheFileAs(want, x)
-            s = s.copy() if s.size else None
-            ih = core._info_hash(pl, s if s is not None else np.zeros(0, np.uint32), d.Hex(), int(x.size))
-            mi = core.MetaInfo(pl, s, d.Hex(), int(x.size), d, ih)
-            self.cas.SetCacheFileMetadata(d.Hex(), mi)
-            out.append(mi)
+            out.append((d, pl, s.copy() if s.size else None, int(x.size)))
+        # the verified blobs' InfoHashes in one batched call
+        ok = [k for k, o in enumerate(out) if not isinstance(o, ValueError)]
+        if ok:
+            flat = [out[k][2] for k in ok if out[k][2] is not None]
+            allsums = np.concatenate(flat) if flat else np.zeros(0, np.uint32)
+            counts = [0 if out[k][2] is None else out[k][2].size for k in ok]
+            offs = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.uint64)
+            ihs = core._info_hash_batch([out[k][1] for k in ok], allsums, offs, counts,
+                                        [out[k][0].Hex() for k in ok], [out[k][3] for k in ok])
+            for k, ih in zip(ok, ihs):
+                d, pl, s, size = out[k]
+                mi = core.MetaInfo(pl, s, d.Hex(), size, d, ih)
+                self.cas.SetCacheFileMetadata(d.Hex(), mi)
+                out[k] = mi
         return out
 
 

@@ -338,3 +338,66 @@ def test_sha_launch_plans_bit_exact(gpu, orc, variant, monkeypatch):
     D.synchronize()
     cdg = cb.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
     assert np.array_equal(cdg, dg), variant
+
+
+class _ReaderOnlyCAS:
+    """A CAS without GetCacheFilePath: GenerateBatch takes the reader route."""
+
+    def __init__(self, cas, stat_extra=0):
+        self.cas, self.stat_extra = cas, stat_extra
+
+    def GetCacheFileStat(self, h):
+        return self.cas.GetCacheFileStat(h)
+
+    def GetCacheFileReader(self, h):
+        return self.cas.GetCacheFileReader(h)
+
+    def SetCacheFileMetadata(self, h, mi):
+        return self.cas.SetCacheFileMetadata(h, mi)
+
+
+@pytest.mark.parametrize("direct,window_mb", [("0", 1), ("1", 1), ("0", 512), ("1", 512)])
+def test_generate_batch_from_files(gpu, orc, tmp_path, direct, window_mb):
+    """krk_piece_sums_files (cache files read straight into pinned staging, pread
+    threads or O_DIRECT) == the reader route == the oracle, with files split over
+    1 MiB windows and sizes off every alignment."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path))
+    rng = np.random.default_rng(int(direct) * 7 + window_mb)
+    lens = [0, 1, 15, 4095, 4096, 4097, 65537, (1 << 20) - 1, 1 << 20, (1 << 20) + 4097, (3 << 20) + 5, 9_000_001]
+    blobs = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    ds = [cas.WriteCacheFile(b) for b in blobs]
+    cfg = {0: 65536, 1 << 20: 1 << 20, 8 << 20: 4 << 20}
+    os.environ["KRK_WINDOW_MB"], os.environ["KRK_FILE_DIRECT"] = str(window_mb), direct
+    try:
+        mis = metainfogen.New(cfg, cas).GenerateBatch(ds)
+        mis_r = metainfogen.New(cfg, _ReaderOnlyCAS(cas)).GenerateBatch(ds)
+    finally:
+        del os.environ["KRK_WINDOW_MB"], os.environ["KRK_FILE_DIRECT"]
+    for mi, mr, d, b in zip(mis, mis_r, ds, blobs):
+        pl = mi.PieceLength()
+        ref = orc.calc_piece_sums(b, pl)[1]
+        assert mi.InfoHash() == mr.InfoHash()
+        assert bytes(mi.InfoHash()) == orc.info_hash(pl, ref, d.Hex(), len(b)), len(b)
+        assert mi.Serialize() == open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read()
+
+
+def test_generate_batch_file_errors(gpu, tmp_path):
+    """Generate's error prefixes (generator.go:41-58) on the file route: a missing
+    cache file -> "cache stat: ...", a file shorter than its stat size ->
+    "create metainfo: read blob: <path>: unexpected EOF"."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path))
+    d = cas.WriteCacheFile(os.urandom(100_000))
+    g = metainfogen.New({0: 4096}, cas)
+    with pytest.raises(IOError, match="^cache stat: "):
+        g.GenerateBatch([core.NewSHA256DigestFromHex("ab" * 32)])
+
+    class Lying(metainfogen.DirCAS):
+        def GetCacheFileStat(self, h):
+            st = super().GetCacheFileStat(h)
+            return os.stat_result((st.st_mode, st.st_ino, st.st_dev, st.st_nlink, st.st_uid, st.st_gid,
+                                   st.st_size + 5000, st.st_atime, st.st_mtime, st.st_ctime))
+
+    with pytest.raises(IOError, match="^create metainfo: read blob: .*: unexpected EOF"):
+        metainfogen.New({0: 4096}, Lying(str(tmp_path))).GenerateBatch([d])
