@@ -352,7 +352,8 @@ def run_regen(a, D, T, rank, world, res):
                 "dtype": "u8", "data": "synthetic (device-generated splitmix64 blobs)",
                 "config": {"workload": WORKLOADS[a.workload]["desc"], "blobs_per_gpu": n, "bytes_per_gpu": bytes_rank,
                            "piece_length": P, "pieces_per_gpu": arena.total_pieces, "mode": "device-resident"},
-                "roofline": roofline_obj("crc32_pieces", bytes_rank / (crc_avg / 1e3) / 1e9, crc_avg, bytes_rank, None),
+                "roofline": roofline_obj("crc32_pieces", bytes_rank / (crc_avg / 1e3) / 1e9, crc_avg, bytes_rank,
+                                         load_traffic(a.pmc_json, a.workload, n).get("crc32_pieces")),
                 "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)}}})
     # spot-check the InfoHashes of the first blobs against the oracle's independent bencode + SHA-1
     if rank == 0:
