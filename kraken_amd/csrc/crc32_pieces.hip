@@ -199,13 +199,14 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
 }
 
 // ---------------------------------------------------------- coalesced layout
-template <class TT, int RG>
+template <class TT, int RG, bool LOADONLY = false>
 __device__ __forceinline__ void step_coal(uint32_t c[4], const u32x4 v[4], const TT& T, const uint32_t* G) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = seg16(gap_shift<RG>(c[k], G), v[k], T);
+    for (int k = 0; k < 4; ++k)
+        c[k] = LOADONLY ? c[k] ^ xor3(v[k].x, v[k].y, v[k].z) ^ v[k].w : seg16(gap_shift<RG>(c[k], G), v[k], T);
 }
 
-template <class TT, int RG>
+template <class TT, int RG, bool LOADONLY = false>
 __device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                   const uint32_t* G, const uint32_t lm[4], const uint32_t* x8pow) {
     uint32_t c[4] = {0u, 0u, 0u, 0u};
@@ -223,15 +224,15 @@ __device__ __forceinline__ uint32_t lane_crc_coal(uint64_t base, uint32_t len, u
             gptr<u32x4> q = p + (s + 1) * S;
 #pragma unroll
             for (int k = 0; k < 4; ++k) b[k] = q[64 * k];
-            step_coal<TT, RG>(c, a, T, G);
+            step_coal<TT, RG, LOADONLY>(c, a, T, G);
             if (s + 2 < nfull) {
                 q = p + (s + 2) * S;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) a[k] = q[64 * k];
             }
-            step_coal<TT, RG>(c, b, T, G);
+            step_coal<TT, RG, LOADONLY>(c, b, T, G);
         }
-        if (s < nfull) step_coal<TT, RG>(c, a, T, G);
+        if (s < nfull) step_coal<TT, RG, LOADONLY>(c, a, T, G);
 #pragma unroll
         for (int k = 0; k < 4; ++k) end[k] = (nfull - 1) * kStep + 1024 * k + 16 * lane + 16;
         s0 = nfull;
@@ -297,7 +298,7 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
     const uint32_t n_items = w.run_items + w.n_items;
     for (uint32_t it = wave0; it < n_items; it += n_waves) {
         const ItemRef ci = fetch_item(w, it);
-        uint32_t c = COAL ? lane_crc_coal<TT, RG>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
+        uint32_t c = COAL ? lane_crc_coal<TT, RG, LOADONLY>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
                           : lane_crc_strided<TT, RG, LOADONLY, NT>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
         // Wave XOR-reduction.
 #pragma unroll
@@ -397,6 +398,10 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
             return launch_variant<32, 4, 1024, false, true, 32, true>(w, tabs, sums, cfg.cus, 1, s);
         case 11:  // timing diagnostic: variant 7's loads and occupancy without the lookups (wrong sums)
             return launch_variant<32, 4, 1024, false, true, 32, false>(w, tabs, sums, cfg.cus, 1, s);
+        case 12:  // coalesced, byte-addressable tables (144 KiB), one 1024-thread block per CU
+            return launch_variant<32, 4, 1024, true, false, 32>(w, tabs, sums, cfg.cus, 1, s);
+        case 13:  // timing diagnostic: variant 12's loads and occupancy without the lookups (wrong sums)
+            return launch_variant<32, 4, 1024, true, true, 32>(w, tabs, sums, cfg.cus, 1, s);
         default:  // strided, 80 KiB LDS: two 512-thread blocks per CU
             return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
     }
