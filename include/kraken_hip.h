@@ -37,6 +37,17 @@ const char* krk_version(void);
 const char* krk_last_error(void);            /* thread-local, never NULL */
 int krk_device_count(int* n);                /* gfx950 devices visible */
 int krk_set_device(int dev);                 /* per calling thread */
+/* Eager context creation (streams, CRC tables) for the devices in dev_mask (bit i =
+ * device i; 0 = the calling thread's current device), so the first request on a
+ * device does not pay it; otherwise contexts are created on first use.  KRK_ENODEV
+ * if a masked device is absent or not gfx950.  (SURVEY.md 8(b) krk_init.) */
+int krk_init(uint64_t dev_mask);
+/* Free every device context: streams, tables, scratch, pinned upload slots and the
+ * staging windows kept across host-path calls (up to 2 x 1 GiB pinned per device).
+ * The caller guarantees no library call is in flight and every krk_digester /
+ * krk_piece_stream / krk_stream handle is freed.  Later calls re-create contexts
+ * lazily. */
+int krk_shutdown(void);
 int krk_synchronize(void);                   /* drain the library's streams on the current device */
 
 /* ------------------------------------------------- CRC-32/IEEE piece sums

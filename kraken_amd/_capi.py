@@ -59,6 +59,8 @@ def _load() -> C.CDLL:
         "krk_last_error": (C.c_char_p, []),
         "krk_device_count": (i, [C.POINTER(C.c_int)]),
         "krk_set_device": (i, [i]),
+        "krk_init": (i, [C.c_uint64]),
+        "krk_shutdown": (i, []),
         "krk_synchronize": (i, []),
         "krk_num_pieces": (C.c_uint64, [C.c_uint64, C.c_int64]),
         "krk_piece_sums_dev": (i, [blobp, C.c_uint64, vp, vp]),

@@ -669,6 +669,38 @@ static void par_copy(const std::vector<CopyTask>& tasks) {
     for (auto& t : th) t.join();
 }
 
+// Everything a device context holds: streams, tables, scratch cache, pinned
+// upload slots, staging windows, the shard-key table.  Only for krk_shutdown.
+static void teardown_device(Device& D) {
+    hipSetDevice(D.id);
+    for (hipStream_t s : {D.s_main, D.s_a, D.s_b})
+        if (s) hipStreamSynchronize(s);
+    delete D.staging;  // drains its windows' events
+    D.staging = nullptr;
+    {
+        std::lock_guard<std::mutex> g(D.cache.mu);
+        for (auto& kv : D.cache.idle) {
+            hipFree(kv.second.p);
+            if (kv.second.ev) hipEventDestroy(kv.second.ev);
+        }
+        D.cache.idle.clear();
+        for (auto& kv : D.cache.live) {  // none unless a call is in flight (contract)
+            hipFree(kv.second.p);
+            if (kv.second.ev) hipEventDestroy(kv.second.ev);
+        }
+        D.cache.live.clear();
+    }
+    for (auto& P : D.slots) {
+        if (P.ev) hipEventSynchronize(P.ev), hipEventDestroy(P.ev);
+        if (P.p) hipHostFree(P.p);
+        P = PinnedSlot();
+    }
+    for (void* p : {(void*)D.shard_kb, (void*)D.shard_koff, (void*)D.shard_bad, (void*)D.d_tabs})
+        if (p) hipFree(p);
+    for (hipStream_t s : {D.s_main, D.s_a, D.s_b})
+        if (s) hipStreamDestroy(s);
+}
+
 // File -> pinned window reads of one window, split over the copy threads at
 // 1 MiB-aligned spans (O_DIRECT needs block-aligned offsets and lengths; every
 // task starts 4 KiB-aligned in both the file and the window).
@@ -743,6 +775,43 @@ int krk_device_count(int* n) {
         if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
     }
     *n = good;
+    return KRK_OK;
+}
+
+int krk_init(uint64_t dev_mask) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error(KRK_ENODEV, "no HIP device visible");
+        return KRK_ENODEV;
+    }
+    const int saved = t_dev;
+    int r = KRK_OK;
+    for (int i = 0; i < n && i < 64 && !r; ++i) {
+        if (dev_mask ? !((dev_mask >> i) & 1) : i != saved) continue;
+        t_dev = i;
+        int rc = KRK_OK;
+        if (!device(&rc)) r = rc;
+    }
+    for (int i = n; i < 64 && !r; ++i)
+        if ((dev_mask >> i) & 1) {
+            set_error(KRK_ENODEV, "device %d out of range (%d visible)", i, n);
+            r = KRK_ENODEV;
+        }
+    t_dev = saved;
+    if (!r) {
+        int rc = KRK_OK;
+        device(&rc);  // restore the calling thread's current device
+    }
+    return r;
+}
+
+int krk_shutdown(void) {
+    std::lock_guard<std::mutex> g(g_dmu);
+    for (auto& D : g_devs)
+        if (D) {
+            teardown_device(*D);
+            D.reset();
+        }
     return KRK_OK;
 }
 

@@ -82,6 +82,17 @@ def set_device(d: int):
     check(lib.krk_set_device(d))
 
 
+def init(dev_mask: int = 0):
+    """Create device contexts eagerly (krk_init): bit i = device i, 0 = current."""
+    check(lib.krk_init(dev_mask))
+
+
+def shutdown():
+    """Free every device context and the pinned staging windows (krk_shutdown).
+    No library call may be in flight; later calls re-create contexts lazily."""
+    check(lib.krk_shutdown())
+
+
 def synchronize():
     check(lib.krk_synchronize())
 

@@ -63,3 +63,27 @@ def test_concurrent_callers_match_serial(gpu):
         for rounds in range(2):
             par = list(ex.map(_work, range(8)))
             assert par == serial
+
+
+def test_init_shutdown_reinit(gpu, orc):
+    """krk_init / krk_shutdown: contexts (and the kept staging windows) are freed and
+    re-created lazily; results are unchanged across the cycle.  A mask bit past the
+    visible devices is KRK_ENODEV."""
+    import numpy as np
+    from kraken_amd import device as Dv
+    from kraken_amd._capi import KRK_ENODEV, lib as L
+    rng = np.random.default_rng(5)
+    data = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in (1, 4097, (2 << 20) + 3)]
+    pls = [4096, 4096, 1 << 20]
+    Dv.init(0)
+    first = Dv.metainfo_digest_host(data, pls)
+    Dv.shutdown()
+    again = Dv.metainfo_digest_host(data, pls)  # lazily re-created context
+    Dv.shutdown()
+    Dv.init(1)
+    third = Dv.metainfo_digest_host(data, pls)
+    for r in (first, again, third):
+        for i, d in enumerate(data):
+            assert np.array_equal(r[0][i], orc.calc_piece_sums(d, pls[i])[1])
+            assert bytes(r[1][i]) == __import__("hashlib").sha256(d.tobytes()).digest()
+    assert L.krk_init(1 << 63) == KRK_ENODEV
