@@ -294,8 +294,11 @@ static int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_
     if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
     if (P.cap < n) {
         if (P.p) hipHostFree(P.p);
-        P.cap = std::max<size_t>(n, 1 << 20);
-        KRK_HIP(hipHostMalloc(&P.p, P.cap, hipHostMallocDefault));
+        P.p = nullptr;  // a failed grow leaves an empty slot, not a dangling one
+        P.cap = 0;
+        const size_t cap = std::max<size_t>(n, 1 << 20);
+        KRK_HIP(hipHostMalloc(&P.p, cap, hipHostMallocDefault));
+        P.cap = cap;
     }
     memcpy(P.p, src, n);
     KRK_HIP(hipMemcpyAsync(*d_out, P.p, n, hipMemcpyHostToDevice, s));
@@ -500,6 +503,23 @@ static ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
     memcpy(j.h, kIV, sizeof kIV);
     return j;
 }
+
+// Device allocations of one host-path call, freed on every return path (hipFree
+// waits for the device, so work still queued on them on an error path is drained).
+struct DevMem {
+    std::vector<void*> ps;
+    ~DevMem() {
+        for (void* p : ps) hipFree(p);
+    }
+    template <class T>
+    hipError_t alloc(T** p, size_t n) {
+        void* v = nullptr;
+        const hipError_t e = hipMalloc(&v, n);
+        if (e == hipSuccess) ps.push_back(v);
+        *p = static_cast<T*>(v);
+        return e;
+    }
+};
 
 // ------------------------------------------------------------------ host staging pipeline
 // Two pinned host windows and two device windows; window k is refilled only after
@@ -889,15 +909,13 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     if (hi == lo) return KRK_OK;
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
     uint32_t* d_sums = nullptr;
-    KRK_HIP(hipMalloc(&d_sums, hi * 4));
+    DevMem mem;
+    KRK_HIP(mem.alloc(&d_sums, hi * 4));
     KRK_HIP(hipMemset(d_sums, 0, hi * 4));
     const size_t W = window_bytes();
     StagingLease lease;
     r = lease_staging(D, W, lease);
-    if (r) {
-        hipFree(d_sums);
-        return r;
-    }
+    if (r) return r;
     Pipeline& pl = *lease.p;
     hipStream_t cp = D->s_a, ks = D->s_b;
     ItemBuilder B;
@@ -940,7 +958,6 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;
     }
-    hipFree(d_sums);
     return r;
 }
 
@@ -962,7 +979,8 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
     const bool want_direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
     uint32_t* d_sums = nullptr;
-    KRK_HIP(hipMalloc(&d_sums, hi * 4));
+    DevMem mem;
+    KRK_HIP(mem.alloc(&d_sums, hi * 4));
     KRK_HIP(hipMemset(d_sums, 0, hi * 4));
     const size_t W = window_bytes();  // a multiple of 1 MiB
     StagingLease lease;
@@ -1051,7 +1069,6 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;
     }
-    hipFree(d_sums);
     return r;
 }
 
@@ -1070,8 +1087,9 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     Pipeline& pl = *lease.p;
     uint8_t* d_dig = nullptr;
     uint32_t* d_state = nullptr;
-    KRK_HIP(hipMalloc(&d_dig, n * 32));
-    KRK_HIP(hipMalloc(&d_state, n * 32));
+    DevMem mem;
+    KRK_HIP(mem.alloc(&d_dig, n * 32));
+    KRK_HIP(mem.alloc(&d_state, n * 32));
     std::vector<uint64_t> off(n, 0);
     std::vector<char> done(n, 0);
     hipStream_t cp = D->s_a, ks = D->s_b;
@@ -1116,8 +1134,6 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
         set_error(KRK_EHIP, "digest copy-out failed");
         r = KRK_EHIP;
     }
-    hipFree(d_dig);
-    hipFree(d_state);
     return r;
 }
 
@@ -1212,9 +1228,10 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     Pipeline& pl = *lease.p;
     uint8_t* d_dig = nullptr;
     uint32_t *d_state = nullptr, *d_sums = nullptr;
-    KRK_HIP(hipMalloc(&d_dig, n * 32));
-    KRK_HIP(hipMalloc(&d_state, n * 32));
-    KRK_HIP(hipMalloc(&d_sums, std::max<uint64_t>(hi, 1) * 4));
+    DevMem mem;
+    KRK_HIP(mem.alloc(&d_dig, n * 32));
+    KRK_HIP(mem.alloc(&d_state, n * 32));
+    KRK_HIP(mem.alloc(&d_sums, std::max<uint64_t>(hi, 1) * 4));
     KRK_HIP(hipMemset(d_sums, 0, std::max<uint64_t>(hi, 1) * 4));
     std::vector<uint64_t> off(n, 0);
     std::vector<char> done(n, 0);
@@ -1298,9 +1315,6 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;
     }
-    hipFree(d_dig);
-    hipFree(d_state);
-    hipFree(d_sums);
     return r;
 }
 
