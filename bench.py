@@ -518,6 +518,13 @@ def run_chunked(a, D, T, rank, world, res):
                             "synth_fill": {"launches": gen_n, "total_ms": round(gen_ms, 1)}},
                 "note": "bounded below by the longest blob's sequential SHA-256 chain (longest_blob / per-stream "
                         "rate) at any GPU count"})
+    # Dominant kernel by device time: SHA-256 over every window (bytes / summed launch time).
+    if sha_n:
+        roof = roofline_obj("sha256_multi", bytes_rank / (sha_ms / 1e3) / 1e9, sha_ms / sha_n, bytes_rank / sha_n,
+                            None)
+        roof["note"] = ("per-stream issue-bound (DESIGN.md 4.2); the windows shrink as blobs finish, so late "
+                        "launches carry few streams")
+        res["roofline"] = roof
     if rank == 0:  # spot-check three blobs against the one-shot device path
         pick = sorted({0, n // 2, n - 1})
         dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
@@ -577,6 +584,17 @@ def run_hrw(a, D, T, rank, world, res):
                            "max_replica": R, "mode": "device-resident (65,536-shard table + gather)"},
                 "kernels": {"hrw_order": {"launches": hn, "avg_ms": round(hms / max(hn, 1), 3)},
                             "hrw_gather": {"launches": gn, "avg_ms": round(gms / max(gn, 1), 3)}}})
+    # Roofline of the per-digest kernel (the gather: HBM-bound, 32-B digest record in,
+    # R owner indices + a count out).  The shard-table kernel's work is fixed (65,536
+    # ShardIDs x N scores: murmur3 + Go math.Log, VALU/f64-bound, not per-digest).
+    g_avg = gms / max(gn, 1)
+    per_digest = 32 + 4 * R + 1
+    roof = roofline_obj("hrw_gather", n * per_digest / (g_avg / 1e3) / 1e9 if g_avg else 0.0, g_avg,
+                        n * per_digest, None)
+    roof["note"] = (f"algorithmic bytes per digest = {per_digest} (32-B digest record + {R} x 4-B owner "
+                    "indices + 1-B count); the hrw_order kernel (65,536-shard table, "
+                    f"{round(hms / max(hn, 1), 3)} ms) is VALU-bound and independent of the digest count")
+    res["roofline"] = roof
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cbl, cl, cc = cpu_baseline_hrw(dig, labels, healthy, R, a.cpu_seconds)
         cbl["outputs_match_gpu"] = bool(np.array_equal(cl, locs_h[:cl.shape[0]]))
