@@ -85,8 +85,9 @@ WORKLOADS = {
     "c4": dict(kind="pieces", desc="C4: one 20 GiB blob per GPU, 256 KiB pieces (81,920), piece sums only"),
     "c3": dict(kind="chunked", desc="C3: 20k blobs of 100 MiB + (rng mod 968,884,225) B, 4 MiB pieces, "
                                     "LPT-sharded by blob, streamed through HBM in windows"),
-    "c5": dict(kind="hrw", desc="C5: 1M seeded 32-B digests -> hashring.Locations (ShardID key), "
-                                "16 origins weight 100, MaxReplica 3, all healthy"),
+    "c5": dict(kind="hrw", steps=50, warmup=5,  # 0.4 ms steps: a few would time launch jitter
+               desc="C5: 1M seeded 32-B digests -> hashring.Locations (ShardID key), "
+                    "16 origins weight 100, MaxReplica 3, all healthy"),
 }
 
 
@@ -649,8 +650,8 @@ def hrw_sweep(D, dbuf, dig, n, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 3; C5: 50)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 1; C5: 5)")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--blobs", type=int, default=0, help="override the blob (or digest) count")
     ap.add_argument("--nodes", type=int, default=16, help="C5: origins in the ring")
@@ -664,6 +665,10 @@ def main():
     ap.add_argument("--no-sweep", action="store_true", help="C5: skip the N x MaxReplica x healthy grid")
     ap.add_argument("--e2e-mb", type=int, default=16, help="bytes per blob for the end-to-end leg (MiB)")
     a = ap.parse_args()
+    if a.steps is None:
+        a.steps = WORKLOADS[a.workload].get("steps", 3)
+    if a.warmup is None:
+        a.warmup = WORKLOADS[a.workload].get("warmup", 1)
 
     rank, world, local = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1), _env_int("LOCAL_RANK", 0)
     dist = None
