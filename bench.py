@@ -82,6 +82,9 @@ WORKLOADS = {
                                        "lengths from {0:1MB, 2GB:4MB, 4GB:8MB}"),
     "c5regen_digest": dict(kind="metainfo", desc="C5 regen blobs with the upload digest as well (metainfo + "
                                                  "SHA-256 per blob)"),
+    "f1verify": dict(kind="verify", desc="Agent piece verify (agentstorage.Torrent.writePiece, torrent.go:174-199): "
+                                         "4,096 received 4 MiB pieces in pageable host memory checked against "
+                                         "GetPieceSum in one pipelined GPU pass; 1 in 64 pieces corrupted"),
     "c4": dict(kind="pieces", desc="C4: one 20 GiB blob per GPU, 256 KiB pieces (81,920), piece sums only"),
     "c3": dict(kind="chunked", desc="C3: 20k blobs of 100 MiB + (rng mod 968,884,225) B, 4 MiB pieces, "
                                     "LPT-sharded by blob, streamed through HBM in windows"),
@@ -374,6 +377,68 @@ def run_regen(a, D, T, rank, world, res):
                  for k in range(m))
         cb["outputs_match_gpu"] = bool(ok)
         cb["sample"] += " (the CPU side times the CRC pass only; its InfoHash is not counted)"
+        res["cpu_baseline"] = cb
+
+
+def run_verify(a, D, T, rank, world, res):
+    """krk_verify_pieces_host over received pieces in host memory
+    (the h.Sum32() != GetPieceSum(pi) check of writePiece, batched).  Inputs are
+    host-resident by definition of this path, so `value` includes the PCIe pass."""
+    import ctypes as C
+    from kraken_amd import agentstorage
+    n, P = a.blobs or 4096, 4 << 20
+    ids = [(3 << 40) + rank * n + i for i in range(n)]
+    arena = D.BlobArena([P] * n, P, blob_ids=ids)  # device-generated piece content
+    out = D.BatchOutputs(arena)
+    D.piece_sums(arena, out)
+    D.synchronize()
+    expected = out.sums.to_host(np.uint32, n).copy()
+    host = np.empty(n * P, dtype=np.uint8)
+    for i in range(n):
+        D.check(D.lib.krk_memcpy_d2h(C.c_void_p(host.ctypes.data + i * P), arena.buf.ptr + int(arena.offsets[i]), P))
+    del out, arena
+    datas = [host[i * P:(i + 1) * P] for i in range(n)]
+    want = np.ones(n, dtype=bool)
+    want[::64] = False
+    exp = expected.copy()
+    exp[~want] ^= 0x5A5A5A5A  # corrupted pieces: GetPieceSum disagrees with the bytes
+    got = [None]
+
+    def step():
+        got[0] = agentstorage.verify_pieces(datas, exp)
+
+    for _ in range(a.warmup):
+        step()
+    T.barrier()
+    with D.KernelTimer():
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        T.barrier()
+        t1 = time.perf_counter()
+        crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
+    elapsed = T.max_over_ranks(t1 - t0)
+    bytes_rank = n * P
+    per_launch = bytes_rank * a.steps / max(crc_n, 1)
+    crc_avg = crc_ms / max(crc_n, 1)
+    roof = roofline_obj("crc32_pieces", per_launch / (crc_avg / 1e3) / 1e9 if crc_n else 0.0, crc_avg, per_launch,
+                        None)
+    roof["note"] = ("one CRC launch per pinned staging window; the call is bounded by the host -> device "
+                    "pass (pageable copy into pinned windows + PCIe), not by the kernel")
+    res.update({"metric": "agent piece-verify GB/s (host pieces, end to end)",
+                "value": round(world * bytes_rank * a.steps / elapsed / 1e9, 3), "unit": "GB/s", "steps": a.steps,
+                "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+                "dtype": "u8", "data": "synthetic (device-generated splitmix64 pieces, copied to pageable host memory)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "pieces_per_gpu": n, "piece_length": P,
+                           "bytes_per_gpu": bytes_rank, "mode": "host buffers (pageable), PCIe-inclusive"},
+                "roofline": roof, "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)}},
+                "verdicts_match": bool(np.array_equal(got[0], want))})
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        m = min(n, 2 * host_cores())
+        cb, _, sums = cpu_baseline_metainfo([P] * m, ids[:m], P, a.cpu_seconds, passes=2)
+        s_, off = sums
+        cb["outputs_match_gpu"] = bool(np.array_equal(np.asarray(s_[:m], dtype=np.uint32), expected[:m]))
+        cb["sample"] += " (one CRC per piece: the reference's hash.Hash32 per received piece)"
         res["cpu_baseline"] = cb
 
 
@@ -684,7 +749,8 @@ def main():
     T = Timer(D, dist)
     res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
     kind = WORKLOADS[a.workload]["kind"]
-    {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen}[kind](
+    {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen,
+     "verify": run_verify}[kind](
         a, D, T, rank, world, res)
     order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
              "vs_baseline", "dtype", "data", "config"]

@@ -60,6 +60,7 @@ for s in "$@"; do
     bc5r) step bench_c5regen 900 python bench.py --workload c5regen ;;
     bc5rd) step bench_c5regen_digest 900 python bench.py --workload c5regen_digest --steps 1 --warmup 1 ;;
     files) step probe_files 600 python tools/probe_files.py ;;
+    bf1) step bench_f1verify 600 python bench.py --workload f1verify ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-ceiling ;;
     pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-ceiling ;;
     pmcf4) step pmc_fetch_c4 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch_c4 -- python3 $R/bench.py --workload c4 --steps 1 --warmup 0 --no-cpu-baseline ;;
