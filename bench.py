@@ -514,6 +514,25 @@ def run_pieces(a, D, T, rank, world, res):
         res["cpu_baseline"] = cb
 
 
+def two_lane_stream_cap(D, n):
+    """Largest stream count <= n whose SHA launch plan is two lanes per stream."""
+    import ctypes as C
+    lanes = C.c_int()
+
+    def two(m):
+        D.check(D.lib.krk_sha_lanes_per_stream(m, C.byref(lanes)))
+        return lanes.value == 2
+    if n == 0 or two(n):
+        return max(n, 1)
+    lo, hi = 1, n  # two(lo) holds, two(hi) does not
+    if not two(lo):
+        return n
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        lo, hi = (mid, hi) if two(mid) else (lo, mid)
+    return lo
+
+
 def run_chunked(a, D, T, rank, world, res):
     """C3: every blob of this rank's LPT shard advances by one chunk per window; the
     next window's bytes are generated on the device (own stream) while the
@@ -529,15 +548,27 @@ def run_chunked(a, D, T, rank, world, res):
     D.check(D.lib.krk_stream_create(C.byref(run_s)))
 
     # Window plan: every live blob advances by the same 64-multiple chunk per window.
+    # Admission: at most `cap` blobs are live, admitted longest first, so the longest
+    # chain starts in window 0 and every window stays on the two-lane SHA plan (a
+    # launch of more streams falls back to one lane per stream, ~0.74x per stream,
+    # DESIGN.md 4.2); a finished blob's slot goes to the next-longest waiting blob.
     L = np.asarray(lens, dtype=np.uint64)
     ids_a = np.asarray(ids, dtype=np.uint64)
-    wins, pos, live = [], np.zeros(n, dtype=np.uint64), np.arange(n)
+    cap = n if a.no_admission else two_lane_stream_cap(D, n)
+    queue = list(np.argsort(-L.astype(np.int64), kind="stable"))
+    wins, pos = [], np.zeros(n, dtype=np.uint64)
+    live = np.asarray(sorted(queue[:cap]), dtype=np.int64)
+    queue = queue[cap:]
     while live.size:
         c = max(64, (W // live.size) // 64 * 64)
         take = np.minimum(np.uint64(c), L[live] - pos[live])
         wins.append((live, pos[live].copy(), take))
         pos[live] += take
         live = live[pos[live] < L[live]]
+        if queue and live.size < cap:
+            k = cap - live.size
+            live = np.sort(np.concatenate([live, np.asarray(queue[:k], dtype=np.int64)]))
+            queue = queue[k:]
 
     def items_of(k):
         blobs, offs, take = wins[k]
@@ -577,7 +608,7 @@ def run_chunked(a, D, T, rank, world, res):
                 "dtype": "u8", "data": "synthetic (generated on the device per window, inside the timed region)",
                 "config": {"workload": WORKLOADS["c3"]["desc"], "blobs_total": a.blobs or 20000,
                            "blobs_this_rank": n, "bytes_this_rank": bytes_rank, "bytes_total": total_bytes,
-                           "windows": len(wins), "window_bytes": W, "piece_length": P,
+                           "windows": len(wins), "window_bytes": W, "live_cap": int(cap), "piece_length": P,
                            "longest_blob": max(lens), "parallelism": f"LPT blob shard x{world}, no collective"},
                 "kernels": {"sha256_multi": {"launches": sha_n, "total_ms": round(sha_ms, 1)},
                             "crc32_pieces": {"launches": crc_n, "total_ms": round(crc_ms, 1)},
@@ -721,6 +752,8 @@ def main():
     ap.add_argument("--blobs", type=int, default=0, help="override the blob (or digest) count")
     ap.add_argument("--nodes", type=int, default=16, help="C5: origins in the ring")
     ap.add_argument("--window-gib", type=int, default=48, help="C3: device window size")
+    ap.add_argument("--no-admission", action="store_true",
+                    help="C3: all blobs live from window 0 (no longest-first admission under the two-lane cap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
