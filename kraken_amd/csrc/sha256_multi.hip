@@ -455,7 +455,10 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 
 // The 64 rounds of one block on a lane pair: 66 instruction-rounds (the A lane
 // idles in the first two, the E lane in the last two).  h[] = this lane's half of
-// the state (A: H0..H3, E: H4..H7), fed forward at the end.  W is read from LDS
+// the state, fed forward at the end: E holds (H4, H5, H6, H7), A holds
+// (H2, H3, H0, H1) -- index k ^ 2 -- so that both lanes enter the first round from
+// h[0], h[1] and feed h[0], h[1] forward from the same registers (no per-lane
+// selects there; only h[2], h[3] need one).  W is read from LDS
 // slot cslot (the E lanes: the block's ring slot; the A lanes: the all-1 slot).
 // Quads 0..2 arrive already loaded in k[]; the rest are read three quads ahead
 // (quad q+1's first W feeds quad q's last z, so a read issued one quad before its
@@ -467,7 +470,7 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
     // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
     // its own starts, so A starts at (H2, H3) and its two results are replaced by
     // H1 and H0.
-    uint32_t R0 = is_e ? h[0] : h[2], R3 = is_e ? h[1] : h[3], R2 = h[2], R1 = h[3], z;
+    uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z;
     // W ring: quad q lives in wq[q % 4]
     u32x4 wq[4];
     wq[1] = k[1];
@@ -486,14 +489,14 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
                      KRK_SHA2_OPERANDS
                      : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
     }
-    R1 = is_e ? R1 : h[1];
+    R1 = is_e ? R1 : h[3];
     {
         uint32_t t1, t2, t3, kk, p;
         asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
                      KRK_SHA2_OPERANDS
                      : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
     }
-    R2 = is_e ? R2 : h[0];
+    R2 = is_e ? R2 : h[2];
     {
         uint32_t t1, t2, t3, kk, p;
         asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
@@ -527,10 +530,12 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
                      KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
                      : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
     }
-    h[0] += is_e ? R0 : T2;
-    h[1] += is_e ? R3 : T1;
-    h[2] += is_e ? R2 : R0;
-    h[3] += is_e ? R1 : R3;
+    // E: (e, f, g, h) = (R0, R3, R2, R1); A: (a, b, c, d) = (T2, T1, R0, R3) into
+    // its (H2, H3, H0, H1) order.
+    h[0] += R0;
+    h[1] += R3;
+    h[2] += is_e ? R2 : T2;
+    h[3] += is_e ? R1 : T1;
 }
 #undef KRK_SHA2_OPERANDS
 #undef KRK_SHA2_CONSTS
@@ -627,49 +632,67 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         const bool is_e = two_lane_is_e(lane);
         const uint32_t half = is_e ? 4u : 0u;
         const TwoLaneConst c{is_e ? 6u : 2u, is_e ? 11u : 13u, is_e ? 25u : 22u, is_e ? 0u : ~0u, is_e ? 0u : 1u};
+        // h[k] = H[4 + k] on E lanes, H[k ^ 2] on A lanes (rounds2's register order).
         uint32_t h[4];
         if (live && (job.flags & kShaFromState)) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) h[k] = out_state[8 * (uint64_t)job.out + half + k];
+            for (int k = 0; k < 4; ++k) h[k] = out_state[8 * (uint64_t)job.out + half + (is_e ? k : k ^ 2)];
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) h[k] = is_e ? job.h[4 + k] : job.h[k];  // no dynamic index: keeps job out of scratch
+            for (int k = 0; k < 4; ++k) h[k] = is_e ? job.h[4 + k] : job.h[k ^ 2];  // no dynamic index: keeps job out of scratch
         }
         __builtin_amdgcn_s_setprio(3);
+        // Blocks every live lane still needs (wave-uniform): no per-lane masking there.
+        const uint32_t common = wave_min(live ? mine : ~0u);
+        // kw2_base without the per-block slot arithmetic: the loop runs one producer
+        // step (an even and an odd block, one slot) per iteration; vslot = the E
+        // lanes' slot offset (the A lanes always read the all-1 slot, vslot = 0).
+        const uint32_t aoff = is_e ? 0u : uint32_t(kRing2) * kSlotWords;
+        const uint32_t base_even = aoff + (lane ^ 15u) * 4, base_odd = aoff + lane * 4;
+        const uint32_t einc = is_e ? uint32_t(kSlotWords) : 0u;
+        uint32_t vslot = 0, slot = 0;
         u32x4 kq[3] = {};
 #ifdef KRK_SHA_CYCLES  // diagnostic build (make cycles): consumer cycles per block
         const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef KRK_SHA_CYCLES
         uint64_t cyc_bar = 0, cyc_rounds = 0;
 #endif
-        for (uint32_t i = 0; i < nb; ++i) {
-#ifdef KRK_SHA_CYCLES
-            const uint64_t cb0 = __builtin_amdgcn_s_memtime();
-#endif
-            if (kTiming == 0 && i % kStep == 0) __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (i == 0) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    kq[q] = *reinterpret_cast<const u32x4*>(ring + kw2_base(0, is_e, lane) + 256 * q);
-            }
+        auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
             uint32_t x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = h[k];
+            rounds2(x, ring, cur, nxt, lane, c, is_e, kq);
+            if (i < common) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) h[k] = x[k];
+            } else if (i < mine) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) h[k] = x[k];
+            }
+        };
+        for (uint32_t i = 0; i < nb; i += 2) {
+#ifdef KRK_SHA_CYCLES
+            const uint64_t cb0 = __builtin_amdgcn_s_memtime();
+#endif
+            if (kTiming == 0) __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (i == 0) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
+            }
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb1 = __builtin_amdgcn_s_memtime();
 #endif
-            rounds2(x, ring, kw2_base(i, is_e, lane), kw2_base(i + 1, is_e, lane), lane, c, is_e, kq);
+            const uint32_t nslot = slot == kRing2 - 1 ? 0u : slot + 1;
+            const uint32_t nvslot = slot == kRing2 - 1 ? 0u : vslot + einc;
+            block(i, base_even + vslot, base_odd + vslot);
+            if (i + 1 < nb) block(i + 1, base_odd + vslot, base_even + nvslot);
+            slot = nslot;
+            vslot = nvslot;
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb2 = __builtin_amdgcn_s_memtime();
             cyc_bar += cb1 - cb0;
             cyc_rounds += cb2 - cb1;
 #endif
-            if (i < mine) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) h[k] = x[k];
-            }
         }
 #ifdef KRK_SHA_CYCLES
         if (blockIdx.x == 0 && lane == 0 && nb)
@@ -678,17 +701,21 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
                    (double)cyc_rounds / nb);
 #endif
         if (live) {
+            uint32_t hs[4];  // back to H order (A lanes hold H[k ^ 2] in h[k])
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hs[k] = is_e ? h[k] : h[k ^ 2];
             if (job.flags & kShaFinal) {
                 uint8_t* o = out_digest + 32 * (uint64_t)job.out + 4 * half;
                 if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
-                    reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+                    reinterpret_cast<uint4*>(o)[0] =
+                        make_uint4(bswap(hs[0]), bswap(hs[1]), bswap(hs[2]), bswap(hs[3]));
                 } else {
-                    for (int k = 0; k < 16; ++k) o[k] = (uint8_t)(h[k >> 2] >> (24 - 8 * (k & 3)));
+                    for (int k = 0; k < 16; ++k) o[k] = (uint8_t)(hs[k >> 2] >> (24 - 8 * (k & 3)));
                 }
             } else {
                 uint32_t* o = out_state + 8 * (uint64_t)job.out + half;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) o[k] = h[k];
+                for (int k = 0; k < 4; ++k) o[k] = hs[k];
             }
         }
     } else {
