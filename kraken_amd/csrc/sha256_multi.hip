@@ -460,25 +460,32 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 // h[0], h[1] and feed h[0], h[1] forward from the same registers (no per-lane
 // selects there; only h[2], h[3] need one).  W is read from LDS
 // slot cslot (the E lanes: the block's ring slot; the A lanes: the all-1 slot).
-// Quads 0..2 arrive already loaded in k[]; the rest are read three quads ahead
-// (quad q+1's first W feeds quad q's last z, so a read issued one quad before its
-// use would stall: ~230 cycles a block), and quads 0..2 of the next block (slot
-// ncslot) are read into k[] during the last quads.
+// Quads 0..kAhead-1 arrive already loaded in k[]; the rest are read kAhead quads
+// ahead (quad q+1's first W feeds quad q's last z, so the read of quad q+1 must have
+// landed when quad q starts: issued one quad before its use it stalled ~230 cycles a
+// block), and quads 0..kAhead-1 of the next block (slot ncslot) are read into k[]
+// during the last quads.
+#ifndef KRK_SHA_AHEAD
+#define KRK_SHA_AHEAD 3
+#endif
+constexpr int kAhead = KRK_SHA_AHEAD;
+static_assert(kAhead >= 2 && kAhead <= 8, "read-ahead distance");
 __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
-                                        uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[3]) {
+                                        uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[kAhead]) {
     // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
     // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
     // its own starts, so A starts at (H2, H3) and its two results are replaced by
     // H1 and H0.
     uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z;
-    // W ring: quad q lives in wq[q % 4]
-    u32x4 wq[4];
-    wq[1] = k[1];
-    wq[2] = k[2];
+    // W ring: quad q lives in wq[q % kRS]
+    constexpr int kRS = kAhead + 1;
+    u32x4 wq[kRS];
+#pragma unroll
+    for (int j = 1; j < kAhead; ++j) wq[j] = k[j];
 #ifdef KRK_SHA_NOLDS  // diagnostic: W from registers (wrong digests) -- prices the LDS reads
-    wq[3] = u32x4{3u, lane, cbase, 7u};
+    wq[kAhead] = u32x4{3u, lane, cbase, 7u};
 #else
-    wq[3] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * 3);
+    wq[kAhead] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * kAhead);
 #endif
     {
         uint32_t t1, t2, t3, kk, p;
@@ -506,19 +513,20 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
     }
 #pragma unroll
     for (int q = 1; q < 16; ++q) {
-        if (q + 3 < 16) {
+        if (q + kAhead < 16) {
 #ifdef KRK_SHA_NOLDS
-            wq[(q + 3) & 3] = u32x4{(uint32_t)q, lane, cbase, 7u};
+            wq[(q + kAhead) % kRS] = u32x4{(uint32_t)q, lane, cbase, 7u};
 #else
-            wq[(q + 3) & 3] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + 3));
+            wq[(q + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + kAhead));
 #endif
         }
-        // The next block's first three quads, read unconditionally (a slot is always
+        // The next block's first kAhead quads, read unconditionally (a slot is always
         // mapped LDS; past the last block the values go unused) so that no branch
         // sinks them to the end of the block, where their latency would be exposed.
-        if (q >= 13) k[q - 13] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - 13));
-        const u32x4& cur = wq[q & 3];
-        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) & 3][0] : c.one_a);
+        if (q >= 16 - kAhead)
+            k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
+        const u32x4& cur = wq[q % kRS];
+        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : c.one_a);
     }
     // Instruction-rounds 64, 65: A runs rounds 62, 63 into T1, T2 (W = 1 on A lanes);
     // the E lanes' registers keep their final state.
@@ -651,7 +659,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         const uint32_t base_even = aoff + (lane ^ 15u) * 4, base_odd = aoff + lane * 4;
         const uint32_t einc = is_e ? uint32_t(kSlotWords) : 0u;
         uint32_t vslot = 0, slot = 0;
-        u32x4 kq[3] = {};
+        u32x4 kq[kAhead] = {};
 #ifdef KRK_SHA_CYCLES  // diagnostic build (make cycles): consumer cycles per block
         const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
         uint64_t cyc_bar = 0, cyc_rounds = 0;
@@ -677,7 +685,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             asm volatile("" ::: "memory");
             if (i == 0) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
+                for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
             }
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb1 = __builtin_amdgcn_s_memtime();
