@@ -516,6 +516,33 @@ def run_pieces(a, D, T, rank, world, res):
         res["cpu_baseline"] = cb
 
 
+def c3_window_plan(lens, W, cap):
+    """C3 windows: [(blob indices, offsets, chunk lengths)].  Every live blob advances by
+    the same 64-multiple chunk per window (about W bytes a window).  Admission: at most
+    `cap` blobs are live, admitted longest first, so the longest chain starts in window 0
+    and every window stays on the two-lane SHA plan (a launch of more streams falls back
+    to one lane per stream, ~0.74x per stream); a finished blob's slot goes
+    to the next-longest waiting blob."""
+    L = np.asarray(lens, dtype=np.uint64)
+    n = L.size
+    cap = max(1, min(int(cap), n)) if n else 1
+    queue = list(np.argsort(-L.astype(np.int64), kind="stable"))
+    wins, pos = [], np.zeros(n, dtype=np.uint64)
+    live = np.asarray(sorted(queue[:cap]), dtype=np.int64)
+    queue = queue[cap:]
+    while live.size:
+        c = max(64, (W // live.size) // 64 * 64)
+        take = np.minimum(np.uint64(c), L[live] - pos[live])
+        wins.append((live, pos[live].copy(), take))
+        pos[live] += take
+        live = live[pos[live] < L[live]]
+        if queue and live.size < cap:
+            k = cap - live.size
+            live = np.sort(np.concatenate([live, np.asarray(queue[:k], dtype=np.int64)]))
+            queue = queue[k:]
+    return wins
+
+
 def two_lane_stream_cap(D, n):
     """Largest stream count <= n whose SHA launch plan is two lanes per stream."""
     import ctypes as C
@@ -549,28 +576,9 @@ def run_chunked(a, D, T, rank, world, res):
     D.check(D.lib.krk_stream_create(C.byref(gen_s)))
     D.check(D.lib.krk_stream_create(C.byref(run_s)))
 
-    # Window plan: every live blob advances by the same 64-multiple chunk per window.
-    # Admission: at most `cap` blobs are live, admitted longest first, so the longest
-    # chain starts in window 0 and every window stays on the two-lane SHA plan (a
-    # launch of more streams falls back to one lane per stream, ~0.74x per stream,
-    # DESIGN.md 4.2); a finished blob's slot goes to the next-longest waiting blob.
-    L = np.asarray(lens, dtype=np.uint64)
     ids_a = np.asarray(ids, dtype=np.uint64)
     cap = n if a.no_admission else two_lane_stream_cap(D, n)
-    queue = list(np.argsort(-L.astype(np.int64), kind="stable"))
-    wins, pos = [], np.zeros(n, dtype=np.uint64)
-    live = np.asarray(sorted(queue[:cap]), dtype=np.int64)
-    queue = queue[cap:]
-    while live.size:
-        c = max(64, (W // live.size) // 64 * 64)
-        take = np.minimum(np.uint64(c), L[live] - pos[live])
-        wins.append((live, pos[live].copy(), take))
-        pos[live] += take
-        live = live[pos[live] < L[live]]
-        if queue and live.size < cap:
-            k = cap - live.size
-            live = np.sort(np.concatenate([live, np.asarray(queue[:k], dtype=np.int64)]))
-            queue = queue[k:]
+    wins = c3_window_plan(lens, W, cap)
 
     def items_of(k):
         blobs, offs, take = wins[k]

@@ -151,3 +151,44 @@ def test_generate_error_wrapping(tmp_path):
     open(os.path.join(cas._dir(d.Hex()), "data"), "wb").close()
     with pytest.raises(IOError, match=r"^get cache file: permission denied"):
         metainfogen.New({0: 1 << 20}, Unreadable(str(tmp_path))).Generate(d)
+
+
+def _plan_checks(lens, W, cap):
+    import bench
+    wins = bench.c3_window_plan(lens, W, cap)
+    L = np.asarray(lens, dtype=np.uint64)
+    covered = np.zeros(len(lens), dtype=np.uint64)
+    started = {}
+    for k, (blobs, offs, take) in enumerate(wins):
+        assert 0 < blobs.size <= max(1, min(cap, len(lens)))
+        assert np.array_equal(offs, covered[blobs])  # each chunk continues its blob
+        assert np.all(take > 0)
+        # every chunk but a blob's last is a multiple of 64 (whole SHA-256 blocks)
+        last = offs + take == L[blobs]
+        assert np.all(take[~last] % 64 == 0)
+        covered[blobs] += take
+        for b in blobs.tolist():
+            started.setdefault(b, k)
+    assert np.array_equal(covered, L)  # every byte exactly once
+    return wins, started
+
+
+def test_c3_window_plan_admits_longest_first_under_cap():
+    """bench.c3_window_plan: bytes covered exactly once, <= cap live blobs a window,
+    and a blob never starts after a shorter one."""
+    rng = np.random.default_rng(7)
+    lens = [int(x) for x in rng.integers(1, 5000, size=300)] + [0 + 64, 12_345, 64 * 1000]
+    W, cap = 64 * 1024, 37
+    wins, started = _plan_checks(lens, W, cap)
+    order = sorted(range(len(lens)), key=lambda i: (-lens[i], i))
+    starts = [started[i] for i in order]
+    assert starts == sorted(starts)
+    assert started[order[0]] == 0
+
+
+def test_c3_window_plan_no_cap_and_single_blob():
+    lens = [1000, 64, 129, 5000]
+    wins, started = _plan_checks(lens, 4096, len(lens))
+    assert all(v == 0 for v in started.values())  # all live from window 0
+    wins, _ = _plan_checks([10**6], 1 << 16, 16384)
+    assert len(wins) == -(-10**6 // (1 << 16))
