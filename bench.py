@@ -661,13 +661,18 @@ def run_hrw(a, D, T, rank, world, res):
     dig = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     dbuf = D.DeviceBuffer(n * 32)
     dbuf.from_host(dig.reshape(-1))
-    locs = D.DeviceBuffer(n * R * 4)
+    # Owner lists as uint8 node indices (krk_ring_locations_u8_dev) when the ring has
+    # <= 255 nodes: a quarter of the bytes to write and to copy back; int32 otherwise.
+    compact = N <= 255 and not a.hrw_int32
+    isz = 1 if compact else 4
+    locs = D.DeviceBuffer(n * R * isz)
     counts = D.DeviceBuffer(n)
-    pin = D.PinnedArray((n, R), np.int32)  # owner lists gathered to pinned host memory
+    pin = D.PinnedArray((n, R), np.uint8 if compact else np.int32)  # owner lists gathered to pinned host memory
     locs_h = pin.a
+    place = D.ring_locations_u8_dev if compact else D.ring_locations_dev
 
     def step():
-        D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts)
+        place(dbuf, n, labels, healthy, R, locs, counts)
         D.synchronize()
         pin.fill_from(locs)
 
@@ -688,23 +693,27 @@ def run_hrw(a, D, T, rank, world, res):
                 "higher_is_better": True, "scaling": "weak", "dtype": "u64+f64",
                 "data": "synthetic (seeded random 32-byte digests)",
                 "config": {"workload": WORKLOADS["c5"]["desc"], "digests_per_gpu": n, "nodes": N,
-                           "max_replica": R, "mode": "device-resident (65,536-shard table + gather)"},
+                           "max_replica": R, "mode": "device-resident (65,536-shard table + gather)",
+                           "owner_index_bytes": isz},
                 "kernels": {"hrw_order": {"launches": hn, "avg_ms": round(hms / max(hn, 1), 3)},
                             "hrw_gather": {"launches": gn, "avg_ms": round(gms / max(gn, 1), 3)}}})
     # Roofline of the per-digest kernel (the gather: HBM-bound, 32-B digest record in,
     # R owner indices + a count out).  The shard-table kernel's work is fixed (65,536
     # ShardIDs x N scores: murmur3 + Go math.Log, VALU/f64-bound, not per-digest).
     g_avg = gms / max(gn, 1)
-    per_digest = 32 + 4 * R + 1
+    per_digest = 32 + isz * R + 1
     roof = roofline_obj("hrw_gather", n * per_digest / (g_avg / 1e3) / 1e9 if g_avg else 0.0, g_avg,
                         n * per_digest, None)
-    roof["note"] = (f"algorithmic bytes per digest = {per_digest} (32-B digest record + {R} x 4-B owner "
+    roof["note"] = (f"algorithmic bytes per digest = {per_digest} (32-B digest record + {R} x {isz}-B owner "
                     "indices + 1-B count); the hrw_order kernel (65,536-shard table, "
                     f"{round(hms / max(hn, 1), 3)} ms) is VALU-bound and independent of the digest count")
     res["roofline"] = roof
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cbl, cl, cc = cpu_baseline_hrw(dig, labels, healthy, R, a.cpu_seconds)
-        cbl["outputs_match_gpu"] = bool(np.array_equal(cl, locs_h[:cl.shape[0]]))
+        got = locs_h[:cl.shape[0]].astype(np.int32)
+        if compact:
+            got[got == 255] = -1
+        cbl["outputs_match_gpu"] = bool(np.array_equal(cl, got))
         res["cpu_baseline"] = cbl
     if rank == 0 and world == 1 and not a.no_sweep:
         res["sweep"] = hrw_sweep(D, dbuf, dig, n, a.steps)
@@ -727,14 +736,14 @@ def hrw_sweep(D, dbuf, dig, n, steps):
         if hf < 1.0:
             rng = np.random.default_rng(0x75 + N)
             healthy[rng.choice(N, N - int(round(N * hf)), replace=False)] = 0
-        locs = D.DeviceBuffer(n * R * 4)
+        locs = D.DeviceBuffer(n * R)
         counts = D.DeviceBuffer(n)
-        pin = D.PinnedArray((n, R), np.int32)
-        D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts, weights=weights)
+        pin = D.PinnedArray((n, R), np.uint8)  # compact owner lists (every grid ring has <= 64 nodes)
+        D.ring_locations_u8_dev(dbuf, n, labels, healthy, R, locs, counts, weights=weights)
         D.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):  # same step as the headline C5 line: results gathered to host
-            D.ring_locations_dev(dbuf, n, labels, healthy, R, locs, counts, weights=weights)
+            D.ring_locations_u8_dev(dbuf, n, labels, healthy, R, locs, counts, weights=weights)
             D.synchronize()
             pin.fill_from(locs)
         el = time.perf_counter() - t0
@@ -764,6 +773,7 @@ def main():
     ap.add_argument("--window-gib", type=int, default=48, help="C3: device window size")
     ap.add_argument("--no-admission", action="store_true",
                     help="C3: all blobs live from window 0 (no longest-first admission under the two-lane cap)")
+    ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))

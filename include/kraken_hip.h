@@ -235,6 +235,12 @@ int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* no
 int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
                            const uint8_t* healthy, int32_t max_replica,
                            int32_t* locs_dev, uint8_t* counts_dev, void* stream);
+/* Compact form for rings of <= 255 nodes (KRK_ERANGE beyond): owner indices as
+ * uint8 (0xFF padded), a quarter of the bytes the caller copies back.  Same
+ * ring.Locations semantics (lib/hashring/ring.go:91-118) as krk_ring_locations_dev. */
+int krk_ring_locations_u8_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                              const uint8_t* healthy, int32_t max_replica,
+                              uint8_t* locs_dev, uint8_t* counts_dev, void* stream);
 
 /* ----------------------------------------------------- synthetic blobs
  * Fills a device buffer with bytes [offset, offset+n) of synthetic blob

@@ -182,23 +182,42 @@ hipError_t launch_ring_filter(const int32_t* order, uint64_t n_rows, uint32_t n_
 
 // Locations(d) depends on d only through ShardID = hex[:4] (core/digest.go:148-150),
 // i.e. the first two digest bytes: gather the precomputed row.
+// One thread per digest: its ShardID row of the owner table.  T = int32_t (-1 pad) or
+// uint8_t (compact owner lists for rings of <= 255 nodes: 0xFF pad, a quarter of the
+// bytes to write and to copy back to the host).
+template <typename T>
 __global__ void shard_gather_kernel(const uint8_t* digests32, uint64_t n, const int32_t* tl,
-                                    const uint8_t* tc, uint32_t row_out, int32_t* locs,
-                                    uint8_t* counts) {
+                                    const uint8_t* tc, uint32_t row_out, T* locs, uint8_t* counts) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t shard = (uint32_t)digests32[32 * i] << 8 | digests32[32 * i + 1];
-    for (uint32_t q = 0; q < row_out; ++q) locs[i * row_out + q] = tl[(uint64_t)shard * row_out + q];
+    for (uint32_t q = 0; q < row_out; ++q) {
+        const int32_t v = tl[(uint64_t)shard * row_out + q];
+        locs[i * row_out + q] = sizeof(T) == 1 ? (T)(v < 0 ? 0xFF : v) : (T)v;
+    }
     counts[i] = tc[shard];
+}
+
+template <typename T>
+static hipError_t launch_gather(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
+                                const uint8_t* table_counts, uint32_t row_out, T* locs, uint8_t* counts,
+                                hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(shard_gather_kernel<T>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       digests32, n, table_locs, table_counts, row_out, locs, counts);
+    return hipGetLastError();
 }
 
 hipError_t launch_shard_gather(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
                                const uint8_t* table_counts, uint32_t row_out, int32_t* locs,
                                uint8_t* counts, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(shard_gather_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                       digests32, n, table_locs, table_counts, row_out, locs, counts);
-    return hipGetLastError();
+    return launch_gather(digests32, n, table_locs, table_counts, row_out, locs, counts, s);
+}
+
+hipError_t launch_shard_gather_u8(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
+                                  const uint8_t* table_counts, uint32_t row_out, uint8_t* locs,
+                                  uint8_t* counts, hipStream_t s) {
+    return launch_gather(digests32, n, table_locs, table_counts, row_out, locs, counts, s);
 }
 
 }  // namespace krk

@@ -128,6 +128,9 @@ hipError_t launch_ring_filter(const int32_t* order, uint64_t n_rows, uint32_t n_
 hipError_t launch_shard_gather(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
                                const uint8_t* table_counts, uint32_t row_out, int32_t* locs,
                                uint8_t* counts, hipStream_t s);
+hipError_t launch_shard_gather_u8(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
+                                  const uint8_t* table_counts, uint32_t row_out, uint8_t* locs,
+                                  uint8_t* counts, hipStream_t s);
 
 // ---------------------------------------------------------------- synthetic data
 // One synthetic chunk: bytes [offset, offset + n) of the blob whose stream seed is `seed`.

@@ -1797,11 +1797,17 @@ int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* no
     return KRK_OK;
 }
 
-int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
-                           const uint8_t* healthy, int32_t max_replica, int32_t* locs_dev, uint8_t* counts_dev,
-                           void* stream) {
+}  // extern "C"
+
+template <typename T>
+static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                              const uint8_t* healthy, int32_t max_replica, T* locs_dev, uint8_t* counts_dev,
+                              void* stream) {
     if (!n) return KRK_OK;
-    KRK_CHECK(digests32_dev && healthy && locs_dev && counts_dev, KRK_EINVAL, "ring_locations_dev: null argument");
+    KRK_CHECK(digests32_dev && healthy && locs_dev && counts_dev && nodes, KRK_EINVAL,
+              "ring_locations_dev: null argument");
+    KRK_CHECK(sizeof(T) != 1 || nodes->n_nodes <= 255, KRK_ERANGE,
+              "ring_locations_u8_dev: %u nodes do not fit 8-bit owner indices (<= 255)", nodes->n_nodes);
     KRK_DEVICE(D);
     hipStream_t s = pick(D, stream);
     const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
@@ -1825,13 +1831,30 @@ int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_n
                           &d_tl, &d_tc, s);
     if (!r) {
         hipError_t e = timed(K_GATHER, s, [&] {
-            return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
+            if constexpr (sizeof(T) == 1)
+                return launch_shard_gather_u8(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
+            else
+                return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
         });
         if (e != hipSuccess) { set_error(KRK_EHIP, "gather launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
     if (d_tl) scratch_free(D, d_tl, s);
     if (d_tc) scratch_free(D, d_tc, s);
     return r;
+}
+
+extern "C" {
+
+int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                           const uint8_t* healthy, int32_t max_replica, int32_t* locs_dev, uint8_t* counts_dev,
+                           void* stream) {
+    return ring_locations_dev(digests32_dev, n, nodes, healthy, max_replica, locs_dev, counts_dev, stream);
+}
+
+int krk_ring_locations_u8_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                              const uint8_t* healthy, int32_t max_replica, uint8_t* locs_dev, uint8_t* counts_dev,
+                              void* stream) {
+    return ring_locations_dev(digests32_dev, n, nodes, healthy, max_replica, locs_dev, counts_dev, stream);
 }
 
 // ---------------------------------------------------------------- synthetic data

@@ -282,6 +282,17 @@ def ring_locations_dev(digests_dev: DeviceBuffer, n: int, labels, healthy, max_r
     del keep
 
 
+def ring_locations_u8_dev(digests_dev: DeviceBuffer, n: int, labels, healthy, max_replica: int,
+                          locs_dev: DeviceBuffer, counts_dev: DeviceBuffer, stream=None, weights=None):
+    """ring_locations_dev with uint8 owner indices (0xFF padded) for rings of <= 255 nodes:
+    a quarter of the owner-list bytes to copy back (krk_ring_locations_u8_dev)."""
+    s, keep = nodes_struct(labels, [100] * len(labels) if weights is None else weights)
+    h = np.ascontiguousarray(healthy, dtype=np.uint8)
+    check(lib.krk_ring_locations_u8_dev(digests_dev.ptr, n, C.byref(s), h.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                         max_replica, locs_dev.ptr, counts_dev.ptr, stream))
+    del keep
+
+
 class KernelTimer:
     """hipEvent-based per-kernel device time (recorded on each kernel's stream)."""
 

@@ -148,3 +148,38 @@ def test_cas_volume_placement(gpu, orc, tmp_path):
     castore.initCASVolumes(str(d), vols)  # idempotent
     with pytest.raises(OSError, match="verify volume"):
         castore.initCASVolumes(str(d), [castore.Volume(str(tmp_path / "missing"), 100)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes,max_replica", [(16, 3), (255, 2), (5, 8)])
+def test_ring_locations_u8_dev_equals_int32_path(gpu, orc, n_nodes, max_replica):
+    """krk_ring_locations_u8_dev: the same owner lists as the int32 path (0xFF where it
+    pads -1), counts identical; spot rows against the oracle."""
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(n_nodes)]
+    rng = np.random.default_rng(1000 + n_nodes)
+    healthy = (rng.random(n_nodes) < 0.75).astype(np.uint8)
+    n = 30001
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    l32, c32 = D.DeviceBuffer(n * max_replica * 4), D.DeviceBuffer(n)
+    l8, c8 = D.DeviceBuffer(n * max_replica), D.DeviceBuffer(n)
+    D.ring_locations_dev(dbuf, n, labels, healthy, max_replica, l32, c32)
+    D.ring_locations_u8_dev(dbuf, n, labels, healthy, max_replica, l8, c8)
+    D.synchronize()
+    a32 = l32.to_host(np.int32, n * max_replica).reshape(n, max_replica)
+    a8 = l8.to_host(np.uint8, n * max_replica).reshape(n, max_replica)
+    assert np.array_equal(np.where(a32 < 0, 255, a32).astype(np.uint8), a8)
+    assert np.array_equal(c32.to_host(np.uint8, n), c8.to_host(np.uint8, n))
+    for i in range(0, n, 997):
+        key = bytes(digests[i, :2]).hex()
+        want = orc.ring_locations(orc.hrw_ordered(key, labels, [100] * n_nodes), healthy, max_replica)
+        assert a8[i, : len(want)].tolist() == want
+
+
+@pytest.mark.gpu
+def test_ring_locations_u8_dev_rejects_256_nodes(gpu):
+    labels = [f"o{i}" for i in range(256)]
+    dbuf, lb, cb = D.DeviceBuffer(32), D.DeviceBuffer(3), D.DeviceBuffer(1)
+    with pytest.raises(Exception, match="255"):
+        D.ring_locations_u8_dev(dbuf, 1, labels, np.ones(256, np.uint8), 3, lb, cb)
