@@ -191,6 +191,14 @@ int krk_info_hash(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
  * blob i has piece_lengths[i], sums[sums_off[i] .. sums_off[i] + n_sums[i]), name
  * names[name_off[i] .. name_off[i+1]), length lengths[i]; out20 receives 20*n bytes.
  * Spread over host threads.  names may be NULL when every name is empty. */
+/* Generator.Generate over device-resident blobs (lib/metainfogen/generator.go:41-58 ->
+ * core.NewMetaInfo, core/metainfo.go:53-79): every blob's piece sums (sums_dev, also
+ * copied to sums_host at blobs[i].sums_offset) and its InfoHash (info_hash20, 20 B a
+ * blob; names/name_off = the blobs' digest hex, the info Name).  The batch runs as up to
+ * 8 groups of about equal bytes back to back on `stream`; each group's sums are copied
+ * back and hashed on host threads while the later groups' kernels run.  Synchronous. */
+int krk_metainfo_batch_dev(const krk_blob* blobs, uint64_t n_blobs, const char* names, const uint64_t* name_off,
+                           uint32_t* sums_dev, uint32_t* sums_host, uint8_t* info_hash20, void* stream);
 int krk_info_hash_batch(const int64_t* piece_lengths, const uint32_t* sums, const uint64_t* sums_off,
                         const uint64_t* n_sums, const char* names, const uint64_t* name_off,
                         const int64_t* lengths, uint64_t n, uint8_t* out20);

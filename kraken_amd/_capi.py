@@ -64,6 +64,7 @@ def _load() -> C.CDLL:
         "krk_synchronize": (i, []),
         "krk_num_pieces": (C.c_uint64, [C.c_uint64, C.c_int64]),
         "krk_piece_sums_dev": (i, [blobp, C.c_uint64, vp, vp]),
+        "krk_metainfo_batch_dev": (i, [blobp, C.c_uint64, C.c_char_p, u64p, vp, u32p, C.POINTER(C.c_uint8), vp]),
         "krk_piece_sums_host": (i, [blobp, C.c_uint64, u32p]),
         "krk_piece_sums_files": (i, [C.POINTER(krk_file_blob), C.c_uint64, u32p]),
         "krk_piece_stream_begin": (i, [C.c_int64, C.POINTER(vp)]),

@@ -870,6 +870,79 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
     return run_jobs(D, jobs, digests_dev, nullptr, pick(D, stream));
 }
 
+int krk_metainfo_batch_dev(const krk_blob* blobs, uint64_t n_blobs, const char* names, const uint64_t* name_off,
+                           uint32_t* sums_dev, uint32_t* sums_host, uint8_t* info_hash20, void* stream) {
+    KRK_DEVICE(D);
+    int r = validate_blobs(blobs, n_blobs);
+    if (r) return r;
+    if (!n_blobs) return KRK_OK;
+    KRK_CHECK(sums_dev && sums_host && info_hash20 && name_off, KRK_EINVAL, "metainfo_batch_dev: null argument");
+    hipStream_t s = pick(D, stream);
+    // Groups of about equal bytes, run back to back on `s`; the host hashes group g
+    // while the device runs groups g+1.. (one event per group).
+    std::vector<int64_t> pl(n_blobs), ln(n_blobs);
+    std::vector<uint64_t> so(n_blobs), ns(n_blobs);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n_blobs; ++i) {
+        pl[i] = blobs[i].piece_length;
+        ln[i] = (int64_t)blobs[i].length;
+        so[i] = blobs[i].sums_offset;
+        ns[i] = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
+        total += blobs[i].length;
+    }
+    const uint64_t G = std::min<uint64_t>(n_blobs, 8);
+    std::vector<uint64_t> cut{0};
+    for (uint64_t i = 0, acc = 0; i < n_blobs && cut.size() < G; ++i) {
+        acc += blobs[i].length;
+        if (acc * G >= total * cut.size() && i + 1 < n_blobs) cut.push_back(i + 1);
+    }
+    cut.push_back(n_blobs);
+    const size_t ng = cut.size() - 1;
+    std::vector<hipEvent_t> ev(ng, nullptr);
+    // sums copies on one of the context's other non-blocking streams (creating a stream
+    // per call costs milliseconds on ROCm)
+    hipStream_t cs = s == D->s_b ? D->s_a : D->s_b;
+    size_t launched = 0;
+    for (size_t g = 0; g < ng && !r; ++g) {
+        if (hipEventCreateWithFlags(&ev[g], hipEventDisableTiming) != hipSuccess) {
+            set_error(KRK_EHIP, "metainfo_batch_dev: event create");
+            r = KRK_EHIP;
+            break;
+        }
+        r = piece_sums_dev(D, blobs + cut[g], cut[g + 1] - cut[g], sums_dev, s);
+        if (!r && hipEventRecord(ev[g], s) != hipSuccess) {
+            set_error(KRK_EHIP, "metainfo_batch_dev: event record");
+            r = KRK_EHIP;
+        }
+        if (!r) ++launched;
+    }
+    for (size_t g = 0; g < launched; ++g) {
+        if (hipEventSynchronize(ev[g]) != hipSuccess) {
+            if (!r) { set_error(KRK_EHIP, "metainfo_batch_dev: kernel failed"); r = KRK_EHIP; }
+            continue;
+        }
+        if (r) continue;  // keep draining the launched groups before returning
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint64_t i = cut[g]; i < cut[g + 1]; ++i)
+            if (ns[i]) { lo = std::min(lo, so[i]); hi = std::max(hi, so[i] + ns[i]); }
+        if (hi > lo) {
+            if (hipMemcpyAsync(sums_host + lo, sums_dev + lo, (hi - lo) * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                hipStreamSynchronize(cs) != hipSuccess) {
+                set_error(KRK_EHIP, "metainfo_batch_dev: sums copy");
+                r = KRK_EHIP;
+                continue;
+            }
+        }
+        const uint64_t a = cut[g], m = cut[g + 1] - cut[g];
+        r = krk_info_hash_batch(pl.data() + a, sums_host, so.data() + a, ns.data() + a, names, name_off + a,
+                                ln.data() + a, m, info_hash20 + 20 * a);
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "metainfo_batch_dev: sync"); r = KRK_EHIP; }
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return r;
+}
+
 int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_dev, uint8_t* digests_dev,
                             void* stream) {
     KRK_DEVICE(D);

@@ -104,6 +104,10 @@ def sha_lanes_per_stream(n_streams: int) -> int:
     return v.value
 
 
+KRK_BLOB_DTYPE = np.dtype([("data", "<u8"), ("length", "<u8"), ("piece_length", "<i8"), ("sums_offset", "<u8")])
+assert KRK_BLOB_DTYPE.itemsize == C.sizeof(krk_blob)
+
+
 class BlobArena:
     """Blobs laid out back to back in one HBM allocation (each 256 B aligned)."""
 
@@ -140,11 +144,17 @@ class BlobArena:
         self.buf.from_host(np.asarray(data, dtype=np.uint8), int(self.offsets[i]))
 
     def blob_structs(self):
-        n = len(self.lengths)
-        arr = (krk_blob * max(n, 1))()
-        for i in range(n):
-            arr[i] = krk_blob(self.buf.ptr + int(self.offsets[i]), int(self.lengths[i]),
-                              int(self.piece_lengths[i]), int(self.sums_off[i]))
+        """krk_blob[] of the arena, built once (column-wise) and cached: the layout
+        never changes after construction."""
+        arr = getattr(self, "_structs", None)
+        if arr is None:
+            n = len(self.lengths)
+            a = np.zeros(max(n, 1), dtype=KRK_BLOB_DTYPE)
+            a["data"][:n] = np.uint64(self.buf.ptr) + self.offsets
+            a["length"][:n], a["piece_length"][:n], a["sums_offset"][:n] = \
+                self.lengths, self.piece_lengths, self.sums_off
+            arr = (krk_blob * max(n, 1)).from_buffer_copy(a.tobytes())
+            self._structs = arr
         return arr
 
     def data_ptrs(self):
@@ -162,6 +172,23 @@ class BatchOutputs:
 
 def piece_sums(arena: BlobArena, out: BatchOutputs, stream=None):
     check(lib.krk_piece_sums_dev(arena.blob_structs(), len(arena.lengths), out.sums.ptr, stream))
+
+
+def metainfo_batch(arena: BlobArena, out: BatchOutputs, names, sums_host: np.ndarray, stream=None) -> np.ndarray:
+    """Generator.Generate over the arena's blobs (krk_metainfo_batch_dev): piece sums into
+    out.sums and sums_host (uint32, arena layout) and the InfoHashes, returned as an
+    (n, 20) uint8 array; the host hashes each group while later groups' kernels run."""
+    n = len(arena.lengths)
+    enc = [x.encode() for x in names]
+    noff = np.zeros(n + 1, dtype=np.uint64)
+    noff[1:] = np.cumsum([len(e) for e in enc]) if n else []
+    ih = np.zeros((max(n, 1), 20), dtype=np.uint8)
+    assert sums_host.dtype == np.uint32 and sums_host.size >= arena.total_pieces
+    check(lib.krk_metainfo_batch_dev(arena.blob_structs(), n, b"".join(enc) or None,
+                                     noff.ctypes.data_as(C.POINTER(C.c_uint64)), out.sums.ptr,
+                                     sums_host.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                     ih.ctypes.data_as(C.POINTER(C.c_uint8)), stream))
+    return ih[:n]
 
 
 def sha256(arena: BlobArena, out: BatchOutputs, stream=None):

@@ -67,8 +67,8 @@ for s in "$@"; do
     pmcw4) step pmc_write_c4 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write_c4 -- python3 $R/bench.py --workload c4 --steps 1 --warmup 0 --no-cpu-baseline ;;
     prof4) step prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4 -- python3 $R/bench.py --workload c4 --no-cpu-baseline ;;
     pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-ceiling ;;
-    pmcf5) step pmc_fetch_c5r 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch_c5r -- python3 $R/bench.py --workload c5regen --steps 1 --warmup 0 --no-cpu-baseline ;;
-    pmcw5) step pmc_write_c5r 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write_c5r -- python3 $R/bench.py --workload c5regen --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmcf5) step pmc_fetch_c5r 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch_c5r -- python3 $R/bench.py --workload c5regen --regen-serial --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmcw5) step pmc_write_c5r 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write_c5r -- python3 $R/bench.py --workload c5regen --regen-serial --steps 1 --warmup 0 --no-cpu-baseline ;;
     prof5) step prof_c5r 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c5r -- python3 $R/bench.py --workload c5regen --no-cpu-baseline ;;
     prof5h) step prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c5 -- python3 $R/bench.py --workload c5 --no-cpu-baseline --no-sweep ;;
     proff1) step prof_f1 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_f1 -- python3 $R/bench.py --workload f1verify --no-cpu-baseline ;;
