@@ -715,7 +715,7 @@ def run_hrw(a, D, T, rank, world, res):
     g_avg = gms / max(gn, 1)
     per_digest = 32 + isz * R + 1
     roof = roofline_obj("hrw_gather", n * per_digest / (g_avg / 1e3) / 1e9 if g_avg else 0.0, g_avg,
-                        n * per_digest, None)
+                        n * per_digest, load_traffic(a.pmc_json, "c5", n).get("hrw_gather") if compact else None)
     roof["note"] = (f"algorithmic bytes per digest = {per_digest} (32-B digest record + {R} x {isz}-B owner "
                     "indices + 1-B count); the hrw_order kernel (65,536-shard table, "
                     f"{round(hms / max(hn, 1), 3)} ms) is VALU-bound and independent of the digest count")

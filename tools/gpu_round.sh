@@ -73,5 +73,7 @@ for s in "$@"; do
     prof5h) step prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c5 -- python3 $R/bench.py --workload c5 --no-cpu-baseline --no-sweep ;;
     proff1) step prof_f1 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_f1 -- python3 $R/bench.py --workload f1verify --no-cpu-baseline ;;
     prof3) step prof_c3 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c3 -- python3 $R/bench.py --workload c3 --no-cpu-baseline ;;
+    pmc5) step pmc_fetch_c5 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch_c5 -- python3 $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline --no-sweep &&
+          step pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write_c5 -- python3 $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline --no-sweep ;;
   esac
 done
