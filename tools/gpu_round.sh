@@ -75,5 +75,9 @@ for s in "$@"; do
     prof3) step prof_c3 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c3 -- python3 $R/bench.py --workload c3 --no-cpu-baseline ;;
     pmc5) step pmc_fetch_c5 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch_c5 -- python3 $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline --no-sweep &&
           step pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write_c5 -- python3 $R/bench.py --workload c5 --steps 2 --warmup 0 --no-cpu-baseline --no-sweep ;;
+    pmcpair) for v in 3 4; do
+              step pmc_pair_v${v}_a 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $R/gpurun_out/pmc_pair_v${v}_a -- python3 $R/tools/probe_perf.py --sha-variant $v --crc-gb 0 --sha 1000:8 &&
+              step pmc_pair_v${v}_b 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY --output-format csv -d $R/gpurun_out/pmc_pair_v${v}_b -- python3 $R/tools/probe_perf.py --sha-variant $v --crc-gb 0 --sha 1000:8 &&
+              step pmc_pair_v${v}_c 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC --output-format csv -d $R/gpurun_out/pmc_pair_v${v}_c -- python3 $R/tools/probe_perf.py --sha-variant $v --crc-gb 0 --sha 1000:8 || exit 1; done ;;
   esac
 done
