@@ -38,6 +38,8 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+from kraken_amd.windowed import c3_lengths  # noqa: E402
+
 METRIC = "metainfo+digest GB/s (device-resident & end-to-end) at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 GAMMA = 0x9E3779B97F4A7C15
@@ -125,11 +127,6 @@ def host_cores() -> int:
 
 
 # ----------------------------------------------------------------- workloads
-def c3_lengths(n_total=20000):
-    """L_i = 104,857,600 + (rng_i mod 968,884,225), rng_i = mix64(0xC3 + i*gamma)."""
-    return [104_857_600 + mix64((0xC3 + i * GAMMA) & M64) % 968_884_225 for i in range(n_total)]
-
-
 def c5regen_lengths(n=1000):
     """Log-uniform in [0, 2^30): L = floor(2^(30*u)) - 1, u from a seeded stream."""
     out = []
@@ -528,94 +525,19 @@ def run_pieces(a, D, T, rank, world, res):
         res["cpu_baseline"] = cb
 
 
-def c3_window_plan(lens, W, cap):
-    """C3 windows: [(blob indices, offsets, chunk lengths)].  Every live blob advances by
-    the same 64-multiple chunk per window (about W bytes a window).  Admission: at most
-    `cap` blobs are live, admitted longest first, so the longest chain starts in window 0
-    and every window stays on the two-lane SHA plan (a launch of more streams falls back
-    to one lane per stream, ~0.74x per stream); a finished blob's slot goes
-    to the next-longest waiting blob."""
-    L = np.asarray(lens, dtype=np.uint64)
-    n = L.size
-    cap = max(1, min(int(cap), n)) if n else 1
-    queue = list(np.argsort(-L.astype(np.int64), kind="stable"))
-    wins, pos = [], np.zeros(n, dtype=np.uint64)
-    live = np.asarray(sorted(queue[:cap]), dtype=np.int64)
-    queue = queue[cap:]
-    while live.size:
-        c = max(64, (W // live.size) // 64 * 64)
-        take = np.minimum(np.uint64(c), L[live] - pos[live])
-        wins.append((live, pos[live].copy(), take))
-        pos[live] += take
-        live = live[pos[live] < L[live]]
-        if queue and live.size < cap:
-            k = cap - live.size
-            live = np.sort(np.concatenate([live, np.asarray(queue[:k], dtype=np.int64)]))
-            queue = queue[k:]
-    return wins
-
-
-def two_lane_stream_cap(D, n):
-    """Largest stream count <= n whose SHA launch plan is two lanes per stream."""
-    import ctypes as C
-    lanes = C.c_int()
-
-    def two(m):
-        D.check(D.lib.krk_sha_lanes_per_stream(m, C.byref(lanes)))
-        return lanes.value == 2
-    if n == 0 or two(n):
-        return max(n, 1)
-    lo, hi = 1, n  # two(lo) holds, two(hi) does not
-    if not two(lo):
-        return n
-    while hi - lo > 1:
-        mid = (lo + hi) // 2
-        lo, hi = (mid, hi) if two(mid) else (lo, mid)
-    return lo
-
-
 def run_chunked(a, D, T, rank, world, res):
     """C3: every blob of this rank's LPT shard advances by one chunk per window; the
-    next window's bytes are generated on the device (own stream) while the
-    current window's kernels run."""
-    import ctypes as C
+    next window's bytes are generated on the device (own stream) while the current
+    window's kernels run (kraken_amd.windowed, the machinery tests/test_gpu_windowed.py
+    checks against the oracle)."""
+    from kraken_amd.windowed import WindowedRun
     ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
     n = len(lens)
-    W = a.window_gib << 30
-    bufs = [D.DeviceBuffer(W + 16 * n), D.DeviceBuffer(W + 16 * n)]
-    cb = D.ChunkedBatch(lens, P)
-    gen_s, run_s = C.c_void_p(), C.c_void_p()
-    D.check(D.lib.krk_stream_create(C.byref(gen_s)))
-    D.check(D.lib.krk_stream_create(C.byref(run_s)))
-
-    ids_a = np.asarray(ids, dtype=np.uint64)
-    cap = n if a.no_admission else two_lane_stream_cap(D, n)
-    wins = c3_window_plan(lens, W, cap)
-
-    def items_of(k):
-        blobs, offs, take = wins[k]
-        dev = np.zeros(take.size, dtype=np.uint64)  # 16-byte aligned chunk addresses in the window
-        dev[1:] = np.cumsum((take + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]
-        dev += np.uint64(bufs[k & 1].ptr)
-        return blobs, dev, offs, take
-
-    def gen(items):
-        blobs, dev, offs, take = items
-        D.synth_fill_chunk_arrays(ids_a[blobs], dev, offs, take, stream=gen_s)
-        D.check(D.lib.krk_stream_sync(gen_s))
-
+    wr = WindowedRun(D, ids, lens, P, a.window_gib << 30, cap=n if a.no_admission else None)
     T.barrier()
     with D.KernelTimer():
         t0 = time.perf_counter()
-        cur = items_of(0)
-        gen(cur)
-        for k in range(len(wins)):
-            D.check(D.lib.krk_stream_sync(run_s))  # window k-1 done: its buffer may be refilled
-            cb.step_arrays(cur[0], cur[1], cur[2], cur[3], stream=run_s)
-            if k + 1 < len(wins):
-                cur = items_of(k + 1)
-                gen(cur)
-        D.check(D.lib.krk_stream_sync(run_s))
+        wr.run()
         T.barrier()
         t1 = time.perf_counter()
         sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
@@ -624,13 +546,14 @@ def run_chunked(a, D, T, rank, world, res):
     elapsed = T.max_over_ranks(t1 - t0)
     bytes_rank = int(sum(lens))
     total_bytes = int(sum(c3_lengths(a.blobs or 20000)))
+    cb = wr.cb
     res.update({"metric": "metainfo+digest GB/s (C3, device-generated windows)",
                 "value": round(total_bytes / elapsed / 1e9, 3), "unit": "GB/s", "steps": 1,
                 "ms_per_step": round(elapsed * 1e3, 3), "higher_is_better": True, "scaling": "strong",
                 "dtype": "u8", "data": "synthetic (generated on the device per window, inside the timed region)",
                 "config": {"workload": WORKLOADS["c3"]["desc"], "blobs_total": a.blobs or 20000,
                            "blobs_this_rank": n, "bytes_this_rank": bytes_rank, "bytes_total": total_bytes,
-                           "windows": len(wins), "window_bytes": W, "live_cap": int(cap), "piece_length": P,
+                           "windows": len(wr.wins), "window_bytes": wr.W, "live_cap": int(wr.cap), "piece_length": P,
                            "longest_blob": max(lens), "parallelism": f"LPT blob shard x{world}, no collective"},
                 "kernels": {"sha256_multi": {"launches": sha_n, "total_ms": round(sha_ms, 1)},
                             "crc32_pieces": {"launches": crc_n, "total_ms": round(crc_ms, 1)},
@@ -648,7 +571,7 @@ def run_chunked(a, D, T, rank, world, res):
         pick = sorted({0, n // 2, n - 1})
         dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
         sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
-        del bufs[:]
+        wr.close()
         arena = D.BlobArena([lens[i] for i in pick], P, blob_ids=[ids[i] for i in pick])
         out = D.BatchOutputs(arena)
         D.metainfo_digest(arena, out)
@@ -660,8 +583,7 @@ def run_chunked(a, D, T, rank, world, res):
             o, ro, cnt = int(cb.sums_off[i]), int(arena.sums_off[k]), int(arena.n_pieces[k])
             ok = ok and np.array_equal(sums[o:o + cnt], rs[ro:ro + cnt])
         res["spot_check_matches_one_shot"] = bool(ok)
-    D.lib.krk_stream_destroy(gen_s)
-    D.lib.krk_stream_destroy(run_s)
+    wr.close()
 
 
 def run_hrw(a, D, T, rank, world, res):

@@ -93,8 +93,11 @@ typedef struct krk_file_blob {
 int krk_piece_sums_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host);
 
 /* Streaming form for NewMetaInfo(d, io.Reader, P): the cgo shim copies each
- * Read() chunk in with _update; CRC state is carried across chunk and piece
- * boundaries on the device.  _end returns the io.CopyN-loop results. */
+ * Read() chunk in with _update.  Bytes go through the device's submission engine
+ * (pooled pinned slots; the CRC requests of all concurrent streams and crc32_update
+ * calls share launches); each slot's piece portions are hashed as independent
+ * messages and folded into the piece sums on the host with the GF(2) combine, so
+ * state crosses slot and piece boundaries.  _end returns the io.CopyN-loop results. */
 typedef struct krk_piece_stream krk_piece_stream;
 int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out);
 int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* host_buf, uint64_t n);
@@ -104,7 +107,10 @@ void krk_piece_stream_free(krk_piece_stream* s);
 
 /* crc32.Update(crc, IEEETable, p) for one buffer (hash.Hash32 Write path used
  * by agentstorage.Torrent.writePiece, lib/torrent/storage/agentstorage/torrent.go:175-199).
- * data is a HOST pointer. */
+ * data is a HOST pointer.  Calls of at most 64 KiB (KRK_CRC_HOST_MAX) run on the
+ * caller's thread (krk_host_crc32_update: no PCIe round trip for a small write);
+ * larger ones go through the device's CRC queue, coalesced with the other pending
+ * requests of the device into one launch. */
 int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
 
 /* Batch piece verification (the same kernel in verify mode): ok_out[i] = 1 iff
@@ -134,14 +140,44 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
 int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
                     uint8_t* digests_host);
 
-/* Streaming Digester: _write may be called any number of times (io.Copy chunks);
- * _sum does not reset (Digester.Digest(), digester.go:41-48) so writing may
- * continue afterwards.  Concurrent digesters share launches. */
+/* Streaming Digester (core.NewDigester, digester.go:34): _write may be called any
+ * number of times (io.Copy chunks); _sum does not reset (Digester.Digest(),
+ * digester.go:41-48) so writing may continue afterwards.  One digester is
+ * single-owner (like hash.Hash); different digesters may be used from different
+ * threads at once.
+ *
+ * Placement, fixed at creation:
+ *   KRK_PLACE_GPU   bytes go through the device's submission engine: the caller copies
+ *                   them into pooled pinned slots (2 MiB, KRK_SLOT_MB) and every
+ *                   pending slot of every GPU digester of the device is digested in
+ *                   ONE multi-stream sha256_multi launch (a dispatcher thread batches
+ *                   them; a digester's midstate chains through its own requests
+ *                   only).  Creation allocates nothing on the device.
+ *   KRK_PLACE_HOST  SHA-NI on the caller's thread (host_meta.cpp): ~2 GB/s per stream
+ *                   against ~50 MB/s for one GPU stream.
+ *   KRK_PLACE_AUTO  (krk_digester_new) HOST while at most N digesters are live in the
+ *                   process, GPU beyond: the crossover where the host's aggregate
+ *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~50 MB/s).
+ *                   N = 40 x the CPUs this process may use, or KRK_DIGESTER_HOST_STREAMS,
+ *                   or krk_set_digester_host_streams (-1 restores the default).
+ * Without a gfx950 device every constructor fails with KRK_ENODEV. */
 typedef struct krk_digester krk_digester;
+#define KRK_PLACE_AUTO 0
+#define KRK_PLACE_HOST 1
+#define KRK_PLACE_GPU 2
 int krk_digester_new(krk_digester** out);
+int krk_digester_new_on(int placement, krk_digester** out);
+int krk_digester_placement(const krk_digester* d, int* placement);
 int krk_digester_write(krk_digester* d, const uint8_t* host_buf, uint64_t n);
 int krk_digester_sum(krk_digester* d, uint8_t out32[32]);
 void krk_digester_free(krk_digester* d);
+int krk_set_digester_host_streams(int64_t n);
+
+/* Submission-engine counters of the calling thread's device: SHA launches and the
+ * jobs they carried (jobs / batches = streams coalesced per launch), CRC launches and
+ * requests, pinned staging bytes held by the slot pool. */
+int krk_engine_stats(uint64_t* sha_batches, uint64_t* sha_jobs, uint64_t* crc_batches,
+                     uint64_t* crc_requests, uint64_t* pinned_bytes);
 
 /* ----------------------------------------- metainfo + digest (batch)
  * Both products for every blob in one call: the Digester SHA-256 of
@@ -182,6 +218,25 @@ int krk_metainfo_digest_chunks_dev(const krk_chunk* chunks, uint64_t n_chunks, u
 int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host,
                              uint8_t* digests_host);
 
+/* ------------------------------------------------------- multi-device
+ * One process, several GPUs (the origin is one process,
+ * origin/cmd/cmd.go:164).  The device set -- the devices of the last krk_init mask,
+ * or krk_set_devices (a device may repeat: several workers on one GPU), default the
+ * calling thread's device -- is where the *_multi calls run and where new Digesters
+ * and piece streams are placed (round-robin).  A *_multi call splits its batch by
+ * bytes (LPT: the longest blob to the least-loaded device), runs the single-device
+ * entry point on every device from its own host thread and gathers the results
+ * into the caller's arrays (same layout as the single-device call).  No collective:
+ * blobs are independent.  Synchronous. */
+int krk_set_devices(const int* devs, uint32_t n);
+int krk_get_devices(int* devs, uint32_t cap, uint32_t* n);
+int krk_metainfo_digest_host_multi(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host,
+                                   uint8_t* digests_host);
+int krk_piece_sums_host_multi(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host);
+int krk_piece_sums_files_multi(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host);
+int krk_sha256_host_multi(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
+                          uint8_t* digests_host);
+
 /* ---------------------------------------------------- InfoHash (host CPU)
  * info.Hash() (core/metainfo.go:37-44): SHA-1 over the bencoded
  * info{PieceLength, PieceSums, Name, Length}.  bencode_out may be NULL. */
@@ -205,6 +260,16 @@ int krk_info_hash_batch(const int64_t* piece_lengths, const uint32_t* sums, cons
 int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
                      const char* name, uint64_t name_len, int64_t length,
                      uint8_t* out, uint64_t cap, uint64_t* written);
+
+/* --------------------------------------- host crossover primitives (CPU)
+ * The host side of the Digester / PieceHash crossovers: a single
+ * SHA-256 stream digests ~2 GB/s on one SHA-NI core vs ~50 MB/s on one GPU stream,
+ * and a small crc32.Update is cheaper on the calling thread than a PCIe round trip,
+ * so a krk_digester with few concurrent peers and a small krk_crc32_update write
+ * run these on the caller's thread.  x86 SHA-NI / PCLMULQDQ when the CPU has them,
+ * portable code otherwise; sha256.Sum256 and crc32.Update(crc, IEEETable, p). */
+int krk_host_sha256(const uint8_t* data, uint64_t n, uint8_t out32[32]);
+int krk_host_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
 
 /* pieceLengthConfig.get (lib/metainfogen/config.go:71-80); thresholds ascending. */
 int64_t krk_piece_length_for_size(const int64_t* thresholds, const int64_t* lengths,
@@ -232,6 +297,12 @@ typedef struct krk_nodes {
 int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys,
                     const krk_nodes* nodes, uint32_t n_out, int32_t* order_out,
                     double* scores_out);
+
+/* hrw.UInt64ToFloat64 (rendezvous.go:99-118) with MaxHashValue = 8 x 0xFF (murmur3's
+ * Sum size): sums8 holds n 8-byte big-endian hash Sums; out[i] = low 53 bits / 2^53,
+ * where all-zero low bits are re-hashed once with murmur3.New64 when rehash != 0 (the
+ * hasher argument; 0 = nil hasher).  Runs the scoring kernel's own device function. */
+int krk_hrw_uint64_to_float64(const uint8_t* sums8, uint64_t n, int rehash, double* out);
 
 /* ring.Locations for raw 32-byte sha256 digests (ShardID = first 2 bytes).
  * healthy: n_nodes flags.  locs_out: n * max(1, max_replica) node indices
@@ -290,6 +361,17 @@ int krk_reset_kernel_stats(void);
  * idle: fewer than one two-lane workgroup per CU).  Diagnostic; bench.py prices
  * the per-stream issue ceiling of that plan. */
 int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes);
+
+/* SHA-256 launch plan, process-wide (default AUTO: two lanes per stream while the
+ * batch leaves SIMDs idle, then two producer/consumer pairs per workgroup, then one
+ * lane).  Every plan is bit-exact; the knob exists for tests and tuning.  The
+ * environment variable KRK_SHA_PLAN, read once at the first launch, sets the same. */
+#define KRK_SHA_PLAN_AUTO 0
+#define KRK_SHA_PLAN_1LANE 1        /* one lane per stream, one pair per workgroup */
+#define KRK_SHA_PLAN_2LANE 2        /* two lanes per stream, one pair per workgroup */
+#define KRK_SHA_PLAN_1LANE_2PAIR 3  /* one lane, two pairs per 4-wave workgroup */
+#define KRK_SHA_PLAN_2LANE_2PAIR 4  /* two lanes, two pairs per workgroup */
+int krk_set_sha_plan(int plan);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("KRK_LIB_PATH") or os.path.join(_HERE, "lib", "libkrak
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip.h")
 
 KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX, KRK_EIO = 0, -1, -2, -3, -4, -5, -6, -7
+KRK_PLACE_AUTO, KRK_PLACE_HOST, KRK_PLACE_GPU = 0, 1, 2
 
 
 class KrakenError(RuntimeError):
@@ -77,6 +78,20 @@ def _load() -> C.CDLL:
         "krk_sha256_dev": (i, [C.POINTER(vp), u64p, C.c_uint64, vp, vp]),
         "krk_sha256_host": (i, [C.POINTER(vp), u64p, C.c_uint64, u8p]),
         "krk_digester_new": (i, [C.POINTER(vp)]),
+        "krk_digester_new_on": (i, [i, C.POINTER(vp)]),
+        "krk_digester_placement": (i, [vp, C.POINTER(C.c_int)]),
+        "krk_set_digester_host_streams": (i, [C.c_int64]),
+        "krk_engine_stats": (i, [u64p, u64p, u64p, u64p, u64p]),
+        "krk_set_devices": (i, [C.POINTER(C.c_int), C.c_uint32]),
+        "krk_get_devices": (i, [C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint32)]),
+        "krk_metainfo_digest_host_multi": (i, [blobp, C.c_uint64, u32p, u8p]),
+        "krk_piece_sums_host_multi": (i, [blobp, C.c_uint64, u32p]),
+        "krk_piece_sums_files_multi": (i, [C.POINTER(krk_file_blob), C.c_uint64, u32p]),
+        "krk_sha256_host_multi": (i, [C.POINTER(vp), u64p, C.c_uint64, u8p]),
+        "krk_host_sha256": (i, [vp, C.c_uint64, u8p]),
+        "krk_host_crc32_update": (i, [C.c_uint32, vp, C.c_uint64, u32p]),
+        "krk_hrw_uint64_to_float64": (i, [u8p, C.c_uint64, i, f64p]),
+        "krk_set_sha_plan": (i, [i]),
         "krk_digester_write": (i, [vp, vp, C.c_uint64]),
         "krk_digester_sum": (i, [vp, u8p]),
         "krk_digester_free": (None, [vp]),

@@ -7,6 +7,7 @@ GPU through the same HRW kernel as the hashring (krk_hrw_ordered)."""
 from __future__ import annotations
 
 import os
+import posixpath
 
 from .hrw import NewRendezvousHash
 
@@ -33,18 +34,30 @@ def initCASVolumes(dir_: str, volumes) -> None:
     for v in volumes:
         if not os.path.exists(v.Location):
             raise OSError(f"verify volume: stat {v.Location}: no such file or directory")
+    base = posixpath.basename(posixpath.normpath(dir_)) if dir_ else "."  # Go path.Base
     for sub, loc in volume_subdirs(volumes).items():
-        src = os.path.join(loc, os.path.basename(dir_), sub)
+        src = posixpath.join(loc, base, sub)
         try:
             os.makedirs(src, mode=0o775, exist_ok=True)
         except OSError as e:
             raise OSError(f"volume source path: {e}") from e
-        tgt = os.path.join(dir_, sub)
+        tgt = posixpath.join(dir_, sub)
         try:
-            if os.path.islink(tgt) or os.path.exists(tgt):
-                if os.path.islink(tgt) and os.readlink(tgt) == src:
-                    continue
-                os.remove(tgt)
-            os.symlink(src, tgt)
+            _create_or_update_symlink(src, tgt)
         except OSError as e:
             raise OSError(f"symlink to volume: {e}") from e
+
+
+def _create_or_update_symlink(src: str, tgt: str) -> None:
+    """createOrUpdateSymlink (lib/store/utils.go:25-47): an existing target that is not
+    a symlink (a regular file, a real directory) is an error and is left in place;
+    a symlink to another source is replaced; a missing target is created."""
+    try:
+        os.stat(tgt)  # follows links, like os.Stat
+    except FileNotFoundError:
+        os.symlink(src, tgt)
+        return
+    existing = os.readlink(tgt)  # OSError (EINVAL) when tgt is not a symlink
+    if existing != src:
+        os.remove(tgt)
+        os.symlink(src, tgt)

@@ -18,7 +18,6 @@ from __future__ import annotations
 import ctypes as C
 import io
 import json
-import re
 
 import numpy as np
 
@@ -28,17 +27,47 @@ SHA256 = "sha256"
 DigestEmptyTar = "sha256:e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 _COPY_BUF = 32 * 1024  # io.Copy's buffer: the Go reader granularity
 
-_HEX = re.compile(r"^[0-9a-fA-F]*$")
+_HEXB = frozenset(b"0123456789abcdefABCDEF")
+
+
+def _go_quote(s: str) -> str:
+    """fmt's %q for the common cases: double quotes, Go escapes."""
+    out = ['"']
+    for ch in s:
+        o = ord(ch)
+        if ch in '"\\':
+            out.append("\\" + ch)
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ch.isprintable():
+            out.append(ch)
+        elif o < 0x80:
+            out.append(f"\\x{o:02x}")
+        elif o <= 0xFFFF:
+            out.append(f"\\u{o:04x}")
+        else:
+            out.append(f"\\U{o:08x}")
+    out.append('"')
+    return "".join(out)
 
 
 # ---------------------------------------------------------------- Digest
 
 def ValidateSHA256(s: str) -> None:
-    """core/digest.go:152-161."""
-    if len(s) != 64:
-        raise ValueError(f"expected 64 characters, got {len(s)} from {s!r}")
-    if not _HEX.match(s):
-        raise ValueError("hex: invalid byte")
+    """core/digest.go:152-161: 64 BYTES (Go len) that hex.DecodeString accepts; the
+    errors read like Go's ("hex: encoding/hex: invalid byte: U+0067 'g'")."""
+    b = s.encode("utf-8", "surrogatepass")
+    if len(b) != 64:
+        raise ValueError(f"expected 64 characters, got {len(b)} from {_go_quote(s)}")
+    for c in b:
+        if c not in _HEXB:
+            r = chr(c)
+            shown = f" '{r}'" if r.isprintable() else ""
+            raise ValueError(f"hex: encoding/hex: invalid byte: U+{c:04X}{shown}")
 
 
 class Digest:
@@ -99,13 +128,22 @@ def ParseSHA256Digest(raw: str) -> Digest:
 
 
 class Digester:
-    """core.Digester: streaming SHA-256 on the GPU (one Merkle-Damgard stream per
-    lane).  Digest() does not reset, exactly like hash.Hash.Sum."""
+    """core.Digester (core/digester.go:28-72).  Digest() does not reset, exactly like
+    hash.Hash.Sum.  placement (krk_digester_new_on): PLACE_GPU batches this digester's
+    bytes with every other GPU digester of the device into multi-stream SHA-256
+    launches; PLACE_HOST runs SHA-NI on the calling thread; PLACE_AUTO (NewDigester)
+    picks HOST while few digesters are live in the process, GPU beyond (the crossover
+    in include/kraken_hip.h)."""
 
-    def __init__(self):
+    def __init__(self, placement: int = 0):
         h = C.c_void_p()
-        check(lib.krk_digester_new(C.byref(h)))
+        check(lib.krk_digester_new_on(placement, C.byref(h)))
         self._h = h
+
+    def placement(self) -> int:
+        v = C.c_int()
+        check(lib.krk_digester_placement(self._h, C.byref(v)))
+        return v.value
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -140,8 +178,11 @@ class Digester:
         return _TeeReader(r, self)
 
 
+PLACE_AUTO, PLACE_HOST, PLACE_GPU = 0, 1, 2
+
+
 def NewDigester() -> Digester:
-    return Digester()
+    return Digester(PLACE_AUTO)
 
 
 class _TeeReader(io.RawIOBase):
@@ -270,22 +311,60 @@ class MetaInfo:
         return json.dumps(obj, separators=(",", ":")).encode()
 
 
+def _json_field(obj: dict, key: str, kind, zero):
+    """encoding/json into a typed struct field: absent or null -> the zero value,
+    a wrong JSON type -> "cannot unmarshal" (Go matches keys case-insensitively)."""
+    v = obj.get(key, None)
+    if v is None:
+        for k2, v2 in obj.items():
+            if k2.lower() == key.lower():
+                v = v2
+                break
+    if v is None:
+        return zero
+    if kind is int:
+        if isinstance(v, bool) or not isinstance(v, int):
+            raise ValueError(f"cannot unmarshal {type(v).__name__} into Go struct field info.{key} of type int64")
+        return v
+    if kind is str:
+        if not isinstance(v, str):
+            raise ValueError(f"cannot unmarshal {type(v).__name__} into Go struct field info.{key} of type string")
+        return v
+    if not isinstance(v, list) or not all(isinstance(x, int) and not isinstance(x, bool) and 0 <= x < 1 << 32
+                                          for x in v):
+        raise ValueError(f"cannot unmarshal {type(v).__name__} into Go struct field info.{key} of type uint32")
+    return v
+
+
 def DeserializeMetaInfo(data: bytes) -> MetaInfo:
-    """core/metainfo.go:136-155."""
+    """core/metainfo.go:136-155.  Missing fields and a null Info take Go's zero values
+    (json.Unmarshal into metaInfoJSON), so a truncated sidecar fails the way the
+    reference does: "parse name: invalid sha256: ..."."""
     try:
         j = json.loads(data)
-        info = j["Info"]
-    except (ValueError, KeyError, TypeError) as e:
+        if j is None:
+            j = {}
+        if not isinstance(j, dict):
+            raise ValueError(f"cannot unmarshal {type(j).__name__} into Go value of type core.metaInfoJSON")
+        info = next((v for k, v in j.items() if k.lower() == "info"), None) if "Info" not in j else j["Info"]
+        if info is None:
+            info = {}
+        if not isinstance(info, dict):
+            raise ValueError(f"cannot unmarshal {type(info).__name__} into Go struct field metaInfoJSON.Info "
+                             "of type core.info")
+        pl = _json_field(info, "PieceLength", int, 0)
+        sums = _json_field(info, "PieceSums", list, None)
+        name = _json_field(info, "Name", str, "")
+        length = _json_field(info, "Length", int, 0)
+    except (ValueError, TypeError) as e:
         raise ValueError(f"json: {e}") from None
-    sums = info.get("PieceSums")
     arr = None if sums is None else np.asarray(sums, dtype=np.uint32)
-    ih = _info_hash(int(info["PieceLength"]), arr if arr is not None else np.zeros(0, np.uint32),
-                    info["Name"], int(info["Length"]))
+    ih = _info_hash(pl, arr if arr is not None else np.zeros(0, np.uint32), name, length)
     try:
-        d = NewSHA256DigestFromHex(info["Name"])
+        d = NewSHA256DigestFromHex(name)
     except ValueError as e:
         raise ValueError(f"parse name: {e}") from None
-    return MetaInfo(int(info["PieceLength"]), arr, info["Name"], int(info["Length"]), d, ih)
+    return MetaInfo(pl, arr, name, length, d, ih)
 
 
 def _as_bytes(p) -> np.ndarray:

@@ -21,11 +21,11 @@
 // the items of one piece may run on any wave, XCD or launch.
 //
 // Tables live in LDS, replicated so that the lanes of a ds_read_b32 half-wave hit
-// distinct banks.  Default (variant 7): the byte-addressable layout of TabP, where a
-// lookup address is one v_perm_b32.  Variants 0-6: replicated R times and interleaved
-// (word (t*256+e)*R + r, lane l reads replica l % R: R = 32 conflict-free, R = 16 at
-// most 2-way), addresses formed by extract + shift + add.  DESIGN.md §4.1 has the
-// measurements of every variant.
+// distinct banks.  Production (variants 7, 8): the byte-addressable layout of TabP,
+// where a lookup address is one v_perm_b32.  The diagnostic build (KRK_DIAG) adds the
+// measured alternatives: replicated R times and interleaved (word (t*256+e)*R + r,
+// lane l reads replica l % R), the coalesced layout, nontemporal loads and load-only
+// timing kernels.  DESIGN.md §4.1 has the measurements of every variant.
 #include <mutex>
 
 #include "kernels.hpp"
@@ -372,10 +372,30 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
     return hipGetLastError();
 }
 
+// Production launch variants (bit-exact): 7 = strided layout, byte-addressable tables
+// with 32 replicas (144 KiB of LDS, one 1024-thread workgroup per CU), the default;
+// 8 = the same with 16 replicas (80 KiB, two workgroups per CU).  Every other layout
+// measured in DESIGN.md 4.1 -- and the load-only timing diagnostics, which give WRONG
+// sums -- is compiled only into the diagnostic build (make diag, -DKRK_DIAG).
+bool crc_variant_valid(int v) {
+#ifdef KRK_DIAG
+    return v >= 0 && v <= 13;
+#else
+    return v == 7 || v == 8;
+#endif
+}
+
 hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, const CrcLaunchCfg& cfg,
                             hipStream_t s) {
     if (uint64_t(w.run_items) + w.n_items == 0) return hipSuccess;
     switch (cfg.variant) {
+        case 7:
+            return launch_variant<32, 4, 1024, false, false, 32>(w, tabs, sums, cfg.cus, 1, s);
+        case 8:
+            return launch_variant<16, 4, 1024, false, false, 16>(w, tabs, sums, cfg.cus, 2, s);
+#ifdef KRK_DIAG
+        case 0:  // strided, interleaved R16 tables, 80 KiB LDS: two 512-thread blocks per CU
+            return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
         case 1:  // 144 KiB LDS: one 1024-thread block per CU
             return launch_variant<32, 4, 1024, false>(w, tabs, sums, cfg.cus, 1, s);
         case 2:  // coalesced, 80 KiB LDS: two 512-thread blocks per CU
@@ -388,10 +408,6 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
             return launch_variant<16, 4, 1024, false>(w, tabs, sums, cfg.cus, 2, s);
         case 6:  // strided, R8 tables (40 KiB), four 512-thread blocks per CU: 32 waves/CU
             return launch_variant<8, 2, 512, false>(w, tabs, sums, cfg.cus, 4, s);
-        case 7:  // strided, byte-addressable tables (v_perm addresses, 144 KiB), one 1024-thread block per CU
-            return launch_variant<32, 4, 1024, false, false, 32>(w, tabs, sums, cfg.cus, 1, s);
-        case 8:  // as 7 with 16 replicas (80 KiB): two 1024-thread blocks per CU
-            return launch_variant<16, 4, 1024, false, false, 16>(w, tabs, sums, cfg.cus, 2, s);
         case 9:  // as 7 with nontemporal data loads
             return launch_variant<32, 4, 1024, false, false, 32, true>(w, tabs, sums, cfg.cus, 1, s);
         case 10:  // timing diagnostic: variant 9's loads and occupancy without the lookups (wrong sums)
@@ -402,8 +418,9 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
             return launch_variant<32, 4, 1024, true, false, 32>(w, tabs, sums, cfg.cus, 1, s);
         case 13:  // timing diagnostic: variant 12's loads and occupancy without the lookups (wrong sums)
             return launch_variant<32, 4, 1024, true, true, 32>(w, tabs, sums, cfg.cus, 1, s);
-        default:  // strided, 80 KiB LDS: two 512-thread blocks per CU
-            return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
+#endif
+        default:
+            return hipErrorInvalidValue;
     }
 }
 

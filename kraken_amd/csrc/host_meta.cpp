@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -122,6 +123,179 @@ static void sha1(const uint8_t* p, size_t n, uint8_t out[20]) {
         for (int k = 0; k < 4; ++k) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
 }
 
+// ----------------------------------------------------------------- SHA-256
+// Host SHA-256 (FIPS 180-4) for the Digester's host crossover: one SHA-NI core
+// digests ~2 GB/s where one GPU stream (two lanes) digests ~50 MB/s, so a process
+// with few concurrent digesters is served faster on its own threads.
+static const uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+static void sha256_blocks_portable(uint32_t h[8], const uint8_t* p, size_t nblocks) {
+    auto ror = [](uint32_t x, int k) { return (x >> k) | (x << (32 - k)); };
+    for (; nblocks; --nblocks, p += 64) {
+        uint32_t w[64];
+        for (int i = 0; i < 16; ++i)
+            w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+        for (int i = 16; i < 64; ++i) {
+            const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+            const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+        }
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+        for (int i = 0; i < 64; ++i) {
+            const uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + kK256[i] + w[i];
+            const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+    }
+}
+
+#if defined(__x86_64__)
+// Four rounds q (4q..4q+3) with the x86 SHA extensions.  Message words rotate
+// through M[0..3]: sha256msg1 at q = 1..12 prepares the words of quad q + 3,
+// sha256msg2 at q = 3..14 completes those of quad q + 1.
+template <int Q>
+__attribute__((target("sha,sse4.1"))) static inline void sha256_quad(__m128i& s0, __m128i& s1, __m128i M[4]) {
+    __m128i msg = _mm_add_epi32(M[Q & 3], _mm_loadu_si128(reinterpret_cast<const __m128i*>(kK256 + 4 * Q)));
+    s1 = _mm_sha256rnds2_epu32(s1, s0, msg);
+    if (Q >= 3 && Q <= 14) {
+        const __m128i t = _mm_alignr_epi8(M[Q & 3], M[(Q + 3) & 3], 4);
+        M[(Q + 1) & 3] = _mm_sha256msg2_epu32(_mm_add_epi32(M[(Q + 1) & 3], t), M[Q & 3]);
+    }
+    msg = _mm_shuffle_epi32(msg, 0x0E);
+    s0 = _mm_sha256rnds2_epu32(s0, s1, msg);
+    if (Q >= 1 && Q <= 12) M[(Q + 3) & 3] = _mm_sha256msg1_epu32(M[(Q + 3) & 3], M[Q & 3]);
+}
+
+template <int... Q>
+__attribute__((target("sha,sse4.1"))) static inline void sha256_quads(__m128i& s0, __m128i& s1, __m128i M[4],
+                                                                       std::integer_sequence<int, Q...>) {
+    (sha256_quad<Q>(s0, s1, M), ...);
+}
+
+__attribute__((target("sha,sse4.1"))) static void sha256_blocks_ni(uint32_t h[8], const uint8_t* p,
+                                                                    size_t nblocks) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    // (a,b,c,d),(e,f,g,h) -> the instruction's (ABEF),(CDGH) operand order
+    __m128i t = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h)), 0xB1);
+    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(h + 4)), 0x1B);
+    __m128i s0 = _mm_alignr_epi8(t, s1, 8);
+    s1 = _mm_blend_epi16(s1, t, 0xF0);
+    __m128i M[4];
+    for (; nblocks; --nblocks, p += 64) {
+        const __m128i s0_save = s0, s1_save = s1;
+        for (int k = 0; k < 4; ++k)
+            M[k] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * k)), bswap);
+        sha256_quads(s0, s1, M, std::make_integer_sequence<int, 16>{});
+        s0 = _mm_add_epi32(s0, s0_save);
+        s1 = _mm_add_epi32(s1, s1_save);
+    }
+    t = _mm_shuffle_epi32(s0, 0x1B);
+    s1 = _mm_shuffle_epi32(s1, 0xB1);
+    s0 = _mm_blend_epi16(t, s1, 0xF0);
+    s1 = _mm_alignr_epi8(s1, t, 8);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h), s0);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(h + 4), s1);
+}
+#endif
+
+// KRK_HOST_PORTABLE=1 forces the portable SHA-256 / CRC-32 routines (tests compare).
+static bool host_portable() {
+    static const bool p = getenv("KRK_HOST_PORTABLE") && atoi(getenv("KRK_HOST_PORTABLE")) > 0;
+    return p;
+}
+
+// ----------------------------------------------------------------- CRC-32
+// Host CRC-32/IEEE (crc32.Update semantics) for the PieceHash crossover (small
+// writes never pay a PCIe round trip): slicing-by-8, and carry-less-multiply
+// folding (4 x 128 bits per step, Barrett reduction) when the CPU has PCLMULQDQ.
+static uint32_t g_crc_tab[8][256];
+static void crc_tables_init() {
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1)));
+        g_crc_tab[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+        for (int t = 1; t < 8; ++t) g_crc_tab[t][i] = (g_crc_tab[t - 1][i] >> 8) ^ g_crc_tab[0][g_crc_tab[t - 1][i] & 0xFF];
+}
+
+// Raw register update (no pre/post inversion).
+static uint32_t crc_raw_sliced(uint32_t c, const uint8_t* p, size_t n) {
+    for (; n >= 8; n -= 8, p += 8) {
+        uint32_t lo, hi;
+        memcpy(&lo, p, 4);
+        memcpy(&hi, p + 4, 4);
+        lo ^= c;
+        c = g_crc_tab[7][lo & 0xFF] ^ g_crc_tab[6][(lo >> 8) & 0xFF] ^ g_crc_tab[5][(lo >> 16) & 0xFF] ^
+            g_crc_tab[4][lo >> 24] ^ g_crc_tab[3][hi & 0xFF] ^ g_crc_tab[2][(hi >> 8) & 0xFF] ^
+            g_crc_tab[1][(hi >> 16) & 0xFF] ^ g_crc_tab[0][hi >> 24];
+    }
+    for (; n; --n, ++p) c = g_crc_tab[0][(c ^ *p) & 0xFF] ^ (c >> 8);
+    return c;
+}
+
+#if defined(__x86_64__)
+// Folding constants of the reflected polynomial (x^k mod P, bit-reflected):
+// 4-way fold (x^(4*128+32), x^(4*128-32)), 1-way fold (x^(128+32), x^(128-32)),
+// 64->32 (x^64), and the Barrett pair (P', mu).
+__attribute__((target("pclmul,sse4.1"))) static inline __m128i fold(__m128i x, __m128i k, __m128i d) {
+    return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11)), d);
+}
+
+__attribute__((target("pclmul,sse4.1"))) static uint32_t crc_raw_clmul(uint32_t c, const uint8_t* p, size_t n) {
+    if (n < 64) return crc_raw_sliced(c, p, n);
+    const __m128i k1k2 = _mm_set_epi64x(0x01c6e41596LL, 0x0154442bd4LL);
+    const __m128i k3k4 = _mm_set_epi64x(0x00ccaa009eLL, 0x01751997d0LL);
+    const __m128i k5 = _mm_set_epi64x(0, 0x0163cd6124LL);
+    const __m128i poly = _mm_set_epi64x(0x01f7011641LL, 0x01db710641LL);
+    const __m128i* q = reinterpret_cast<const __m128i*>(p);
+    __m128i x1 = _mm_loadu_si128(q + 0), x2 = _mm_loadu_si128(q + 1);
+    __m128i x3 = _mm_loadu_si128(q + 2), x4 = _mm_loadu_si128(q + 3);
+    x1 = _mm_xor_si128(x1, _mm_cvtsi32_si128((int)c));
+    q += 4;
+    n -= 64;
+    for (; n >= 64; n -= 64, q += 4) {
+        x1 = fold(x1, k1k2, _mm_loadu_si128(q + 0));
+        x2 = fold(x2, k1k2, _mm_loadu_si128(q + 1));
+        x3 = fold(x3, k1k2, _mm_loadu_si128(q + 2));
+        x4 = fold(x4, k1k2, _mm_loadu_si128(q + 3));
+    }
+    x1 = fold(x1, k3k4, x2);
+    x1 = fold(x1, k3k4, x3);
+    x1 = fold(x1, k3k4, x4);
+    for (; n >= 16; n -= 16, ++q) x1 = fold(x1, k3k4, _mm_loadu_si128(q));
+    // 128 -> 64 bits
+    const __m128i mask32 = _mm_setr_epi32(~0, 0, ~0, 0);
+    __m128i x2b = _mm_clmulepi64_si128(x1, k3k4, 0x10);
+    x1 = _mm_xor_si128(_mm_srli_si128(x1, 8), x2b);
+    x2b = _mm_srli_si128(x1, 4);
+    x1 = _mm_and_si128(x1, mask32);
+    x1 = _mm_xor_si128(_mm_clmulepi64_si128(x1, k5, 0x00), x2b);
+    // Barrett reduction 64 -> 32
+    x2b = _mm_and_si128(x1, mask32);
+    x2b = _mm_clmulepi64_si128(x2b, poly, 0x10);
+    x2b = _mm_and_si128(x2b, mask32);
+    x2b = _mm_clmulepi64_si128(x2b, poly, 0x00);
+    x1 = _mm_xor_si128(x1, x2b);
+    c = (uint32_t)_mm_extract_epi32(x1, 1);
+    return crc_raw_sliced(c, reinterpret_cast<const uint8_t*>(q), n);
+}
+
+static bool have_clmul() {
+    static const bool ok = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+    return ok;
+}
+#endif
+
 // --------------------------------------------------------------- bencode
 // Decimal digits of v at the END of buf[0..20); returns the first digit's index.
 static int put_u64(char* buf, uint64_t v) {
@@ -188,9 +362,65 @@ void bencode_info(std::string& out, int64_t piece_length, const uint32_t* sums, 
 }
 
 }  // namespace
+
+void host_sha256_blocks(uint32_t h[8], const uint8_t* p, size_t nblocks) {
+#if defined(__x86_64__)
+    if (!host_portable() && have_sha_ni()) return sha256_blocks_ni(h, p, nblocks);
+#endif
+    sha256_blocks_portable(h, p, nblocks);
+}
+
+// Digest of (absorbed bytes folded into h) || tail[0..n) without touching h.
+void host_sha256_final(const uint32_t h[8], uint64_t absorbed, const uint8_t* tail, size_t n, uint8_t out[32]) {
+    uint32_t s[8];
+    memcpy(s, h, sizeof s);
+    host_sha256_blocks(s, tail, n / 64);
+    const size_t r = n % 64;
+    uint8_t b[128] = {};
+    memcpy(b, tail + n - r, r);
+    b[r] = 0x80;
+    const size_t tl = r < 56 ? 64 : 128;
+    const uint64_t bits = (absorbed + n) * 8;
+    for (int i = 0; i < 8; ++i) b[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    host_sha256_blocks(s, b, tl / 64);
+    for (int i = 0; i < 8; ++i)
+        for (int k = 0; k < 4; ++k) out[4 * i + k] = (uint8_t)(s[i] >> (24 - 8 * k));
+}
+
+// crc32.Update(crc, IEEETable, p).
+uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n) {
+    static std::once_flag once;
+    std::call_once(once, crc_tables_init);
+    uint32_t c = ~crc;
+#if defined(__x86_64__)
+    if (!host_portable() && have_clmul()) return ~crc_raw_clmul(c, p, n);
+#endif
+    return ~crc_raw_sliced(c, p, n);
+}
+
 }  // namespace krk
 
 extern "C" {
+
+int krk_host_sha256(const uint8_t* data, uint64_t n, uint8_t out32[32]) {
+    if (!out32 || (n && !data)) {
+        krk::set_error(KRK_EINVAL, "host_sha256: null argument");
+        return KRK_EINVAL;
+    }
+    static const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    krk::host_sha256_final(iv, 0, data, n, out32);
+    return KRK_OK;
+}
+
+int krk_host_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out) {
+    if (!out || (n && !data)) {
+        krk::set_error(KRK_EINVAL, "host_crc32_update: null argument");
+        return KRK_EINVAL;
+    }
+    *out = krk::host_crc32_update(crc, data, n);
+    return KRK_OK;
+}
 
 int krk_info_hash(int64_t piece_length, const uint32_t* sums, uint64_t n_sums, const char* name,
                   uint64_t name_len, int64_t length, uint8_t out20[20]) {

@@ -80,20 +80,41 @@ __device__ double go_log(double x) {
     return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
 }
 
-__device__ double hrw_score(const uint8_t* key, uint32_t klen, const uint8_t* label, uint32_t llen,
-                            int64_t weight) {
-#pragma clang fp contract(off)
+// hrw.UInt64ToFloat64 (rendezvous.go:99-118) of the murmur3 Sum h1 (its 8 big-endian
+// bytes) with MaxHashValue = 8 x 0xFF: the low 53 bits; when they are all zero and a
+// hasher is given (every production caller: rehash = true), murmur3 of the 8 Sum bytes
+// once more; / 2^53, exact.
+__device__ __forceinline__ double u64_to_f64(uint64_t h1, bool rehash) {
     const uint64_t m53 = (1ULL << 53) - 1;
-    const uint64_t h1 = murmur3_h1_cat(key, klen, label, llen);
     uint64_t val = h1 & m53;
-    if (val == 0) {  // rendezvous.go:111-116: rehash the 8 big-endian Sum bytes once
+    if (val == 0 && rehash) {  // rendezvous.go:111-116
         uint8_t be[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) be[i] = (uint8_t)(h1 >> (56 - 8 * i));
         val = murmur3_h1_cat(be, 8, be, 0) & m53;
     }
-    const double sc = (double)val / 9007199254740992.0;  // / 2^53, exact
+    return (double)val / 9007199254740992.0;
+}
+
+__device__ double hrw_score(const uint8_t* key, uint32_t klen, const uint8_t* label, uint32_t llen,
+                            int64_t weight) {
+#pragma clang fp contract(off)
+    const double sc = u64_to_f64(murmur3_h1_cat(key, klen, label, llen), true);
     return -(double)weight / go_log(sc);
+}
+
+// UInt64ToFloat64 over n given Sum values (big-endian uint64 each): the same device
+// function the scoring kernel runs, so the rehash branch -- reached by 2^-53 of the
+// scored pairs -- is exercised with chosen inputs (rendezvous_test.go:59-98).
+__global__ void u64_to_f64_kernel(const uint64_t* vals, uint64_t n, int rehash, double* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = u64_to_f64(vals[i], rehash != 0);
+}
+
+hipError_t launch_u64_to_f64(const uint64_t* vals, uint64_t n, int rehash, double* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(u64_to_f64_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, vals, n, rehash, out);
+    return hipGetLastError();
 }
 
 constexpr int kHrwBlock = 256;

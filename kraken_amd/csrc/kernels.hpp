@@ -73,6 +73,7 @@ struct CrcLaunchCfg {
     int variant;       // crc32_pieces.hip launch_crc_items; default 7 (byte-addressable tables)
 };
 
+bool crc_variant_valid(int variant);
 hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, const CrcLaunchCfg& cfg,
                             hipStream_t s);
 
@@ -102,6 +103,10 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
                          uint32_t* out_state, hipStream_t s);
 // Lanes per stream launch_sha256 uses for a batch of n_jobs streams (1 or 2).
 int sha_lanes_for(uint32_t n_jobs);
+// Process-wide launch plan (KRK_SHA_PLAN_* of kraken_hip.h; diagnostic plans >= 100
+// only in the KRK_DIAG build).
+bool sha_plan_valid(int plan);
+void set_sha_plan(int plan);
 
 // ---------------------------------------------------------------- HRW
 // Scores for (key, node) pairs and the per-key descending order.
@@ -119,6 +124,8 @@ struct HrwArgs {
     double* scores;           // nullable: n_keys * n_nodes
 };
 hipError_t launch_hrw_order(const HrwArgs& a, hipStream_t s);
+// hrw.UInt64ToFloat64 of n Sum values (as uint64) on the device.
+hipError_t launch_u64_to_f64(const uint64_t* vals, uint64_t n, int rehash, double* out, hipStream_t s);
 
 // Locations filter over full orders (n_out == n_nodes rows).
 hipError_t launch_ring_filter(const int32_t* order, uint64_t n_rows, uint32_t n_nodes,

@@ -20,13 +20,10 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/kraken_hip.h"
-#include "crc_math.hpp"
-#include "kernels.hpp"
+#include "runtime.hpp"
 
 namespace krk {
 
-// ------------------------------------------------------------------ errors
 thread_local std::string t_err;
 thread_local int t_dev = 0;
 
@@ -38,470 +35,6 @@ void set_error(int code, const char* fmt, ...) {
     va_end(ap);
     (void)code;
     t_err = buf;
-}
-
-#define KRK_HIP(expr)                                                                 \
-    do {                                                                              \
-        hipError_t e_ = (expr);                                                       \
-        if (e_ != hipSuccess) {                                                       \
-            set_error(KRK_EHIP, "%s: %s", #expr, hipGetErrorString(e_));              \
-            return KRK_EHIP;                                                          \
-        }                                                                             \
-    } while (0)
-
-#define KRK_CHECK(cond, code, ...)        \
-    do {                                  \
-        if (!(cond)) {                    \
-            set_error(code, __VA_ARGS__); \
-            return code;                  \
-        }                                 \
-    } while (0)
-
-// ------------------------------------------------------------------ timing
-enum Kern { K_CRC, K_SHA, K_HRW, K_FILTER, K_GATHER, K_SYNTH, K_N };
-static const char* kKernNames[K_N] = {"crc32_pieces", "sha256_multi", "hrw_order",
-                                      "ring_filter",  "hrw_gather",   "synth_fill"};
-static std::atomic<bool> g_timing{false};
-struct Pending {
-    hipEvent_t a, b;
-    int k, dev;
-};
-static std::mutex g_tmu;
-static std::vector<Pending> g_pending;
-static double g_ms[K_N];
-static uint64_t g_cnt[K_N];
-
-template <class F>
-static hipError_t timed(int k, hipStream_t s, F&& f) {
-    if (!g_timing.load(std::memory_order_relaxed)) return f();
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    hipEventRecord(a, s);
-    hipError_t e = f();
-    hipEventRecord(b, s);
-    std::lock_guard<std::mutex> g(g_tmu);
-    g_pending.push_back({a, b, k, t_dev});
-    return e;
-}
-
-static void drain_timing() {
-    std::lock_guard<std::mutex> g(g_tmu);
-    int cur = 0;
-    hipGetDevice(&cur);
-    for (auto& p : g_pending) {
-        hipSetDevice(p.dev);
-        hipEventSynchronize(p.b);
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
-            g_ms[p.k] += ms;
-            g_cnt[p.k] += 1;
-        }
-        hipEventDestroy(p.a);
-        hipEventDestroy(p.b);
-    }
-    g_pending.clear();
-    hipSetDevice(cur);
-}
-
-// ------------------------------------------------------------------ device
-struct PinnedSlot {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipEvent_t ev = nullptr;
-    bool busy = false;
-};
-
-// Stream-ordered device scratch.  Blocks are power-of-two sized and stay with the
-// device context; a released block carries an event recorded on the releasing
-// stream and its next user's stream waits on that event, so reuse is ordered on
-// the device with no host stall and no allocator work per call.
-struct DevCache {
-    struct Blk {
-        void* p = nullptr;
-        size_t cap = 0;
-        hipEvent_t ev = nullptr;
-        bool pending = false;
-    };
-    std::mutex mu;
-    std::unordered_map<void*, Blk> live;
-    std::unordered_multimap<size_t, Blk> idle;
-
-    hipError_t alloc(void** out, size_t n, hipStream_t s) {
-        size_t cap = 256;
-        while (cap < n) cap <<= 1;
-        Blk b;
-        {
-            std::lock_guard<std::mutex> g(mu);
-            auto it = idle.find(cap);
-            if (it != idle.end()) {
-                b = it->second;
-                idle.erase(it);
-            }
-        }
-        hipError_t e = hipSuccess;
-        if (b.p) {
-            if (b.pending) e = hipStreamWaitEvent(s, b.ev, 0);
-        } else {
-            e = hipMalloc(&b.p, cap);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
-            b.cap = cap;
-        }
-        if (e != hipSuccess) return e;
-        std::lock_guard<std::mutex> g(mu);
-        live[b.p] = b;
-        *out = b.p;
-        return hipSuccess;
-    }
-    void release(void* p, hipStream_t s) {
-        if (!p) return;
-        std::lock_guard<std::mutex> g(mu);
-        auto it = live.find(p);
-        if (it == live.end()) return;
-        Blk b = it->second;
-        live.erase(it);
-        b.pending = hipEventRecord(b.ev, s) == hipSuccess;
-        if (!b.pending) hipStreamSynchronize(s);
-        idle.emplace(b.cap, b);
-    }
-};
-
-struct Pipeline;
-
-struct Device {
-    DevCache cache;
-    // Staging windows of the host paths, kept across calls (pinning 2 x 256 MiB
-    // costs ~0.2 s, a third of a 16 GB end-to-end batch).  Leaked at exit like the
-    // other device resources: freeing pinned memory during static destruction can
-    // race the HIP runtime's own teardown.
-    Pipeline* staging = nullptr;
-    std::mutex staging_mu;
-    // The 65,536 ShardID keys (2 bytes each) of the Locations shard table, uploaded
-    // once: constant input of every krk_ring_locations_dev call.
-    uint8_t* shard_kb = nullptr;
-    uint64_t* shard_koff = nullptr;
-    uint8_t* shard_bad = nullptr;
-    std::once_flag shard_once;
-    int shard_rc = 0;
-    int id = 0;
-    int cus = 0;
-    hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
-    uint32_t* d_tabs = nullptr;
-    int crc_variant = 0;
-    std::mutex mu;
-    PinnedSlot slots[8];
-    unsigned next_slot = 0;
-};
-
-template <class T>
-static hipError_t scratch_alloc(Device* D, T** p, size_t n, hipStream_t s) {
-    void* v = nullptr;
-    hipError_t e = D->cache.alloc(&v, n, s);
-    *p = static_cast<T*>(v);
-    return e;
-}
-static void scratch_free(Device* D, void* p, hipStream_t s) { D->cache.release(p, s); }
-
-static std::mutex g_dmu;
-static std::vector<std::unique_ptr<Device>> g_devs;
-static X8Pow g_x8;
-static std::once_flag g_x8_once;
-
-static const X8Pow& x8() {
-    std::call_once(g_x8_once, [] { g_x8 = make_x8pow(); });
-    return g_x8;
-}
-
-static int init_device(Device& D, int id) {
-    D.id = id;
-    KRK_HIP(hipSetDevice(id));
-    hipDeviceProp_t prop;
-    KRK_HIP(hipGetDeviceProperties(&prop, id));
-    KRK_CHECK(strncmp(prop.gcnArchName, "gfx950", 6) == 0, KRK_ENODEV,
-              "device %d is %s, this build targets gfx950 (MI355X)", id, prop.gcnArchName);
-    D.cus = prop.multiProcessorCount;
-    KRK_HIP(hipStreamCreateWithFlags(&D.s_main, hipStreamNonBlocking));
-    KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
-    KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
-    std::vector<uint32_t> tabs(kTabWords);
-    make_slice_tables(tabs.data() + kTabT);
-    const X8Pow& xp = x8();
-    make_shift_tables(tabs.data() + kTabG, x8n(kGap, xp.v));
-    for (int l = 0; l < 64; ++l) tabs[kTabLaneMul + l] = x8n(uint64_t(63 - l) * kSeg, xp.v);
-    for (int k = 0; k < 64; ++k) tabs[kTabX8Pow + k] = xp.v[k];
-    make_shift_tables(tabs.data() + kTabGC, x8n(kGapC, xp.v));
-    for (int k = 0; k < 4; ++k)
-        for (int l = 0; l < 64; ++l)
-            tabs[kTabLaneMulC + k * 64 + l] = x8n(uint64_t(kGapC) - 1024 * k - 16 * l, xp.v);
-    KRK_HIP(hipMalloc(&D.d_tabs, kTabWords * 4));
-    KRK_HIP(hipMemcpy(D.d_tabs, tabs.data(), kTabWords * 4, hipMemcpyHostToDevice));
-    const char* v = getenv("KRK_CRC_VARIANT");
-    D.crc_variant = v ? atoi(v) : 7;  // byte-addressable tables (crc32_pieces.hip)
-    return KRK_OK;
-}
-
-static Device* device(int* rc) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
-        set_error(KRK_ENODEV, "no HIP device visible");
-        *rc = KRK_ENODEV;
-        return nullptr;
-    }
-    if (t_dev < 0 || t_dev >= n) {
-        set_error(KRK_ENODEV, "device %d out of range (%d visible)", t_dev, n);
-        *rc = KRK_ENODEV;
-        return nullptr;
-    }
-    std::lock_guard<std::mutex> g(g_dmu);
-    if ((int)g_devs.size() < n) g_devs.resize(n);
-    if (!g_devs[t_dev]) {
-        auto D = std::make_unique<Device>();
-        int r = init_device(*D, t_dev);
-        if (r != KRK_OK) {
-            *rc = r;
-            return nullptr;
-        }
-        g_devs[t_dev] = std::move(D);
-    }
-    if (hipSetDevice(t_dev) != hipSuccess) {
-        set_error(KRK_EHIP, "hipSetDevice(%d) failed", t_dev);
-        *rc = KRK_EHIP;
-        return nullptr;
-    }
-    *rc = KRK_OK;
-    return g_devs[t_dev].get();
-}
-
-#define KRK_DEVICE(D)         \
-    int rc_ = KRK_OK;         \
-    Device* D = device(&rc_); \
-    if (!D) return rc_;
-
-static hipStream_t pick(Device* D, void* s) { return s ? static_cast<hipStream_t>(s) : D->s_main; }
-
-// Stage `n` host bytes through a pinned slot into a fresh stream-ordered device
-// scratch block (released with scratch_free by the caller).
-static int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_t s) {
-    *d_out = nullptr;
-    if (!n) return KRK_OK;
-    KRK_HIP(scratch_alloc(D, d_out, n, s));
-    std::lock_guard<std::mutex> g(D->mu);
-    PinnedSlot& P = D->slots[D->next_slot++ % 8];
-    if (P.busy) {
-        KRK_HIP(hipEventSynchronize(P.ev));
-        P.busy = false;
-    }
-    if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
-    if (P.cap < n) {
-        if (P.p) hipHostFree(P.p);
-        P.p = nullptr;  // a failed grow leaves an empty slot, not a dangling one
-        P.cap = 0;
-        const size_t cap = std::max<size_t>(n, 1 << 20);
-        KRK_HIP(hipHostMalloc(&P.p, cap, hipHostMallocDefault));
-        P.cap = cap;
-    }
-    memcpy(P.p, src, n);
-    KRK_HIP(hipMemcpyAsync(*d_out, P.p, n, hipMemcpyHostToDevice, s));
-    KRK_HIP(hipEventRecord(P.ev, s));
-    P.busy = true;
-    return KRK_OK;
-}
-
-// ------------------------------------------------------------------ CRC items
-// The work of one CRC launch: runs of whole pieces (expanded into items on the
-// device) plus explicit items for partial pieces and seeded CRCs.
-struct CrcBatch {
-    std::vector<CrcRun> runs;
-    std::vector<CrcItem> items;
-    std::vector<uint32_t> consts;
-    std::unordered_map<uint64_t, uint32_t> pat;  // piece length -> consts index of its pattern
-    uint64_t run_items = 0;
-    bool empty() const { return runs.empty() && items.empty(); }
-};
-
-// Items for bytes [a, b) of one blob (length L, pieces of P bytes), where blob byte
-// `a` lives at device address `base`.  `seed` is the register the IEEE CRC starts
-// from (~crc of crc32.Update; ~0 for PieceHash()).
-struct ItemBuilder {
-    std::unordered_map<uint64_t, uint32_t> cache;
-
-    uint32_t X(uint64_t n) {
-        if (n == 0) return kOne;
-        auto it = cache.find(n);
-        if (it != cache.end()) return it->second;
-        const uint32_t v = x8n(n, x8().v);
-        cache.emplace(n, v);
-        return v;
-    }
-
-    void piece(std::vector<CrcItem>& out, uint64_t ptr_of_ps, uint64_t ps, uint64_t pe, uint64_t s,
-               uint64_t e, uint32_t out_idx, uint32_t seed) {
-        // Items start at multiples of kItemBytes from the piece start (or at s).
-        for (uint64_t q = s; q < e;) {
-            const uint64_t next = std::min(e, ps + ((q - ps) / kItemBytes + 1) * kItemBytes);
-            CrcItem it{};
-            it.ptr = ptr_of_ps + (q - ps);
-            it.len = (uint32_t)(next - q);
-            it.out = out_idx;
-            it.mul = X(pe - next);
-            it.xr = (q == ps) ? (gf2_mulmod(seed, X(pe - ps)) ^ 0xFFFFFFFFu) : 0u;
-            out.push_back(it);
-            q = next;
-        }
-    }
-
-    // consts index of the whole-piece pattern for piece length P (item muls, then xr).
-    uint32_t pattern(CrcBatch& B, uint64_t P) {
-        auto it = B.pat.find(P);
-        if (it != B.pat.end()) return it->second;
-        const uint32_t at = (uint32_t)B.consts.size();
-        for (uint64_t q = 0; q < P; q += kItemBytes) B.consts.push_back(X(P - std::min(q + kItemBytes, P)));
-        B.consts.push_back(gf2_mulmod(0xFFFFFFFFu, X(P)) ^ 0xFFFFFFFFu);
-        B.pat.emplace(P, at);
-        return at;
-    }
-
-    // Whole pieces [f0, f1) of a blob whose piece f0 starts at device address ptr.
-    void run(CrcBatch& B, uint64_t ptr, uint64_t f0, uint64_t f1, uint64_t P, uint64_t sums_off) {
-        const uint64_t ipp = (P + kItemBytes - 1) / kItemBytes;
-        const uint32_t cpat = pattern(B, P);
-        for (uint64_t f = f0; f < f1;) {  // a run's item count stays below 2^31
-            const uint64_t n = std::min<uint64_t>(f1 - f, std::max<uint64_t>(1, (1ull << 31) / ipp));
-            CrcRun r{};
-            r.ptr = ptr + (f - f0) * P;
-            r.plen = P;
-            r.n_pieces = (uint32_t)n;
-            r.out = (uint32_t)(sums_off + f);
-            r.item_base = (uint32_t)B.run_items;
-            r.ipp = (uint32_t)ipp;
-            r.cpat = cpat;
-            B.runs.push_back(r);
-            B.run_items += n * ipp;
-            f += n;
-        }
-    }
-
-    void add(CrcBatch& B, uint64_t base, uint64_t a, uint64_t b, uint64_t L, uint64_t P, uint64_t sums_off,
-             uint32_t seed = 0xFFFFFFFFu) {
-        if (a >= b) return;
-        const uint64_t pa = a / P, pb = (b - 1) / P;  // pieces touched, inclusive
-        // Whole pieces [f0, f1): inside [a, b), full length, unseeded -> one run.
-        uint64_t f0 = (a + P - 1) / P, f1 = std::min(b, L) / P;
-        if (seed != 0xFFFFFFFFu || f1 <= f0) f0 = f1 = pb + 1;
-        for (uint64_t pi = pa; pi <= pb; ++pi) {
-            if (pi == f0) {
-                run(B, base + f0 * P - a, f0, f1, P, sums_off);
-                pi = f1 - 1;
-                continue;
-            }
-            const uint64_t ps = pi * P, pe = std::min(ps + P, L);
-            const uint64_t s = std::max(a, ps), e = std::min(b, pe);
-            const uint64_t ptr_ps = base + ps - a;  // may point before base; only offsets >= s used
-            piece(B.items, ptr_ps, ps, pe, s, e, (uint32_t)(sums_off + pi), seed);
-        }
-    }
-};
-
-static int validate_blobs(const krk_blob* blobs, uint64_t n) {
-    KRK_CHECK(n == 0 || blobs, KRK_EINVAL, "blobs is NULL");
-    for (uint64_t i = 0; i < n; ++i) {
-        KRK_CHECK(blobs[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
-        KRK_CHECK(blobs[i].length == 0 || blobs[i].data, KRK_EINVAL, "blob %llu: data is NULL",
-                  (unsigned long long)i);
-        const uint64_t np = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
-        KRK_CHECK(blobs[i].sums_offset + np <= 0xFFFFFFFFull, KRK_EINVAL,
-                  "sums index exceeds 2^32 in one call");
-    }
-    return KRK_OK;
-}
-
-// Zero the sums span [lo, hi) that the blobs cover.
-static void sums_span(const krk_blob* blobs, uint64_t n, uint64_t* lo, uint64_t* hi) {
-    *lo = UINT64_MAX;
-    *hi = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t np = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
-        if (!np) continue;
-        *lo = std::min(*lo, blobs[i].sums_offset);
-        *hi = std::max(*hi, blobs[i].sums_offset + np);
-    }
-    if (*lo > *hi) *lo = *hi = 0;
-}
-
-static int run_items(Device* D, const CrcBatch& B, uint32_t* sums_dev, hipStream_t s) {
-    if (B.empty()) return KRK_OK;
-    KRK_CHECK(B.run_items + B.items.size() < (1ull << 32), KRK_EINVAL, "more than 2^32 CRC work items in one call");
-    // One upload: [runs][items][consts], each part 16-byte aligned.
-    const size_t nr = B.runs.size() * sizeof(CrcRun), ni = B.items.size() * sizeof(CrcItem);
-    const size_t nc = B.consts.size() * 4;
-    std::vector<uint8_t> pack(nr + ni + nc);
-    if (nr) memcpy(pack.data(), B.runs.data(), nr);
-    if (ni) memcpy(pack.data() + nr, B.items.data(), ni);
-    if (nc) memcpy(pack.data() + nr + ni, B.consts.data(), nc);
-    void* d_pack = nullptr;
-    int r = upload(D, pack.data(), pack.size(), &d_pack, s);
-    if (r) return r;
-    const uint8_t* dp = static_cast<const uint8_t*>(d_pack);
-    CrcWork w{};
-    w.runs = reinterpret_cast<const CrcRun*>(dp);
-    w.items = reinterpret_cast<const CrcItem*>(dp + nr);
-    w.consts = reinterpret_cast<const uint32_t*>(dp + nr + ni);
-    w.n_runs = (uint32_t)B.runs.size();
-    w.run_items = (uint32_t)B.run_items;
-    w.n_items = (uint32_t)B.items.size();
-    CrcLaunchCfg cfg{D->cus, D->crc_variant};
-    hipError_t e = timed(K_CRC, s, [&] { return launch_crc_items(w, D->d_tabs, sums_dev, cfg, s); });
-    scratch_free(D, d_pack, s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
-    return KRK_OK;
-}
-
-static int piece_sums_dev(Device* D, const krk_blob* blobs, uint64_t n, uint32_t* sums_dev, hipStream_t s) {
-    int r = validate_blobs(blobs, n);
-    if (r) return r;
-    uint64_t lo, hi;
-    sums_span(blobs, n, &lo, &hi);
-    if (hi == lo) return KRK_OK;
-    KRK_CHECK(sums_dev, KRK_EINVAL, "sums_dev is NULL");
-    KRK_HIP(hipMemsetAsync(sums_dev + lo, 0, (hi - lo) * 4, s));
-    ItemBuilder B;
-    CrcBatch items;
-    for (uint64_t i = 0; i < n; ++i)
-        B.add(items, reinterpret_cast<uint64_t>(blobs[i].data), 0, blobs[i].length, blobs[i].length,
-              (uint64_t)blobs[i].piece_length, blobs[i].sums_offset);
-    return run_items(D, items, sums_dev, s);
-}
-
-// ------------------------------------------------------------------ SHA jobs
-static const uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
-                                0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-
-static int run_jobs(Device* D, std::vector<ShaJob>& jobs, uint8_t* digests_dev, uint32_t* state_dev,
-                    hipStream_t s) {
-    if (jobs.empty()) return KRK_OK;
-    // Longest streams first: lanes of one wave then carry similar lengths.
-    std::stable_sort(jobs.begin(), jobs.end(), [](const ShaJob& a, const ShaJob& b) { return a.len > b.len; });
-    void* d_jobs = nullptr;
-    int r = upload(D, jobs.data(), jobs.size() * sizeof(ShaJob), &d_jobs, s);
-    if (r) return r;
-    hipError_t e = timed(K_SHA, s, [&] {
-        return launch_sha256(static_cast<const ShaJob*>(d_jobs), (uint32_t)jobs.size(), digests_dev,
-                             state_dev, s);
-    });
-    scratch_free(D, d_jobs, s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", hipGetErrorString(e));
-    return KRK_OK;
-}
-
-static ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
-    ShaJob j{};
-    j.ptr = reinterpret_cast<uint64_t>(p);
-    j.len = len;
-    j.prefix = 0;
-    j.out = out;
-    j.flags = kShaFinal;
-    memcpy(j.h, kIV, sizeof kIV);
-    return j;
 }
 
 // Device allocations of one host-path call, freed on every return path (hipFree
@@ -689,6 +222,9 @@ static void par_copy(const std::vector<CopyTask>& tasks) {
     for (auto& t : th) t.join();
 }
 
+void engine_teardown(Device& D);                 // engine.cpp
+void set_device_set_from_mask(uint64_t mask);    // multidev.cpp
+
 // Everything a device context holds: streams, tables, scratch cache, pinned
 // upload slots, staging windows, the shard-key table.  Only for krk_shutdown.
 static void teardown_device(Device& D) {
@@ -821,6 +357,7 @@ int krk_init(uint64_t dev_mask) {
     if (!r) {
         int rc = KRK_OK;
         device(&rc);  // restore the calling thread's current device
+        if (dev_mask) set_device_set_from_mask(dev_mask);  // the multi-device entry points' devices
     }
     return r;
 }
@@ -829,6 +366,7 @@ int krk_shutdown(void) {
     std::lock_guard<std::mutex> g(g_dmu);
     for (auto& D : g_devs)
         if (D) {
+            engine_teardown(*D);  // dispatcher threads first: they launch on this context
             teardown_device(*D);
             D.reset();
         }
@@ -1391,142 +929,6 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     return r;
 }
 
-// ---------------------------------------------------------------- piece stream
-struct krk_piece_stream {
-    Device* D = nullptr;
-    uint64_t P = 0;
-    size_t W = 0;
-    Pipeline pl;
-    int cur = 0;
-    size_t fill = 0;
-    uint64_t flushed = 0;  // bytes already handed to the device
-    uint32_t* d_sums = nullptr;
-    uint64_t sums_cap = 0;
-    ItemBuilder B;
-    int err = KRK_OK;
-};
-
-static int stream_grow_sums(krk_piece_stream* s, uint64_t need) {
-    if (need <= s->sums_cap) return KRK_OK;
-    uint64_t cap = std::max<uint64_t>(need, s->sums_cap * 2 + 1024);
-    uint32_t* n = nullptr;
-    KRK_HIP(scratch_alloc(s->D, &n, cap * 4, s->D->s_b));
-    KRK_HIP(hipMemsetAsync(n, 0, cap * 4, s->D->s_b));
-    if (s->d_sums) {
-        KRK_HIP(hipMemcpyAsync(n, s->d_sums, s->sums_cap * 4, hipMemcpyDeviceToDevice, s->D->s_b));
-        scratch_free(s->D, s->d_sums, s->D->s_b);
-    }
-    s->d_sums = n;
-    s->sums_cap = cap;
-    return KRK_OK;
-}
-
-static int stream_flush(krk_piece_stream* s, bool final) {
-    Window& w = s->pl.w[s->cur];
-    const uint64_t a = s->flushed, b = s->flushed + s->fill;
-    const uint64_t L = b;  // non-final flushes hold whole pieces only, so L = b is exact for them
-    if (s->fill) {
-        int r = stream_grow_sums(s, krk_num_pieces(b, (int64_t)s->P));
-        if (r) return r;
-        CrcBatch items;
-        s->B.add(items, reinterpret_cast<uint64_t>(w.dev), a, b, L, s->P, 0);
-        KRK_HIP(s->pl.h2d(s->cur, s->fill, s->D->s_a));
-        KRK_HIP(hipStreamWaitEvent(s->D->s_b, w.copied, 0));
-        r = run_items(s->D, items, s->d_sums, s->D->s_b);
-        if (r) return r;
-        KRK_HIP(s->pl.release(s->cur, 0, s->D->s_b));
-    }
-    s->flushed = b;
-    s->fill = 0;
-    (void)final;
-    s->cur ^= 1;
-    return s->pl.acquire(s->cur);
-}
-
-int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out) {
-    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
-    KRK_CHECK(piece_length > 0, KRK_EINVAL, "piece length must be positive");
-    KRK_DEVICE(D);
-    auto* s = new krk_piece_stream();
-    s->D = D;
-    s->P = (uint64_t)piece_length;
-    const uint64_t target = 64ull << 20;
-    s->W = (size_t)(s->P * std::max<uint64_t>(1, target / s->P));
-    int r = s->pl.init(s->W);
-    if (r) { delete s; return r; }
-    *out = s;
-    return KRK_OK;
-}
-
-int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
-    KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
-    if (s->err) return s->err;
-    KRK_CHECK(n == 0 || buf, KRK_EINVAL, "buffer is NULL");
-    KRK_HIP(hipSetDevice(s->D->id));
-    while (n) {
-        const size_t take = std::min<uint64_t>(n, s->W - s->fill);
-        memcpy(s->pl.w[s->cur].host + s->fill, buf, take);
-        s->fill += take;
-        buf += take;
-        n -= take;
-        if (s->fill == s->W) {
-            int r = stream_flush(s, false);
-            if (r) return s->err = r;
-        }
-    }
-    return KRK_OK;
-}
-
-int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, uint64_t* n_sums,
-                         uint64_t* length) {
-    KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
-    if (s->err) return s->err;
-    KRK_HIP(hipSetDevice(s->D->id));
-    int r = stream_flush(s, true);
-    if (r) return r;
-    KRK_HIP(hipStreamSynchronize(s->D->s_b));
-    const uint64_t np = krk_num_pieces(s->flushed, (int64_t)s->P);
-    if (n_sums) *n_sums = np;
-    if (length) *length = s->flushed;
-    KRK_CHECK(np <= cap || !sums_out, KRK_ERANGE, "sums capacity %llu < %llu pieces", (unsigned long long)cap,
-              (unsigned long long)np);
-    if (sums_out && np) KRK_HIP(hipMemcpy(sums_out, s->d_sums, np * 4, hipMemcpyDeviceToHost));
-    return KRK_OK;
-}
-
-void krk_piece_stream_free(krk_piece_stream* s) {
-    if (!s) return;
-    hipSetDevice(s->D->id);
-    hipStreamSynchronize(s->D->s_b);
-    scratch_free(s->D, s->d_sums, s->D->s_b);
-    delete s;
-}
-
-int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out) {
-    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
-    if (n == 0) { *out = crc; return KRK_OK; }
-    KRK_CHECK(data, KRK_EINVAL, "data is NULL");
-    KRK_DEVICE(D);
-    hipStream_t s = D->s_main;
-    uint8_t* d_buf = nullptr;
-    uint32_t* d_sum = nullptr;
-    KRK_HIP(scratch_alloc(D, reinterpret_cast<void**>(&d_buf), n + 4, s));
-    KRK_HIP(scratch_alloc(D, reinterpret_cast<void**>(&d_sum), 4, s));
-    KRK_HIP(hipMemcpyAsync(d_buf, data, n, hipMemcpyHostToDevice, s));
-    KRK_HIP(hipMemsetAsync(d_sum, 0, 4, s));
-    ItemBuilder B;
-    CrcBatch items;
-    // crc32.Update(crc, IEEETable, p) = ~raw(~crc, p): one piece seeded with ~crc.
-    B.add(items, reinterpret_cast<uint64_t>(d_buf), 0, n, n, n, 0, ~crc);
-    int r = run_items(D, items, d_sum, s);
-    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
-    if (!r && hipMemcpy(out, d_sum, 4, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
-    scratch_free(D, d_buf, s);
-    scratch_free(D, d_sum, s);
-    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "crc32_update sync"); r = KRK_EHIP; }
-    return r;
-}
-
 int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, uint8_t* ok_out_host, void* stream) {
     KRK_CHECK(blob && expected_host && ok_out_host, KRK_EINVAL, "verify: null argument");
     KRK_DEVICE(D);
@@ -1569,116 +971,6 @@ int krk_verify_pieces_host(const uint8_t* const* data, const uint64_t* lengths, 
     if (r) return r;
     for (uint64_t i = 0; i < n; ++i) ok_out[i] = sums[i] == expected[i];
     return KRK_OK;
-}
-
-// ---------------------------------------------------------------- digester
-struct krk_digester {
-    Device* D = nullptr;
-    Pipeline pl;
-    size_t W = 0;
-    int cur = 0;
-    size_t fill = 0;
-    uint64_t absorbed = 0;  // bytes folded into the device midstate
-    uint32_t* d_state = nullptr;
-    uint8_t* d_dig = nullptr;
-};
-
-static int digester_flush_blocks(krk_digester* d) {
-    // Fold the whole-block prefix of the pending bytes into the midstate.
-    const size_t nb = d->fill & ~size_t(63);
-    if (!nb) return KRK_OK;
-    Window& w = d->pl.w[d->cur];
-    hipStream_t s = d->D->s_b;
-    KRK_HIP(hipMemcpyAsync(w.dev, w.host, nb, hipMemcpyHostToDevice, s));
-    std::vector<ShaJob> jobs(1);
-    ShaJob& j = jobs[0];
-    j = ShaJob{};
-    j.ptr = reinterpret_cast<uint64_t>(w.dev);
-    j.len = nb;
-    j.prefix = d->absorbed;
-    j.out = 0;
-    j.flags = d->absorbed ? kShaFromState : 0;
-    memcpy(j.h, kIV, sizeof kIV);
-    int r = run_jobs(d->D, jobs, d->d_dig, d->d_state, s);
-    if (r) return r;
-    KRK_HIP(hipEventRecord(w.consumed, s));
-    w.inflight = true;
-    d->absorbed += nb;
-    const size_t rest = d->fill - nb;
-    const int nxt = d->cur ^ 1;
-    r = d->pl.acquire(nxt);
-    if (r) return r;
-    if (rest) memcpy(d->pl.w[nxt].host, w.host + nb, rest);
-    d->fill = rest;
-    d->cur = nxt;
-    return KRK_OK;
-}
-
-int krk_digester_new(krk_digester** out) {
-    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
-    KRK_DEVICE(D);
-    auto* d = new krk_digester();
-    d->D = D;
-    d->W = 16u << 20;
-    int r = d->pl.init(d->W + 64);
-    if (!r && hipMalloc(&d->d_state, 32) != hipSuccess) r = KRK_ENOMEM;
-    if (!r && hipMalloc(&d->d_dig, 32) != hipSuccess) r = KRK_ENOMEM;
-    if (r) { delete d; set_error(r, "digester allocation failed"); return r; }
-    *out = d;
-    return KRK_OK;
-}
-
-int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
-    KRK_CHECK(d, KRK_EINVAL, "digester is NULL");
-    KRK_CHECK(n == 0 || buf, KRK_EINVAL, "buffer is NULL");
-    KRK_HIP(hipSetDevice(d->D->id));
-    while (n) {
-        const size_t take = std::min<uint64_t>(n, d->W - d->fill);
-        memcpy(d->pl.w[d->cur].host + d->fill, buf, take);
-        d->fill += take;
-        buf += take;
-        n -= take;
-        if (d->fill == d->W) {
-            int r = digester_flush_blocks(d);
-            if (r) return r;
-        }
-    }
-    return KRK_OK;
-}
-
-int krk_digester_sum(krk_digester* d, uint8_t out32[32]) {
-    KRK_CHECK(d && out32, KRK_EINVAL, "digester_sum: null argument");
-    KRK_HIP(hipSetDevice(d->D->id));
-    int r = digester_flush_blocks(d);
-    if (r) return r;
-    // Final job over the (< 64 B) pending tail from the midstate; the midstate is
-    // left untouched, so writing may continue (Digest() does not reset).
-    Window& w = d->pl.w[d->cur];
-    hipStream_t s = d->D->s_b;
-    if (d->fill) KRK_HIP(hipMemcpyAsync(w.dev, w.host, d->fill, hipMemcpyHostToDevice, s));
-    std::vector<ShaJob> jobs(1);
-    ShaJob& j = jobs[0];
-    j = ShaJob{};
-    j.ptr = reinterpret_cast<uint64_t>(w.dev);
-    j.len = d->fill;
-    j.prefix = d->absorbed;
-    j.out = 0;
-    j.flags = kShaFinal | (d->absorbed ? kShaFromState : 0);
-    memcpy(j.h, kIV, sizeof kIV);
-    r = run_jobs(d->D, jobs, d->d_dig, d->d_state, s);
-    if (r) return r;
-    KRK_HIP(hipStreamSynchronize(s));
-    KRK_HIP(hipMemcpy(out32, d->d_dig, 32, hipMemcpyDeviceToHost));
-    return KRK_OK;
-}
-
-void krk_digester_free(krk_digester* d) {
-    if (!d) return;
-    hipSetDevice(d->D->id);
-    hipStreamSynchronize(d->D->s_b);
-    hipFree(d->d_state);
-    hipFree(d->d_dig);
-    delete d;
 }
 
 // ---------------------------------------------------------------- HRW
@@ -1765,6 +1057,8 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
                     uint32_t n_out, int32_t* order_out, double* scores_out) {
     if (!n_keys) return KRK_OK;
     KRK_CHECK(keys && key_off && order_out, KRK_EINVAL, "hrw_ordered: null argument");
+    // rows are n_out wide (-1 padded past the node count); bounded like the node count
+    KRK_CHECK(n_out <= 4096, KRK_EINVAL, "n_out %u exceeds 4096", n_out);
     KRK_DEVICE(D);
     hipStream_t s = D->s_main;
     // hex.DecodeString per key (rendezvous.go:154-157).
@@ -1819,6 +1113,32 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
         set_error(KRK_EHEX, "invalid hex key: Score is NaN");
         return KRK_EHEX;
     }
+    return r;
+}
+
+int krk_hrw_uint64_to_float64(const uint8_t* sums8, uint64_t n, int rehash, double* out) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(sums8 && out, KRK_EINVAL, "hrw_uint64_to_float64: null argument");
+    KRK_DEVICE(D);
+    hipStream_t s = D->s_main;
+    std::vector<uint64_t> v(n);
+    for (uint64_t i = 0; i < n; ++i) {  // binary.BigEndian.Uint64
+        uint64_t x = 0;
+        for (int k = 0; k < 8; ++k) x = x << 8 | sums8[8 * i + k];
+        v[i] = x;
+    }
+    void* d_v = nullptr;
+    double* d_o = nullptr;
+    int r = upload(D, v.data(), n * 8, &d_v, s);
+    if (!r && scratch_alloc(D, &d_o, n * 8, s) != hipSuccess) r = KRK_ENOMEM;
+    if (!r) {
+        hipError_t e = launch_u64_to_f64(static_cast<const uint64_t*>(d_v), n, rehash, d_o, s);
+        if (e != hipSuccess) { set_error(KRK_EHIP, "u64_to_f64 launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "u64_to_f64 sync"); r = KRK_EHIP; }
+    if (!r && hipMemcpy(out, d_o, n * 8, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
+    if (d_v) scratch_free(D, d_v, s);
+    if (d_o) scratch_free(D, d_o, s);
     return r;
 }
 
@@ -2060,6 +1380,11 @@ int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes) {
     KRK_DEVICE(D);
     (void)D;
     *lanes = sha_lanes_for((uint32_t)n_streams);
+    return KRK_OK;
+}
+int krk_set_sha_plan(int plan) {
+    KRK_CHECK(sha_plan_valid(plan), KRK_EINVAL, "unknown SHA-256 launch plan %d", plan);
+    set_sha_plan(plan);
     return KRK_OK;
 }
 int krk_reset_kernel_stats(void) {

@@ -1,0 +1,508 @@
+// runtime.hpp -- internal to libkraken_hip: device contexts, the stream-ordered
+// scratch cache, the CRC work builder and the SHA job runner shared by the C ABI
+// (runtime.cpp) and the submission engine (engine.cpp).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kraken_hip.h"
+#include "crc_math.hpp"
+#include "kernels.hpp"
+
+namespace krk {
+
+// ------------------------------------------------------------------ errors
+extern thread_local std::string t_err;
+extern thread_local int t_dev;
+
+void set_error(int code, const char* fmt, ...);
+
+#define KRK_HIP(expr)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            set_error(KRK_EHIP, "%s: %s", #expr, hipGetErrorString(e_));              \
+            return KRK_EHIP;                                                          \
+        }                                                                             \
+    } while (0)
+
+#define KRK_CHECK(cond, code, ...)        \
+    do {                                  \
+        if (!(cond)) {                    \
+            set_error(code, __VA_ARGS__); \
+            return code;                  \
+        }                                 \
+    } while (0)
+
+// ------------------------------------------------------------------ timing
+enum Kern { K_CRC, K_SHA, K_HRW, K_FILTER, K_GATHER, K_SYNTH, K_N };
+inline const char* kKernNames[K_N] = {"crc32_pieces", "sha256_multi", "hrw_order",
+                                      "ring_filter",  "hrw_gather",   "synth_fill"};
+inline std::atomic<bool> g_timing{false};
+struct Pending {
+    hipEvent_t a, b;
+    int k, dev;
+};
+inline std::mutex g_tmu;
+inline std::vector<Pending> g_pending;
+inline double g_ms[K_N];
+inline uint64_t g_cnt[K_N];
+
+template <class F>
+inline hipError_t timed(int k, hipStream_t s, F&& f) {
+    if (!g_timing.load(std::memory_order_relaxed)) return f();
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, s);
+    hipError_t e = f();
+    hipEventRecord(b, s);
+    std::lock_guard<std::mutex> g(g_tmu);
+    g_pending.push_back({a, b, k, t_dev});
+    return e;
+}
+
+inline void drain_timing() {
+    std::lock_guard<std::mutex> g(g_tmu);
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (auto& p : g_pending) {
+        hipSetDevice(p.dev);
+        hipEventSynchronize(p.b);
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            g_ms[p.k] += ms;
+            g_cnt[p.k] += 1;
+        }
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    g_pending.clear();
+    hipSetDevice(cur);
+}
+
+// ------------------------------------------------------------------ device
+struct PinnedSlot {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool busy = false;
+};
+
+// Stream-ordered device scratch.  Blocks are power-of-two sized and stay with the
+// device context; a released block carries an event recorded on the releasing
+// stream and its next user's stream waits on that event, so reuse is ordered on
+// the device with no host stall and no allocator work per call.
+struct DevCache {
+    struct Blk {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    std::mutex mu;
+    std::unordered_map<void*, Blk> live;
+    std::unordered_multimap<size_t, Blk> idle;
+
+    hipError_t alloc(void** out, size_t n, hipStream_t s) {
+        size_t cap = 256;
+        while (cap < n) cap <<= 1;
+        Blk b;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = idle.find(cap);
+            if (it != idle.end()) {
+                b = it->second;
+                idle.erase(it);
+            }
+        }
+        hipError_t e = hipSuccess;
+        if (b.p) {
+            if (b.pending) e = hipStreamWaitEvent(s, b.ev, 0);
+        } else {
+            e = hipMalloc(&b.p, cap);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+            b.cap = cap;
+        }
+        if (e != hipSuccess) return e;
+        std::lock_guard<std::mutex> g(mu);
+        live[b.p] = b;
+        *out = b.p;
+        return hipSuccess;
+    }
+    void release(void* p, hipStream_t s) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        auto it = live.find(p);
+        if (it == live.end()) return;
+        Blk b = it->second;
+        live.erase(it);
+        b.pending = hipEventRecord(b.ev, s) == hipSuccess;
+        if (!b.pending) hipStreamSynchronize(s);
+        idle.emplace(b.cap, b);
+    }
+};
+
+struct Pipeline;
+struct Engine;
+
+struct Device {
+    // Submission engine (engine.cpp): the batching queues of the streaming
+    // Digester / piece-stream / crc32.Update calls, created on first use.
+    Engine* engine = nullptr;
+    std::mutex engine_mu;
+    DevCache cache;
+    // Staging windows of the host paths, kept across calls (pinning 2 x 256 MiB
+    // costs ~0.2 s, a third of a 16 GB end-to-end batch).  Leaked at exit like the
+    // other device resources: freeing pinned memory during static destruction can
+    // race the HIP runtime's own teardown.
+    Pipeline* staging = nullptr;
+    std::mutex staging_mu;
+    // The 65,536 ShardID keys (2 bytes each) of the Locations shard table, uploaded
+    // once: constant input of every krk_ring_locations_dev call.
+    uint8_t* shard_kb = nullptr;
+    uint64_t* shard_koff = nullptr;
+    uint8_t* shard_bad = nullptr;
+    std::once_flag shard_once;
+    int shard_rc = 0;
+    int id = 0;
+    int cus = 0;
+    hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
+    uint32_t* d_tabs = nullptr;
+    int crc_variant = 0;
+    std::mutex mu;
+    PinnedSlot slots[8];
+    unsigned next_slot = 0;
+};
+
+template <class T>
+inline hipError_t scratch_alloc(Device* D, T** p, size_t n, hipStream_t s) {
+    void* v = nullptr;
+    hipError_t e = D->cache.alloc(&v, n, s);
+    *p = static_cast<T*>(v);
+    return e;
+}
+inline void scratch_free(Device* D, void* p, hipStream_t s) { D->cache.release(p, s); }
+
+inline std::mutex g_dmu;
+inline std::vector<std::unique_ptr<Device>> g_devs;
+inline X8Pow g_x8;
+inline std::once_flag g_x8_once;
+
+inline const X8Pow& x8() {
+    std::call_once(g_x8_once, [] { g_x8 = make_x8pow(); });
+    return g_x8;
+}
+
+inline int init_device(Device& D, int id) {
+    D.id = id;
+    KRK_HIP(hipSetDevice(id));
+    hipDeviceProp_t prop;
+    KRK_HIP(hipGetDeviceProperties(&prop, id));
+    KRK_CHECK(strncmp(prop.gcnArchName, "gfx950", 6) == 0, KRK_ENODEV,
+              "device %d is %s, this build targets gfx950 (MI355X)", id, prop.gcnArchName);
+    D.cus = prop.multiProcessorCount;
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_main, hipStreamNonBlocking));
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
+    std::vector<uint32_t> tabs(kTabWords);
+    make_slice_tables(tabs.data() + kTabT);
+    const X8Pow& xp = x8();
+    make_shift_tables(tabs.data() + kTabG, x8n(kGap, xp.v));
+    for (int l = 0; l < 64; ++l) tabs[kTabLaneMul + l] = x8n(uint64_t(63 - l) * kSeg, xp.v);
+    for (int k = 0; k < 64; ++k) tabs[kTabX8Pow + k] = xp.v[k];
+    make_shift_tables(tabs.data() + kTabGC, x8n(kGapC, xp.v));
+    for (int k = 0; k < 4; ++k)
+        for (int l = 0; l < 64; ++l)
+            tabs[kTabLaneMulC + k * 64 + l] = x8n(uint64_t(kGapC) - 1024 * k - 16 * l, xp.v);
+    KRK_HIP(hipMalloc(&D.d_tabs, kTabWords * 4));
+    KRK_HIP(hipMemcpy(D.d_tabs, tabs.data(), kTabWords * 4, hipMemcpyHostToDevice));
+    // Launch variant, read once per device context (crc32_pieces.hip: 7 = byte-addressable
+    // tables, the default; 8 = its 16-replica form; the rest only in the KRK_DIAG build).
+    const char* v = getenv("KRK_CRC_VARIANT");
+    D.crc_variant = crc_variant_valid(v ? atoi(v) : 7) ? (v ? atoi(v) : 7) : 7;
+    return KRK_OK;
+}
+
+// The context of device `id` (created on first use); also makes it the calling
+// thread's current HIP device.
+inline Device* device_id(int id, int* rc) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error(KRK_ENODEV, "no HIP device visible");
+        *rc = KRK_ENODEV;
+        return nullptr;
+    }
+    if (id < 0 || id >= n) {
+        set_error(KRK_ENODEV, "device %d out of range (%d visible)", id, n);
+        *rc = KRK_ENODEV;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_dmu);
+    if ((int)g_devs.size() < n) g_devs.resize(n);
+    if (!g_devs[id]) {
+        auto D = std::make_unique<Device>();
+        int r = init_device(*D, id);
+        if (r != KRK_OK) {
+            *rc = r;
+            return nullptr;
+        }
+        g_devs[id] = std::move(D);
+    }
+    if (hipSetDevice(id) != hipSuccess) {
+        set_error(KRK_EHIP, "hipSetDevice(%d) failed", id);
+        *rc = KRK_EHIP;
+        return nullptr;
+    }
+    *rc = KRK_OK;
+    return g_devs[id].get();
+}
+
+// The calling thread's device (krk_set_device).
+inline Device* device(int* rc) { return device_id(t_dev, rc); }
+
+#define KRK_DEVICE(D)         \
+    int rc_ = KRK_OK;         \
+    Device* D = device(&rc_); \
+    if (!D) return rc_;
+
+inline hipStream_t pick(Device* D, void* s) { return s ? static_cast<hipStream_t>(s) : D->s_main; }
+
+// Stage `n` host bytes through a pinned slot into a fresh stream-ordered device
+// scratch block (released with scratch_free by the caller).
+inline int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_t s) {
+    *d_out = nullptr;
+    if (!n) return KRK_OK;
+    KRK_HIP(scratch_alloc(D, d_out, n, s));
+    std::lock_guard<std::mutex> g(D->mu);
+    PinnedSlot& P = D->slots[D->next_slot++ % 8];
+    if (P.busy) {
+        KRK_HIP(hipEventSynchronize(P.ev));
+        P.busy = false;
+    }
+    if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
+    if (P.cap < n) {
+        if (P.p) hipHostFree(P.p);
+        P.p = nullptr;  // a failed grow leaves an empty slot, not a dangling one
+        P.cap = 0;
+        const size_t cap = std::max<size_t>(n, 1 << 20);
+        KRK_HIP(hipHostMalloc(&P.p, cap, hipHostMallocDefault));
+        P.cap = cap;
+    }
+    memcpy(P.p, src, n);
+    KRK_HIP(hipMemcpyAsync(*d_out, P.p, n, hipMemcpyHostToDevice, s));
+    KRK_HIP(hipEventRecord(P.ev, s));
+    P.busy = true;
+    return KRK_OK;
+}
+
+// ------------------------------------------------------------------ CRC items
+// The work of one CRC launch: runs of whole pieces (expanded into items on the
+// device) plus explicit items for partial pieces and seeded CRCs.
+struct CrcBatch {
+    std::vector<CrcRun> runs;
+    std::vector<CrcItem> items;
+    std::vector<uint32_t> consts;
+    std::unordered_map<uint64_t, uint32_t> pat;  // piece length -> consts index of its pattern
+    uint64_t run_items = 0;
+    bool empty() const { return runs.empty() && items.empty(); }
+};
+
+// Items for bytes [a, b) of one blob (length L, pieces of P bytes), where blob byte
+// `a` lives at device address `base`.  `seed` is the register the IEEE CRC starts
+// from (~crc of crc32.Update; ~0 for PieceHash()).
+struct ItemBuilder {
+    std::unordered_map<uint64_t, uint32_t> cache;
+
+    uint32_t X(uint64_t n) {
+        if (n == 0) return kOne;
+        auto it = cache.find(n);
+        if (it != cache.end()) return it->second;
+        const uint32_t v = x8n(n, x8().v);
+        cache.emplace(n, v);
+        return v;
+    }
+
+    void piece(std::vector<CrcItem>& out, uint64_t ptr_of_ps, uint64_t ps, uint64_t pe, uint64_t s,
+               uint64_t e, uint32_t out_idx, uint32_t seed) {
+        // Items start at multiples of kItemBytes from the piece start (or at s).
+        for (uint64_t q = s; q < e;) {
+            const uint64_t next = std::min(e, ps + ((q - ps) / kItemBytes + 1) * kItemBytes);
+            CrcItem it{};
+            it.ptr = ptr_of_ps + (q - ps);
+            it.len = (uint32_t)(next - q);
+            it.out = out_idx;
+            it.mul = X(pe - next);
+            it.xr = (q == ps) ? (gf2_mulmod(seed, X(pe - ps)) ^ 0xFFFFFFFFu) : 0u;
+            out.push_back(it);
+            q = next;
+        }
+    }
+
+    // consts index of the whole-piece pattern for piece length P (item muls, then xr).
+    uint32_t pattern(CrcBatch& B, uint64_t P) {
+        auto it = B.pat.find(P);
+        if (it != B.pat.end()) return it->second;
+        const uint32_t at = (uint32_t)B.consts.size();
+        for (uint64_t q = 0; q < P; q += kItemBytes) B.consts.push_back(X(P - std::min(q + kItemBytes, P)));
+        B.consts.push_back(gf2_mulmod(0xFFFFFFFFu, X(P)) ^ 0xFFFFFFFFu);
+        B.pat.emplace(P, at);
+        return at;
+    }
+
+    // Whole pieces [f0, f1) of a blob whose piece f0 starts at device address ptr.
+    void run(CrcBatch& B, uint64_t ptr, uint64_t f0, uint64_t f1, uint64_t P, uint64_t sums_off) {
+        const uint64_t ipp = (P + kItemBytes - 1) / kItemBytes;
+        const uint32_t cpat = pattern(B, P);
+        for (uint64_t f = f0; f < f1;) {  // a run's item count stays below 2^31
+            const uint64_t n = std::min<uint64_t>(f1 - f, std::max<uint64_t>(1, (1ull << 31) / ipp));
+            CrcRun r{};
+            r.ptr = ptr + (f - f0) * P;
+            r.plen = P;
+            r.n_pieces = (uint32_t)n;
+            r.out = (uint32_t)(sums_off + f);
+            r.item_base = (uint32_t)B.run_items;
+            r.ipp = (uint32_t)ipp;
+            r.cpat = cpat;
+            B.runs.push_back(r);
+            B.run_items += n * ipp;
+            f += n;
+        }
+    }
+
+    void add(CrcBatch& B, uint64_t base, uint64_t a, uint64_t b, uint64_t L, uint64_t P, uint64_t sums_off,
+             uint32_t seed = 0xFFFFFFFFu) {
+        if (a >= b) return;
+        const uint64_t pa = a / P, pb = (b - 1) / P;  // pieces touched, inclusive
+        // Whole pieces [f0, f1): inside [a, b), full length, unseeded -> one run.
+        uint64_t f0 = (a + P - 1) / P, f1 = std::min(b, L) / P;
+        if (seed != 0xFFFFFFFFu || f1 <= f0) f0 = f1 = pb + 1;
+        for (uint64_t pi = pa; pi <= pb; ++pi) {
+            if (pi == f0) {
+                run(B, base + f0 * P - a, f0, f1, P, sums_off);
+                pi = f1 - 1;
+                continue;
+            }
+            const uint64_t ps = pi * P, pe = std::min(ps + P, L);
+            const uint64_t s = std::max(a, ps), e = std::min(b, pe);
+            const uint64_t ptr_ps = base + ps - a;  // may point before base; only offsets >= s used
+            piece(B.items, ptr_ps, ps, pe, s, e, (uint32_t)(sums_off + pi), seed);
+        }
+    }
+};
+
+inline int validate_blobs(const krk_blob* blobs, uint64_t n) {
+    KRK_CHECK(n == 0 || blobs, KRK_EINVAL, "blobs is NULL");
+    for (uint64_t i = 0; i < n; ++i) {
+        KRK_CHECK(blobs[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
+        KRK_CHECK(blobs[i].length == 0 || blobs[i].data, KRK_EINVAL, "blob %llu: data is NULL",
+                  (unsigned long long)i);
+        const uint64_t np = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
+        KRK_CHECK(blobs[i].sums_offset + np <= 0xFFFFFFFFull, KRK_EINVAL,
+                  "sums index exceeds 2^32 in one call");
+    }
+    return KRK_OK;
+}
+
+// Zero the sums span [lo, hi) that the blobs cover.
+inline void sums_span(const krk_blob* blobs, uint64_t n, uint64_t* lo, uint64_t* hi) {
+    *lo = UINT64_MAX;
+    *hi = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t np = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
+        if (!np) continue;
+        *lo = std::min(*lo, blobs[i].sums_offset);
+        *hi = std::max(*hi, blobs[i].sums_offset + np);
+    }
+    if (*lo > *hi) *lo = *hi = 0;
+}
+
+inline int run_items(Device* D, const CrcBatch& B, uint32_t* sums_dev, hipStream_t s) {
+    if (B.empty()) return KRK_OK;
+    KRK_CHECK(B.run_items + B.items.size() < (1ull << 32), KRK_EINVAL, "more than 2^32 CRC work items in one call");
+    // One upload: [runs][items][consts], each part 16-byte aligned.
+    const size_t nr = B.runs.size() * sizeof(CrcRun), ni = B.items.size() * sizeof(CrcItem);
+    const size_t nc = B.consts.size() * 4;
+    std::vector<uint8_t> pack(nr + ni + nc);
+    if (nr) memcpy(pack.data(), B.runs.data(), nr);
+    if (ni) memcpy(pack.data() + nr, B.items.data(), ni);
+    if (nc) memcpy(pack.data() + nr + ni, B.consts.data(), nc);
+    void* d_pack = nullptr;
+    int r = upload(D, pack.data(), pack.size(), &d_pack, s);
+    if (r) return r;
+    const uint8_t* dp = static_cast<const uint8_t*>(d_pack);
+    CrcWork w{};
+    w.runs = reinterpret_cast<const CrcRun*>(dp);
+    w.items = reinterpret_cast<const CrcItem*>(dp + nr);
+    w.consts = reinterpret_cast<const uint32_t*>(dp + nr + ni);
+    w.n_runs = (uint32_t)B.runs.size();
+    w.run_items = (uint32_t)B.run_items;
+    w.n_items = (uint32_t)B.items.size();
+    CrcLaunchCfg cfg{D->cus, D->crc_variant};
+    hipError_t e = timed(K_CRC, s, [&] { return launch_crc_items(w, D->d_tabs, sums_dev, cfg, s); });
+    scratch_free(D, d_pack, s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+inline int piece_sums_dev(Device* D, const krk_blob* blobs, uint64_t n, uint32_t* sums_dev, hipStream_t s) {
+    int r = validate_blobs(blobs, n);
+    if (r) return r;
+    uint64_t lo, hi;
+    sums_span(blobs, n, &lo, &hi);
+    if (hi == lo) return KRK_OK;
+    KRK_CHECK(sums_dev, KRK_EINVAL, "sums_dev is NULL");
+    KRK_HIP(hipMemsetAsync(sums_dev + lo, 0, (hi - lo) * 4, s));
+    ItemBuilder B;
+    CrcBatch items;
+    for (uint64_t i = 0; i < n; ++i)
+        B.add(items, reinterpret_cast<uint64_t>(blobs[i].data), 0, blobs[i].length, blobs[i].length,
+              (uint64_t)blobs[i].piece_length, blobs[i].sums_offset);
+    return run_items(D, items, sums_dev, s);
+}
+
+// ------------------------------------------------------------------ SHA jobs
+inline const uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+inline int run_jobs(Device* D, std::vector<ShaJob>& jobs, uint8_t* digests_dev, uint32_t* state_dev,
+                    hipStream_t s) {
+    if (jobs.empty()) return KRK_OK;
+    // Longest streams first: lanes of one wave then carry similar lengths.
+    std::stable_sort(jobs.begin(), jobs.end(), [](const ShaJob& a, const ShaJob& b) { return a.len > b.len; });
+    void* d_jobs = nullptr;
+    int r = upload(D, jobs.data(), jobs.size() * sizeof(ShaJob), &d_jobs, s);
+    if (r) return r;
+    hipError_t e = timed(K_SHA, s, [&] {
+        return launch_sha256(static_cast<const ShaJob*>(d_jobs), (uint32_t)jobs.size(), digests_dev,
+                             state_dev, s);
+    });
+    scratch_free(D, d_jobs, s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
+    ShaJob j{};
+    j.ptr = reinterpret_cast<uint64_t>(p);
+    j.len = len;
+    j.prefix = 0;
+    j.out = out;
+    j.flags = kShaFinal;
+    memcpy(j.h, kIV, sizeof kIV);
+    return j;
+}
+
+
+}  // namespace krk

@@ -2,13 +2,25 @@
 // core/digester.go:28-72 over crypto/sha256).
 //
 // SHA-256 is a sequential Merkle-Damgard chain per blob, so parallelism comes only
-// from independent blobs: one lane = one stream, 64 streams per wave, one wave per
-// workgroup so the waves spread over CUs/SIMDs.  Every lane loads its own next
-// 64-byte blocks two blocks ahead (the stream bandwidth is tiny, latency is what
-// needs hiding) and runs the 64 rounds fully unrolled in registers with
-// v_alignbit rotates; no LDS, no MFMA (integer/bitwise work).
+// from independent blobs.  Production kernel: sha256_ws_kernel, a wave-specialised
+// workgroup of producer/consumer wave pairs:
+//  * the producer wave loads each stream's 64-byte blocks two steps ahead, builds
+//    the padded tail blocks, expands the message schedule and writes
+//    KW[r] = W[r] + K[r] into an LDS ring;
+//  * the consumer wave runs only the rounds, reading KW from the ring with
+//    ds_read_b128, one s_barrier per producer step.
+// Streams per consumer wave: 32 with two lanes per stream (the A lane carries the
+// a..d history, the E lane e..h, a 9-instruction round; chosen while the batch
+// leaves SIMDs idle) or 64 with one lane (a 14-instruction round).  Jobs start from
+// the IV or a midstate (streaming Digester, windowed host paths) and either write
+// the digest (final, padding done here) or the midstate back.  No MFMA: the work is
+// 32-bit integer rotate/xor/add.
 #include <stdlib.h>
 
+#include <atomic>
+#include <mutex>
+
+#include "../../include/kraken_hip.h"
 #include "kernels.hpp"
 #include "device_util.hpp"
 
@@ -31,6 +43,7 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
 }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
+#ifdef KRK_DIAG  // one lane does loads + schedule + rounds: the round-1 baseline kernel
 // One compression of the 16 big-endian words w[] into state h[].
 __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) {
     constexpr uint32_t K[64] = {KRK_K256};
@@ -142,6 +155,8 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
         for (int k = 0; k < 8; ++k) o[k] = h[k];
     }
 }
+
+#endif  // KRK_DIAG
 
 // ---------------------------------------------------------------------------
 // Wave-specialised variant.  A workgroup = 2 waves over the same 64 streams:
@@ -787,19 +802,40 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     }
 }
 
-// KRK_SHA_VARIANT: 0 = one lane does loads + schedule + rounds; 1 = wave-specialised,
-// one lane per stream; 2 = its rounds-only timing diagnostic (wrong digests);
-// 3 = wave-specialised, two lanes per stream; 4 = its timing diagnostic;
-// 5/6 = producer-only timing diagnostics (one/two lanes); 7 = producer-only with
-// no global loads (two lanes).
-// 8/9 = 1/3 with two producer/consumer pairs per workgroup.
-// Default (-1): auto_variant (two lanes while the batch leaves SIMDs idle, else one).
-// Read at every launch (a getenv is cheap next to any SHA launch), so tests can
-// cover each variant in one process.
-static int sha_variant() {
-    const char* e = getenv("KRK_SHA_VARIANT");
-    return e ? atoi(e) : -1;
+// Launch plans.  Production (every plan bit-exact):
+//   KRK_SHA_PLAN_1LANE        one lane per stream, one producer/consumer pair per workgroup
+//   KRK_SHA_PLAN_2LANE        two lanes per stream, one pair per workgroup
+//   KRK_SHA_PLAN_1LANE_2PAIR  one lane, two pairs per 4-wave workgroup
+//   KRK_SHA_PLAN_2LANE_2PAIR  two lanes, two pairs per workgroup
+//   KRK_SHA_PLAN_AUTO         auto_plan() below
+// The plan is process-wide state set by krk_set_sha_plan (or KRK_SHA_PLAN read once,
+// at the first launch); it is not re-read per launch.  The timing diagnostics
+// (rounds-only consumer, producer-only, no-load producer: WRONG digests) and the
+// one-lane-does-everything kernel exist only in the diagnostic build (make diag,
+// -DKRK_DIAG), selected there with plan numbers 100 + the old variant number.
+static std::atomic<int> g_sha_plan{-1};
+
+static int sha_plan() {
+    int p = g_sha_plan.load(std::memory_order_relaxed);
+    if (p >= 0) return p;
+    const char* e = getenv("KRK_SHA_PLAN");
+    int want = e ? atoi(e) : KRK_SHA_PLAN_AUTO;
+    if (!sha_plan_valid(want)) want = KRK_SHA_PLAN_AUTO;
+    int expect = -1;
+    g_sha_plan.compare_exchange_strong(expect, want);
+    return g_sha_plan.load(std::memory_order_relaxed);
 }
+
+bool sha_plan_valid(int p) {
+    if (p >= KRK_SHA_PLAN_AUTO && p <= KRK_SHA_PLAN_2LANE_2PAIR) return true;
+#ifdef KRK_DIAG
+    return p >= 100 && p <= 107;
+#else
+    return false;
+#endif
+}
+
+void set_sha_plan(int p) { g_sha_plan.store(p, std::memory_order_relaxed); }
 
 // Streams up to which two lanes per stream win: two two-lane workgroups (64 KiB of
 // LDS each) per CU.  Measured (tools/probe_perf.py, profiles/r01/sha_compact_ring.jsonl):
@@ -817,60 +853,71 @@ static uint32_t device_cus() {
     }();
     return n;
 }
-static uint32_t two_lane_max_streams() {
-    static uint32_t n = [] {
-        const char* e = getenv("KRK_SHA_TWO_LANE_MAX");
-        return e ? (uint32_t)strtoul(e, nullptr, 10) : device_cus() * 64u;
-    }();
-    return n;
-}
+static uint32_t two_lane_max_streams() { return device_cus() * 64u; }
 
 // Automatic plan: two lanes, one pair per workgroup (a workgroup per CU) up to
 // 32 x CUs streams; two lanes, two pairs per workgroup up to 64 x CUs; one lane, two
 // pairs per workgroup beyond.
-static int auto_variant(uint32_t n_jobs) {
-    if (n_jobs <= device_cus() * 32u && n_jobs <= two_lane_max_streams()) return 3;
-    return n_jobs <= two_lane_max_streams() ? 9 : 8;
+static int auto_plan(uint32_t n_jobs) {
+    if (n_jobs <= device_cus() * 32u) return KRK_SHA_PLAN_2LANE;
+    return n_jobs <= two_lane_max_streams() ? KRK_SHA_PLAN_2LANE_2PAIR : KRK_SHA_PLAN_1LANE_2PAIR;
 }
 
-static bool variant_two_lanes(int v) { return v == 3 || v == 4 || v == 6 || v == 7 || v == 9; }
+static int resolve_plan(uint32_t n_jobs) {
+    const int p = sha_plan();
+    return p == KRK_SHA_PLAN_AUTO ? auto_plan(n_jobs) : p;
+}
 
-int sha_lanes_for(uint32_t n_jobs) {
-    int v = sha_variant();
-    if (v < 0) v = auto_variant(n_jobs);
-    return variant_two_lanes(v) ? 2 : 1;
+static bool plan_two_lanes(int p) {
+    return p == KRK_SHA_PLAN_2LANE || p == KRK_SHA_PLAN_2LANE_2PAIR || p == 103 || p == 104 || p == 106 ||
+           p == 107;
+}
+
+int sha_lanes_for(uint32_t n_jobs) { return plan_two_lanes(resolve_plan(n_jobs)) ? 2 : 1; }
+
+template <int kTiming, bool kTwo, int kGroups>
+static hipError_t launch_ws(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest, uint32_t* out_state,
+                            hipStream_t s) {
+    constexpr size_t lds = size_t(kGroups) * size_t(kTwo ? kRing2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB a pair
+    auto* k = &sha256_ws_kernel<kTiming, kTwo, kGroups>;
+    static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [k] {
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    });
+    if (attr_err != hipSuccess) return attr_err;
+    constexpr uint32_t per = (kTwo ? 32u : 64u) * kGroups;
+    hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * kGroups), lds, s, jobs, n_jobs, out_digest,
+                       out_state);
+    return hipGetLastError();
 }
 
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;
-    int v = sha_variant();
-    if (v < 0) v = auto_variant(n_jobs);
-    if (v >= 1 && v <= 9) {
-        // 1/3: production (one/two lanes); 2/4: consumer only; 5/6/7: producer only;
-        // 8/9: production, two producer/consumer pairs per workgroup (one/two lanes)
-        const bool two = variant_two_lanes(v);
-        const int groups = v >= 8 ? 2 : 1;
-        const size_t lds = size_t(groups) * size_t(two ? kRing2 + 1 : kSlots) * kSlotWords * 4;  // 64 KiB a pair
-        auto* k = v == 1 ? &sha256_ws_kernel<0, false>
-                : v == 2 ? &sha256_ws_kernel<1, false>
-                : v == 3 ? &sha256_ws_kernel<0, true>
-                : v == 4 ? &sha256_ws_kernel<1, true>
-                : v == 5 ? &sha256_ws_kernel<2, false>
-                : v == 6 ? &sha256_ws_kernel<2, true>
-                : v == 7 ? &sha256_ws_kernel<3, true>
-                : v == 8 ? &sha256_ws_kernel<0, false, 2>
-                         : &sha256_ws_kernel<0, true, 2>;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        const uint32_t per = (two ? 32u : 64u) * groups;
-        hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * groups), lds, s, jobs, n_jobs, out_digest,
-                           out_state);
-    } else {
-        hipLaunchKernelGGL(sha256_multi_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, s, jobs, n_jobs, out_digest,
-                           out_state);
+    switch (resolve_plan(n_jobs)) {
+        case KRK_SHA_PLAN_1LANE: return launch_ws<0, false, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case KRK_SHA_PLAN_2LANE: return launch_ws<0, true, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case KRK_SHA_PLAN_1LANE_2PAIR: return launch_ws<0, false, 2>(jobs, n_jobs, out_digest, out_state, s);
+        case KRK_SHA_PLAN_2LANE_2PAIR: return launch_ws<0, true, 2>(jobs, n_jobs, out_digest, out_state, s);
+#ifdef KRK_DIAG
+        // diagnostics (WRONG digests except 100): rounds-only consumer (102 one lane, 104 two
+        // lanes), producer-only (105 / 106), producer without global loads (107)
+        case 100:
+            hipLaunchKernelGGL(sha256_multi_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, s, jobs, n_jobs,
+                               out_digest, out_state);
+            return hipGetLastError();
+        case 101: return launch_ws<0, false, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 102: return launch_ws<1, false, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 103: return launch_ws<0, true, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 104: return launch_ws<1, true, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 105: return launch_ws<2, false, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 106: return launch_ws<2, true, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 107: return launch_ws<3, true, 1>(jobs, n_jobs, out_digest, out_state, s);
+#endif
+        default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 }  // namespace krk

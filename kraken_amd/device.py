@@ -202,9 +202,25 @@ def metainfo_digest(arena: BlobArena, out: BatchOutputs, stream=None):
                                       out.digests.ptr, stream))
 
 
-def metainfo_digest_host(datas, piece_lengths):
+def set_devices(devs):
+    """The process's device set (krk_set_devices): where the *_multi calls run and new
+    Digesters / piece streams are placed; repeats allowed; [] = the calling thread's device."""
+    arr = (C.c_int * max(len(devs), 1))(*devs)
+    check(lib.krk_set_devices(arr, len(devs)))
+
+
+def get_devices():
+    n = C.c_uint32()
+    check(lib.krk_get_devices(None, 0, C.byref(n)))
+    arr = (C.c_int * max(n.value, 1))()
+    check(lib.krk_get_devices(arr, n.value, C.byref(n)))
+    return list(arr[:n.value])
+
+
+def metainfo_digest_host(datas, piece_lengths, multi: bool = False):
     """End-to-end batch over HOST buffers (numpy uint8 arrays, pageable or
-    pinned): one PCIe pass feeds both kernels.  Returns (sums per blob, digests)."""
+    pinned): one PCIe pass feeds both kernels.  Returns (sums per blob, digests).
+    multi: krk_metainfo_digest_host_multi (LPT over the device set)."""
     n = len(datas)
     pls = np.broadcast_to(np.asarray(piece_lengths, dtype=np.int64), (n,))
     counts = [int(lib.krk_num_pieces(int(d.size), int(p))) for d, p in zip(datas, pls)]
@@ -215,8 +231,8 @@ def metainfo_digest_host(datas, piece_lengths):
         arr[i] = krk_blob(d.ctypes.data if d.size else None, int(d.size), int(pls[i]), int(offs[i]))
     sums = np.zeros(max(int(offs[-1]), 1), dtype=np.uint32)
     dg = np.zeros((max(n, 1), 32), dtype=np.uint8)
-    check(lib.krk_metainfo_digest_host(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                       dg.ctypes.data_as(C.POINTER(C.c_uint8))))
+    fn = lib.krk_metainfo_digest_host_multi if multi else lib.krk_metainfo_digest_host
+    check(fn(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)), dg.ctypes.data_as(C.POINTER(C.c_uint8))))
     return [sums[int(offs[i]):int(offs[i + 1])] for i in range(n)], dg[:n]
 
 

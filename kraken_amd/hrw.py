@@ -61,6 +61,12 @@ def _ordered(keys, nodes, n_out: int, want_scores: bool = False):
     return order[:, :n_out], scores
 
 
+def _check_n(n: int) -> None:
+    # The reference slices nodes[:n] (rendezvous.go:216), which panics for n < 0.
+    if n < 0:
+        raise ValueError(f"slice bounds out of range [:{n}]")
+
+
 class RendezvousHash:
     """lib/hrw/rendezvous.go:55-60.  Hash is always murmur3 (ring.go:150); the
     reference's other HashFactory/ScoreFunc choices are test-only."""
@@ -84,6 +90,7 @@ class RendezvousHash:
         return None, -1
 
     def GetOrderedNodes(self, key: str, n: int) -> list[RendezvousHashNode]:
+        _check_n(n)
         if not self.Nodes:
             return []
         m = min(n, len(self.Nodes))
@@ -92,6 +99,7 @@ class RendezvousHash:
 
     def GetOrderedNodesBatch(self, keys, n: int) -> np.ndarray:
         """Batched GetOrderedNodes: int32 [len(keys), min(n, N)] node indices."""
+        _check_n(n)
         m = min(n, len(self.Nodes))
         order, _ = _ordered(list(keys), self.Nodes, m)
         return order

@@ -160,3 +160,78 @@ def test_info_hash_batch_matches_single(orc):
     for i in range(n):
         s = sums[off[i]:off[i] + ns[i]]
         assert bytes(got[i]) == orc.info_hash(int(pls[i]), s, names[i], int(lens[i])), i
+
+
+def test_production_library_has_no_diagnostic_kernels():
+    """The timing diagnostics (wrong results by design) and the measured-but-unused
+    layouts are compiled only into the KRK_DIAG build (make diag): the production .so
+    carries exactly the production kernel instantiations."""
+    out = subprocess.run(["nm", "-C", _capi.LIB_PATH], capture_output=True, text=True).stdout
+    kern = sorted({l.split(" ", 2)[2] for l in out.splitlines() if "__device_stub__" in l})
+    sha = [k for k in kern if "sha256" in k]
+    crc = [k for k in kern if "crc_items_kernel" in k]
+    assert sha and crc
+    assert all("sha256_ws_kernel<0," in k for k in sha), sha  # kTiming = 0 only
+    assert not any("sha256_multi_kernel" in k for k in kern)
+    # crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>: strided, no load-only, no NT
+    assert all(k.split("<")[1].startswith(("32, 4, 1024, false, false, 32, false",
+                                           "16, 4, 1024, false, false, 16, false")) for k in crc), crc
+    assert b"KRK_SHA_VARIANT" not in open(_capi.LIB_PATH, "rb").read()
+
+
+def test_host_crossover_primitives_match_hashlib_zlib():
+    import hashlib
+    import zlib
+    rng = np.random.default_rng(11)
+    for n in list(range(0, 200)) + [255, 256, 1023, 4096, 65535, 65536, (1 << 20) + 5]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        o = (C.c_uint8 * 32)()
+        check(lib.krk_host_sha256(d, n, o))
+        assert bytes(o) == hashlib.sha256(d).digest(), n
+        seed = int(rng.integers(0, 2 ** 32))
+        c = C.c_uint32()
+        check(lib.krk_host_crc32_update(seed, d, n, C.byref(c)))
+        assert c.value == zlib.crc32(d, seed), n
+
+
+_HOST_SCRIPT = """
+import sys, ctypes as C, numpy as np
+sys.path.insert(0, sys.argv[1])
+from kraken_amd._capi import lib
+rng = np.random.default_rng(5)
+out = []
+for n in [0, 1, 63, 64, 65, 127, 128, 1000, 4096, 100000]:
+    d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    o = (C.c_uint8 * 32)(); c = C.c_uint32()
+    lib.krk_host_sha256(d, n, o); lib.krk_host_crc32_update(7, d, n, C.byref(c))
+    out.append(bytes(o).hex() + "%08x" % c.value)
+print(" ".join(out))
+"""
+
+
+def test_host_crossover_ni_matches_portable(tmp_path):
+    """SHA-NI / PCLMULQDQ routines (when this CPU has them) equal the portable ones."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "h.py"
+    f.write_text(_HOST_SCRIPT)
+    runs = [subprocess.run([sys.executable, str(f), root], capture_output=True, text=True,
+                           env={**os.environ, "KRK_HOST_PORTABLE": v}) for v in ("0", "1")]
+    assert all(r.returncode == 0 for r in runs), [r.stderr for r in runs]
+    assert runs[0].stdout == runs[1].stdout and len(runs[0].stdout.split()) == 10
+
+
+def test_streaming_constructors_need_a_device():
+    """Even the host placement of a Digester needs the gfx950 device the library
+    serves: without one every constructor is KRK_ENODEV (no CPU fallback)."""
+    n = C.c_int(-1)
+    check(lib.krk_device_count(C.byref(n)))
+    if n.value > 0:
+        pytest.skip("a GPU is visible")
+    h = C.c_void_p()
+    for p in (_capi.KRK_PLACE_AUTO, _capi.KRK_PLACE_HOST, _capi.KRK_PLACE_GPU):
+        assert lib.krk_digester_new_on(p, C.byref(h)) == KRK_ENODEV
+    assert lib.krk_digester_new_on(7, C.byref(h)) == _capi.KRK_EINVAL
+    blob = (_capi.krk_blob * 1)(_capi.krk_blob(None, 0, 4, 0))
+    assert lib.krk_metainfo_digest_host_multi(blob, 1, None, (C.c_uint8 * 32)()) == KRK_ENODEV

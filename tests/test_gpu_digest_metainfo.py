@@ -308,12 +308,23 @@ def test_regenerate_all_cas_sidecars(gpu, orc, tmp_path):
         assert got == _go_json(65536, ref, d.Hex(), len(b))
 
 
-@pytest.mark.parametrize("variant", ["1", "3", "8", "9"])
-def test_sha_launch_plans_bit_exact(gpu, orc, variant, monkeypatch):
-    """Every production SHA-256 plan (one / two lanes per stream; one / two
-    producer-consumer pairs per workgroup) on a batch of mixed lengths and
+@pytest.fixture
+def sha_plan():
+    """Sets a process-wide SHA-256 launch plan (krk_set_sha_plan), restores AUTO after."""
+    from kraken_amd._capi import lib as L
+
+    def set_plan(p):
+        check(L.krk_set_sha_plan(p))
+    yield set_plan
+    check(L.krk_set_sha_plan(0))
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+def test_sha_launch_plans_bit_exact(gpu, orc, variant, sha_plan):
+    """Every production SHA-256 plan (KRK_SHA_PLAN_*: one / two lanes per stream; one /
+    two producer-consumer pairs per workgroup) on a batch of mixed lengths and
     alignments, one-shot and from midstates (chunked), against hashlib."""
-    monkeypatch.setenv("KRK_SHA_VARIANT", variant)
+    sha_plan(variant)
     rng = np.random.default_rng(int(variant))
     lens = [int(x) for x in rng.integers(0, 300_000, 300)] + [0, 1, 55, 56, 63, 64, 65, 119, 120, 128]
     arena = D.BlobArena(lens, 1 << 16, blob_ids=range(900, 900 + len(lens)), misalign=int(variant) % 3)

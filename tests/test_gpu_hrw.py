@@ -183,3 +183,36 @@ def test_ring_locations_u8_dev_rejects_256_nodes(gpu):
     dbuf, lb, cb = D.DeviceBuffer(32), D.DeviceBuffer(3), D.DeviceBuffer(1)
     with pytest.raises(Exception, match="255"):
         D.ring_locations_u8_dev(dbuf, 1, labels, np.ones(256, np.uint8), 3, lb, cb)
+
+
+def _u64_to_f64_dev(vals, rehash):
+    import ctypes as C
+    from kraken_amd._capi import check, lib
+    be = np.array(vals, dtype=">u8").view(np.uint8)
+    out = np.zeros(len(vals), dtype=np.float64)
+    check(lib.krk_hrw_uint64_to_float64(be.ctypes.data_as(C.POINTER(C.c_uint8)), len(vals), int(rehash),
+                                        out.ctypes.data_as(C.POINTER(C.c_double))))
+    return out
+
+
+def test_uint64_to_float64_rehash_branch_on_device(gpu, orc):
+    """lib/hrw/rendezvous_test.go:59-98 (TestScoreFunctionUint64ToFloat64BadValues): the
+    12 Sum values 2^53 .. 2^64 (the last wraps to 0 in Go's int) have all-zero low 53
+    bits.  With a nil hasher the score is 0.0; with murmur3 it is re-hashed once and is
+    non-zero with a finite log -- through the scoring kernel's own device function, bit
+    for bit against the oracle.  Random Sums (no rehash) must match too."""
+    vals = [((1 << 53) << i) & ((1 << 64) - 1) for i in range(12)]
+    assert all(v & ((1 << 53) - 1) == 0 for v in vals)
+    nil = _u64_to_f64_dev(vals, False)
+    assert (nil == 0.0).all()
+    got = _u64_to_f64_dev(vals, True)
+    for v, g in zip(vals, got):
+        want = orc.uint64_to_float64(v, True)
+        assert g.tobytes() == np.float64(want).tobytes(), hex(v)
+        assert g != 0.0 and np.isfinite(np.log(g))
+        assert np.isfinite(orc.go_log(float(g)))
+    rng = np.random.default_rng(53)
+    rnd = [int(x) for x in rng.integers(0, 2 ** 63, 4096, dtype=np.int64)] + [0, (1 << 64) - 1, (1 << 53) - 1]
+    got = _u64_to_f64_dev(rnd, True)
+    for v, g in zip(rnd, got):
+        assert g.tobytes() == np.float64(orc.uint64_to_float64(v, True)).tobytes(), hex(v)

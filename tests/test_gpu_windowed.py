@@ -1,0 +1,74 @@
+"""Config C3's windowed path (kraken_amd.windowed, the machinery bench.py's C3 line
+runs): blobs larger in total than HBM advance chunk by chunk through two device
+windows -- SHA-256 from per-blob midstates, piece CRCs XOR-accumulated by byte range
+(krk_metainfo_digest_chunks_dev) -- with the next window generated on its own stream
+and blobs admitted longest first under the live cap.  A scaled C3: 1,500 blobs drawn
+from the C3 length law with every length divided by 16 (6.5-67 MB,
+byte-granular, so nearly every blob ends in a partial piece), 4 MiB pieces.  Every
+blob is checked against the one-shot device path, sampled blobs against hashlib /
+the oracle."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from kraken_amd import device as D
+from kraken_amd.windowed import WindowedRun, c3_lengths, window_plan
+
+pytestmark = pytest.mark.gpu
+
+N, SCALE, P = 1500, 16, 4 << 20
+
+
+@pytest.fixture(scope="module")
+def one_shot(gpu):
+    lens = c3_lengths(N, scale=SCALE)
+    ids = [(2 << 40) + i for i in range(N)]
+    arena = D.BlobArena(lens, P, blob_ids=ids)
+    out = D.BatchOutputs(arena)
+    D.metainfo_digest(arena, out)
+    D.synchronize()
+    dg = out.digests.to_host(np.uint8, 32 * N).reshape(-1, 32)
+    sums = out.sums.to_host(np.uint32, arena.total_pieces)
+    offs, counts = arena.sums_off.copy(), arena.n_pieces.copy()
+    del arena, out
+    return lens, ids, dg, sums, offs, counts
+
+
+@pytest.mark.parametrize("window_gib,cap", [(4, None), (1, 200)])
+def test_windowed_c3_matches_one_shot_and_oracle(one_shot, orc, window_gib, cap):
+    lens, ids, dg1, sums1, offs1, counts1 = one_shot
+    wr = WindowedRun(D, ids, lens, P, window_gib << 30, cap=cap)
+    if cap is None:
+        assert wr.cap >= N  # production admission: the two-lane cap exceeds this batch
+    else:
+        live = max(len(w[0]) for w in wr.wins)
+        assert live <= cap < N and len(wr.wins) > 50
+    wr.run()
+    cb = wr.cb
+    dg = cb.digests.to_host(np.uint8, 32 * N).reshape(-1, 32)
+    sums = cb.sums.to_host(np.uint32, cb.total_pieces)
+    wr.close()
+    assert np.array_equal(dg, dg1)
+    for i in range(N):
+        a, b = int(cb.sums_off[i]), int(offs1[i])
+        assert np.array_equal(sums[a:a + int(counts1[i])], sums1[b:b + int(counts1[i])]), i
+    L = np.asarray(lens)
+    partial = int(np.flatnonzero(L % P)[0])
+    for i in sorted({int(L.argmin()), int(L.argmax()), partial, 7, 777}):
+        data = orc.synth(ids[i], lens[i])
+        assert bytes(dg[i]) == hashlib.sha256(data.tobytes()).digest(), i
+        a = int(cb.sums_off[i])
+        assert np.array_equal(sums[a:a + int(counts1[i])], orc.calc_piece_sums(data, P)[1]), i
+
+
+def test_window_plan_covers_c3_law_once():
+    """The plan itself at the production scale of one rank's C3 shard (host only)."""
+    lens = c3_lengths(2500)
+    wins = window_plan(lens, 48 << 30, 8192)
+    pos = np.zeros(len(lens), dtype=np.uint64)
+    for blobs, offs, take in wins:
+        assert np.array_equal(pos[blobs], offs)
+        assert ((take % 64 == 0) | (offs + take == np.asarray(lens, dtype=np.uint64)[blobs])).all()
+        pos[blobs] += take
+    assert np.array_equal(pos, np.asarray(lens, dtype=np.uint64))

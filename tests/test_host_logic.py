@@ -4,7 +4,7 @@ import os
 import numpy as np
 import pytest
 
-from kraken_amd import core, metainfogen
+from kraken_amd import core, hrw, metainfogen
 
 
 def test_digest_parse_and_validate():
@@ -154,8 +154,8 @@ def test_generate_error_wrapping(tmp_path):
 
 
 def _plan_checks(lens, W, cap):
-    import bench
-    wins = bench.c3_window_plan(lens, W, cap)
+    from kraken_amd.windowed import window_plan
+    wins = window_plan(lens, W, cap)
     L = np.asarray(lens, dtype=np.uint64)
     covered = np.zeros(len(lens), dtype=np.uint64)
     started = {}
@@ -174,7 +174,7 @@ def _plan_checks(lens, W, cap):
 
 
 def test_c3_window_plan_admits_longest_first_under_cap():
-    """bench.c3_window_plan: bytes covered exactly once, <= cap live blobs a window,
+    """kraken_amd.windowed.window_plan: bytes covered exactly once, <= cap live blobs a window,
     and a blob never starts after a shorter one."""
     rng = np.random.default_rng(7)
     lens = [int(x) for x in rng.integers(1, 5000, size=300)] + [0 + 64, 12_345, 64 * 1000]
@@ -192,3 +192,67 @@ def test_c3_window_plan_no_cap_and_single_blob():
     assert all(v == 0 for v in started.values())  # all live from window 0
     wins, _ = _plan_checks([10**6], 1 << 16, 16384)
     assert len(wins) == -(-10**6 // (1 << 16))
+
+
+def test_validate_sha256_go_errors():
+    """core/digest.go:152-161 via hex.DecodeString: a trailing newline is an invalid
+    byte (the length counts bytes, as Go's len does)."""
+    good = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+    core.ValidateSHA256(good)
+    core.ValidateSHA256(good.upper())
+    with pytest.raises(ValueError, match=r"^hex: encoding/hex: invalid byte: U\+000A$"):
+        core.ValidateSHA256(good[:63] + "\n")
+    with pytest.raises(ValueError, match=r"^hex: encoding/hex: invalid byte: U\+0067 'g'$"):
+        core.ValidateSHA256("g" + good[1:])
+    with pytest.raises(ValueError, match=r'^expected 64 characters, got 2 from "ab"$'):
+        core.ValidateSHA256("ab")
+    with pytest.raises(ValueError, match=r"^invalid sha256: expected 64 characters"):
+        core.NewSHA256DigestFromHex(good + "\n")
+
+
+def test_deserialize_partial_sidecar_zero_values():
+    """json.Unmarshal fills absent fields (and a null Info) with zero values, so a
+    truncated or partial _torrentmeta fails on the name, like the reference."""
+    for raw in (b'{"Info":null}', b'{}', b'{"Info":{"PieceLength":4}}', b'null',
+                b'{"Info":{"PieceSums":[1,2],"Length":3}}'):
+        with pytest.raises(ValueError, match=r'^parse name: invalid sha256: expected 64 characters, got 0 from ""$'):
+            core.DeserializeMetaInfo(raw)
+    with pytest.raises(ValueError, match=r"^json: "):
+        core.DeserializeMetaInfo(b'{"Info":{"PieceLength":"x"}}')
+    with pytest.raises(ValueError, match=r"^json: "):
+        core.DeserializeMetaInfo(b'[1]')
+
+
+def test_get_ordered_nodes_negative_n():
+    """GetOrderedNodes(key, n < 0): the reference panics on nodes[:n]; never reaches the device."""
+    rh = hrw.NewRendezvousHash()
+    rh.AddNode("a", 100)
+    with pytest.raises(ValueError):
+        rh.GetOrderedNodes("00ff", -1)
+    with pytest.raises(ValueError):
+        rh.GetOrderedNodesBatch(["00ff"], -3)
+
+
+def test_cas_volume_symlink_refuses_non_links(tmp_path):
+    """createOrUpdateSymlink (lib/store/utils.go:25-47): a regular file or a real
+    directory at <dir>/<subdir> is an error and stays in place (initCASVolumes wraps
+    it as "symlink to volume: ...")."""
+    from kraken_amd import castore
+    vol = tmp_path / "vol"
+    vol.mkdir()
+    d = tmp_path / "cas"
+    d.mkdir()
+    (d / "00").write_bytes(b"user data")
+    with pytest.raises(OSError):
+        castore._create_or_update_symlink(str(vol / "cas" / "00"), str(d / "00"))
+    assert (d / "00").read_bytes() == b"user data"
+    (d / "01").mkdir()
+    with pytest.raises(OSError):
+        castore._create_or_update_symlink(str(vol / "x"), str(d / "01"))
+    assert (d / "01").is_dir() and not (d / "01").is_symlink()
+    # existing link to another place is replaced; a missing target is created
+    os.symlink(str(vol), str(d / "02"))
+    castore._create_or_update_symlink(str(vol / "cas" / "02"), str(d / "02"))
+    assert os.readlink(str(d / "02")) == str(vol / "cas" / "02")
+    castore._create_or_update_symlink(str(vol / "cas" / "03"), str(d / "03"))
+    assert os.readlink(str(d / "03")) == str(vol / "cas" / "03")
