@@ -45,34 +45,43 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 GAMMA = 0x9E3779B97F4A7C15
 M64 = (1 << 64) - 1
 
-# Per-stream SHA-256 issue ceiling (Kernels): the consumer wave alone,
-# running its blocks' rounds with no producer and no barrier (the diagnostic
-# kernel variants: 2 for one lane per stream, 4 for two), measured live on this
-# box by sha_issue_ceiling() -- the rounds' own issue time.  The SHA kernel's
-# fraction of it is roofline.issue_bound.frac.
-SHA_DIAG_VARIANT = {1: "2", 2: "4"}
+# Per-stream SHA-256 issue ceiling, from the ISA and the clock:
+# the VALU instructions per block of the production consumer loop, counted in the
+# disassembly of the loaded library's gfx950 code object (tools/sha_isa.py), each
+# costing >= 4 cycles for a wave alone on its SIMD (MI355X_MICROARCH.md 'vector-
+# instruction ISSUE cost'), at the shader clock measured by a probe kernel that
+# runs beside a SHA-256 launch (krk_device_clock_mhz).
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def sha_issue_ceiling(D, lanes, streams=64, mb=8):
-    """Per-stream MB/s of the rounds-only diagnostic kernel for the given plan."""
-    old = os.environ.get("KRK_SHA_VARIANT")
-    os.environ["KRK_SHA_VARIANT"] = SHA_DIAG_VARIANT[lanes]
+def sha_isa_ceiling(D, launch):
+    """(isa counts, clock MHz, per-stream ceiling MB/s); launch() starts one SHA-256
+    batch asynchronously, the clock is read while it runs."""
+    import ctypes as C
+    import sha_isa
     try:
-        arena = D.BlobArena([mb << 20] * streams, 1 << 20)
-        out = D.BatchOutputs(arena)
-        D.sha256(arena, out)  # warm
-        D.synchronize()
-        with D.KernelTimer():
-            D.sha256(arena, out)
-            D.synchronize()
-            _, ms = D.KernelTimer.stats("sha256_multi")
-        del arena, out
-        return (mb << 20) / (ms / 1e3) / 1e6
-    finally:
-        if old is None:
-            os.environ.pop("KRK_SHA_VARIANT", None)
-        else:
-            os.environ["KRK_SHA_VARIANT"] = old
+        isa = sha_isa.count(D.lib._name)
+    except Exception as e:  # tools missing on the box: report, never guess
+        return {"error": f"{type(e).__name__}: {e}"}, None, None
+    s = C.c_void_p()
+    D.check(D.lib.krk_stream_create(C.byref(s)))
+    mhz = C.c_double()
+    launch()
+    time.sleep(0.3)  # inside the launch (C2: ~2 s)
+    D.check(D.lib.krk_device_clock_mhz(s, C.byref(mhz)))
+    D.synchronize()
+    D.lib.krk_stream_destroy(s)
+    return isa, mhz.value, sha_isa.ceiling_mbps(isa, mhz.value)
+
+
+def load_valu(workload):
+    """VALU / LDS utilisation per kernel from the committed rocprofv3 PMC passes
+    (tools/pmc_valu.py -> profiles/r02/valu_<workload>.json)."""
+    path = os.path.join(ROOT, "profiles", "r02", f"valu_{workload}.json")
+    try:
+        return json.load(open(path)), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        return {}, None
 
 
 WORKLOADS = {
@@ -226,6 +235,39 @@ def roofline_obj(kernel, gbps, avg_ms, bytes_launch, traffic):
             "algorithmic_bytes_per_launch": bytes_launch}
 
 
+def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
+    """sha256_multi is bound by per-stream VALU issue, not HBM: one sequential
+    Merkle-Damgard chain per blob.  peak = streams x the ISA per-stream ceiling; the
+    HBM fraction is kept beside it."""
+    lanes = D.sha_lanes_per_stream(n)
+    per_stream = max(lens) / (avg_ms / 1e3) / 1e6
+    roof = {"kernel": "sha256_multi", "bound": "valu_issue_per_stream", "achieved": round(gbps, 2),
+            "peak": None, "unit": "GB/s", "frac": None, "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5)}}
+    ib = {"achieved_per_stream_MBps": round(per_stream, 2), "streams": n, "lanes_per_stream": lanes}
+    if lanes == 2 and not a.no_ceiling:
+        isa, mhz, ceil = sha_isa_ceiling(D, launch)
+        if ceil:
+            ib.update({"ceiling_per_stream_MBps": round(ceil, 2), "frac": round(per_stream / ceil, 4),
+                       "clock_mhz": round(mhz, 1), "valu_per_block": isa["valu_per_block"],
+                       "round_valu_per_block": isa["round_valu_per_block"],
+                       "lds_per_block": isa["lds_per_block"], "salu_per_block": isa["salu_per_block"],
+                       "ceiling_source": ("ISA: VALU instructions per 64-byte block in the production consumer "
+                                          "loop (llvm-objdump of the loaded code object, tools/sha_isa.py) x 4 "
+                                          "cycles per VALU for a lone wave (MI355X_MICROARCH.md:489) at the "
+                                          "shader clock measured beside a SHA launch (krk_device_clock_mhz)")})
+            peak = n * ceil / 1e3
+            roof.update({"peak": round(peak, 2), "frac": round(gbps / peak, 4)})
+        else:
+            ib["ceiling_error"] = isa.get("error")
+    roof["issue_bound"] = ib
+    roof["note"] = ("SHA-256 is one sequential Merkle-Damgard chain per blob (two lanes each here): the kernel is "
+                    "bound by the per-stream VALU issue of its consumer waves (32 of the chip's 1,024 SIMDs for "
+                    "1,000 streams), not by HBM; peak = streams x ISA per-stream ceiling, hbm.frac beside it")
+    return roof
+
+
 def load_traffic(path, workload, n):
     """Per-launch HBM bytes from the PMC passes: profiles/pmc_traffic.json (C2) or
     profiles/pmc_traffic_<workload>.json (tools/pmc_traffic.py)."""
@@ -255,6 +297,11 @@ def run_metainfo(a, D, T, rank, world, res):
         pin_s.fill_from(out.sums)
         pin_d.fill_from(out.digests)
 
+    if a.e2e_only:  # profiler passes of the host path: no device-resident launch in the trace
+        res.update({"metric": METRIC + " (end-to-end leg only)", "unit": "GB/s", "steps": 1,
+                    "end_to_end": end_to_end(D, T, arena, n, min(a.e2e_mb << 20, lens[0]), P, None, world)})
+        res["value"] = res["end_to_end"]["value"]
+        return
     for _ in range(a.warmup):
         step()
     T.barrier()
@@ -276,19 +323,15 @@ def run_metainfo(a, D, T, rank, world, res):
     dominant = "sha256_multi" if sha_avg >= crc_avg else "crc32_pieces"
     roof = roofline_obj(dominant, sha_gbps if dominant == "sha256_multi" else crc_gbps,
                         sha_avg if dominant == "sha256_multi" else crc_avg, bytes_rank, traffic.get(dominant))
+    roof_crc = roofline_obj("crc32_pieces", crc_gbps, crc_avg, bytes_rank, traffic.get("crc32_pieces"))
+    valu, valu_src = load_valu(a.workload)
+    if valu_src and valu.get("device_resident", {}).get("crc32_pieces"):
+        roof_crc["valu"] = dict(valu["device_resident"]["crc32_pieces"], source=valu_src)
     if dominant == "sha256_multi":
-        per_stream = max(lens) / (sha_avg / 1e3) / 1e6
-        lanes = D.sha_lanes_per_stream(n)
-        ceil = None if a.no_ceiling else sha_issue_ceiling(D, lanes)
-        roof["note"] = ("SHA-256 is one sequential Merkle-Damgard chain per blob (one or two lanes each): this "
-                        "kernel is bound by per-stream VALU issue, not HBM; issue_bound compares the longest "
-                        "stream's rate with the per-stream issue ceiling of the same plan (DESIGN.md)")
-        roof["issue_bound"] = {"achieved_per_stream_MBps": round(per_stream, 2),
-                               "ceiling_per_stream_MBps": round(ceil, 2) if ceil else None,
-                               "frac": round(per_stream / ceil, 4) if ceil else None, "streams": n,
-                               "lanes_per_stream": lanes,
-                               "ceiling_source": f"rounds-only diagnostic kernel (variant {SHA_DIAG_VARIANT[lanes]}: "
-                                                 "no producer, no barrier), measured in this run"}
+        roof = sha_roofline(a, D, n, lens, sha_gbps, sha_avg, bytes_rank, traffic.get("sha256_multi"),
+                            lambda: D.metainfo_digest(arena, out))
+    if valu_src and valu.get("device_resident", {}).get(dominant):
+        roof["valu"] = dict(valu["device_resident"][dominant], source=valu_src)
     res.update({"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "steps": a.steps,
                 "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
                 "scaling": "weak", "dtype": "u8",
@@ -297,12 +340,14 @@ def run_metainfo(a, D, T, rank, world, res):
                            "bytes_per_gpu": bytes_rank, "piece_length": P, "mode": "device-resident",
                            "parallelism": f"blob-sharded x{world}, no collective"},
                 "roofline": roof,
-                "roofline_crc": roofline_obj("crc32_pieces", crc_gbps, crc_avg, bytes_rank,
-                                             traffic.get("crc32_pieces")),
+                "roofline_crc": roof_crc,
                 "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)},
                             "sha256_multi": {"launches": sha_n, "avg_ms": round(sha_avg, 3)}}})
     if a.workload == "c2" and not a.no_e2e:
         res["end_to_end"] = end_to_end(D, T, arena, n, min(a.e2e_mb << 20, lens[0]), P, out, world)
+        ev = valu.get("end_to_end") if valu_src else None
+        if ev:
+            res["end_to_end"]["valu"] = dict(ev, source=valu_src)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         m = min(n, 2 * host_cores())  # bounded sample: the first blobs of this workload
         cb, dg, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds)
@@ -461,18 +506,26 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
     datas = [np.empty(Le, dtype=np.uint8) for _ in range(n)]
     for i, d in enumerate(datas):  # the device blobs' prefixes (device-generated content)
         D.check(D.lib.krk_memcpy_d2h(d.ctypes.data_as(C.c_void_p), arena.buf.ptr + int(arena.offsets[i]), Le))
-    D.metainfo_digest_host(datas[:2], P)  # warm the staging windows
+    D.metainfo_digest_host([d[:1 << 20] for d in datas[:2]], P)  # warm the staging windows (short chains)
     T.barrier()
     t0 = time.perf_counter()
     sums, dg = D.metainfo_digest_host(datas, P)
     el = T.max_over_ranks(time.perf_counter() - t0)
-    dev_sums = out.sums.to_host(np.uint32, arena.total_pieces)
     k = Le // P
-    ok = all(np.array_equal(sums[i][:k], dev_sums[int(arena.sums_off[i]):int(arena.sums_off[i]) + k])
-             for i in range(n)) if k else None
-    return {"value": round(world * n * Le / el / 1e9, 3), "unit": "GB/s", "blobs_per_gpu": n, "blob_bytes": Le,
-            "seconds": round(el, 3), "source": "pageable host memory (numpy), copied into pinned windows",
-            "bound": "PCIe H2D / host staging copy / SHA per-stream rate", "sums_match_device_run": ok}
+    ok = None
+    if out is not None and k:
+        dev_sums = out.sums.to_host(np.uint32, arena.total_pieces)
+        ok = all(np.array_equal(sums[i][:k], dev_sums[int(arena.sums_off[i]):int(arena.sums_off[i]) + k])
+                 for i in range(n))
+    res = {"value": round(world * n * Le / el / 1e9, 3), "unit": "GB/s", "blobs_per_gpu": n, "blob_bytes": Le,
+           "seconds": round(el, 3), "source": "pageable host memory (numpy), copied into pinned windows",
+           "bound": "PCIe H2D (one pass per byte) and the per-blob SHA-256 chain (blob_bytes / per-stream rate)",
+           "sums_match_device_run": ok}
+    if out is not None and Le == int(arena.lengths[0]) and (arena.lengths == Le).all():  # whole blobs
+        dev_dg = out.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
+        res["digests_match_device_run"] = bool(np.array_equal(dg, dev_dg))
+    del datas
+    return res
 
 
 def run_pieces(a, D, T, rank, world, res):
@@ -717,7 +770,9 @@ def main():
                     help="skip the live SHA issue-ceiling run (profiler passes: keeps its launches out of the trace)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers, PCIe) leg")
     ap.add_argument("--no-sweep", action="store_true", help="C5: skip the N x MaxReplica x healthy grid")
-    ap.add_argument("--e2e-mb", type=int, default=16, help="bytes per blob for the end-to-end leg (MiB)")
+    ap.add_argument("--e2e-mb", type=int, default=100, help="bytes per blob for the end-to-end leg (MiB; C2: 100)")
+    ap.add_argument("--e2e-only", action="store_true",
+                    help="C2: only the end-to-end leg (profiler passes of the host path)")
     a = ap.parse_args()
     if a.steps is None:
         a.steps = WORKLOADS[a.workload].get("steps", 3)

@@ -353,6 +353,11 @@ int krk_stream_sync(void* s);
  * for kernel name "crc32_pieces", "sha256_multi", "hrw_shard_table",
  * "hrw_gather" or "synth_fill" (timed launches are synchronised lazily). */
 int krk_set_timing(int on);
+/* Shader clock of the calling thread's device, measured by a one-wave probe kernel on
+ * `stream` (NULL = the library's stream): s_memtime cycles over s_memrealtime (100 MHz)
+ * ticks of a ~2 ms spin.  Launched while another kernel runs it reads the clock the chip
+ * holds under that load (bench.py prices the SHA-256 issue ceiling with it). */
+int krk_device_clock_mhz(void* stream, double* mhz);
 int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms);
 int krk_reset_kernel_stats(void);
 

@@ -92,6 +92,7 @@ def _load() -> C.CDLL:
         "krk_host_crc32_update": (i, [C.c_uint32, vp, C.c_uint64, u32p]),
         "krk_hrw_uint64_to_float64": (i, [u8p, C.c_uint64, i, f64p]),
         "krk_set_sha_plan": (i, [i]),
+        "krk_device_clock_mhz": (i, [vp, f64p]),
         "krk_digester_write": (i, [vp, vp, C.c_uint64]),
         "krk_digester_sum": (i, [vp, u8p]),
         "krk_digester_free": (None, [vp]),

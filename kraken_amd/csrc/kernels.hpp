@@ -148,6 +148,8 @@ struct SynthChunk {
     uint64_t n;
 };
 hipError_t launch_synth_fill_chunks(const SynthChunk* chunks, uint32_t n_chunks, int variant, hipStream_t s);
+// Shader clock probe: out[0] = shader cycles, out[1] = 100 MHz ticks of one spin.
+hipError_t launch_clock_probe(uint32_t spins, uint64_t* out, hipStream_t s);
 hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n,
                              int variant, hipStream_t s);
 

@@ -1382,6 +1382,23 @@ int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes) {
     *lanes = sha_lanes_for((uint32_t)n_streams);
     return KRK_OK;
 }
+int krk_device_clock_mhz(void* stream, double* mhz) {
+    KRK_CHECK(mhz, KRK_EINVAL, "mhz is NULL");
+    KRK_DEVICE(D);
+    hipStream_t s = pick(D, stream);
+    uint64_t* d_out = nullptr;
+    KRK_HIP(scratch_alloc(D, &d_out, 32, s));
+    uint64_t h[3] = {0, 0, 0};
+    hipError_t e = launch_clock_probe(1u << 20, d_out, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d_out, 24, hipMemcpyDeviceToHost, s);
+    scratch_free(D, d_out, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "clock probe: %s", hipGetErrorString(e));
+    KRK_CHECK(h[1] > 0, KRK_EHIP, "clock probe: no realtime ticks");
+    *mhz = (double)h[0] / (double)h[1] * 100.0;
+    return KRK_OK;
+}
+
 int krk_set_sha_plan(int plan) {
     KRK_CHECK(sha_plan_valid(plan), KRK_EINVAL, "unknown SHA-256 launch plan %d", plan);
     set_sha_plan(plan);

@@ -108,4 +108,29 @@ hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint6
     return hipGetLastError();
 }
 
+// Shader clock probe (measurement support): one wave spins on a dependent VALU chain
+// and stamps s_memtime (shader cycles) and s_memrealtime (constant 100 MHz) around it;
+// clock = d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
+// Launched beside a running kernel it reads the clock the chip holds under that load.
+__global__ void __launch_bounds__(64) clock_probe_kernel(uint32_t spins, uint32_t seed, uint64_t* out) {
+    uint32_t x = seed + threadIdx.x;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    for (uint32_t i = 0; i < spins; ++i) x = x * 1664525u + 1013904223u;
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = r1 - r0;
+        out[2] = x;
+    }
+}
+
+hipError_t launch_clock_probe(uint32_t spins, uint64_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, spins, 12345u, out);
+    return hipGetLastError();
+}
+
 }  // namespace krk

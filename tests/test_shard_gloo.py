@@ -1,7 +1,7 @@
-"""Multi-process (world_size 2, gloo, CPU) coverage of the N>1 path: LPT blob
-sharding and the host gather of per-blob results.  The per-blob compute here is
-the CPU oracle (no GPU in this suite); the GPU path is the same code with the
-HIP kernels as the compute."""
+"""Multi-process (world_size 2, gloo, CPU) coverage of the N>1 control plane: LPT
+blob sharding and the host gather of per-blob results.  The per-blob compute here
+is the CPU oracle (no GPU in this suite); tests/test_gpu_shard_gloo.py runs the same
+sharding and gather with the product (the C ABI on the GPU) as the compute."""
 import os
 import socket
 

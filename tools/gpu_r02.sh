@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-2 GPU session steps (one gpurun call runs several): each step under its own
+# time limit, stopping at the first crash / timeout / GPU fault.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$PWD
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name $(date +%T)" >&2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >&2
+  tail -3 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
+  if grep -qiE "memory fault|illegal memory access|memory access fault|device not stable" "gpurun_out/$name.log"; then
+    echo "stopping after $name (GPU fault in log)" >&2; exit 3
+  fi
+  return 0
+}
+P1="GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS"
+P2="GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAIT_INST_LDS"
+C2="--steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-ceiling"
+for s in "$@"; do
+  case $s in
+    test) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 900 python bench.py ;;
+    bench20) step bench20 900 python bench.py --steps 20 --warmup 5 ;;
+    prof) step prof_c2 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c2 -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-ceiling ;;
+    valu) step valu_c2_p1 600 rocprofv3 --kernel-trace --pmc $P1 --output-format csv -d $R/gpurun_out/valu_c2_p1 -- python3 $R/bench.py $C2 &&
+          step valu_c2_p2 600 rocprofv3 --kernel-trace --pmc $P2 --output-format csv -d $R/gpurun_out/valu_c2_p2 -- python3 $R/bench.py $C2 &&
+          step valu_c2_json 120 python tools/pmc_valu.py --dirs gpurun_out/valu_c2_p1 gpurun_out/valu_c2_p2 --mode device_resident --out gpurun_out/valu_c2.json --what "bench.py C2, one step: krk_metainfo_digest_dev over 1000 x 100 MiB in HBM" ;;
+    value2e) step valu_e2e_p1 900 rocprofv3 --kernel-trace --pmc $P1 --output-format csv -d $R/gpurun_out/valu_e2e_p1 -- python3 $R/bench.py --e2e-only --no-cpu-baseline &&
+          step valu_e2e_p2 900 rocprofv3 --kernel-trace --pmc $P2 --output-format csv -d $R/gpurun_out/valu_e2e_p2 -- python3 $R/bench.py --e2e-only --no-cpu-baseline &&
+          step valu_e2e_json 120 python tools/pmc_valu.py --dirs gpurun_out/valu_e2e_p1 gpurun_out/valu_e2e_p2 --mode end_to_end --out gpurun_out/valu_c2.json --what "bench.py C2 end-to-end leg: krk_metainfo_digest_host over 1000 x 100 MiB in pageable host memory (the step before it, one device-resident step, is included in the device_resident block of its own pass)" ;;
+  esac
+done

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Instruction count of the production SHA-256 consumer loop, from the disassembly
+of the gfx950 code object inside libkraken_hip.so (the ISA side of the per-stream
+issue ceiling that bench.py reports for sha256_multi).
+
+The .hip_fatbin section holds one clang offload bundle per translation unit; the one
+with sha256_ws_kernel is unbundled and disassembled with the ROCm LLVM tools.  In the
+two-lane kernel (sha256_ws_kernel<0, true, 1>) every instruction-round has exactly one
+`v_add_u32_dpp ... row_mirror`, so the consumer's block loop is the backward-branch
+loop whose body holds those DPP adds (one loop iteration = one producer step = two
+blocks).  Per block we count every VALU instruction (the wave must issue each at >= 4
+cycles when alone on its SIMD, MI355X_MICROARCH.md 'vector-instruction ISSUE cost'),
+the 9-instruction rounds among them, and the LDS / SALU instructions beside them.
+
+    python tools/sha_isa.py [lib.so] [--json out.json]
+"""
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+KERNEL = "sha256_ws_kernel<0, true, 1>"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _disasm(lib_path: str) -> str:
+    with tempfile.TemporaryDirectory() as td:
+        fb = os.path.join(td, "fatbin.bin")
+        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", lib_path, os.devnull],
+                       check=True, capture_output=True)
+        blob = open(fb, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
+        for k, a in enumerate(starts):
+            e = starts[k + 1] if k + 1 < len(starts) else len(blob)
+            b, o = os.path.join(td, f"b{k}.bin"), os.path.join(td, f"c{k}.o")
+            open(b, "wb").write(blob[a:e])
+            r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={b}", f"--output={o}"],
+                               capture_output=True)
+            if r.returncode:
+                continue
+            s = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--demangle", o], check=True, capture_output=True,
+                               text=True).stdout
+            if KERNEL in s:
+                return s
+    raise RuntimeError(f"{KERNEL} not found in {lib_path}")
+
+
+def count(lib_path: str) -> dict:
+    lines = _disasm(lib_path).splitlines()
+    head = [i for i, l in enumerate(lines) if l.endswith(">:") and KERNEL in l][0]
+    nxt = [i for i, l in enumerate(lines) if i > head and l.endswith(">:")]
+    body = lines[head + 1:nxt[0] if nxt else len(lines)]
+    ins = []  # (address, text, branch target or None)
+    for l in body:
+        m = re.match(r"\s+(\S.*?)\s*//\s*([0-9A-Fa-f]+):", l)
+        if not m:
+            continue
+        t = re.search(r"\+0x([0-9a-f]+)>\s*$", l)
+        ins.append((int(m.group(2), 16), m.group(1), t.group(1) if t else None))
+    base = ins[0][0]
+    loops = []
+    for k, (a, t, tgt) in enumerate(ins):
+        if tgt is not None and t.startswith(("s_cbranch", "s_branch")):
+            dst = base + int(tgt, 16)  # objdump prints targets relative to the symbol start
+            if dst <= a:
+                loop = [x for x in ins if dst <= x[0] <= a]
+                loops.append(loop)
+    # the consumer's step loop: the shortest loop holding the most rounds (an inner
+    # back-edge that re-runs only part of a step does not count as the step)
+    most = max(sum("row_mirror" in x[1] for x in lp) for lp in loops)
+    loop = min((lp for lp in loops if sum("row_mirror" in x[1] for x in lp) == most), key=len)
+    dpp = sum("row_mirror" in x[1] for x in loop)
+    blocks = dpp // 66
+    assert blocks >= 1 and dpp == 66 * blocks, dpp
+    valu = sum(x[1].startswith("v_") for x in loop)
+    lds = sum(x[1].startswith("ds_") for x in loop)
+    salu = sum(x[1].startswith("s_") for x in loop)
+    mix = {}
+    for x in loop:
+        op = x[1].split()[0]
+        mix[op] = mix.get(op, 0) + 1
+    return {"instruction_mix_per_iteration": dict(sorted(mix.items(), key=lambda kv: -kv[1])),"kernel": KERNEL, "loop_instructions": len(loop), "blocks_per_iteration": blocks,
+            "instruction_rounds_per_block": dpp // blocks, "round_valu_per_block": 9 * (dpp // blocks),
+            "valu_per_block": valu / blocks, "lds_per_block": lds / blocks, "salu_per_block": salu / blocks,
+            "issue_cycles_per_valu": 4, "source": "llvm-objdump of the gfx950 code object in " +
+            os.path.relpath(lib_path, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))}
+
+
+def ceiling_mbps(isa: dict, clock_mhz: float) -> float:
+    """Per-stream ceiling: one 64-byte block per (VALU per block x 4 cycles)."""
+    return 64.0 * clock_mhz / (isa["valu_per_block"] * isa["issue_cycles_per_valu"])
+
+
+if __name__ == "__main__":
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    lib = args[0] if args else os.path.join(root, "kraken_amd", "lib", "libkraken_hip.so")
+    res = count(lib)
+    res["ceiling_per_stream_MBps_at_2400MHz"] = round(ceiling_mbps(res, 2400.0), 3)
+    print(json.dumps(res, indent=1))
+    if "--json" in sys.argv:
+        out = sys.argv[sys.argv.index("--json") + 1]
+        json.dump(res, open(out, "w"), indent=1)
