@@ -140,7 +140,7 @@ __device__ __forceinline__ u32x4 ld16(gptr<u32x4> p) {
     else return *p;
 }
 
-template <class TT, int RG, bool LOADONLY = false, bool NT = false>
+template <class TT, int RG, bool LOADONLY = false, bool NT = false, bool DEEP = false>
 __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                      const uint32_t* G, uint32_t lane_mul,
                                                      const uint32_t* x8pow) {
@@ -149,24 +149,53 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
     const uint32_t nfull = len / kStep;
     if ((base & 15) == 0) {
         if (nfull > 0) {
-            // Two register sets in ping-pong: the next step's 4 x 16 B are in
-            // flight while the current step's lookups run.
             gptr<u32x4> p = as_global<u32x4>(base + lane * kSeg);
             constexpr uint32_t S = kStep / 16;
-            u32x4 a0 = ld16<NT>(p), a1 = ld16<NT>(p + 1), a2 = ld16<NT>(p + 2), a3 = ld16<NT>(p + 3);
-            u32x4 b0, b1, b2, b3;
-            uint32_t s = 0;
-            for (; s + 2 <= nfull; s += 2) {
-                gptr<u32x4> q = p + (s + 1) * S;
-                b0 = ld16<NT>(q); b1 = ld16<NT>(q + 1); b2 = ld16<NT>(q + 2); b3 = ld16<NT>(q + 3);
-                c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
-                if (s + 2 < nfull) {
-                    q = p + (s + 2) * S;
-                    a0 = ld16<NT>(q); a1 = ld16<NT>(q + 1); a2 = ld16<NT>(q + 2); a3 = ld16<NT>(q + 3);
+            if constexpr (DEEP) {
+                // Three register sets in rotation: the loads of step s + 2 are in flight
+                // while step s's lookups run (8 KiB a wave ahead instead of 4).
+                u32x4 a0, a1, a2, a3, b0, b1, b2, b3, e0, e1, e2, e3;
+                a0 = ld16<NT>(p); a1 = ld16<NT>(p + 1); a2 = ld16<NT>(p + 2); a3 = ld16<NT>(p + 3);
+                if (nfull > 1) {
+                    gptr<u32x4> q = p + S;
+                    b0 = ld16<NT>(q); b1 = ld16<NT>(q + 1); b2 = ld16<NT>(q + 2); b3 = ld16<NT>(q + 3);
                 }
-                c = step64<TT, RG, LOADONLY>(c, b0, b1, b2, b3, T, G);
+                uint32_t s = 0;
+                for (; s + 3 <= nfull; s += 3) {
+                    gptr<u32x4> q = p + (s + 2) * S;
+                    e0 = ld16<NT>(q); e1 = ld16<NT>(q + 1); e2 = ld16<NT>(q + 2); e3 = ld16<NT>(q + 3);
+                    c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
+                    if (s + 3 < nfull) {
+                        q = p + (s + 3) * S;
+                        a0 = ld16<NT>(q); a1 = ld16<NT>(q + 1); a2 = ld16<NT>(q + 2); a3 = ld16<NT>(q + 3);
+                    }
+                    c = step64<TT, RG, LOADONLY>(c, b0, b1, b2, b3, T, G);
+                    if (s + 4 < nfull) {
+                        q = p + (s + 4) * S;
+                        b0 = ld16<NT>(q); b1 = ld16<NT>(q + 1); b2 = ld16<NT>(q + 2); b3 = ld16<NT>(q + 3);
+                    }
+                    c = step64<TT, RG, LOADONLY>(c, e0, e1, e2, e3, T, G);
+                }
+                if (s < nfull) c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
+                if (s + 1 < nfull) c = step64<TT, RG, LOADONLY>(c, b0, b1, b2, b3, T, G);
+            } else {
+                // Two register sets in ping-pong: the next step's 4 x 16 B are in
+                // flight while the current step's lookups run.
+                u32x4 a0 = ld16<NT>(p), a1 = ld16<NT>(p + 1), a2 = ld16<NT>(p + 2), a3 = ld16<NT>(p + 3);
+                u32x4 b0, b1, b2, b3;
+                uint32_t s = 0;
+                for (; s + 2 <= nfull; s += 2) {
+                    gptr<u32x4> q = p + (s + 1) * S;
+                    b0 = ld16<NT>(q); b1 = ld16<NT>(q + 1); b2 = ld16<NT>(q + 2); b3 = ld16<NT>(q + 3);
+                    c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
+                    if (s + 2 < nfull) {
+                        q = p + (s + 2) * S;
+                        a0 = ld16<NT>(q); a1 = ld16<NT>(q + 1); a2 = ld16<NT>(q + 2); a3 = ld16<NT>(q + 3);
+                    }
+                    c = step64<TT, RG, LOADONLY>(c, b0, b1, b2, b3, T, G);
+                }
+                if (s < nfull) c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
             }
-            if (s < nfull) c = step64<TT, RG, LOADONLY>(c, a0, a1, a2, a3, T, G);
             end = (nfull - 1) * kStep + (lane + 1) * kSeg;
         }
         const uint32_t ts = nfull * kStep + lane * kSeg;
@@ -291,15 +320,31 @@ __device__ __forceinline__ ItemRef fetch_item(const CrcWork& w, uint32_t it) {
             jj == 0 ? w.consts[r.cpat + r.ipp] : 0u};
 }
 
-template <class TT, int RG, bool COAL, bool LOADONLY, bool NT>
+// A wave's next item: the static stride (it + n_waves), or, with the work queue, the
+// next unclaimed item (one atomicAdd by lane 0, broadcast) -- a wave on a CU that
+// started late or runs slower (beside another kernel) simply claims fewer items.
+template <bool QUEUE>
+__device__ __forceinline__ uint32_t next_item(const CrcWork& w, uint32_t it, uint32_t n_waves, uint32_t lane) {
+    if constexpr (QUEUE) {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(w.next, 1u);
+        return __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
+    } else {
+        return it + n_waves;
+    }
+}
+
+template <class TT, int RG, bool COAL, bool LOADONLY, bool NT, bool DEEP, bool QUEUE = false>
 __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const uint32_t* G, const uint32_t lm[4],
                                           const uint32_t* x8pow, uint32_t lane, uint32_t wave0, uint32_t n_waves,
                                           uint32_t* sums) {
     const uint32_t n_items = w.run_items + w.n_items;
-    for (uint32_t it = wave0; it < n_items; it += n_waves) {
+    // every wave leaves once the queue head passes n_items (no wave waits on another)
+    for (uint32_t it = QUEUE ? next_item<true>(w, 0, 0, lane) : wave0; it < n_items;
+         it = next_item<QUEUE>(w, it, n_waves, lane)) {
         const ItemRef ci = fetch_item(w, it);
         uint32_t c = COAL ? lane_crc_coal<TT, RG, LOADONLY>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
-                          : lane_crc_strided<TT, RG, LOADONLY, NT>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
+                          : lane_crc_strided<TT, RG, LOADONLY, NT, DEEP>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
         // Wave XOR-reduction.
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c ^= __shfl_xor(c, off, 64);
@@ -310,7 +355,8 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
     }
 }
 
-template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false>
+template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false, bool DEEP = false,
+          bool QUEUE = false>
 __global__ void __launch_bounds__(BLOCK)
 crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -342,23 +388,24 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
         if ((uint32_t)(size_t)(lds_u32p)lds != 0) __builtin_trap();
         TabP<PERM> T;
         T.loff = (1u << 16) | ((lane % PERM) << 2);
-        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT, DEEP, QUEUE>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
     } else {
         Tab<R> T;
         T.lo = lds + (lane % R);
         T.hi = lds + 2 * 256 * R + (lane % R);
-        item_loop<Tab<R>, RG, COAL, LOADONLY, NT>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+        item_loop<Tab<R>, RG, COAL, LOADONLY, NT, DEEP, QUEUE>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
     }
 }
 
-template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false>
+template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false,
+          bool DEEP = false, bool QUEUE = false>
 static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
                                  int blocks_per_cu, hipStream_t s) {
     constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4;
     static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>),
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (attr_err != hipSuccess) return attr_err;
@@ -368,20 +415,23 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
     uint64_t cap = uint64_t(cus) * blocks_per_cu;
     uint32_t grid = (uint32_t)(want < cap ? want : cap);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
+    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
     return hipGetLastError();
 }
 
-// Production launch variants (bit-exact): 7 = strided layout, byte-addressable tables
-// with 32 replicas (144 KiB of LDS, one 1024-thread workgroup per CU), the default;
-// 8 = the same with 16 replicas (80 KiB, two workgroups per CU).  Every other layout
+// Production launch variants (bit-exact): 16 = strided layout, byte-addressable tables
+// with 32 replicas (144 KiB of LDS, one 1024-thread workgroup per CU) and the work
+// queue, the default (+2.5-3 % over the static stride: 6.03-6.09 TB/s on 4 MiB pieces,
+// 6.05 on 256 KiB, tools/crc_try.sh); 7 = the same with a static item stride; 8 = 7
+// with 16 replicas (80 KiB, two workgroups per CU); 14 / 17 = 7 / 16 with three load
+// sets in rotation; 15 = 14 with 8 gap-table replicas (160 KiB).  Every other layout
 // measured in DESIGN.md 4.1 -- and the load-only timing diagnostics, which give WRONG
 // sums -- is compiled only into the diagnostic build (make diag, -DKRK_DIAG).
 bool crc_variant_valid(int v) {
 #ifdef KRK_DIAG
-    return v >= 0 && v <= 13;
+    return v >= 0 && v <= 17;
 #else
-    return v == 7 || v == 8;
+    return v == 7 || v == 8 || v == 14 || v == 15 || v == 16 || v == 17;
 #endif
 }
 
@@ -393,6 +443,16 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
             return launch_variant<32, 4, 1024, false, false, 32>(w, tabs, sums, cfg.cus, 1, s);
         case 8:
             return launch_variant<16, 4, 1024, false, false, 16>(w, tabs, sums, cfg.cus, 2, s);
+        case 14:  // 7 with three load sets in rotation (two steps of loads in flight)
+            return launch_variant<32, 4, 1024, false, false, 32, false, true>(w, tabs, sums, cfg.cus, 1, s);
+        case 15:  // 14 with 8 gap-table replicas (160 KiB of LDS: fewer bank conflicts on the gap lookups)
+            return launch_variant<32, 8, 1024, false, false, 32, false, true>(w, tabs, sums, cfg.cus, 1, s);
+        case 16:  // 7 with the work queue (items claimed by atomicAdd instead of a static stride)
+            return w.next ? launch_variant<32, 4, 1024, false, false, 32, false, false, true>(w, tabs, sums, cfg.cus, 1, s)
+                          : hipErrorInvalidValue;
+        case 17:  // 14 with the work queue
+            return w.next ? launch_variant<32, 4, 1024, false, false, 32, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
+                          : hipErrorInvalidValue;
 #ifdef KRK_DIAG
         case 0:  // strided, interleaved R16 tables, 80 KiB LDS: two 512-thread blocks per CU
             return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);

@@ -66,6 +66,7 @@ struct CrcWork {
     uint32_t run_items;
     uint32_t n_items;
     uint32_t pad;
+    uint32_t* next;  // work-queue head (zeroed per launch): waves claim items by atomicAdd
 };
 
 struct CrcLaunchCfg {

@@ -228,10 +228,12 @@ inline int init_device(Device& D, int id) {
             tabs[kTabLaneMulC + k * 64 + l] = x8n(uint64_t(kGapC) - 1024 * k - 16 * l, xp.v);
     KRK_HIP(hipMalloc(&D.d_tabs, kTabWords * 4));
     KRK_HIP(hipMemcpy(D.d_tabs, tabs.data(), kTabWords * 4, hipMemcpyHostToDevice));
-    // Launch variant, read once per device context (crc32_pieces.hip: 7 = byte-addressable
-    // tables, the default; 8 = its 16-replica form; the rest only in the KRK_DIAG build).
+    // Launch variant, read once per device context (crc32_pieces.hip: 16 = byte-addressable
+    // tables with the work queue, the default; 7 = the same with a static item stride; 8,
+    // 14, 15, 17 = measured alternatives; the rest only in the KRK_DIAG build).
     const char* v = getenv("KRK_CRC_VARIANT");
-    D.crc_variant = crc_variant_valid(v ? atoi(v) : 7) ? (v ? atoi(v) : 7) : 7;
+    const int want = v ? atoi(v) : 16;
+    D.crc_variant = crc_variant_valid(want) ? want : 16;
     return KRK_OK;
 }
 
@@ -449,8 +451,16 @@ inline int run_items(Device* D, const CrcBatch& B, uint32_t* sums_dev, hipStream
     w.n_runs = (uint32_t)B.runs.size();
     w.run_items = (uint32_t)B.run_items;
     w.n_items = (uint32_t)B.items.size();
+    uint32_t* d_next = nullptr;  // the work-queue head, zeroed in stream order
+    if (scratch_alloc(D, &d_next, 4, s) != hipSuccess || hipMemsetAsync(d_next, 0, 4, s) != hipSuccess) {
+        scratch_free(D, d_pack, s);
+        set_error(KRK_EHIP, "crc32_pieces: work-queue head");
+        return KRK_EHIP;
+    }
+    w.next = d_next;
     CrcLaunchCfg cfg{D->cus, D->crc_variant};
     hipError_t e = timed(K_CRC, s, [&] { return launch_crc_items(w, D->d_tabs, sums_dev, cfg, s); });
+    scratch_free(D, d_next, s);
     scratch_free(D, d_pack, s);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
     return KRK_OK;

@@ -175,6 +175,7 @@ def test_production_library_has_no_diagnostic_kernels():
     assert not any("sha256_multi_kernel" in k for k in kern)
     # crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>: strided, no load-only, no NT
     assert all(k.split("<")[1].startswith(("32, 4, 1024, false, false, 32, false",
+                                           "32, 8, 1024, false, false, 32, false",
                                            "16, 4, 1024, false, false, 16, false")) for k in crc), crc
     assert b"KRK_SHA_VARIANT" not in open(_capi.LIB_PATH, "rb").read()
 

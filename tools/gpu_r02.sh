@@ -36,3 +36,18 @@ for s in "$@"; do
           step valu_e2e_json 120 python tools/pmc_valu.py --dirs gpurun_out/valu_e2e_p1 gpurun_out/valu_e2e_p2 --mode end_to_end --out gpurun_out/valu_c2.json --what "bench.py C2 end-to-end leg: krk_metainfo_digest_host over 1000 x 100 MiB in pageable host memory (the step before it, one device-resident step, is included in the device_resident block of its own pass)" ;;
   esac
 done
+for s in "$@"; do
+  case $s in
+    vop) step micro_vopcost 120 tools/micro/vopcost ;;
+    prof4) step prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4 -- python3 $R/bench.py --workload c4 --no-cpu-baseline ;;
+    prof5) step prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c5 -- python3 $R/bench.py --workload c5 --no-cpu-baseline --no-sweep ;;
+    prof3) step prof_c3 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c3 -- python3 $R/bench.py --workload c3 --no-cpu-baseline ;;
+    bc1) step bench_c1 600 python bench.py --workload c1 --steps 1 --warmup 1 ;;
+    bc3) step bench_c3 900 python bench.py --workload c3 ;;
+    bc4) step bench_c4 600 python bench.py --workload c4 ;;
+    bc5) step bench_c5 600 python bench.py --workload c5 ;;
+    bc5r) step bench_c5regen 900 python bench.py --workload c5regen ;;
+    bf1) step bench_f1verify 600 python bench.py --workload f1verify ;;
+    crcspec) step crc_spec 600 python tools/probe_perf.py --crc-spec 16:100:4096,16:256:256 --sha none ;;
+  esac
+done

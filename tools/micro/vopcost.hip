@@ -189,6 +189,12 @@ __global__ void cost(unsigned long long* out, unsigned* sink) {
     if (K == 23) BODY("v_add3_u32 %0, %0, %5, %6\n\tv_add3_u32 %1, %1, %5, %6\n\tv_add3_u32 %2, %2, %5, %6\n\tv_add3_u32 %3, %3, %5, %6");
     // dependent through a DPP source read (needs 2 wait states: here filled by 2 independent ops)
     if (K == 24) BODY("v_add_u32_dpp %0, %0, %5 row_mirror row_mask:0xf bank_mask:0xf\n\tv_add_u32_e32 %1, %1, %5\n\tv_add_u32_e32 %2, %2, %5");
+    // encoding size vs operand count: a VOP2 add with a 32-bit literal is 8 bytes with two sources
+    if (K == 25) BODY("v_add_u32_e32 %0, 0x12345, %5");
+    if (K == 26) BODY("v_fma_f32 %0, %4, %5, %6");
+    if (K == 27) BODY("v_mov_b32_e32 %0, 0x12345");
+    if (K == 28) BODY("v_add_u32_e32 %0, %4, %5\n\tv_add3_u32 %1, %4, %5, %6");
+    if (K == 29) BODY("v_add_u32_e32 %0, %4, %5\n\tv_add_u32_e32 %1, %4, %6\n\tv_add3_u32 %2, %4, %5, %6");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
         out[K] = t1 - t0;
@@ -212,13 +218,16 @@ int main() {
                            "xad 3 vgprs", "add VOP2", "add VOP3 (e64)", "add DPP", "lshl_add v,imm,v",
                            "bitop3 2 vgprs+sgpr", "xor VOP2", "cndmask VOP2", "DEP add VOP2", "DEP add3",
                            "DEP alignbit", "DEP bitop3", "DEP dpp+s_nop1 (per pair)", "s_nop 1", "2 chains add3 (per pair)",
-                           "4 chains add3 (per 4)", "DEP dpp + 2 indep (per 3)"};
+                           "4 chains add3 (per 4)", "DEP dpp + 2 indep (per 3)", "add VOP2 + literal (8B)",
+                           "fma_f32 (VOP3 8B)", "mov VOP1 + literal (8B)", "add VOP2 + add3 (per pair)",
+                           "2 add VOP2 + add3 (per 3)"};
     for (int rep = 0; rep < 3; ++rep) {
         run<0>(d, sink); run<1>(d, sink); run<2>(d, sink); run<3>(d, sink); run<4>(d, sink); run<5>(d, sink);
         run<6>(d, sink); run<7>(d, sink); run<8>(d, sink); run<9>(d, sink); run<10>(d, sink); run<11>(d, sink);
         run<12>(d, sink); run<13>(d, sink); run<14>(d, sink); run<15>(d, sink);
         run<16>(d, sink); run<17>(d, sink); run<18>(d, sink); run<19>(d, sink); run<20>(d, sink); run<21>(d, sink);
-        run<22>(d, sink); run<23>(d, sink); run<24>(d, sink);
+        run<22>(d, sink); run<23>(d, sink); run<24>(d, sink); run<25>(d, sink); run<26>(d, sink);
+        run<27>(d, sink); run<28>(d, sink); run<29>(d, sink);
         hipLaunchKernelGGL(rcost<0>, 1, 64, 0, 0, d, sink);
         hipLaunchKernelGGL(rcost<1>, 1, 64, 0, 0, d, sink);
         hipLaunchKernelGGL(rcost<2>, 1, 64, 0, 0, d, sink);
@@ -237,7 +246,7 @@ int main() {
         unsigned long long h[128];
         hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
         if (rep == 2)
-            for (int k = 0; k < 25; ++k)
+            for (int k = 0; k < 30; ++k)
                 printf("%-26s %.2f cycles/instr  (%.3f GHz)\n", names[k], h[k] / (256.0 * 64), h[k] / (h[64 + k] * 10.0));
         if (rep == 2) {
             const char* rn[] = {"round VGPR-shift DPP", "round imm-shift DPP", "round VGPR-shift add", "round imm-shift add"};

@@ -69,13 +69,15 @@ if __name__ == "__main__":
     ap.add_argument("--crc-gb", type=float, default=16)
     ap.add_argument("--sha", default="64:8,1024:8,4096:4,16384:1")
     ap.add_argument("--variant", default="0")
-    ap.add_argument("--sha-variant", default="-1")
+    ap.add_argument("--sha-plan", type=int, default=0,
+                    help="krk_set_sha_plan: 0 auto, 1-4 production, 100-107 diagnostics (KRK_DIAG build, "
+                         "KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so)")
     ap.add_argument("--c2", action="store_true")
     ap.add_argument("--crc-spec", default="", help="gb:blob_mb:piece_kb,... custom CRC shapes")
     a = ap.parse_args()
     os.environ["KRK_CRC_VARIANT"] = a.variant
-    os.environ["KRK_SHA_VARIANT"] = a.sha_variant
     D.set_device(0)
+    D.check(D.lib.krk_set_sha_plan(a.sha_plan))
     res = []
     if a.c2:
         print(json.dumps(crc_concurrent(1000, 100, 4 << 20)), flush=True)
