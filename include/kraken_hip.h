@@ -310,6 +310,14 @@ int krk_hrw_uint64_to_float64(const uint8_t* sums8, uint64_t n, int rehash, doub
 int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* nodes,
                        const uint8_t* healthy, int32_t max_replica,
                        int32_t* locs_out, uint8_t* counts_out);
+/* The whole ring in one call: Locations(d) depends on d only through ShardID =
+ * hex[:4] (core/digest.go:148-150), so the 65,536 possible owner lists are computed
+ * once per membership or health change (ring.Refresh, lib/hashring/ring.go:141-165)
+ * and Locations becomes a host lookup: row ((d[0] << 8) | d[1]) of locs_out
+ * (65,536 x max(1, max_replica) node indices, -1 padded) with counts_out[row] valid
+ * entries.  Same semantics as krk_ring_locations. */
+int krk_ring_owner_table(const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica,
+                         int32_t* locs_out, uint8_t* counts_out);
 /* Device-resident form (digests/locs/counts are device pointers). */
 int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
                            const uint8_t* healthy, int32_t max_replica,

@@ -108,6 +108,7 @@ def _load() -> C.CDLL:
         "krk_hrw_ordered": (i, [C.c_char_p, u64p, C.c_uint64, nodesp, C.c_uint32, i32p, f64p]),
         "krk_ring_locations": (i, [u8p, C.c_uint64, nodesp, u8p, C.c_int32, i32p, u8p]),
         "krk_ring_locations_dev": (i, [vp, C.c_uint64, nodesp, u8p, C.c_int32, vp, vp, vp]),
+        "krk_ring_owner_table": (i, [nodesp, u8p, C.c_int32, i32p, u8p]),
         "krk_ring_locations_u8_dev": (i, [vp, C.c_uint64, nodesp, u8p, C.c_int32, vp, vp, vp]),
         "krk_synth_fill_dev": (i, [vp, C.c_uint64, C.c_uint64, C.c_uint64, i, vp]),
         "krk_synth_fill_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, i, vp]),

@@ -1192,18 +1192,10 @@ int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* no
 
 }  // extern "C"
 
-template <typename T>
-static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
-                              const uint8_t* healthy, int32_t max_replica, T* locs_dev, uint8_t* counts_dev,
-                              void* stream) {
-    if (!n) return KRK_OK;
-    KRK_CHECK(digests32_dev && healthy && locs_dev && counts_dev && nodes, KRK_EINVAL,
-              "ring_locations_dev: null argument");
-    KRK_CHECK(sizeof(T) != 1 || nodes->n_nodes <= 255, KRK_ERANGE,
-              "ring_locations_u8_dev: %u nodes do not fit 8-bit owner indices (<= 255)", nodes->n_nodes);
-    KRK_DEVICE(D);
-    hipStream_t s = pick(D, stream);
-    const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
+// The 65,536-row owner table (one row per ShardID) on the device: d_tl rows of row_out
+// node indices (-1 padded), d_tc counts.  Released by the caller with scratch_free.
+static int shard_owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica,
+                             uint32_t row_out, int32_t** d_tl, uint8_t** d_tc, hipStream_t s) {
     std::call_once(D->shard_once, [D] {
         std::vector<uint32_t> shards(65536);
         std::iota(shards.begin(), shards.end(), 0u);
@@ -1218,10 +1210,25 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
             D->shard_rc = KRK_ENOMEM;
     });
     KRK_CHECK(D->shard_rc == KRK_OK, D->shard_rc, "shard key table allocation failed");
+    return hrw_table_dev(D, D->shard_kb, D->shard_koff, D->shard_bad, 65536, nodes, healthy, max_replica, row_out,
+                         d_tl, d_tc, s);
+}
+
+template <typename T>
+static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
+                              const uint8_t* healthy, int32_t max_replica, T* locs_dev, uint8_t* counts_dev,
+                              void* stream) {
+    if (!n) return KRK_OK;
+    KRK_CHECK(digests32_dev && healthy && locs_dev && counts_dev && nodes, KRK_EINVAL,
+              "ring_locations_dev: null argument");
+    KRK_CHECK(sizeof(T) != 1 || nodes->n_nodes <= 255, KRK_ERANGE,
+              "ring_locations_u8_dev: %u nodes do not fit 8-bit owner indices (<= 255)", nodes->n_nodes);
+    KRK_DEVICE(D);
+    hipStream_t s = pick(D, stream);
+    const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
     int32_t* d_tl = nullptr;
     uint8_t* d_tc = nullptr;
-    int r = hrw_table_dev(D, D->shard_kb, D->shard_koff, D->shard_bad, 65536, nodes, healthy, max_replica, row_out,
-                          &d_tl, &d_tc, s);
+    int r = shard_owner_table(D, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, s);
     if (!r) {
         hipError_t e = timed(K_GATHER, s, [&] {
             if constexpr (sizeof(T) == 1)
@@ -1237,6 +1244,26 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
 }
 
 extern "C" {
+
+int krk_ring_owner_table(const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica, int32_t* locs_out,
+                         uint8_t* counts_out) {
+    KRK_CHECK(nodes && healthy && locs_out && counts_out, KRK_EINVAL, "ring_owner_table: null argument");
+    KRK_DEVICE(D);
+    hipStream_t s = D->s_main;
+    const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
+    int32_t* d_tl = nullptr;
+    uint8_t* d_tc = nullptr;
+    int r = shard_owner_table(D, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, s);
+    if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "owner table sync"); r = KRK_EHIP; }
+    if (!r && (hipMemcpy(locs_out, d_tl, size_t(65536) * row_out * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(counts_out, d_tc, 65536, hipMemcpyDeviceToHost) != hipSuccess)) {
+        set_error(KRK_EHIP, "owner table copy");
+        r = KRK_EHIP;
+    }
+    if (d_tl) scratch_free(D, d_tl, s);
+    if (d_tc) scratch_free(D, d_tc, s);
+    return r;
+}
 
 int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
                            const uint8_t* healthy, int32_t max_replica, int32_t* locs_dev, uint8_t* counts_dev,

@@ -4,8 +4,13 @@
 digest's ShardID (core/digest.go:148-150) over every member (weight 100,
 ring.go:28,150-153), then the healthy filter: no healthy node -> [order[0]];
 else walk the order while (no location yet or i < MaxReplica), keeping healthy
-nodes.  Membership/health monitoring (Monitor/Refresh) is out of scope: the
-caller passes the member list and the healthy set.
+nodes.  Membership/health monitoring (Monitor, the health filters) is out of scope:
+the caller passes the member list and the healthy set.
+
+Locations depends on the digest only through its 2-byte ShardID, so Refresh (the
+reference rebuilds its hrw object there, ring.go:141-165) computes all 65,536 owner
+lists on the GPU in one call (krk_ring_owner_table) and Locations is a host lookup
+-- the binding INTEGRATION.md gives the Go ring.
 """
 from __future__ import annotations
 
@@ -34,6 +39,18 @@ class Ring:
     def set_healthy(self, healthy) -> None:
         hs = set(healthy)
         self._healthy = np.array([1 if a in hs else 0 for a in self.addrs], dtype=np.uint8)
+        self._table = None  # rebuilt by the next Refresh / Locations
+
+    def Refresh(self) -> None:
+        """The 65,536-row owner table for the current members and healthy set."""
+        row = max(1, self.max_replica)
+        locs = np.full((65536, row), -1, dtype=np.int32)
+        counts = np.zeros(65536, dtype=np.uint8)
+        nt = _NodeTable(self.hash.Nodes)
+        check(lib.krk_ring_owner_table(C.byref(nt.s), self._healthy.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                       self.max_replica, locs.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       counts.ctypes.data_as(C.POINTER(C.c_uint8))))
+        self._table = (locs, counts)
 
     def Contains(self, addr: str) -> bool:
         return addr in self.addrs
@@ -52,9 +69,12 @@ class Ring:
         return locs, counts
 
     def Locations(self, d) -> list[str]:
-        raw = np.frombuffer(bytes.fromhex(d.Hex()), dtype=np.uint8)
-        locs, counts = self._raw(raw)
-        return [self.addrs[int(j)] for j in locs[0, : counts[0]]]
+        """ring.Locations (lib/hashring/ring.go:91-118): a lookup of the ShardID's row."""
+        if self._table is None:
+            self.Refresh()
+        locs, counts = self._table
+        shard = int(d.ShardID(), 16)
+        return [self.addrs[int(j)] for j in locs[shard, : counts[shard]]]
 
     def LocationsBatch(self, digests32: np.ndarray):
         """Raw 32-byte digests -> (int32 [n, max(1,MaxReplica)] node indices, uint8 [n] counts)."""

@@ -216,3 +216,32 @@ def test_uint64_to_float64_rehash_branch_on_device(gpu, orc):
     got = _u64_to_f64_dev(rnd, True)
     for v, g in zip(rnd, got):
         assert g.tobytes() == np.float64(orc.uint64_to_float64(v, True)).tobytes(), hex(v)
+
+
+@pytest.mark.parametrize("n_nodes,max_replica", [(3, 2), (16, 3), (64, 2)])
+def test_ring_owner_table_lookup(gpu, orc, n_nodes, max_replica):
+    """Ring.Refresh builds all 65,536 owner lists (krk_ring_owner_table); Locations is a
+    host lookup of the ShardID row.  Every 97th row against the oracle, the lookups
+    against the per-call path, and a health change followed by Refresh."""
+    from kraken_amd import core
+    rng = np.random.default_rng(n_nodes * 7 + max_replica)
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(n_nodes)]
+    healthy = (rng.random(n_nodes) < 0.75).astype(np.uint8)
+    healthy[0] = 1
+    ring = hashring.Ring(labels, [l for l, h in zip(labels, healthy) if h], max_replica)
+    ring.Refresh()
+    locs, counts = ring._table
+    assert locs.shape == (65536, max(1, max_replica))
+    for shard in range(0, 65536, 97):
+        key = f"{shard:04x}"
+        ref = orc.ring_locations(orc.hrw_ordered(key, labels, [100] * n_nodes), healthy, max_replica)
+        assert locs[shard, : counts[shard]].tolist() == ref, key
+    digests = rng.integers(0, 256, size=(500, 32), dtype=np.uint8)
+    bl, bc = ring.LocationsBatch(digests)
+    for i in range(len(digests)):
+        d = core.NewSHA256DigestFromHex(bytes(digests[i]).hex())
+        assert ring.Locations(d) == [labels[j] for j in bl[i, : bc[i]]]
+    ring.set_healthy([])  # all unhealthy: [order[0]] per shard
+    d = core.NewSHA256DigestFromHex(bytes(digests[0]).hex())
+    key = d.ShardID()
+    assert ring.Locations(d) == [labels[orc.hrw_ordered(key, labels, [100] * n_nodes)[0]]]
