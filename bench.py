@@ -76,12 +76,19 @@ def sha_isa_ceiling(D, launch):
 
 def load_valu(workload):
     """VALU / LDS utilisation per kernel from the committed rocprofv3 PMC passes
-    (tools/pmc_valu.py -> profiles/r02/valu_<workload>.json)."""
+    (tools/pmc_valu.py -> profiles/r02/valu_<workload>.json); the raw counters stay in
+    that file, the derived fractions go into the bench line."""
     path = os.path.join(ROOT, "profiles", "r02", f"valu_{workload}.json")
     try:
-        return json.load(open(path)), os.path.relpath(path, ROOT)
+        d = json.load(open(path))
     except (OSError, ValueError):
         return {}, None
+    keep = ("valu_issue_frac_per_wave", "valu_busy_chip_pct", "lds_issue_frac_per_wave", "lds_bank_conflict_frac",
+            "wait_any_frac_per_wave", "wait_inst_any_frac_per_wave", "clock_mhz", "kernel_ms", "dispatches")
+    out = {}
+    for mode in ("device_resident", "end_to_end"):
+        out[mode] = {k: {m: v[m] for m in keep if m in v} for k, v in d.get(mode, {}).items() if isinstance(v, dict)}
+    return out, os.path.relpath(path, ROOT)
 
 
 WORKLOADS = {
@@ -241,7 +248,7 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
     HBM fraction is kept beside it."""
     lanes = D.sha_lanes_per_stream(n)
     per_stream = max(lens) / (avg_ms / 1e3) / 1e6
-    roof = {"kernel": "sha256_multi", "bound": "valu_issue_per_stream", "achieved": round(gbps, 2),
+    roof = {"kernel": "sha256_multi", "bound": "valu", "achieved": round(gbps, 2),
             "peak": None, "unit": "GB/s", "frac": None, "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
             "algorithmic_bytes_per_launch": bytes_launch,
             "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5)}}
@@ -262,9 +269,10 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
         else:
             ib["ceiling_error"] = isa.get("error")
     roof["issue_bound"] = ib
-    roof["note"] = ("SHA-256 is one sequential Merkle-Damgard chain per blob (two lanes each here): the kernel is "
-                    "bound by the per-stream VALU issue of its consumer waves (32 of the chip's 1,024 SIMDs for "
-                    "1,000 streams), not by HBM; peak = streams x ISA per-stream ceiling, hbm.frac beside it")
+    roof["note"] = ("bound 'valu': SHA-256 is one sequential Merkle-Damgard chain per blob (two lanes each here), so "
+                    "the kernel is bound by the per-stream VALU issue of its consumer waves (32 of the chip's 1,024 "
+                    "SIMDs for 1,000 streams), not by HBM; peak = streams x ISA per-stream ceiling, hbm.frac beside "
+                    "it (DESIGN.md 4.2)")
     return roof
 
 
@@ -347,7 +355,8 @@ def run_metainfo(a, D, T, rank, world, res):
         res["end_to_end"] = end_to_end(D, T, arena, n, min(a.e2e_mb << 20, lens[0]), P, out, world)
         ev = valu.get("end_to_end") if valu_src else None
         if ev:
-            res["end_to_end"]["valu"] = dict(ev, source=valu_src)
+            res["end_to_end"]["valu"] = {"sha256_multi": ev.get("sha256_multi"), "crc32_pieces": ev.get("crc32_pieces"),
+                                         "source": valu_src}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         m = min(n, 2 * host_cores())  # bounded sample: the first blobs of this workload
         cb, dg, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds)
