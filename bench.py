@@ -266,6 +266,14 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
                                           "shader clock measured beside a SHA launch (krk_device_clock_mhz)")})
             peak = n * ceil / 1e3
             roof.update({"peak": round(peak, 2), "frac": round(gbps / peak, 4)})
+            import sha_isa
+            fc = sha_isa.fetch_ceiling_mbps(isa, mhz)
+            ib["fetch_bound"] = {"code_bytes_per_block": isa["code_bytes_per_block"],
+                                 "fetch_bytes_per_cycle": round(sha_isa.FETCH_BYTES_PER_CYCLE, 3),
+                                 "ceiling_per_stream_MBps": round(fc, 2), "frac": round(per_stream / fc, 4),
+                                 "source": "one wave's code fetch, measured: 8-byte encodings issue every 4.64 "
+                                           "cycles whatever the operands (tools/micro/vopcost.hip, "
+                                           "profiles/r02/micro_vop_encoding_cost.txt)"}
         else:
             ib["ceiling_error"] = isa.get("error")
     roof["issue_bound"] = ib

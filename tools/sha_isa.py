@@ -56,14 +56,14 @@ def count(lib_path: str) -> dict:
     body = lines[head + 1:nxt[0] if nxt else len(lines)]
     ins = []  # (address, text, branch target or None)
     for l in body:
-        m = re.match(r"\s+(\S.*?)\s*//\s*([0-9A-Fa-f]+):", l)
+        m = re.match(r"\s+(\S.*?)\s*//\s*([0-9A-Fa-f]+):\s*([0-9A-F]{8})(?: ([0-9A-F]{8}))?", l)
         if not m:
             continue
         t = re.search(r"\+0x([0-9a-f]+)>\s*$", l)
-        ins.append((int(m.group(2), 16), m.group(1), t.group(1) if t else None))
+        ins.append((int(m.group(2), 16), m.group(1), t.group(1) if t else None, 4 if m.group(4) is None else 8))
     base = ins[0][0]
     loops = []
-    for k, (a, t, tgt) in enumerate(ins):
+    for k, (a, t, tgt, _) in enumerate(ins):
         if tgt is not None and t.startswith(("s_cbranch", "s_branch")):
             dst = base + int(tgt, 16)  # objdump prints targets relative to the symbol start
             if dst <= a:
@@ -79,6 +79,7 @@ def count(lib_path: str) -> dict:
     valu = sum(x[1].startswith("v_") for x in loop)
     lds = sum(x[1].startswith("ds_") for x in loop)
     salu = sum(x[1].startswith("s_") for x in loop)
+    nbytes = sum(x[3] for x in loop)
     mix = {}
     for x in loop:
         op = x[1].split()[0]
@@ -86,6 +87,7 @@ def count(lib_path: str) -> dict:
     return {"instruction_mix_per_iteration": dict(sorted(mix.items(), key=lambda kv: -kv[1])),"kernel": KERNEL, "loop_instructions": len(loop), "blocks_per_iteration": blocks,
             "instruction_rounds_per_block": dpp // blocks, "round_valu_per_block": 9 * (dpp // blocks),
             "valu_per_block": valu / blocks, "lds_per_block": lds / blocks, "salu_per_block": salu / blocks,
+            "code_bytes_per_block": nbytes / blocks,
             "issue_cycles_per_valu": 4, "source": "llvm-objdump of the gfx950 code object in " +
             os.path.relpath(lib_path, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))}
 
@@ -95,12 +97,25 @@ def ceiling_mbps(isa: dict, clock_mhz: float) -> float:
     return 64.0 * clock_mhz / (isa["valu_per_block"] * isa["issue_cycles_per_valu"])
 
 
+# A lone wave's instruction stream, measured (tools/micro/vopcost.hip,
+# profiles/r02/micro_vop_encoding_cost.txt): 8-byte encodings -- VOP3, DPP, and even a
+# VOP2 or VOP1 carrying a 32-bit literal -- issue every 4.64 cycles, 4-byte VOP2 every
+# 4.16, whatever the operands: the wave is fed about 8 B of code per 4.64 cycles.
+FETCH_BYTES_PER_CYCLE = 8 / 4.64
+
+
+def fetch_ceiling_mbps(isa: dict, clock_mhz: float) -> float:
+    """Per-stream ceiling set by the consumer loop's code bytes at the measured fetch rate."""
+    return 64.0 * clock_mhz / (isa["code_bytes_per_block"] / FETCH_BYTES_PER_CYCLE)
+
+
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     lib = args[0] if args else os.path.join(root, "kraken_amd", "lib", "libkraken_hip.so")
     res = count(lib)
     res["ceiling_per_stream_MBps_at_2400MHz"] = round(ceiling_mbps(res, 2400.0), 3)
+    res["fetch_ceiling_per_stream_MBps_at_2400MHz"] = round(fetch_ceiling_mbps(res, 2400.0), 3)
     print(json.dumps(res, indent=1))
     if "--json" in sys.argv:
         out = sys.argv[sys.argv.index("--json") + 1]
