@@ -54,13 +54,13 @@ M64 = (1 << 64) - 1
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def sha_isa_ceiling(D, launch):
+def sha_isa_ceiling(D, launch, lanes):
     """(isa counts, clock MHz, per-stream ceiling MB/s); launch() starts one SHA-256
     batch asynchronously, the clock is read while it runs."""
     import ctypes as C
     import sha_isa
     try:
-        isa = sha_isa.count(D.lib._name)
+        isa = sha_isa.count(D.lib._name, lanes)
     except Exception as e:  # tools missing on the box: report, never guess
         return {"error": f"{type(e).__name__}: {e}"}, None, None
     s = C.c_void_p()
@@ -253,8 +253,8 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
             "algorithmic_bytes_per_launch": bytes_launch,
             "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5)}}
     ib = {"achieved_per_stream_MBps": round(per_stream, 2), "streams": n, "lanes_per_stream": lanes}
-    if lanes == 2 and not a.no_ceiling:
-        isa, mhz, ceil = sha_isa_ceiling(D, launch)
+    if lanes in (2, 8) and not a.no_ceiling:
+        isa, mhz, ceil = sha_isa_ceiling(D, launch, lanes)
         if ceil:
             ib.update({"ceiling_per_stream_MBps": round(ceil, 2), "frac": round(per_stream / ceil, 4),
                        "clock_mhz": round(mhz, 1), "valu_per_block": isa["valu_per_block"],
@@ -277,10 +277,11 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
         else:
             ib["ceiling_error"] = isa.get("error")
     roof["issue_bound"] = ib
-    roof["note"] = ("bound 'valu': SHA-256 is one sequential Merkle-Damgard chain per blob (two lanes each here), so "
-                    "the kernel is bound by the per-stream VALU issue of its consumer waves (32 of the chip's 1,024 "
-                    "SIMDs for 1,000 streams), not by HBM; peak = streams x ISA per-stream ceiling, hbm.frac beside "
-                    "it (DESIGN.md 4.2)")
+    waves = -(-n // (64 // lanes)) if lanes in (2, 8) else -(-n // 64)
+    roof["note"] = (f"bound 'valu': SHA-256 is one sequential Merkle-Damgard chain per blob ({lanes} lane(s) each "
+                    f"here), so the kernel is bound by the per-stream VALU issue of its consumer waves ({waves} of the "
+                    f"chip's 1,024 SIMDs for {n:,} streams), not by HBM; peak = streams x ISA per-stream ceiling, "
+                    "hbm.frac beside it; fetch_bound = the same loop priced by its code bytes (DESIGN.md 4.2)")
     return roof
 
 

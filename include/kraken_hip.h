@@ -369,21 +369,23 @@ int krk_device_clock_mhz(void* stream, double* mhz);
 int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms);
 int krk_reset_kernel_stats(void);
 
-/* SHA-256 launch plan: lanes per stream (1 or 2) the library uses for a batch of
- * n_streams streams on the current device (two lanes while the batch leaves SIMDs
- * idle: fewer than one two-lane workgroup per CU).  Diagnostic; bench.py prices
- * the per-stream issue ceiling of that plan. */
+/* SHA-256 launch plan: lanes per stream (1, 2 or 8) the library uses for a batch of
+ * n_streams streams on the current device (more lanes a stream -- a shorter chain a
+ * block -- while the batch leaves SIMDs idle).  Diagnostic; bench.py prices the
+ * per-stream issue ceiling of that plan. */
 int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes);
 
-/* SHA-256 launch plan, process-wide (default AUTO: two lanes per stream while the
- * batch leaves SIMDs idle, then two producer/consumer pairs per workgroup, then one
- * lane).  Every plan is bit-exact; the knob exists for tests and tuning.  The
+/* SHA-256 launch plan, process-wide (default AUTO: eight lanes per stream while the
+ * batch leaves SIMDs idle, then two lanes, then two producer/consumer pairs per
+ * workgroup, then one lane).  Every plan is bit-exact; the knob exists for tests and tuning.  The
  * environment variable KRK_SHA_PLAN, read once at the first launch, sets the same. */
 #define KRK_SHA_PLAN_AUTO 0
 #define KRK_SHA_PLAN_1LANE 1        /* one lane per stream, one pair per workgroup */
 #define KRK_SHA_PLAN_2LANE 2        /* two lanes per stream, one pair per workgroup */
 #define KRK_SHA_PLAN_1LANE_2PAIR 3  /* one lane, two pairs per 4-wave workgroup */
 #define KRK_SHA_PLAN_2LANE_2PAIR 4  /* two lanes, two pairs per workgroup */
+#define KRK_SHA_PLAN_8LANE 5        /* eight lanes per stream, one pair per workgroup */
+#define KRK_SHA_PLAN_8LANE_2PAIR 6  /* eight lanes, two pairs per workgroup */
 int krk_set_sha_plan(int plan);
 
 #ifdef __cplusplus

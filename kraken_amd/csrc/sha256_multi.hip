@@ -325,8 +325,8 @@ __device__ __forceinline__ void produce_step(const ShaJob& job, uint32_t b, uint
     } else {
         fetch(job, ob + 2 * kStep, next, safe);
     }
-    // one lane per stream: block ob in slot ob % kNs; two: slot (ob / 2) % kRing2
-    const uint32_t base = kStep == 2 ? kw_base((ob >> 1) % (kNs / 2), col) : kw_base(ob % kNs, col);
+    // one slot a step: block ob in slot (ob / kStep) % (kNs / kStep) (ob - b < kStep)
+    const uint32_t base = kw_base((ob / kStep) % (kNs / kStep), col);
     if (act) build<kNs>(job, ob, use, base, lds);
 }
 
@@ -454,18 +454,58 @@ struct TwoLaneConst {
       [R0] "+v"(R0), [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
 #define KRK_SHA2_CONSTS [r1] "v"(c.r1), [r2] "v"(c.r2), [r3] "v"(c.r3), [ma] "v"(c.ma)
 
+// ---------------------------------------------------------------------------
+// Eight lanes per stream.  Four of the two-lane round's nine instructions compute
+// Sigma (three v_alignbit rotations + an xor3).  Here a stream has an E quad and an
+// A quad of lanes: the three active lanes of a quad carry the same history and each
+// rotates by ONE of the three Sigma amounts (r1 per lane), and two quad_perm DPP
+// xors combine the three rotations so every active lane ends with the full Sigma:
+// eight instructions a round (one v_alignbit + two DPP xors in place of three
+// v_alignbit + the xor3), all 8-byte encodings, whose fetch sets the pace of a lone
+// wave (tools/micro/sha8lane.hip: 2,684 vs 2,920 cycles a block, bit-exact).  The
+// rest is the two-lane round: k / F (Maj or Ch), z for the next round, one cross
+// add P = partner's x1 + z, x0' = S + F + P, the A quad two rounds behind the E quad.
+// Lane layout: in each DPP row of 16 lanes quads 0 / 1 are the E quads of streams
+// 2r / 2r + 1 and quads 2 / 3 their A quads, so row_ror:8 pairs E with A; lane 3 of
+// each quad rotates once and its state is never read.  8 streams a wave.  The first
+// DPP xor reads t1 three instructions after it is written (two wait states needed),
+// the cross add reads a register written a round earlier.
+#define KRK_SHA8_ROUND(X0, X1, X2, NX, WN)                                                   \
+    "v_alignbit_b32 %[t1], %[" #X0 "], %[" #X0 "], %[r1]\n\t"                               \
+    "v_bitop3_b32 %[k], %[" #X0 "], %[" #X1 "], %[ma] bitop3:0x2d\n\t"                      \
+    "v_bitop3_b32 %[k], %[k], %[" #X2 "], %[" #X1 "] bitop3:0xca\n\t"                       \
+    "v_xor_b32_dpp %[t2], %[t1], %[t1] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"  \
+    "v_xor_b32_dpp %[t2], %[t1], %[t2] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"  \
+    "v_add_u32_dpp %[p], %[" #X1 "], %[z] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"          \
+    "v_xad_u32 %[z], %[" #X2 "], %[ma], %[" #WN "]\n\t"                                     \
+    "v_add3_u32 %[" #NX "], %[t2], %[k], %[p]\n\t"
+#define KRK_SHA8_OPERANDS                                                                    \
+    : [t1] "=&v"(t1), [t2] "=&v"(t2), [k] "=&v"(kk), [p] "=&v"(p), [z] "+v"(z), [R0] "+v"(R0), \
+      [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
+#define KRK_SHA8_CONSTS [r1] "v"(c.r1), [ma] "v"(c.ma)
+
 // Instruction-rounds 4q..4q+3; W of rounds 4q+1..4q+4 (for the z's).  History
 // registers rotate: in instruction-round n, x0 = R[n%4], x3 = R[(n+1)%4].
+template <int kL>
 __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
                                           const TwoLaneConst& c, uint32_t w1, uint32_t w2, uint32_t w3,
                                           uint32_t w4) {
     uint32_t t1, t2, t3, kk, p;
-    asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
-                 KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
-                 KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
-                 KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
-                 KRK_SHA2_OPERANDS
-                 : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
+    if constexpr (kL == 8)
+        asm volatile(KRK_SHA8_ROUND(R0, R3, R2, R1, w1)
+                     KRK_SHA8_ROUND(R1, R0, R3, R2, w2)
+                     KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
+                     KRK_SHA8_ROUND(R3, R2, R1, R0, w4)
+                     KRK_SHA8_OPERANDS
+                     : KRK_SHA8_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
+    else
+        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
+                     KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                     KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
+    (void)t3;
 }
 
 // The 64 rounds of one block on a lane pair: 66 instruction-rounds (the A lane
@@ -485,12 +525,13 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 #endif
 constexpr int kAhead = KRK_SHA_AHEAD;
 static_assert(kAhead >= 2 && kAhead <= 8, "read-ahead distance");
+template <int kL>
 __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
                                         uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[kAhead]) {
     // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
     // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
     // its own starts, so A starts at (H2, H3) and its two results are replaced by
-    // H1 and H0.
+    // H1 and H0.  kL = 2 or 8 lanes a stream (KRK_SHA2_ROUND / KRK_SHA8_ROUND).
     uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z;
     // W ring: quad q lives in wq[q % kRS]
     constexpr int kRS = kAhead + 1;
@@ -504,27 +545,46 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
 #endif
     {
         uint32_t t1, t2, t3, kk, p;
-        // s_nop 0 + the xad: two wait states before the DPP read of R3.
-        asm volatile("s_nop 0\n\t"
-                     "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
-                     KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
+        if constexpr (kL == 8)  // the round's DPP reads come five instructions in: no s_nop
+            asm volatile("v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
+                         KRK_SHA8_ROUND(R0, R3, R2, R1, w1)
+                         KRK_SHA8_OPERANDS
+                         : KRK_SHA8_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
+        else  // s_nop 0 + the xad: two wait states before the DPP read of R3.
+            asm volatile("s_nop 0\n\t"
+                         "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
+                         KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
+                         KRK_SHA2_OPERANDS
+                         : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
+        (void)t3;
     }
     R1 = is_e ? R1 : h[3];
     {
         uint32_t t1, t2, t3, kk, p;
-        asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
+        if constexpr (kL == 8)
+            asm volatile(KRK_SHA8_ROUND(R1, R0, R3, R2, w2)
+                         KRK_SHA8_OPERANDS
+                         : KRK_SHA8_CONSTS, [w2] "v"(k[0][2]));
+        else
+            asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                         KRK_SHA2_OPERANDS
+                         : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
+        (void)t3;
     }
     R2 = is_e ? R2 : h[2];
     {
         uint32_t t1, t2, t3, kk, p;
-        asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
-                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
+        if constexpr (kL == 8)
+            asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
+                         KRK_SHA8_ROUND(R3, R2, R1, R0, w4)
+                         KRK_SHA8_OPERANDS
+                         : KRK_SHA8_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
+        else
+            asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                         KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
+                         KRK_SHA2_OPERANDS
+                         : KRK_SHA2_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
+        (void)t3;
     }
 #pragma unroll
     for (int q = 1; q < 16; ++q) {
@@ -541,17 +601,24 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
         if (q >= 16 - kAhead)
             k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
         const u32x4& cur = wq[q % kRS];
-        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : c.one_a);
+        sha2_quad<kL>(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : c.one_a);
     }
     // Instruction-rounds 64, 65: A runs rounds 62, 63 into T1, T2 (W = 1 on A lanes);
     // the E lanes' registers keep their final state.
     uint32_t T1, T2;
     {
         uint32_t t1, t2, t3, kk, p;
-        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
-                     KRK_SHA2_ROUND(T1, R0, R3, T2, w)
-                     KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
-                     : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
+        if constexpr (kL == 8)
+            asm volatile(KRK_SHA8_ROUND(R0, R3, R2, T1, w)
+                         KRK_SHA8_ROUND(T1, R0, R3, T2, w)
+                         KRK_SHA8_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
+                         : KRK_SHA8_CONSTS, [w] "v"(c.one_a));
+        else
+            asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
+                         KRK_SHA2_ROUND(T1, R0, R3, T2, w)
+                         KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
+                         : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
+        (void)t3;
     }
     // E: (e, f, g, h) = (R0, R3, R2, R1); A: (a, b, c, d) = (T2, T1, R0, R3) into
     // its (H2, H3, H0, H1) order.
@@ -562,6 +629,8 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
 }
 #undef KRK_SHA2_OPERANDS
 #undef KRK_SHA2_CONSTS
+#undef KRK_SHA8_OPERANDS
+#undef KRK_SHA8_CONSTS
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
@@ -683,7 +752,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             uint32_t x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = h[k];
-            rounds2(x, ring, cur, nxt, lane, c, is_e, kq);
+            rounds2<2>(x, ring, cur, nxt, lane, c, is_e, kq);
             if (i < common) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) h[k] = x[k];
@@ -802,11 +871,154 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     }
 }
 
+// Eight lanes per stream (KRK_SHA8_ROUND above): a workgroup holds kGroups
+// producer/consumer pairs over 8 streams each.  The producer's 64 lanes build 64
+// different blocks per step -- lane p block b + p / 8 of stream p % 8 -- into its own
+// column of the step's ring slot, so a step is 8 blocks a stream and the pair passes
+// one barrier per 8 blocks (the producer runs 1/8 of the time it did with two lanes a
+// stream, where a step was 2 blocks).  Ring: 3 slots of one step + the all-1 slot the
+// A quads read W from, 64 KiB a pair.  The consumer's E quad of stream s reads block
+// jj of a slot at column jj * 8 + s (every active lane of the quad the same address:
+// an LDS broadcast), its A quad the all-1 slot.
+// kTiming 1 (diagnostic build only, WRONG digests): the producer returns at once and
+// the consumer runs its rounds on whatever the ring holds with no barriers -- the
+// consumer's own time per block.
+template <int kTiming, int kGroups>
+__global__ void __launch_bounds__(128 * kGroups)
+sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __restrict__ out_digest,
+                 uint32_t* __restrict__ out_state) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ring_all[];
+    constexpr int kStep8 = 8, kRing8 = 3, kNs = kStep8 * kRing8;
+    constexpr uint32_t kPer = 8;  // streams per pair
+    constexpr uint32_t kRingWords = uint32_t(kRing8 + 1) * kSlotWords;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const bool producer = wave < (uint32_t)kGroups;
+    const uint32_t grp = wave % kGroups;
+    uint32_t* ring = ring_all + grp * kRingWords;
+    const uint32_t sbase = blockIdx.x * kPer * kGroups;
+    const uint32_t quad = (lane >> 2) & 3;
+    const uint32_t me = producer ? (lane & 7) : (lane >> 4) * 2 + (quad & 1);
+    const uint32_t j = sbase + grp * kPer + me;
+    const bool live = j < n_jobs;
+    ShaJob job{};
+    if (live) job = jobs[j];
+    const uint32_t mine = live ? job_blocks(job) : 0u;
+    uint32_t nb = 0;
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const uint32_t jj = sbase + g * kPer + me;
+        if (jj < n_jobs) nb = max(nb, g == (int)grp ? mine : job_blocks(jobs[jj]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, off, 64));
+    nb = __builtin_amdgcn_readfirstlane(nb);
+
+    if (producer && kTiming == 1) return;
+    if (producer) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) *reinterpret_cast<u32x4*>(ring + kw_index(kRing8, q, lane)) = u32x4{1u, 1u, 1u, 1u};
+        u32x4 R0[kRaw], R1[kRaw], R2[kRaw];
+        const uint64_t safe = reinterpret_cast<uint64_t>(jobs);
+        const uint32_t par = lane >> 3;  // this lane's block within a step
+        uint32_t passed = 0;
+        fetch(job, par, R0, safe);
+        fetch(job, par + kStep8, R1, safe);
+        for (uint32_t b = 0; b < nb; b += 3 * kStep8) {
+            produce_step<kNs, kStep8>(job, b, b + par, nb, lane, ring, R0, R2, safe, passed);
+            produce_step<kNs, kStep8>(job, b + kStep8, b + kStep8 + par, nb, lane, ring, R1, R0, safe, passed);
+            produce_step<kNs, kStep8>(job, b + 2 * kStep8, b + 2 * kStep8 + par, nb, lane, ring, R2, R1, safe, passed);
+        }
+        while (passed < (nb + kStep8 - 1) / kStep8) {
+            __syncthreads();
+            ++passed;
+        }
+        return;
+    }
+    const bool is_e = quad < 2;
+    const uint32_t pos = lane & 3;
+    const uint32_t half = is_e ? 4u : 0u;
+    // this lane's Sigma rotation: E quads Sigma1 (6, 11, 25), A quads Sigma0 (2, 13, 22)
+    const uint32_t r1 = is_e ? (pos == 1 ? 11u : pos == 2 ? 25u : 6u) : (pos == 1 ? 13u : pos == 2 ? 22u : 2u);
+    const TwoLaneConst c{r1, 0u, 0u, is_e ? 0u : ~0u, is_e ? 0u : 1u};
+    uint32_t h[4];  // H[4 + k] on E lanes, H[k ^ 2] on A lanes (rounds2's register order)
+    if (live && (job.flags & kShaFromState)) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = out_state[8 * (uint64_t)job.out + half + (is_e ? k : k ^ 2)];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = is_e ? job.h[4 + k] : job.h[k ^ 2];
+    }
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t common = wave_min(live ? mine : ~0u);
+    // Word offsets: E lanes read block jj of ring slot sl at column jj * 8 + me, i.e.
+    // lbase + sl * kSlotWords + jj * 32; A lanes always the all-1 slot.
+    const uint32_t lbase = is_e ? me * 4u : uint32_t(kRing8) * kSlotWords;
+    const uint32_t binc = is_e ? 32u : 0u, sinc = is_e ? uint32_t(kSlotWords) : 0u;
+    // voff: this lane's offset of block i (E: slot base vslot + jj * 32; A: 0)
+    uint32_t voff = 0, vslot = 0, slot = 0;
+    u32x4 kq[kAhead] = {};
+    auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = h[k];
+        rounds2<8>(x, ring, cur, nxt, lane, c, is_e, kq);
+        if (i < common) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[k] = x[k];
+        } else if (i < mine) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[k] = x[k];
+        }
+    };
+    // Two blocks an iteration (a step's 8 blocks never straddle an iteration).
+    for (uint32_t i = 0; i < nb; i += 2) {
+        const uint32_t jj = i & (kStep8 - 1);
+        if (jj == 0) {
+            if (kTiming == 0) __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (i == 0) {
+#pragma unroll
+                for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + lbase + 256 * q);
+            }
+        }
+        const bool last = jj == kStep8 - 2;
+        const uint32_t nvslot = slot == kRing8 - 1 ? 0u : vslot + sinc;
+        const uint32_t o1 = voff + binc, o2 = last ? nvslot : o1 + binc;
+        block(i, lbase + voff, lbase + o1);
+        if (i + 1 < nb) block(i + 1, lbase + o1, lbase + o2);
+        voff = o2;
+        if (last) {
+            slot = slot == kRing8 - 1 ? 0u : slot + 1;
+            vslot = nvslot;
+        }
+    }
+    if (live && pos == 0) {
+        uint32_t hs[4];  // back to H order
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hs[k] = is_e ? h[k] : h[k ^ 2];
+        if (job.flags & kShaFinal) {
+            uint8_t* o = out_digest + 32 * (uint64_t)job.out + 4 * half;
+            if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+                reinterpret_cast<uint4*>(o)[0] = make_uint4(bswap(hs[0]), bswap(hs[1]), bswap(hs[2]), bswap(hs[3]));
+            } else {
+                for (int k = 0; k < 16; ++k) o[k] = (uint8_t)(hs[k >> 2] >> (24 - 8 * (k & 3)));
+            }
+        } else {
+            uint32_t* o = out_state + 8 * (uint64_t)job.out + half;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = hs[k];
+        }
+    }
+}
+
 // Launch plans.  Production (every plan bit-exact):
 //   KRK_SHA_PLAN_1LANE        one lane per stream, one producer/consumer pair per workgroup
 //   KRK_SHA_PLAN_2LANE        two lanes per stream, one pair per workgroup
 //   KRK_SHA_PLAN_1LANE_2PAIR  one lane, two pairs per 4-wave workgroup
 //   KRK_SHA_PLAN_2LANE_2PAIR  two lanes, two pairs per workgroup
+//   KRK_SHA_PLAN_8LANE        eight lanes per stream (sha256_w8_kernel), one pair per workgroup
+//   KRK_SHA_PLAN_8LANE_2PAIR  eight lanes, two pairs per workgroup
 //   KRK_SHA_PLAN_AUTO         auto_plan() below
 // The plan is process-wide state set by krk_set_sha_plan (or KRK_SHA_PLAN read once,
 // at the first launch); it is not re-read per launch.  The timing diagnostics
@@ -827,9 +1039,9 @@ static int sha_plan() {
 }
 
 bool sha_plan_valid(int p) {
-    if (p >= KRK_SHA_PLAN_AUTO && p <= KRK_SHA_PLAN_2LANE_2PAIR) return true;
+    if (p >= KRK_SHA_PLAN_AUTO && p <= KRK_SHA_PLAN_8LANE_2PAIR) return true;
 #ifdef KRK_DIAG
-    return p >= 100 && p <= 107;
+    return p >= 100 && p <= 108;
 #else
     return false;
 #endif
@@ -855,10 +1067,13 @@ static uint32_t device_cus() {
 }
 static uint32_t two_lane_max_streams() { return device_cus() * 64u; }
 
-// Automatic plan: two lanes, one pair per workgroup (a workgroup per CU) up to
-// 32 x CUs streams; two lanes, two pairs per workgroup up to 64 x CUs; one lane, two
-// pairs per workgroup beyond.
+// Automatic plan: eight lanes a stream up to 16 x CUs streams (two 64 KiB pairs per
+// CU; at 4,096 streams 52.6 MB/s a stream vs 49.8 with two lanes, at 8,192 the
+// eight-lane grid runs in two waves of workgroups and halves, tools/probe_perf.py);
+// two lanes, one pair per workgroup up to 32 x CUs; two lanes, two pairs per
+// workgroup up to 64 x CUs; one lane, two pairs per workgroup beyond.
 static int auto_plan(uint32_t n_jobs) {
+    if (n_jobs <= device_cus() * 16u) return KRK_SHA_PLAN_8LANE;
     if (n_jobs <= device_cus() * 32u) return KRK_SHA_PLAN_2LANE;
     return n_jobs <= two_lane_max_streams() ? KRK_SHA_PLAN_2LANE_2PAIR : KRK_SHA_PLAN_1LANE_2PAIR;
 }
@@ -873,7 +1088,30 @@ static bool plan_two_lanes(int p) {
            p == 107;
 }
 
-int sha_lanes_for(uint32_t n_jobs) { return plan_two_lanes(resolve_plan(n_jobs)) ? 2 : 1; }
+static bool plan_eight_lanes(int p) { return p == KRK_SHA_PLAN_8LANE || p == KRK_SHA_PLAN_8LANE_2PAIR || p == 108; }
+
+int sha_lanes_for(uint32_t n_jobs) {
+    const int p = resolve_plan(n_jobs);
+    return plan_eight_lanes(p) ? 8 : plan_two_lanes(p) ? 2 : 1;
+}
+
+template <int kTiming, int kGroups>
+static hipError_t launch_w8(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest, uint32_t* out_state,
+                            hipStream_t s) {
+    constexpr size_t lds = size_t(kGroups) * 4 * kSlotWords * 4;  // 3 ring slots + the all-1 slot: 64 KiB a pair
+    auto* k = &sha256_w8_kernel<kTiming, kGroups>;
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [k] {
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    });
+    if (attr_err != hipSuccess) return attr_err;
+    constexpr uint32_t per = 8u * kGroups;
+    hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * kGroups), lds, s, jobs, n_jobs, out_digest,
+                       out_state);
+    return hipGetLastError();
+}
 
 template <int kTiming, bool kTwo, int kGroups>
 static hipError_t launch_ws(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest, uint32_t* out_state,
@@ -901,6 +1139,8 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
         case KRK_SHA_PLAN_2LANE: return launch_ws<0, true, 1>(jobs, n_jobs, out_digest, out_state, s);
         case KRK_SHA_PLAN_1LANE_2PAIR: return launch_ws<0, false, 2>(jobs, n_jobs, out_digest, out_state, s);
         case KRK_SHA_PLAN_2LANE_2PAIR: return launch_ws<0, true, 2>(jobs, n_jobs, out_digest, out_state, s);
+        case KRK_SHA_PLAN_8LANE: return launch_w8<0, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case KRK_SHA_PLAN_8LANE_2PAIR: return launch_w8<0, 2>(jobs, n_jobs, out_digest, out_state, s);
 #ifdef KRK_DIAG
         // diagnostics (WRONG digests except 100): rounds-only consumer (102 one lane, 104 two
         // lanes), producer-only (105 / 106), producer without global loads (107)
@@ -915,6 +1155,7 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
         case 105: return launch_ws<2, false, 1>(jobs, n_jobs, out_digest, out_state, s);
         case 106: return launch_ws<2, true, 1>(jobs, n_jobs, out_digest, out_state, s);
         case 107: return launch_ws<3, true, 1>(jobs, n_jobs, out_digest, out_state, s);
+        case 108: return launch_w8<1, 1>(jobs, n_jobs, out_digest, out_state, s);  // eight-lane rounds only
 #endif
         default: return hipErrorInvalidValue;
     }

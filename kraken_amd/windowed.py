@@ -57,15 +57,16 @@ def window_plan(lens, W, cap):
 
 
 def two_lane_stream_cap(D, n):
-    """Largest stream count <= n whose SHA launch plan is two lanes per stream."""
-    if n == 0 or D.sha_lanes_per_stream(n) == 2:
+    """Largest stream count <= n whose SHA launch plan runs a stream on more than one
+    lane (eight or two lanes per stream; the one-lane plan's chain is the slowest)."""
+    if n == 0 or D.sha_lanes_per_stream(n) >= 2:
         return max(n, 1)
-    lo, hi = 1, n  # two lanes at lo, one at hi
-    if D.sha_lanes_per_stream(lo) != 2:
+    lo, hi = 1, n  # several lanes at lo, one at hi
+    if D.sha_lanes_per_stream(lo) < 2:
         return n
     while hi - lo > 1:
         mid = (lo + hi) // 2
-        lo, hi = (mid, hi) if D.sha_lanes_per_stream(mid) == 2 else (lo, mid)
+        lo, hi = (mid, hi) if D.sha_lanes_per_stream(mid) >= 2 else (lo, mid)
     return lo
 
 

@@ -171,7 +171,7 @@ def test_production_library_has_no_diagnostic_kernels():
     sha = [k for k in kern if "sha256" in k]
     crc = [k for k in kern if "crc_items_kernel" in k]
     assert sha and crc
-    assert all("sha256_ws_kernel<0," in k for k in sha), sha  # kTiming = 0 only
+    assert all(("sha256_ws_kernel<0," in k or "sha256_w8_kernel<0," in k) for k in sha), sha  # kTiming = 0 only
     assert not any("sha256_multi_kernel" in k for k in kern)
     # crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT>: strided, no load-only, no NT
     assert all(k.split("<")[1].startswith(("32, 4, 1024, false, false, 32, false",

@@ -319,10 +319,10 @@ def sha_plan():
     check(L.krk_set_sha_plan(0))
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 def test_sha_launch_plans_bit_exact(gpu, orc, variant, sha_plan):
-    """Every production SHA-256 plan (KRK_SHA_PLAN_*: one / two lanes per stream; one /
-    two producer-consumer pairs per workgroup) on a batch of mixed lengths and
+    """Every production SHA-256 plan (KRK_SHA_PLAN_*: one / two / eight lanes per
+    stream; one / two producer-consumer pairs per workgroup) on a batch of mixed lengths and
     alignments, one-shot and from midstates (chunked), against hashlib."""
     sha_plan(variant)
     rng = np.random.default_rng(int(variant))

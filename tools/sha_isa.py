@@ -22,11 +22,15 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNEL = "sha256_ws_kernel<0, true, 1>"
+KERNEL = "sha256_ws_kernel<0, true, 1>"  # two lanes per stream
+KERNELS = {2: KERNEL, 8: "sha256_w8_kernel<0, 1>"}
+# the one cross-lane add of every instruction-round, and the VALU ops of a round
+ROUND_MARK = {2: "row_mirror", 8: "row_ror:8"}
+ROUND_OPS = {2: 9, 8: 8}
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
-def _disasm(lib_path: str) -> str:
+def _disasm(lib_path: str, kernel: str = KERNEL) -> str:
     with tempfile.TemporaryDirectory() as td:
         fb = os.path.join(td, "fatbin.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", lib_path, os.devnull],
@@ -44,14 +48,15 @@ def _disasm(lib_path: str) -> str:
                 continue
             s = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--demangle", o], check=True, capture_output=True,
                                text=True).stdout
-            if KERNEL in s:
+            if kernel in s:
                 return s
-    raise RuntimeError(f"{KERNEL} not found in {lib_path}")
+    raise RuntimeError(f"{kernel} not found in {lib_path}")
 
 
-def count(lib_path: str) -> dict:
-    lines = _disasm(lib_path).splitlines()
-    head = [i for i, l in enumerate(lines) if l.endswith(">:") and KERNEL in l][0]
+def count(lib_path: str, lanes: int = 2) -> dict:
+    kernel, mark = KERNELS[lanes], ROUND_MARK[lanes]
+    lines = _disasm(lib_path, kernel).splitlines()
+    head = [i for i, l in enumerate(lines) if l.endswith(">:") and kernel in l][0]
     nxt = [i for i, l in enumerate(lines) if i > head and l.endswith(">:")]
     body = lines[head + 1:nxt[0] if nxt else len(lines)]
     ins = []  # (address, text, branch target or None)
@@ -71,9 +76,9 @@ def count(lib_path: str) -> dict:
                 loops.append(loop)
     # the consumer's step loop: the shortest loop holding the most rounds (an inner
     # back-edge that re-runs only part of a step does not count as the step)
-    most = max(sum("row_mirror" in x[1] for x in lp) for lp in loops)
-    loop = min((lp for lp in loops if sum("row_mirror" in x[1] for x in lp) == most), key=len)
-    dpp = sum("row_mirror" in x[1] for x in loop)
+    most = max(sum(mark in x[1] for x in lp) for lp in loops)
+    loop = min((lp for lp in loops if sum(mark in x[1] for x in lp) == most), key=len)
+    dpp = sum(mark in x[1] for x in loop)
     blocks = dpp // 66
     assert blocks >= 1 and dpp == 66 * blocks, dpp
     valu = sum(x[1].startswith("v_") for x in loop)
@@ -84,8 +89,8 @@ def count(lib_path: str) -> dict:
     for x in loop:
         op = x[1].split()[0]
         mix[op] = mix.get(op, 0) + 1
-    return {"instruction_mix_per_iteration": dict(sorted(mix.items(), key=lambda kv: -kv[1])),"kernel": KERNEL, "loop_instructions": len(loop), "blocks_per_iteration": blocks,
-            "instruction_rounds_per_block": dpp // blocks, "round_valu_per_block": 9 * (dpp // blocks),
+    return {"instruction_mix_per_iteration": dict(sorted(mix.items(), key=lambda kv: -kv[1])),"kernel": kernel, "lanes_per_stream": lanes, "loop_instructions": len(loop), "blocks_per_iteration": blocks,
+            "instruction_rounds_per_block": dpp // blocks, "round_valu_per_block": ROUND_OPS[lanes] * (dpp // blocks),
             "valu_per_block": valu / blocks, "lds_per_block": lds / blocks, "salu_per_block": salu / blocks,
             "code_bytes_per_block": nbytes / blocks,
             "issue_cycles_per_valu": 4, "source": "llvm-objdump of the gfx950 code object in " +
@@ -111,9 +116,11 @@ def fetch_ceiling_mbps(isa: dict, clock_mhz: float) -> float:
 
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
+    lanes = int(argv[argv.index("--lanes") + 1]) if "--lanes" in argv else 2
+    args = [a for i, a in enumerate(argv) if not a.startswith("--") and (i == 0 or argv[i - 1] not in ("--lanes", "--json"))]
     lib = args[0] if args else os.path.join(root, "kraken_amd", "lib", "libkraken_hip.so")
-    res = count(lib)
+    res = count(lib, lanes)
     res["ceiling_per_stream_MBps_at_2400MHz"] = round(ceiling_mbps(res, 2400.0), 3)
     res["fetch_ceiling_per_stream_MBps_at_2400MHz"] = round(fetch_ceiling_mbps(res, 2400.0), 3)
     print(json.dumps(res, indent=1))
