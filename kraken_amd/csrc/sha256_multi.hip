@@ -524,6 +524,9 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 #define KRK_SHA_AHEAD 3
 #endif
 constexpr int kAhead = KRK_SHA_AHEAD;
+#ifndef KRK_SHA8_UNROLL
+#define KRK_SHA8_UNROLL 2  // eight-lane consumer: blocks per loop iteration
+#endif
 static_assert(kAhead >= 2 && kAhead <= 8, "read-ahead distance");
 template <int kL>
 __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
@@ -629,6 +632,121 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
 }
 #undef KRK_SHA2_OPERANDS
 #undef KRK_SHA2_CONSTS
+
+// Eight lanes a stream, blocks pipelined: the A quad runs rounds 62, 63 of block i
+// while the E quad already runs rounds 0, 1 of block i + 1, so a block costs 64
+// instruction-rounds instead of 66.  State crosses blocks in registers: R0..R3 (the
+// history, same register roles as rounds2), z, and each half's chaining value hE
+// (E quads: H4..H7, 0 on A lanes) / hA (A quads: H2, H3, H0, H1, 0 on E lanes) --
+// masked to its own quad so that one unmasked add feeds one half forward and adds 0
+// to the other.  Per block (instruction-rounds n = 2 .. 65 of block i):
+//   n = 2 .. 63: both halves (E round n, A round n - 2);
+//   F1 (E finished block i): R += hE (E's feed-forward); E's round 0 of block i + 1
+//      reads d through the cross add as A's raw a61, so its z also takes the A
+//      half's H3 (partner's hA[1], via DPP) and the feed-forward of h (hE[3]); A's
+//      rounds 62, 63 read e63, e64 through the cross add from registers E has just
+//      fed forward, so A's z gives back H5 now and H4 after n = 64;
+//      hE <- R where i < this stream's block count;
+//   n = 64: E round 0 of block i + 1 (W = its KW0 .. KW1), A round 62;
+//   F2: E's round 1 reads raw a62 as d: z += partner's hA[0] (H2); A: z -= H4
+//      (both in one register cc formed in F1);
+//   n = 65: E round 1, A round 63;
+//   F3 (A finished block i): A's round 0 of block i + 1 takes -d from z formed on raw
+//      a61: z -= hA[1]; R += hA; hA <- R where i < the block count.
+// A finished stream's lanes keep computing on garbage; their hE / hA stay frozen.
+__device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                        uint32_t hE[4], uint32_t hA[4], uint32_t mineE, uint32_t mineA,
+                                        uint32_t i, const uint32_t* lds, uint32_t cbase, uint32_t nbase,
+                                        const TwoLaneConst& c, u32x4 k[kAhead]) {
+    constexpr int kRS = kAhead + 1;
+    u32x4 wq[kRS];
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) wq[j] = k[j];
+    wq[kAhead] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * kAhead);
+    {
+        uint32_t t1, t2, kk, p;
+        asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
+                     KRK_SHA8_ROUND(R3, R2, R1, R0, w4)
+                     : [t1] "=&v"(t1), [t2] "=&v"(t2), [k] "=&v"(kk), [p] "=&v"(p), [z] "+v"(z), [R0] "+v"(R0),
+                       [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
+                     : KRK_SHA8_CONSTS, [w3] "v"(wq[0][3]), [w4] "v"(wq[1][0]));
+    }
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+        if (q + kAhead < 16)
+            wq[(q + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + kAhead));
+        if (q >= 16 - kAhead)
+            k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
+        const u32x4& cur = wq[q % kRS];
+        sha2_quad<8>(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : k[0][0]);
+    }
+    {
+        // F1, n = 64, F2, n = 65, F3.  The cross terms go through one DPP each: every
+        // lane forms hA - hE of its own (E lanes: -hE, A lanes: hA) and reads its
+        // partner's, so E picks up the A half's H2 / H3 and A gives back E's H4 / H5.
+        // (v_subrev_u32_dpp swizzles its second operand on gfx950, tools/micro/dppsem.hip,
+        // so it is not used.)  Every VGPR a DPP instruction reads is written at least two
+        // instructions earlier.
+        uint32_t t1, t2, kk, p, cc, dd, c2;
+        asm volatile("v_sub_u32_e32 %[cc], %[a0], %[e0]\n\t"   // own hA0 - hE0
+                     "v_sub_u32_e32 %[dd], %[a1], %[e1]\n\t"   // own hA1 - hE1
+                     "v_add_u32_e32 %[R0], %[e0], %[R0]\n\t"
+                     "v_add_u32_e32 %[R3], %[e1], %[R3]\n\t"
+                     "v_mov_b32_dpp %[c2], %[cc] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"  // E: H2 of A, A: -H4
+                     "v_add_u32_dpp %[z], %[dd], %[z] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"  // E: +H3 of A, A: -H5
+                     "v_add_u32_e32 %[R2], %[e2], %[R2]\n\t"
+                     "v_add_u32_e32 %[R1], %[e3], %[R1]\n\t"
+                     "v_add_u32_e32 %[z], %[e3], %[z]\n\t"
+                     "v_cmp_lt_u32_e32 vcc, %[i], %[mineE]\n\t"
+                     "v_cndmask_b32_e32 %[e0], %[e0], %[R0], vcc\n\t"
+                     "v_cndmask_b32_e32 %[e1], %[e1], %[R3], vcc\n\t"
+                     "v_cndmask_b32_e32 %[e2], %[e2], %[R2], vcc\n\t"
+                     "v_cndmask_b32_e32 %[e3], %[e3], %[R1], vcc\n\t"
+                     KRK_SHA8_ROUND(R0, R3, R2, R1, w1)
+                     "v_add_u32_e32 %[z], %[c2], %[z]\n\t"
+                     KRK_SHA8_ROUND(R1, R0, R3, R2, w2)
+                     "v_sub_u32_e32 %[z], %[z], %[a1]\n\t"
+                     "v_add_u32_e32 %[R0], %[a0], %[R0]\n\t"
+                     "v_add_u32_e32 %[R3], %[a1], %[R3]\n\t"
+                     "v_add_u32_e32 %[R2], %[a2], %[R2]\n\t"
+                     "v_add_u32_e32 %[R1], %[a3], %[R1]\n\t"
+                     "v_cmp_lt_u32_e32 vcc, %[i], %[mineA]\n\t"
+                     "v_cndmask_b32_e32 %[a0], %[a0], %[R0], vcc\n\t"
+                     "v_cndmask_b32_e32 %[a1], %[a1], %[R3], vcc\n\t"
+                     "v_cndmask_b32_e32 %[a2], %[a2], %[R2], vcc\n\t"
+                     "v_cndmask_b32_e32 %[a3], %[a3], %[R1], vcc\n\t"
+                     : [t1] "=&v"(t1), [t2] "=&v"(t2), [k] "=&v"(kk), [p] "=&v"(p), [cc] "=&v"(cc), [dd] "=&v"(dd),
+                       [c2] "=&v"(c2), [z] "+v"(z),
+                       [R0] "+v"(R0), [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3), [e0] "+v"(hE[0]),
+                       [e1] "+v"(hE[1]), [e2] "+v"(hE[2]), [e3] "+v"(hE[3]), [a0] "+v"(hA[0]), [a1] "+v"(hA[1]),
+                       [a2] "+v"(hA[2]), [a3] "+v"(hA[3])
+                     : KRK_SHA8_CONSTS, [w1] "v"(k[0][1]), [w2] "v"(k[0][2]), [i] "s"(i), [mineE] "v"(mineE),
+                       [mineA] "v"(mineA)
+                     : "vcc");
+    }
+}
+
+// Instruction-rounds 0, 1 of a stream's first block (E rounds 0, 1; A idles and its
+// two results are replaced by H1, H0: rounds2's start).
+__device__ __forceinline__ void prologue8p(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                           const uint32_t h[4], bool is_e, const TwoLaneConst& c,
+                                           const u32x4& k0) {
+    {
+        uint32_t t1, t2, kk, p;
+        asm volatile("v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
+                     KRK_SHA8_ROUND(R0, R3, R2, R1, w1)
+                     KRK_SHA8_OPERANDS
+                     : KRK_SHA8_CONSTS, [w0] "v"(k0[0]), [w1] "v"(k0[1]));
+    }
+    R1 = is_e ? R1 : h[3];
+    {
+        uint32_t t1, t2, kk, p;
+        asm volatile(KRK_SHA8_ROUND(R1, R0, R3, R2, w2)
+                     KRK_SHA8_OPERANDS
+                     : KRK_SHA8_CONSTS, [w2] "v"(k0[2]));
+    }
+    R2 = is_e ? R2 : h[2];
+}
 #undef KRK_SHA8_OPERANDS
 #undef KRK_SHA8_CONSTS
 
@@ -958,6 +1076,20 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     // voff: this lane's offset of block i (E: slot base vslot + jj * 32; A: 0)
     uint32_t voff = 0, vslot = 0, slot = 0;
     u32x4 kq[kAhead] = {};
+#ifndef KRK_SHA8_SKEW  // blocks pipelined (block8p): 64 instruction-rounds a block
+    uint32_t hE[4], hA[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        hE[k] = is_e ? h[k] : 0u;
+        hA[k] = is_e ? 0u : h[k];
+    }
+    const uint32_t mineE = is_e ? mine : 0u, mineA = is_e ? 0u : mine;
+    uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z = 0;
+    (void)common;
+    auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
+        block8p(R0, R1, R2, R3, z, hE, hA, mineE, mineA, i, ring, cur, nxt, c, kq);
+    };
+#else  // KRK_SHA8_SKEW (experiment build): 66 instruction-rounds a block (rounds2)
     auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
         uint32_t x[4];
 #pragma unroll
@@ -971,28 +1103,46 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             for (int k = 0; k < 4; ++k) h[k] = x[k];
         }
     };
-    // Two blocks an iteration (a step's 8 blocks never straddle an iteration).
-    for (uint32_t i = 0; i < nb; i += 2) {
+#endif
+    // kU blocks an iteration (a step's 8 blocks never straddle an iteration): one block
+    // an iteration ran at 52.9 MB/s a stream, two at 55.0 (fewer taken branches and
+    // less loop bookkeeping per block).
+    constexpr uint32_t kU = KRK_SHA8_UNROLL;
+    static_assert(kU == 1 || kU == 2 || kU == 4 || kU == 8, "blocks per iteration divide a step");
+    if (nb) {  // step 0's barrier, the first quads, and (pipelined) rounds 0, 1 of block 0
+        if (kTiming == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + lbase + 256 * q);
+#ifndef KRK_SHA8_SKEW
+        prologue8p(R0, R1, R2, R3, z, h, is_e, c, kq[0]);
+#endif
+    }
+    for (uint32_t i = 0; i < nb; i += kU) {
         const uint32_t jj = i & (kStep8 - 1);
-        if (jj == 0) {
+        if (jj == 0 && i) {
             if (kTiming == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            if (i == 0) {
-#pragma unroll
-                for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + lbase + 256 * q);
-            }
         }
-        const bool last = jj == kStep8 - 2;
+        const bool last = jj == kStep8 - kU;
         const uint32_t nvslot = slot == kRing8 - 1 ? 0u : vslot + sinc;
-        const uint32_t o1 = voff + binc, o2 = last ? nvslot : o1 + binc;
-        block(i, lbase + voff, lbase + o1);
-        if (i + 1 < nb) block(i + 1, lbase + o1, lbase + o2);
-        voff = o2;
+        uint32_t o = voff;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t on = (u == kU - 1 && last) ? nvslot : o + binc;
+            if (u == 0 || i + u < nb) block(i + u, lbase + o, lbase + on);
+            o = on;
+        }
+        voff = o;
         if (last) {
             slot = slot == kRing8 - 1 ? 0u : slot + 1;
             vslot = nvslot;
         }
     }
+#ifndef KRK_SHA8_SKEW
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h[k] = is_e ? hE[k] : hA[k];
+#endif
     if (live && pos == 0) {
         uint32_t hs[4];  // back to H order
 #pragma unroll

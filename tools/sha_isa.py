@@ -25,8 +25,9 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 KERNEL = "sha256_ws_kernel<0, true, 1>"  # two lanes per stream
 KERNELS = {2: KERNEL, 8: "sha256_w8_kernel<0, 1>"}
 # the one cross-lane add of every instruction-round, and the VALU ops of a round
-ROUND_MARK = {2: "row_mirror", 8: "row_ror:8"}
+ROUND_MARK = {2: "row_mirror", 8: "quad_perm:[1,2,0,3]"}
 ROUND_OPS = {2: 9, 8: 8}
+ROUNDS_PER_BLOCK = {2: 66, 8: 64}  # the eight-lane consumer pipelines blocks (block8p)
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
@@ -79,8 +80,8 @@ def count(lib_path: str, lanes: int = 2) -> dict:
     most = max(sum(mark in x[1] for x in lp) for lp in loops)
     loop = min((lp for lp in loops if sum(mark in x[1] for x in lp) == most), key=len)
     dpp = sum(mark in x[1] for x in loop)
-    blocks = dpp // 66
-    assert blocks >= 1 and dpp == 66 * blocks, dpp
+    blocks = dpp // ROUNDS_PER_BLOCK[lanes]
+    assert blocks >= 1 and dpp == ROUNDS_PER_BLOCK[lanes] * blocks, dpp
     valu = sum(x[1].startswith("v_") for x in loop)
     lds = sum(x[1].startswith("ds_") for x in loop)
     salu = sum(x[1].startswith("s_") for x in loop)
