@@ -662,7 +662,11 @@ __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2
     u32x4 wq[kRS];
 #pragma unroll
     for (int j = 0; j < kAhead; ++j) wq[j] = k[j];
+#ifdef KRK_SHA_NOLDS
+    wq[kAhead] = u32x4{3u, cbase, 5u, 7u};
+#else
     wq[kAhead] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * kAhead);
+#endif
     {
         uint32_t t1, t2, kk, p;
         asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
@@ -674,9 +678,17 @@ __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2
 #pragma unroll
     for (int q = 1; q < 16; ++q) {
         if (q + kAhead < 16)
+#ifdef KRK_SHA_NOLDS
+            wq[(q + kAhead) % kRS] = u32x4{(uint32_t)q, cbase, 5u, 7u};
+#else
             wq[(q + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + kAhead));
+#endif
         if (q >= 16 - kAhead)
+#ifdef KRK_SHA_NOLDS
+            k[q - (16 - kAhead)] = u32x4{(uint32_t)q, nbase, 5u, 7u};
+#else
             k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
+#endif
         const u32x4& cur = wq[q % kRS];
         sha2_quad<8>(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : k[0][0]);
     }

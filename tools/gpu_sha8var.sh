@@ -4,9 +4,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-    tests/test_gpu_digest_metainfo.py -k "sha or digester" > gpurun_out/sha8_pytest.log 2>&1 || { tail -30 gpurun_out/sha8_pytest.log; exit 1; }
-tail -2 gpurun_out/sha8_pytest.log
+if [ "${TESTS:-1}" = 1 ]; then
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+      tests/test_gpu_digest_metainfo.py -k "sha or digester" > gpurun_out/sha8_pytest.log 2>&1 || { tail -30 gpurun_out/sha8_pytest.log; exit 1; }
+  tail -2 gpurun_out/sha8_pytest.log
+fi
 out=gpurun_out/sha8var.jsonl; : > $out
 for v in prod ${VARS:-skew} prod; do
   lib=kraken_amd/lib/var_$v/libkraken_hip.so; [ $v = prod ] && lib=kraken_amd/lib/libkraken_hip.so
@@ -15,6 +17,7 @@ for v in prod ${VARS:-skew} prod; do
   sed "s/^{/{\"build\": \"$v\", /" gpurun_out/sha8var_$v.log >> $out
 done
 cut -c1-160 $out
+[ "${BENCH:-1}" = 1 ] || exit 0
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 > gpurun_out/sha8_bench.log 2>&1 || { tail -30 gpurun_out/sha8_bench.log; exit 1; }
 python3 -c "
 import json
