@@ -171,6 +171,8 @@ constexpr int kSlots = 4;
 constexpr int kSlots2 = 6;           // two lanes: block positions in the ring ...
 constexpr int kRing2 = kSlots2 / 2;  // ... in 3 slots, two blocks per slot (A / E columns)
 constexpr int kSlotWords = 64 * 64;  // 64 rounds x 64 lanes
+// eight lanes: 1 KiB of 1s past the all-1 slot (the A lanes' column walks one block ahead)
+constexpr uint32_t kOnesPad8 = 256;
 
 // LDS image of one slot: [round/4][lane][4] words -> a lane's 4 consecutive KW
 // are one conflict-free ds_read_b128 / ds_write_b128 across the wave.
@@ -1020,7 +1022,7 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     extern __shared__ __attribute__((aligned(16))) uint32_t ring_all[];
     constexpr int kStep8 = 8, kRing8 = 3, kNs = kStep8 * kRing8;
     constexpr uint32_t kPer = 8;  // streams per pair
-    constexpr uint32_t kRingWords = uint32_t(kRing8 + 1) * kSlotWords;
+    constexpr uint32_t kRingWords = uint32_t(kRing8 + 1) * kSlotWords + kOnesPad8;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
     const bool producer = wave < (uint32_t)kGroups;
@@ -1048,6 +1050,7 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     if (producer) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) *reinterpret_cast<u32x4*>(ring + kw_index(kRing8, q, lane)) = u32x4{1u, 1u, 1u, 1u};
+        *reinterpret_cast<u32x4*>(ring + (kRing8 + 1) * kSlotWords + lane * 4) = u32x4{1u, 1u, 1u, 1u};  // pad
         u32x4 R0[kRaw], R1[kRaw], R2[kRaw];
         const uint64_t safe = reinterpret_cast<uint64_t>(jobs);
         const uint32_t par = lane >> 3;  // this lane's block within a step
@@ -1083,8 +1086,11 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     const uint32_t common = wave_min(live ? mine : ~0u);
     // Word offsets: E lanes read block jj of ring slot sl at column jj * 8 + me, i.e.
     // lbase + sl * kSlotWords + jj * 32; A lanes always the all-1 slot.
-    const uint32_t lbase = is_e ? me * 4u : uint32_t(kRing8) * kSlotWords;
-    const uint32_t binc = is_e ? 32u : 0u, sinc = is_e ? uint32_t(kSlotWords) : 0u;
+    // A lanes: one broadcast address in the all-1 slot, column 8 (jj + 1), 32 banks
+    // away from the E lanes' eight columns of the same block (the same banks at a
+    // different address were a 2-way conflict on every read: 9 % of the LDS cycles).
+    const uint32_t lbase = is_e ? me * 4u : uint32_t(kRing8) * kSlotWords + 32u;
+    const uint32_t binc = 32u, sinc = is_e ? uint32_t(kSlotWords) : 0u;
     // voff: this lane's offset of block i (E: slot base vslot + jj * 32; A: 0)
     uint32_t voff = 0, vslot = 0, slot = 0;
     u32x4 kq[kAhead] = {};
@@ -1260,7 +1266,7 @@ int sha_lanes_for(uint32_t n_jobs) {
 template <int kTiming, int kGroups>
 static hipError_t launch_w8(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest, uint32_t* out_state,
                             hipStream_t s) {
-    constexpr size_t lds = size_t(kGroups) * 4 * kSlotWords * 4;  // 3 ring slots + the all-1 slot: 64 KiB a pair
+    constexpr size_t lds = size_t(kGroups) * (4 * kSlotWords + kOnesPad8) * 4;  // 3 ring slots + the all-1 slot: 65 KiB a pair
     auto* k = &sha256_w8_kernel<kTiming, kGroups>;
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;

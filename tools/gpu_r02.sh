@@ -39,14 +39,17 @@ done
 for s in "$@"; do
   case $s in
     vop) step micro_vopcost 120 tools/micro/vopcost ;;
+    pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py $C2 ;;
+    pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py $C2 ;;
+    bc1) step bench_c1 600 python bench.py --workload c1 --steps 1 --warmup 1 ;;
     prof4) step prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4 -- python3 $R/bench.py --workload c4 --no-cpu-baseline ;;
     prof5) step prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c5 -- python3 $R/bench.py --workload c5 --no-cpu-baseline --no-sweep ;;
     prof3) step prof_c3 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c3 -- python3 $R/bench.py --workload c3 --no-cpu-baseline ;;
-    bc1) step bench_c1 600 python bench.py --workload c1 --steps 1 --warmup 1 ;;
     bc3) step bench_c3 900 python bench.py --workload c3 ;;
     bc4) step bench_c4 600 python bench.py --workload c4 ;;
     bc5) step bench_c5 600 python bench.py --workload c5 ;;
     bc5r) step bench_c5regen 900 python bench.py --workload c5regen ;;
+    bc5rd) step bench_c5regen_digest 900 python bench.py --workload c5regen_digest --steps 1 --warmup 1 ;;
     bf1) step bench_f1verify 600 python bench.py --workload f1verify ;;
     crcspec) step crc_spec 600 python tools/probe_perf.py --crc-spec 16:100:4096,16:256:256 --sha none ;;
   esac
