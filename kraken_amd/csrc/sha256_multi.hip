@@ -9,9 +9,11 @@
 //    KW[r] = W[r] + K[r] into an LDS ring;
 //  * the consumer wave runs only the rounds, reading KW from the ring with
 //    ds_read_b128, one s_barrier per producer step.
-// Streams per consumer wave: 32 with two lanes per stream (the A lane carries the
-// a..d history, the E lane e..h, a 9-instruction round; chosen while the batch
-// leaves SIMDs idle) or 64 with one lane (a 14-instruction round).  Jobs start from
+// Streams per consumer wave: 8 with eight lanes per stream (sha256_w8_kernel: an E quad
+// and an A quad, Sigma rotated across the quad, an 8-instruction round, blocks
+// pipelined; up to 16 x CUs streams), 32 with two lanes (the A lane carries the a..d
+// history, the E lane e..h, a 9-instruction round) or 64 with one lane (a
+// 14-instruction round) as the batch fills the chip.  Jobs start from
 // the IV or a midstate (streaming Digester, windowed host paths) and either write
 // the digest (final, padding done here) or the midstate back.  No MFMA: the work is
 // 32-bit integer rotate/xor/add.
