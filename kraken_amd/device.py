@@ -98,7 +98,7 @@ def synchronize():
 
 
 def sha_lanes_per_stream(n_streams: int) -> int:
-    """Lanes per SHA-256 stream the library uses for a batch of n_streams (1 or 2)."""
+    """Lanes per SHA-256 stream the library uses for a batch of n_streams (1, 2 or 8)."""
     v = C.c_int(0)
     check(lib.krk_sha_lanes_per_stream(n_streams, C.byref(v)))
     return v.value

@@ -6,6 +6,8 @@ everything in seconds: sampled oracle checks plus size-independent properties.
   the chunked path (SHA-256 from per-blob midstates, CRC items cut at chunk edges
   that split pieces) must give the same 1,000 digests and 25,000 sums as the
   one-shot path (two different work decompositions of the same bytes).
+* C1 (configs[0]: one 1 GiB blob): the whole SHA-256 chain on one stream and the
+  256 piece sums against hashlib / the oracle.
 * C4 (configs[3]: one 20 GiB blob, 256 KiB pieces): sampled pieces against the
   oracle (content regenerated at the piece's offset), and CRC linearity -- the
   81,920 piece sums combined with crc(A||B) = shift(crc(A), |B|) ^ crc(B) equal the
@@ -86,6 +88,21 @@ def test_c2_full_size_decomposition_invariance(gpu, orc):
     D.synchronize()
     assert np.array_equal(cb.sums.to_host(np.uint32, arena.total_pieces), sums)
     assert np.array_equal(cb.digests.to_host(np.uint8, 32 * n).reshape(n, 32), dg)
+
+
+def test_c1_full_size_one_stream(gpu, orc):
+    """C1 (configs[0]: one 1 GiB blob, 4 MiB pieces): NewMetaInfo + Digester of ONE
+    stream at full size -- the SHA-256 chain runs 16,777,216 blocks on one eight-lane
+    stream (~19 s), the CRC 256 pieces beside it."""
+    L, P = 1 << 30, 4 << 20
+    arena = D.BlobArena([L], P, blob_ids=[0])
+    out = D.BatchOutputs(arena)
+    assert D.sha_lanes_per_stream(1) == 8
+    D.metainfo_digest(arena, out)
+    D.synchronize()
+    data = orc.synth(0, L)
+    assert bytes(out.digests.to_host(np.uint8, 32)) == hashlib.sha256(data).digest()
+    assert np.array_equal(out.sums.to_host(np.uint32, L // P), orc.calc_piece_sums(data, P)[1])
 
 
 def test_c4_full_size_sampled_and_linear(gpu, orc):
