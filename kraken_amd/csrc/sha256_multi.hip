@@ -637,6 +637,18 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
 #undef KRK_SHA2_OPERANDS
 #undef KRK_SHA2_CONSTS
 
+// Rounds n = 4j + 2 .. 4j + 5 of an eight-lane block (block8p), the register roles of
+// instruction-rounds 2 .. 5: W operands are W[n + 1] for the z of the next round.
+__device__ __forceinline__ void sha8_quad2(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                           const TwoLaneConst& c, uint32_t w1, uint32_t w2, uint32_t w3,
+                                           uint32_t w4) {
+    uint32_t t1, t2, kk, p;
+    asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w1) KRK_SHA8_ROUND(R3, R2, R1, R0, w2)
+                 KRK_SHA8_ROUND(R0, R3, R2, R1, w3) KRK_SHA8_ROUND(R1, R0, R3, R2, w4)
+                 KRK_SHA8_OPERANDS
+                 : KRK_SHA8_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
+}
+
 // Eight lanes a stream, blocks pipelined: the A quad runs rounds 62, 63 of block i
 // while the E quad already runs rounds 0, 1 of block i + 1, so a block costs 64
 // instruction-rounds instead of 66.  State crosses blocks in registers: R0..R3 (the
@@ -666,35 +678,38 @@ __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2
     u32x4 wq[kRS];
 #pragma unroll
     for (int j = 0; j < kAhead; ++j) wq[j] = k[j];
+    // Rounds n = 2 .. 61 in 15 asm blocks of four, n = 4j + 2 .. 4j + 5 (W: quad j's last
+    // word, quad j + 1's first three), each W read between two blocks -- two rounds into
+    // a W quad.  Issued right before a W quad's rounds a read cost ~16 cycles of the
+    // wave's stream, two rounds in ~8, its code bytes (tools/micro/sha8lds.hip,
+    // profiles/r02/micro_sha8lds.txt); and the read + its wait between two asm blocks
+    // are the two wait states the hazard recognizer would otherwise pad there.
+#pragma unroll
+    for (int j = 0; j < 15; ++j) {
 #ifdef KRK_SHA_NOLDS
-    wq[kAhead] = u32x4{3u, cbase, 5u, 7u};
+        if (j + kAhead < 16) wq[(j + kAhead) % kRS] = u32x4{(uint32_t)j, cbase, 5u, 7u};
+        else k[j + kAhead - 16] = u32x4{(uint32_t)j, nbase, 5u, 7u};
 #else
-    wq[kAhead] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * kAhead);
+        if (j + kAhead < 16)
+            wq[(j + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (j + kAhead));
+        else  // the next block's first quads
+            k[j + kAhead - 16] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (j + kAhead - 16));
+#endif
+        const u32x4& a = wq[j % kRS];
+        const u32x4& b = wq[(j + 1) % kRS];
+        sha8_quad2(R0, R1, R2, R3, z, c, a[3], b[0], b[1], b[2]);
+    }
+#ifdef KRK_SHA_NOLDS
+    k[kAhead - 1] = u32x4{15u, nbase, 5u, 7u};
+#else
+    k[kAhead - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead - 1));
 #endif
     {
-        uint32_t t1, t2, kk, p;
+        uint32_t t1, t2, kk, p;  // n = 62, 63
         asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
                      KRK_SHA8_ROUND(R3, R2, R1, R0, w4)
-                     : [t1] "=&v"(t1), [t2] "=&v"(t2), [k] "=&v"(kk), [p] "=&v"(p), [z] "+v"(z), [R0] "+v"(R0),
-                       [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3)
-                     : KRK_SHA8_CONSTS, [w3] "v"(wq[0][3]), [w4] "v"(wq[1][0]));
-    }
-#pragma unroll
-    for (int q = 1; q < 16; ++q) {
-        if (q + kAhead < 16)
-#ifdef KRK_SHA_NOLDS
-            wq[(q + kAhead) % kRS] = u32x4{(uint32_t)q, cbase, 5u, 7u};
-#else
-            wq[(q + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + kAhead));
-#endif
-        if (q >= 16 - kAhead)
-#ifdef KRK_SHA_NOLDS
-            k[q - (16 - kAhead)] = u32x4{(uint32_t)q, nbase, 5u, 7u};
-#else
-            k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
-#endif
-        const u32x4& cur = wq[q % kRS];
-        sha2_quad<8>(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : k[0][0]);
+                     KRK_SHA8_OPERANDS
+                     : KRK_SHA8_CONSTS, [w3] "v"(wq[15 % kRS][3]), [w4] "v"(k[0][0]));
     }
     {
         // F1, n = 64, F2, n = 65, F3.  The cross terms go through one DPP each: every
