@@ -154,10 +154,10 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *                   them; a digester's midstate chains through its own requests
  *                   only).  Creation allocates nothing on the device.
  *   KRK_PLACE_HOST  SHA-NI on the caller's thread (host_meta.cpp): ~2 GB/s per stream
- *                   against ~50 MB/s for one GPU stream.
+ *                   against ~56 MB/s for one GPU stream.
  *   KRK_PLACE_AUTO  (krk_digester_new) HOST while at most N digesters are live in the
  *                   process, GPU beyond: the crossover where the host's aggregate
- *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~50 MB/s).
+ *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~56 MB/s).
  *                   N = 40 x the CPUs this process may use, or KRK_DIGESTER_HOST_STREAMS,
  *                   or krk_set_digester_host_streams (-1 restores the default).
  * Without a gfx950 device every constructor fails with KRK_ENODEV. */
@@ -263,7 +263,7 @@ int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums
 
 /* --------------------------------------- host crossover primitives (CPU)
  * The host side of the Digester / PieceHash crossovers: a single
- * SHA-256 stream digests ~2 GB/s on one SHA-NI core vs ~50 MB/s on one GPU stream,
+ * SHA-256 stream digests ~2 GB/s on one SHA-NI core vs ~56 MB/s on one GPU stream,
  * and a small crc32.Update is cheaper on the calling thread than a PCIe round trip,
  * so a krk_digester with few concurrent peers and a small krk_crc32_update write
  * run these on the caller's thread.  x86 SHA-NI / PCLMULQDQ when the CPU has them,

@@ -33,9 +33,10 @@ def window_plan(lens, W, cap):
     """Windows: [(blob indices, offsets, chunk lengths)].  Every live blob advances by
     the same 64-multiple chunk per window (about W bytes a window).  Admission: at most
     `cap` blobs are live, admitted longest first, so the longest chain starts in window 0
-    and every window stays on the two-lane SHA plan (a launch of more streams falls back
-    to one lane per stream, ~0.74x per stream); a finished blob's slot goes
-    to the next-longest waiting blob."""
+    and every window stays on a multi-lane SHA plan (eight lanes a stream up to 16 x CUs
+    live streams, two up to 64 x CUs; a launch of more streams falls back to one lane per
+    stream, ~0.7x per stream); a finished blob's slot goes to the
+    next-longest waiting blob."""
     L = np.asarray(lens, dtype=np.uint64)
     n = L.size
     cap = max(1, min(int(cap), n)) if n else 1
