@@ -341,6 +341,10 @@ def run_metainfo(a, D, T, rank, world, res):
     roof = roofline_obj(dominant, sha_gbps if dominant == "sha256_multi" else crc_gbps,
                         sha_avg if dominant == "sha256_multi" else crc_avg, bytes_rank, traffic.get(dominant))
     roof_crc = roofline_obj("crc32_pieces", crc_gbps, crc_avg, bytes_rank, traffic.get("crc32_pieces"))
+    roof_crc["note"] = ("launched together with sha256_multi (krk_metainfo_digest_dev), so it runs on the CUs the "
+                        "SHA workgroups leave free (their LDS rings keep a CRC workgroup off a CU that holds one) "
+                        "and its time is hidden inside the SHA launch; alone on the chip it is the C4 line "
+                        "(DESIGN.md 4.1)")
     valu, valu_src = load_valu(a.workload)
     if valu_src and valu.get("device_resident", {}).get("crc32_pieces"):
         roof_crc["valu"] = dict(valu["device_resident"]["crc32_pieces"], source=valu_src)

@@ -103,12 +103,17 @@ struct PinnedSlot {
 // Stream-ordered device scratch.  Blocks are power-of-two sized and stay with the
 // device context; a released block carries an event recorded on the releasing
 // stream and its next user's stream waits on that event, so reuse is ordered on
-// the device with no host stall and no allocator work per call.
+// the device with no host stall and no allocator work per call.  A block is taken
+// from another stream only once its event has completed: waiting on a block still
+// held behind another stream's long kernel would serialize independent streams (the
+// CRC launch of krk_metainfo_digest_dev queued behind the whole SHA-256 kernel when
+// both took blocks of one size), so a fresh block is allocated instead.
 struct DevCache {
     struct Blk {
         void* p = nullptr;
         size_t cap = 0;
         hipEvent_t ev = nullptr;
+        hipStream_t s = nullptr;  // the stream that released it
         bool pending = false;
     };
     std::mutex mu;
@@ -121,15 +126,24 @@ struct DevCache {
         Blk b;
         {
             std::lock_guard<std::mutex> g(mu);
-            auto it = idle.find(cap);
-            if (it != idle.end()) {
-                b = it->second;
-                idle.erase(it);
+            auto r = idle.equal_range(cap);
+            auto pick = idle.end();
+            for (auto it = r.first; it != r.second; ++it) {
+                const Blk& c = it->second;
+                if (!c.pending || c.s == s) {  // free, or ordered by this stream already
+                    pick = it;
+                    break;
+                }
+                if (pick == idle.end() && hipEventQuery(c.ev) == hipSuccess) pick = it;
+            }
+            if (pick != idle.end()) {
+                b = pick->second;
+                idle.erase(pick);
             }
         }
         hipError_t e = hipSuccess;
         if (b.p) {
-            if (b.pending) e = hipStreamWaitEvent(s, b.ev, 0);
+            if (b.pending) e = hipStreamWaitEvent(s, b.ev, 0);  // free when s released it
         } else {
             e = hipMalloc(&b.p, cap);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
@@ -148,6 +162,7 @@ struct DevCache {
         if (it == live.end()) return;
         Blk b = it->second;
         live.erase(it);
+        b.s = s;
         b.pending = hipEventRecord(b.ev, s) == hipSuccess;
         if (!b.pending) hipStreamSynchronize(s);
         idle.emplace(b.cap, b);

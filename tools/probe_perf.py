@@ -73,6 +73,7 @@ if __name__ == "__main__":
                     help="krk_set_sha_plan: 0 auto, 1-4 production, 100-107 diagnostics (KRK_DIAG build, "
                          "KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so)")
     ap.add_argument("--c2", action="store_true")
+    ap.add_argument("--split", default="", help="n:blob_mb:piece_kb,... CRC alone / SHA alone / both (c2_split shape)")
     ap.add_argument("--crc-spec", default="", help="gb:blob_mb:piece_kb,... custom CRC shapes")
     a = ap.parse_args()
     os.environ["KRK_CRC_VARIANT"] = a.variant
@@ -81,6 +82,11 @@ if __name__ == "__main__":
     res = []
     if a.c2:
         print(json.dumps(crc_concurrent(1000, 100, 4 << 20)), flush=True)
+        sys.exit(0)
+    if a.split:
+        for spec in a.split.split(","):
+            n, mb, pk = map(int, spec.split(":"))
+            print(json.dumps(dict(crc_concurrent(n, mb, pk << 10), plan=a.sha_plan)), flush=True)
         sys.exit(0)
     if a.crc_spec:
         for spec in a.crc_spec.split(","):
