@@ -354,6 +354,12 @@ int krk_memcpy_d2h(void* dst_host, const void* src_dev, uint64_t n);
 int krk_stream_create(void** out);
 int krk_stream_destroy(void* s);
 int krk_stream_sync(void* s);
+/* Events (a window loop waits for ONE earlier window's kernels while the next
+ * window's are already queued behind them on the same stream). */
+int krk_event_create(void** out);
+int krk_event_record(void* ev, void* stream);
+int krk_event_sync(void* ev);
+int krk_event_destroy(void* ev);
 
 /* Kernel timing: when enabled, every kernel launch is bracketed by hipEvents
  * recorded on the stream the kernel runs on; krk_kernel_stats returns the

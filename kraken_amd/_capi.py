@@ -121,6 +121,10 @@ def _load() -> C.CDLL:
         "krk_stream_create": (i, [C.POINTER(vp)]),
         "krk_stream_destroy": (i, [vp]),
         "krk_stream_sync": (i, [vp]),
+        "krk_event_create": (i, [C.POINTER(vp)]),
+        "krk_event_record": (i, [vp, vp]),
+        "krk_event_sync": (i, [vp]),
+        "krk_event_destroy": (i, [vp]),
         "krk_set_timing": (i, [i]),
         "krk_sha_lanes_per_stream": (i, [C.c_uint64, C.POINTER(C.c_int)]),
         "krk_kernel_stats": (i, [C.c_char_p, u64p, f64p]),

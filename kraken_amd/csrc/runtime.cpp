@@ -1384,6 +1384,31 @@ int krk_stream_sync(void* s) {
     return KRK_OK;
 }
 
+int krk_event_create(void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    hipEvent_t e;
+    KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = e;
+    return KRK_OK;
+}
+int krk_event_record(void* ev, void* stream) {
+    KRK_CHECK(ev, KRK_EINVAL, "event is NULL");
+    KRK_DEVICE(D);
+    KRK_HIP(hipEventRecord(static_cast<hipEvent_t>(ev), pick(D, stream)));
+    return KRK_OK;
+}
+int krk_event_sync(void* ev) {
+    KRK_CHECK(ev, KRK_EINVAL, "event is NULL");
+    KRK_HIP(hipEventSynchronize(static_cast<hipEvent_t>(ev)));
+    return KRK_OK;
+}
+int krk_event_destroy(void* ev) {
+    if (ev) hipEventDestroy(static_cast<hipEvent_t>(ev));
+    return KRK_OK;
+}
+
 int krk_set_timing(int on) {
     g_timing.store(on != 0);
     return KRK_OK;

@@ -105,16 +105,28 @@ class WindowedRun:
         self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
 
     def run(self):
+        """Window k's kernels are queued before the host waits for window k-1's (an
+        event after each window), so the device goes from one window to the next with
+        no host round trip; window k+1 is generated into k-1's buffer once k-1 is done."""
         D = self.D
         cur = self._items(0)
         self._gen(cur)
-        for k in range(len(self.wins)):
-            D.check(D.lib.krk_stream_sync(self.run_s))  # window k-1 done: its buffer may be refilled
-            self.cb.step_arrays(cur[0], cur[1], cur[2], cur[3], stream=self.run_s)
-            if k + 1 < len(self.wins):
-                cur = self._items(k + 1)
-                self._gen(cur)
-        D.check(D.lib.krk_stream_sync(self.run_s))
+        evs = [C.c_void_p(), C.c_void_p()]
+        for e in evs:
+            D.check(D.lib.krk_event_create(C.byref(e)))
+        try:
+            for k in range(len(self.wins)):
+                self.cb.step_arrays(cur[0], cur[1], cur[2], cur[3], stream=self.run_s)
+                D.check(D.lib.krk_event_record(evs[k & 1], self.run_s))
+                if k + 1 < len(self.wins):
+                    if k:  # window k-1 read buffer (k+1) & 1
+                        D.check(D.lib.krk_event_sync(evs[(k - 1) & 1]))
+                    cur = self._items(k + 1)
+                    self._gen(cur)
+            D.check(D.lib.krk_stream_sync(self.run_s))
+        finally:
+            for e in evs:
+                D.lib.krk_event_destroy(e)
 
     def close(self):
         for b in self.bufs:
