@@ -364,6 +364,8 @@ def run_metainfo(a, D, T, rank, world, res):
                 "roofline_crc": roof_crc,
                 "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)},
                             "sha256_multi": {"launches": sha_n, "avg_ms": round(sha_avg, 3)}}})
+    if a.workload in ("c1", "c5regen_digest") and not a.no_offload:
+        res["host_offload"] = host_offload_leg(a, D, T, step, lens, world, dg_h, n)
     if a.workload == "c2" and not a.no_e2e:
         res["end_to_end"] = end_to_end(D, T, arena, n, min(a.e2e_mb << 20, lens[0]), P, out, world)
         ev = valu.get("end_to_end") if valu_src else None
@@ -380,6 +382,38 @@ def run_metainfo(a, D, T, rank, world, res):
             ok = ok and np.array_equal(s[int(off[k]):int(off[k + 1])], sums_h[o:o + cnt])
         cb["outputs_match_gpu"] = bool(ok)
         res["cpu_baseline"] = cb
+
+
+def host_offload_leg(a, D, T, step, lens, world, dg_h, n):
+    """The same batch with krk_set_sha_host_offload(host cores): the longest SHA-256
+    chains on host threads (x86 SHA extensions, read out of HBM), the rest and every
+    piece CRC on the GPU.  Reported beside `value` (which stays the GPU-only path): it
+    is what a chain-bound batch (C1's one 1 GiB blob, the log-uniform regen batch) gets
+    from the library with the offload on."""
+    thr = host_cores()
+    idx, g_s, h_s = D.sha_offload_plan(lens, thr)
+    gpu_only = dg_h.copy()  # step() gathers the digests into dg_h
+    D.set_sha_host_offload(thr)
+    try:
+        for _ in range(a.warmup):
+            step()
+        T.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        T.barrier()
+        el = T.max_over_ranks(time.perf_counter() - t0)
+    finally:
+        D.set_sha_host_offload(0)
+    total = int(sum(lens))
+    return {"value": round(world * total * a.steps / el / 1e9, 3), "unit": "GB/s",
+            "ms_per_step": round(el / a.steps * 1e3, 3), "host_threads": thr, "blobs_on_host": int(idx.size),
+            "bytes_on_host": int(sum(int(lens[i]) for i in idx)), "blobs": n,
+            "model_s": {"gpu": round(g_s, 3), "host": round(h_s, 3)},
+            "digests_match_gpu_only": bool(np.array_equal(dg_h, gpu_only)),
+            "what": "krk_metainfo_digest_dev with krk_set_sha_host_offload(host cores): the planner's longest "
+                    "blobs hashed on host threads from HBM through pinned double buffers while the GPU hashes "
+                    "the rest and every blob's piece CRCs (DESIGN.md 4.2)"}
 
 
 def run_regen(a, D, T, rank, world, res):
@@ -845,6 +879,8 @@ def main():
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the live SHA issue-ceiling run (profiler passes: keeps its launches out of the trace)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers, PCIe) leg")
+    ap.add_argument("--no-offload", action="store_true",
+                    help="C1 / c5regen_digest: skip the SHA-256 host-offload leg")
     ap.add_argument("--no-sweep", action="store_true", help="C5: skip the N x MaxReplica x healthy grid")
     ap.add_argument("--e2e-mb", type=int, default=100, help="bytes per blob for the end-to-end leg (MiB; C2: 100)")
     ap.add_argument("--e2e-only", action="store_true",

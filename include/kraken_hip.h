@@ -394,6 +394,22 @@ int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes);
 #define KRK_SHA_PLAN_8LANE_2PAIR 6  /* eight lanes, two pairs per workgroup */
 int krk_set_sha_plan(int plan);
 
+/* Host offload of the longest SHA-256 chains, process-wide (default 0 = off).  With
+ * threads > 0, krk_sha256_dev and krk_metainfo_digest_dev hand the longest blobs of a
+ * batch to up to `threads` host threads (x86 SHA extensions, ~2 GB/s a thread against
+ * ~56 MB/s a GPU stream), which read them from device memory through pinned double
+ * buffers while the GPU hashes the rest and every blob's piece CRCs; the digests land in
+ * digests_dev as before.  How many go to the host minimises max(GPU time, host time) and
+ * is 0 unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host,
+ * 1,000 equal 100 MiB blobs (C2) stay on the GPU.  The call then returns after the host
+ * part is hashed (the GPU part stays asynchronous on `stream`). */
+int krk_set_sha_host_offload(int threads);
+/* The offload plan for `n` blob lengths on `threads` host threads and a device of `cus`
+ * CUs, without a device: the indices (longest first) to host_idx (room for n, may be
+ * NULL), their count to n_host, and the modelled GPU / host seconds (may be NULL). */
+int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
+                         uint64_t* n_host, double* gpu_seconds, double* host_seconds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -125,6 +125,9 @@ def _load() -> C.CDLL:
         "krk_event_record": (i, [vp, vp]),
         "krk_event_sync": (i, [vp]),
         "krk_event_destroy": (i, [vp]),
+        "krk_set_sha_host_offload": (i, [i]),
+        "krk_sha_offload_plan": (i, [C.POINTER(C.c_uint64), C.c_uint64, i, i, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "krk_set_timing": (i, [i]),
         "krk_sha_lanes_per_stream": (i, [C.c_uint64, C.POINTER(C.c_int)]),
         "krk_kernel_stats": (i, [C.c_char_p, u64p, f64p]),

@@ -100,6 +100,9 @@ struct alignas(16) ShaJob {
 };
 static_assert(sizeof(ShaJob) == 64, "ShaJob layout");
 
+// Digests computed elsewhere (host offload) into digests[32 * idx]: n records of a
+// little-endian uint32 idx + 32 digest bytes.
+hipError_t launch_digest_scatter(const uint8_t* rec, uint32_t n, uint8_t* digests, hipStream_t s);
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s);
 // Lanes per stream launch_sha256 uses for a batch of n_jobs streams (1 or 2).

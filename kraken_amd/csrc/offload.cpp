@@ -1,0 +1,272 @@
+// offload.cpp -- host offload of the longest SHA-256 chains of a device-resident batch
+// (krk_set_sha_host_offload; used by krk_sha256_dev and krk_metainfo_digest_dev).
+//
+// SHA-256 is one sequential chain per blob (core/digester.go:28-72).  A GPU stream runs
+// at ~56 MB/s (eight lanes), one x86 core with the SHA extensions at
+// ~2 GB/s.  A batch whose longest blobs dominate (C1: one 1 GiB blob; the log-uniform
+// regen batches of C5) therefore finishes sooner when host threads take the longest
+// chains -- reading them out of HBM through pinned double buffers -- while the GPU
+// hashes the rest and the piece CRCs of every blob.  The planner picks how many of the
+// longest blobs go to the host by minimising max(GPU time, host time); a batch of equal
+// blobs (C2) gains nothing (the GPU's chain is the same blob length) and stays on the GPU.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <queue>
+#include <thread>
+
+#include "runtime.hpp"
+
+namespace krk {
+
+void host_sha256_blocks(uint32_t h[8], const uint8_t* p, size_t nblocks);
+void host_sha256_final(const uint32_t h[8], uint64_t absorbed, const uint8_t* tail, size_t n, uint8_t out[32]);
+
+namespace {
+
+std::atomic<int> g_off_threads{0};
+
+constexpr uint64_t kOffChunk = 8ull << 20;  // D2H chunk (multiple of 64)
+constexpr double kD2H = 50e9;               // device -> pinned host, bytes/s (PCIe Gen5 x16, measured 54)
+
+// One host thread hashing, bytes/s: measured once (16 MiB) and derated for the clock a
+// fully loaded socket holds.
+double host_rate() {
+    static const double r = [] {
+        std::vector<uint8_t> buf(16u << 20, 0x5a);
+        uint32_t h[8];
+        memcpy(h, kIV, sizeof h);
+        host_sha256_blocks(h, buf.data(), 1024);  // warm
+        const auto t0 = std::chrono::steady_clock::now();
+        host_sha256_blocks(h, buf.data(), buf.size() / 64);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return 0.85 * buf.size() / std::max(s, 1e-6);
+    }();
+    return r;
+}
+
+// GPU time of m streams (longest `longest` bytes, `bytes` in all) under the AUTO launch
+// plan: the longest chain at the plan's per-stream rate, or the chip's aggregate SHA
+// throughput when the streams outnumber what runs at once (measured on MI355X,
+// profiles/r02/sha_plans_c3shape.jsonl; aggregates scale with the CU count).
+double gpu_seconds(uint64_t longest, double bytes, uint64_t m, int cus) {
+    if (!m) return 0;
+    const double scale = cus / 256.0;
+    double r, cap;
+    if (m <= 16ull * (uint64_t)cus) {
+        r = 55e6;
+        cap = 1e30;
+    } else if (m <= 64ull * (uint64_t)cus) {
+        r = 48e6;
+        cap = 790e9 * scale;
+    } else {
+        r = 33e6;
+        cap = 1.1e12 * scale;
+    }
+    return std::max(longest / r, bytes / std::min(m * r, cap));
+}
+
+// One host thread's copy resources: buffer b is filled on stream s[b].  Completion is
+// awaited with hipStreamSynchronize, not an event: an event record is a packet on the
+// stream's hardware queue, and with more streams than hardware queues (4) it can sit
+// behind the batch's own long SHA-256 kernel (tools/micro/d2h_probe.hip: copy kernels
+// on 4 of 16 streams waited 1 s for a 1 s kernel on a fifth), while the DMA copies
+// themselves do not wait for it.
+struct Worker {
+    hipStream_t s[2] = {nullptr, nullptr};
+    uint8_t* buf[2] = {nullptr, nullptr};
+};
+
+}  // namespace
+
+struct OffloadPool {
+    std::mutex mu;  // one offload phase at a time per device
+    std::vector<Worker> w;
+};
+
+// The longest blobs to hash on `threads` host threads (indices into lens, longest
+// first); empty when the host would not shorten the batch by at least 10 %.
+std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
+                                   double* host_s) {
+    std::vector<uint32_t> order(n);
+    for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
+    std::vector<double> suffix(n + 1, 0.0);
+    for (uint64_t k = n; k-- > 0;) suffix[k] = suffix[k + 1] + (double)lens[order[k]];
+    const double f0 = n ? gpu_seconds(lens[order[0]], suffix[0], n, cus) : 0.0;
+    double best = f0, best_g = f0, best_h = 0;
+    uint64_t best_k = 0;
+    if (threads > 0 && n) {
+        const double rh = host_rate();
+        std::priority_queue<double, std::vector<double>, std::greater<double>> load;
+        for (int t = 0; t < threads; ++t) load.push(0.0);
+        double maxload = 0, hbytes = 0;
+        for (uint64_t k = 1; k <= n; ++k) {
+            const double L = (double)lens[order[k - 1]];
+            if (L == 0) break;  // empty blobs are not worth a thread
+            const double l = load.top() + L;
+            load.pop();
+            load.push(l);
+            maxload = std::max(maxload, l);
+            hbytes += L;
+            const double h = std::max(maxload / rh, hbytes / kD2H);
+            const double g = k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, cus) : 0.0;
+            if (std::max(g, h) < best) {
+                best = std::max(g, h);
+                best_k = k;
+                best_g = g;
+                best_h = h;
+            }
+            if (h > f0) break;  // the host alone is already slower than no offload
+        }
+        if (best > 0.9 * f0) {
+            best_k = 0;
+            best_g = f0;
+            best_h = 0;
+        }
+    }
+    if (gpu_s) *gpu_s = best_g;
+    if (host_s) *host_s = best_h;
+    order.resize(best_k);
+    return order;
+}
+
+int offload_threads() { return g_off_threads.load(std::memory_order_relaxed); }
+
+// Hash blobs (device pointers, lengths) on up to `threads` host threads; digest j to
+// out + 32 j.  The D2H copies start once `ready` (recorded on the caller's stream: the
+// bytes may still be being written there) has completed.  Blocks until all are hashed.
+int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
+                 hipEvent_t ready, uint8_t* out) {
+    if (ptrs.empty()) return KRK_OK;
+    {
+        std::lock_guard<std::mutex> g(D->offload_mu);
+        if (!D->offload) D->offload = new OffloadPool();
+    }
+    OffloadPool& P = *D->offload;
+    std::lock_guard<std::mutex> g(P.mu);
+    const int T = (int)std::min<size_t>((size_t)threads, ptrs.size());
+    while ((int)P.w.size() < T) {
+        Worker w;
+        for (int b = 0; b < 2; ++b) {
+            KRK_HIP(hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking));
+            KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault));
+        }
+        P.w.push_back(w);
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<int> err{0};
+    static const bool trace = getenv("KRK_TRACE") && atoi(getenv("KRK_TRACE")) > 0;
+    std::vector<double> t_wait(T, 0.0), t_hash(T, 0.0);
+    const auto t_start = std::chrono::steady_clock::now();
+    auto secs = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t)
+        pool.emplace_back([&, t] {
+            Worker& W = P.w[t];
+            // The host waits for `ready` (the caller's stream up to the call; the batch's own
+            // kernels come after it): a stream wait packet could queue behind those kernels.
+            if (hipSetDevice(D->id) != hipSuccess || hipEventSynchronize(ready) != hipSuccess) {
+                err.store(1);
+                return;
+            }
+            for (size_t j; !err.load() && (j = next.fetch_add(1)) < ptrs.size();) {
+                const uint8_t* src = ptrs[j];
+                const uint64_t L = lens[j];
+                const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
+                auto issue = [&](uint64_t c) {
+                    const uint64_t o = c * kOffChunk, m = std::min(kOffChunk, L - o);
+                    return m == 0 ||
+                           hipMemcpyAsync(W.buf[c & 1], src + o, m, hipMemcpyDeviceToHost, W.s[c & 1]) == hipSuccess;
+                };
+                uint32_t h[8];
+                memcpy(h, kIV, sizeof h);
+                uint64_t absorbed = 0;
+                bool ok = issue(0);
+                for (uint64_t c = 0; ok && c < nch; ++c) {
+                    if (c + 1 < nch) ok = issue(c + 1);  // into the other buffer, hashed at c - 1
+                    const auto tw = std::chrono::steady_clock::now();
+                    if (!ok || hipStreamSynchronize(W.s[c & 1]) != hipSuccess) {
+                        ok = false;
+                        break;
+                    }
+                    const auto th = std::chrono::steady_clock::now();
+                    t_wait[t] += std::chrono::duration<double>(th - tw).count();
+                    const uint64_t m = std::min(kOffChunk, L - c * kOffChunk);
+                    if (c + 1 < nch) {
+                        host_sha256_blocks(h, W.buf[c & 1], m / 64);
+                        absorbed += m;
+                    } else {
+                        host_sha256_final(h, absorbed, W.buf[c & 1], m, out + 32 * j);
+                    }
+                    t_hash[t] += secs(th);
+                }
+                if (!ok) {
+                    hipStreamSynchronize(W.s[0]);  // leave no copy in flight into the buffers
+                    hipStreamSynchronize(W.s[1]);
+                    err.store(1);
+                }
+            }
+        });
+    for (auto& th : pool) th.join();
+    if (trace) {
+        uint64_t bytes = 0;
+        for (uint64_t L : lens) bytes += L;
+        double w = 0, h = 0;
+        for (int t = 0; t < T; ++t) {
+            w += t_wait[t];
+            h += t_hash[t];
+        }
+        fprintf(stderr, "krk_trace sha_offload: threads=%d blobs=%zu bytes=%llu wall=%.3fs wait=%.3fs hash=%.3fs (thread sums)\n",
+                T, ptrs.size(), (unsigned long long)bytes, secs(t_start), w, h);
+    }
+    KRK_CHECK(!err.load(), KRK_EHIP, "sha256 host offload: device-to-host copy failed");
+    return KRK_OK;
+}
+
+// Write host-computed digests into digests_dev (record j: 4-byte blob index, 32-byte
+// digest) on stream s: one upload + one scatter launch.
+int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,
+                  hipStream_t s) {
+    if (idx.empty()) return KRK_OK;
+    std::vector<uint8_t> rec(idx.size() * 36);
+    for (size_t j = 0; j < idx.size(); ++j) {
+        memcpy(&rec[36 * j], &idx[j], 4);
+        memcpy(&rec[36 * j + 4], dig + 32 * j, 32);
+    }
+    void* d = nullptr;
+    int r = upload(D, rec.data(), rec.size(), &d, s);
+    if (r) return r;
+    hipError_t e = launch_digest_scatter(static_cast<const uint8_t*>(d), (uint32_t)idx.size(), digests_dev, s);
+    scratch_free(D, d, s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "digest scatter launch: %s", hipGetErrorString(e));
+    return KRK_OK;
+}
+
+}  // namespace krk
+
+using namespace krk;
+
+extern "C" {
+
+int krk_set_sha_host_offload(int threads) {
+    KRK_CHECK(threads >= 0 && threads <= 1024, KRK_EINVAL, "host offload threads %d outside 0..1024", threads);
+    g_off_threads.store(threads);
+    return KRK_OK;
+}
+
+int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
+                         uint64_t* n_host, double* gpu_seconds_out, double* host_seconds_out) {
+    KRK_CHECK(n == 0 || lengths, KRK_EINVAL, "lengths is NULL");
+    KRK_CHECK(n_host, KRK_EINVAL, "n_host is NULL");
+    KRK_CHECK(threads >= 0 && cus > 0, KRK_EINVAL, "threads must be >= 0 and cus > 0");
+    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, cus, gpu_seconds_out, host_seconds_out);
+    *n_host = idx.size();
+    if (host_idx && !idx.empty()) memcpy(host_idx, idx.data(), idx.size() * 4);
+    return KRK_OK;
+}
+
+}  // extern "C"

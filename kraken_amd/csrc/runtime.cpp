@@ -398,14 +398,56 @@ int krk_piece_sums_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_d
     return piece_sums_dev(D, blobs, n_blobs, sums_dev, pick(D, stream));
 }
 
+// The blobs of a device-resident batch the host offload takes (krk_set_sha_host_offload;
+// empty when it is off or would not shorten the batch), and a per-blob mark.
+static std::vector<uint32_t> offload_split(Device* D, const uint64_t* lens, uint64_t n, std::vector<char>& on_host) {
+    on_host.assign(n, 0);
+    const int T = offload_threads();
+    if (T <= 0 || n == 0) return {};
+    std::vector<uint32_t> host = offload_plan(lens, n, T, D->cus, nullptr, nullptr);
+    for (uint32_t i : host) on_host[i] = 1;
+    return host;
+}
+
+// Hash the offloaded blobs on host threads (their D2H waits for `ready`) and store the
+// digests into digests_dev on stream s.
+static int offload_run(Device* D, const std::vector<uint32_t>& host, const uint8_t* const* ptrs,
+                       const uint64_t* lens, hipEvent_t ready, uint8_t* digests_dev, hipStream_t s) {
+    std::vector<const uint8_t*> p(host.size());
+    std::vector<uint64_t> l(host.size());
+    for (size_t j = 0; j < host.size(); ++j) {
+        p[j] = ptrs[host[j]];
+        l[j] = lens[host[j]];
+    }
+    std::vector<uint8_t> dig(32 * host.size());
+    int r = offload_hash(D, p, l, offload_threads(), ready, dig.data());
+    return r ? r : offload_store(D, host, dig.data(), digests_dev, s);
+}
+
 int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n, uint8_t* digests_dev,
                    void* stream) {
     KRK_DEVICE(D);
     if (!n) return KRK_OK;
     KRK_CHECK(data_dev && lengths && digests_dev, KRK_EINVAL, "sha256_dev: null argument");
-    std::vector<ShaJob> jobs(n);
-    for (uint64_t i = 0; i < n; ++i) jobs[i] = full_job(data_dev[i], lengths[i], (uint32_t)i);
-    return run_jobs(D, jobs, digests_dev, nullptr, pick(D, stream));
+    hipStream_t s = pick(D, stream);
+    std::vector<char> on_host;
+    const std::vector<uint32_t> host = offload_split(D, lengths, n, on_host);
+    std::vector<ShaJob> jobs;
+    jobs.reserve(n);
+    for (uint64_t i = 0; i < n; ++i)
+        if (!on_host[i]) jobs.push_back(full_job(data_dev[i], lengths[i], (uint32_t)i));
+    if (host.empty()) return run_jobs(D, jobs, digests_dev, nullptr, s);
+    hipEvent_t ready;
+    KRK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    int r = KRK_OK;
+    if (hipEventRecord(ready, s) != hipSuccess) {
+        set_error(KRK_EHIP, "sha256_dev: event record failed");
+        r = KRK_EHIP;
+    }
+    if (!r) r = run_jobs(D, jobs, digests_dev, nullptr, s);  // the GPU part runs while the host hashes
+    if (!r) r = offload_run(D, host, data_dev, lengths, ready, digests_dev, s);
+    hipEventDestroy(ready);
+    return r;
 }
 
 int krk_metainfo_batch_dev(const krk_blob* blobs, uint64_t n_blobs, const char* names, const uint64_t* name_off,
@@ -496,15 +538,27 @@ int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* s
     KRK_HIP(hipEventRecord(fork, s));
     KRK_HIP(hipStreamWaitEvent(D->s_a, fork, 0));
     KRK_HIP(hipStreamWaitEvent(D->s_b, fork, 0));
+    // The longest chains may go to host threads (krk_set_sha_host_offload), off by default.
+    std::vector<uint64_t> lens(n_blobs);
+    std::vector<const uint8_t*> ptrs(n_blobs);
+    for (uint64_t i = 0; i < n_blobs; ++i) {
+        lens[i] = blobs[i].length;
+        ptrs[i] = blobs[i].data;
+    }
+    std::vector<char> on_host;
+    const std::vector<uint32_t> host = offload_split(D, lens.data(), n_blobs, on_host);
     // SHA first: it is the long pole; the CRC kernel fills the rest of the chip.
-    std::vector<ShaJob> jobs(n_blobs);
-    for (uint64_t i = 0; i < n_blobs; ++i) jobs[i] = full_job(blobs[i].data, blobs[i].length, (uint32_t)i);
+    std::vector<ShaJob> jobs;
+    jobs.reserve(n_blobs);
+    for (uint64_t i = 0; i < n_blobs; ++i)
+        if (!on_host[i]) jobs.push_back(full_job(blobs[i].data, blobs[i].length, (uint32_t)i));
     r = run_jobs(D, jobs, digests_dev, nullptr, D->s_a);
     if (!r) r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
     hipEventRecord(j1, D->s_a);
     hipEventRecord(j2, D->s_b);
     hipStreamWaitEvent(s, j1, 0);
     hipStreamWaitEvent(s, j2, 0);
+    if (!r && !host.empty()) r = offload_run(D, host, ptrs.data(), lens.data(), fork, digests_dev, s);
     hipEventDestroy(fork);
     hipEventDestroy(j1);
     hipEventDestroy(j2);

@@ -171,6 +171,7 @@ struct DevCache {
 
 struct Pipeline;
 struct Engine;
+struct OffloadPool;
 
 struct Device {
     // Submission engine (engine.cpp): the batching queues of the streaming
@@ -184,6 +185,9 @@ struct Device {
     // race the HIP runtime's own teardown.
     Pipeline* staging = nullptr;
     std::mutex staging_mu;
+    // Host threads + pinned double buffers of the SHA-256 host offload (offload.cpp).
+    OffloadPool* offload = nullptr;
+    std::mutex offload_mu;
     // The 65,536 ShardID keys (2 bytes each) of the Locations shard table, uploaded
     // once: constant input of every krk_ring_locations_dev call.
     uint8_t* shard_kb = nullptr;
@@ -529,5 +533,16 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
     return j;
 }
 
+
+
+// SHA-256 host offload (offload.cpp): the longest blobs of a device-resident batch
+// hashed on host threads while the GPU hashes the rest (krk_set_sha_host_offload).
+int offload_threads();
+std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
+                                   double* host_s);
+int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
+                 hipEvent_t ready, uint8_t* out);
+int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,
+                  hipStream_t s);
 
 }  // namespace krk

@@ -1346,4 +1346,21 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
     }
 }
 
+// Host-offloaded digests into their batch slots (offload.cpp): record j = 4-byte blob
+// index + 32-byte digest; one byte per thread (digests_dev has no alignment promise).
+__global__ void __launch_bounds__(256) digest_scatter_kernel(const uint8_t* __restrict__ rec, uint32_t n,
+                                                             uint8_t* __restrict__ digests) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * 32) return;
+    const uint8_t* r = rec + 36 * (t / 32);
+    const uint32_t idx = (uint32_t)r[0] | ((uint32_t)r[1] << 8) | ((uint32_t)r[2] << 16) | ((uint32_t)r[3] << 24);
+    digests[32ull * idx + t % 32] = r[4 + t % 32];
+}
+
+hipError_t launch_digest_scatter(const uint8_t* rec, uint32_t n, uint8_t* digests, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(digest_scatter_kernel, dim3((n * 32 + 255) / 256), dim3(256), 0, s, rec, n, digests);
+    return hipGetLastError();
+}
+
 }  // namespace krk

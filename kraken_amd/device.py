@@ -202,6 +202,23 @@ def metainfo_digest(arena: BlobArena, out: BatchOutputs, stream=None):
                                       out.digests.ptr, stream))
 
 
+def set_sha_host_offload(threads: int):
+    """krk_set_sha_host_offload: up to `threads` host threads take the longest SHA-256
+    chains of sha256 / metainfo_digest batches (0 = off, the default)."""
+    check(lib.krk_set_sha_host_offload(int(threads)))
+
+
+def sha_offload_plan(lengths, threads: int, cus: int = 256):
+    """krk_sha_offload_plan: (indices of the blobs the host would hash, longest first,
+    modelled GPU seconds, modelled host seconds) -- no device needed."""
+    L = np.ascontiguousarray(lengths, dtype=np.uint64)
+    idx = np.zeros(max(L.size, 1), dtype=np.uint32)
+    k, g, h = C.c_uint64(0), C.c_double(0), C.c_double(0)
+    check(lib.krk_sha_offload_plan(L.ctypes.data_as(C.POINTER(C.c_uint64)), L.size, int(threads), int(cus),
+                                   idx.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(k), C.byref(g), C.byref(h)))
+    return idx[:k.value].copy(), g.value, h.value
+
+
 def set_devices(devs):
     """The process's device set (krk_set_devices): where the *_multi calls run and new
     Digesters / piece streams are placed; repeats allowed; [] = the calling thread's device."""

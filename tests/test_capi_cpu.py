@@ -236,3 +236,26 @@ def test_streaming_constructors_need_a_device():
     assert lib.krk_digester_new_on(7, C.byref(h)) == _capi.KRK_EINVAL
     blob = (_capi.krk_blob * 1)(_capi.krk_blob(None, 0, 4, 0))
     assert lib.krk_metainfo_digest_host_multi(blob, 1, None, (C.c_uint8 * 32)()) == KRK_ENODEV
+
+
+def test_sha_offload_plan():
+    """krk_sha_offload_plan (host offload of the longest SHA-256 chains): equal blobs
+    stay on the GPU, a lone long blob goes to the host, a log-uniform batch hands over
+    exactly its longest blobs and shortens its modelled makespan; threads = 0 is off."""
+    from kraken_amd import device as D
+    idx, g, h = D.sha_offload_plan([100 << 20] * 1000, 16)  # C2
+    assert idx.size == 0 and h == 0.0 and g > 1.0
+    idx, g, h = D.sha_offload_plan([1 << 30], 16)  # C1
+    assert list(idx) == [0] and g == 0.0 and 0 < h < 5.0
+    rng = np.random.default_rng(7)
+    lens = np.exp(rng.uniform(np.log(4096), np.log(1 << 30), 1000)).astype(np.uint64)
+    idx, g, h = D.sha_offload_plan(lens, 16)
+    g0 = D.sha_offload_plan(lens, 0)[1]
+    assert 0 < idx.size < lens.size and max(g, h) < 0.9 * g0
+    order = np.argsort(-lens.astype(np.int64), kind="stable")
+    assert np.array_equal(idx, order[:idx.size])  # the longest ones, longest first
+    assert D.sha_offload_plan(lens, 0)[0].size == 0
+    assert D.sha_offload_plan([], 16)[0].size == 0
+    assert D.sha_offload_plan([0, 0, 0], 16)[0].size == 0
+    with pytest.raises(Exception):
+        D.sha_offload_plan(lens, -1)

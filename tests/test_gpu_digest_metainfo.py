@@ -412,3 +412,36 @@ def test_generate_batch_file_errors(gpu, tmp_path):
 
     with pytest.raises(IOError, match="^create metainfo: read blob: .*: unexpected EOF"):
         metainfogen.New({0: 4096}, Lying(str(tmp_path))).GenerateBatch([d])
+
+
+@pytest.mark.parametrize("misalign", [0, 3])
+def test_sha_host_offload_bit_exact(gpu, orc, misalign):
+    """krk_set_sha_host_offload: the longest blobs are hashed on host threads (read out of
+    HBM in 8 MiB double-buffered chunks: lengths on, around and past chunk edges), the
+    rest on the GPU; digests (krk_sha256_dev, krk_metainfo_digest_dev) and piece sums
+    equal hashlib / the oracle."""
+    big = [(40 << 20) + 13, 17 << 20, 8 << 20, (8 << 20) + 64, (16 << 20) - 1]
+    lens = big + [65536 + 7 * i for i in range(200)] + [0, 1, 63, 64]
+    ids = list(range(5000, 5000 + len(lens)))
+    P = 1 << 20
+    host_idx = D.sha_offload_plan(lens, 8, 256)[0]
+    assert set(host_idx.tolist()) >= set(range(len(big)))  # the long ones go to the host
+    arena = D.BlobArena(lens, P, blob_ids=ids, misalign=misalign)
+    out = D.BatchOutputs(arena)
+    want = [hashlib.sha256(orc.synth(b, L).tobytes()).digest() for b, L in zip(ids, lens)]
+    try:
+        D.set_sha_host_offload(8)
+        for fn in (D.sha256, D.metainfo_digest):
+            out.digests.from_host(np.zeros(32 * len(lens), dtype=np.uint8))
+            fn(arena, out)
+            D.synchronize()
+            dg = out.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+            for i in range(len(lens)):
+                assert bytes(dg[i]) == want[i], (fn.__name__, i, lens[i])
+        sums = out.sums.to_host(np.uint32, max(arena.total_pieces, 1))
+        for i, (b, L) in enumerate(zip(ids, lens)):
+            ref = orc.calc_piece_sums(orc.synth(b, L), P)[1]
+            o = int(arena.sums_off[i])
+            assert np.array_equal(sums[o:o + len(ref)], ref), i
+    finally:
+        D.set_sha_host_offload(0)
