@@ -402,7 +402,9 @@ int krk_set_sha_plan(int plan);
  * digests_dev as before.  How many go to the host minimises max(GPU time, host time) and
  * is 0 unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host,
  * 1,000 equal 100 MiB blobs (C2) stay on the GPU.  The call then returns after the host
- * part is hashed (the GPU part stays asynchronous on `stream`). */
+ * part is hashed (the GPU part stays asynchronous on `stream`).  The host-buffer entry
+ * points (krk_sha256_host, krk_metainfo_digest_host) hash their offloaded blobs in place:
+ * no device round trip, and krk_sha256_host does not upload them at all. */
 int krk_set_sha_host_offload(int threads);
 /* The offload plan for `n` blob lengths on `threads` host threads and a device of `cus`
  * CUs, without a device: the indices (longest first) to host_idx (room for n, may be

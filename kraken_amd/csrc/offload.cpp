@@ -88,13 +88,16 @@ struct OffloadPool {
 // The longest blobs to hash on `threads` host threads (indices into lens, longest
 // first); empty when the host would not shorten the batch by at least 10 %.
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
-                                   double* host_s) {
+                                   double* host_s, bool host_resident) {
     std::vector<uint32_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
     std::vector<double> suffix(n + 1, 0.0);
     for (uint64_t k = n; k-- > 0;) suffix[k] = suffix[k + 1] + (double)lens[order[k]];
-    const double f0 = n ? gpu_seconds(lens[order[0]], suffix[0], n, cus) : 0.0;
+    // Host-resident blobs (krk_metainfo_digest_host) all still cross PCIe for their piece
+    // CRCs, so the GPU side never beats bytes / H2D; the host hashes them in place (no D2H).
+    const double link = host_resident ? suffix[0] / kD2H : 0.0;
+    const double f0 = n ? std::max(link, gpu_seconds(lens[order[0]], suffix[0], n, cus)) : 0.0;
     double best = f0, best_g = f0, best_h = 0;
     uint64_t best_k = 0;
     if (threads > 0 && n) {
@@ -110,8 +113,8 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
             load.push(l);
             maxload = std::max(maxload, l);
             hbytes += L;
-            const double h = std::max(maxload / rh, hbytes / kD2H);
-            const double g = k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, cus) : 0.0;
+            const double h = host_resident ? maxload / rh : std::max(maxload / rh, hbytes / kD2H);
+            const double g = std::max(link, k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, cus) : 0.0);
             if (std::max(g, h) < best) {
                 best = std::max(g, h);
                 best_k = k;
@@ -227,6 +230,25 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     return KRK_OK;
 }
 
+// Hash host-resident blobs on up to `threads` threads (next-longest first); digest j to
+// out + 32 j.
+void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
+                       uint8_t* out) {
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t j; (j = next.fetch_add(1)) < ptrs.size();) {
+            uint32_t h[8];
+            memcpy(h, kIV, sizeof h);
+            host_sha256_final(h, 0, ptrs[j], lens[j], out + 32 * j);
+        }
+    };
+    const int T = (int)std::min<size_t>((size_t)std::max(threads, 1), ptrs.size());
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+}
+
 // Write host-computed digests into digests_dev (record j: 4-byte blob index, 32-byte
 // digest) on stream s: one upload + one scatter launch.
 int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,
@@ -263,7 +285,7 @@ int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int c
     KRK_CHECK(n == 0 || lengths, KRK_EINVAL, "lengths is NULL");
     KRK_CHECK(n_host, KRK_EINVAL, "n_host is NULL");
     KRK_CHECK(threads >= 0 && cus > 0, KRK_EINVAL, "threads must be >= 0 and cus > 0");
-    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, cus, gpu_seconds_out, host_seconds_out);
+    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, cus, gpu_seconds_out, host_seconds_out, false);
     *n_host = idx.size();
     if (host_idx && !idx.empty()) memcpy(host_idx, idx.data(), idx.size() * 4);
     return KRK_OK;

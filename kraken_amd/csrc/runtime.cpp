@@ -759,6 +759,34 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     std::vector<char> done(n, 0);
     hipStream_t cp = D->s_a, ks = D->s_b;
     uint64_t remaining = n;
+    // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed in
+    // place on host threads and never cross PCIe.
+    std::vector<uint32_t> host;
+    if (offload_threads() > 0) {
+        host = offload_plan(lengths, n, offload_threads(), D->cus, nullptr, nullptr, true);
+        for (uint32_t i : host) {
+            done[i] = 1;
+            --remaining;
+        }
+    }
+    std::vector<uint8_t> host_dig(32 * host.size());
+    std::thread host_th;
+    if (!host.empty())
+        host_th = std::thread([&] {
+            std::vector<const uint8_t*> p(host.size());
+            std::vector<uint64_t> l(host.size());
+            for (size_t j = 0; j < host.size(); ++j) {
+                p[j] = data_host[host[j]];
+                l[j] = lengths[host[j]];
+            }
+            offload_hash_host(p, l, offload_threads(), host_dig.data());
+        });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{host_th};
     int k = 0;
     while (!r && remaining) {
         r = pl.acquire(k);
@@ -799,6 +827,8 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
         set_error(KRK_EHIP, "digest copy-out failed");
         r = KRK_EHIP;
     }
+    if (host_th.joinable()) host_th.join();
+    for (size_t q = 0; q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
     return r;
 }
 
@@ -901,6 +931,35 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     std::vector<uint64_t> off(n, 0);
     std::vector<char> done(n, 0);
     hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
+    // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed in
+    // place on host threads while the windows below carry every blob's bytes to the
+    // piece CRCs and the others' SHA-256 to the GPU.
+    std::vector<char> on_host(n, 0);
+    std::vector<uint32_t> host;
+    if (offload_threads() > 0) {
+        std::vector<uint64_t> lens(n);
+        for (uint64_t i = 0; i < n; ++i) lens[i] = blobs[i].length;
+        host = offload_plan(lens.data(), n, offload_threads(), D->cus, nullptr, nullptr, true);
+        for (uint32_t i : host) on_host[i] = 1;
+    }
+    std::vector<uint8_t> host_dig(32 * host.size());
+    std::thread host_th;
+    if (!host.empty())
+        host_th = std::thread([&] {
+            std::vector<const uint8_t*> p(host.size());
+            std::vector<uint64_t> l(host.size());
+            for (size_t j = 0; j < host.size(); ++j) {
+                p[j] = blobs[host[j]].data;
+                l[j] = blobs[host[j]].length;
+            }
+            offload_hash_host(p, l, offload_threads(), host_dig.data());
+        });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{host_th};
     ItemBuilder B;
     uint64_t remaining = n;
     int k = 0;
@@ -928,14 +987,16 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
                 copies.push_back({w.host + fill, b.data + off[i], take});
                 B.add(items, dev, off[i], off[i] + take, b.length, (uint64_t)b.piece_length, b.sums_offset);
             }
-            ShaJob j{};
-            j.ptr = dev;
-            j.len = take;
-            j.prefix = off[i];
-            j.out = (uint32_t)i;
-            j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
-            memcpy(j.h, kIV, sizeof kIV);
-            jobs.push_back(j);
+            if (!on_host[i]) {
+                ShaJob j{};
+                j.ptr = dev;
+                j.len = take;
+                j.prefix = off[i];
+                j.out = (uint32_t)i;
+                j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
+                memcpy(j.h, kIV, sizeof kIV);
+                jobs.push_back(j);
+            }
             off[i] += take;
             fill += (take + 15) & ~uint64_t(15);
             if (fin) { done[i] = 1; --remaining; }
@@ -976,6 +1037,8 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         set_error(KRK_EHIP, "digest copy-out failed");
         r = KRK_EHIP;
     }
+    if (host_th.joinable()) host_th.join();
+    for (size_t q = 0; q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
     if (!r && hi > lo && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;

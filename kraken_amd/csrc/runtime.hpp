@@ -539,7 +539,9 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 // hashed on host threads while the GPU hashes the rest (krk_set_sha_host_offload).
 int offload_threads();
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
-                                   double* host_s);
+                                   double* host_s, bool host_resident = false);
+void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
+                       uint8_t* out);
 int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
                  hipEvent_t ready, uint8_t* out);
 int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,

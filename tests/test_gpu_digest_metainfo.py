@@ -445,3 +445,33 @@ def test_sha_host_offload_bit_exact(gpu, orc, misalign):
             assert np.array_equal(sums[o:o + len(ref)], ref), i
     finally:
         D.set_sha_host_offload(0)
+
+
+@pytest.mark.parametrize("window_mb", ["1", None])
+def test_sha_host_offload_host_buffers(gpu, orc, window_mb):
+    """The host-buffer entry points with the offload on: the longest blobs are hashed in
+    place on host threads (krk_sha256_host never uploads them; krk_metainfo_digest_host
+    still carries their bytes to the piece CRCs); digests and sums equal hashlib / oracle."""
+    rng = np.random.default_rng(31)
+    sizes = [(24 << 20) + 5, 9 << 20, 0, 1, 63, 64, 1000] + [70_000 + 13 * i for i in range(60)]
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in sizes]
+    assert set(D.sha_offload_plan(sizes, 4)[0].tolist()) >= {0, 1}
+    ptrs = (C.c_void_p * len(datas))(*[d.ctypes.data if d.size else None for d in datas])
+    lens = np.array(sizes, dtype=np.uint64)
+    want = [hashlib.sha256(d.tobytes()).digest() for d in datas]
+    if window_mb:
+        os.environ["KRK_WINDOW_MB"] = window_mb
+    try:
+        D.set_sha_host_offload(4)
+        out = np.zeros((len(datas), 32), dtype=np.uint8)
+        check(lib.krk_sha256_host(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), len(datas),
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        for i in range(len(datas)):
+            assert bytes(out[i]) == want[i], ("sha256_host", i, sizes[i])
+        sums, dg = D.metainfo_digest_host(datas, 1 << 20)
+        for i, d in enumerate(datas):
+            assert bytes(dg[i]) == want[i], ("metainfo_digest_host", i, sizes[i])
+            assert np.array_equal(sums[i], orc.calc_piece_sums(d, 1 << 20)[1]), i
+    finally:
+        D.set_sha_host_offload(0)
+        os.environ.pop("KRK_WINDOW_MB", None)
