@@ -230,6 +230,18 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     return KRK_OK;
 }
 
+void offload_teardown(Device& D) {
+    OffloadPool* P = D.offload;
+    if (!P) return;
+    for (Worker& w : P->w)
+        for (int b = 0; b < 2; ++b) {
+            if (w.s[b]) hipStreamSynchronize(w.s[b]), hipStreamDestroy(w.s[b]);
+            if (w.buf[b]) hipHostFree(w.buf[b]);
+        }
+    delete P;
+    D.offload = nullptr;
+}
+
 // Hash host-resident blobs on up to `threads` threads (next-longest first); digest j to
 // out + 32 j.
 void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,

@@ -233,6 +233,7 @@ static void teardown_device(Device& D) {
         if (s) hipStreamSynchronize(s);
     delete D.staging;  // drains its windows' events
     D.staging = nullptr;
+    offload_teardown(D);
     {
         std::lock_guard<std::mutex> g(D.cache.mu);
         for (auto& kv : D.cache.idle) {

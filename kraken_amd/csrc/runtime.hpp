@@ -540,6 +540,7 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 int offload_threads();
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
                                    double* host_s, bool host_resident = false);
+void offload_teardown(Device& D);  // krk_shutdown: the offload threads' streams and pinned buffers
 void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
                        uint8_t* out);
 int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
