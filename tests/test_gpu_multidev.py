@@ -87,3 +87,20 @@ def test_device_set_rejects_absent_device(gpu):
     bad = (C.c_int * 1)(4096)
     assert lib.krk_set_devices(bad, 1) == KRK_ENODEV
     assert D.get_devices() == [0]
+
+
+def test_metainfo_digest_host_multi_with_offload(two_workers, orc):
+    """The *_multi split with the SHA-256 host offload on: each worker's batch hands its
+    longest blobs to host threads (the two workers share one device context, so their
+    offload phases take turns on its thread pool); results equal hashlib / the oracle."""
+    rng = np.random.default_rng(9)
+    datas = [rng.integers(0, 256, L, dtype=np.uint8) for L in
+             [(20 << 20) + 1, 12 << 20, 9 << 20] + [int(x) for x in rng.integers(0, 1 << 20, 30)]]
+    try:
+        D.set_sha_host_offload(4)
+        sums, dg = D.metainfo_digest_host(datas, 1 << 20, multi=True)
+    finally:
+        D.set_sha_host_offload(0)
+    for i, d in enumerate(datas):
+        assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), i
+        assert np.array_equal(sums[i], orc.calc_piece_sums(d, 1 << 20)[1]), i
