@@ -490,25 +490,16 @@ struct TwoLaneConst {
 
 // Instruction-rounds 4q..4q+3; W of rounds 4q+1..4q+4 (for the z's).  History
 // registers rotate: in instruction-round n, x0 = R[n%4], x3 = R[(n+1)%4].
-template <int kL>
 __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
                                           const TwoLaneConst& c, uint32_t w1, uint32_t w2, uint32_t w3,
                                           uint32_t w4) {
     uint32_t t1, t2, t3, kk, p;
-    if constexpr (kL == 8)
-        asm volatile(KRK_SHA8_ROUND(R0, R3, R2, R1, w1)
-                     KRK_SHA8_ROUND(R1, R0, R3, R2, w2)
-                     KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
-                     KRK_SHA8_ROUND(R3, R2, R1, R0, w4)
-                     KRK_SHA8_OPERANDS
-                     : KRK_SHA8_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
-    else
-        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
-                     KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
-                     KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
-                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
+    asm volatile(KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
+                 KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                 KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                 KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
+                 KRK_SHA2_OPERANDS
+                 : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
     (void)t3;
 }
 
@@ -532,13 +523,12 @@ constexpr int kAhead = KRK_SHA_AHEAD;
 #define KRK_SHA8_UNROLL 2  // eight-lane consumer: blocks per loop iteration
 #endif
 static_assert(kAhead >= 2 && kAhead <= 8, "read-ahead distance");
-template <int kL>
 __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
                                         uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[kAhead]) {
     // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
     // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
     // its own starts, so A starts at (H2, H3) and its two results are replaced by
-    // H1 and H0.  kL = 2 or 8 lanes a stream (KRK_SHA2_ROUND / KRK_SHA8_ROUND).
+    // H1 and H0.
     uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z;
     // W ring: quad q lives in wq[q % kRS]
     constexpr int kRS = kAhead + 1;
@@ -552,45 +542,29 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
 #endif
     {
         uint32_t t1, t2, t3, kk, p;
-        if constexpr (kL == 8)  // the round's DPP reads come five instructions in: no s_nop
-            asm volatile("v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
-                         KRK_SHA8_ROUND(R0, R3, R2, R1, w1)
-                         KRK_SHA8_OPERANDS
-                         : KRK_SHA8_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
-        else  // s_nop 0 + the xad: two wait states before the DPP read of R3.
-            asm volatile("s_nop 0\n\t"
-                         "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
-                         KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
-                         KRK_SHA2_OPERANDS
-                         : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
+        // s_nop 0 + the xad: two wait states before the DPP read of R3.
+        asm volatile("s_nop 0\n\t"
+                     "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
+                     KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
         (void)t3;
     }
     R1 = is_e ? R1 : h[3];
     {
         uint32_t t1, t2, t3, kk, p;
-        if constexpr (kL == 8)
-            asm volatile(KRK_SHA8_ROUND(R1, R0, R3, R2, w2)
-                         KRK_SHA8_OPERANDS
-                         : KRK_SHA8_CONSTS, [w2] "v"(k[0][2]));
-        else
-            asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
-                         KRK_SHA2_OPERANDS
-                         : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
+        asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
         (void)t3;
     }
     R2 = is_e ? R2 : h[2];
     {
         uint32_t t1, t2, t3, kk, p;
-        if constexpr (kL == 8)
-            asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
-                         KRK_SHA8_ROUND(R3, R2, R1, R0, w4)
-                         KRK_SHA8_OPERANDS
-                         : KRK_SHA8_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
-        else
-            asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
-                         KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
-                         KRK_SHA2_OPERANDS
-                         : KRK_SHA2_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
+        asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
         (void)t3;
     }
 #pragma unroll
@@ -608,23 +582,17 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
         if (q >= 16 - kAhead)
             k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
         const u32x4& cur = wq[q % kRS];
-        sha2_quad<kL>(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : c.one_a);
+        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : c.one_a);
     }
     // Instruction-rounds 64, 65: A runs rounds 62, 63 into T1, T2 (W = 1 on A lanes);
     // the E lanes' registers keep their final state.
     uint32_t T1, T2;
     {
         uint32_t t1, t2, t3, kk, p;
-        if constexpr (kL == 8)
-            asm volatile(KRK_SHA8_ROUND(R0, R3, R2, T1, w)
-                         KRK_SHA8_ROUND(T1, R0, R3, T2, w)
-                         KRK_SHA8_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
-                         : KRK_SHA8_CONSTS, [w] "v"(c.one_a));
-        else
-            asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
-                         KRK_SHA2_ROUND(T1, R0, R3, T2, w)
-                         KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
-                         : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
+        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
+                     KRK_SHA2_ROUND(T1, R0, R3, T2, w)
+                     KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
+                     : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
         (void)t3;
     }
     // E: (e, f, g, h) = (R0, R3, R2, R1); A: (a, b, c, d) = (T2, T1, R0, R3) into
@@ -901,7 +869,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             uint32_t x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = h[k];
-            rounds2<2>(x, ring, cur, nxt, lane, c, is_e, kq);
+            rounds2(x, ring, cur, nxt, lane, c, is_e, kq);
             if (i < common) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) h[k] = x[k];
@@ -1100,7 +1068,6 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         for (int k = 0; k < 4; ++k) h[k] = is_e ? job.h[4 + k] : job.h[k ^ 2];
     }
     __builtin_amdgcn_s_setprio(3);
-    const uint32_t common = wave_min(live ? mine : ~0u);
     // Word offsets: E lanes read block jj of ring slot sl at column jj * 8 + me, i.e.
     // lbase + sl * kSlotWords + jj * 32; A lanes always the all-1 slot.
     // A lanes: one broadcast address in the all-1 slot, column 8 (jj + 1), 32 banks
@@ -1111,7 +1078,8 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     // voff: this lane's offset of block i (E: slot base vslot + jj * 32; A: 0)
     uint32_t voff = 0, vslot = 0, slot = 0;
     u32x4 kq[kAhead] = {};
-#ifndef KRK_SHA8_SKEW  // blocks pipelined (block8p): 64 instruction-rounds a block
+    // Blocks pipelined (block8p): 64 instruction-rounds a block; each half's chaining
+    // value lives on its own lanes (0 on the other half).
     uint32_t hE[4], hA[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1120,25 +1088,9 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     }
     const uint32_t mineE = is_e ? mine : 0u, mineA = is_e ? 0u : mine;
     uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z = 0;
-    (void)common;
     auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
         block8p(R0, R1, R2, R3, z, hE, hA, mineE, mineA, i, ring, cur, nxt, c, kq);
     };
-#else  // KRK_SHA8_SKEW (experiment build): 66 instruction-rounds a block (rounds2)
-    auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
-        uint32_t x[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = h[k];
-        rounds2<8>(x, ring, cur, nxt, lane, c, is_e, kq);
-        if (i < common) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) h[k] = x[k];
-        } else if (i < mine) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) h[k] = x[k];
-        }
-    };
-#endif
     // kU blocks an iteration (a step's 8 blocks never straddle an iteration): one block
     // an iteration ran at 52.9 MB/s a stream, two at 55.0 (fewer taken branches and
     // less loop bookkeeping per block).
@@ -1149,9 +1101,7 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + lbase + 256 * q);
-#ifndef KRK_SHA8_SKEW
         prologue8p(R0, R1, R2, R3, z, h, is_e, c, kq[0]);
-#endif
     }
     for (uint32_t i = 0; i < nb; i += kU) {
         const uint32_t jj = i & (kStep8 - 1);
@@ -1174,10 +1124,8 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             vslot = nvslot;
         }
     }
-#ifndef KRK_SHA8_SKEW
 #pragma unroll
     for (int k = 0; k < 4; ++k) h[k] = is_e ? hE[k] : hA[k];
-#endif
     if (live && pos == 0) {
         uint32_t hs[4];  // back to H order
 #pragma unroll

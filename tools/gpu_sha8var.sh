@@ -10,7 +10,7 @@ if [ "${TESTS:-1}" = 1 ]; then
   tail -2 gpurun_out/sha8_pytest.log
 fi
 out=gpurun_out/sha8var.jsonl; : > $out
-for v in prod ${VARS-skew} prod; do
+for v in prod ${VARS-} prod; do  # VARS: names of `make var` builds
   lib=kraken_amd/lib/var_$v/libkraken_hip.so; [ $v = prod ] && lib=kraken_amd/lib/libkraken_hip.so
   KRK_LIB_PATH=$lib timeout -k 10 120 python -u tools/probe_perf.py --crc-gb 0 --sha-plan ${PLAN:-5} --sha "1000:16,1000:16" \
       > gpurun_out/sha8var_$v.log 2>&1 || { tail -20 gpurun_out/sha8var_$v.log; exit 1; }
