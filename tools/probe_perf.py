@@ -68,7 +68,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--crc-gb", type=float, default=16)
     ap.add_argument("--sha", default="64:8,1024:8,4096:4,16384:1")
-    ap.add_argument("--variant", default="0")
+    ap.add_argument("--variant", default="16", help="KRK_CRC_VARIANT (production: 7, 8, 14-17; default 16)")
     ap.add_argument("--sha-plan", type=int, default=0,
                     help="krk_set_sha_plan: 0 auto, 1-4 production, 100-107 diagnostics (KRK_DIAG build, "
                          "KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so)")
