@@ -149,7 +149,8 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     }
     OffloadPool& P = *D->offload;
     std::lock_guard<std::mutex> g(P.mu);
-    const int T = (int)std::min<size_t>((size_t)threads, ptrs.size());
+    // at least one thread: the knob may have been lowered since the plan was made
+    const int T = (int)std::min<size_t>((size_t)std::max(threads, 1), ptrs.size());
     while ((int)P.w.size() < T) {
         Worker w;
         for (int b = 0; b < 2; ++b) {
