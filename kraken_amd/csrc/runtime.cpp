@@ -1099,28 +1099,42 @@ static int hexv(char c) {
     return -1;
 }
 
+// A ring's node table (label bytes, label offsets, weights) and, for the Locations
+// table, the healthy flags: ONE upload (one copy on the stream instead of four).
 struct DevNodes {
-    void* labels = nullptr;
-    void* off = nullptr;
-    void* w = nullptr;
+    void* pack = nullptr;
+    const uint8_t* labels = nullptr;
+    const uint64_t* off = nullptr;
+    const int64_t* w = nullptr;
+    const uint8_t* healthy = nullptr;
 };
 
-static int upload_nodes(Device* D, const krk_nodes* nodes, DevNodes& dn, hipStream_t s) {
+static int upload_nodes(Device* D, const krk_nodes* nodes, DevNodes& dn, hipStream_t s,
+                        const uint8_t* healthy = nullptr) {
     KRK_CHECK(nodes && nodes->n_nodes > 0 && nodes->label_off && nodes->weights, KRK_EINVAL,
               "nodes: empty or null");
     KRK_CHECK(nodes->n_nodes <= 4096, KRK_EINVAL, "more than 4096 nodes");
-    const uint64_t lb = nodes->label_off[nodes->n_nodes];
-    int r = KRK_OK;
-    if (lb) r = upload(D, nodes->labels, lb, &dn.labels, s);
-    if (!r) r = upload(D, nodes->label_off, (nodes->n_nodes + 1) * 8, &dn.off, s);
-    if (!r) r = upload(D, nodes->weights, nodes->n_nodes * 8, &dn.w, s);
-    return r;
+    const uint64_t N = nodes->n_nodes, lb = nodes->label_off[N];
+    KRK_CHECK(lb == 0 || nodes->labels, KRK_EINVAL, "nodes: labels are null");
+    const size_t o_w = (N + 1) * 8, o_lab = o_w + N * 8, o_h = o_lab + lb;  // 8-byte parts first
+    std::vector<uint8_t> pk(o_h + (healthy ? N : 0) + 1, 0);
+    memcpy(pk.data(), nodes->label_off, (N + 1) * 8);
+    memcpy(pk.data() + o_w, nodes->weights, N * 8);
+    if (lb) memcpy(pk.data() + o_lab, nodes->labels, lb);
+    if (healthy) memcpy(pk.data() + o_h, healthy, N);
+    int r = upload(D, pk.data(), pk.size(), &dn.pack, s);
+    if (r) return r;
+    const uint8_t* b = static_cast<const uint8_t*>(dn.pack);
+    dn.off = reinterpret_cast<const uint64_t*>(b);
+    dn.w = reinterpret_cast<const int64_t*>(b + o_w);
+    dn.labels = b + o_lab;
+    dn.healthy = healthy ? b + o_h : nullptr;
+    return KRK_OK;
 }
 
 static void free_nodes(Device* D, DevNodes& dn, hipStream_t s) {
-    if (dn.labels) scratch_free(D, dn.labels, s);
-    if (dn.off) scratch_free(D, dn.off, s);
-    if (dn.w) scratch_free(D, dn.w, s);
+    if (dn.pack) scratch_free(D, dn.pack, s);
+    dn = DevNodes();
 }
 
 // Order + Locations table for nk decoded keys already on the device; result rows
@@ -1130,28 +1144,23 @@ static int hrw_table_dev(Device* D, const void* d_kb, const void* d_koff, const 
                          int32_t** d_locs, uint8_t** d_counts, hipStream_t s) {
     const uint32_t N = nodes->n_nodes;
     DevNodes dn;
-    int r = upload_nodes(D, nodes, dn, s);
-    void* d_h = nullptr;
+    int r = upload_nodes(D, nodes, dn, s, healthy);
     int32_t* d_order = nullptr;
-    if (!r) r = upload(D, healthy, N, &d_h, s);
     if (!r && scratch_alloc(D, reinterpret_cast<void**>(&d_order), nk * N * 4, s) != hipSuccess) r = KRK_ENOMEM;
     if (!r && scratch_alloc(D, reinterpret_cast<void**>(d_locs), nk * row_out * 4, s) != hipSuccess) r = KRK_ENOMEM;
     if (!r && scratch_alloc(D, reinterpret_cast<void**>(d_counts), nk, s) != hipSuccess) r = KRK_ENOMEM;
     if (!r) {
-        HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), nk,
-                  static_cast<const uint8_t*>(dn.labels), static_cast<const uint64_t*>(dn.off),
-                  static_cast<const int64_t*>(dn.w), N, N, static_cast<const uint8_t*>(d_bad), d_order, nullptr};
+        HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), nk, dn.labels, dn.off,
+                  dn.w, N, N, static_cast<const uint8_t*>(d_bad), d_order, nullptr};
         hipError_t e = timed(K_HRW, s, [&] { return launch_hrw_order(a, s); });
         if (e == hipSuccess)
             e = timed(K_FILTER, s, [&] {
-                return launch_ring_filter(d_order, nk, N, static_cast<const uint8_t*>(d_h), max_replica, row_out,
-                                          *d_locs, *d_counts, s);
+                return launch_ring_filter(d_order, nk, N, dn.healthy, max_replica, row_out, *d_locs, *d_counts, s);
             });
         if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
     free_nodes(D, dn, s);
-    for (void* p : {d_h, static_cast<void*>(d_order)})
-        if (p) scratch_free(D, p, s);
+    if (d_order) scratch_free(D, d_order, s);
     return r;
 }
 
@@ -1211,9 +1220,8 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
     if (!r && scores_out && scratch_alloc(D, reinterpret_cast<void**>(&d_sc), n_keys * N * 8, s) != hipSuccess)
         r = KRK_ENOMEM;
     if (!r) {
-        HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), n_keys,
-                  static_cast<const uint8_t*>(dn.labels), static_cast<const uint64_t*>(dn.off),
-                  static_cast<const int64_t*>(dn.w), N, n_out, static_cast<const uint8_t*>(d_bad), d_order, d_sc};
+        HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), n_keys, dn.labels, dn.off,
+                  dn.w, N, n_out, static_cast<const uint8_t*>(d_bad), d_order, d_sc};
         hipError_t e = n_out ? timed(K_HRW, s, [&] { return launch_hrw_order(a, s); }) : hipSuccess;
         if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
     }
