@@ -519,6 +519,9 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
 #define KRK_SHA_AHEAD 3
 #endif
 constexpr int kAhead = KRK_SHA_AHEAD;
+#ifndef KRK_SHA2_PIPELINED
+#define KRK_SHA2_PIPELINED 1  // two-lane consumer: blocks pipelined (block2p) instead of rounds2
+#endif
 #ifndef KRK_SHA8_UNROLL
 #define KRK_SHA8_UNROLL 2  // eight-lane consumer: blocks per loop iteration
 #endif
@@ -602,8 +605,6 @@ __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint
     h[2] += is_e ? R2 : T2;
     h[3] += is_e ? R1 : T1;
 }
-#undef KRK_SHA2_OPERANDS
-#undef KRK_SHA2_CONSTS
 
 // Rounds n = 4j + 2 .. 4j + 5 of an eight-lane block (block8p), the register roles of
 // instruction-rounds 2 .. 5: W operands are W[n + 1] for the z of the next round.
@@ -746,6 +747,155 @@ __device__ __forceinline__ void prologue8p(uint32_t& R0, uint32_t& R1, uint32_t&
     }
     R2 = is_e ? R2 : h[2];
 }
+// Two-lane counterparts (block2p, sha2_quad2, prologue2p): the same pipelined block on
+// the two-lane round (KRK_SHA2_ROUND, partner lane by row_mirror), 64 instruction-rounds
+// a block instead of rounds2's 66.  The two-lane round opens with its DPP add, so the
+// F2 compensation of z is folded into round 64's W operand (w1 + c2) instead of being
+// added between rounds 64 and 65.
+// Rounds n = 4j + 2 .. 4j + 5 of a two-lane block (block2p), the register roles of
+// instruction-rounds 2 .. 5: W operands are W[n + 1] for the z of the next round.
+__device__ __forceinline__ void sha2_quad2(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                           const TwoLaneConst& c, uint32_t w1, uint32_t w2, uint32_t w3,
+                                           uint32_t w4) {
+    uint32_t t1, t2, t3, kk, p;
+    asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w1) KRK_SHA2_ROUND(R3, R2, R1, R0, w2)
+                 KRK_SHA2_ROUND(R0, R3, R2, R1, w3) KRK_SHA2_ROUND(R1, R0, R3, R2, w4)
+                 KRK_SHA2_OPERANDS
+                 : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
+}
+
+// Eight lanes a stream, blocks pipelined: the A quad runs rounds 62, 63 of block i
+// while the E quad already runs rounds 0, 1 of block i + 1, so a block costs 64
+// instruction-rounds instead of 66.  State crosses blocks in registers: R0..R3 (the
+// history, same register roles as rounds2), z, and each half's chaining value hE
+// (E quads: H4..H7, 0 on A lanes) / hA (A quads: H2, H3, H0, H1, 0 on E lanes) --
+// masked to its own quad so that one unmasked add feeds one half forward and adds 0
+// to the other.  Per block (instruction-rounds n = 2 .. 65 of block i):
+//   n = 2 .. 63: both halves (E round n, A round n - 2);
+//   F1 (E finished block i): R += hE (E's feed-forward); E's round 0 of block i + 1
+//      reads d through the cross add as A's raw a61, so its z also takes the A
+//      half's H3 (partner's hA[1], via DPP) and the feed-forward of h (hE[3]); A's
+//      rounds 62, 63 read e63, e64 through the cross add from registers E has just
+//      fed forward, so A's z gives back H5 now and H4 after n = 64;
+//      hE <- R where i < this stream's block count;
+//   n = 64: E round 0 of block i + 1 (W = its KW0 .. KW1), A round 62;
+//   F2: E's round 1 reads raw a62 as d: z += partner's hA[0] (H2); A: z -= H4
+//      (both in one register cc formed in F1);
+//   n = 65: E round 1, A round 63;
+//   F3 (A finished block i): A's round 0 of block i + 1 takes -d from z formed on raw
+//      a61: z -= hA[1]; R += hA; hA <- R where i < the block count.
+// A finished stream's lanes keep computing on garbage; their hE / hA stay frozen.
+__device__ __forceinline__ void block2p(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                        uint32_t hE[4], uint32_t hA[4], uint32_t mineE, uint32_t mineA,
+                                        uint32_t i, const uint32_t* lds, uint32_t cbase, uint32_t nbase,
+                                        const TwoLaneConst& c, u32x4 k[kAhead]) {
+    constexpr int kRS = kAhead + 1;
+    u32x4 wq[kRS];
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) wq[j] = k[j];
+    // Rounds n = 2 .. 61 in 15 asm blocks of four, n = 4j + 2 .. 4j + 5 (W: quad j's last
+    // word, quad j + 1's first three), each W read between two blocks -- two rounds into
+    // a W quad.  Issued right before a W quad's rounds a read cost ~16 cycles of the
+    // wave's stream, two rounds in ~8, its code bytes (tools/micro/sha8lds.hip,
+    // profiles/r02/micro_sha8lds.txt); and the read + its wait between two asm blocks
+    // are the two wait states the hazard recognizer would otherwise pad there.
+#pragma unroll
+    for (int j = 0; j < 15; ++j) {
+#ifdef KRK_SHA_NOLDS
+        if (j + kAhead < 16) wq[(j + kAhead) % kRS] = u32x4{(uint32_t)j, cbase, 5u, 7u};
+        else k[j + kAhead - 16] = u32x4{(uint32_t)j, nbase, 5u, 7u};
+#else
+        if (j + kAhead < 16)
+            wq[(j + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (j + kAhead));
+        else  // the next block's first quads
+            k[j + kAhead - 16] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (j + kAhead - 16));
+#endif
+        const u32x4& a = wq[j % kRS];
+        const u32x4& b = wq[(j + 1) % kRS];
+        sha2_quad2(R0, R1, R2, R3, z, c, a[3], b[0], b[1], b[2]);
+    }
+#ifdef KRK_SHA_NOLDS
+    k[kAhead - 1] = u32x4{15u, nbase, 5u, 7u};
+#else
+    k[kAhead - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead - 1));
+#endif
+    {
+        uint32_t t1, t2, t3, kk, p;  // n = 62, 63
+        asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
+                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w3] "v"(wq[15 % kRS][3]), [w4] "v"(k[0][0]));
+    }
+    {
+        // F1, n = 64, F2, n = 65, F3.  The cross terms go through one DPP each: every
+        // lane forms hA - hE of its own (E lanes: -hE, A lanes: hA) and reads its
+        // partner's, so E picks up the A half's H2 / H3 and A gives back E's H4 / H5.
+        // (v_subrev_u32_dpp swizzles its second operand on gfx950, tools/micro/dppsem.hip,
+        // so it is not used.)  Every VGPR a DPP instruction reads is written at least two
+        // instructions earlier.
+        uint32_t t1, t2, t3, kk, p, cc, dd, c2, w1c;
+        asm volatile("v_sub_u32_e32 %[cc], %[a0], %[e0]\n\t"   // own hA0 - hE0
+                     "v_sub_u32_e32 %[dd], %[a1], %[e1]\n\t"   // own hA1 - hE1
+                     "v_add_u32_e32 %[R0], %[e0], %[R0]\n\t"
+                     "v_add_u32_e32 %[R3], %[e1], %[R3]\n\t"
+                     "v_mov_b32_dpp %[c2], %[cc] row_mirror row_mask:0xf bank_mask:0xf\n\t"  // E: H2 of A, A: -H4
+                     "v_add_u32_dpp %[z], %[dd], %[z] row_mirror row_mask:0xf bank_mask:0xf\n\t"  // E: +H3 of A, A: -H5
+                     "v_add_u32_e32 %[R2], %[e2], %[R2]\n\t"
+                     "v_add_u32_e32 %[R1], %[e3], %[R1]\n\t"
+                     "v_add_u32_e32 %[z], %[e3], %[z]\n\t"
+                     "v_cmp_lt_u32_e32 vcc, %[i], %[mineE]\n\t"
+                     "v_cndmask_b32_e32 %[e0], %[e0], %[R0], vcc\n\t"
+                     "v_cndmask_b32_e32 %[e1], %[e1], %[R3], vcc\n\t"
+                     "v_cndmask_b32_e32 %[e2], %[e2], %[R2], vcc\n\t"
+                     "v_cndmask_b32_e32 %[e3], %[e3], %[R1], vcc\n\t"
+                     "v_add_u32_e32 %[w1c], %[c2], %[w1]\n\t"  // F2 folded into round 64's W
+                     KRK_SHA2_ROUND(R0, R3, R2, R1, w1c)
+                     KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                     "v_sub_u32_e32 %[z], %[z], %[a1]\n\t"
+                     "v_add_u32_e32 %[R0], %[a0], %[R0]\n\t"
+                     "v_add_u32_e32 %[R3], %[a1], %[R3]\n\t"
+                     "v_add_u32_e32 %[R2], %[a2], %[R2]\n\t"
+                     "v_add_u32_e32 %[R1], %[a3], %[R1]\n\t"
+                     "v_cmp_lt_u32_e32 vcc, %[i], %[mineA]\n\t"
+                     "v_cndmask_b32_e32 %[a0], %[a0], %[R0], vcc\n\t"
+                     "v_cndmask_b32_e32 %[a1], %[a1], %[R3], vcc\n\t"
+                     "v_cndmask_b32_e32 %[a2], %[a2], %[R2], vcc\n\t"
+                     "v_cndmask_b32_e32 %[a3], %[a3], %[R1], vcc\n\t"
+                     : [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [k] "=&v"(kk), [p] "=&v"(p), [cc] "=&v"(cc),
+                       [dd] "=&v"(dd), [c2] "=&v"(c2), [w1c] "=&v"(w1c), [z] "+v"(z),
+                       [R0] "+v"(R0), [R1] "+v"(R1), [R2] "+v"(R2), [R3] "+v"(R3), [e0] "+v"(hE[0]),
+                       [e1] "+v"(hE[1]), [e2] "+v"(hE[2]), [e3] "+v"(hE[3]), [a0] "+v"(hA[0]), [a1] "+v"(hA[1]),
+                       [a2] "+v"(hA[2]), [a3] "+v"(hA[3])
+                     : KRK_SHA2_CONSTS, [w1] "v"(k[0][1]), [w2] "v"(k[0][2]), [i] "s"(i), [mineE] "v"(mineE),
+                       [mineA] "v"(mineA)
+                     : "vcc");
+    }
+}
+
+// Instruction-rounds 0, 1 of a stream's first block (E rounds 0, 1; A idles and its
+// two results are replaced by H1, H0: rounds2's start).
+__device__ __forceinline__ void prologue2p(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                           const uint32_t h[4], bool is_e, const TwoLaneConst& c,
+                                           const u32x4& k0) {
+    {
+        uint32_t t1, t2, t3, kk, p;
+        asm volatile("s_nop 0\n\t"
+                     "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
+                     KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w0] "v"(k0[0]), [w1] "v"(k0[1]));
+    }
+    R1 = is_e ? R1 : h[3];
+    {
+        uint32_t t1, t2, t3, kk, p;
+        asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
+                     KRK_SHA2_OPERANDS
+                     : KRK_SHA2_CONSTS, [w2] "v"(k0[2]));
+    }
+    R2 = is_e ? R2 : h[2];
+}
+#undef KRK_SHA2_OPERANDS
+#undef KRK_SHA2_CONSTS
 #undef KRK_SHA8_OPERANDS
 #undef KRK_SHA8_CONSTS
 
@@ -865,6 +1015,22 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
         uint64_t cyc_bar = 0, cyc_rounds = 0;
 #endif
+#if KRK_SHA2_PIPELINED
+        // Blocks pipelined (block2p): 64 instruction-rounds a block, each half's chaining
+        // value on its own lanes (0 on the other half).
+        uint32_t hE[4], hA[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            hE[k] = is_e ? h[k] : 0u;
+            hA[k] = is_e ? 0u : h[k];
+        }
+        const uint32_t mineE = is_e ? mine : 0u, mineA = is_e ? 0u : mine;
+        uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z = 0;
+        (void)common;
+        auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
+            block2p(R0, R1, R2, R3, z, hE, hA, mineE, mineA, i, ring, cur, nxt, c, kq);
+        };
+#else
         auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
             uint32_t x[4];
 #pragma unroll
@@ -878,15 +1044,23 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
                 for (int k = 0; k < 4; ++k) h[k] = x[k];
             }
         };
+#endif
+        if (nb) {  // step 0's barrier, the first quads, and (pipelined) rounds 0, 1 of block 0
+            if (kTiming == 0) __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
+#if KRK_SHA2_PIPELINED
+            prologue2p(R0, R1, R2, R3, z, h, is_e, c, kq[0]);
+#endif
+        }
         for (uint32_t i = 0; i < nb; i += 2) {
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb0 = __builtin_amdgcn_s_memtime();
 #endif
-            if (kTiming == 0) __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (i == 0) {
-#pragma unroll
-                for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
+            if (i) {
+                if (kTiming == 0) __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
             }
 #ifdef KRK_SHA_CYCLES
             const uint64_t cb1 = __builtin_amdgcn_s_memtime();
@@ -908,6 +1082,10 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             printf("KRK_SHA_CYCLES timing=%d two=1 blocks=%u cycles/block=%.1f barrier+setup=%.1f rounds2=%.1f\n",
                    kTiming, nb, (double)(__builtin_amdgcn_s_memtime() - cyc0) / nb, (double)cyc_bar / nb,
                    (double)cyc_rounds / nb);
+#endif
+#if KRK_SHA2_PIPELINED
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = is_e ? hE[k] : hA[k];
 #endif
         if (live) {
             uint32_t hs[4];  // back to H order (A lanes hold H[k ^ 2] in h[k])

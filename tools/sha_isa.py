@@ -25,9 +25,10 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 KERNEL = "sha256_ws_kernel<0, true, 1>"  # two lanes per stream
 KERNELS = {2: KERNEL, 8: "sha256_w8_kernel<0, 1>"}
 # the one cross-lane add of every instruction-round, and the VALU ops of a round
-ROUND_MARK = {2: "row_mirror", 8: "quad_perm:[1,2,0,3]"}
+ROUND_MARK = {2: "bitop3:0x96", 8: "quad_perm:[1,2,0,3]"}  # once per instruction-round
+SELECT_MARK = {2: "row_mirror", 8: "quad_perm:[1,2,0,3]"}  # only in consumer code (finds its loop)
 ROUND_OPS = {2: 9, 8: 8}
-ROUNDS_PER_BLOCK = {2: 66, 8: 64}  # the eight-lane consumer pipelines blocks (block8p)
+ROUNDS_PER_BLOCK = {2: 64, 8: 64}  # both consumers pipeline blocks (block2p, block8p)
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
@@ -55,7 +56,7 @@ def _disasm(lib_path: str, kernel: str = KERNEL) -> str:
 
 
 def count(lib_path: str, lanes: int = 2) -> dict:
-    kernel, mark = KERNELS[lanes], ROUND_MARK[lanes]
+    kernel, mark, sel = KERNELS[lanes], ROUND_MARK[lanes], SELECT_MARK[lanes]
     lines = _disasm(lib_path, kernel).splitlines()
     head = [i for i, l in enumerate(lines) if l.endswith(">:") and kernel in l][0]
     nxt = [i for i, l in enumerate(lines) if i > head and l.endswith(">:")]
@@ -77,8 +78,8 @@ def count(lib_path: str, lanes: int = 2) -> dict:
                 loops.append(loop)
     # the consumer's step loop: the shortest loop holding the most rounds (an inner
     # back-edge that re-runs only part of a step does not count as the step)
-    most = max(sum(mark in x[1] for x in lp) for lp in loops)
-    loop = min((lp for lp in loops if sum(mark in x[1] for x in lp) == most), key=len)
+    most = max(sum(sel in x[1] for x in lp) for lp in loops)
+    loop = min((lp for lp in loops if sum(sel in x[1] for x in lp) == most), key=len)
     dpp = sum(mark in x[1] for x in loop)
     blocks = dpp // ROUNDS_PER_BLOCK[lanes]
     assert blocks >= 1 and dpp == ROUNDS_PER_BLOCK[lanes] * blocks, dpp
