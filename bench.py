@@ -237,7 +237,7 @@ class Timer:
 
 
 def roofline_obj(kernel, gbps, avg_ms, bytes_launch, traffic):
-    return {"kernel": kernel, "bound": "hbm", "achieved": round(gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(gbps / HBM_PEAK_GBPS, 5), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
             "algorithmic_bytes_per_launch": bytes_launch}
 
@@ -248,7 +248,7 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
     HBM fraction is kept beside it."""
     lanes = D.sha_lanes_per_stream(n)
     per_stream = max(lens) / (avg_ms / 1e3) / 1e6
-    roof = {"kernel": "sha256_multi", "bound": "valu", "achieved": round(gbps, 2),
+    roof = {"kernel": "sha256_multi", "bound": "valu", "achieved": round(gbps, 4),
             "peak": None, "unit": "GB/s", "frac": None, "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
             "algorithmic_bytes_per_launch": bytes_launch,
             "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5)}}
@@ -265,7 +265,7 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
                                           "cycles per VALU for a lone wave (MI355X_MICROARCH.md:489) at the "
                                           "shader clock measured beside a SHA launch (krk_device_clock_mhz)")})
             peak = n * ceil / 1e3
-            roof.update({"peak": round(peak, 2), "frac": round(gbps / peak, 4)})
+            roof.update({"peak": round(peak, 4), "frac": round(gbps / peak, 4)})
             import sha_isa
             fc = sha_isa.fetch_ceiling_mbps(isa, mhz)
             ib["fetch_bound"] = {"code_bytes_per_block": isa["code_bytes_per_block"],
