@@ -611,8 +611,43 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
     if out is not None and Le == int(arena.lengths[0]) and (arena.lengths == Le).all():  # whole blobs
         dev_dg = out.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
         res["digests_match_device_run"] = bool(np.array_equal(dg, dev_dg))
+    hyb = [host_hybrid(D, T, datas, P, thr, sums, dg, world) for thr in E2E_HYBRID_THREADS]
+    if hyb:
+        res["host_hybrid"] = hyb[0] if len(hyb) == 1 else hyb
     del datas
     return res
+
+
+# Host threads of the end-to-end leg's hybrid pass (KRK_BENCH_HYBRID="8,16"; "" = none).
+E2E_HYBRID_THREADS = [int(x) for x in os.environ.get("KRK_BENCH_HYBRID", "4").split(",") if x.strip()]
+
+
+def host_hybrid(D, T, datas, P, thr, sums_gpu, dg_gpu, world):
+    """The end-to-end batch again with krk_set_sha_host_offload(thr): the planner hands the
+    host the blobs the link would carry past the GPU's own chain time; those are hashed
+    and piece-summed in place on host threads and never uploaded, the rest go through
+    the windows as before.  Reported beside the GPU-only end-to-end figure, with the
+    outputs checked equal to it."""
+    lens = [int(d.size) for d in datas]
+    idx, g_s, h_s = D.sha_offload_plan(lens, thr, mode=D.OFFLOAD_HOST_WHOLE)
+    passes = []
+    D.set_sha_host_offload(thr)
+    try:
+        for _ in range(E2E_PASSES):
+            T.barrier()
+            t0 = time.perf_counter()
+            sums, dg = D.metainfo_digest_host(datas, P)
+            passes.append(T.max_over_ranks(time.perf_counter() - t0))
+    finally:
+        D.set_sha_host_offload(0)
+    el = float(np.median(passes))
+    same = bool(np.array_equal(dg, dg_gpu)) and all(np.array_equal(a, b) for a, b in zip(sums, sums_gpu))
+    return {"threads": thr, "value": round(world * sum(lens) / el / 1e9, 3), "unit": "GB/s",
+            "seconds": round(el, 3), "passes_s": [round(x, 3) for x in passes], "blobs_on_host": int(idx.size),
+            "model_s": {"gpu": round(g_s, 3), "host": round(h_s, 3)}, "outputs_match_gpu_only": same,
+            "what": "krk_metainfo_digest_host with krk_set_sha_host_offload(threads): the planner's blobs are "
+                    "hashed and piece-summed in place on host threads and never cross PCIe, the rest as in the "
+                    "GPU-only pass (DESIGN.md 4.5); median of the passes"}
 
 
 def run_pieces(a, D, T, rank, world, res):

@@ -403,14 +403,25 @@ int krk_set_sha_plan(int plan);
  * is 0 unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host,
  * 1,000 equal 100 MiB blobs (C2) stay on the GPU.  The call then returns after the host
  * part is hashed (the GPU part stays asynchronous on `stream`).  The host-buffer entry
- * points (krk_sha256_host, krk_metainfo_digest_host) hash their offloaded blobs in place:
- * no device round trip, and krk_sha256_host does not upload them at all. */
+ * points work on their offloaded blobs in place and never upload them: krk_sha256_host
+ * hashes them, krk_metainfo_digest_host hashes them AND computes their piece sums (the
+ * SHA-256 pass and the CRC pass of a blob are separate host tasks), so the bytes that
+ * cross the host link shrink by theirs (the threshold there is 3 %). */
 int krk_set_sha_host_offload(int threads);
 /* The offload plan for `n` blob lengths on `threads` host threads and a device of `cus`
  * CUs, without a device: the indices (longest first) to host_idx (room for n, may be
- * NULL), their count to n_host, and the modelled GPU / host seconds (may be NULL). */
+ * NULL), their count to n_host, and the modelled GPU / host seconds (may be NULL).
+ * krk_sha_offload_plan plans a device-resident batch (krk_sha256_dev,
+ * krk_metainfo_digest_dev); krk_host_offload_plan plans for `mode`
+ * KRK_OFFLOAD_DEVICE (the same), KRK_OFFLOAD_HOST_SHA (krk_sha256_host) or
+ * KRK_OFFLOAD_HOST_WHOLE (krk_metainfo_digest_host). */
+#define KRK_OFFLOAD_DEVICE 0
+#define KRK_OFFLOAD_HOST_SHA 1
+#define KRK_OFFLOAD_HOST_WHOLE 2
 int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
                          uint64_t* n_host, double* gpu_seconds, double* host_seconds);
+int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, int mode, uint32_t* host_idx,
+                          uint64_t* n_host, double* gpu_seconds, double* host_seconds);
 
 #ifdef __cplusplus
 }

@@ -128,6 +128,8 @@ def _load() -> C.CDLL:
         "krk_set_sha_host_offload": (i, [i]),
         "krk_sha_offload_plan": (i, [C.POINTER(C.c_uint64), C.c_uint64, i, i, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+        "krk_host_offload_plan": (i, [C.POINTER(C.c_uint64), C.c_uint64, i, i, i, C.POINTER(C.c_uint32),
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "krk_set_timing": (i, [i]),
         "krk_sha_lanes_per_stream": (i, [C.c_uint64, C.POINTER(C.c_int)]),
         "krk_kernel_stats": (i, [C.c_char_p, u64p, f64p]),

@@ -1,5 +1,6 @@
-// offload.cpp -- host offload of the longest SHA-256 chains of a device-resident batch
-// (krk_set_sha_host_offload; used by krk_sha256_dev and krk_metainfo_digest_dev).
+// offload.cpp -- host offload of the longest SHA-256 chains of a batch
+// (krk_set_sha_host_offload; used by krk_sha256_dev / krk_metainfo_digest_dev on blobs in
+// HBM and by krk_sha256_host / krk_metainfo_digest_host on blobs in host memory).
 //
 // SHA-256 is one sequential chain per blob (core/digester.go:28-72).  A GPU stream runs
 // at ~56 MB/s (eight lanes), one x86 core with the SHA extensions at
@@ -9,6 +10,10 @@
 // hashes the rest and the piece CRCs of every blob.  The planner picks how many of the
 // longest blobs go to the host by minimising max(GPU time, host time); a batch of equal
 // blobs (C2) gains nothing (the GPU's chain is the same blob length) and stays on the GPU.
+// Blobs in host memory are worked on in place, never uploaded; krk_metainfo_digest_host's
+// host blobs get their piece sums on the host too, which takes their bytes off the host
+// link -- C2 end-to-end, link-bound, then hands the host the blobs the link would carry
+// past the GPU's own chain time.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -22,6 +27,7 @@ namespace krk {
 
 void host_sha256_blocks(uint32_t h[8], const uint8_t* p, size_t nblocks);
 void host_sha256_final(const uint32_t h[8], uint64_t absorbed, const uint8_t* tail, size_t n, uint8_t out[32]);
+uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);
 
 namespace {
 
@@ -29,20 +35,33 @@ std::atomic<int> g_off_threads{0};
 
 constexpr uint64_t kOffChunk = 8ull << 20;  // D2H chunk (multiple of 64)
 constexpr double kD2H = 50e9;               // device -> pinned host, bytes/s (PCIe Gen5 x16, measured 54)
+// Host-resident batches: pageable -> pinned copy + H2D through the staging windows,
+// bytes/s (C2 end-to-end measured 39.5-54.4 GB/s box to box).
+constexpr double kLinkHost = 45e9;
 
-// One host thread hashing, bytes/s: measured once (16 MiB) and derated for the clock a
-// fully loaded socket holds.
+// One host thread, bytes/s: measured once (16 MiB) and derated for the clock a fully
+// loaded socket holds.  SHA-256 (x86 SHA extensions) and the piece CRC (PCLMUL folding).
+double time_rate(const std::function<void(const uint8_t*, size_t)>& f) {
+    std::vector<uint8_t> buf(16u << 20, 0x5a);
+    f(buf.data(), 64 << 10);  // warm
+    const auto t0 = std::chrono::steady_clock::now();
+    f(buf.data(), buf.size());
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0.85 * buf.size() / std::max(s, 1e-6);
+}
 double host_rate() {
-    static const double r = [] {
-        std::vector<uint8_t> buf(16u << 20, 0x5a);
+    static const double r = time_rate([](const uint8_t* p, size_t n) {
         uint32_t h[8];
         memcpy(h, kIV, sizeof h);
-        host_sha256_blocks(h, buf.data(), 1024);  // warm
-        const auto t0 = std::chrono::steady_clock::now();
-        host_sha256_blocks(h, buf.data(), buf.size() / 64);
-        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        return 0.85 * buf.size() / std::max(s, 1e-6);
-    }();
+        host_sha256_blocks(h, p, n / 64);
+    });
+    return r;
+}
+double host_crc_rate() {
+    static const double r = time_rate([](const uint8_t* p, size_t n) {
+        volatile uint32_t c = host_crc32_update(0, p, n);
+        (void)c;
+    });
     return r;
 }
 
@@ -86,35 +105,47 @@ struct OffloadPool {
 };
 
 // The longest blobs to hash on `threads` host threads (indices into lens, longest
-// first); empty when the host would not shorten the batch by at least 10 %.
+// first); empty when the host would not shorten the batch by at least 10 % (device-
+// resident: the host's D2H reads share the PCIe link and the chip's memory with the
+// GPU part) or 3 % (host-resident: the host's blobs simply stay off the link).
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
-                                   double* host_s, bool host_resident) {
+                                   double* host_s, int mode) {
     std::vector<uint32_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
     std::vector<double> suffix(n + 1, 0.0);
     for (uint64_t k = n; k-- > 0;) suffix[k] = suffix[k + 1] + (double)lens[order[k]];
-    // Host-resident blobs (krk_metainfo_digest_host) all still cross PCIe for their piece
-    // CRCs, so the GPU side never beats bytes / H2D; the host hashes them in place (no D2H).
-    const double link = host_resident ? suffix[0] / kD2H : 0.0;
-    const double f0 = n ? std::max(link, gpu_seconds(lens[order[0]], suffix[0], n, cus)) : 0.0;
+    // GPU side with blobs k.. on the GPU: their longest chain / the chip's SHA rate, and for
+    // host-resident batches their bytes over the host link (the host's blobs never cross).
+    auto gpu_side = [&](uint64_t k) {
+        double g = k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, cus) : 0.0;
+        if (mode != kOffDevice) g = std::max(g, suffix[k] / kLinkHost);
+        return g;
+    };
+    const double f0 = n ? gpu_side(0) : 0.0;
     double best = f0, best_g = f0, best_h = 0;
     uint64_t best_k = 0;
     if (threads > 0 && n) {
-        const double rh = host_rate();
+        const double rs = host_rate(), rc = mode == kOffHostWhole ? host_crc_rate() : 0.0;
+        // LPT over host threads of the tasks, in seconds: a SHA-256 pass per blob, and in
+        // kOffHostWhole a piece-CRC pass per blob as its own task.
         std::priority_queue<double, std::vector<double>, std::greater<double>> load;
         for (int t = 0; t < threads; ++t) load.push(0.0);
         double maxload = 0, hbytes = 0;
-        for (uint64_t k = 1; k <= n; ++k) {
-            const double L = (double)lens[order[k - 1]];
-            if (L == 0) break;  // empty blobs are not worth a thread
-            const double l = load.top() + L;
+        auto put = [&](double sec) {
+            const double l = load.top() + sec;
             load.pop();
             load.push(l);
             maxload = std::max(maxload, l);
+        };
+        for (uint64_t k = 1; k <= n; ++k) {
+            const double L = (double)lens[order[k - 1]];
+            if (L == 0) break;  // empty blobs are not worth a thread
+            put(L / rs);
+            if (mode == kOffHostWhole) put(L / rc);
             hbytes += L;
-            const double h = host_resident ? maxload / rh : std::max(maxload / rh, hbytes / kD2H);
-            const double g = std::max(link, k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, cus) : 0.0);
+            const double h = mode == kOffDevice ? std::max(maxload, hbytes / kD2H) : maxload;
+            const double g = gpu_side(k);
             if (std::max(g, h) < best) {
                 best = std::max(g, h);
                 best_k = k;
@@ -123,7 +154,7 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
             }
             if (h > f0) break;  // the host alone is already slower than no offload
         }
-        if (best > 0.9 * f0) {
+        if (best > (mode == kOffDevice ? 0.9 : 0.97) * f0) {
             best_k = 0;
             best_g = f0;
             best_h = 0;
@@ -262,6 +293,43 @@ void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vecto
     for (auto& th : pool) th.join();
 }
 
+void offload_whole_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens,
+                        const std::vector<uint64_t>& plen, const std::vector<uint32_t*>& sums, int threads,
+                        uint8_t* out) {
+    // Task t: blob t / 2, its SHA-256 pass (even t) or its piece-CRC pass (odd t), in
+    // order of cost (the CRC pass runs ~6x the SHA-256 rate on one core).
+    const double rs = host_rate(), rc = host_crc_rate();
+    std::vector<std::pair<double, size_t>> tasks;
+    tasks.reserve(2 * ptrs.size());
+    for (size_t j = 0; j < ptrs.size(); ++j) {
+        tasks.push_back({lens[j] / rs, 2 * j});
+        if (lens[j]) tasks.push_back({lens[j] / rc, 2 * j + 1});  // an empty blob has no pieces
+    }
+    std::stable_sort(tasks.begin(), tasks.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t q; (q = next.fetch_add(1)) < tasks.size();) {
+            const size_t j = tasks[q].second / 2;
+            const uint8_t* p = ptrs[j];
+            const uint64_t L = lens[j];
+            if (tasks[q].second % 2 == 0) {
+                uint32_t h[8];
+                memcpy(h, kIV, sizeof h);
+                host_sha256_final(h, 0, p, L, out + 32 * j);
+            } else {
+                // core/metainfo.go:157-179: piece i = bytes [iP, min((i+1)P, L)), crc32 each
+                const uint64_t P = plen[j];
+                for (uint64_t o = 0, i = 0; o < L; o += P, ++i) sums[j][i] = host_crc32_update(0, p + o, std::min(P, L - o));
+            }
+        }
+    };
+    const int T = (int)std::min<size_t>((size_t)std::max(threads, 1), tasks.size());
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+}
+
 // Write host-computed digests into digests_dev (record j: 4-byte blob index, 32-byte
 // digest) on stream s: one upload + one scatter launch.
 int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,
@@ -293,15 +361,25 @@ int krk_set_sha_host_offload(int threads) {
     return KRK_OK;
 }
 
-int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
-                         uint64_t* n_host, double* gpu_seconds_out, double* host_seconds_out) {
+int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, int mode, uint32_t* host_idx,
+                          uint64_t* n_host, double* gpu_seconds_out, double* host_seconds_out) {
     KRK_CHECK(n == 0 || lengths, KRK_EINVAL, "lengths is NULL");
     KRK_CHECK(n_host, KRK_EINVAL, "n_host is NULL");
     KRK_CHECK(threads >= 0 && cus > 0, KRK_EINVAL, "threads must be >= 0 and cus > 0");
-    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, cus, gpu_seconds_out, host_seconds_out, false);
+    static_assert(KRK_OFFLOAD_DEVICE == kOffDevice && KRK_OFFLOAD_HOST_SHA == kOffHostSha &&
+                      KRK_OFFLOAD_HOST_WHOLE == kOffHostWhole,
+                  "offload modes");
+    KRK_CHECK(mode >= KRK_OFFLOAD_DEVICE && mode <= KRK_OFFLOAD_HOST_WHOLE, KRK_EINVAL, "offload mode %d", mode);
+    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, cus, gpu_seconds_out, host_seconds_out, mode);
     *n_host = idx.size();
     if (host_idx && !idx.empty()) memcpy(host_idx, idx.data(), idx.size() * 4);
     return KRK_OK;
+}
+
+int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
+                         uint64_t* n_host, double* gpu_seconds_out, double* host_seconds_out) {
+    return krk_host_offload_plan(lengths, n, threads, cus, KRK_OFFLOAD_DEVICE, host_idx, n_host, gpu_seconds_out,
+                                 host_seconds_out);
 }
 
 }  // extern "C"

@@ -764,7 +764,7 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     // place on host threads and never cross PCIe.
     std::vector<uint32_t> host;
     if (offload_threads() > 0) {
-        host = offload_plan(lengths, n, offload_threads(), D->cus, nullptr, nullptr, true);
+        host = offload_plan(lengths, n, offload_threads(), D->cus, nullptr, nullptr, kOffHostSha);
         for (uint32_t i : host) {
             done[i] = 1;
             --remaining;
@@ -912,12 +912,24 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     uint64_t lo, hi;
     sums_span(blobs, n, &lo, &hi);
     KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
+    // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed and
+    // piece-summed in place on host threads and never cross the host link; the windows
+    // below carry the others' bytes to both kernels.
+    std::vector<char> on_host(n, 0);
+    std::vector<uint32_t> host;
+    if (offload_threads() > 0) {
+        std::vector<uint64_t> lens(n);
+        for (uint64_t i = 0; i < n; ++i) lens[i] = blobs[i].length;
+        host = offload_plan(lens.data(), n, offload_threads(), D->cus, nullptr, nullptr, kOffHostWhole);
+        for (uint32_t i : host) on_host[i] = 1;
+    }
+    const uint64_t n_gpu = n - host.size();
     const size_t W = window_bytes();
     // Every unfinished blob contributes up to C bytes per window, so the SHA
     // streams all advance together (multiple of 64: only final chunks are partial).
-    uint64_t C = (W / n) & ~uint64_t(63);
+    uint64_t C = (W / std::max<uint64_t>(n_gpu, 1)) & ~uint64_t(63);
     if (C < 64) C = 64;
-    const size_t cap = std::max<size_t>(W, C * n + 16 * n);
+    const size_t cap = std::max<size_t>(W, C * n_gpu + 16 * n_gpu);
     StagingLease lease;
     r = lease_staging(D, cap, lease);
     if (r) return r;
@@ -930,30 +942,30 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     KRK_HIP(mem.alloc(&d_sums, std::max<uint64_t>(hi, 1) * 4));
     KRK_HIP(hipMemset(d_sums, 0, std::max<uint64_t>(hi, 1) * 4));
     std::vector<uint64_t> off(n, 0);
-    std::vector<char> done(n, 0);
+    std::vector<char> done(on_host);
     hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
-    // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed in
-    // place on host threads while the windows below carry every blob's bytes to the
-    // piece CRCs and the others' SHA-256 to the GPU.
-    std::vector<char> on_host(n, 0);
-    std::vector<uint32_t> host;
-    if (offload_threads() > 0) {
-        std::vector<uint64_t> lens(n);
-        for (uint64_t i = 0; i < n; ++i) lens[i] = blobs[i].length;
-        host = offload_plan(lens.data(), n, offload_threads(), D->cus, nullptr, nullptr, true);
-        for (uint32_t i : host) on_host[i] = 1;
-    }
+    // The host blobs' digests and piece sums land in host_dig / host_sums (host_sums_off[j]
+    // = where blob host[j]'s first sum sits there) and go to the caller's arrays after the
+    // device results are copied out.
     std::vector<uint8_t> host_dig(32 * host.size());
+    std::vector<uint64_t> host_sums_off(host.size() + 1, 0);
+    for (size_t j = 0; j < host.size(); ++j)
+        host_sums_off[j + 1] =
+            host_sums_off[j] + krk_num_pieces(blobs[host[j]].length, blobs[host[j]].piece_length);
+    std::vector<uint32_t> host_sums(host_sums_off.back());
     std::thread host_th;
     if (!host.empty())
         host_th = std::thread([&] {
             std::vector<const uint8_t*> p(host.size());
-            std::vector<uint64_t> l(host.size());
+            std::vector<uint64_t> l(host.size()), pl(host.size());
+            std::vector<uint32_t*> so(host.size());
             for (size_t j = 0; j < host.size(); ++j) {
                 p[j] = blobs[host[j]].data;
                 l[j] = blobs[host[j]].length;
+                pl[j] = (uint64_t)blobs[host[j]].piece_length;
+                so[j] = host_sums.data() + host_sums_off[j];
             }
-            offload_hash_host(p, l, offload_threads(), host_dig.data());
+            offload_whole_host(p, l, pl, so, offload_threads(), host_dig.data());
         });
     struct Joiner {
         std::thread& t;
@@ -962,7 +974,7 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         }
     } joiner{host_th};
     ItemBuilder B;
-    uint64_t remaining = n;
+    uint64_t remaining = n_gpu;
     int k = 0;
     double t_acq = 0, t_build = 0, t_copy = 0, t_enq = 0, t0 = wall_s();
     int n_win = 0;
@@ -988,16 +1000,14 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
                 copies.push_back({w.host + fill, b.data + off[i], take});
                 B.add(items, dev, off[i], off[i] + take, b.length, (uint64_t)b.piece_length, b.sums_offset);
             }
-            if (!on_host[i]) {
-                ShaJob j{};
-                j.ptr = dev;
-                j.len = take;
-                j.prefix = off[i];
-                j.out = (uint32_t)i;
-                j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
-                memcpy(j.h, kIV, sizeof kIV);
-                jobs.push_back(j);
-            }
+            ShaJob j{};
+            j.ptr = dev;
+            j.len = take;
+            j.prefix = off[i];
+            j.out = (uint32_t)i;
+            j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
+            memcpy(j.h, kIV, sizeof kIV);
+            jobs.push_back(j);
             off[i] += take;
             fill += (take + 15) & ~uint64_t(15);
             if (fin) { done[i] = 1; --remaining; }
@@ -1044,6 +1054,10 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;
     }
+    for (size_t q = 0; !r && q < host.size(); ++q)
+        if (host_sums_off[q + 1] > host_sums_off[q])
+            memcpy(sums_host + blobs[host[q]].sums_offset, &host_sums[host_sums_off[q]],
+                   (host_sums_off[q + 1] - host_sums_off[q]) * 4);
     return r;
 }
 

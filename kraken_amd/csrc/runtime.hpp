@@ -535,14 +535,29 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 
 
 
-// SHA-256 host offload (offload.cpp): the longest blobs of a device-resident batch
-// hashed on host threads while the GPU hashes the rest (krk_set_sha_host_offload).
+// SHA-256 host offload (offload.cpp): the longest blobs of a batch hashed on host threads
+// while the GPU hashes the rest (krk_set_sha_host_offload).  Where the batch lives
+// decides what the host saves:
+//  * kOffDevice: blobs in HBM; the host reads its blobs out over D2H, the GPU still
+//    computes every piece CRC (krk_sha256_dev, krk_metainfo_digest_dev);
+//  * kOffHostSha: blobs in host memory, digests only; the host's blobs are hashed in place
+//    and never uploaded (krk_sha256_host);
+//  * kOffHostWhole: blobs in host memory, digests and piece sums; the host's blobs are
+//    hashed AND piece-summed in place and never uploaded (krk_metainfo_digest_host) --
+//    the batch's bytes over the host link shrink by theirs.
+enum OffMode { kOffDevice = 0, kOffHostSha = 1, kOffHostWhole = 2 };
 int offload_threads();
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
-                                   double* host_s, bool host_resident = false);
+                                   double* host_s, int mode = kOffDevice);
 void offload_teardown(Device& D);  // krk_shutdown: the offload threads' streams and pinned buffers
 void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
                        uint8_t* out);
+// kOffHostWhole: blob j's digest to out + 32 j and its piece sums (piece length plen[j])
+// to sums[j][0 .. ceil(len / plen)), on up to `threads` threads; the SHA-256 pass and the
+// CRC pass of a blob are separate tasks, longest first.
+void offload_whole_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens,
+                        const std::vector<uint64_t>& plen, const std::vector<uint32_t*>& sums, int threads,
+                        uint8_t* out);
 int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
                  hipEvent_t ready, uint8_t* out);
 int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,

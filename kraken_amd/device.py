@@ -208,14 +208,20 @@ def set_sha_host_offload(threads: int):
     check(lib.krk_set_sha_host_offload(int(threads)))
 
 
-def sha_offload_plan(lengths, threads: int, cus: int = 256):
-    """krk_sha_offload_plan: (indices of the blobs the host would hash, longest first,
-    modelled GPU seconds, modelled host seconds) -- no device needed."""
+OFFLOAD_DEVICE, OFFLOAD_HOST_SHA, OFFLOAD_HOST_WHOLE = 0, 1, 2
+
+
+def sha_offload_plan(lengths, threads: int, cus: int = 256, mode: int = OFFLOAD_DEVICE):
+    """krk_host_offload_plan: (indices of the blobs the host would take, longest first,
+    modelled GPU seconds, modelled host seconds) -- no device needed.  mode: a batch in
+    HBM (OFFLOAD_DEVICE), host blobs hashed only (OFFLOAD_HOST_SHA, sha256_host) or hashed
+    and piece-summed on the host (OFFLOAD_HOST_WHOLE, metainfo_digest_host)."""
     L = np.ascontiguousarray(lengths, dtype=np.uint64)
     idx = np.zeros(max(L.size, 1), dtype=np.uint32)
     k, g, h = C.c_uint64(0), C.c_double(0), C.c_double(0)
-    check(lib.krk_sha_offload_plan(L.ctypes.data_as(C.POINTER(C.c_uint64)), L.size, int(threads), int(cus),
-                                   idx.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(k), C.byref(g), C.byref(h)))
+    check(lib.krk_host_offload_plan(L.ctypes.data_as(C.POINTER(C.c_uint64)), L.size, int(threads), int(cus),
+                                    int(mode), idx.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(k), C.byref(g),
+                                    C.byref(h)))
     return idx[:k.value].copy(), g.value, h.value
 
 

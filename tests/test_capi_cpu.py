@@ -259,3 +259,24 @@ def test_sha_offload_plan():
     assert D.sha_offload_plan([0, 0, 0], 16)[0].size == 0
     with pytest.raises(Exception):
         D.sha_offload_plan(lens, -1)
+
+
+def test_host_offload_plan_modes():
+    """krk_host_offload_plan: blobs in host memory.  C2 (1,000 x 100 MiB) is bound by the
+    host link, so with the whole-blob mode (hash + piece sums on the host, never uploaded)
+    the host takes some blobs and the modelled makespan drops to the GPU's own chain time;
+    a batch in HBM (KRK_OFFLOAD_DEVICE) keeps every equal blob on the GPU."""
+    from kraken_amd import device as D
+    c2 = [100 << 20] * 1000
+    g0 = D.sha_offload_plan(c2, 0, mode=D.OFFLOAD_HOST_WHOLE)[1]
+    assert abs(g0 - 1000 * (100 << 20) / 45e9) < 1e-6  # link-bound with no offload
+    idx, g, h = D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_HOST_WHOLE)
+    assert max(g, h) <= g0
+    if idx.size:  # host cores with the SHA extensions: the link sheds the host's blobs
+        assert max(g, h) < 0.97 * g0 and g >= (100 << 20) / 55e6 - 1e-9
+        assert sorted(idx.tolist()) == list(range(idx.size))  # equal lengths: stable order
+    assert D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_DEVICE)[0].size == 0
+    idx, g, h = D.sha_offload_plan([1 << 30], 4, mode=D.OFFLOAD_HOST_SHA)  # C1 from host memory
+    assert list(idx) == [0] and g == 0.0 and h > 0
+    with pytest.raises(Exception):
+        D.sha_offload_plan(c2, 4, mode=3)

@@ -449,13 +449,17 @@ def test_sha_host_offload_bit_exact(gpu, orc, misalign):
 
 @pytest.mark.parametrize("window_mb", ["1", None])
 def test_sha_host_offload_host_buffers(gpu, orc, window_mb):
-    """The host-buffer entry points with the offload on: the longest blobs are hashed in
-    place on host threads (krk_sha256_host never uploads them; krk_metainfo_digest_host
-    still carries their bytes to the piece CRCs); digests and sums equal hashlib / oracle."""
+    """The host-buffer entry points with the offload on: the longest blobs are worked on
+    in place on host threads and never uploaded (krk_sha256_host hashes them,
+    krk_metainfo_digest_host hashes them and computes their piece sums on the host, the
+    rest -- including the empty blob -- go through the windows); digests and sums equal
+    hashlib / oracle."""
     rng = np.random.default_rng(31)
     sizes = [(24 << 20) + 5, 9 << 20, 0, 1, 63, 64, 1000] + [70_000 + 13 * i for i in range(60)]
     datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in sizes]
-    assert set(D.sha_offload_plan(sizes, 4)[0].tolist()) >= {0, 1}
+    for mode in (D.OFFLOAD_HOST_SHA, D.OFFLOAD_HOST_WHOLE):
+        host = set(D.sha_offload_plan(sizes, 4, mode=mode)[0].tolist())
+        assert host >= {0, 1} and 2 not in host and len(host) < len(sizes) - 1
     ptrs = (C.c_void_p * len(datas))(*[d.ctypes.data if d.size else None for d in datas])
     lens = np.array(sizes, dtype=np.uint64)
     want = [hashlib.sha256(d.tobytes()).digest() for d in datas]
@@ -475,3 +479,26 @@ def test_sha_host_offload_host_buffers(gpu, orc, window_mb):
     finally:
         D.set_sha_host_offload(0)
         os.environ.pop("KRK_WINDOW_MB", None)
+
+
+def test_host_whole_offload_piece_lengths(gpu, orc):
+    """krk_metainfo_digest_host with the whole-blob host offload at several piece lengths
+    (partial last pieces, 4 KiB and one-byte pieces): the MiB blobs are hashed and
+    piece-summed on host threads, the small ones and the empty one go through the windows;
+    piece sums and digests equal the oracle / hashlib."""
+    rng = np.random.default_rng(5)
+    sizes = [3 << 20, (2 << 20) + 1, 1 << 20, 4097, 0, 65, 1]
+    datas = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in sizes]
+    host = set(D.sha_offload_plan(sizes, 8, mode=D.OFFLOAD_HOST_WHOLE)[0].tolist())
+    assert host >= {0, 1, 2} and 4 not in host
+    try:
+        D.set_sha_host_offload(8)
+        for P in (1 << 20, 4096, 1):
+            if P == 1:
+                datas, sizes = datas[3:], sizes[3:]  # one-byte pieces: keep the piece count small
+            sums, dg = D.metainfo_digest_host(datas, P)
+            for i, d in enumerate(datas):
+                assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), (P, i)
+                assert np.array_equal(sums[i], orc.calc_piece_sums(d, P)[1]), (P, i)
+    finally:
+        D.set_sha_host_offload(0)
