@@ -708,7 +708,8 @@ def run_chunked(a, D, T, rank, world, res):
     from kraken_amd.windowed import WindowedRun
     ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
     n = len(lens)
-    wr = WindowedRun(D, ids, lens, P, a.window_gib << 30, cap=n if a.no_admission else None)
+    wr = WindowedRun(D, ids, lens, P, a.window_gib << 30,
+                     cap=n if a.no_admission else (a.live_cap or None))
     T.barrier()
     with D.KernelTimer():
         t0 = time.perf_counter()
@@ -903,6 +904,7 @@ def main():
     ap.add_argument("--blobs", type=int, default=0, help="override the blob (or digest) count")
     ap.add_argument("--nodes", type=int, default=16, help="C5: origins in the ring")
     ap.add_argument("--window-gib", type=int, default=48, help="C3: device window size")
+    ap.add_argument("--live-cap", type=int, default=0, help="C3: live streams per window (0 = the planner's)")
     ap.add_argument("--no-admission", action="store_true",
                     help="C3: all blobs live from window 0 (no longest-first admission under the two-lane cap)")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")

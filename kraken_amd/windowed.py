@@ -71,6 +71,19 @@ def two_lane_stream_cap(D, n):
     return lo
 
 
+def window_stream_cap(D, n):
+    """Live streams per window: at most 7/8 of the largest multi-lane stream count (a
+    multiple of the two-pair workgroup's 64 streams).  At the full two-lane count
+    (64 x CUs) every CU holds a 128 KiB SHA workgroup and the window's piece-CRC launch
+    (144 KiB workgroups) waits for the SHA launch to end; with an eighth of the CUs left
+    free it runs inside it, and the chain of the longest blob -- not the live count --
+    still sets the run time.  C3 on one MI355X (bench --live-cap): 16,384 live 494 GB/s,
+    15,360 522, 14,336 524, 13,824 523, 13,312 522, 12,288 509 (profiles/r02/c3_live_cap.jsonl)."""
+    full = two_lane_stream_cap(D, 1 << 30) if n else 1
+    cap = max(64, (full * 7 // 8) // 64 * 64)
+    return max(1, min(n, cap))
+
+
 class WindowedRun:
     """One batch of synthetic blobs (ids, lens, piece length P) streamed through two
     device windows of W bytes: window k+1 is generated on `gen` while window k's
@@ -84,7 +97,7 @@ class WindowedRun:
         self.P = P
         self.W = int(W)
         n = len(self.lens)
-        self.cap = two_lane_stream_cap(D, n) if cap is None else int(cap)
+        self.cap = window_stream_cap(D, n) if cap is None else int(cap)
         self.wins = window_plan(self.lens, self.W, self.cap)
         self.bufs = [D.DeviceBuffer(self.W + 16 * n), D.DeviceBuffer(self.W + 16 * n)]
         self.cb = D.ChunkedBatch(self.lens, P)
