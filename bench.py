@@ -706,7 +706,11 @@ def run_chunked(a, D, T, rank, world, res):
     window's kernels run (kraken_amd.windowed, the machinery tests/test_gpu_windowed.py
     checks against the oracle)."""
     from kraken_amd.windowed import WindowedRun
-    ids, lens, P = workload_blobs(a.workload, rank, world, a.blobs)
+    # --emulate-world W: run rank `rank`'s LPT shard of a W-GPU run on this one GPU (ranks
+    # share nothing, so a W-GPU run takes as long as its slowest shard; rank 0 holds the
+    # longest blob, whose chain bounds every shard).
+    shard_world = a.emulate_world or world
+    ids, lens, P = workload_blobs(a.workload, rank, shard_world, a.blobs)
     n = len(lens)
     wr = WindowedRun(D, ids, lens, P, a.window_gib << 30,
                      cap=n if a.no_admission else (a.live_cap or None))
@@ -730,7 +734,11 @@ def run_chunked(a, D, T, rank, world, res):
                 "config": {"workload": WORKLOADS["c3"]["desc"], "blobs_total": a.blobs or 20000,
                            "blobs_this_rank": n, "bytes_this_rank": bytes_rank, "bytes_total": total_bytes,
                            "windows": len(wr.wins), "window_bytes": wr.W, "live_cap": int(wr.cap), "piece_length": P,
-                           "longest_blob": max(lens), "parallelism": f"LPT blob shard x{world}, no collective"},
+                           "longest_blob": max(lens), "parallelism": f"LPT blob shard x{shard_world}, no collective",
+                           **({"emulated_world": shard_world,
+                               "emulation": f"rank {rank}'s shard of a {shard_world}-GPU run on one GPU; value = all "
+                                            f"{shard_world} shards' bytes / this shard's time (it holds the longest "
+                                            f"blob)"} if a.emulate_world else {})},
                 "kernels": {"sha256_multi": {"launches": sha_n, "total_ms": round(sha_ms, 1)},
                             "crc32_pieces": {"launches": crc_n, "total_ms": round(crc_ms, 1)},
                             "synth_fill": {"launches": gen_n, "total_ms": round(gen_ms, 1)}},
@@ -905,6 +913,8 @@ def main():
     ap.add_argument("--nodes", type=int, default=16, help="C5: origins in the ring")
     ap.add_argument("--window-gib", type=int, default=48, help="C3: device window size")
     ap.add_argument("--live-cap", type=int, default=0, help="C3: live streams per window (0 = the planner's)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="C3: run rank 0's LPT shard of an N-GPU run on this GPU (no collective exists to emulate)")
     ap.add_argument("--no-admission", action="store_true",
                     help="C3: all blobs live from window 0 (no longest-first admission under the two-lane cap)")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
