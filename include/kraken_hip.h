@@ -351,6 +351,9 @@ int krk_host_alloc(uint64_t bytes, void** out);
 int krk_host_free(void* p);
 int krk_memcpy_h2d(void* dst_dev, const void* src_host, uint64_t n);
 int krk_memcpy_d2h(void* dst_host, const void* src_dev, uint64_t n);
+/* Queued on `stream` (NULL = the library's stream): dst_host should be pinned
+ * (krk_host_alloc) for the copy to overlap the host. */
+int krk_memcpy_d2h_async(void* dst_host, const void* src_dev, uint64_t n, void* stream);
 int krk_stream_create(void** out);
 int krk_stream_destroy(void* s);
 int krk_stream_sync(void* s);

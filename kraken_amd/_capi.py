@@ -118,6 +118,7 @@ def _load() -> C.CDLL:
         "krk_host_free": (i, [vp]),
         "krk_memcpy_h2d": (i, [vp, vp, C.c_uint64]),
         "krk_memcpy_d2h": (i, [vp, vp, C.c_uint64]),
+        "krk_memcpy_d2h_async": (i, [vp, vp, C.c_uint64, vp]),
         "krk_stream_create": (i, [C.POINTER(vp)]),
         "krk_stream_destroy": (i, [vp]),
         "krk_stream_sync": (i, [vp]),

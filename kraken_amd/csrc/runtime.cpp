@@ -1505,6 +1505,11 @@ int krk_memcpy_d2h(void* dst, const void* src, uint64_t n) {
     KRK_HIP(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return KRK_OK;
 }
+int krk_memcpy_d2h_async(void* dst, const void* src, uint64_t n, void* stream) {
+    KRK_DEVICE(D);
+    KRK_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, pick(D, stream)));
+    return KRK_OK;
+}
 int krk_stream_create(void** out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_DEVICE(D);

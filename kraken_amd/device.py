@@ -63,6 +63,11 @@ class PinnedArray:
             check(lib.krk_memcpy_d2h(self.ptr, dev.ptr + offset, self.array_nbytes))
         return self.a
 
+    def fill_from_async(self, dev: "DeviceBuffer", stream, offset: int = 0):
+        """Queue the copy on `stream`; self.a is valid once that stream is synchronised."""
+        if self.array_nbytes:
+            check(lib.krk_memcpy_d2h_async(self.ptr, dev.ptr + offset, self.array_nbytes, stream))
+
     def __del__(self):
         try:
             if self.ptr:
