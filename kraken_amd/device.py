@@ -179,17 +179,26 @@ def piece_sums(arena: BlobArena, out: BatchOutputs, stream=None):
     check(lib.krk_piece_sums_dev(arena.blob_structs(), len(arena.lengths), out.sums.ptr, stream))
 
 
+def pack_names(names):
+    """The (bytes, offsets) layout krk_metainfo_batch_dev takes for the blobs' names."""
+    enc = [x.encode() for x in names]
+    noff = np.zeros(len(enc) + 1, dtype=np.uint64)
+    noff[1:] = np.cumsum([len(e) for e in enc]) if enc else []
+    return b"".join(enc), noff
+
+
 def metainfo_batch(arena: BlobArena, out: BatchOutputs, names, sums_host: np.ndarray, stream=None) -> np.ndarray:
     """Generator.Generate over the arena's blobs (krk_metainfo_batch_dev): piece sums into
     out.sums and sums_host (uint32, arena layout) and the InfoHashes, returned as an
-    (n, 20) uint8 array; the host hashes each group while later groups' kernels run."""
+    (n, 20) uint8 array; the host hashes each group while later groups' kernels run.
+    names: the blobs' names (str), or pack_names() of them."""
     n = len(arena.lengths)
-    enc = [x.encode() for x in names]
-    noff = np.zeros(n + 1, dtype=np.uint64)
-    noff[1:] = np.cumsum([len(e) for e in enc]) if n else []
+    buf, noff = names if isinstance(names, tuple) else pack_names(names)
+    if noff.size != n + 1:
+        raise ValueError(f"metainfo_batch: {noff.size - 1} names for {n} blobs")
     ih = np.zeros((max(n, 1), 20), dtype=np.uint8)
     assert sums_host.dtype == np.uint32 and sums_host.size >= arena.total_pieces
-    check(lib.krk_metainfo_batch_dev(arena.blob_structs(), n, b"".join(enc) or None,
+    check(lib.krk_metainfo_batch_dev(arena.blob_structs(), n, buf or None,
                                      noff.ctypes.data_as(C.POINTER(C.c_uint64)), out.sums.ptr,
                                      sums_host.ctypes.data_as(C.POINTER(C.c_uint32)),
                                      ih.ctypes.data_as(C.POINTER(C.c_uint8)), stream))
