@@ -30,7 +30,7 @@ for s in "$@"; do
     c3cap) for c in ${CAPS:-16384 13824 12288}; do step bench_c3_cap$c 600 python bench.py --workload c3 --no-cpu-baseline --no-ceiling --live-cap $c || exit 1; done ;;
     c3w8) step bench_c3_w8 600 python bench.py --workload c3 --no-cpu-baseline --emulate-world 8 ;;
     c4pipe) step bench_c4 600 python bench.py --workload c4 ;;
-    e2ehyb) step e2e_hybrid 900 env KRK_BENCH_HYBRID=4,8,16 python bench.py --e2e-only --no-cpu-baseline ;;
+    e2ehyb) step e2e_hybrid 900 env KRK_BENCH_HYBRID=${HYB:-4,8,16} python bench.py --e2e-only --no-cpu-baseline ;;
     testoff) step pytest_offload 300 python -u -m pytest tests/test_gpu_digest_metainfo.py -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread -k offload ;;
     prof) step prof_c2 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c2 -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-ceiling ;;
     valu) step valu_c2_p1 600 rocprofv3 --kernel-trace --pmc $P1 --output-format csv -d $R/gpurun_out/valu_c2_p1 -- python3 $R/bench.py $C2 &&
