@@ -618,6 +618,42 @@ __device__ __forceinline__ void sha8_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
                  : KRK_SHA8_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
 }
 
+// W quads a read group of the eight-lane consumer covers (KRK_SHA8_GROUP): 3 (default) =
+// three quads read between 12-round asm blocks, four quads ahead (a group's last block
+// needs quad j + 3, read one group earlier), so ONE s_waitcnt precedes every 12 rounds;
+// 1 = one read and one wait per 4 rounds (round 2's first form).  C2-shaped A/B on one
+// box (profiles/r02/sha8_read_groups.jsonl): 56.2 MB/s a stream with one read a group,
+// 57.2 with pairs, 58.7 with threes, 58.3 with fives (two asm statements a group).
+#ifndef KRK_SHA8_GROUP
+#define KRK_SHA8_GROUP 3
+#endif
+static_assert(KRK_SHA8_GROUP == 1 || KRK_SHA8_GROUP == 3, "read group of the eight-lane consumer");
+#if KRK_SHA8_GROUP == 3 && !defined(KRK_SHA_NOLDS)
+#define KRK_SHA8_G3 1
+constexpr int kAhead8 = 4;
+#else
+#define KRK_SHA8_G3 0
+constexpr int kAhead8 = kAhead;
+#endif
+// Twelve eight-lane rounds, n = 4j + 2 .. 4j + 13: W quads a = j, b = j + 1, d = j + 2,
+// e = j + 3 (each block of four takes its first quad's last word and the next quad's
+// first three).
+__device__ __forceinline__ void sha8_dodec2(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                            const TwoLaneConst& c, const u32x4& a, const u32x4& b, const u32x4& d,
+                                            const u32x4& e) {
+    uint32_t t1, t2, kk, p;
+    asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w1) KRK_SHA8_ROUND(R3, R2, R1, R0, w2)
+                 KRK_SHA8_ROUND(R0, R3, R2, R1, w3) KRK_SHA8_ROUND(R1, R0, R3, R2, w4)
+                 KRK_SHA8_ROUND(R2, R1, R0, R3, w5) KRK_SHA8_ROUND(R3, R2, R1, R0, w6)
+                 KRK_SHA8_ROUND(R0, R3, R2, R1, w7) KRK_SHA8_ROUND(R1, R0, R3, R2, w8)
+                 KRK_SHA8_ROUND(R2, R1, R0, R3, w9) KRK_SHA8_ROUND(R3, R2, R1, R0, w10)
+                 KRK_SHA8_ROUND(R0, R3, R2, R1, w11) KRK_SHA8_ROUND(R1, R0, R3, R2, w12)
+                 KRK_SHA8_OPERANDS
+                 : KRK_SHA8_CONSTS, [w1] "v"(a[3]), [w2] "v"(b[0]), [w3] "v"(b[1]), [w4] "v"(b[2]),
+                   [w5] "v"(b[3]), [w6] "v"(d[0]), [w7] "v"(d[1]), [w8] "v"(d[2]), [w9] "v"(d[3]),
+                   [w10] "v"(e[0]), [w11] "v"(e[1]), [w12] "v"(e[2]));
+}
+
 // Eight lanes a stream, blocks pipelined: the A quad runs rounds 62, 63 of block i
 // while the E quad already runs rounds 0, 1 of block i + 1, so a block costs 64
 // instruction-rounds instead of 66.  State crosses blocks in registers: R0..R3 (the
@@ -642,17 +678,36 @@ __device__ __forceinline__ void sha8_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
 __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
                                         uint32_t hE[4], uint32_t hA[4], uint32_t mineE, uint32_t mineA,
                                         uint32_t i, const uint32_t* lds, uint32_t cbase, uint32_t nbase,
-                                        const TwoLaneConst& c, u32x4 k[kAhead]) {
-    constexpr int kRS = kAhead + 1;
+                                        const TwoLaneConst& c, u32x4 k[kAhead8]) {
+    constexpr int kRS = kAhead8 + 1;
     u32x4 wq[kRS];
 #pragma unroll
-    for (int j = 0; j < kAhead; ++j) wq[j] = k[j];
-    // Rounds n = 2 .. 61 in 15 asm blocks of four, n = 4j + 2 .. 4j + 5 (W: quad j's last
-    // word, quad j + 1's first three), each W read between two blocks -- two rounds into
-    // a W quad.  Issued right before a W quad's rounds a read cost ~16 cycles of the
-    // wave's stream, two rounds in ~8, its code bytes (tools/micro/sha8lds.hip,
-    // profiles/r02/micro_sha8lds.txt); and the read + its wait between two asm blocks
-    // are the two wait states the hazard recognizer would otherwise pad there.
+    for (int j = 0; j < kAhead8; ++j) wq[j] = k[j];
+    // Rounds n = 2 .. 61.  Production (KRK_SHA8_GROUP 3): 5 asm blocks of twelve rounds,
+    // the next three W quads read before each (four quads ahead), so one s_waitcnt per
+    // twelve rounds.  Otherwise 15 asm blocks of four, n = 4j + 2 .. 4j + 5 (W: quad j's
+    // last word, quad j + 1's first three), each W read between two blocks -- two rounds
+    // into a W quad (issued right before a W quad's rounds a read cost ~16 cycles of the
+    // wave's stream, two rounds in ~8, tools/micro/sha8lds.hip); the read + its wait
+    // between two asm blocks are the two wait states the hazard recognizer would pad.
+#if KRK_SHA8_G3
+    constexpr int RS = kAhead8 + 3;
+    u32x4 wr[RS];
+#pragma unroll
+    for (int j = 0; j < kAhead8; ++j) wr[j] = wq[j];
+    auto rd = [&](int q) {  // W quad q of this block (q < 16) or q - 16 of the next block
+        if (q < 16) wr[q % RS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * q);
+        else k[q - 16] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - 16));
+    };
+#pragma unroll
+    for (int j = 0; j < 15; j += 3) {
+        rd(j + kAhead8);
+        rd(j + kAhead8 + 1);
+        rd(j + kAhead8 + 2);
+        sha8_dodec2(R0, R1, R2, R3, z, c, wr[j % RS], wr[(j + 1) % RS], wr[(j + 2) % RS], wr[(j + 3) % RS]);
+    }
+    wq[15 % kRS] = wr[15 % RS];
+#else
 #pragma unroll
     for (int j = 0; j < 15; ++j) {
 #ifdef KRK_SHA_NOLDS
@@ -668,10 +723,11 @@ __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2
         const u32x4& b = wq[(j + 1) % kRS];
         sha8_quad2(R0, R1, R2, R3, z, c, a[3], b[0], b[1], b[2]);
     }
+#endif
 #ifdef KRK_SHA_NOLDS
-    k[kAhead - 1] = u32x4{15u, nbase, 5u, 7u};
+    k[kAhead8 - 1] = u32x4{15u, nbase, 5u, 7u};
 #else
-    k[kAhead - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead - 1));
+    k[kAhead8 - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead8 - 1));
 #endif
     {
         uint32_t t1, t2, kk, p;  // n = 62, 63
@@ -763,6 +819,7 @@ __device__ __forceinline__ void sha2_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
                  KRK_SHA2_OPERANDS
                  : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
 }
+
 
 // Eight lanes a stream, blocks pipelined: the A quad runs rounds 62, 63 of block i
 // while the E quad already runs rounds 0, 1 of block i + 1, so a block costs 64
@@ -1255,7 +1312,7 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     const uint32_t binc = 32u, sinc = is_e ? uint32_t(kSlotWords) : 0u;
     // voff: this lane's offset of block i (E: slot base vslot + jj * 32; A: 0)
     uint32_t voff = 0, vslot = 0, slot = 0;
-    u32x4 kq[kAhead] = {};
+    u32x4 kq[kAhead8] = {};
     // Blocks pipelined (block8p): 64 instruction-rounds a block; each half's chaining
     // value lives on its own lanes (0 on the other half).
     uint32_t hE[4], hA[4];
@@ -1278,7 +1335,7 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         if (kTiming == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + lbase + 256 * q);
+        for (int q = 0; q < kAhead8; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + lbase + 256 * q);
         prologue8p(R0, R1, R2, R3, z, h, is_e, c, kq[0]);
     }
     for (uint32_t i = 0; i < nb; i += kU) {
