@@ -523,7 +523,7 @@ constexpr int kAhead = KRK_SHA_AHEAD;
 #define KRK_SHA2_PIPELINED 1  // two-lane consumer: blocks pipelined (block2p) instead of rounds2
 #endif
 #ifndef KRK_SHA8_UNROLL
-#define KRK_SHA8_UNROLL 2  // eight-lane consumer: blocks per loop iteration
+#define KRK_SHA8_UNROLL 4  // eight-lane consumer: blocks per loop iteration
 #endif
 static_assert(kAhead >= 2 && kAhead <= 8, "read-ahead distance");
 __device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
@@ -1328,7 +1328,8 @@ sha256_w8_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
     };
     // kU blocks an iteration (a step's 8 blocks never straddle an iteration): one block
     // an iteration ran at 52.9 MB/s a stream, two at 55.0 (fewer taken branches and
-    // less loop bookkeeping per block).
+    // less loop bookkeeping per block); with the W read groups, four 59.1 vs two 58.8,
+    // eight 59.1 (profiles/r02/sha8_unroll.jsonl).
     constexpr uint32_t kU = KRK_SHA8_UNROLL;
     static_assert(kU == 1 || kU == 2 || kU == 4 || kU == 8, "blocks per iteration divide a step");
     if (nb) {  // step 0's barrier, the first quads, and (pipelined) rounds 0, 1 of block 0
