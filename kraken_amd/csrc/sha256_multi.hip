@@ -820,6 +820,39 @@ __device__ __forceinline__ void sha2_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
                  : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
 }
 
+// The two-lane consumer's W read group (KRK_SHA2_GROUP): 3 (default) = as the eight-lane
+// KRK_SHA8_GROUP 3 (three quads read four ahead, twelve rounds a wait); 1 = one read and
+// one wait per four rounds.  Same-box A/B (profiles/r02/sha2_read_groups.jsonl): 16,384
+// streams 49.7 -> 51.6 MB/s a stream, 8,192 streams 50.4 -> 51.9 (pairs were 0.5 % slower
+// than one read a quad).
+#ifndef KRK_SHA2_GROUP
+#define KRK_SHA2_GROUP 3
+#endif
+static_assert(KRK_SHA2_GROUP == 1 || KRK_SHA2_GROUP == 3, "read group of the two-lane consumer");
+#if KRK_SHA2_GROUP == 3 && KRK_SHA2_PIPELINED && !defined(KRK_SHA_NOLDS)
+#define KRK_SHA2_G3 1
+constexpr int kAhead2 = 4;
+#else
+#define KRK_SHA2_G3 0
+constexpr int kAhead2 = kAhead;
+#endif
+__device__ __forceinline__ void sha2_dodec2(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
+                                            const TwoLaneConst& c, const u32x4& a, const u32x4& b, const u32x4& d,
+                                            const u32x4& e) {
+    uint32_t t1, t2, t3, kk, p;
+    asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w1) KRK_SHA2_ROUND(R3, R2, R1, R0, w2)
+                 KRK_SHA2_ROUND(R0, R3, R2, R1, w3) KRK_SHA2_ROUND(R1, R0, R3, R2, w4)
+                 KRK_SHA2_ROUND(R2, R1, R0, R3, w5) KRK_SHA2_ROUND(R3, R2, R1, R0, w6)
+                 KRK_SHA2_ROUND(R0, R3, R2, R1, w7) KRK_SHA2_ROUND(R1, R0, R3, R2, w8)
+                 KRK_SHA2_ROUND(R2, R1, R0, R3, w9) KRK_SHA2_ROUND(R3, R2, R1, R0, w10)
+                 KRK_SHA2_ROUND(R0, R3, R2, R1, w11) KRK_SHA2_ROUND(R1, R0, R3, R2, w12)
+                 KRK_SHA2_OPERANDS
+                 : KRK_SHA2_CONSTS, [w1] "v"(a[3]), [w2] "v"(b[0]), [w3] "v"(b[1]), [w4] "v"(b[2]),
+                   [w5] "v"(b[3]), [w6] "v"(d[0]), [w7] "v"(d[1]), [w8] "v"(d[2]), [w9] "v"(d[3]),
+                   [w10] "v"(e[0]), [w11] "v"(e[1]), [w12] "v"(e[2]));
+    (void)t3;
+}
+
 
 // Eight lanes a stream, blocks pipelined: the A quad runs rounds 62, 63 of block i
 // while the E quad already runs rounds 0, 1 of block i + 1, so a block costs 64
@@ -845,17 +878,35 @@ __device__ __forceinline__ void sha2_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
 __device__ __forceinline__ void block2p(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
                                         uint32_t hE[4], uint32_t hA[4], uint32_t mineE, uint32_t mineA,
                                         uint32_t i, const uint32_t* lds, uint32_t cbase, uint32_t nbase,
-                                        const TwoLaneConst& c, u32x4 k[kAhead]) {
-    constexpr int kRS = kAhead + 1;
+                                        const TwoLaneConst& c, u32x4 k[kAhead2]) {
+    constexpr int kRS = kAhead2 + 1;
     u32x4 wq[kRS];
 #pragma unroll
-    for (int j = 0; j < kAhead; ++j) wq[j] = k[j];
+    for (int j = 0; j < kAhead2; ++j) wq[j] = k[j];
     // Rounds n = 2 .. 61 in 15 asm blocks of four, n = 4j + 2 .. 4j + 5 (W: quad j's last
     // word, quad j + 1's first three), each W read between two blocks -- two rounds into
     // a W quad.  Issued right before a W quad's rounds a read cost ~16 cycles of the
     // wave's stream, two rounds in ~8, its code bytes (tools/micro/sha8lds.hip,
     // profiles/r02/micro_sha8lds.txt); and the read + its wait between two asm blocks
     // are the two wait states the hazard recognizer would otherwise pad there.
+#if KRK_SHA2_G3
+    constexpr int RS = kAhead2 + 3;
+    u32x4 wr[RS];
+#pragma unroll
+    for (int j = 0; j < kAhead2; ++j) wr[j] = wq[j];
+    auto rd = [&](int q) {  // W quad q of this block (q < 16) or q - 16 of the next block
+        if (q < 16) wr[q % RS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * q);
+        else k[q - 16] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - 16));
+    };
+#pragma unroll
+    for (int j = 0; j < 15; j += 3) {
+        rd(j + kAhead2);
+        rd(j + kAhead2 + 1);
+        rd(j + kAhead2 + 2);
+        sha2_dodec2(R0, R1, R2, R3, z, c, wr[j % RS], wr[(j + 1) % RS], wr[(j + 2) % RS], wr[(j + 3) % RS]);
+    }
+    wq[15 % kRS] = wr[15 % RS];
+#else
 #pragma unroll
     for (int j = 0; j < 15; ++j) {
 #ifdef KRK_SHA_NOLDS
@@ -871,10 +922,11 @@ __device__ __forceinline__ void block2p(uint32_t& R0, uint32_t& R1, uint32_t& R2
         const u32x4& b = wq[(j + 1) % kRS];
         sha2_quad2(R0, R1, R2, R3, z, c, a[3], b[0], b[1], b[2]);
     }
+#endif
 #ifdef KRK_SHA_NOLDS
-    k[kAhead - 1] = u32x4{15u, nbase, 5u, 7u};
+    k[kAhead2 - 1] = u32x4{15u, nbase, 5u, 7u};
 #else
-    k[kAhead - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead - 1));
+    k[kAhead2 - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead2 - 1));
 #endif
     {
         uint32_t t1, t2, t3, kk, p;  // n = 62, 63
@@ -1067,7 +1119,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         const uint32_t base_even = aoff + (lane ^ 15u) * 4, base_odd = aoff + lane * 4;
         const uint32_t einc = is_e ? uint32_t(kSlotWords) : 0u;
         uint32_t vslot = 0, slot = 0;
-        u32x4 kq[kAhead] = {};
+        u32x4 kq[kAhead2] = {};
 #ifdef KRK_SHA_CYCLES  // diagnostic build (make cycles): consumer cycles per block
         const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
         uint64_t cyc_bar = 0, cyc_rounds = 0;
@@ -1106,7 +1158,7 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
             if (kTiming == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int q = 0; q < kAhead; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
+            for (int q = 0; q < kAhead2; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
 #if KRK_SHA2_PIPELINED
             prologue2p(R0, R1, R2, R3, z, h, is_e, c, kq[0]);
 #endif
