@@ -623,7 +623,9 @@ __device__ __forceinline__ void sha8_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
 // needs quad j + 3, read one group earlier), so ONE s_waitcnt precedes every 12 rounds;
 // 1 = one read and one wait per 4 rounds (round 2's first form).  C2-shaped A/B on one
 // box (profiles/r02/sha8_read_groups.jsonl): 56.2 MB/s a stream with one read a group,
-// 57.2 with pairs, 58.7 with threes, 58.3 with fives (two asm statements a group).
+// 57.2 with pairs, 58.7 with threes, 58.3 with fives (two asm statements a group); the
+// threes' reads issued mid-way through the previous group (two six-round statements)
+// instead of right before its wait: 59.1 vs 59.2 (profiles/r02/sha8_read_split.jsonl).
 #ifndef KRK_SHA8_GROUP
 #define KRK_SHA8_GROUP 3
 #endif
