@@ -3,7 +3,7 @@
 // HBM and by krk_sha256_host / krk_metainfo_digest_host on blobs in host memory).
 //
 // SHA-256 is one sequential chain per blob (core/digester.go:28-72).  A GPU stream runs
-// at ~56 MB/s (eight lanes), one x86 core with the SHA extensions at
+// at ~59 MB/s (eight lanes), one x86 core with the SHA extensions at
 // ~2 GB/s.  A batch whose longest blobs dominate (C1: one 1 GiB blob; the log-uniform
 // regen batches of C5) therefore finishes sooner when host threads take the longest
 // chains -- reading them out of HBM through pinned double buffers -- while the GPU
@@ -68,17 +68,18 @@ double host_crc_rate() {
 // GPU time of m streams (longest `longest` bytes, `bytes` in all) under the AUTO launch
 // plan: the longest chain at the plan's per-stream rate, or the chip's aggregate SHA
 // throughput when the streams outnumber what runs at once (measured on MI355X,
-// profiles/r02/sha_plans_c3shape.jsonl; aggregates scale with the CU count).
+// profiles/r02/sha_plans_c3shape.jsonl with the rates of sha8_read_groups.jsonl and
+// sha2_read_groups.jsonl; aggregates scale with the CU count).
 double gpu_seconds(uint64_t longest, double bytes, uint64_t m, int cus) {
     if (!m) return 0;
     const double scale = cus / 256.0;
     double r, cap;
     if (m <= 16ull * (uint64_t)cus) {
-        r = 55e6;
+        r = 58e6;
         cap = 1e30;
     } else if (m <= 64ull * (uint64_t)cus) {
-        r = 48e6;
-        cap = 790e9 * scale;
+        r = 51e6;
+        cap = 840e9 * scale;
     } else {
         r = 33e6;
         cap = 1.1e12 * scale;
