@@ -154,10 +154,10 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *                   them; a digester's midstate chains through its own requests
  *                   only).  Creation allocates nothing on the device.
  *   KRK_PLACE_HOST  SHA-NI on the caller's thread (host_meta.cpp): ~2 GB/s per stream
- *                   against ~56 MB/s for one GPU stream.
+ *                   against ~59 MB/s for one GPU stream.
  *   KRK_PLACE_AUTO  (krk_digester_new) HOST while at most N digesters are live in the
  *                   process, GPU beyond: the crossover where the host's aggregate
- *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~56 MB/s).
+ *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~59 MB/s).
  *                   N = 40 x the CPUs this process may use, or KRK_DIGESTER_HOST_STREAMS,
  *                   or krk_set_digester_host_streams (-1 restores the default).
  * Without a gfx950 device every constructor fails with KRK_ENODEV. */
@@ -263,7 +263,7 @@ int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums
 
 /* --------------------------------------- host crossover primitives (CPU)
  * The host side of the Digester / PieceHash crossovers: a single
- * SHA-256 stream digests ~2 GB/s on one SHA-NI core vs ~56 MB/s on one GPU stream,
+ * SHA-256 stream digests ~2 GB/s on one SHA-NI core vs ~59 MB/s on one GPU stream,
  * and a small crc32.Update is cheaper on the calling thread than a PCIe round trip,
  * so a krk_digester with few concurrent peers and a small krk_crc32_update write
  * run these on the caller's thread.  x86 SHA-NI / PCLMULQDQ when the CPU has them,
@@ -400,7 +400,7 @@ int krk_set_sha_plan(int plan);
 /* Host offload of the longest SHA-256 chains, process-wide (default 0 = off).  With
  * threads > 0, krk_sha256_dev and krk_metainfo_digest_dev hand the longest blobs of a
  * batch to up to `threads` host threads (x86 SHA extensions, ~2 GB/s a thread against
- * ~56 MB/s a GPU stream), which read them from device memory through pinned double
+ * ~59 MB/s a GPU stream), which read them from device memory through pinned double
  * buffers while the GPU hashes the rest and every blob's piece CRCs; the digests land in
  * digests_dev as before.  How many go to the host minimises max(GPU time, host time) and
  * is 0 unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host,

@@ -25,7 +25,7 @@
 // be known when its bytes are submitted.
 //
 // Host crossovers: a digester created while few digesters are live
-// runs SHA-NI on its caller's thread (one core ~2 GB/s vs one GPU stream ~56 MB/s);
+// runs SHA-NI on its caller's thread (one core ~2 GB/s vs one GPU stream ~59 MB/s);
 // crc32.Update calls of at most KRK_CRC_HOST_MAX bytes run on the caller's thread
 // (no PCIe round trip for a small write).  Both are product code (host_meta.cpp).
 #include <sched.h>
@@ -493,7 +493,7 @@ unsigned host_threads() {
 }
 
 // Live digesters up to which new ones run on their caller's thread: where the host's
-// aggregate (threads x ~2 GB/s SHA-NI) still beats the GPU's (streams x ~56 MB/s),
+// aggregate (threads x ~2 GB/s SHA-NI) still beats the GPU's (streams x ~59 MB/s),
 // i.e. 40 streams per host thread.  KRK_DIGESTER_HOST_STREAMS / krk_set_digester_host_streams.
 int64_t host_stream_limit() {
     int64_t v = g_host_streams.load(std::memory_order_relaxed);
