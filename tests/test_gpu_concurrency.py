@@ -87,3 +87,29 @@ def test_init_shutdown_reinit(gpu, orc):
             assert np.array_equal(r[0][i], orc.calc_piece_sums(d, pls[i])[1])
             assert bytes(r[1][i]) == __import__("hashlib").sha256(d.tobytes()).digest()
     assert L.krk_init(1 << 63) == KRK_ENODEV
+
+
+def test_async_d2h_on_two_streams(gpu):
+    """krk_memcpy_d2h_async (the C4 back-to-back steps): copies queued on two library streams
+    behind piece-sum launches land in pinned arrays once each stream is synchronised, and
+    equal the synchronous copy."""
+    import ctypes as C
+    arena = D.BlobArena([(3 << 20) + 5, 1 << 20, 77], 1 << 18, blob_ids=[9, 10, 11])
+    outs = [D.BatchOutputs(arena), D.BatchOutputs(arena)]
+    pins = [D.PinnedArray((arena.total_pieces,), np.uint32) for _ in range(2)]
+    streams = [C.c_void_p(), C.c_void_p()]
+    for st in streams:
+        D.check(D.lib.krk_stream_create(C.byref(st)))
+    try:
+        for k in range(2):
+            D.piece_sums(arena, outs[k], stream=streams[k])
+            pins[k].fill_from_async(outs[k].sums, streams[k])
+        for st in streams:
+            D.check(D.lib.krk_stream_sync(st))
+        want = outs[0].sums.to_host(np.uint32, arena.total_pieces)
+        assert want.any()
+        for p in pins:
+            assert np.array_equal(p.a, want)
+    finally:
+        for st in streams:
+            D.lib.krk_stream_destroy(st)
