@@ -30,6 +30,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -203,6 +204,42 @@ def cpu_baseline_metainfo(lens_sample, ids_sample, piece, target_s, passes=3):
     return info, dg, sums
 
 
+C3_CPU_SAMPLE = 256
+
+
+def cpu_baseline_c3(ids, lens, P, dg_gpu, sums_gpu, sums_off_gpu):
+    """C3's CPU baseline (BASELINE.md 2: a seeded 256-blob subset, GB/s): the reference's
+    two passes per blob (origin/blobserver/uploader.go:74-94 digest, then
+    lib/metainfogen/generator.go:41-58 piece sums) on every host core, one blob per
+    thread.  The sample's blobs (100 MiB - 1 GiB each, ~150 GB) cannot all be held, so
+    each thread materialises its next blob untimed in its own buffer and times only the
+    passes (oracle orc_baseline_run_lazy); rate = bytes / (summed busy time / threads).
+    Every sampled blob's digest and piece sums are compared with the GPU run's."""
+    from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
+    O.build()
+    n = len(lens)
+    m = min(n, C3_CPU_SAMPLE)
+    pick = np.sort(np.random.default_rng(0xC3).choice(n, m, replace=False))
+    threads = min(host_cores(), m)
+    lens_s = [int(lens[i]) for i in pick]
+    busy, dgc, (s, off) = O.baseline_run_lazy([ids[i] for i in pick], lens_s, P, threads)
+    ok = True
+    for k, i in enumerate(pick):
+        o, cnt = int(sums_off_gpu[i]), int(off[k + 1] - off[k])
+        ok = ok and bytes(dgc[k]) == bytes(dg_gpu[i]) and np.array_equal(s[int(off[k]):int(off[k + 1])],
+                                                                         sums_gpu[o:o + cnt])
+    total = sum(lens_s)
+    wall = busy / threads
+    return {"value": round(total / wall / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": (f"{m} seeded C3 blobs ({total / 1e9:.1f} GB, {min(lens_s) >> 20}-{max(lens_s) >> 20} MiB): "
+                       "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL), 32 KiB chunks, one blob per thread, "
+                       f"{threads} threads; each blob generated untimed into its thread's buffer, rate = bytes / "
+                       f"(summed busy {busy:.1f} s / threads), oracle/oracle.c"),
+            "seconds": round(wall, 2), "have_shani": bool(O.lib().orc_have_shani()),
+            "have_clmul": bool(O.lib().orc_have_clmul()), "outputs_match_gpu": bool(ok),
+            "blobs_checked_against_gpu": int(m)}
+
+
 def cpu_baseline_hrw(digests, labels, healthy, max_replica, target_s):
     from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
     O.build()
@@ -237,10 +274,18 @@ class Timer:
         return float(t.item())
 
 
+TRAFFIC_SOURCE = ("rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this workload committed under profiles/ "
+                  "(tools/pmc_traffic.py): NOT measured in this run (counters need their own profiler process)")
+VALU_NOTE = "rocprofv3 PMC passes committed under profiles/ (tools/pmc_valu.py): NOT measured in this run"
+
+
 def roofline_obj(kernel, gbps, avg_ms, bytes_launch, traffic):
-    return {"kernel": kernel, "bound": "hbm", "achieved": round(gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(gbps / HBM_PEAK_GBPS, 5), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
-            "algorithmic_bytes_per_launch": bytes_launch}
+    r = {"kernel": kernel, "bound": "hbm", "achieved": round(gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(gbps / HBM_PEAK_GBPS, 5), "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
+         "algorithmic_bytes_per_launch": bytes_launch}
+    if traffic is not None:
+        r["traffic_source"] = TRAFFIC_SOURCE
+    return r
 
 
 def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
@@ -253,6 +298,8 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
             "peak": None, "unit": "GB/s", "frac": None, "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
             "algorithmic_bytes_per_launch": bytes_launch,
             "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5)}}
+    if traffic is not None:
+        roof["traffic_source"] = TRAFFIC_SOURCE
     ib = {"achieved_per_stream_MBps": round(per_stream, 2), "streams": n, "lanes_per_stream": lanes}
     if lanes in (2, 8) and not a.no_ceiling:
         isa, mhz, ceil = sha_isa_ceiling(D, launch, lanes)
@@ -348,12 +395,14 @@ def run_metainfo(a, D, T, rank, world, res):
                         "(DESIGN.md 4.1)")
     valu, valu_src = load_valu(a.workload)
     if valu_src and valu.get("device_resident", {}).get("crc32_pieces"):
-        roof_crc["valu"] = dict(valu["device_resident"]["crc32_pieces"], source=valu_src)
+        roof_crc["valu"] = dict(valu["device_resident"]["crc32_pieces"], source=valu_src, measured_in_this_run=False,
+                               note=VALU_NOTE)
     if dominant == "sha256_multi":
         roof = sha_roofline(a, D, n, lens, sha_gbps, sha_avg, bytes_rank, traffic.get("sha256_multi"),
                             lambda: D.metainfo_digest(arena, out))
     if valu_src and valu.get("device_resident", {}).get(dominant):
-        roof["valu"] = dict(valu["device_resident"][dominant], source=valu_src)
+        roof["valu"] = dict(valu["device_resident"][dominant], source=valu_src, measured_in_this_run=False,
+                            note=VALU_NOTE)
     res.update({"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "steps": a.steps,
                 "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
                 "scaling": "weak", "dtype": "u8",
@@ -372,7 +421,7 @@ def run_metainfo(a, D, T, rank, world, res):
         ev = valu.get("end_to_end") if valu_src else None
         if ev:
             res["end_to_end"]["valu"] = {"sha256_multi": ev.get("sha256_multi"), "crc32_pieces": ev.get("crc32_pieces"),
-                                         "source": valu_src}
+                                         "source": valu_src, "measured_in_this_run": False, "note": VALU_NOTE}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         m = min(n, 2 * host_cores())  # bounded sample: the first blobs of this workload
         cb, dg, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds)
@@ -814,10 +863,12 @@ def run_chunked(a, D, T, rank, world, res):
                         "bytes over the longest blob's chain at the per-stream ISA ceiling (no schedule beats it); "
                         "the windows shrink as blobs finish, so late launches carry few streams")
         res["roofline"] = roof
+    dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
+    sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_c3(ids, lens, P, dg, sums, cb.sums_off)
     if rank == 0:  # spot-check three blobs against the one-shot device path
         pick = sorted({0, n // 2, n - 1})
-        dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
-        sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
         wr.close()
         arena = D.BlobArena([lens[i] for i in pick], P, blob_ids=[ids[i] for i in pick])
         out = D.BatchOutputs(arena)
@@ -943,9 +994,66 @@ def hrw_sweep(D, dbuf, dig, n, steps):
     return out
 
 
+def visible_devices() -> int:
+    """gfx950 devices a rank would see, counted in a child process so that the parent
+    (which only spawns and waits) never initialises the GPU itself."""
+    r = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); "
+                        "from kraken_amd import device as D; print(D.device_count())" % ROOT],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, devices=None, rehearse=False, script=None):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this same
+    command (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, as
+    torch.distributed.run would set them) and wait for them; rank 0 prints the line.
+    Fewer than N visible devices is an error unless `rehearse` (ranks then share the
+    visible devices round-robin and the line says so).  Returns the exit code: 0 only
+    if every rank exited 0; a failed rank ends the others."""
+    if devices is None:
+        devices = visible_devices()
+    if devices < n and not rehearse:
+        print(f"bench.py: --gpus {n} but {devices} gfx950 device(s) visible; pass --rehearse to run {n} ranks "
+              f"on {devices} device(s)", file=sys.stderr, flush=True)
+        return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KRK_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:  # the exact processes this call started
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); without a launcher's WORLD_SIZE, N rank processes are spawned")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow --gpus N on fewer than N devices (ranks share devices; the line says so)")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 3; C5: 50)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 1; C5: 5)")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
@@ -978,7 +1086,11 @@ def main():
     if a.warmup is None:
         a.warmup = WORKLOADS[a.workload].get("warmup", 1)
 
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:], rehearse=a.rehearse))
     rank, world, local = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1), _env_int("LOCAL_RANK", 0)
+    if world != a.gpus and "WORLD_SIZE" in os.environ:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     dist = None
     if world > 1:
         import torch.distributed as dist  # control-plane barrier/max only; no data-path collective
@@ -987,10 +1099,15 @@ def main():
 
     from kraken_amd import device as D
 
-    # one process per GPU; modulo the visible count so a multi-rank rehearsal can share one GPU
-    D.set_device(local % max(1, D.device_count()))
+    # one process per GPU; a --rehearse run shares the visible devices round-robin
+    ndev = D.device_count()
+    if world > ndev and not a.rehearse:
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} gfx950 device(s) visible (pass --rehearse to share)")
+    D.set_device(local % max(1, ndev))
     T = Timer(D, dist)
     res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
+    if world > ndev:
+        res["rehearsal"] = f"{world} ranks on {ndev} device(s): not an N-GPU measurement"
     kind = WORKLOADS[a.workload]["kind"]
     {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen,
      "verify": run_verify}[kind](

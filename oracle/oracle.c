@@ -731,6 +731,55 @@ double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint6
     return t1 - t0;
 }
 
+/* Bounded-memory form for samples too large to hold at once (C3's blobs are 100 MiB -
+ * 1 GiB): each worker thread owns one buffer, takes the next blob, materialises it
+ * (untimed) and times only its two passes.  Returns the summed busy seconds of all
+ * threads; bytes / (busy / threads) is the rate the cores sustain while every one of
+ * them has a blob to hash -- the reference's steady state of many concurrent uploads,
+ * without the end-of-sample tail of a one-shot batch. */
+typedef struct { bl_job* J; const uint64_t* idx; uint64_t maxlen; double busy; } lazy_arg;
+static void* lazy_worker(void* a) {
+    lazy_arg* A = (lazy_arg*)a;
+    bl_job* J = A->J;
+    uint8_t* buf = (uint8_t*)malloc(A->maxlen ? A->maxlen : 1);
+    for (;;) {
+        uint64_t b = __atomic_fetch_add(&J->next, 1, __ATOMIC_RELAXED);
+        if (b >= J->n) break;
+        orc_synth_fill(A->idx[b], 0, buf, J->lengths[b], 0);
+        J->bufs[b] = buf;
+        double t0 = now_s();
+        bl_blob(J, b);
+        A->busy += now_s() - t0;
+        J->bufs[b] = NULL;
+    }
+    free(buf);
+    return NULL;
+}
+
+double orc_baseline_run_lazy(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
+                             int64_t piece_len, int n_threads, int passes, uint8_t* digests_out,
+                             uint32_t* sums_out, const uint64_t* sums_off) {
+    if (n_threads < 1) n_threads = 1;
+    bl_job J;
+    memset(&J, 0, sizeof J);
+    J.bufs = (uint8_t**)calloc(n_blobs ? n_blobs : 1, sizeof(uint8_t*));
+    J.lengths = lengths; J.n = n_blobs; J.piece_len = piece_len; J.fast = 1;
+    J.passes = passes ? passes : 3;
+    J.digests = digests_out; J.sums = sums_out; J.sums_off = sums_off; J.next = 0;
+    uint64_t maxlen = 0;
+    for (uint64_t b = 0; b < n_blobs; b++) maxlen = lengths[b] > maxlen ? lengths[b] : maxlen;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    lazy_arg* la = (lazy_arg*)calloc((size_t)n_threads, sizeof(lazy_arg));
+    for (int i = 0; i < n_threads; i++) {
+        la[i].J = &J; la[i].idx = blob_idx; la[i].maxlen = maxlen;
+        pthread_create(&th[i], NULL, lazy_worker, &la[i]);
+    }
+    double busy = 0;
+    for (int i = 0; i < n_threads; i++) { pthread_join(th[i], NULL); busy += la[i].busy; }
+    free(la); free(th); free(J.bufs);
+    return busy;
+}
+
 typedef struct {
     const uint8_t* digests; uint64_t n; const char* labels; const uint64_t* label_off;
     uint32_t n_nodes; const uint8_t* healthy; int32_t max_replica;

@@ -97,6 +97,12 @@ void orc_synth_fill(uint64_t blob_idx, uint64_t off, uint8_t* out, uint64_t n, i
 double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
                         int64_t piece_len, int n_threads, int fast, int passes, uint64_t repeats,
                         uint8_t* digests_out, uint32_t* sums_out, const uint64_t* sums_off);
+/* Bounded-memory form (one buffer per thread; each blob materialised untimed just
+ * before its passes): returns the SUMMED busy seconds of the threads, so the
+ * sustained rate is bytes / (busy / n_threads).  Always the fast (SHA-NI/PCLMUL) path. */
+double orc_baseline_run_lazy(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
+                             int64_t piece_len, int n_threads, int passes, uint8_t* digests_out,
+                             uint32_t* sums_out, const uint64_t* sums_off);
 /* HRW baseline: GetOrderedNodes + Locations per digest on n_threads. */
 double orc_baseline_hrw(const uint8_t* digests, uint64_t n, const char* labels,
                         const uint64_t* label_off, uint32_t n_nodes, const uint8_t* healthy,

@@ -54,6 +54,8 @@ def _load() -> C.CDLL:
         "orc_synth_fill": (None, [C.c_uint64, C.c_uint64, u8p, C.c_uint64, C.c_int]),
         "orc_baseline_run": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_uint64, u8p, u32p, u64p]),
+        "orc_baseline_run_lazy": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
+                                               u8p, u32p, u64p]),
         "orc_baseline_hrw": (C.c_double, [u8p, C.c_uint64, C.c_char_p, u64p, C.c_uint32, u8p,
                                           C.c_int32, C.c_int, i32p, u8p]),
     }
@@ -248,6 +250,21 @@ def baseline_run(blob_idx, lengths, piece_length: int, threads: int, fast: bool 
     t = lib().orc_baseline_run(_ptr(bi, C.c_uint64), _ptr(ln, C.c_uint64), len(bi), piece_length,
                                threads, 1 if fast else 0, passes, repeats, dp, sp, op)
     return t, dg, (sums, off) if want_outputs else None
+
+
+def baseline_run_lazy(blob_idx, lengths, piece_length: int, threads: int, passes: int = 3):
+    """orc_baseline_run_lazy: one buffer per thread, each blob generated untimed before
+    its passes.  Returns (summed busy seconds, digests, (sums, offsets))."""
+    bi = np.ascontiguousarray(np.asarray(blob_idx, dtype=np.uint64))
+    ln = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+    dg = np.zeros((len(bi), 32), dtype=np.uint8)
+    npieces = [(int(l) + piece_length - 1) // piece_length for l in ln]
+    off = np.zeros(len(bi) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(npieces)
+    sums = np.zeros(max(int(off[-1]), 1), dtype=np.uint32)
+    busy = lib().orc_baseline_run_lazy(_ptr(bi, C.c_uint64), _ptr(ln, C.c_uint64), len(bi), piece_length, threads,
+                                       passes, _ptr(dg, C.c_uint8), _ptr(sums, C.c_uint32), _ptr(off, C.c_uint64))
+    return busy, dg, (sums, off)
 
 
 def baseline_hrw(digests: np.ndarray, labels, healthy, max_replica: int, threads: int):
