@@ -151,8 +151,10 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *                   them into pooled pinned slots (2 MiB, KRK_SLOT_MB) and every
  *                   pending slot of every GPU digester of the device is digested in
  *                   ONE multi-stream sha256_multi launch (a dispatcher thread batches
- *                   them; a digester's midstate chains through its own requests
- *                   only).  Creation allocates nothing on the device.
+ *                   them).  A digester's midstate lives in an HBM row of the engine,
+ *                   so its requests chain through the device in stream order and the
+ *                   next launch is queued behind the running one (up to 4 requests
+ *                   of a digester in flight).  Creation allocates nothing on the device.
  *   KRK_PLACE_HOST  SHA-NI on the caller's thread (host_meta.cpp): ~2 GB/s per stream
  *                   against ~59 MB/s for one GPU stream.
  *   KRK_PLACE_AUTO  (krk_digester_new) HOST while at most N digesters are live in the
@@ -178,6 +180,14 @@ int krk_set_digester_host_streams(int64_t n);
  * requests, pinned staging bytes held by the slot pool. */
 int krk_engine_stats(uint64_t* sha_batches, uint64_t* sha_jobs, uint64_t* crc_batches,
                      uint64_t* crc_requests, uint64_t* pinned_bytes);
+/* The slot pool's HARD cap on pinned staging bytes for the calling thread's device
+ * (default KRK_SLOT_POOL_MB = 4096 MiB; at least one 16-slot chunk).  At the cap a
+ * writer waits for a slot to come back (backpressure) instead of pinning more: slots
+ * are held only by requests in flight, never by an idle digester or piece stream (their
+ * partial data stays in their own host buffer).  Lowering the cap frees nothing already
+ * pinned.  bytes == 0 only reads: *cap_out = the cap, *waits_out = how many times a
+ * writer waited at it (either may be NULL). */
+int krk_engine_set_pool_cap(uint64_t bytes, uint64_t* cap_out, uint64_t* waits_out);
 
 /* ----------------------------------------- metainfo + digest (batch)
  * Both products for every blob in one call: the Digester SHA-256 of
@@ -376,6 +386,22 @@ int krk_set_timing(int on);
  * holds under that load (bench.py prices the SHA-256 issue ceiling with it). */
 int krk_device_clock_mhz(void* stream, double* mhz);
 int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms);
+/* Every timed launch of `kernel` since the last reset, in the order the host issued
+ * them: device, SHA-256 plan (KRK_SHA_PLAN_*; 0 for other kernels), work units
+ * (streams for sha256_multi, work items + runs for crc32_pieces, else 0) and the
+ * launch's start / end in ms after the device's first timed launch (hipEvents on the
+ * launch's own stream, so launches on different streams of one device share the
+ * clock).  Up to `cap` records to out (may be NULL), the total count to *n; the
+ * library keeps the first 2^20 launches.  Lets a test check which plan a launch ran
+ * and whether two launches overlapped on the device. */
+typedef struct krk_launch_rec {
+    int32_t device;
+    int32_t plan;
+    uint64_t units;
+    double start_ms;
+    double end_ms;
+} krk_launch_rec;
+int krk_kernel_timeline(const char* kernel, krk_launch_rec* out, uint64_t cap, uint64_t* n);
 int krk_reset_kernel_stats(void);
 
 /* SHA-256 launch plan: lanes per stream (1, 2 or 8) the library uses for a batch of
@@ -383,6 +409,9 @@ int krk_reset_kernel_stats(void);
  * block -- while the batch leaves SIMDs idle).  Diagnostic; bench.py prices the
  * per-stream issue ceiling of that plan. */
 int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes);
+/* The launch plan itself (KRK_SHA_PLAN_1LANE .. KRK_SHA_PLAN_8LANE_2PAIR below) for a
+ * batch of n_streams streams on the current device under the current plan setting. */
+int krk_sha_plan_for(uint64_t n_streams, int* plan);
 
 /* SHA-256 launch plan, process-wide (default AUTO: eight lanes per stream while the
  * batch leaves SIMDs idle, then two lanes, then two producer/consumer pairs per

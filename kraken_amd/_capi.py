@@ -39,6 +39,11 @@ class krk_chunk(C.Structure):
                 ("blob", C.c_uint64)]
 
 
+class krk_launch_rec(C.Structure):
+    _fields_ = [("device", C.c_int32), ("plan", C.c_int32), ("units", C.c_uint64), ("start_ms", C.c_double),
+                ("end_ms", C.c_double)]
+
+
 class krk_nodes(C.Structure):
     _fields_ = [("labels", C.c_char_p), ("label_off", C.POINTER(C.c_uint64)),
                 ("weights", C.POINTER(C.c_int64)), ("n_nodes", C.c_uint32)]
@@ -82,6 +87,7 @@ def _load() -> C.CDLL:
         "krk_digester_placement": (i, [vp, C.POINTER(C.c_int)]),
         "krk_set_digester_host_streams": (i, [C.c_int64]),
         "krk_engine_stats": (i, [u64p, u64p, u64p, u64p, u64p]),
+        "krk_engine_set_pool_cap": (i, [C.c_uint64, u64p, u64p]),
         "krk_set_devices": (i, [C.POINTER(C.c_int), C.c_uint32]),
         "krk_get_devices": (i, [C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint32)]),
         "krk_metainfo_digest_host_multi": (i, [blobp, C.c_uint64, u32p, u8p]),
@@ -135,6 +141,8 @@ def _load() -> C.CDLL:
         "krk_sha_lanes_per_stream": (i, [C.c_uint64, C.POINTER(C.c_int)]),
         "krk_kernel_stats": (i, [C.c_char_p, u64p, f64p]),
         "krk_reset_kernel_stats": (i, []),
+        "krk_kernel_timeline": (i, [C.c_char_p, C.POINTER(krk_launch_rec), C.c_uint64, u64p]),
+        "krk_sha_plan_for": (i, [C.c_uint64, C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

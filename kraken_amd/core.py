@@ -311,53 +311,100 @@ class MetaInfo:
         return json.dumps(obj, separators=(",", ":")).encode()
 
 
-def _json_field(obj: dict, key: str, kind, zero):
-    """encoding/json into a typed struct field: absent or null -> the zero value,
-    a wrong JSON type -> "cannot unmarshal" (Go matches keys case-insensitively)."""
-    v = obj.get(key, None)
-    if v is None:
-        for k2, v2 in obj.items():
-            if k2.lower() == key.lower():
-                v = v2
-                break
-    if v is None:
-        return zero
-    if kind is int:
-        if isinstance(v, bool) or not isinstance(v, int):
-            raise ValueError(f"cannot unmarshal {type(v).__name__} into Go struct field info.{key} of type int64")
-        return v
-    if kind is str:
-        if not isinstance(v, str):
-            raise ValueError(f"cannot unmarshal {type(v).__name__} into Go struct field info.{key} of type string")
-        return v
-    if not isinstance(v, list) or not all(isinstance(x, int) and not isinstance(x, bool) and 0 <= x < 1 << 32
-                                          for x in v):
-        raise ValueError(f"cannot unmarshal {type(v).__name__} into Go struct field info.{key} of type uint32")
-    return v
+class _JObj(list):
+    """A JSON object as its (key, value) pairs in document order (duplicates kept)."""
+
+
+class _JNum(str):
+    """A JSON number that is not an integer literal, kept as its text."""
+
+
+def _go_kind(v) -> str:
+    if isinstance(v, _JObj):
+        return "object"
+    if isinstance(v, list):
+        return "array"
+    if isinstance(v, bool):
+        return "bool"
+    if isinstance(v, (int, _JNum)):
+        return "number"
+    return "string"
+
+
+def _type_error(v, field: str, gotype: str) -> ValueError:
+    what = f"number {v}" if isinstance(v, (int, _JNum)) and not isinstance(v, bool) else _go_kind(v)
+    return ValueError(f"cannot unmarshal {what} into Go struct field {field} of type {gotype}")
+
+
+_INFO_FIELDS = {"PieceLength": "int64", "PieceSums": "[]uint32", "Name": "string", "Length": "int64"}
+
+
+def _match_field(key: str, fields) -> str | None:
+    """encoding/json field lookup: the exact name, else a case-insensitive match."""
+    if key in fields:
+        return key
+    return next((f for f in fields if f.lower() == key.lower()), None)
+
+
+def _decode_info(pairs) -> dict:
+    """json.Unmarshal of an object into core.info (core/metainfo.go:29-35): keys are
+    applied in document order (a later duplicate wins); null leaves an int64 / string
+    field unchanged and sets the slice to nil; a value of the wrong kind, or a number
+    outside the field's range, is Go's UnmarshalTypeError."""
+    out = {"PieceLength": 0, "PieceSums": None, "Name": "", "Length": 0}
+    for key, v in pairs:
+        f = _match_field(key, _INFO_FIELDS)
+        if f is None:
+            continue
+        field = f"info.{f}"
+        if f in ("PieceLength", "Length"):
+            if v is None:
+                continue
+            if isinstance(v, bool) or not isinstance(v, int) or not -(1 << 63) <= v < (1 << 63):
+                raise _type_error(v, field, "int64")
+            out[f] = v
+        elif f == "Name":
+            if v is None:
+                continue
+            if not isinstance(v, str) or isinstance(v, _JNum):
+                raise _type_error(v, field, "string")
+            out[f] = str(v)
+        else:
+            if v is None:
+                out[f] = None
+                continue
+            if not isinstance(v, list) or isinstance(v, _JObj):
+                raise _type_error(v, field, "[]uint32")
+            for x in v:
+                if isinstance(x, bool) or not isinstance(x, int) or not 0 <= x < (1 << 32):
+                    raise _type_error(x, field, "uint32")
+            out[f] = list(v)
+    return out
 
 
 def DeserializeMetaInfo(data: bytes) -> MetaInfo:
-    """core/metainfo.go:136-155.  Missing fields and a null Info take Go's zero values
-    (json.Unmarshal into metaInfoJSON), so a truncated sidecar fails the way the
-    reference does: "parse name: invalid sha256: ..."."""
+    """core/metainfo.go:136-155 with encoding/json's rules for metaInfoJSON: missing
+    fields and a null Info take Go's zero values, so a truncated sidecar fails the way
+    the reference does ("parse name: invalid sha256: ..."); type and range errors read
+    "json: cannot unmarshal <kind> into Go struct field info.<Field> of type <T>"."""
     try:
-        j = json.loads(data)
+        j = json.loads(data, object_pairs_hook=_JObj, parse_float=_JNum)
         if j is None:
-            j = {}
-        if not isinstance(j, dict):
-            raise ValueError(f"cannot unmarshal {type(j).__name__} into Go value of type core.metaInfoJSON")
-        info = next((v for k, v in j.items() if k.lower() == "info"), None) if "Info" not in j else j["Info"]
-        if info is None:
-            info = {}
-        if not isinstance(info, dict):
-            raise ValueError(f"cannot unmarshal {type(info).__name__} into Go struct field metaInfoJSON.Info "
-                             "of type core.info")
-        pl = _json_field(info, "PieceLength", int, 0)
-        sums = _json_field(info, "PieceSums", list, None)
-        name = _json_field(info, "Name", str, "")
-        length = _json_field(info, "Length", int, 0)
+            j = _JObj()
+        if not isinstance(j, _JObj):
+            raise ValueError(f"cannot unmarshal {_go_kind(j)} into Go value of type core.metaInfoJSON")
+        info = _JObj()
+        for key, v in j:
+            if _match_field(key, ("Info",)) is None or v is None:
+                continue
+            if not isinstance(v, _JObj):
+                raise ValueError(f"cannot unmarshal {_go_kind(v)} into Go struct field metaInfoJSON.Info "
+                                 "of type core.info")
+            info = _JObj(list(info) + list(v))  # a repeated Info key merges into the same struct
+        fields = _decode_info(info)
     except (ValueError, TypeError) as e:
         raise ValueError(f"json: {e}") from None
+    pl, sums, name, length = fields["PieceLength"], fields["PieceSums"], fields["Name"], fields["Length"]
     arr = None if sums is None else np.asarray(sums, dtype=np.uint32)
     ih = _info_hash(pl, arr if arr is not None else np.zeros(0, np.uint32), name, length)
     try:

@@ -438,6 +438,7 @@ bool crc_variant_valid(int v) {
 hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, const CrcLaunchCfg& cfg,
                             hipStream_t s) {
     if (uint64_t(w.run_items) + w.n_items == 0) return hipSuccess;
+    t_launch_units = uint64_t(w.run_items) + w.n_items;
     switch (cfg.variant) {
         case 7:
             return launch_variant<32, 4, 1024, false, false, 32>(w, tabs, sums, cfg.cus, 1, s);

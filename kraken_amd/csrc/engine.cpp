@@ -7,24 +7,35 @@
 // a PieceHash per received piece).  One launch per call would serialise them and
 // leave the chip empty, so every device context owns:
 //
-//  * a pool of fixed-size pinned staging slots, each with a device mirror: a caller
-//    copies its bytes into a slot on its own thread and issues the slot's H2D on the
-//    engine's copy stream -- no pinning per call, no per-call device allocation;
-//  * two queues, each drained by a dispatcher thread that coalesces every pending
-//    request into ONE launch: SHA-256 requests (one Merkle-Damgard stream each, so
-//    a batch of concurrent digesters is a multi-stream sha256_multi launch) and
-//    CRC-32 requests (crc32_pieces over every pending byte range).
+//  * a pool of fixed-size pinned staging slots, each with a device mirror, under a
+//    HARD pinned-bytes cap (KRK_SLOT_POOL_MB, krk_engine_set_pool_cap): a caller copies
+//    its bytes into a slot on its own thread and issues the slot's H2D on the engine's
+//    copy stream; at the cap it waits for a release (backpressure).  Slots are held
+//    only by requests in flight, which the engine always completes -- an owner keeps
+//    its partial data in its own host buffer between calls -- so the wait ends;
+//  * two queues (SHA-256, CRC-32), each with a dispatcher thread that coalesces the
+//    pending requests into ONE launch and a completer thread that retires launches in
+//    order, so up to kMaxInflight launches per queue are on the device at once and the
+//    host's job building, result copies and wake-ups overlap the kernels.
 //
-// Ordering is per request owner, not device-global: a digester's midstate lives on
-// the host between its requests and goes into the next job's descriptor, so the SHA
-// dispatcher takes at most one request per digester per batch (batches run one
-// after the other).  CRC requests carry no state at all: each piece portion is
-// hashed as an independent message and the host folds portions together with the
-// GF(2) combine crc(A||B) = crc(A) * x^(8|B|) ^ crc(B) (crc_math.hpp), so any
-// number of a stream's requests may share a batch and a stream's piece end need not
-// be known when its bytes are submitted.
+// SHA-256 (Digester): every GPU digester owns a row of the engine's HBM state table
+// (8 words) and digest table (32 B).  A request's job starts from that row
+// (kShaFromState, or the IV for the first request) and writes it back, so a
+// digester's requests chain through the device in stream order: the dispatcher takes
+// at most one request per digester per launch and may launch the next batch behind the
+// running one without waiting for its results.  It forms that next batch once every
+// digester of the running batch has its next request queued, or shortly before the
+// running batch is due to end (estimated from the measured per-byte time of earlier
+// batches), so a digester whose next request arrives a little late still makes the
+// next launch.  Only final requests copy anything back (their digests).
 //
-// Host crossovers (DESIGN.md 4.5): a digester created while few digesters are live
+// CRC-32 (PieceHash / piece streams): requests carry no state: each piece portion is
+// hashed as an independent message and the owner's piece sums are folded on the
+// completer thread with the GF(2) combine crc(A||B) = crc(A) * x^(8|B|) ^ crc(B)
+// (crc_math.hpp), in submission order, so any number of a stream's requests may share
+// a launch and a stream's piece end need not be known when its bytes are submitted.
+//
+// Host crossovers (DESIGN.md 4.6): a digester created while few digesters are live
 // runs SHA-NI on its caller's thread (one core ~2 GB/s vs one GPU stream ~59 MB/s);
 // crc32.Update calls of at most KRK_CRC_HOST_MAX bytes run on the caller's thread
 // (no PCIe round trip for a small write).  Both are product code (host_meta.cpp).
@@ -34,6 +45,7 @@
 #include <condition_variable>
 #include <deque>
 #include <thread>
+#include <unordered_map>
 #include <unordered_set>
 
 #include "runtime.hpp"
@@ -45,6 +57,8 @@ void host_sha256_final(const uint32_t h[8], uint64_t absorbed, const uint8_t* ta
 uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);
 
 namespace {
+
+using Clock = std::chrono::steady_clock;
 
 size_t env_size(const char* k, size_t dflt) {
     const char* v = getenv(k);
@@ -64,31 +78,40 @@ class SlotPool {
   public:
     size_t S = 0;  // bytes per slot (multiple of 64)
 
-    int init(size_t slot_bytes, size_t cap_bytes) {
+    void init(size_t slot_bytes, size_t cap_bytes) {
         S = slot_bytes;
-        cap_ = std::max(cap_bytes, S * kPerChunk);
-        return KRK_OK;
+        set_cap(cap_bytes);
     }
 
-    // A free slot; grows the pool one chunk at a time up to its cap, then waits for a
-    // release.  Call with the owning device current.
+    // The hard cap on pinned bytes (at least one chunk).  Lowering it never frees
+    // slots already allocated; it stops further growth.
+    void set_cap(size_t cap_bytes) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            cap_ = std::max(cap_bytes, S * kPerChunk);
+        }
+        cv_.notify_all();
+    }
+
+    // A free slot: grows the pool one chunk at a time while under the cap, else waits
+    // for a release (backpressure).  Call with the owning device current.
     Slot* acquire(int* rc) {
         std::unique_lock<std::mutex> lk(mu_);
-        while (free_.empty()) {
-            // At the cap, wait for a release; the cap is soft: if nothing comes back within
-            // 100 ms (every slot held by an owner that is still filling it) grow anyway
-            // rather than deadlock.
-            if (allocated_ + S * kPerChunk > cap_ &&
-                cv_.wait_for(lk, std::chrono::milliseconds(100)) == std::cv_status::no_timeout)
+        for (;;) {
+            if (!free_.empty()) {
+                Slot* s = free_.back();
+                free_.pop_back();
+                *rc = KRK_OK;
+                return s;
+            }
+            if (allocated_ + S * kPerChunk <= cap_) {
+                *rc = grow();
+                if (*rc) return nullptr;
                 continue;
-            if (!free_.empty()) break;
-            *rc = grow();
-            if (*rc) return nullptr;
+            }
+            ++waits_;
+            cv_.wait(lk);
         }
-        Slot* s = free_.back();
-        free_.pop_back();
-        *rc = KRK_OK;
-        return s;
     }
 
     void release(Slot* s) {
@@ -103,6 +126,14 @@ class SlotPool {
     size_t pinned_bytes() {
         std::lock_guard<std::mutex> g(mu_);
         return allocated_;
+    }
+    size_t cap() {
+        std::lock_guard<std::mutex> g(mu_);
+        return cap_;
+    }
+    uint64_t waits() {
+        std::lock_guard<std::mutex> g(mu_);
+        return waits_;
     }
 
     void destroy() {
@@ -131,21 +162,35 @@ class SlotPool {
     std::vector<void*> host_, dev_;
     size_t allocated_ = 0;
     size_t cap_ = 0;
+    uint64_t waits_ = 0;
 
-    int grow() {  // with mu_ held
+    // With mu_ held.  Everything is created before anything is published, and a
+    // failure undoes what this call made: the pool never holds a half-built chunk.
+    int grow() {
         const size_t bytes = S * kPerChunk;
+        hipEvent_t ev[kPerChunk] = {};
+        for (int i = 0; i < kPerChunk; ++i) {
+            const hipError_t e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+            if (e != hipSuccess) {
+                for (int j = 0; j < i; ++j) hipEventDestroy(ev[j]);
+                set_error(KRK_EHIP, "engine: slot events: %s", hipGetErrorString(e));
+                return KRK_EHIP;
+            }
+        }
         void *h = nullptr, *d = nullptr;
-        KRK_HIP(hipHostMalloc(&h, bytes, hipHostMallocDefault));
-        if (hipMalloc(&d, bytes) != hipSuccess) {
-            hipHostFree(h);
-            set_error(KRK_ENOMEM, "engine: device staging slots (%zu bytes)", bytes);
+        if (hipHostMalloc(&h, bytes, hipHostMallocDefault) != hipSuccess) h = nullptr;
+        if (h && hipMalloc(&d, bytes) != hipSuccess) d = nullptr;
+        if (!h || !d) {
+            if (h) hipHostFree(h);
+            for (auto& e : ev) hipEventDestroy(e);
+            set_error(KRK_ENOMEM, "engine: %s staging slots (%zu bytes)", h ? "device" : "pinned host", bytes);
             return KRK_ENOMEM;
         }
         std::unique_ptr<Slot[]> c(new Slot[kPerChunk]);
         for (int i = 0; i < kPerChunk; ++i) {
             c[i].host = static_cast<uint8_t*>(h) + i * S;
             c[i].dev = static_cast<uint8_t*>(d) + i * S;
-            KRK_HIP(hipEventCreateWithFlags(&c[i].h2d, hipEventDisableTiming));
+            c[i].h2d = ev[i];
             free_.push_back(&c[i]);
         }
         host_.push_back(h);
@@ -162,45 +207,78 @@ struct Waiter {
     std::condition_variable cv;
 };
 
-enum ReqKind { kReqSha, kReqCrc };
-
 struct Req {
-    ReqKind kind = kReqSha;
-    Slot* slot = nullptr;
-    bool release_slot = true;
+    Slot* slot = nullptr;  // released when the request completes
     uint64_t len = 0;
-    const void* owner = nullptr;  // ordering key (SHA: one request per owner per batch)
+    uint64_t seq = 0;             // order of the slot's H2D on the copy stream
+    const void* owner = nullptr;  // ordering key (SHA: one request per owner per launch)
     Waiter* w = nullptr;
-    // SHA: bytes absorbed before this request; final = pad and write the digest.
+    Clock::time_point t_submit;
+    // SHA: the owner's state-table row, bytes absorbed before this request; final =
+    // pad and write the digest (the state row is left as it was: no reset).
+    uint32_t row = 0;
     uint64_t prefix = 0;
     bool final = false;
-    uint32_t* mid = nullptr;  // the owner's midstate (read at dispatch, written on completion)
     uint8_t digest[32] = {};
     // CRC: stream offset of the slot's first byte and the piece length (0: the request
     // is one portion); crcs[k] = crc32 of portion k as an independent message.
     uint64_t off = 0;
     uint64_t P = 0;
     std::vector<uint32_t> crcs;
-    void (*on_done)(Req*) = nullptr;  // runs on the dispatcher thread, in FIFO order
+    void (*on_done)(Req*) = nullptr;  // runs on the completer thread, in FIFO order
     void* ctx = nullptr;
     int rc = KRK_OK;
     std::string err;
     bool done = false;
 };
 
-struct Queue {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<Req*> q;
-    bool stop = false;
-    std::thread th;
-    hipStream_t s = nullptr;
-    uint8_t* h_out = nullptr;  // pinned result buffer, grown on demand
-    size_t h_cap = 0;
+constexpr int kMaxInflight = 3;           // launches per queue on the device at once
+constexpr size_t kOwnerInflight = 4;      // requests per digester / piece stream in flight
+constexpr uint32_t kStateRows = 65536;    // GPU digesters per device (state + digest rows)
+constexpr uint64_t kMaxCrcBatchBytes = 4ull << 30;
+
+struct Inflight {
+    std::vector<Req*> batch;
+    hipEvent_t done = nullptr;
+    int rc = KRK_OK;
+    std::string err;
+    int out_i = -1;  // the queue's pinned result buffer this launch writes
+    uint64_t max_len = 0;
+    Clock::time_point t_launch;
+    // SHA: digest rows [row0, row0 + nrows) copied back (final requests)
+    uint32_t row0 = 0, nrows = 0;
+    // CRC: request i's portion CRCs at base[i] .. base[i + 1] of the results
+    std::vector<uint64_t> base;
+    uint64_t total = 0;
 };
 
-constexpr size_t kMaxShaBatch = 65536;
-constexpr uint64_t kMaxCrcBatchBytes = 4ull << 30;
+struct Queue {
+    std::mutex mu;
+    std::condition_variable cv;       // dispatcher: requests, a retired launch, stop
+    std::condition_variable cv_done;  // completer: a launch to retire
+    std::deque<Req*> q;
+    std::deque<Inflight*> inflight;   // launch order
+    bool stop = false, disp_exited = false;
+    std::thread th, th_done;
+    hipStream_t s = nullptr;
+    uint8_t* out[kMaxInflight] = {};  // pinned result buffers, grown on demand
+    size_t out_cap[kMaxInflight] = {};
+    bool out_busy[kMaxInflight] = {};
+    // SHA coalescing: per owner, requests queued and non-final requests in launches on
+    // the device; `missing` counts owners with requests on the device but none queued
+    // (and no final request formed: a digester that asked for its digest is not
+    // expected back).  A new batch is formed early only when missing == 0.
+    struct Own {
+        int queued = 0, flying = 0;
+        bool closed = false;
+    };
+    bool coalesce = false;  // the SHA queue
+    std::unordered_map<const void*, Own> own;
+    int64_t missing = 0;
+    Clock::time_point due;                        // expected end of the last launch
+    Clock::time_point last_done;                  // when the previous launch retired
+    double ns_per_byte = 1e9 / 59e6;              // per-stream SHA time, EMA of measured launches
+};
 
 }  // namespace
 
@@ -209,74 +287,94 @@ struct Engine {
     int dev = 0;
     SlotPool pool;
     hipStream_t s_copy = nullptr;
+    std::mutex copy_mu;
+    uint64_t copy_seq = 0;
     Queue sha, crc;
+    uint32_t* d_state = nullptr;  // kStateRows x 8 words
+    uint8_t* d_digest = nullptr;  // kStateRows x 32 B
+    std::mutex row_mu;
+    std::vector<uint32_t> free_rows;
+    uint32_t next_row = 0;
+    uint64_t coalesce_us = 2000;  // idle device: how long the first request waits for company
+    uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
+    uint64_t crc_launches = 0;
     std::atomic<uint64_t> sha_batches{0}, sha_jobs{0}, crc_batches{0}, crc_reqs{0};
 };
 
 namespace {
 
-void finish(Req* r, int rc) {
+void finish(Req* r, int rc, const std::string& err) {
     r->rc = rc;
-    if (rc != KRK_OK) r->err = t_err;
+    if (rc != KRK_OK) r->err = err;
     if (r->on_done) r->on_done(r);
     std::lock_guard<std::mutex> g(r->w->mu);
     r->done = true;
     r->w->cv.notify_all();
 }
 
-int grow_out(Queue& Q, size_t n) {
-    if (Q.h_cap >= n) return KRK_OK;
-    if (Q.h_out) hipHostFree(Q.h_out);
-    Q.h_out = nullptr;
-    Q.h_cap = 0;
+int grow_out(Queue& Q, int i, size_t n) {
+    if (Q.out_cap[i] >= n) return KRK_OK;
+    if (Q.out[i]) hipHostFree(Q.out[i]);
+    Q.out[i] = nullptr;
+    Q.out_cap[i] = 0;
     const size_t cap = std::max<size_t>(n, 1 << 20);
-    KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&Q.h_out), cap, hipHostMallocDefault));
-    Q.h_cap = cap;
+    KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&Q.out[i]), cap, hipHostMallocDefault));
+    Q.out_cap[i] = cap;
     return KRK_OK;
 }
 
-// One multi-stream SHA-256 launch over the batch: each request is one job whose
-// initial state is its owner's midstate; outputs (32-B midstate or digest per job)
-// come back in one D2H.
-int run_sha_batch(Engine* E, std::vector<Req*>& batch) {
+// The copy stream's H2D of every request of a batch is done once the last-staged one is
+// (one stream, copies in seq order): one wait instead of one per request.
+int wait_staged(Queue& Q, const std::vector<Req*>& batch) {
+    const Req* last = nullptr;
+    for (const Req* r : batch)
+        if (r->slot && r->len && (!last || r->seq > last->seq)) last = r;
+    if (last) KRK_HIP(hipStreamWaitEvent(Q.s, last->slot->h2d, 0));
+    return KRK_OK;
+}
+
+// One multi-stream SHA-256 launch: job i runs from its owner's state row (or the IV)
+// and writes the row back (non-final) or the owner's digest row (final).
+int launch_sha(Engine* E, Inflight* f) {
     Device* D = E->D;
     Queue& Q = E->sha;
-    const size_t n = batch.size();
+    const size_t n = f->batch.size();
     std::vector<ShaJob> jobs(n);
+    uint32_t lo = UINT32_MAX, hi = 0;
     for (size_t i = 0; i < n; ++i) {
-        Req* r = batch[i];
+        Req* r = f->batch[i];
         ShaJob& j = jobs[i];
         j = ShaJob{};
-        j.ptr = reinterpret_cast<uint64_t>(r->slot ? r->slot->dev : nullptr);
+        j.ptr = reinterpret_cast<uint64_t>(r->slot ? r->slot->dev : reinterpret_cast<uint8_t*>(E->d_state));
         j.len = r->len;
         j.prefix = r->prefix;
-        j.out = (uint32_t)i;
-        j.flags = r->final ? kShaFinal : 0;
-        memcpy(j.h, r->mid, 32);
-        if (r->slot && r->len) KRK_HIP(hipStreamWaitEvent(Q.s, r->slot->h2d, 0));
+        j.out = r->row;
+        j.flags = (r->final ? kShaFinal : 0) | (r->prefix ? kShaFromState : 0);
+        memcpy(j.h, kIV, 32);
+        f->max_len = std::max<uint64_t>(f->max_len, r->len);
+        if (r->final) lo = std::min(lo, r->row), hi = std::max(hi, r->row);
     }
-    uint8_t* d_out = nullptr;
-    KRK_HIP(scratch_alloc(D, &d_out, 64 * n, Q.s));
-    int rc = run_jobs(D, jobs, d_out + 32 * n, reinterpret_cast<uint32_t*>(d_out), Q.s);
-    if (!rc) rc = grow_out(Q, 64 * n);
-    if (!rc && hipMemcpyAsync(Q.h_out, d_out, 64 * n, hipMemcpyDeviceToHost, Q.s) != hipSuccess) {
-        set_error(KRK_EHIP, "engine: SHA result copy");
-        rc = KRK_EHIP;
+    int rc = wait_staged(Q, f->batch);
+    if (!rc) rc = run_jobs(D, jobs, E->d_digest, E->d_state, Q.s);
+    if (!rc && lo <= hi) {
+        f->row0 = lo;
+        f->nrows = hi - lo + 1;
+        rc = grow_out(Q, f->out_i, 32ull * f->nrows);
+        if (!rc && hipMemcpyAsync(Q.out[f->out_i], E->d_digest + 32ull * lo, 32ull * f->nrows, hipMemcpyDeviceToHost,
+                                  Q.s) != hipSuccess) {
+            set_error(KRK_EHIP, "engine: SHA digest copy");
+            rc = KRK_EHIP;
+        }
     }
-    scratch_free(D, d_out, Q.s);
-    if (hipStreamSynchronize(Q.s) != hipSuccess && !rc) {
-        set_error(KRK_EHIP, "engine: SHA batch failed");
-        rc = KRK_EHIP;
-    }
-    if (rc) return rc;
-    for (size_t i = 0; i < n; ++i) {
-        Req* r = batch[i];
-        if (r->final) memcpy(r->digest, Q.h_out + 32 * n + 32 * i, 32);
-        else memcpy(r->mid, Q.h_out + 32 * i, 32);  // the owner waits for this request: no race
-    }
+    return rc;
+}
+
+void complete_sha(Engine* E, Inflight* f) {
+    if (f->rc) return;
+    for (Req* r : f->batch)
+        if (r->final) memcpy(r->digest, E->sha.out[f->out_i] + 32ull * (r->row - f->row0), 32);
     E->sha_batches.fetch_add(1, std::memory_order_relaxed);
-    E->sha_jobs.fetch_add(n, std::memory_order_relaxed);
-    return KRK_OK;
+    E->sha_jobs.fetch_add(f->batch.size(), std::memory_order_relaxed);
 }
 
 // Portions of stream bytes [a, a+len) cut at multiples of P (P == 0: one portion).
@@ -313,23 +411,24 @@ Portions portions(uint64_t a, uint64_t len, uint64_t P) {
     return p;
 }
 
-int run_crc_batch(Engine* E, std::vector<Req*>& batch) {
+int launch_crc(Engine* E, Inflight* f) {
     Device* D = E->D;
     Queue& Q = E->crc;
     ItemBuilder B;
     CrcBatch cb;
-    std::vector<uint64_t> base(batch.size());
+    auto& batch = f->batch;
+    f->base.assign(batch.size() + 1, 0);
     uint64_t total = 0;
     for (size_t i = 0; i < batch.size(); ++i) {
         Req* r = batch[i];
-        base[i] = total;
+        f->base[i] = total;
         const Portions p = portions(r->off, r->len, r->P);
         total += p.count;
+        f->max_len = std::max<uint64_t>(f->max_len, r->len);
         if (!p.count) continue;
-        KRK_HIP(hipStreamWaitEvent(Q.s, r->slot->h2d, 0));
         const uint64_t dev = reinterpret_cast<uint64_t>(r->slot->dev);
         const uint64_t a = r->off, b = r->off + r->len;
-        uint64_t idx = base[i];
+        uint64_t idx = f->base[i];
         auto part = [&](uint64_t s, uint64_t e) {  // a portion hashed as its own message
             B.piece(cb.items, dev + (s - a), s, e, s, e, (uint32_t)idx++, 0xFFFFFFFFu);
         };
@@ -340,53 +439,99 @@ int run_crc_batch(Engine* E, std::vector<Req*>& batch) {
         }
         if (p.tail) part(std::max(a, p.f1 * r->P), b);
     }
+    f->base[batch.size()] = total;
+    f->total = total;
     if (total >= (1ull << 32)) {
         set_error(KRK_EINVAL, "engine: more than 2^32 CRC portions in one batch");
         return KRK_EINVAL;
     }
+    if (!total) return KRK_OK;
+    int rc = wait_staged(Q, batch);
+    if (rc) return rc;
     uint32_t* d_sums = nullptr;
-    if (total) {
-        KRK_HIP(scratch_alloc(D, &d_sums, total * 4, Q.s));
-        KRK_HIP(hipMemsetAsync(d_sums, 0, total * 4, Q.s));
+    KRK_HIP(scratch_alloc(D, &d_sums, total * 4, Q.s));
+    if (hipMemsetAsync(d_sums, 0, total * 4, Q.s) != hipSuccess) {
+        set_error(KRK_EHIP, "engine: CRC sums clear");
+        rc = KRK_EHIP;
     }
-    int rc = total ? run_items(D, cb, d_sums, Q.s) : KRK_OK;
-    if (!rc && total) rc = grow_out(Q, total * 4);
-    if (!rc && total && hipMemcpyAsync(Q.h_out, d_sums, total * 4, hipMemcpyDeviceToHost, Q.s) != hipSuccess) {
+    if (!rc) rc = run_items(D, cb, d_sums, Q.s);
+    if (!rc) rc = grow_out(Q, f->out_i, total * 4);
+    if (!rc && hipMemcpyAsync(Q.out[f->out_i], d_sums, total * 4, hipMemcpyDeviceToHost, Q.s) != hipSuccess) {
         set_error(KRK_EHIP, "engine: CRC result copy");
         rc = KRK_EHIP;
     }
-    if (d_sums) scratch_free(D, d_sums, Q.s);
-    if (hipStreamSynchronize(Q.s) != hipSuccess && !rc) {
-        set_error(KRK_EHIP, "engine: CRC batch failed");
-        rc = KRK_EHIP;
-    }
-    if (rc) return rc;
-    const uint32_t* res = reinterpret_cast<const uint32_t*>(Q.h_out);
-    for (size_t i = 0; i < batch.size(); ++i) {
-        const uint64_t c = (i + 1 < batch.size() ? base[i + 1] : total) - base[i];
-        batch[i]->crcs.assign(res + base[i], res + base[i] + c);
-    }
-    E->crc_batches.fetch_add(1, std::memory_order_relaxed);
-    E->crc_reqs.fetch_add(batch.size(), std::memory_order_relaxed);
-    return KRK_OK;
+    scratch_free(D, d_sums, Q.s);
+    return rc;
 }
+
+void complete_crc(Engine* E, Inflight* f) {
+    if (f->rc) return;
+    const uint32_t* res = reinterpret_cast<const uint32_t*>(E->crc.out[f->out_i]);
+    for (size_t i = 0; i < f->batch.size(); ++i) f->batch[i]->crcs.assign(res + f->base[i], res + f->base[i + 1]);
+    E->crc_batches.fetch_add(1, std::memory_order_relaxed);
+    E->crc_reqs.fetch_add(f->batch.size(), std::memory_order_relaxed);
+}
+
+// Owner bookkeeping for the SHA coalescing (with Q.mu held): apply `f` to o's counts
+// and keep Q.missing = #owners with requests on the device, none queued, not closed.
+template <class F>
+void own_update(Queue& Q, const void* o, F&& f) {
+    Queue::Own& w = Q.own[o];
+    const bool before = w.flying > 0 && w.queued == 0 && !w.closed;
+    f(w);
+    const bool after = w.flying > 0 && w.queued == 0 && !w.closed;
+    Q.missing += (after ? 1 : 0) - (before ? 1 : 0);
+    if (w.queued == 0 && w.flying == 0) Q.own.erase(o);
+}
+
+// Every owner with requests on the device has its next request queued.
+bool expected_present(const Queue& Q) { return !Q.inflight.empty() && Q.missing == 0 && !Q.q.empty(); }
 
 void dispatcher(Engine* E, Queue* Q, bool sha) {
     hipSetDevice(E->dev);
     t_dev = E->dev;
-    std::vector<Req*> batch;
     for (;;) {
+        auto* f = new Inflight();
         {
             std::unique_lock<std::mutex> lk(Q->mu);
-            Q->cv.wait(lk, [&] { return Q->stop || !Q->q.empty(); });
-            if (Q->q.empty()) return;  // stop requested and drained
+            Q->cv.wait(lk, [&] { return (Q->stop && Q->q.empty()) || (!Q->q.empty() && Q->inflight.size() < kMaxInflight); });
+            if (Q->q.empty()) {  // stop requested and drained
+                delete f;
+                Q->disp_exited = true;
+                Q->cv_done.notify_all();
+                return;
+            }
             if (sha) {
-                // FIFO, the oldest request of each owner (its midstate chains through
-                // the batches, which run one after the other)
+                // Coalesce: on an idle device the first request waits coalesce_us for
+                // company; behind running launches, the next batch is formed once every
+                // owner with requests on the device has its next request queued, or ~1 ms
+                // before the last launch is due to end.  (Forming it as soon as SOME owners
+                // are back splits the owners into groups that alternate between launches:
+                // each would then run at a fraction of the per-stream rate.)
+                for (;;) {
+                    if (Q->stop || expected_present(*Q)) break;  // every owner on the device is back
+                    const auto until = Q->inflight.empty()
+                                           ? Q->q.front()->t_submit + std::chrono::microseconds(E->coalesce_us)
+                                           : Q->due - std::chrono::milliseconds(1);
+                    if (Clock::now() >= until) break;
+                    Q->cv.wait_until(lk, until);
+                    if (Q->q.empty()) break;
+                }
+                if (Q->q.empty()) {
+                    delete f;
+                    continue;
+                }
+                // FIFO, the oldest request of each owner (its state row chains through
+                // the launches, which run one after the other on the queue's stream)
                 std::unordered_set<const void*> seen;
-                for (auto it = Q->q.begin(); it != Q->q.end() && batch.size() < kMaxShaBatch;) {
+                for (auto it = Q->q.begin(); it != Q->q.end() && f->batch.size() < kStateRows;) {
                     if (seen.insert((*it)->owner).second) {
-                        batch.push_back(*it);
+                        Req* r = *it;
+                        f->batch.push_back(r);
+                        own_update(*Q, r->owner, [&](Queue::Own& w) {
+                            --w.queued;
+                            if (r->final) w.closed = true;
+                        });
                         it = Q->q.erase(it);
                     } else {
                         ++it;
@@ -394,30 +539,125 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                 }
             } else {
                 uint64_t bytes = 0;
-                while (!Q->q.empty() && (batch.empty() || bytes + Q->q.front()->len <= kMaxCrcBatchBytes)) {
+                while (!Q->q.empty() && (f->batch.empty() || bytes + Q->q.front()->len <= kMaxCrcBatchBytes)) {
                     bytes += Q->q.front()->len;
-                    batch.push_back(Q->q.front());
+                    f->batch.push_back(Q->q.front());
                     Q->q.pop_front();
                 }
             }
+            for (int i = 0; i < kMaxInflight; ++i)
+                if (!Q->out_busy[i]) {
+                    Q->out_busy[i] = true;
+                    f->out_i = i;
+                    break;
+                }
         }
-        const int rc = sha ? run_sha_batch(E, batch) : run_crc_batch(E, batch);
-        for (Req* r : batch) {
-            if (r->release_slot) E->pool.release(r->slot);
-            finish(r, rc);
+        f->t_launch = Clock::now();
+        if (!sha && ++E->crc_launches == E->fail_crc_at) {
+            set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
+                      (unsigned long long)E->crc_launches);
+            f->rc = KRK_EHIP;
+        } else {
+            f->rc = sha ? launch_sha(E, f) : launch_crc(E, f);
         }
-        batch.clear();
+        if (!f->rc) {
+            if (hipEventCreateWithFlags(&f->done, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(f->done, Q->s) != hipSuccess) {
+                set_error(KRK_EHIP, "engine: launch event");
+                f->rc = KRK_EHIP;
+            }
+        }
+        if (f->rc) f->err = t_err;
+        {
+            std::lock_guard<std::mutex> g(Q->mu);
+            if (sha) {
+                for (const Req* r : f->batch)
+                    if (!r->final) own_update(*Q, r->owner, [](Queue::Own& w) { ++w.flying; });
+                const auto start = std::max(f->t_launch, Q->inflight.empty() ? f->t_launch : Q->due);
+                Q->due = start + std::chrono::nanoseconds((int64_t)(Q->ns_per_byte * (double)f->max_len));
+            }
+            Q->inflight.push_back(f);
+        }
+        Q->cv_done.notify_one();
+    }
+}
+
+// Retires launches in order: waits for the device, hands results to the requests,
+// releases their slots and wakes their owners.
+void completer(Engine* E, Queue* Q, bool sha) {
+    hipSetDevice(E->dev);
+    t_dev = E->dev;
+    for (;;) {
+        Inflight* f = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(Q->mu);
+            Q->cv_done.wait(lk, [&] { return !Q->inflight.empty() || Q->disp_exited; });
+            if (Q->inflight.empty()) return;
+            f = Q->inflight.front();
+        }
+        if (!f->rc && f->done && hipEventSynchronize(f->done) != hipSuccess) {
+            set_error(KRK_EHIP, "engine: %s batch failed", sha ? "SHA" : "CRC");
+            f->rc = KRK_EHIP;
+            f->err = t_err;
+        }
+        const auto t_done = Clock::now();
+        if (sha) complete_sha(E, f);
+        else complete_crc(E, f);
+        {
+            // bookkeeping first: once finished, a request (and its owner) may be freed
+            std::lock_guard<std::mutex> g(Q->mu);
+            Q->inflight.pop_front();
+            if (f->out_i >= 0) Q->out_busy[f->out_i] = false;
+            if (sha) {
+                for (const Req* r : f->batch)
+                    if (!r->final) own_update(*Q, r->owner, [](Queue::Own& w) { --w.flying; });
+                if (!f->rc && f->max_len >= (256u << 10)) {  // per-stream time of this launch
+                    const auto start = std::max(f->t_launch, Q->last_done);
+                    const double ns =
+                        (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_done - start).count();
+                    Q->ns_per_byte = 0.7 * Q->ns_per_byte + 0.3 * (ns / (double)f->max_len);
+                }
+            }
+            Q->last_done = t_done;
+        }
+        for (Req* r : f->batch) {
+            E->pool.release(r->slot);
+            finish(r, f->rc, f->err);
+        }
+        if (f->done) hipEventDestroy(f->done);
+        Q->cv.notify_all();
+        delete f;
     }
 }
 
 int engine_start(Engine* E) {
     E->pool.init(env_size("KRK_SLOT_MB", 2) << 20, env_size("KRK_SLOT_POOL_MB", 4096) << 20);
+    E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 2000);
+    E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
+    KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
+    KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));
     KRK_HIP(hipStreamCreateWithFlags(&E->s_copy, hipStreamNonBlocking));
     KRK_HIP(hipStreamCreateWithFlags(&E->sha.s, hipStreamNonBlocking));
     KRK_HIP(hipStreamCreateWithFlags(&E->crc.s, hipStreamNonBlocking));
+    E->sha.last_done = E->crc.last_done = Clock::now();
+    E->sha.coalesce = true;
     E->sha.th = std::thread(dispatcher, E, &E->sha, true);
+    E->sha.th_done = std::thread(completer, E, &E->sha, true);
     E->crc.th = std::thread(dispatcher, E, &E->crc, false);
+    E->crc.th_done = std::thread(completer, E, &E->crc, false);
     return KRK_OK;
+}
+
+void engine_free_resources(Engine* E) {
+    hipSetDevice(E->dev);
+    for (hipStream_t s : {E->s_copy, E->sha.s, E->crc.s})
+        if (s) hipStreamSynchronize(s), hipStreamDestroy(s);
+    for (Queue* Q : {&E->sha, &E->crc})
+        for (auto& p : Q->out)
+            if (p) hipHostFree(p), p = nullptr;
+    if (E->d_state) hipFree(E->d_state);
+    if (E->d_digest) hipFree(E->d_digest);
+    E->pool.destroy();
 }
 
 // The engine of device `id`, started on first use.
@@ -430,8 +670,9 @@ Engine* engine_of(int id, int* rc) {
         E->D = D;
         E->dev = id;
         *rc = engine_start(E);
-        if (*rc) {
-            delete E;  // threads not started when a stream creation failed
+        if (*rc) {  // threads start last: none runs when an allocation failed
+            engine_free_resources(E);
+            delete E;
             return nullptr;
         }
         D->engine = E;
@@ -439,24 +680,55 @@ Engine* engine_of(int id, int* rc) {
     return D->engine;
 }
 
-// Copy done by the caller: issue the slot's H2D (bytes [0, n)) on the copy stream.
-int stage(Engine* E, Slot* s, size_t n) {
-    if (!n) return KRK_OK;
+// r's slot holds r->len bytes copied by the caller: issue its H2D on the copy stream.
+int stage(Engine* E, Req* r) {
+    if (!r->len) return KRK_OK;
     KRK_HIP(hipSetDevice(E->dev));
-    KRK_HIP(hipMemcpyAsync(s->dev, s->host, n, hipMemcpyHostToDevice, E->s_copy));
-    KRK_HIP(hipEventRecord(s->h2d, E->s_copy));
+    std::lock_guard<std::mutex> g(E->copy_mu);
+    KRK_HIP(hipMemcpyAsync(r->slot->dev, r->slot->host, r->len, hipMemcpyHostToDevice, E->s_copy));
+    KRK_HIP(hipEventRecord(r->slot->h2d, E->s_copy));
+    r->seq = ++E->copy_seq;
     return KRK_OK;
 }
 
 void submit(Queue& Q, Req* r) {
+    r->t_submit = Clock::now();
     {
         std::lock_guard<std::mutex> g(Q.mu);
         Q.q.push_back(r);
+        if (Q.coalesce)
+            own_update(Q, r->owner, [](Queue::Own& w) {
+                ++w.queued;
+                w.closed = false;
+            });
     }
-    Q.cv.notify_one();
+    Q.cv.notify_all();
 }
 
-// Wait for r, return its status (the dispatcher's error text moves to this thread).
+// A request over `len` bytes of `src` (copied into a fresh slot on this thread).
+int make_req(Engine* E, const uint8_t* src, uint64_t len, Req** out) {
+    *out = nullptr;
+    Slot* sl = nullptr;
+    if (len) {
+        int rc = KRK_OK;
+        sl = E->pool.acquire(&rc);
+        if (!sl) return rc;
+        memcpy(sl->host, src, len);
+    }
+    auto* r = new Req();
+    r->slot = sl;
+    r->len = len;
+    const int rc = stage(E, r);
+    if (rc) {
+        E->pool.release(sl);
+        delete r;
+        return rc;
+    }
+    *out = r;
+    return KRK_OK;
+}
+
+// Wait for r, return its status (the engine's error text moves to this thread).
 int wait_req(Req* r) {
     std::unique_lock<std::mutex> lk(r->w->mu);
     r->w->cv.wait(lk, [&] { return r->done; });
@@ -471,14 +743,33 @@ void engine_stop(Engine* E) {
             Q->stop = true;
         }
         Q->cv.notify_all();
+        Q->cv_done.notify_all();
         if (Q->th.joinable()) Q->th.join();
+        if (Q->th_done.joinable()) Q->th_done.join();
     }
-    hipSetDevice(E->dev);
-    for (hipStream_t s : {E->s_copy, E->sha.s, E->crc.s})
-        if (s) hipStreamSynchronize(s), hipStreamDestroy(s);
-    for (Queue* Q : {&E->sha, &E->crc})
-        if (Q->h_out) hipHostFree(Q->h_out);
-    E->pool.destroy();
+    engine_free_resources(E);
+}
+
+uint32_t row_acquire(Engine* E, int* rc) {
+    std::lock_guard<std::mutex> g(E->row_mu);
+    if (!E->free_rows.empty()) {
+        const uint32_t r = E->free_rows.back();
+        E->free_rows.pop_back();
+        *rc = KRK_OK;
+        return r;
+    }
+    if (E->next_row < kStateRows) {
+        *rc = KRK_OK;
+        return E->next_row++;
+    }
+    set_error(KRK_ENOMEM, "engine: more than %u GPU digesters on one device", kStateRows);
+    *rc = KRK_ENOMEM;
+    return 0;
+}
+
+void row_release(Engine* E, uint32_t row) {
+    std::lock_guard<std::mutex> g(E->row_mu);
+    E->free_rows.push_back(row);
 }
 
 // ------------------------------------------------------------------ placement
@@ -516,16 +807,19 @@ using namespace krk;
 // ======================================================================= Digester
 struct krk_digester {
     Engine* E = nullptr;  // null: host placement
-    uint32_t h[8];        // midstate after every completed request (host: after every block)
+    // host placement: midstate after every block and the partial block
+    uint32_t h[8];
     uint64_t absorbed = 0;
-    // host placement: the partial block
     uint8_t tail[64];
     size_t ntail = 0;
-    // GPU placement
-    Slot* cur = nullptr;  // slot being filled
+    // GPU placement: the engine state row, bytes not yet submitted (pend[0, fill)),
+    // bytes handed to the engine, requests in flight (submission order)
+    uint32_t row = 0;
+    std::unique_ptr<uint8_t[]> pend;
     size_t fill = 0;
-    uint64_t submitted = 0;  // bytes handed to the engine
+    uint64_t submitted = 0;
     std::deque<Req*> inflight;
+    uint8_t last_digest[32] = {};
     Waiter w;
     int err = KRK_OK;
     std::string err_msg;
@@ -539,7 +833,7 @@ int digester_drain(krk_digester* d, size_t keep) {
         Req* r = d->inflight.front();
         const int rc = wait_req(r);
         d->inflight.pop_front();
-        if (rc == KRK_OK) d->absorbed += r->len;
+        if (rc == KRK_OK && r->final) memcpy(d->last_digest, r->digest, 32);
         delete r;
         if (rc && !d->err) {
             d->err = rc;
@@ -550,33 +844,20 @@ int digester_drain(krk_digester* d, size_t keep) {
     return d->err;
 }
 
-int digester_submit(krk_digester* d, bool final) {
-    Engine* E = d->E;
-    if (!d->cur) {  // a final job with no pending bytes still needs a slot address
-        int rc = KRK_OK;
-        d->cur = E->pool.acquire(&rc);
-        if (!d->cur) return rc;
-        d->fill = 0;
-    }
-    int rc = stage(E, d->cur, d->fill);
+int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool final) {
+    int rc = digester_drain(d, kOwnerInflight - 1);
     if (rc) return rc;
-    auto* r = new Req();
-    r->kind = kReqSha;
-    r->slot = d->cur;
-    r->len = d->fill;
+    Req* r = nullptr;
+    rc = make_req(d->E, src, len, &r);
+    if (rc) return rc;
     r->owner = d;
     r->w = &d->w;
+    r->row = d->row;
     r->prefix = d->submitted;
     r->final = final;
-    r->mid = d->h;
-    r->release_slot = !final;  // after Digest() the digester keeps writing into its slot
     d->inflight.push_back(r);
-    submit(E->sha, r);
-    if (!final) {
-        d->submitted += d->fill;
-        d->cur = nullptr;
-        d->fill = 0;
-    }
+    submit(d->E->sha, r);
+    if (!final) d->submitted += len;
     return KRK_OK;
 }
 
@@ -598,7 +879,8 @@ int krk_digester_new_on(int placement, krk_digester** out) {
     if (!host) {
         int rc = KRK_OK;
         d->E = engine_of(place_device(), &rc);
-        if (!d->E) {
+        if (d->E) d->row = row_acquire(d->E, &rc);
+        if (rc) {
             delete d;
             g_live_digesters.fetch_sub(1);
             return rc;
@@ -642,25 +924,25 @@ int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
         t_err = d->err_msg;
         return d->err;
     }
-    Engine* E = d->E;
-    const size_t S = E->pool.S;
+    const size_t S = d->E->pool.S;
     while (n) {
-        if (!d->cur) {
-            // at most two requests of this digester in flight: the one running and the next
-            int rc = digester_drain(d, 1);
+        if (d->fill == 0 && n >= S) {  // a whole slot straight from the caller's buffer
+            const int rc = digester_submit(d, buf, S, false);
             if (rc) return rc;
-            d->cur = E->pool.acquire(&rc);
-            if (!d->cur) return rc;
-            d->fill = 0;
+            buf += S;
+            n -= S;
+            continue;
         }
+        if (!d->pend) d->pend.reset(new uint8_t[S]);
         const size_t take = std::min<uint64_t>(n, S - d->fill);
-        memcpy(d->cur->host + d->fill, buf, take);
+        memcpy(d->pend.get() + d->fill, buf, take);
         d->fill += take;
         buf += take;
         n -= take;
         if (d->fill == S) {
-            int rc = digester_submit(d, false);
+            const int rc = digester_submit(d, d->pend.get(), S, false);
             if (rc) return rc;
+            d->fill = 0;
         }
     }
     return KRK_OK;
@@ -672,15 +954,14 @@ int krk_digester_sum(krk_digester* d, uint8_t out32[32]) {
         host_sha256_final(d->h, d->absorbed, d->tail, d->ntail, out32);
         return KRK_OK;
     }
-    int rc = digester_drain(d, 0);  // the midstate is current once nothing is in flight
-    if (rc) return rc;
-    rc = digester_submit(d, true);
-    if (rc) return rc;
-    Req* r = d->inflight.back();
-    rc = wait_req(r);
-    d->inflight.pop_back();
-    if (!rc) memcpy(out32, r->digest, 32);
-    delete r;
+    if (d->err) {
+        t_err = d->err_msg;
+        return d->err;
+    }
+    // the pending bytes stay pending (Digest() does not reset: writing may continue)
+    int rc = digester_submit(d, d->pend.get(), d->fill, true);
+    if (!rc) rc = digester_drain(d, 0);
+    if (!rc) memcpy(out32, d->last_digest, 32);
     return rc;
 }
 
@@ -688,7 +969,7 @@ void krk_digester_free(krk_digester* d) {
     if (!d) return;
     if (d->E) {
         digester_drain(d, 0);
-        d->E->pool.release(d->cur);
+        row_release(d->E, d->row);
     }
     g_live_digesters.fetch_sub(1);
     delete d;
@@ -705,10 +986,12 @@ int krk_set_digester_host_streams(int64_t n) {
 struct krk_piece_stream {
     Engine* E = nullptr;
     uint64_t P = 0;
-    Slot* cur = nullptr;
+    std::unique_ptr<uint8_t[]> pend;  // bytes not yet submitted
     size_t fill = 0;
     uint64_t submitted = 0;       // stream bytes handed to the engine
-    std::vector<uint32_t> sums;   // folded on the dispatcher thread, in submission order
+    std::vector<uint32_t> sums;   // folded on the completer thread, in submission order
+    std::atomic<bool> fold_stop{false};    // completer thread: a request failed or broke the order, stop folding
+    std::atomic<bool> fold_broken{false};  // completer thread: a continuation arrived with no start
     std::deque<Req*> inflight;
     Waiter w;
     int err = KRK_OK;
@@ -717,10 +1000,17 @@ struct krk_piece_stream {
 
 namespace {
 
-// Fold a request's portion CRCs into the stream's piece sums (dispatcher thread).
+// Fold a request's portion CRCs into the stream's piece sums (completer thread, the
+// stream's requests in submission order).  Once a request has failed, later ones are
+// not folded: a portion that continues a piece begun in the failed request would index
+// a sum that was never written.
 void stream_fold(Req* r) {
-    if (r->rc) return;
     auto* s = static_cast<krk_piece_stream*>(r->ctx);
+    if (s->fold_stop) return;
+    if (r->rc) {  // the owner sees r->rc when it drains r
+        s->fold_stop = true;
+        return;
+    }
     const uint64_t a = r->off, b = r->off + r->len, P = r->P;
     uint64_t q = a;
     for (uint32_t c : r->crcs) {
@@ -729,8 +1019,12 @@ void stream_fold(Req* r) {
         if (q % P == 0) {
             if (s->sums.size() <= pi) s->sums.resize(pi + 1);
             s->sums[pi] = c;
-        } else {
+        } else if (pi < s->sums.size()) {
             s->sums[pi] = gf2_mulmod(s->sums[pi], x8n(e - q, x8().v)) ^ c;
+        } else {  // a continuation with no start: never expected in submission order
+            s->fold_broken = true;
+            s->fold_stop = true;
+            return;
         }
         q = e;
     }
@@ -747,18 +1041,22 @@ int stream_drain(krk_piece_stream* s, size_t keep) {
             s->err_msg = t_err;
         }
     }
+    if (!s->err && s->fold_broken) {
+        set_error(KRK_EHIP, "engine: piece stream portions out of order");
+        s->err = KRK_EHIP;
+        s->err_msg = t_err;
+    }
     if (s->err) t_err = s->err_msg;
     return s->err;
 }
 
-int stream_submit(krk_piece_stream* s) {
-    if (!s->fill) return KRK_OK;
-    int rc = stage(s->E, s->cur, s->fill);
+int stream_submit(krk_piece_stream* s, const uint8_t* src, uint64_t len) {
+    if (!len) return KRK_OK;
+    int rc = stream_drain(s, kOwnerInflight - 1);
     if (rc) return rc;
-    auto* r = new Req();
-    r->kind = kReqCrc;
-    r->slot = s->cur;
-    r->len = s->fill;
+    Req* r = nullptr;
+    rc = make_req(s->E, src, len, &r);
+    if (rc) return rc;
     r->owner = s;
     r->w = &s->w;
     r->off = s->submitted;
@@ -767,9 +1065,7 @@ int stream_submit(krk_piece_stream* s) {
     r->ctx = s;
     s->inflight.push_back(r);
     submit(s->E->crc, r);
-    s->submitted += s->fill;
-    s->cur = nullptr;
-    s->fill = 0;
+    s->submitted += len;
     return KRK_OK;
 }
 
@@ -802,21 +1098,23 @@ int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n)
     }
     const size_t S = s->E->pool.S;
     while (n) {
-        if (!s->cur) {
-            int rc = stream_drain(s, 3);  // a few requests in flight: the slots recycle
+        if (s->fill == 0 && n >= S) {
+            const int rc = stream_submit(s, buf, S);
             if (rc) return rc;
-            s->cur = s->E->pool.acquire(&rc);
-            if (!s->cur) return rc;
-            s->fill = 0;
+            buf += S;
+            n -= S;
+            continue;
         }
+        if (!s->pend) s->pend.reset(new uint8_t[S]);
         const size_t take = std::min<uint64_t>(n, S - s->fill);
-        memcpy(s->cur->host + s->fill, buf, take);
+        memcpy(s->pend.get() + s->fill, buf, take);
         s->fill += take;
         buf += take;
         n -= take;
         if (s->fill == S) {
-            int rc = stream_submit(s);
+            const int rc = stream_submit(s, s->pend.get(), S);
             if (rc) return rc;
+            s->fill = 0;
         }
     }
     return KRK_OK;
@@ -829,7 +1127,8 @@ int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, 
         t_err = s->err_msg;
         return s->err;
     }
-    int rc = stream_submit(s);
+    int rc = stream_submit(s, s->pend.get(), s->fill);
+    if (!rc) s->fill = 0;
     if (!rc) rc = stream_drain(s, 0);
     if (rc) return rc;
     const uint64_t np = krk_num_pieces(s->submitted, (int64_t)s->P);
@@ -837,6 +1136,8 @@ int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, 
     if (length) *length = s->submitted;
     KRK_CHECK(np <= cap || !sums_out, KRK_ERANGE, "sums capacity %llu < %llu pieces", (unsigned long long)cap,
               (unsigned long long)np);
+    KRK_CHECK(s->sums.size() >= np, KRK_EHIP, "engine: %llu of %llu piece sums folded",
+              (unsigned long long)s->sums.size(), (unsigned long long)np);
     if (sums_out && np) memcpy(sums_out, s->sums.data(), np * 4);
     return KRK_OK;
 }
@@ -844,7 +1145,6 @@ int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, 
 void krk_piece_stream_free(krk_piece_stream* s) {
     if (!s) return;
     stream_drain(s, 0);
-    s->E->pool.release(s->cur);
     delete s;
 }
 
@@ -863,22 +1163,24 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
     Engine* E = engine_of(place_device(), &rc);
     if (!E) return rc;
     Waiter w;
-    std::vector<Req*> reqs;
+    std::deque<Req*> reqs;
     const size_t S = E->pool.S;
+    uint32_t c = crc;
+    auto retire = [&](Req* r) {
+        const int e = wait_req(r);
+        if (e && !rc) rc = e;
+        if (!rc) c = gf2_mulmod(c, x8n(r->len, x8().v)) ^ r->crcs[0];
+        delete r;
+    };
     for (uint64_t off = 0; off < n && !rc; off += S) {
-        Slot* sl = E->pool.acquire(&rc);
-        if (!sl) break;
-        const size_t take = std::min<uint64_t>(S, n - off);
-        memcpy(sl->host, data + off, take);
-        rc = stage(E, sl, take);
-        if (rc) {
-            E->pool.release(sl);
-            break;
+        if (reqs.size() >= kOwnerInflight) {  // bounded: the slots recycle
+            retire(reqs.front());
+            reqs.pop_front();
+            if (rc) break;
         }
-        auto* r = new Req();
-        r->kind = kReqCrc;
-        r->slot = sl;
-        r->len = take;
+        Req* r = nullptr;
+        rc = make_req(E, data + off, std::min<uint64_t>(S, n - off), &r);
+        if (rc) break;
         r->owner = &w;
         r->w = &w;
         r->off = off;
@@ -886,13 +1188,7 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
         reqs.push_back(r);
         submit(E->crc, r);
     }
-    uint32_t c = crc;
-    for (Req* r : reqs) {
-        const int e = wait_req(r);
-        if (e && !rc) rc = e;
-        if (!rc) c = gf2_mulmod(c, x8n(r->len, x8().v)) ^ r->crcs[0];
-        delete r;
-    }
+    for (Req* r : reqs) retire(r);
     if (!rc) *out = c;
     return rc;
 }
@@ -917,10 +1213,21 @@ int krk_engine_stats(uint64_t* sha_batches, uint64_t* sha_jobs, uint64_t* crc_ba
     return KRK_OK;
 }
 
+int krk_engine_set_pool_cap(uint64_t bytes, uint64_t* cap_out, uint64_t* waits_out) {
+    KRK_DEVICE(D0);
+    int rc = KRK_OK;
+    Engine* E = engine_of(D0->id, &rc);
+    if (!E) return rc;
+    if (bytes) E->pool.set_cap(bytes);
+    if (cap_out) *cap_out = E->pool.cap();
+    if (waits_out) *waits_out = E->pool.waits();
+    return KRK_OK;
+}
+
 }  // extern "C"
 
 namespace krk {
-// krk_shutdown: stop the engine of D (its dispatcher threads drain their queues).
+// krk_shutdown: stop the engine of D (its dispatcher and completer threads drain their queues).
 void engine_teardown(Device& D) {
     std::lock_guard<std::mutex> g(D.engine_mu);
     if (D.engine) {

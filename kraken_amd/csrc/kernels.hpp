@@ -5,6 +5,12 @@
 
 namespace krk {
 
+// What the last launcher on this thread launched, for the kernel timeline
+// (krk_kernel_timeline): SHA-256 plan id (KRK_SHA_PLAN_*) and work units (streams for
+// SHA-256, work items + runs for CRC).  Written by the launchers, read by timed().
+inline thread_local int t_launch_plan = 0;
+inline thread_local uint64_t t_launch_units = 0;
+
 // ---------------------------------------------------------------- CRC pieces
 // One work item = a contiguous byte run inside ONE piece, processed by one wave.
 // Its raw CRC is shifted to the piece end (mul = x^(8*(piece_end - item_end))) and
@@ -107,6 +113,7 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
                          uint32_t* out_state, hipStream_t s);
 // Lanes per stream launch_sha256 uses for a batch of n_jobs streams (1 or 2).
 int sha_lanes_for(uint32_t n_jobs);
+int sha_plan_for(uint32_t n_jobs);  // KRK_SHA_PLAN_* the next launch of n_jobs streams uses
 // Process-wide launch plan (KRK_SHA_PLAN_* of kraken_hip.h; diagnostic plans >= 100
 // only in the KRK_DIAG build).
 bool sha_plan_valid(int plan);

@@ -1605,6 +1605,41 @@ int krk_reset_kernel_stats(void) {
     drain_timing();
     std::lock_guard<std::mutex> g(g_tmu);
     for (int k = 0; k < K_N; ++k) { g_ms[k] = 0; g_cnt[k] = 0; }
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (int d = 0; d < kMaxDevs; ++d)
+        if (g_origin[d]) {
+            hipSetDevice(d);
+            hipEventDestroy(g_origin[d]);
+            g_origin[d] = nullptr;
+        }
+    hipSetDevice(cur);
+    g_timeline.clear();
+    return KRK_OK;
+}
+int krk_kernel_timeline(const char* kernel, krk_launch_rec* out, uint64_t cap, uint64_t* n) {
+    KRK_CHECK(kernel && n, KRK_EINVAL, "kernel or n is NULL");
+    int want = -1;
+    for (int k = 0; k < K_N; ++k)
+        if (strcmp(kernel, kKernNames[k]) == 0) want = k;
+    KRK_CHECK(want >= 0, KRK_EINVAL, "unknown kernel '%s'", kernel);
+    drain_timing();
+    std::lock_guard<std::mutex> g(g_tmu);
+    uint64_t m = 0;
+    for (const auto& r : g_timeline) {
+        if (r.k != want) continue;
+        if (out && m < cap) out[m] = {r.dev, r.plan, r.units, r.t0, r.t1};
+        ++m;
+    }
+    *n = m;
+    return KRK_OK;
+}
+int krk_sha_plan_for(uint64_t n_streams, int* plan) {
+    KRK_CHECK(plan, KRK_EINVAL, "plan is NULL");
+    KRK_CHECK(n_streams <= 0xffffffffull, KRK_ERANGE, "too many streams");
+    KRK_DEVICE(D);
+    (void)D;
+    *plan = sha_plan_for((uint32_t)n_streams);
     return KRK_OK;
 }
 

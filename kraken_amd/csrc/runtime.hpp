@@ -52,10 +52,20 @@ inline const char* kKernNames[K_N] = {"crc32_pieces", "sha256_multi", "hrw_order
 inline std::atomic<bool> g_timing{false};
 struct Pending {
     hipEvent_t a, b;
-    int k, dev;
+    int k, dev, plan;
+    uint64_t units;
 };
+struct TimelineRec {
+    int k, dev, plan;
+    uint64_t units;
+    double t0, t1;  // ms after the device's first timed launch since the last reset
+};
+constexpr size_t kTimelineCap = 1u << 20;
+constexpr int kMaxDevs = 64;
 inline std::mutex g_tmu;
 inline std::vector<Pending> g_pending;
+inline std::vector<TimelineRec> g_timeline;
+inline hipEvent_t g_origin[kMaxDevs];  // per device: the first timed launch's start event
 inline double g_ms[K_N];
 inline uint64_t g_cnt[K_N];
 
@@ -66,10 +76,12 @@ inline hipError_t timed(int k, hipStream_t s, F&& f) {
     hipEventCreate(&a);
     hipEventCreate(&b);
     hipEventRecord(a, s);
+    t_launch_plan = 0;
+    t_launch_units = 0;
     hipError_t e = f();
     hipEventRecord(b, s);
     std::lock_guard<std::mutex> g(g_tmu);
-    g_pending.push_back({a, b, k, t_dev});
+    g_pending.push_back({a, b, k, t_dev, t_launch_plan, t_launch_units});
     return e;
 }
 
@@ -81,11 +93,23 @@ inline void drain_timing() {
         hipSetDevice(p.dev);
         hipEventSynchronize(p.b);
         float ms = 0;
+        bool keep_a = false;
         if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
             g_ms[p.k] += ms;
             g_cnt[p.k] += 1;
+            if (p.dev >= 0 && p.dev < kMaxDevs) {
+                if (!g_origin[p.dev]) {
+                    g_origin[p.dev] = p.a;
+                    keep_a = true;
+                }
+                float t0 = 0, t1 = 0;
+                if (g_timeline.size() < kTimelineCap &&
+                    hipEventElapsedTime(&t0, g_origin[p.dev], p.a) == hipSuccess &&
+                    hipEventElapsedTime(&t1, g_origin[p.dev], p.b) == hipSuccess)
+                    g_timeline.push_back({p.k, p.dev, p.plan, p.units, (double)t0, (double)t1});
+            }
         }
-        hipEventDestroy(p.a);
+        if (!keep_a) hipEventDestroy(p.a);
         hipEventDestroy(p.b);
     }
     g_pending.clear();

@@ -1513,6 +1513,8 @@ static bool plan_two_lanes(int p) {
 
 static bool plan_eight_lanes(int p) { return p == KRK_SHA_PLAN_8LANE || p == KRK_SHA_PLAN_8LANE_2PAIR || p == 108; }
 
+int sha_plan_for(uint32_t n_jobs) { return resolve_plan(n_jobs); }
+
 int sha_lanes_for(uint32_t n_jobs) {
     const int p = resolve_plan(n_jobs);
     return plan_eight_lanes(p) ? 8 : plan_two_lanes(p) ? 2 : 1;
@@ -1557,7 +1559,10 @@ static hipError_t launch_ws(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_di
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;
-    switch (resolve_plan(n_jobs)) {
+    const int plan = resolve_plan(n_jobs);
+    t_launch_plan = plan;
+    t_launch_units = n_jobs;
+    switch (plan) {
         case KRK_SHA_PLAN_1LANE: return launch_ws<0, false, 1>(jobs, n_jobs, out_digest, out_state, s);
         case KRK_SHA_PLAN_2LANE: return launch_ws<0, true, 1>(jobs, n_jobs, out_digest, out_state, s);
         case KRK_SHA_PLAN_1LANE_2PAIR: return launch_ws<0, false, 2>(jobs, n_jobs, out_digest, out_state, s);

@@ -6,7 +6,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._capi import check, krk_blob, krk_chunk, krk_nodes, lib
+from ._capi import check, krk_blob, krk_chunk, krk_launch_rec, krk_nodes, lib
 
 ALIGN = 256  # every blob starts 256-byte aligned in the arena
 
@@ -106,6 +106,16 @@ def sha_lanes_per_stream(n_streams: int) -> int:
     """Lanes per SHA-256 stream the library uses for a batch of n_streams (1, 2 or 8)."""
     v = C.c_int(0)
     check(lib.krk_sha_lanes_per_stream(n_streams, C.byref(v)))
+    return v.value
+
+
+SHA_PLAN_NAMES = {1: "1lane", 2: "2lane", 3: "1lane_2pair", 4: "2lane_2pair", 5: "8lane", 6: "8lane_2pair"}
+
+
+def sha_plan_for(n_streams: int) -> int:
+    """KRK_SHA_PLAN_* id the library launches for a batch of n_streams (SHA_PLAN_NAMES)."""
+    v = C.c_int(0)
+    check(lib.krk_sha_plan_for(n_streams, C.byref(v)))
     return v.value
 
 
@@ -383,6 +393,16 @@ class KernelTimer:
 
     def __exit__(self, *a):
         check(lib.krk_set_timing(0))
+
+    @staticmethod
+    def timeline(kernel: str):
+        """[(plan, units, start_ms, end_ms)] of every timed launch of `kernel` since the
+        timer was entered (krk_kernel_timeline)."""
+        n = C.c_uint64()
+        check(lib.krk_kernel_timeline(kernel.encode(), None, 0, C.byref(n)))
+        recs = (krk_launch_rec * max(1, n.value))()
+        check(lib.krk_kernel_timeline(kernel.encode(), recs, n.value, C.byref(n)))
+        return [(r.plan, r.units, r.start_ms, r.end_ms) for r in recs[:n.value]]
 
     @staticmethod
     def stats(kernel: str):

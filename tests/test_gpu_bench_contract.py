@@ -34,3 +34,27 @@ def test_bench_json_line_contract(gpu):
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["outputs_match_gpu"] is True
+
+
+def test_bench_gpus_2_spawns_two_ranks(gpu):
+    """`bench.py --gpus 2` with no launcher spawns two rank processes (here sharing the
+    one GPU: --rehearse) and reports the whole job: n_gpus == 2 and value == both
+    ranks' bytes over the max-over-ranks time."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse", "--blobs", "20",
+                        "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-e2e", "--no-ceiling"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 1 and "rehearsal" in d
+    assert d["config"]["blobs_per_gpu"] == 20 and d["config"]["parallelism"].startswith("blob-sharded x2")
+    want = 2 * d["config"]["bytes_per_gpu"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3) / 1e9
+    assert abs(d["value"] - want) / want < 1e-3, (d["value"], want)
+
+
+def test_bench_gpus_more_than_visible_refused(gpu):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpu.device_count() + 1),
+                        "--blobs", "2", "--steps", "1", "--no-cpu-baseline", "--no-e2e"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode != 0 and "--rehearse" in r.stderr and not r.stdout.strip()

@@ -43,6 +43,68 @@ def test_metainfo_backwards_compatibility_kat():
     assert back.InfoHash() == mi.InfoHash()
 
 
+def test_metainfo_serialize_bytes_pinned_by_fixture():
+    """Serialize (core/metainfo.go:131-134, json.Marshal of
+    metaInfoJSON{info}) emits exactly {"Info": <the fixture's Info object>} for the
+    production metainfo of core/metainfo_test.go:68 -- field order PieceLength,
+    PieceSums, Name, Length, no spaces -- whether the MetaInfo was deserialized from the
+    fixture or built from its fields."""
+    info = (b'{"PieceLength":4194304,"PieceSums":[2131691452],"Name":'
+            b'"289314c356bc2a19802c3e31505506db30ea81a0bcaea4ec3e079524c8ac3cf5","Length":236}')
+    raw = b'{"Info":' + info + b',"Announce":"","AnnounceList":null,"CreationDate":0,"Comment":"","CreatedBy":""}'
+    assert core.DeserializeMetaInfo(raw).Serialize() == b'{"Info":' + info + b'}'
+    name = "289314c356bc2a19802c3e31505506db30ea81a0bcaea4ec3e079524c8ac3cf5"
+    d = core.NewSHA256DigestFromHex(name)
+    ih = core.NewInfoHashFromHex("85b978c4377625b3963df406d0dd3a1da5a7d9c3")
+    built = core.MetaInfo(4194304, np.array([2131691452], dtype=np.uint32), name, 236, d, ih)
+    assert built.Serialize() == b'{"Info":' + info + b'}'
+    # nil PieceSums (a zero-length blob: calcPieceSums returns nil) marshals as null
+    empty = core.MetaInfo(4194304, None, name, 0, d, ih)
+    assert empty.Serialize() == (b'{"Info":{"PieceLength":4194304,"PieceSums":null,"Name":"' + name.encode() +
+                                 b'","Length":0}}')
+
+
+def test_deserialize_follows_encoding_json():
+    """encoding/json rules for metaInfoJSON -- the exact key wins over a
+    case-folded one and a later duplicate over an earlier one; null leaves an int64 /
+    string field at its value and sets the slice to nil; type and range errors are
+    "cannot unmarshal <kind> into Go struct field info.<Field> of type <T>"."""
+    name = "289314c356bc2a19802c3e31505506db30ea81a0bcaea4ec3e079524c8ac3cf5"
+
+    def mk(fields: str) -> bytes:
+        return ('{"Info":{' + fields + '}}').encode()
+
+    base = f'"PieceLength":4194304,"PieceSums":[2131691452],"Name":"{name}"'
+    mi = core.DeserializeMetaInfo(mk(base + ',"Length":236'))
+    assert mi.InfoHash().Hex() == "85b978c4377625b3963df406d0dd3a1da5a7d9c3"
+    # case-insensitive key, later duplicate wins, null keeps the value
+    assert core.DeserializeMetaInfo(mk(base + ',"length":5,"Length":236')).Length() == 236
+    assert core.DeserializeMetaInfo(mk(base + ',"Length":236,"LENGTH":7')).Length() == 7
+    assert core.DeserializeMetaInfo(mk(base + ',"Length":236,"Length":null')).Length() == 236
+    assert core.DeserializeMetaInfo(mk(f'"PieceLength":4,"PieceSums":null,"Name":"{name}"')).PieceSums().size == 0
+    cases = [
+        (',"Length":9223372036854775808', "cannot unmarshal number 9223372036854775808 into Go struct field "
+                                          "info.Length of type int64"),
+        (',"Length":1.5', "cannot unmarshal number 1.5 into Go struct field info.Length of type int64"),
+        (',"Length":"236"', "cannot unmarshal string into Go struct field info.Length of type int64"),
+        (',"Length":true', "cannot unmarshal bool into Go struct field info.Length of type int64"),
+    ]
+    for extra, msg in cases:
+        with pytest.raises(ValueError) as ei:
+            core.DeserializeMetaInfo(mk(base + extra))
+        assert str(ei.value) == "json: " + msg, extra
+    bad_sums = [('[4294967296]', "number 4294967296", "uint32"), ('[-1]', "number -1", "uint32"),
+                ('["x"]', "string", "uint32"), ('{"a":1}', "object", "[]uint32"), ('7', "number 7", "[]uint32")]
+    for arr, what, typ in bad_sums:
+        with pytest.raises(ValueError) as ei:
+            core.DeserializeMetaInfo(mk(f'"PieceLength":4,"PieceSums":{arr},"Name":"{name}","Length":1'))
+        assert str(ei.value) == f"json: cannot unmarshal {what} into Go struct field info.PieceSums of type {typ}"
+    with pytest.raises(ValueError, match="json: cannot unmarshal array into Go value of type core.metaInfoJSON"):
+        core.DeserializeMetaInfo(b"[]")
+    with pytest.raises(ValueError, match="parse name"):
+        core.DeserializeMetaInfo(b'{"Info":null}')
+
+
 def test_metainfo_serialization_limit():
     """core/metainfo_test.go:78-120: 100 GB / 2 MB pieces stays under 512 MB of JSON."""
     n = (100 << 30) // (2 << 20)
