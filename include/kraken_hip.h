@@ -440,9 +440,31 @@ int krk_set_sha_plan(int plan);
  * SHA-256 pass and the CRC pass of a blob are separate host tasks), so the bytes that
  * cross the host link shrink by theirs (the threshold there is 3 %). */
 int krk_set_sha_host_offload(int threads);
-/* The offload plan for `n` blob lengths on `threads` host threads and a device of `cus`
- * CUs, without a device: the indices (longest first) to host_idx (room for n, may be
- * NULL), their count to n_host, and the modelled GPU / host seconds (may be NULL).
+/* The rates the planners use (krk_host_offload_plan, the offload of the batch entry
+ * points, the host/GPU split of the CRC-only host entry points), per device:
+ * sha_stream_bps = one SHA-256 stream's rate at full residency under each AUTO tier
+ * (eight lanes up to 16 x CUs streams, two lanes up to 64 x CUs, one lane beyond),
+ * pinned D2H / H2D copy rates, one host thread's SHA-256 and CRC-32 rates.  Measured on
+ * the calling thread's device at first use (~50 ms: each tier's launch plan timed on
+ * 16 / 64 / 128 x CUs streams, a 64 MiB pinned copy each way); without a device the
+ * nominal MI355X figures (source 0).  krk_planner_rates_set overrides them process-wide
+ * (NULL restores the measured ones): tests inject rates, an operator pins them. */
+#define KRK_RATES_NOMINAL 0
+#define KRK_RATES_MEASURED 1
+#define KRK_RATES_SET 2
+typedef struct krk_planner_rates {
+    double sha_stream_bps[3];
+    double d2h_bps, h2d_bps;
+    double host_sha_bps, host_crc_bps;
+    int32_t cus;
+    int32_t source;
+} krk_planner_rates;
+int krk_planner_rates_get(krk_planner_rates* out);
+int krk_planner_rates_set(const krk_planner_rates* in);
+/* The offload plan for `n` blob lengths on `threads` host threads with the planner rates
+ * (krk_planner_rates_get; `cus` > 0 overrides their CU count), no device work: the
+ * indices (longest first) to host_idx (room for n, may be NULL), their count to n_host,
+ * and the modelled GPU / host seconds (may be NULL).
  * krk_sha_offload_plan plans a device-resident batch (krk_sha256_dev,
  * krk_metainfo_digest_dev); krk_host_offload_plan plans for `mode`
  * KRK_OFFLOAD_DEVICE (the same), KRK_OFFLOAD_HOST_SHA (krk_sha256_host) or

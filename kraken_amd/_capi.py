@@ -44,6 +44,12 @@ class krk_launch_rec(C.Structure):
                 ("end_ms", C.c_double)]
 
 
+class krk_planner_rates(C.Structure):
+    _fields_ = [("sha_stream_bps", C.c_double * 3), ("d2h_bps", C.c_double), ("h2d_bps", C.c_double),
+                ("host_sha_bps", C.c_double), ("host_crc_bps", C.c_double), ("cus", C.c_int32),
+                ("source", C.c_int32)]
+
+
 class krk_nodes(C.Structure):
     _fields_ = [("labels", C.c_char_p), ("label_off", C.POINTER(C.c_uint64)),
                 ("weights", C.POINTER(C.c_int64)), ("n_nodes", C.c_uint32)]
@@ -88,6 +94,8 @@ def _load() -> C.CDLL:
         "krk_set_digester_host_streams": (i, [C.c_int64]),
         "krk_engine_stats": (i, [u64p, u64p, u64p, u64p, u64p]),
         "krk_engine_set_pool_cap": (i, [C.c_uint64, u64p, u64p]),
+        "krk_planner_rates_get": (i, [C.POINTER(krk_planner_rates)]),
+        "krk_planner_rates_set": (i, [C.POINTER(krk_planner_rates)]),
         "krk_set_devices": (i, [C.POINTER(C.c_int), C.c_uint32]),
         "krk_get_devices": (i, [C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint32)]),
         "krk_metainfo_digest_host_multi": (i, [blobp, C.c_uint64, u32p, u8p]),

@@ -114,6 +114,9 @@ hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_diges
 // Lanes per stream launch_sha256 uses for a batch of n_jobs streams (1 or 2).
 int sha_lanes_for(uint32_t n_jobs);
 int sha_plan_for(uint32_t n_jobs);  // KRK_SHA_PLAN_* the next launch of n_jobs streams uses
+// One launch on a given plan whatever the process-wide setting (planner calibration).
+hipError_t launch_sha256_plan(int plan, const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
+                              uint32_t* out_state, hipStream_t s);
 // Process-wide launch plan (KRK_SHA_PLAN_* of kraken_hip.h; diagnostic plans >= 100
 // only in the KRK_DIAG build).
 bool sha_plan_valid(int plan);

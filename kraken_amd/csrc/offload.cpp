@@ -34,10 +34,6 @@ namespace {
 std::atomic<int> g_off_threads{0};
 
 constexpr uint64_t kOffChunk = 8ull << 20;  // D2H chunk (multiple of 64)
-constexpr double kD2H = 50e9;               // device -> pinned host, bytes/s (PCIe Gen5 x16, measured 54)
-// Host-resident batches: pageable -> pinned copy + H2D through the staging windows,
-// bytes/s (C2 end-to-end measured 39.5-54.4 GB/s box to box).
-constexpr double kLinkHost = 45e9;
 
 // One host thread, bytes/s: measured once (16 MiB) and derated for the clock a fully
 // loaded socket holds.  SHA-256 (x86 SHA extensions) and the piece CRC (PCLMUL folding).
@@ -65,25 +61,120 @@ double host_crc_rate() {
     return r;
 }
 
-// GPU time of m streams (longest `longest` bytes, `bytes` in all) under the AUTO launch
-// plan: the longest chain at the plan's per-stream rate, or the chip's aggregate SHA
-// throughput when the streams outnumber what runs at once (measured on MI355X,
-// profiles/r02/sha_plans_c3shape.jsonl with the rates of sha8_read_groups.jsonl and
-// sha2_read_groups.jsonl; aggregates scale with the CU count).
-double gpu_seconds(uint64_t longest, double bytes, uint64_t m, int cus) {
-    if (!m) return 0;
-    const double scale = cus / 256.0;
-    double r, cap;
-    if (m <= 16ull * (uint64_t)cus) {
-        r = 58e6;
-        cap = 1e30;
-    } else if (m <= 64ull * (uint64_t)cus) {
-        r = 51e6;
-        cap = 840e9 * scale;
-    } else {
-        r = 33e6;
-        cap = 1.1e12 * scale;
+// ------------------------------------------------------------------ planner rates
+// Kernel geometry (a property of the code, not of the box): the AUTO launch plan's three
+// tiers -- eight lanes a stream up to 16 x CUs streams, two lanes up to 64 x CUs, one
+// lane beyond -- and the streams each tier keeps resident per CU (one pair a workgroup
+// at eight lanes, two pairs of 32 / 64 streams at two / one lane(s)).
+constexpr uint64_t kTierMaxPerCu[2] = {16, 64};
+constexpr uint64_t kResidentPerCu[3] = {16, 64, 128};
+constexpr int kTierPlan[3] = {KRK_SHA_PLAN_8LANE, KRK_SHA_PLAN_2LANE_2PAIR, KRK_SHA_PLAN_1LANE_2PAIR};
+
+int tier_of(uint64_t m, int cus) {
+    return m <= kTierMaxPerCu[0] * (uint64_t)cus ? 0 : m <= kTierMaxPerCu[1] * (uint64_t)cus ? 1 : 2;
+}
+
+// Without a device and without krk_planner_rates_set (planning on a host that has no
+// GPU, e.g. the CPU tests): one MI355X as measured in rounds 1-2 -- per-stream rates at
+// full residency of 52.6 / 51.6 / 35.7 MB/s (profiles/r02/sha8_probe_c2shape.jsonl,
+// sha2_read_groups.jsonl), PCIe Gen5 x16 pinned copies of 54 GB/s.
+Rates nominal_rates(int cus) {
+    Rates R{};
+    R.stream[0] = 52.6e6;
+    R.stream[1] = 51.6e6;
+    R.stream[2] = 35.7e6;
+    R.d2h = R.h2d = 54e9;
+    R.host_sha = host_rate();
+    R.host_crc = host_crc_rate();
+    R.cus = cus > 0 ? cus : 256;
+    R.source = KRK_RATES_NOMINAL;
+    return R;
+}
+
+// The device's own rates, measured once per device and process (~50 ms): each SHA-256
+// tier's plan timed on 16 / 64 / 128 x CUs streams of 256 KiB (every stream reads the
+// same bytes: the kernel is issue-bound, not HBM-bound), pinned 64 MiB copies each way.
+int calibrate(Device* D, Rates& R) {
+    R = Rates{};
+    R.cus = D->cus;
+    KRK_HIP(hipSetDevice(D->id));
+    const uint64_t L = 256u << 10, C = 64u << 20;
+    const uint32_t mmax = (uint32_t)(kResidentPerCu[2] * (uint64_t)D->cus);
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    uint8_t *d_in = nullptr, *d_dig = nullptr, *d_copy = nullptr, *h_copy = nullptr;
+    uint32_t* d_state = nullptr;
+    ShaJob* d_jobs = nullptr;
+    int rc = KRK_OK;
+    auto ok = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && !rc) {
+            set_error(KRK_EHIP, "planner calibration: %s: %s", what, hipGetErrorString(e));
+            rc = KRK_EHIP;
+        }
+        return !rc;
+    };
+    auto timed_ms = [&](const std::function<hipError_t()>& f) {
+        float ms = 0;
+        for (int rep = 0; rep < 2 && !rc; ++rep) {  // the first run loads code and warms up
+            ok(hipEventRecord(e0, s), "event");
+            ok(f(), "launch");
+            ok(hipEventRecord(e1, s), "event");
+            ok(hipEventSynchronize(e1), "sync");
+            ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+        }
+        return (double)std::max(ms, 1e-3f);
+    };
+    if (ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
+        ok(hipEventCreate(&e0), "event") && ok(hipEventCreate(&e1), "event") &&
+        ok(hipMalloc(&d_in, L), "alloc") && ok(hipMalloc(&d_state, 32ull * mmax), "alloc") &&
+        ok(hipMalloc(&d_dig, 32ull * mmax), "alloc") && ok(hipMalloc(&d_jobs, sizeof(ShaJob) * mmax), "alloc") &&
+        ok(hipMemsetAsync(d_in, 0x5a, L, s), "memset")) {
+        std::vector<ShaJob> jobs(mmax);
+        for (uint32_t i = 0; i < mmax; ++i) {
+            jobs[i] = ShaJob{};
+            jobs[i].ptr = reinterpret_cast<uint64_t>(d_in);
+            jobs[i].len = L;
+            jobs[i].out = i;
+            memcpy(jobs[i].h, kIV, 32);
+        }
+        if (ok(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(ShaJob) * mmax, hipMemcpyHostToDevice, s), "upload"))
+            for (int t = 0; t < 3 && !rc; ++t) {
+                const uint32_t m = (uint32_t)(kResidentPerCu[t] * (uint64_t)D->cus);
+                const double ms = timed_ms([&] { return launch_sha256_plan(kTierPlan[t], d_jobs, m, d_dig, d_state, s); });
+                R.stream[t] = (double)L / (ms * 1e-3);
+            }
     }
+    if (!rc && ok(hipMalloc(&d_copy, C), "alloc") && ok(hipHostMalloc(reinterpret_cast<void**>(&h_copy), C, 0), "pin")) {
+        R.h2d = (double)C / (timed_ms([&] { return hipMemcpyAsync(d_copy, h_copy, C, hipMemcpyHostToDevice, s); }) * 1e-3);
+        R.d2h = (double)C / (timed_ms([&] { return hipMemcpyAsync(h_copy, d_copy, C, hipMemcpyDeviceToHost, s); }) * 1e-3);
+    }
+    if (s) hipStreamSynchronize(s);
+    for (void* p : {(void*)d_in, (void*)d_state, (void*)d_dig, (void*)d_jobs, (void*)d_copy})
+        if (p) hipFree(p);
+    if (h_copy) hipHostFree(h_copy);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    if (s) hipStreamDestroy(s);
+    R.host_sha = host_rate();
+    R.host_crc = host_crc_rate();
+    R.source = KRK_RATES_MEASURED;
+    return rc;
+}
+
+std::mutex g_rates_mu;
+bool g_rates_set = false;
+Rates g_rates_override{};
+std::vector<std::pair<int, Rates>> g_rates_measured;  // per device id
+
+// GPU time of m streams (longest `longest` bytes, `bytes` in all) under the AUTO launch
+// plan: the longest chain at the tier's per-stream rate, or the streams' bytes at the
+// tier's aggregate (per-stream rate x streams resident on the chip) when they outnumber
+// what runs at once.
+double gpu_seconds(uint64_t longest, double bytes, uint64_t m, const Rates& R) {
+    if (!m) return 0;
+    const int t = tier_of(m, R.cus);
+    const double r = R.stream[t];
+    const double cap = (double)kResidentPerCu[t] * R.cus * r;
     return std::max(longest / r, bytes / std::min(m * r, cap));
 }
 
@@ -109,7 +200,26 @@ struct OffloadPool {
 // first); empty when the host would not shorten the batch by at least 10 % (device-
 // resident: the host's D2H reads share the PCIe link and the chip's memory with the
 // GPU part) or 3 % (host-resident: the host's blobs simply stay off the link).
-std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
+Rates planner_rates(Device* D) {
+    std::lock_guard<std::mutex> g(g_rates_mu);
+    if (g_rates_set) return g_rates_override;
+    if (!D) return nominal_rates(0);
+    for (auto& [id, R] : g_rates_measured)
+        if (id == D->id) return R;
+    Rates R{};
+    if (calibrate(D, R) != KRK_OK) {  // a failed calibration plans with the nominal rates
+        R = nominal_rates(D->cus);
+    }
+    g_rates_measured.push_back({D->id, R});
+    return R;
+}
+
+// Host-resident batches: the caller's pageable bytes are copied into pinned windows on
+// host threads while the previous window uploads; measured end to end at ~0.85 of the
+// pinned H2D rate (C2 end-to-end 45.7-54.4 GB/s against 54 GB/s pinned).
+double host_link(const Rates& R) { return 0.85 * R.h2d; }
+
+std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode) {
     std::vector<uint32_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
@@ -119,15 +229,15 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
     // GPU side with blobs k.. on the GPU: their longest chain / the chip's SHA rate, and for
     // host-resident batches their bytes over the host link (the host's blobs never cross).
     auto gpu_side = [&](uint64_t k) {
-        double g = k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, cus) : 0.0;
-        if (mode != kOffDevice) g = std::max(g, suffix[k] / kLinkHost);
+        double g = k < n ? gpu_seconds(lens[order[k]], suffix[k], n - k, R) : 0.0;
+        if (mode != kOffDevice) g = std::max(g, suffix[k] / host_link(R));
         return g;
     };
     const double f0 = n ? gpu_side(0) : 0.0;
     double best = f0, best_g = f0, best_h = 0;
     uint64_t best_k = 0;
     if (threads > 0 && n) {
-        const double rs = host_rate(), rc = mode == kOffHostWhole ? host_crc_rate() : 0.0;
+        const double rs = R.host_sha, rc = mode == kOffHostWhole ? R.host_crc : 0.0;
         // LPT over host threads of the tasks, in seconds: a SHA-256 pass per blob, and in
         // kOffHostWhole a piece-CRC pass per blob as its own task.
         std::priority_queue<double, std::vector<double>, std::greater<double>> load;
@@ -145,7 +255,7 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
             put(L / rs);
             if (mode == kOffHostWhole) put(L / rc);
             hbytes += L;
-            const double h = mode == kOffDevice ? std::max(maxload, hbytes / kD2H) : maxload;
+            const double h = mode == kOffDevice ? std::max(maxload, hbytes / R.d2h) : maxload;
             const double g = gpu_side(k);
             if (std::max(g, h) < best) {
                 best = std::max(g, h);
@@ -366,14 +476,54 @@ int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int 
                           uint64_t* n_host, double* gpu_seconds_out, double* host_seconds_out) {
     KRK_CHECK(n == 0 || lengths, KRK_EINVAL, "lengths is NULL");
     KRK_CHECK(n_host, KRK_EINVAL, "n_host is NULL");
-    KRK_CHECK(threads >= 0 && cus > 0, KRK_EINVAL, "threads must be >= 0 and cus > 0");
+    KRK_CHECK(threads >= 0 && cus >= 0, KRK_EINVAL, "threads and cus must be >= 0");
     static_assert(KRK_OFFLOAD_DEVICE == kOffDevice && KRK_OFFLOAD_HOST_SHA == kOffHostSha &&
                       KRK_OFFLOAD_HOST_WHOLE == kOffHostWhole,
                   "offload modes");
     KRK_CHECK(mode >= KRK_OFFLOAD_DEVICE && mode <= KRK_OFFLOAD_HOST_WHOLE, KRK_EINVAL, "offload mode %d", mode);
-    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, cus, gpu_seconds_out, host_seconds_out, mode);
+    int drc = KRK_OK;
+    Device* D = device(&drc);  // none: the override or the nominal rates
+    Rates R = planner_rates(D);
+    if (cus > 0) R.cus = cus;
+    std::vector<uint32_t> idx = offload_plan(lengths, n, threads, R, gpu_seconds_out, host_seconds_out, mode);
     *n_host = idx.size();
     if (host_idx && !idx.empty()) memcpy(host_idx, idx.data(), idx.size() * 4);
+    return KRK_OK;
+}
+
+int krk_planner_rates_get(krk_planner_rates* out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    int drc = KRK_OK;
+    const Rates R = planner_rates(device(&drc));
+    for (int t = 0; t < 3; ++t) out->sha_stream_bps[t] = R.stream[t];
+    out->d2h_bps = R.d2h;
+    out->h2d_bps = R.h2d;
+    out->host_sha_bps = R.host_sha;
+    out->host_crc_bps = R.host_crc;
+    out->cus = R.cus;
+    out->source = R.source;
+    return KRK_OK;
+}
+
+int krk_planner_rates_set(const krk_planner_rates* in) {
+    std::lock_guard<std::mutex> g(g_rates_mu);
+    if (!in) {
+        g_rates_set = false;
+        return KRK_OK;
+    }
+    KRK_CHECK(in->sha_stream_bps[0] > 0 && in->sha_stream_bps[1] > 0 && in->sha_stream_bps[2] > 0 &&
+                  in->d2h_bps > 0 && in->h2d_bps > 0 && in->host_sha_bps > 0 && in->host_crc_bps > 0 && in->cus > 0,
+              KRK_EINVAL, "planner rates must be positive");
+    Rates R{};
+    for (int t = 0; t < 3; ++t) R.stream[t] = in->sha_stream_bps[t];
+    R.d2h = in->d2h_bps;
+    R.h2d = in->h2d_bps;
+    R.host_sha = in->host_sha_bps;
+    R.host_crc = in->host_crc_bps;
+    R.cus = in->cus;
+    R.source = KRK_RATES_SET;
+    g_rates_override = R;
+    g_rates_set = true;
     return KRK_OK;
 }
 

@@ -405,7 +405,7 @@ static std::vector<uint32_t> offload_split(Device* D, const uint64_t* lens, uint
     on_host.assign(n, 0);
     const int T = offload_threads();
     if (T <= 0 || n == 0) return {};
-    std::vector<uint32_t> host = offload_plan(lens, n, T, D->cus, nullptr, nullptr);
+    std::vector<uint32_t> host = offload_plan(lens, n, T, planner_rates(D), nullptr, nullptr);
     for (uint32_t i : host) on_host[i] = 1;
     return host;
 }
@@ -764,7 +764,7 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     // place on host threads and never cross PCIe.
     std::vector<uint32_t> host;
     if (offload_threads() > 0) {
-        host = offload_plan(lengths, n, offload_threads(), D->cus, nullptr, nullptr, kOffHostSha);
+        host = offload_plan(lengths, n, offload_threads(), planner_rates(D), nullptr, nullptr, kOffHostSha);
         for (uint32_t i : host) {
             done[i] = 1;
             --remaining;
@@ -920,7 +920,7 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     if (offload_threads() > 0) {
         std::vector<uint64_t> lens(n);
         for (uint64_t i = 0; i < n; ++i) lens[i] = blobs[i].length;
-        host = offload_plan(lens.data(), n, offload_threads(), D->cus, nullptr, nullptr, kOffHostWhole);
+        host = offload_plan(lens.data(), n, offload_threads(), planner_rates(D), nullptr, nullptr, kOffHostWhole);
         for (uint32_t i : host) on_host[i] = 1;
     }
     const uint64_t n_gpu = n - host.size();

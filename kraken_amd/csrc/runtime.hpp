@@ -571,7 +571,18 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 //    the batch's bytes over the host link shrink by theirs.
 enum OffMode { kOffDevice = 0, kOffHostSha = 1, kOffHostWhole = 2 };
 int offload_threads();
-std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, int cus, double* gpu_s,
+// What the planners know about this box (offload.cpp): per-stream SHA-256 rate of each
+// AUTO tier at full residency (eight / two / one lane(s)), pinned D2H / H2D, one host
+// thread's SHA-256 and CRC-32; measured on the device at first use.
+struct Rates {
+    double stream[3];
+    double d2h, h2d, host_sha, host_crc;
+    int cus;
+    int source;  // KRK_RATES_*
+};
+Rates planner_rates(Device* D);  // D == nullptr: the override or the nominal rates
+double host_link(const Rates& R);
+std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode = kOffDevice);
 void offload_teardown(Device& D);  // krk_shutdown: the offload threads' streams and pinned buffers
 void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,

@@ -1559,7 +1559,12 @@ static hipError_t launch_ws(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_di
 hipError_t launch_sha256(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
                          uint32_t* out_state, hipStream_t s) {
     if (!n_jobs) return hipSuccess;
-    const int plan = resolve_plan(n_jobs);
+    return launch_sha256_plan(resolve_plan(n_jobs), jobs, n_jobs, out_digest, out_state, s);
+}
+
+hipError_t launch_sha256_plan(int plan, const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_digest,
+                              uint32_t* out_state, hipStream_t s) {
+    if (!n_jobs) return hipSuccess;
     t_launch_plan = plan;
     t_launch_units = n_jobs;
     switch (plan) {

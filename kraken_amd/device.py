@@ -6,7 +6,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._capi import check, krk_blob, krk_chunk, krk_launch_rec, krk_nodes, lib
+from ._capi import check, krk_blob, krk_chunk, krk_launch_rec, krk_nodes, krk_planner_rates, lib
 
 ALIGN = 256  # every blob starts 256-byte aligned in the arena
 
@@ -235,9 +235,37 @@ def set_sha_host_offload(threads: int):
 OFFLOAD_DEVICE, OFFLOAD_HOST_SHA, OFFLOAD_HOST_WHOLE = 0, 1, 2
 
 
-def sha_offload_plan(lengths, threads: int, cus: int = 256, mode: int = OFFLOAD_DEVICE):
+RATES_SOURCE = {0: "nominal", 1: "measured", 2: "set"}
+
+
+def planner_rates() -> dict:
+    """krk_planner_rates_get: the rates the planners use on this thread's device
+    (measured there at first use; nominal without a device; or what was set)."""
+    r = krk_planner_rates()
+    check(lib.krk_planner_rates_get(C.byref(r)))
+    return {"sha_stream_bps": list(r.sha_stream_bps), "d2h_bps": r.d2h_bps, "h2d_bps": r.h2d_bps,
+            "host_sha_bps": r.host_sha_bps, "host_crc_bps": r.host_crc_bps, "cus": r.cus,
+            "source": RATES_SOURCE.get(r.source, r.source)}
+
+
+def set_planner_rates(rates: dict | None):
+    """krk_planner_rates_set (None: back to the measured / nominal rates)."""
+    if rates is None:
+        check(lib.krk_planner_rates_set(None))
+        return
+    r = krk_planner_rates()
+    for k, v in enumerate(rates["sha_stream_bps"]):
+        r.sha_stream_bps[k] = v
+    r.d2h_bps, r.h2d_bps = rates["d2h_bps"], rates["h2d_bps"]
+    r.host_sha_bps, r.host_crc_bps = rates["host_sha_bps"], rates["host_crc_bps"]
+    r.cus = rates["cus"]
+    check(lib.krk_planner_rates_set(C.byref(r)))
+
+
+def sha_offload_plan(lengths, threads: int, cus: int = 0, mode: int = OFFLOAD_DEVICE):
     """krk_host_offload_plan: (indices of the blobs the host would take, longest first,
-    modelled GPU seconds, modelled host seconds) -- no device needed.  mode: a batch in
+    modelled GPU seconds, modelled host seconds) -- no device work (planner_rates(); cus
+    > 0 overrides their CU count).  mode: a batch in
     HBM (OFFLOAD_DEVICE), host blobs hashed only (OFFLOAD_HOST_SHA, sha256_host) or hashed
     and piece-summed on the host (OFFLOAD_HOST_WHOLE, metainfo_digest_host)."""
     L = np.ascontiguousarray(lengths, dtype=np.uint64)

@@ -268,15 +268,50 @@ def test_host_offload_plan_modes():
     a batch in HBM (KRK_OFFLOAD_DEVICE) keeps every equal blob on the GPU."""
     from kraken_amd import device as D
     c2 = [100 << 20] * 1000
+    R = D.planner_rates()
+    assert R["source"] == "nominal" and R["cus"] == 256  # no device here
     g0 = D.sha_offload_plan(c2, 0, mode=D.OFFLOAD_HOST_WHOLE)[1]
-    assert abs(g0 - 1000 * (100 << 20) / 45e9) < 1e-6  # link-bound with no offload
+    assert abs(g0 - 1000 * (100 << 20) / (0.85 * R["h2d_bps"])) < 1e-6  # link-bound with no offload
     idx, g, h = D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_HOST_WHOLE)
     assert max(g, h) <= g0
     if idx.size:  # host cores with the SHA extensions: the link sheds the host's blobs
-        assert max(g, h) < 0.97 * g0 and g >= (100 << 20) / 58e6 - 1e-9
+        assert max(g, h) < 0.97 * g0 and g >= (100 << 20) / R["sha_stream_bps"][0] - 1e-9
         assert sorted(idx.tolist()) == list(range(idx.size))  # equal lengths: stable order
     assert D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_DEVICE)[0].size == 0
     idx, g, h = D.sha_offload_plan([1 << 30], 4, mode=D.OFFLOAD_HOST_SHA)  # C1 from host memory
     assert list(idx) == [0] and g == 0.0 and h > 0
     with pytest.raises(Exception):
         D.sha_offload_plan(c2, 4, mode=3)
+
+
+def test_planner_moves_with_injected_rates():
+    """the planner's rates are data (measured on the device at first
+    use, krk_planner_rates_set to inject), not box constants.  Faster GPU streams keep a
+    lone long blob on the GPU; a slower host link makes the host take more blobs of a
+    host-resident C2 batch; more CUs move a 20,000-stream batch to a faster tier."""
+    from kraken_amd import device as D
+    nominal = D.planner_rates()
+    try:
+        fast_gpu = dict(nominal, sha_stream_bps=[4e9, 4e9, 4e9])
+        D.set_planner_rates(fast_gpu)
+        assert D.planner_rates()["source"] == "set"
+        assert D.sha_offload_plan([1 << 30], 16)[0].size == 0  # GPU chain now beats the host thread
+        D.set_planner_rates(dict(nominal, sha_stream_bps=[1e6, 1e6, 1e6]))
+        assert list(D.sha_offload_plan([1 << 30], 16)[0]) == [0]
+        c2 = [100 << 20] * 1000
+        D.set_planner_rates(nominal)
+        n_fast_link = D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_HOST_WHOLE)[0].size
+        D.set_planner_rates(dict(nominal, h2d_bps=nominal["h2d_bps"] / 4))
+        n_slow_link = D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_HOST_WHOLE)[0].size
+        assert n_slow_link > n_fast_link
+        # 20,000 streams: one-lane tier on 256 CUs, two-lane tier on 512 CUs
+        D.set_planner_rates(dict(nominal, sha_stream_bps=[60e6, 50e6, 10e6]))
+        g256 = D.sha_offload_plan([1 << 20] * 20000, 0, cus=256)[1]
+        g512 = D.sha_offload_plan([1 << 20] * 20000, 0, cus=512)[1]
+        assert abs(g256 - 20000 * (1 << 20) / (128 * 256 * 10e6)) < 1e-9 or abs(g256 - (1 << 20) / 10e6) < 1e-9
+        assert abs(g512 - (1 << 20) / 50e6) < 1e-9
+        with pytest.raises(Exception):
+            D.set_planner_rates(dict(nominal, d2h_bps=0.0))
+    finally:
+        D.set_planner_rates(None)
+    assert D.planner_rates()["source"] == "nominal"
