@@ -546,7 +546,12 @@ def run_regen(a, D, T, rank, world, res):
 def run_verify(a, D, T, rank, world, res):
     """krk_verify_pieces_host over received pieces in host memory
     (the h.Sum32() != GetPieceSum(pi) check of writePiece, batched).  Inputs are
-    host-resident by definition of this path, so `value` includes the PCIe pass."""
+    host-resident by definition of this path, so `value` includes the PCIe pass.  The
+    pieces sit in pinned receive buffers (krk_host_alloc, as INTEGRATION.md has the agent
+    allocate them): the library splits the batch between host PCLMUL threads and DMA
+    into the GPU by the measured rates.  `pageable` repeats it from ordinary memory
+    (there the GPU side would cost a host copy per byte, so the split keeps it on the
+    host unless a core copies faster than it CRCs)."""
     import ctypes as C
     from kraken_amd import agentstorage
     n, P = a.blobs or 4096, 4 << 20
@@ -556,7 +561,8 @@ def run_verify(a, D, T, rank, world, res):
     D.piece_sums(arena, out)
     D.synchronize()
     expected = out.sums.to_host(np.uint32, n).copy()
-    host = np.empty(n * P, dtype=np.uint8)
+    pin = D.PinnedArray((n * P,), np.uint8)
+    host = pin.a
     for i in range(n):
         D.check(D.lib.krk_memcpy_d2h(C.c_void_p(host.ctypes.data + i * P), arena.buf.ptr + int(arena.offsets[i]), P))
     del out, arena
@@ -582,20 +588,39 @@ def run_verify(a, D, T, rank, world, res):
         crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
     elapsed = T.max_over_ranks(t1 - t0)
     bytes_rank = n * P
+    rates = D.planner_rates()
     per_launch = bytes_rank * a.steps / max(crc_n, 1)
     crc_avg = crc_ms / max(crc_n, 1)
     roof = roofline_obj("crc32_pieces", per_launch / (crc_avg / 1e3) / 1e9 if crc_n else 0.0, crc_avg, per_launch,
                         None)
-    roof["note"] = ("one CRC launch per pinned staging window; the call is bounded by the host -> device "
-                    "pass (pageable copy into pinned windows + PCIe), not by the kernel")
+    roof["note"] = ("the GPU's share of the pieces goes up by DMA in pinned windows, one CRC launch per window; "
+                    "the call is bounded by the host link and the host threads' PCLMUL rate, not by the kernel")
     res.update({"metric": "agent piece-verify GB/s (host pieces, end to end)",
                 "value": round(world * bytes_rank * a.steps / elapsed / 1e9, 3), "unit": "GB/s", "steps": a.steps,
                 "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-                "dtype": "u8", "data": "synthetic (device-generated splitmix64 pieces, copied to pageable host memory)",
+                "dtype": "u8", "data": "synthetic (device-generated splitmix64 pieces, copied to pinned host memory)",
                 "config": {"workload": WORKLOADS[a.workload]["desc"], "pieces_per_gpu": n, "piece_length": P,
-                           "bytes_per_gpu": bytes_rank, "mode": "host buffers (pageable), PCIe-inclusive"},
+                           "bytes_per_gpu": bytes_rank, "mode": "host buffers (pinned receive buffers), "
+                                                                 "host threads + GPU by measured rates"},
                 "roofline": roof, "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)}},
+                "planner_rates": {k: (round(v / 1e9, 3) if isinstance(v, float) else v) for k, v in rates.items()
+                                  if k != "sha_stream_bps"},
                 "verdicts_match": bool(np.array_equal(got[0], want))})
+    # the same pieces from pageable memory
+    pg = np.empty(n * P, dtype=np.uint8)
+    pg[:] = host
+    pdatas = [pg[i * P:(i + 1) * P] for i in range(n)]
+    pv = agentstorage.verify_pieces(pdatas, exp)
+    T.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        pv = agentstorage.verify_pieces(pdatas, exp)
+    T.barrier()
+    el = T.max_over_ranks(time.perf_counter() - t0)
+    res["pageable"] = {"value": round(world * bytes_rank * a.steps / el / 1e9, 3), "unit": "GB/s",
+                       "verdicts_match": bool(np.array_equal(pv, want)),
+                       "what": "the same batch from pageable host memory (numpy)"}
+    del pg, pdatas
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         # 512 pieces = 2 GiB of distinct bytes: a sample of a few hundred MiB would sit in the
         # host's last-level cache across the repeated passes and overstate the CPU rate

@@ -444,7 +444,7 @@ int krk_set_sha_host_offload(int threads);
  * points, the host/GPU split of the CRC-only host entry points), per device:
  * sha_stream_bps = one SHA-256 stream's rate at full residency under each AUTO tier
  * (eight lanes up to 16 x CUs streams, two lanes up to 64 x CUs, one lane beyond),
- * pinned D2H / H2D copy rates, one host thread's SHA-256 and CRC-32 rates.  Measured on
+ * pinned D2H / H2D copy rates, one host thread's SHA-256, CRC-32 and memcpy rates.  Measured on
  * the calling thread's device at first use (~50 ms: each tier's launch plan timed on
  * 16 / 64 / 128 x CUs streams, a 64 MiB pinned copy each way); without a device the
  * nominal MI355X figures (source 0).  krk_planner_rates_set overrides them process-wide
@@ -455,7 +455,7 @@ int krk_set_sha_host_offload(int threads);
 typedef struct krk_planner_rates {
     double sha_stream_bps[3];
     double d2h_bps, h2d_bps;
-    double host_sha_bps, host_crc_bps;
+    double host_sha_bps, host_crc_bps, host_copy_bps;
     int32_t cus;
     int32_t source;
 } krk_planner_rates;

@@ -46,7 +46,8 @@ class krk_launch_rec(C.Structure):
 
 class krk_planner_rates(C.Structure):
     _fields_ = [("sha_stream_bps", C.c_double * 3), ("d2h_bps", C.c_double), ("h2d_bps", C.c_double),
-                ("host_sha_bps", C.c_double), ("host_crc_bps", C.c_double), ("cus", C.c_int32),
+                ("host_sha_bps", C.c_double), ("host_crc_bps", C.c_double), ("host_copy_bps", C.c_double),
+                ("cus", C.c_int32),
                 ("source", C.c_int32)]
 
 

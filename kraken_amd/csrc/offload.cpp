@@ -14,6 +14,8 @@
 // host blobs get their piece sums on the host too, which takes their bytes off the host
 // link -- C2 end-to-end, link-bound, then hands the host the blobs the link would carry
 // past the GPU's own chain time.
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -53,6 +55,13 @@ double host_rate() {
     });
     return r;
 }
+double host_copy_rate() {
+    static const double r = [] {
+        std::vector<uint8_t> dst(16u << 20);
+        return time_rate([&](const uint8_t* p, size_t n) { memcpy(dst.data(), p, n); });
+    }();
+    return r;
+}
 double host_crc_rate() {
     static const double r = time_rate([](const uint8_t* p, size_t n) {
         volatile uint32_t c = host_crc32_update(0, p, n);
@@ -86,6 +95,7 @@ Rates nominal_rates(int cus) {
     R.d2h = R.h2d = 54e9;
     R.host_sha = host_rate();
     R.host_crc = host_crc_rate();
+    R.host_copy = host_copy_rate();
     R.cus = cus > 0 ? cus : 256;
     R.source = KRK_RATES_NOMINAL;
     return R;
@@ -157,6 +167,7 @@ int calibrate(Device* D, Rates& R) {
     if (s) hipStreamDestroy(s);
     R.host_sha = host_rate();
     R.host_crc = host_crc_rate();
+    R.host_copy = host_copy_rate();
     R.source = KRK_RATES_MEASURED;
     return rc;
 }
@@ -278,6 +289,26 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
 }
 
 int offload_threads() { return g_off_threads.load(std::memory_order_relaxed); }
+
+int host_cpu_budget() {
+    static const int n = [] {
+        int c = 1;
+        cpu_set_t set;
+        c = sched_getaffinity(0, sizeof set, &set) == 0 ? std::max(1, CPU_COUNT(&set))
+                                                        : (int)std::max(1u, std::thread::hardware_concurrency());
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota> <period>" or "max <period>"
+            char q[32] = {0};
+            long long per = 0;
+            if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+                c = std::min<int>(c, std::max<long long>(1, atoll(q) / per));
+            fclose(f);
+        }
+        if (const char* e = getenv("OMP_NUM_THREADS"))
+            if (atoi(e) > 0) c = std::min(c, atoi(e));
+        return c;
+    }();
+    return n;
+}
 
 // Hash blobs (device pointers, lengths) on up to `threads` host threads; digest j to
 // out + 32 j.  The D2H copies start once `ready` (recorded on the caller's stream: the
@@ -500,6 +531,7 @@ int krk_planner_rates_get(krk_planner_rates* out) {
     out->h2d_bps = R.h2d;
     out->host_sha_bps = R.host_sha;
     out->host_crc_bps = R.host_crc;
+    out->host_copy_bps = R.host_copy;
     out->cus = R.cus;
     out->source = R.source;
     return KRK_OK;
@@ -512,7 +544,7 @@ int krk_planner_rates_set(const krk_planner_rates* in) {
         return KRK_OK;
     }
     KRK_CHECK(in->sha_stream_bps[0] > 0 && in->sha_stream_bps[1] > 0 && in->sha_stream_bps[2] > 0 &&
-                  in->d2h_bps > 0 && in->h2d_bps > 0 && in->host_sha_bps > 0 && in->host_crc_bps > 0 && in->cus > 0,
+                  in->d2h_bps > 0 && in->h2d_bps > 0 && in->host_sha_bps > 0 && in->host_crc_bps > 0 && in->host_copy_bps > 0 && in->cus > 0,
               KRK_EINVAL, "planner rates must be positive");
     Rates R{};
     for (int t = 0; t < 3; ++t) R.stream[t] = in->sha_stream_bps[t];
@@ -520,6 +552,7 @@ int krk_planner_rates_set(const krk_planner_rates* in) {
     R.h2d = in->h2d_bps;
     R.host_sha = in->host_sha_bps;
     R.host_crc = in->host_crc_bps;
+    R.host_copy = in->host_copy_bps;
     R.cus = in->cus;
     R.source = KRK_RATES_SET;
     g_rates_override = R;

@@ -72,6 +72,12 @@ struct Window {
 // refilled once its H2D is done; the H2D into its device side waits (on the copy
 // stream only) for the kernels that read the previous contents, so the upload of
 // window k+1 overlaps the kernels of window k.
+struct CopyTask {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+
 struct Pipeline {
     Window w[2];
     ~Pipeline() {
@@ -122,6 +128,24 @@ struct Pipeline {
             }
         hipError_t e = hipMemcpyAsync(x.dev, x.host, n, hipMemcpyHostToDevice, cp);
         if (e == hipSuccess) e = hipEventRecord(x.copied, cp);
+        if (e == hipSuccess) x.copying = true;
+        return e;
+    }
+    // The caller's pinned bytes DMA'd straight into device window k (tasks' dst are
+    // device addresses in it), after the kernels that read its last contents.
+    hipError_t h2d_direct(int k, const std::vector<CopyTask>& tasks, hipStream_t cp) {
+        Window& x = w[k];
+        for (int i = 0; i < 2; ++i)
+            if (x.done_pending[i]) {
+                hipError_t e = hipStreamWaitEvent(cp, x.done[i], 0);
+                if (e != hipSuccess) return e;
+                x.done_pending[i] = false;
+            }
+        for (const auto& t : tasks) {
+            hipError_t e = hipMemcpyAsync(t.dst, t.src, t.n, hipMemcpyHostToDevice, cp);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipEventRecord(x.copied, cp);
         if (e == hipSuccess) x.copying = true;
         return e;
     }
@@ -185,11 +209,6 @@ static int lease_staging(Device* D, size_t cap, StagingLease& L) {
 
 // Host -> pinned staging copies of one window, split over a few threads (one
 // host thread's memcpy is well below the PCIe rate).  KRK_COPY_THREADS overrides.
-struct CopyTask {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-};
 
 static unsigned copy_threads() {
     const char* v = getenv("KRK_COPY_THREADS");
@@ -566,10 +585,12 @@ int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* s
     return r;
 }
 
-int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
-    KRK_DEVICE(D);
-    int r = validate_blobs(blobs, n_blobs);
-    if (r) return r;
+// The GPU pass of krk_piece_sums_host over host blobs: windows of their bytes go up
+// (pageable bytes through the pinned staging windows; `direct`: the caller's bytes are
+// pinned and DMA'd straight into the device window) and the CRC kernel runs on each.
+static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host,
+                               bool direct) {
+    int r = KRK_OK;
     uint64_t lo, hi;
     sums_span(blobs, n_blobs, &lo, &hi);
     if (hi == lo) return KRK_OK;
@@ -598,7 +619,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
             const krk_blob& b = blobs[bi];
             const uint64_t take = std::min<uint64_t>(b.length - boff, W - fill);
             if (take) {
-                copies.push_back({w.host + fill, b.data + boff, take});
+                copies.push_back({(direct ? w.dev : w.host) + fill, b.data + boff, take});
                 B.add(items, reinterpret_cast<uint64_t>(w.dev + fill), boff, boff + take, b.length,
                       (uint64_t)b.piece_length, b.sums_offset);
             }
@@ -608,8 +629,8 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
             fill = (fill + 15) & ~size_t(15);
             if (boff >= b.length) { ++bi; boff = 0; }
         }
-        par_copy(copies);
-        if (pl.h2d(k, std::min(fill, W), cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
+        const hipError_t up = direct ? pl.h2d_direct(k, copies, cp) : (par_copy(copies), pl.h2d(k, std::min(fill, W), cp));
+        if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "piece_sums_host: staging copy failed");
             r = KRK_EHIP;
             break;
@@ -624,6 +645,99 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         set_error(KRK_EHIP, "sums copy-out failed");
         r = KRK_EHIP;
     }
+    return r;
+}
+
+// krk_piece_sums_host / krk_verify_pieces_host: the reference hashes each received
+// piece on the host (lib/torrent/storage/agentstorage/torrent.go:182-193), and one host
+// core's PCLMUL CRC (~12 GB/s) is within a few x of what the host link carries to the
+// GPU, so the batch is split by bytes, whole pieces at a time, between host threads and
+// the GPU pass in proportion to the measured rates (planner_rates):
+//  * pinned caller bytes: the GPU side costs no host CPU (DMA straight into the device
+//    window), so the GPU takes h2d / (h2d + threads x crc) of the bytes;
+//  * pageable bytes: the GPU side needs a host memcpy into pinned staging, so it helps
+//    only if a core copies faster than it CRCs; otherwise everything stays on the host.
+// Host threads = the CPUs this process may use (affinity and cgroup quota).
+struct PieceTask {
+    const uint8_t* p;
+    uint64_t n;
+    uint64_t out;
+};
+
+static bool host_pinned(const void* p, uint64_t n) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) return false;
+    if (n > 1 && (hipPointerGetAttributes(&a, static_cast<const uint8_t*>(p) + n - 1) != hipSuccess ||
+                  a.type != hipMemoryTypeHost))
+        return false;
+    return true;
+}
+
+int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
+    KRK_DEVICE(D);
+    int r = validate_blobs(blobs, n_blobs);
+    if (r) return r;
+    uint64_t lo, hi;
+    sums_span(blobs, n_blobs, &lo, &hi);
+    if (hi == lo) return KRK_OK;
+    KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
+    const Rates R = planner_rates(D);
+    const int T = host_cpu_budget();
+    bool all_pinned = true;
+    double bytes = 0;
+    for (uint64_t i = 0; i < n_blobs; ++i) {
+        bytes += (double)blobs[i].length;
+        if (all_pinned && blobs[i].length && !host_pinned(blobs[i].data, blobs[i].length)) all_pinned = false;
+    }
+    const double c = R.host_crc, H = T * c;
+    double gpu_frac;
+    if (all_pinned) {
+        gpu_frac = R.h2d / (R.h2d + H);
+    } else {
+        const double m = R.host_copy, L = host_link(R);
+        gpu_frac = m > c ? std::min(1.0, (1.0 / c) / (T / L + 1.0 / c - 1.0 / m)) : 0.0;
+    }
+    if (const char* e = getenv("KRK_CRC_GPU_FRACTION")) gpu_frac = std::clamp(atof(e), 0.0, 1.0);
+    // Whole pieces to the GPU until its share of the bytes is reached, the rest to the host.
+    const double quota = gpu_frac * bytes;
+    double gbytes = 0;
+    std::vector<krk_blob> gpu;
+    std::vector<uint64_t> gpu_dst;  // sums_host index of each GPU blob's first sum
+    std::vector<PieceTask> host;
+    uint64_t g_sums = 0;
+    for (uint64_t i = 0; i < n_blobs; ++i) {
+        const krk_blob& b = blobs[i];
+        const uint64_t P = (uint64_t)b.piece_length, np = krk_num_pieces(b.length, b.piece_length);
+        uint64_t q = 0;  // pieces [0, q) of this blob go to the GPU
+        while (q < np && gbytes < quota) {
+            gbytes += (double)std::min(P, b.length - q * P);
+            ++q;
+        }
+        if (q) {
+            gpu.push_back(krk_blob{b.data, std::min(b.length, q * P), b.piece_length, g_sums});
+            gpu_dst.push_back(b.sums_offset);
+            g_sums += q;
+        }
+        for (uint64_t k = q; k < np; ++k) host.push_back({b.data + k * P, std::min(P, b.length - k * P), b.sums_offset + k});
+    }
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t j; (j = next.fetch_add(1)) < host.size();)
+            sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
+    };
+    std::vector<std::thread> pool;
+    const int TH = (int)std::min<size_t>((size_t)T, host.size());
+    for (int t = 0; t < TH; ++t) pool.emplace_back(work);
+    if (!gpu.empty()) {
+        std::vector<uint32_t> gs(g_sums);
+        r = piece_sums_host_gpu(D, gpu.data(), gpu.size(), gs.data(), all_pinned);
+        if (!r)
+            for (size_t j = 0; j < gpu.size(); ++j) {
+                const uint64_t cnt = krk_num_pieces(gpu[j].length, gpu[j].piece_length);
+                memcpy(sums_host + gpu_dst[j], gs.data() + gpu[j].sums_offset, cnt * 4);
+            }
+    }
+    for (auto& t : pool) t.join();
     return r;
 }
 

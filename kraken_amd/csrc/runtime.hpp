@@ -576,11 +576,13 @@ int offload_threads();
 // thread's SHA-256 and CRC-32; measured on the device at first use.
 struct Rates {
     double stream[3];
-    double d2h, h2d, host_sha, host_crc;
+    double d2h, h2d, host_sha, host_crc, host_copy;
     int cus;
     int source;  // KRK_RATES_*
 };
 Rates planner_rates(Device* D);  // D == nullptr: the override or the nominal rates
+int host_cpu_budget();           // CPUs this process may use: affinity, cgroup quota, OMP_NUM_THREADS
+uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);  // host_meta.cpp
 double host_link(const Rates& R);
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode = kOffDevice);

@@ -235,6 +235,28 @@ def set_sha_host_offload(threads: int):
 OFFLOAD_DEVICE, OFFLOAD_HOST_SHA, OFFLOAD_HOST_WHOLE = 0, 1, 2
 
 
+def piece_sums_host(datas, piece_length: int):
+    """krk_piece_sums_host over host buffers (numpy uint8 arrays or bytes): each one's
+    piece sums (calcPieceSums), split between host threads and the GPU by the planner."""
+    arrs = [np.frombuffer(d, dtype=np.uint8) if isinstance(d, (bytes, bytearray)) else d for d in datas]
+    n = len(arrs)
+    blobs = (krk_blob * max(n, 1))()
+    off = 0
+    counts = []
+    for i, a in enumerate(arrs):
+        cnt = int(lib.krk_num_pieces(int(a.size), int(piece_length)))
+        blobs[i] = krk_blob(a.ctypes.data if a.size else None, int(a.size), int(piece_length), off)
+        counts.append(cnt)
+        off += cnt
+    sums = np.zeros(max(off, 1), dtype=np.uint32)
+    check(lib.krk_piece_sums_host(blobs, n, sums.ctypes.data_as(C.POINTER(C.c_uint32))))
+    out, o = [], 0
+    for c in counts:
+        out.append(sums[o:o + c].copy())
+        o += c
+    return out
+
+
 RATES_SOURCE = {0: "nominal", 1: "measured", 2: "set"}
 
 
@@ -244,7 +266,8 @@ def planner_rates() -> dict:
     r = krk_planner_rates()
     check(lib.krk_planner_rates_get(C.byref(r)))
     return {"sha_stream_bps": list(r.sha_stream_bps), "d2h_bps": r.d2h_bps, "h2d_bps": r.h2d_bps,
-            "host_sha_bps": r.host_sha_bps, "host_crc_bps": r.host_crc_bps, "cus": r.cus,
+            "host_sha_bps": r.host_sha_bps, "host_crc_bps": r.host_crc_bps, "host_copy_bps": r.host_copy_bps,
+            "cus": r.cus,
             "source": RATES_SOURCE.get(r.source, r.source)}
 
 
@@ -258,6 +281,7 @@ def set_planner_rates(rates: dict | None):
         r.sha_stream_bps[k] = v
     r.d2h_bps, r.h2d_bps = rates["d2h_bps"], rates["h2d_bps"]
     r.host_sha_bps, r.host_crc_bps = rates["host_sha_bps"], rates["host_crc_bps"]
+    r.host_copy_bps = rates["host_copy_bps"]
     r.cus = rates["cus"]
     check(lib.krk_planner_rates_set(C.byref(r)))
 

@@ -62,3 +62,40 @@ def test_torrent_write_pieces(gpu, tmp_path):
     assert all(e is None for e in t.WritePieces(rest).values())
     assert t.Complete()
     assert open(tmp_path / "download", "rb").read() == blob
+
+
+@pytest.mark.parametrize("frac", ["auto", "0", "0.5", "1"])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_gpu_split_bit_exact(gpu, monkeypatch, frac, pinned):
+    """krk_piece_sums_host / krk_verify_pieces_host split a batch
+    between host PCLMUL threads and the GPU pass (pinned caller bytes: DMA straight into
+    the device window) by the measured rates; every split -- all host, half, all GPU,
+    the planner's own -- gives zlib's sums and the same verdicts, for pieces of ragged
+    lengths in pinned and pageable memory, and multi-piece blobs split mid-blob."""
+    from kraken_amd import device as D
+    if frac != "auto":
+        monkeypatch.setenv("KRK_CRC_GPU_FRACTION", frac)
+    rng = np.random.default_rng(99)
+    lens = [int(x) for x in rng.integers(1, 3 << 20, 200)] + [0, 1, 4 << 20]
+    total = sum(lens)
+    if pinned:
+        buf = D.PinnedArray((total,), np.uint8)
+        arr = buf.a
+    else:
+        arr = np.empty(total, dtype=np.uint8)
+    arr[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    datas = [arr[offs[i]:offs[i + 1]] for i in range(len(lens))]
+    expected = np.array([zlib.crc32(d.tobytes()) for d in datas], dtype=np.uint32)
+    flip = rng.choice(len(lens), 20, replace=False)
+    exp = expected.copy()
+    exp[flip] ^= 0x10
+    want = np.ones(len(lens), dtype=bool)
+    want[flip] = False
+    assert np.array_equal(agentstorage.verify_pieces(datas, exp), want)
+    # multi-piece blobs (64 KiB + 3 B pieces): the split may cut a blob between pieces
+    P = (64 << 10) + 3
+    big = [arr[: 40 * P + 17], arr[5: 5 + 7 * P]]
+    for b, s in zip(big, D.piece_sums_host(big, P)):
+        want_s = [zlib.crc32(b[k:k + P].tobytes()) for k in range(0, b.size, P)]
+        assert [int(x) for x in s] == want_s
