@@ -264,6 +264,7 @@ struct Queue {
     uint8_t* out[kMaxInflight] = {};  // pinned result buffers, grown on demand
     size_t out_cap[kMaxInflight] = {};
     bool out_busy[kMaxInflight] = {};
+    std::vector<uint8_t*> retired;    // grown-out result buffers
     // SHA coalescing: per owner, requests queued and non-final requests in launches on
     // the device; `missing` counts owners with requests on the device but none queued
     // (and no final request formed: a digester that asked for its digest is not
@@ -276,6 +277,7 @@ struct Queue {
     std::unordered_map<const void*, Own> own;
     int64_t missing = 0;
     Clock::time_point due;                        // expected end of the last launch
+    Clock::time_point last_arrival;               // an owner with nothing on the device queued a request
     Clock::time_point last_done;                  // when the previous launch retired
     double ns_per_byte = 1e9 / 59e6;              // per-stream SHA time, EMA of measured launches
 };
@@ -295,8 +297,10 @@ struct Engine {
     std::mutex row_mu;
     std::vector<uint32_t> free_rows;
     uint32_t next_row = 0;
-    uint64_t coalesce_us = 2000;  // idle device: how long the first request waits for company
+    uint64_t coalesce_us = 8000;  // idle device: the longest the first request waits for company
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
+    bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
+    Clock::time_point t0 = Clock::now();
     uint64_t crc_launches = 0;
     std::atomic<uint64_t> sha_batches{0}, sha_jobs{0}, crc_batches{0}, crc_reqs{0};
 };
@@ -314,10 +318,12 @@ void finish(Req* r, int rc, const std::string& err) {
 
 int grow_out(Queue& Q, int i, size_t n) {
     if (Q.out_cap[i] >= n) return KRK_OK;
-    if (Q.out[i]) hipHostFree(Q.out[i]);
+    // freeing pinned memory waits for the whole device: the old buffer is kept until teardown
+    if (Q.out[i]) Q.retired.push_back(Q.out[i]);
     Q.out[i] = nullptr;
     Q.out_cap[i] = 0;
-    const size_t cap = std::max<size_t>(n, 1 << 20);
+    size_t cap = 1 << 20;
+    while (cap < n) cap <<= 1;
     KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&Q.out[i]), cap, hipHostMallocDefault));
     Q.out_cap[i] = cap;
     return KRK_OK;
@@ -492,6 +498,9 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
     t_dev = E->dev;
     for (;;) {
         auto* f = new Inflight();
+        char reason = '-';
+        size_t depth = 0, queued = 0;
+        int64_t missing = 0;
         {
             std::unique_lock<std::mutex> lk(Q->mu);
             Q->cv.wait(lk, [&] { return (Q->stop && Q->q.empty()) || (!Q->q.empty() && Q->inflight.size() < kMaxInflight); });
@@ -508,11 +517,20 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                 // before the last launch is due to end.  (Forming it as soon as SOME owners
                 // are back splits the owners into groups that alternate between launches:
                 // each would then run at a fraction of the per-stream rate.)
+                reason = 'T';
                 for (;;) {
-                    if (Q->stop || expected_present(*Q)) break;  // every owner on the device is back
-                    const auto until = Q->inflight.empty()
-                                           ? Q->q.front()->t_submit + std::chrono::microseconds(E->coalesce_us)
-                                           : Q->due - std::chrono::milliseconds(1);
+                    if (Q->stop || expected_present(*Q)) {  // every owner on the device is back
+                        reason = Q->stop ? 'S' : 'P';
+                        break;
+                    }
+                    // idle device: wait while owners keep arriving (until 1 ms passes with no new
+                    // one, at most coalesce_us after the first request), so that uploads that
+                    // start together also start on the device together
+                    const auto until =
+                        Q->inflight.empty()
+                            ? std::min(Q->q.front()->t_submit + std::chrono::microseconds(E->coalesce_us),
+                                       Q->last_arrival + std::chrono::milliseconds(1))
+                            : Q->due - std::chrono::milliseconds(1);
                     if (Clock::now() >= until) break;
                     Q->cv.wait_until(lk, until);
                     if (Q->q.empty()) break;
@@ -545,6 +563,9 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                     Q->q.pop_front();
                 }
             }
+            depth = Q->inflight.size();
+            queued = Q->q.size();
+            missing = Q->missing;
             for (int i = 0; i < kMaxInflight; ++i)
                 if (!Q->out_busy[i]) {
                     Q->out_busy[i] = true;
@@ -553,6 +574,10 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                 }
         }
         f->t_launch = Clock::now();
+        if (sha && E->trace)
+            fprintf(stderr, "krk_engine sha t=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
+                    std::chrono::duration<double, std::milli>(f->t_launch - E->t0).count(), f->batch.size(), reason,
+                    depth, queued, (long long)missing, Q->ns_per_byte);
         if (!sha && ++E->crc_launches == E->fail_crc_at) {
             set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
                       (unsigned long long)E->crc_launches);
@@ -632,8 +657,9 @@ void completer(Engine* E, Queue* Q, bool sha) {
 
 int engine_start(Engine* E) {
     E->pool.init(env_size("KRK_SLOT_MB", 2) << 20, env_size("KRK_SLOT_POOL_MB", 4096) << 20);
-    E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 2000);
+    E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 8000);
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
+    E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
     KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));
     KRK_HIP(hipStreamCreateWithFlags(&E->s_copy, hipStreamNonBlocking));
@@ -652,9 +678,12 @@ void engine_free_resources(Engine* E) {
     hipSetDevice(E->dev);
     for (hipStream_t s : {E->s_copy, E->sha.s, E->crc.s})
         if (s) hipStreamSynchronize(s), hipStreamDestroy(s);
-    for (Queue* Q : {&E->sha, &E->crc})
+    for (Queue* Q : {&E->sha, &E->crc}) {
         for (auto& p : Q->out)
             if (p) hipHostFree(p), p = nullptr;
+        for (uint8_t* p : Q->retired) hipHostFree(p);
+        Q->retired.clear();
+    }
     if (E->d_state) hipFree(E->d_state);
     if (E->d_digest) hipFree(E->d_digest);
     E->pool.destroy();
@@ -697,7 +726,8 @@ void submit(Queue& Q, Req* r) {
         std::lock_guard<std::mutex> g(Q.mu);
         Q.q.push_back(r);
         if (Q.coalesce)
-            own_update(Q, r->owner, [](Queue::Own& w) {
+            own_update(Q, r->owner, [&](Queue::Own& w) {
+                if (w.queued == 0 && w.flying == 0) Q.last_arrival = r->t_submit;
                 ++w.queued;
                 w.closed = false;
             });

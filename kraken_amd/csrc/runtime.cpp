@@ -271,6 +271,8 @@ static void teardown_device(Device& D) {
         if (P.p) hipHostFree(P.p);
         P = PinnedSlot();
     }
+    for (void* p : D.retired_pinned) hipHostFree(p);
+    D.retired_pinned.clear();
     for (void* p : {(void*)D.shard_kb, (void*)D.shard_koff, (void*)D.shard_bad, (void*)D.d_tabs})
         if (p) hipFree(p);
     for (hipStream_t s : {D.s_main, D.s_a, D.s_b})

@@ -227,6 +227,7 @@ struct Device {
     std::mutex mu;
     PinnedSlot slots[8];
     unsigned next_slot = 0;
+    std::vector<void*> retired_pinned;  // grown-out upload buffers (freed at krk_shutdown)
 };
 
 template <class T>
@@ -257,8 +258,17 @@ inline int init_device(Device& D, int id) {
               "device %d is %s, this build targets gfx950 (MI355X)", id, prop.gcnArchName);
     D.cus = prop.multiProcessorCount;
     KRK_HIP(hipStreamCreateWithFlags(&D.s_main, hipStreamNonBlocking));
-    KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
-    KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
+    {
+        // KRK_STREAM_MODE (experiment): 0 plain streams; 1 s_a and s_b with a CU mask of
+        // every CU (a dedicated hardware queue each); 2 only s_b (the CRC side).
+        const char* m = getenv("KRK_STREAM_MODE");
+        const int mode = m ? atoi(m) : 0;
+        std::vector<uint32_t> all((D.cus + 31) / 32, 0xFFFFFFFFu);
+        if (mode == 1) KRK_HIP(hipExtStreamCreateWithCUMask(&D.s_a, (uint32_t)all.size(), all.data()));
+        else KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
+        if (mode == 1 || mode == 2) KRK_HIP(hipExtStreamCreateWithCUMask(&D.s_b, (uint32_t)all.size(), all.data()));
+        else KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
+    }
     std::vector<uint32_t> tabs(kTabWords);
     make_slice_tables(tabs.data() + kTabT);
     const X8Pow& xp = x8();
@@ -338,10 +348,14 @@ inline int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_
     }
     if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
     if (P.cap < n) {
-        if (P.p) hipHostFree(P.p);
+        // hipHostFree waits for the whole device (a kernel of another stream included), so
+        // a grown slot's old buffer is kept until krk_shutdown: freeing it here held the C3
+        // windows' CRC launch back until the window's SHA-256 kernel had ended.
+        if (P.p) D->retired_pinned.push_back(P.p);
         P.p = nullptr;  // a failed grow leaves an empty slot, not a dangling one
         P.cap = 0;
-        const size_t cap = std::max<size_t>(n, 1 << 20);
+        size_t cap = 1 << 20;
+        while (cap < n) cap <<= 1;
         KRK_HIP(hipHostMalloc(&P.p, cap, hipHostMallocDefault));
         P.cap = cap;
     }

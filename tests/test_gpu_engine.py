@@ -113,23 +113,32 @@ def test_256_concurrent_gpu_digesters(gpu):
         lib.krk_digester_free(h)
     b0 = _stats()
 
+    import threading
+    bar = [threading.Barrier(n + 1)]
+
     def work(i):
         r = np.random.default_rng(i)
         d = core.Digester(KRK_PLACE_GPU)
         m, pos = datas[i], 0
+        bar[0].wait()  # 256 uploads in progress at once: they start together
         while pos < L:
             k = min(L - pos, int(r.integers(1, 1 << 20)))
             d._write(m[pos:pos + k])
             pos += k
         return d.Digest().Hex()
 
-    with ThreadPoolExecutor(n) as ex:  # first round grows the pinned slot pool (one-time pinning)
-        assert list(ex.map(work, range(n))) == want
+    def run():
+        bar[0] = threading.Barrier(n + 1)
+        with ThreadPoolExecutor(n) as ex:
+            futs = [ex.submit(work, i) for i in range(n)]
+            bar[0].wait()  # the timed region starts when every thread holds its digester
+            t0 = time.perf_counter()
+            got = [f.result() for f in futs]
+            return got, time.perf_counter() - t0
+
+    assert run()[0] == want  # first round grows the pinned slot pool (one-time pinning)
     b0 = _stats()
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(n) as ex:
-        got = list(ex.map(work, range(n)))
-    el = time.perf_counter() - t0
+    got, el = run()
     b1 = _stats()
     assert got == want
     agg = n * L / el

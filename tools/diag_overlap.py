@@ -23,6 +23,14 @@ def show(tag, k):
         print(f"{tag} {k:13s} #{i} plan={plan} units={units} start={a:9.3f} end={b:9.3f} dur={b - a:8.3f}")
 
 
+def overlap_count():
+    """Windows whose CRC launch ended before their SHA launch did (ran beside it)."""
+    sha = D.KernelTimer.timeline("sha256_multi")
+    crc = D.KernelTimer.timeline("crc32_pieces")
+    inside = sum(1 for s, c in zip(sha, crc) if c[3] <= s[3])
+    return inside, min(len(sha), len(crc))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--extra-streams", type=int, default=0)
@@ -45,6 +53,8 @@ def main():
         wr.run()
         for k in ("sha256_multi", "crc32_pieces", "synth_fill"):
             show("c3", k)
+        print("c3 CRC inside SHA: %d of %d windows (KRK_STREAM_MODE=%s)" % (*overlap_count(),
+                                                                          os.environ.get("KRK_STREAM_MODE", "0")))
     wr.close()
     n = 1000
     arena = D.BlobArena([16 << 20] * n, 4 << 20, blob_ids=range(n))
