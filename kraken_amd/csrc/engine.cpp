@@ -114,6 +114,23 @@ class SlotPool {
         }
     }
 
+    // A slot for an owner to fill in place between calls, only while more than `reserve`
+    // slots stay free or growable: the reserve is left to submissions (which block), so
+    // slots held by idle owners can never starve the requests that release slots.
+    Slot* try_acquire(size_t reserve) {
+        std::lock_guard<std::mutex> g(mu_);
+        const size_t growable = cap_ > allocated_ ? (cap_ - allocated_) / S : 0;
+        if (free_.size() + growable <= reserve) return nullptr;
+        if (free_.empty() && grow() != KRK_OK) return nullptr;
+        Slot* s = free_.back();
+        free_.pop_back();
+        return s;
+    }
+    size_t reserve() {
+        std::lock_guard<std::mutex> g(mu_);
+        return std::max<size_t>(kPerChunk, cap_ / S / 4);
+    }
+
     void release(Slot* s) {
         if (!s) return;
         {
@@ -233,7 +250,7 @@ struct Req {
 };
 
 constexpr int kMaxInflight = 3;           // launches per queue on the device at once
-constexpr size_t kOwnerInflight = 4;      // requests per digester / piece stream in flight
+size_t g_owner_inflight = 4;  // requests per digester / piece stream in flight (KRK_OWNER_INFLIGHT)
 constexpr uint32_t kStateRows = 65536;    // GPU digesters per device (state + digest rows)
 constexpr uint64_t kMaxCrcBatchBytes = 4ull << 30;
 
@@ -296,13 +313,19 @@ struct Engine {
     uint8_t* d_digest = nullptr;  // kStateRows x 32 B
     std::mutex row_mu;
     std::vector<uint32_t> free_rows;
+    // Host buffers (pool.S bytes, pageable) that digesters and piece streams fill between
+    // submissions, recycled so that a new owner's first bytes do not page-fault a fresh
+    // 2 MiB allocation (256 new uploads: half a GiB of first-touch faults).
+    std::mutex pend_mu;
+    std::vector<std::unique_ptr<uint8_t[]>> pend_free;
     uint32_t next_row = 0;
-    uint64_t coalesce_us = 8000;  // idle device: the longest the first request waits for company
+    uint64_t coalesce_us = 30000;  // idle device: the longest the first request waits for company
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
     bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
     Clock::time_point t0 = Clock::now();
     uint64_t crc_launches = 0;
     std::atomic<uint64_t> sha_batches{0}, sha_jobs{0}, crc_batches{0}, crc_reqs{0};
+    std::atomic<int64_t> live_digesters{0};  // GPU digesters placed on this engine
 };
 
 namespace {
@@ -490,8 +513,13 @@ void own_update(Queue& Q, const void* o, F&& f) {
     if (w.queued == 0 && w.flying == 0) Q.own.erase(o);
 }
 
-// Every owner with requests on the device has its next request queued.
-bool expected_present(const Queue& Q) { return !Q.inflight.empty() && Q.missing == 0 && !Q.q.empty(); }
+// Every owner with requests on the device has its next request queued; on an idle
+// device, every live GPU digester of the engine has one queued.
+bool expected_present(const Queue& Q, int64_t live) {
+    if (Q.q.empty()) return false;
+    if (Q.inflight.empty()) return live > 0 && (int64_t)Q.own.size() >= live;
+    return Q.missing == 0;
+}
 
 void dispatcher(Engine* E, Queue* Q, bool sha) {
     hipSetDevice(E->dev);
@@ -519,17 +547,18 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                 // each would then run at a fraction of the per-stream rate.)
                 reason = 'T';
                 for (;;) {
-                    if (Q->stop || expected_present(*Q)) {  // every owner on the device is back
+                    if (Q->stop || expected_present(*Q, E->live_digesters.load(std::memory_order_relaxed))) {  // every owner on the device is back
                         reason = Q->stop ? 'S' : 'P';
                         break;
                     }
-                    // idle device: wait while owners keep arriving (until 1 ms passes with no new
-                    // one, at most coalesce_us after the first request), so that uploads that
-                    // start together also start on the device together
+                    // idle device: wait until every live GPU digester has a request queued, or
+                    // 3 ms pass with no new owner, at most coalesce_us after the first request,
+                    // so that uploads that start together also start on the device together
+                    // (a digester that misses the first launch runs a whole launch behind)
                     const auto until =
                         Q->inflight.empty()
                             ? std::min(Q->q.front()->t_submit + std::chrono::microseconds(E->coalesce_us),
-                                       Q->last_arrival + std::chrono::milliseconds(1))
+                                       Q->last_arrival + std::chrono::milliseconds(3))
                             : Q->due - std::chrono::milliseconds(1);
                     if (Clock::now() >= until) break;
                     Q->cv.wait_until(lk, until);
@@ -656,8 +685,10 @@ void completer(Engine* E, Queue* Q, bool sha) {
 }
 
 int engine_start(Engine* E) {
-    E->pool.init(env_size("KRK_SLOT_MB", 2) << 20, env_size("KRK_SLOT_POOL_MB", 4096) << 20);
-    E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 8000);
+    const size_t slot = getenv("KRK_SLOT_KB") ? (env_size("KRK_SLOT_KB", 2048) << 10) : (env_size("KRK_SLOT_MB", 2) << 20);
+    E->pool.init((slot + 63) & ~size_t(63), env_size("KRK_SLOT_POOL_MB", 4096) << 20);
+    g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 4));
+    E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 30000);
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
     E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
@@ -802,6 +833,24 @@ void row_release(Engine* E, uint32_t row) {
     E->free_rows.push_back(row);
 }
 
+std::unique_ptr<uint8_t[]> pend_acquire(Engine* E) {
+    {
+        std::lock_guard<std::mutex> g(E->pend_mu);
+        if (!E->pend_free.empty()) {
+            auto b = std::move(E->pend_free.back());
+            E->pend_free.pop_back();
+            return b;
+        }
+    }
+    return std::unique_ptr<uint8_t[]>(new uint8_t[E->pool.S]);
+}
+
+void pend_release(Engine* E, std::unique_ptr<uint8_t[]> b) {
+    if (!b) return;
+    std::lock_guard<std::mutex> g(E->pend_mu);
+    if (E->pend_free.size() < 4096) E->pend_free.push_back(std::move(b));
+}
+
 // ------------------------------------------------------------------ placement
 std::atomic<int64_t> g_live_digesters{0};
 std::atomic<int64_t> g_host_streams{-1};  // -1: default (host threads x per-stream rate ratio)
@@ -845,7 +894,8 @@ struct krk_digester {
     // GPU placement: the engine state row, bytes not yet submitted (pend[0, fill)),
     // bytes handed to the engine, requests in flight (submission order)
     uint32_t row = 0;
-    std::unique_ptr<uint8_t[]> pend;
+    Slot* cur = nullptr;               // pending bytes filled in place in a staging slot, or
+    std::unique_ptr<uint8_t[]> pend;   // in a host buffer when the pool is near its cap
     size_t fill = 0;
     uint64_t submitted = 0;
     std::deque<Req*> inflight;
@@ -874,12 +924,29 @@ int digester_drain(krk_digester* d, size_t keep) {
     return d->err;
 }
 
-int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool final) {
-    int rc = digester_drain(d, kOwnerInflight - 1);
-    if (rc) return rc;
+// Submit `len` bytes: from the slot `sl` the digester filled in place (handed over to the
+// request), else copied from `src` into a fresh slot.
+int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool final, Slot* sl = nullptr) {
+    int rc = digester_drain(d, g_owner_inflight - 1);
+    if (rc) {
+        d->E->pool.release(sl);
+        return rc;
+    }
     Req* r = nullptr;
-    rc = make_req(d->E, src, len, &r);
-    if (rc) return rc;
+    if (sl) {
+        r = new Req();
+        r->slot = sl;
+        r->len = len;
+        rc = stage(d->E, r);
+        if (rc) {
+            d->E->pool.release(sl);
+            delete r;
+            return rc;
+        }
+    } else {
+        rc = make_req(d->E, src, len, &r);
+        if (rc) return rc;
+    }
     r->owner = d;
     r->w = &d->w;
     r->row = d->row;
@@ -910,6 +977,7 @@ int krk_digester_new_on(int placement, krk_digester** out) {
         int rc = KRK_OK;
         d->E = engine_of(place_device(), &rc);
         if (d->E) d->row = row_acquire(d->E, &rc);
+        if (d->E && !rc) d->E->live_digesters.fetch_add(1);
         if (rc) {
             delete d;
             g_live_digesters.fetch_sub(1);
@@ -954,7 +1022,8 @@ int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
         t_err = d->err_msg;
         return d->err;
     }
-    const size_t S = d->E->pool.S;
+    Engine* E = d->E;
+    const size_t S = E->pool.S;
     while (n) {
         if (d->fill == 0 && n >= S) {  // a whole slot straight from the caller's buffer
             const int rc = digester_submit(d, buf, S, false);
@@ -963,14 +1032,23 @@ int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
             n -= S;
             continue;
         }
-        if (!d->pend) d->pend.reset(new uint8_t[S]);
+        if (d->fill == 0 && !d->cur) d->cur = E->pool.try_acquire(E->pool.reserve());
+        uint8_t* dst;
+        if (d->cur) {
+            dst = d->cur->host;
+        } else {
+            if (!d->pend) d->pend = pend_acquire(E);
+            dst = d->pend.get();
+        }
         const size_t take = std::min<uint64_t>(n, S - d->fill);
-        memcpy(d->pend.get() + d->fill, buf, take);
+        memcpy(dst + d->fill, buf, take);
         d->fill += take;
         buf += take;
         n -= take;
         if (d->fill == S) {
-            const int rc = digester_submit(d, d->pend.get(), S, false);
+            Slot* sl = d->cur;
+            d->cur = nullptr;
+            const int rc = digester_submit(d, dst, S, false, sl);
             if (rc) return rc;
             d->fill = 0;
         }
@@ -988,8 +1066,16 @@ int krk_digester_sum(krk_digester* d, uint8_t out32[32]) {
         t_err = d->err_msg;
         return d->err;
     }
-    // the pending bytes stay pending (Digest() does not reset: writing may continue)
-    int rc = digester_submit(d, d->pend.get(), d->fill, true);
+    // the pending bytes stay pending (Digest() does not reset: writing may continue): a
+    // slot filled in place goes with the final request and its bytes move to the host
+    // buffer
+    Slot* sl = d->cur;
+    if (sl) {
+        if (!d->pend) d->pend = pend_acquire(d->E);
+        memcpy(d->pend.get(), sl->host, d->fill);
+        d->cur = nullptr;
+    }
+    int rc = digester_submit(d, d->pend.get(), d->fill, true, sl);
     if (!rc) rc = digester_drain(d, 0);
     if (!rc) memcpy(out32, d->last_digest, 32);
     return rc;
@@ -999,7 +1085,10 @@ void krk_digester_free(krk_digester* d) {
     if (!d) return;
     if (d->E) {
         digester_drain(d, 0);
+        d->E->pool.release(d->cur);
         row_release(d->E, d->row);
+        pend_release(d->E, std::move(d->pend));
+        d->E->live_digesters.fetch_sub(1);
     }
     g_live_digesters.fetch_sub(1);
     delete d;
@@ -1082,7 +1171,7 @@ int stream_drain(krk_piece_stream* s, size_t keep) {
 
 int stream_submit(krk_piece_stream* s, const uint8_t* src, uint64_t len) {
     if (!len) return KRK_OK;
-    int rc = stream_drain(s, kOwnerInflight - 1);
+    int rc = stream_drain(s, g_owner_inflight - 1);
     if (rc) return rc;
     Req* r = nullptr;
     rc = make_req(s->E, src, len, &r);
@@ -1135,7 +1224,7 @@ int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n)
             n -= S;
             continue;
         }
-        if (!s->pend) s->pend.reset(new uint8_t[S]);
+        if (!s->pend) s->pend = pend_acquire(s->E);
         const size_t take = std::min<uint64_t>(n, S - s->fill);
         memcpy(s->pend.get() + s->fill, buf, take);
         s->fill += take;
@@ -1175,6 +1264,7 @@ int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, 
 void krk_piece_stream_free(krk_piece_stream* s) {
     if (!s) return;
     stream_drain(s, 0);
+    pend_release(s->E, std::move(s->pend));
     delete s;
 }
 
@@ -1203,7 +1293,7 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
         delete r;
     };
     for (uint64_t off = 0; off < n && !rc; off += S) {
-        if (reqs.size() >= kOwnerInflight) {  // bounded: the slots recycle
+        if (reqs.size() >= g_owner_inflight) {  // bounded: the slots recycle
             retire(reqs.front());
             reqs.pop_front();
             if (rc) break;

@@ -1,0 +1,105 @@
+// digesters.cpp -- N concurrent GPU Digesters driven from native threads, the way the
+// reference's goroutines drive core.Digester (origin/blobserver/uploader.go:75,
+// lib/store/ca_store.go:119): each thread owns one digester, writes its blob in
+// random-sized chunks (io.Copy-like), then asks for the digest.  Links the product
+// library through its C ABI only (include/kraken_hip.h), as a cgo caller would.
+//
+//   digesters <n_threads> <MiB per digester> <rounds> [max write bytes]
+//
+// Prints one JSON line per round: aggregate GB/s (timed from the moment every thread
+// holds its digester until the last digest), streams per SHA launch, and whether every
+// digest equals krk_host_sha256 of the same bytes (the host SHA-NI path, itself checked
+// against hashlib by tests/test_capi_cpu.py).  Exit 1 on any mismatch or error.
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "../../include/kraken_hip.h"
+
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 256;
+    const size_t L = (size_t)(argc > 2 ? atoi(argv[2]) : 16) << 20;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 2;
+    const size_t maxw = argc > 4 ? strtoull(argv[4], nullptr, 10) : (1u << 20);
+    if (n < 1 || L == 0 || maxw == 0) return 2;
+    if (krk_set_device(0) != KRK_OK) {
+        fprintf(stderr, "no device: %s\n", krk_last_error());
+        return 1;
+    }
+    // blob i = bytes [i * 4096, i * 4096 + L) of one random buffer
+    std::vector<uint8_t> base(L + (size_t)n * 4096);
+    std::mt19937_64 g(256);
+    for (size_t k = 0; k + 8 <= base.size(); k += 8) {
+        const uint64_t v = g();
+        memcpy(&base[k], &v, 8);
+    }
+    std::vector<std::array<uint8_t, 32>> want(n);
+    {
+        std::vector<std::thread> th;
+        std::atomic<int> next{0};
+        for (int t = 0; t < 16; ++t)
+            th.emplace_back([&] {
+                for (int i; (i = next.fetch_add(1)) < n;) krk_host_sha256(base.data() + (size_t)i * 4096, L, want[i].data());
+            });
+        for (auto& t : th) t.join();
+    }
+    bool all_ok = true;
+    for (int r = 0; r < rounds; ++r) {
+        uint64_t b0[5], b1[5];
+        krk_engine_stats(&b0[0], &b0[1], &b0[2], &b0[3], &b0[4]);
+        // start line: every thread holds its digester, then all are released at once
+        // (an atomic flag, not a condition variable: waking 256 waiters one mutex handoff
+        // at a time took ~15 ms, which the timed region would have charged to the engine)
+        std::atomic<int> ready{0};
+        std::atomic<bool> go{false};
+        std::atomic<int> bad{0};
+        std::vector<std::thread> th;
+        for (int i = 0; i < n; ++i)
+            th.emplace_back([&, i] {
+                krk_set_device(0);
+                krk_digester* d = nullptr;
+                if (krk_digester_new_on(KRK_PLACE_GPU, &d) != KRK_OK) {
+                    bad.fetch_add(1);
+                    return;
+                }
+                std::mt19937_64 rg(i * 7919 + r);
+                ready.fetch_add(1);
+                while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+                const uint8_t* p = base.data() + (size_t)i * 4096;
+                for (size_t pos = 0; pos < L;) {
+                    const size_t k = std::min<size_t>(L - pos, 1 + rg() % maxw);
+                    if (krk_digester_write(d, p + pos, k) != KRK_OK) {
+                        bad.fetch_add(1);
+                        break;
+                    }
+                    pos += k;
+                }
+                uint8_t out[32];
+                if (krk_digester_sum(d, out) != KRK_OK || memcmp(out, want[i].data(), 32) != 0) bad.fetch_add(1);
+                krk_digester_free(d);
+            });
+        while (ready.load() < n) std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        go.store(true, std::memory_order_release);
+        for (auto& t : th) t.join();
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        krk_engine_stats(&b1[0], &b1[1], &b1[2], &b1[3], &b1[4]);
+        const double agg = (double)n * L / el;
+        const bool ok = bad.load() == 0;
+        all_ok = all_ok && ok;
+        printf("{\"round\": %d, \"digesters\": %d, \"bytes_each\": %zu, \"seconds\": %.4f, \"GBps\": %.3f, "
+               "\"MBps_per_stream\": %.2f, \"sha_launches\": %llu, \"streams_per_launch\": %.1f, "
+               "\"pinned_bytes\": %llu, \"digests_match\": %s}\n",
+               r, n, L, el, agg / 1e9, agg / n / 1e6, (unsigned long long)(b1[0] - b0[0]),
+               (double)(b1[1] - b0[1]) / (double)std::max<uint64_t>(1, b1[0] - b0[0]),
+               (unsigned long long)b1[4], ok ? "true" : "false");
+        fflush(stdout);
+    }
+    return all_ok ? 0 : 1;
+}
