@@ -148,13 +148,14 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *
  * Placement, fixed at creation:
  *   KRK_PLACE_GPU   bytes go through the device's submission engine: the caller copies
- *                   them into pooled pinned slots (2 MiB, KRK_SLOT_MB) and every
+ *                   them into pooled pinned slots (512 KiB, KRK_SLOT_KB) and every
  *                   pending slot of every GPU digester of the device is digested in
  *                   ONE multi-stream sha256_multi launch (a dispatcher thread batches
  *                   them).  A digester's midstate lives in an HBM row of the engine,
  *                   so its requests chain through the device in stream order and the
- *                   next launch is queued behind the running one (up to 4 requests
- *                   of a digester in flight).  Creation allocates nothing on the device.
+ *                   next launch is queued behind the running one (up to 8 requests
+ *                   of a digester in flight; the kernel reads the pinned slots in
+ *                   place).  Creation allocates nothing on the device.
  *   KRK_PLACE_HOST  SHA-NI on the caller's thread (host_meta.cpp): ~2 GB/s per stream
  *                   against ~59 MB/s for one GPU stream.
  *   KRK_PLACE_AUTO  (krk_digester_new) HOST while at most N digesters are live in the

@@ -69,8 +69,9 @@ size_t env_size(const char* k, size_t dflt) {
 
 // ------------------------------------------------------------------ slots
 struct Slot {
-    uint8_t* host = nullptr;  // pinned
-    uint8_t* dev = nullptr;   // device mirror
+    uint8_t* host = nullptr;      // pinned, mapped into the device's address space
+    const uint8_t* mapped = nullptr;  // `host` as the device addresses it (zero-copy reads)
+    uint8_t* dev = nullptr;       // device mirror (CRC requests are copied here)
     hipEvent_t h2d = nullptr;  // the last H2D of this slot
 };
 
@@ -194,10 +195,13 @@ class SlotPool {
                 return KRK_EHIP;
             }
         }
-        void *h = nullptr, *d = nullptr;
-        if (hipHostMalloc(&h, bytes, hipHostMallocDefault) != hipSuccess) h = nullptr;
-        if (h && hipMalloc(&d, bytes) != hipSuccess) d = nullptr;
-        if (!h || !d) {
+        void *h = nullptr, *d = nullptr, *hm = nullptr;
+        // coherent: the SHA-256 kernel reads a slot straight over PCIe (no H2D copy), and a
+        // reused slot must never be served from a stale GPU cache line
+        if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) h = nullptr;
+        if (h && hipHostGetDevicePointer(&hm, h, 0) != hipSuccess) hm = nullptr;
+        if (h && hm && hipMalloc(&d, bytes) != hipSuccess) d = nullptr;
+        if (!h || !hm || !d) {
             if (h) hipHostFree(h);
             for (auto& e : ev) hipEventDestroy(e);
             set_error(KRK_ENOMEM, "engine: %s staging slots (%zu bytes)", h ? "device" : "pinned host", bytes);
@@ -206,6 +210,7 @@ class SlotPool {
         std::unique_ptr<Slot[]> c(new Slot[kPerChunk]);
         for (int i = 0; i < kPerChunk; ++i) {
             c[i].host = static_cast<uint8_t*>(h) + i * S;
+            c[i].mapped = static_cast<const uint8_t*>(hm) + i * S;
             c[i].dev = static_cast<uint8_t*>(d) + i * S;
             c[i].h2d = ev[i];
             free_.push_back(&c[i]);
@@ -250,7 +255,11 @@ struct Req {
 };
 
 constexpr int kMaxInflight = 3;           // launches per queue on the device at once
-size_t g_owner_inflight = 4;  // requests per digester / piece stream in flight (KRK_OWNER_INFLIGHT)
+// Requests per digester / piece stream in flight (KRK_OWNER_INFLIGHT).  With 512 KiB
+// slots a launch of 256 streams is ~9 ms, so 8 in flight keep ~70 ms of each owner's
+// bytes ahead of the device: an owner whose writer thread was descheduled for a while
+// still makes the next launch.
+size_t g_owner_inflight = 8;
 constexpr uint32_t kStateRows = 65536;    // GPU digesters per device (state + digest rows)
 constexpr uint64_t kMaxCrcBatchBytes = 4ull << 30;
 
@@ -320,8 +329,10 @@ struct Engine {
     std::vector<std::unique_ptr<uint8_t[]>> pend_free;
     uint32_t next_row = 0;
     uint64_t coalesce_us = 30000;  // idle device: the longest the first request waits for company
+    uint64_t quiet_us = 3000;      // ... or this long with no new owner (KRK_SHA_QUIET_US)
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
     bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
+    bool sha_zero_copy = true;    // SHA jobs read the pinned slots directly (KRK_SHA_ZERO_COPY=0: H2D first)
     Clock::time_point t0 = Clock::now();
     uint64_t crc_launches = 0;
     std::atomic<uint64_t> sha_batches{0}, sha_jobs{0}, crc_batches{0}, crc_reqs{0};
@@ -374,7 +385,10 @@ int launch_sha(Engine* E, Inflight* f) {
         Req* r = f->batch[i];
         ShaJob& j = jobs[i];
         j = ShaJob{};
-        j.ptr = reinterpret_cast<uint64_t>(r->slot ? r->slot->dev : reinterpret_cast<uint8_t*>(E->d_state));
+        // zero-copy: the producer waves load the pinned slot over PCIe (59 MB/s a stream is
+        // far below the link; its loads run two steps ahead of the rounds)
+        j.ptr = reinterpret_cast<uint64_t>(r->slot ? (E->sha_zero_copy ? r->slot->mapped : r->slot->dev)
+                                                   : reinterpret_cast<const uint8_t*>(E->d_state));
         j.len = r->len;
         j.prefix = r->prefix;
         j.out = r->row;
@@ -383,7 +397,7 @@ int launch_sha(Engine* E, Inflight* f) {
         f->max_len = std::max<uint64_t>(f->max_len, r->len);
         if (r->final) lo = std::min(lo, r->row), hi = std::max(hi, r->row);
     }
-    int rc = wait_staged(Q, f->batch);
+    int rc = E->sha_zero_copy ? KRK_OK : wait_staged(Q, f->batch);
     if (!rc) rc = run_jobs(D, jobs, E->d_digest, E->d_state, Q.s);
     if (!rc && lo <= hi) {
         f->row0 = lo;
@@ -558,7 +572,7 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                     const auto until =
                         Q->inflight.empty()
                             ? std::min(Q->q.front()->t_submit + std::chrono::microseconds(E->coalesce_us),
-                                       Q->last_arrival + std::chrono::milliseconds(3))
+                                       Q->last_arrival + std::chrono::microseconds(E->quiet_us))
                             : Q->due - std::chrono::milliseconds(1);
                     if (Clock::now() >= until) break;
                     Q->cv.wait_until(lk, until);
@@ -685,12 +699,19 @@ void completer(Engine* E, Queue* Q, bool sha) {
 }
 
 int engine_start(Engine* E) {
-    const size_t slot = getenv("KRK_SLOT_KB") ? (env_size("KRK_SLOT_KB", 2048) << 10) : (env_size("KRK_SLOT_MB", 2) << 20);
+    // 512 KiB slots (KRK_SLOT_KB / KRK_SLOT_MB): a digester that misses a launch falls one
+    // launch behind for good, so the launch should be short; 256 concurrent digesters from
+    // native threads, same box, interleaved (tests/native/digesters.cpp): 2 MiB slots with 4
+    // in flight 8.8-12.6 GB/s, 512 KiB with 8 in flight 11.1-14.2 GB/s (zero-copy).
+    const size_t slot = getenv("KRK_SLOT_KB") ? (env_size("KRK_SLOT_KB", 512) << 10)
+                                              : getenv("KRK_SLOT_MB") ? (env_size("KRK_SLOT_MB", 2) << 20) : (512u << 10);
     E->pool.init((slot + 63) & ~size_t(63), env_size("KRK_SLOT_POOL_MB", 4096) << 20);
-    g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 4));
+    g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 8));
     E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 30000);
+    E->quiet_us = env_size("KRK_SHA_QUIET_US", 3000);
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
     E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
+    if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->sha_zero_copy = atoi(z) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
     KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));
     KRK_HIP(hipStreamCreateWithFlags(&E->s_copy, hipStreamNonBlocking));
@@ -766,8 +787,9 @@ void submit(Queue& Q, Req* r) {
     Q.cv.notify_all();
 }
 
-// A request over `len` bytes of `src` (copied into a fresh slot on this thread).
-int make_req(Engine* E, const uint8_t* src, uint64_t len, Req** out) {
+// A request over `len` bytes of `src` (copied into a fresh slot on this thread; its H2D
+// issued unless the kernel reads the slot in place).
+int make_req(Engine* E, const uint8_t* src, uint64_t len, Req** out, bool h2d = true) {
     *out = nullptr;
     Slot* sl = nullptr;
     if (len) {
@@ -779,7 +801,7 @@ int make_req(Engine* E, const uint8_t* src, uint64_t len, Req** out) {
     auto* r = new Req();
     r->slot = sl;
     r->len = len;
-    const int rc = stage(E, r);
+    const int rc = h2d ? stage(E, r) : KRK_OK;
     if (rc) {
         E->pool.release(sl);
         delete r;
@@ -933,18 +955,19 @@ int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool fina
         return rc;
     }
     Req* r = nullptr;
+    const bool h2d = !d->E->sha_zero_copy;
     if (sl) {
         r = new Req();
         r->slot = sl;
         r->len = len;
-        rc = stage(d->E, r);
+        rc = h2d ? stage(d->E, r) : KRK_OK;
         if (rc) {
             d->E->pool.release(sl);
             delete r;
             return rc;
         }
     } else {
-        rc = make_req(d->E, src, len, &r);
+        rc = make_req(d->E, src, len, &r, h2d);
         if (rc) return rc;
     }
     r->owner = d;

@@ -19,7 +19,7 @@ from kraken_amd._capi import KRK_PLACE_AUTO, KRK_PLACE_GPU, KRK_PLACE_HOST, chec
 
 pytestmark = pytest.mark.gpu
 
-SLOT = 2 << 20  # the engine's default slot (KRK_SLOT_MB)
+SLOT = 512 << 10  # the engine's default slot (KRK_SLOT_KB)
 
 
 def _stats():
