@@ -75,6 +75,16 @@ int krk_piece_sums_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_d
  * kernel.  Synchronous.  This is the batch form of Generator.Generate's
  * NewMetaInfo call (lib/metainfogen/generator.go:41-58). */
 int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host);
+/* krk_piece_sums_host and krk_verify_pieces_host split a batch, whole pieces at a time,
+ * between host PCLMUL threads (the reference's own placement: one hash.Hash32 per piece,
+ * lib/torrent/storage/agentstorage/torrent.go:182-193) and the GPU pass.  Pinned caller
+ * bytes (krk_host_alloc) are DMA'd straight into the device windows and the GPU takes a
+ * share learned from the previous calls' measured rates of both sides (first call: the
+ * planner rates' model, at most 10 %); pageable bytes stay on the host (a staging copy per
+ * byte costs more than the GPU saves).  KRK_CRC_GPU_FRACTION forces the share.  This
+ * returns the calling thread's last split in bytes and the share the next pinned batch
+ * will use (-1 until learned). */
+int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction);
 
 /* Piece sums of cache FILES: the batch form of Generator.Generate reading the
  * CAS cache file itself (lib/metainfogen/generator.go:41-58: GetCacheFileReader

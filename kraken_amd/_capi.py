@@ -79,6 +79,7 @@ def _load() -> C.CDLL:
         "krk_piece_sums_dev": (i, [blobp, C.c_uint64, vp, vp]),
         "krk_metainfo_batch_dev": (i, [blobp, C.c_uint64, C.c_char_p, u64p, vp, u32p, C.POINTER(C.c_uint8), vp]),
         "krk_piece_sums_host": (i, [blobp, C.c_uint64, u32p]),
+        "krk_crc_host_split": (i, [u64p, u64p, f64p]),
         "krk_piece_sums_files": (i, [C.POINTER(krk_file_blob), C.c_uint64, u32p]),
         "krk_piece_stream_begin": (i, [C.c_int64, C.POINTER(vp)]),
         "krk_piece_stream_update": (i, [vp, vp, C.c_uint64]),

@@ -666,6 +666,11 @@ struct PieceTask {
     uint64_t out;
 };
 
+// GPU share of pinned CRC batches learned from earlier calls (-1: none yet), and the
+// calling thread's last split (krk_crc_host_split).
+static std::atomic<double> g_crc_split{-1.0};
+static thread_local uint64_t t_split_gpu = 0, t_split_host = 0;
+
 static bool host_pinned(const void* p, uint64_t n) {
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) return false;
@@ -691,15 +696,20 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         bytes += (double)blobs[i].length;
         if (all_pinned && blobs[i].length && !host_pinned(blobs[i].data, blobs[i].length)) all_pinned = false;
     }
+    // Pinned bytes: the GPU's share starts from the rates' model, capped at 10 %, and is then
+    // set from what the previous calls measured (each side's bytes over its own wall time
+    // while both ran): the DMA reads share the host's memory with the CRC threads, so the
+    // static model overestimates the GPU side (f1verify, same box: 10 % 282 GB/s, 20 % 182,
+    // host only 228).  Pageable bytes stay on the host: a copy into pinned staging per byte
+    // cost more than the GPU saved (host only 241 GB/s, the model's split 202).
     const double c = R.host_crc, H = T * c;
-    double gpu_frac;
+    double gpu_frac = 0.0;
     if (all_pinned) {
-        gpu_frac = R.h2d / (R.h2d + H);
-    } else {
-        const double m = R.host_copy, L = host_link(R);
-        gpu_frac = m > c ? std::min(1.0, (1.0 / c) / (T / L + 1.0 / c - 1.0 / m)) : 0.0;
+        const double learned = g_crc_split.load(std::memory_order_relaxed);
+        gpu_frac = learned >= 0 ? learned : std::min(0.10, R.h2d / (R.h2d + H));
     }
-    if (const char* e = getenv("KRK_CRC_GPU_FRACTION")) gpu_frac = std::clamp(atof(e), 0.0, 1.0);
+    const char* forced = getenv("KRK_CRC_GPU_FRACTION");
+    if (forced) gpu_frac = std::clamp(atof(forced), 0.0, 1.0);
     // Whole pieces to the GPU until its share of the bytes is reached, the rest to the host.
     const double quota = gpu_frac * bytes;
     double gbytes = 0;
@@ -723,16 +733,25 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         for (uint64_t k = q; k < np; ++k) host.push_back({b.data + k * P, std::min(P, b.length - k * P), b.sums_offset + k});
     }
     std::atomic<size_t> next{0};
+    std::atomic<int> running{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::atomic<int64_t> host_end_ns{0};
     auto work = [&] {
         for (size_t j; (j = next.fetch_add(1)) < host.size();)
             sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
+        if (running.fetch_sub(1) == 1)  // the last host thread: the host side's wall time
+            host_end_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                                  .count());
     };
     std::vector<std::thread> pool;
     const int TH = (int)std::min<size_t>((size_t)T, host.size());
+    running.store(TH);
     for (int t = 0; t < TH; ++t) pool.emplace_back(work);
+    double gpu_s = 0;
     if (!gpu.empty()) {
         std::vector<uint32_t> gs(g_sums);
         r = piece_sums_host_gpu(D, gpu.data(), gpu.size(), gs.data(), all_pinned);
+        gpu_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (!r)
             for (size_t j = 0; j < gpu.size(); ++j) {
                 const uint64_t cnt = krk_num_pieces(gpu[j].length, gpu[j].piece_length);
@@ -740,7 +759,23 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
             }
     }
     for (auto& t : pool) t.join();
+    const double hbytes = bytes - gbytes, host_s = host_end_ns.load() * 1e-9;
+    t_split_gpu = (uint64_t)gbytes;
+    t_split_host = (uint64_t)hbytes;
+    if (!r && all_pinned && !forced && gbytes >= (64u << 20) && hbytes >= (64u << 20) && gpu_s > 0 && host_s > 0) {
+        // the split where both sides would have ended together at the rates just measured
+        const double rg = gbytes / gpu_s, rh = hbytes / host_s, want = rg / (rg + rh);
+        const double cur = g_crc_split.load(std::memory_order_relaxed);
+        g_crc_split.store(cur >= 0 ? 0.5 * cur + 0.5 * want : want, std::memory_order_relaxed);
+    }
     return r;
+}
+
+int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction) {
+    if (gpu_bytes) *gpu_bytes = t_split_gpu;
+    if (host_bytes) *host_bytes = t_split_host;
+    if (gpu_fraction) *gpu_fraction = g_crc_split.load(std::memory_order_relaxed);
+    return KRK_OK;
 }
 
 int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_host) {

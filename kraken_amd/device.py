@@ -257,6 +257,14 @@ def piece_sums_host(datas, piece_length: int):
     return out
 
 
+def crc_host_split():
+    """(GPU bytes, host bytes) of this thread's last krk_piece_sums_host / verify call and
+    the GPU share the next pinned batch will use (-1 until learned)."""
+    g, h, f = C.c_uint64(), C.c_uint64(), C.c_double()
+    check(lib.krk_crc_host_split(C.byref(g), C.byref(h), C.byref(f)))
+    return g.value, h.value, f.value
+
+
 RATES_SOURCE = {0: "nominal", 1: "measured", 2: "set"}
 
 
