@@ -666,7 +666,12 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
     bytes per blob are capped to 40 % of the host memory over the ranks (reported)."""
     import ctypes as C
     want = Le
-    cap = int(0.4 * host_mem_budget() / max(1, world) / max(1, n)) // P * P
+    # host memory per rank: 40 % of the host's over the ranks, and at most 24 GiB a rank when
+    # several ranks share the node (8 ranks x 100 GB of pageable copies would crowd the host)
+    per_rank = 0.4 * host_mem_budget() / max(1, world)
+    if world > 1:
+        per_rank = min(per_rank, 24 << 30)
+    cap = int(per_rank / max(1, n)) // P * P
     if cap < Le:
         Le = max(P, cap)
     datas = [np.empty(Le, dtype=np.uint8) for _ in range(n)]
@@ -687,7 +692,8 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
         ok = all(np.array_equal(sums[i][:k], dev_sums[int(arena.sums_off[i]):int(arena.sums_off[i]) + k])
                  for i in range(n))
     res = {"value": round(world * n * Le / el / 1e9, 3), "unit": "GB/s", "blobs_per_gpu": n, "blob_bytes": Le,
-           **({"blob_bytes_requested": want, "capped_by": "host memory / ranks"} if Le < want else {}),
+           **({"blob_bytes_requested": want, "capped_by": "host memory per rank (40 % / ranks, <= 24 GiB with "
+                                                          "several ranks)"} if Le < want else {}),
            "seconds": round(el, 3), "passes_s": [round(x, 3) for x in passes],
            "source": "pageable host memory (numpy), copied into pinned windows; median of the passes",
            "bound": "PCIe H2D (one pass per byte) and the per-blob SHA-256 chain (blob_bytes / per-stream rate)",
