@@ -59,13 +59,16 @@ int shard_run(const std::vector<uint64_t>& bytes, F&& part) {
     const auto idx = lpt(bytes, devs.size());
     std::vector<int> rc(devs.size(), KRK_OK);
     std::vector<std::string> msg(devs.size());
+    const int share = std::max(1, host_cpu_budget() / (int)std::max<size_t>(1, devs.size()));
     auto work = [&](size_t w) {
         if (idx[w].empty()) return;
-        const int saved = t_dev;
+        const int saved = t_dev, saved_share = t_host_share;
         t_dev = devs[w];
+        t_host_share = share;  // this worker's share of the host threads
         rc[w] = part(w, idx[w]);
         if (rc[w]) msg[w] = t_err;
         t_dev = saved;
+        t_host_share = saved_share;
     };
     std::vector<std::thread> th;
     for (size_t w = 1; w < devs.size(); ++w) th.emplace_back(work, w);

@@ -202,9 +202,12 @@ struct Worker {
 
 }  // namespace
 
+// Per device: sets of worker resources (two streams + two pinned buffers a thread).  Each
+// offload phase takes a set of its own, so concurrent callers on one device (several
+// krk_sha256_dev callers, *_multi workers sharing a GPU) hash at the same time.
 struct OffloadPool {
-    std::mutex mu;  // one offload phase at a time per device
-    std::vector<Worker> w;
+    std::mutex mu;
+    std::vector<std::vector<Worker>> free_sets;
 };
 
 // The longest blobs to hash on `threads` host threads (indices into lens, longest
@@ -321,16 +324,37 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
         if (!D->offload) D->offload = new OffloadPool();
     }
     OffloadPool& P = *D->offload;
-    std::lock_guard<std::mutex> g(P.mu);
     // at least one thread: the knob may have been lowered since the plan was made
     const int T = (int)std::min<size_t>((size_t)std::max(threads, 1), ptrs.size());
-    while ((int)P.w.size() < T) {
+    std::vector<Worker> set;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        if (!P.free_sets.empty()) {
+            set = std::move(P.free_sets.back());
+            P.free_sets.pop_back();
+        }
+    }
+    struct Return {  // the set goes back to the pool whatever happens below
+        OffloadPool& P;
+        std::vector<Worker>& set;
+        ~Return() {
+            std::lock_guard<std::mutex> g(P.mu);
+            P.free_sets.push_back(std::move(set));
+        }
+    } give_back{P, set};
+    while ((int)set.size() < T) {
         Worker w;
         for (int b = 0; b < 2; ++b) {
             KRK_HIP(hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking));
-            KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault));
+            if (hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault) != hipSuccess) {
+                for (int c = 0; c <= b; ++c)
+                    if (w.s[c]) hipStreamDestroy(w.s[c]);
+                if (b) hipHostFree(w.buf[0]);
+                set_error(KRK_ENOMEM, "sha256 host offload: pinned buffers");
+                return KRK_ENOMEM;
+            }
         }
-        P.w.push_back(w);
+        set.push_back(w);
     }
     std::atomic<size_t> next{0};
     std::atomic<int> err{0};
@@ -343,7 +367,7 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     std::vector<std::thread> pool;
     for (int t = 0; t < T; ++t)
         pool.emplace_back([&, t] {
-            Worker& W = P.w[t];
+            Worker& W = set[t];
             // The host waits for `ready` (the caller's stream up to the call; the batch's own
             // kernels come after it): a stream wait packet could queue behind those kernels.
             if (hipSetDevice(D->id) != hipSuccess || hipEventSynchronize(ready) != hipSuccess) {
@@ -404,14 +428,15 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     return KRK_OK;
 }
 
-void offload_teardown(Device& D) {
+void offload_teardown(Device& D) {  // krk_shutdown: no offload phase is running (contract)
     OffloadPool* P = D.offload;
     if (!P) return;
-    for (Worker& w : P->w)
-        for (int b = 0; b < 2; ++b) {
-            if (w.s[b]) hipStreamSynchronize(w.s[b]), hipStreamDestroy(w.s[b]);
-            if (w.buf[b]) hipHostFree(w.buf[b]);
-        }
+    for (auto& set : P->free_sets)
+        for (Worker& w : set)
+            for (int b = 0; b < 2; ++b) {
+                if (w.s[b]) hipStreamSynchronize(w.s[b]), hipStreamDestroy(w.s[b]);
+                if (w.buf[b]) hipHostFree(w.buf[b]);
+            }
     delete P;
     D.offload = nullptr;
 }

@@ -213,7 +213,7 @@ static int lease_staging(Device* D, size_t cap, StagingLease& L) {
 static unsigned copy_threads() {
     const char* v = getenv("KRK_COPY_THREADS");
     if (v) return std::max(1u, (unsigned)strtoul(v, nullptr, 10));
-    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    return std::max(1u, std::min(16u, (unsigned)host_threads_for_call()));
 }
 
 static void par_copy(const std::vector<CopyTask>& tasks) {
@@ -689,7 +689,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     if (hi == lo) return KRK_OK;
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
     const Rates R = planner_rates(D);
-    const int T = host_cpu_budget();
+    const int T = host_threads_for_call();
     bool all_pinned = true;
     double bytes = 0;
     for (uint64_t i = 0; i < n_blobs; ++i) {

@@ -596,6 +596,10 @@ struct Rates {
 };
 Rates planner_rates(Device* D);  // D == nullptr: the override or the nominal rates
 int host_cpu_budget();           // CPUs this process may use: affinity, cgroup quota, OMP_NUM_THREADS
+// Host threads a call on this thread may use (0: host_cpu_budget()): a *_multi worker runs
+// with its share of the budget, so N devices' workers do not start N x 16 copy threads.
+inline thread_local int t_host_share = 0;
+inline int host_threads_for_call() { return t_host_share > 0 ? t_host_share : host_cpu_budget(); }
 uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);  // host_meta.cpp
 double host_link(const Rates& R);
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,

@@ -104,3 +104,20 @@ def test_metainfo_digest_host_multi_with_offload(two_workers, orc):
     for i, d in enumerate(datas):
         assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), i
         assert np.array_equal(sums[i], orc.calc_piece_sums(d, 1 << 20)[1]), i
+
+
+def test_eight_workers_share_the_host(gpu, orc):
+    """the device set at 8 entries (device 0 eight times here) -- the
+    LPT split, 8 concurrent workers each with its share of the host threads (their copy
+    threads no longer 8 x 16), the gather -- with every blob equal to the oracle."""
+    D.set_devices([0] * 8)
+    try:
+        assert D.get_devices() == [0] * 8
+        datas = _blobs(8, n=61)
+        P = 1 << 20
+        sums, dg = D.metainfo_digest_host(datas, [P] * len(datas), multi=True)
+        for i, d in enumerate(datas):
+            assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), i
+            assert np.array_equal(sums[i], orc.calc_piece_sums(d, P)[1]), i
+    finally:
+        D.set_devices([])
