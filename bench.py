@@ -77,12 +77,17 @@ def sha_isa_ceiling(D, launch, lanes):
 
 def load_valu(workload):
     """VALU / LDS utilisation per kernel from the committed rocprofv3 PMC passes
-    (tools/pmc_valu.py -> profiles/r02/valu_<workload>.json); the raw counters stay in
+    (tools/pmc_valu.py -> profiles/r03/valu_<workload>.json); the raw counters stay in
     that file, the derived fractions go into the bench line."""
-    path = os.path.join(ROOT, "profiles", "r02", f"valu_{workload}.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
+    d, path = None, None
+    for rnd in ("r03", "r02"):  # the newest round's passes
+        path = os.path.join(ROOT, "profiles", rnd, f"valu_{workload}.json")
+        try:
+            d = json.load(open(path))
+            break
+        except (OSError, ValueError):
+            d = None
+    if d is None:
         return {}, None
     keep = ("valu_issue_frac_per_wave", "valu_busy_chip_pct", "lds_issue_frac_per_wave", "lds_bank_conflict_frac",
             "wait_any_frac_per_wave", "wait_inst_any_frac_per_wave", "clock_mhz", "kernel_ms", "dispatches")

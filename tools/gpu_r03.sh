@@ -45,6 +45,9 @@ for s in "$@"; do
   case $s in
     vop) step micro_vopcost 120 tools/micro/vopcost ;;
     nd) for cfg in "2048 4" "1024 6" "512 8"; do set -- $cfg; step nd_$1_$2 150 env KRK_SLOT_KB=$1 KRK_OWNER_INFLIGHT=$2 tests/native/digesters 256 16 4 || exit 1; done ;;
+    traffic) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py $C2 &&
+             step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py $C2 &&
+             step pmc_traffic_json 120 python tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --out gpurun_out/pmc_traffic.json ;;
     n2) step bench_n2 600 python bench.py --gpus 2 --rehearse --blobs 200 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e ;;
     pmcf) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -- python3 $R/bench.py $C2 ;;
     pmcw) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -- python3 $R/bench.py $C2 ;;
