@@ -924,6 +924,50 @@ def run_chunked(a, D, T, rank, world, res):
             ok = ok and np.array_equal(sums[o:o + cnt], rs[ro:ro + cnt])
         res["spot_check_matches_one_shot"] = bool(ok)
     wr.close()
+    if a.host_lane:
+        res["host_offload"] = run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums)
+
+
+def run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums):
+    """C3 with the host lane (kraken_amd.windowed): the K longest blobs of the shard are
+    generated into a device buffer of their own, their piece CRCs run on the GPU and their
+    SHA-256 on host threads reading HBM, while the windows run the rest.  GPU + host
+    throughput: reported beside the GPU-only value, never as it.  K from the planner
+    (windowed.host_lane_plan over krk_planner_rates) unless --host-lane-k."""
+    from kraken_amd.windowed import WindowedRun, host_lane_plan, window_stream_cap
+    threads = max(1, host_cores() - 1)  # one core stays with the window loop
+    W = a.window_gib << 30
+    cap = len(lens) if a.no_admission else (a.live_cap or window_stream_cap(D, len(lens)))
+    rates = D.planner_rates()
+    k, model_s, model0_s = host_lane_plan(D, lens, W, cap, threads, rates=rates)
+    if a.host_lane_k >= 0:
+        k = min(a.host_lane_k, len(lens))
+    out = {"blobs_on_host": int(k), "threads": threads,
+           "modelled_s": round(model_s, 3), "modelled_gpu_only_s": round(model0_s, 3),
+           "planner_rates": {"sha_stream_MBps": [round(x / 1e6, 2) for x in rates["sha_stream_bps"]],
+                             "host_sha_GBps_per_thread": round(rates["host_sha_bps"] / 1e9, 3),
+                             "d2h_GBps": round(rates["d2h_bps"] / 1e9, 2), "source": rates["source"]},
+           "what": "GPU + host: the longest blobs hashed by host threads reading them out of HBM (SHA-NI) while "
+                   "the GPU windows run the rest; their piece CRCs stay on the GPU"}
+    if k == 0:
+        out["note"] = "the planner keeps every blob on the GPU (the lane would not shorten the run by 2 %)"
+        return out
+    wr = WindowedRun(D, ids, lens, P, W, cap=cap if (a.no_admission or a.live_cap) else None,
+                     host_lane=(k, threads), device=a.device)
+    T.barrier()
+    t0 = time.perf_counter()
+    wr.run()
+    T.barrier()
+    el = T.max_over_ranks(time.perf_counter() - t0)
+    n = len(lens)
+    dg2 = wr.cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
+    s2 = wr.cb.sums.to_host(np.uint32, max(wr.cb.total_pieces, 1))
+    wr.close()
+    out.update({"value": round(total_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el * 1e3, 3),
+                "host_bytes": int(sum(lens[i] for i in wr.lane_blobs)), "lane_s": round(wr.lane_seconds, 3),
+                "windows": len(wr.wins),
+                "matches_gpu_only": bool(np.array_equal(dg2, dg) and np.array_equal(s2, sums))})
+    return out
 
 
 def run_hrw(a, D, T, rank, world, res):
@@ -1107,6 +1151,10 @@ def main():
                     help="C3: run rank 0's LPT shard of an N-GPU run on this GPU (no collective exists to emulate)")
     ap.add_argument("--no-admission", action="store_true",
                     help="C3: all blobs live from window 0 (no longest-first admission under the two-lane cap)")
+    ap.add_argument("--host-lane", action="store_true",
+                    help="C3: also run the batch with the host lane (the longest blobs hashed on host threads "
+                         "while the windows run the rest), reported as host_offload beside the GPU-only value")
+    ap.add_argument("--host-lane-k", type=int, default=-1, help="C3: blobs the host lane takes (-1 = the planner's)")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
     ap.add_argument("--regen-serial", action="store_true",
                     help="c5regen: piece sums then InfoHashes (no krk_metainfo_batch_dev pipelining)")
@@ -1145,7 +1193,8 @@ def main():
     ndev = D.device_count()
     if world > ndev and not a.rehearse:
         raise SystemExit(f"bench.py: {world} ranks but {ndev} gfx950 device(s) visible (pass --rehearse to share)")
-    D.set_device(local % max(1, ndev))
+    a.device = local % max(1, ndev)
+    D.set_device(a.device)
     T = Timer(D, dist)
     res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
     if world > ndev:

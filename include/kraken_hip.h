@@ -146,6 +146,15 @@ int krk_verify_pieces_host(const uint8_t* const* data, const uint64_t* lengths, 
 int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n,
                    uint8_t* digests_dev, void* stream);
 
+/* Device-resident batch hashed by host threads (x86 SHA extensions): up to `threads`
+ * threads (<= 0: the CPUs this process may use) each read a blob out of device memory
+ * through their own pinned double buffers, after the work queued on `stream` up to the
+ * call; digests_host n*32 bytes.  Synchronous.  The host lane of a windowed batch
+ * (kraken_amd/windowed.py): the longest chains of a larger-than-HBM batch hashed on the
+ * host while the GPU windows run the rest. */
+int krk_sha256_dev_on_host(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n, int threads,
+                           void* stream, uint8_t* digests_host);
+
 /* Host batch: HOST data pointers; digests_host n*32 bytes.  Synchronous. */
 int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
                     uint8_t* digests_host);
@@ -376,6 +385,11 @@ int krk_memcpy_d2h(void* dst_host, const void* src_dev, uint64_t n);
  * (krk_host_alloc) for the copy to overlap the host. */
 int krk_memcpy_d2h_async(void* dst_host, const void* src_dev, uint64_t n, void* stream);
 int krk_stream_create(void** out);
+/* A stream of the given priority: -1 high, 0 normal, 1 low (HIP's priority range).
+ * Streams of another priority run on hardware queues of their own: a stream that holds
+ * long kernels (a C3 window's SHA-256 launch runs ~0.6 s) is kept off the queues the
+ * short work shares, which would otherwise wait behind it. */
+int krk_stream_create_prio(int priority, void** out);
 int krk_stream_destroy(void* s);
 int krk_stream_sync(void* s);
 /* Events (a window loop waits for ONE earlier window's kernels while the next

@@ -90,6 +90,7 @@ def _load() -> C.CDLL:
         "krk_verify_pieces_host": (i, [C.POINTER(vp), u64p, u32p, C.c_uint64, u8p]),
         "krk_sha256_dev": (i, [C.POINTER(vp), u64p, C.c_uint64, vp, vp]),
         "krk_sha256_host": (i, [C.POINTER(vp), u64p, C.c_uint64, u8p]),
+        "krk_sha256_dev_on_host": (i, [C.POINTER(vp), u64p, C.c_uint64, i, vp, u8p]),
         "krk_digester_new": (i, [C.POINTER(vp)]),
         "krk_digester_new_on": (i, [i, C.POINTER(vp)]),
         "krk_digester_placement": (i, [vp, C.POINTER(C.c_int)]),
@@ -136,6 +137,7 @@ def _load() -> C.CDLL:
         "krk_memcpy_d2h": (i, [vp, vp, C.c_uint64]),
         "krk_memcpy_d2h_async": (i, [vp, vp, C.c_uint64, vp]),
         "krk_stream_create": (i, [C.POINTER(vp)]),
+        "krk_stream_create_prio": (i, [i, C.POINTER(vp)]),
         "krk_stream_destroy": (i, [vp]),
         "krk_stream_sync": (i, [vp]),
         "krk_event_create": (i, [C.POINTER(vp)]),

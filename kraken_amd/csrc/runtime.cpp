@@ -267,10 +267,11 @@ static void teardown_device(Device& D) {
         D.cache.live.clear();
     }
     for (auto& P : D.slots) {
-        if (P.ev) hipEventSynchronize(P.ev), hipEventDestroy(P.ev);
-        if (P.p) hipHostFree(P.p);
-        P = PinnedSlot();
+        if (P->ev) hipEventSynchronize(P->ev), hipEventDestroy(P->ev);
+        if (P->p) hipHostFree(P->p);
     }
+    D.slots.clear();
+    D.next_slot = 0;
     for (void* p : D.retired_pinned) hipHostFree(p);
     D.retired_pinned.clear();
     for (void* p : {(void*)D.shard_kb, (void*)D.shard_koff, (void*)D.shard_bad, (void*)D.d_tabs})
@@ -468,6 +469,28 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
     }
     if (!r) r = run_jobs(D, jobs, digests_dev, nullptr, s);  // the GPU part runs while the host hashes
     if (!r) r = offload_run(D, host, data_dev, lengths, ready, digests_dev, s);
+    hipEventDestroy(ready);
+    return r;
+}
+
+int krk_sha256_dev_on_host(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n, int threads,
+                           void* stream, uint8_t* digests_host) {
+    KRK_DEVICE(D);
+    if (!n) return KRK_OK;
+    KRK_CHECK(data_dev && lengths && digests_host, KRK_EINVAL, "sha256_dev_on_host: null argument");
+    hipStream_t s = pick(D, stream);
+    hipEvent_t ready;
+    KRK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    int r = KRK_OK;
+    if (hipEventRecord(ready, s) != hipSuccess) {
+        set_error(KRK_EHIP, "sha256_dev_on_host: event record failed");
+        r = KRK_EHIP;
+    }
+    if (!r) {
+        const std::vector<const uint8_t*> p(data_dev, data_dev + n);
+        const std::vector<uint64_t> l(lengths, lengths + n);
+        r = offload_hash(D, p, l, threads > 0 ? threads : host_threads_for_call(), ready, digests_host);
+    }
     hipEventDestroy(ready);
     return r;
 }
@@ -1667,6 +1690,18 @@ int krk_stream_create(void** out) {
     (void)D;
     hipStream_t s;
     KRK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = s;
+    return KRK_OK;
+}
+int krk_stream_create_prio(int priority, void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    int least = 0, greatest = 0;  // HIP: numerically lower = higher priority
+    KRK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const int p = priority < 0 ? greatest : priority > 0 ? least : (least + greatest) / 2;
+    hipStream_t s;
+    KRK_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p));
     *out = s;
     return KRK_OK;
 }

@@ -117,6 +117,7 @@ inline void drain_timing() {
 }
 
 // ------------------------------------------------------------------ device
+constexpr size_t kMaxUploadSlots = 64;
 struct PinnedSlot {
     void* p = nullptr;
     size_t cap = 0;
@@ -225,8 +226,8 @@ struct Device {
     uint32_t* d_tabs = nullptr;
     int crc_variant = 0;
     std::mutex mu;
-    PinnedSlot slots[8];
-    unsigned next_slot = 0;
+    std::vector<std::unique_ptr<PinnedSlot>> slots;  // upload(): grows while every slot is in flight
+    size_t next_slot = 0;
     std::vector<void*> retired_pinned;  // grown-out upload buffers (freed at krk_shutdown)
 };
 
@@ -341,11 +342,31 @@ inline int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_
     if (!n) return KRK_OK;
     KRK_HIP(scratch_alloc(D, d_out, n, s));
     std::lock_guard<std::mutex> g(D->mu);
-    PinnedSlot& P = D->slots[D->next_slot++ % 8];
-    if (P.busy) {
-        KRK_HIP(hipEventSynchronize(P.ev));
-        P.busy = false;
+    // A slot whose last copy is done.  A copy queued behind a long kernel of its stream
+    // (a C3 window's chunk upload waits for the window before it, ~0.6 s of SHA-256) keeps
+    // its slot busy that long: such slots are skipped and the pool grows instead of
+    // waiting -- waiting here, under the device lock, held every other caller's upload
+    // (the C3 host lane's CRC launches) behind that kernel.
+    PinnedSlot* pick_slot = nullptr;
+    const size_t ns = D->slots.size();
+    for (size_t k = 0; k < ns && !pick_slot; ++k) {
+        PinnedSlot& c = *D->slots[(D->next_slot + k) % ns];
+        if (c.busy && hipEventQuery(c.ev) == hipSuccess) c.busy = false;
+        if (!c.busy) {
+            pick_slot = &c;
+            D->next_slot = (D->next_slot + k + 1) % ns;
+        }
     }
+    if (!pick_slot && ns < kMaxUploadSlots) {
+        D->slots.push_back(std::make_unique<PinnedSlot>());
+        pick_slot = D->slots.back().get();
+    }
+    if (!pick_slot) {  // every slot in flight: wait for the next in turn
+        pick_slot = D->slots[D->next_slot++ % ns].get();
+        KRK_HIP(hipEventSynchronize(pick_slot->ev));
+        pick_slot->busy = false;
+    }
+    PinnedSlot& P = *pick_slot;
     if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
     if (P.cap < n) {
         // hipHostFree waits for the whole device (a kernel of another stream included), so

@@ -221,6 +221,28 @@ def sha256(arena: BlobArena, out: BatchOutputs, stream=None):
                              out.digests.ptr, stream))
 
 
+def sha256_dev_on_host(ptrs, lens, threads: int = 0, stream=None) -> np.ndarray:
+    """krk_sha256_dev_on_host: device blobs (numpy device addresses + lengths) hashed by
+    up to `threads` host threads after `stream`'s queued work; (n, 32) uint8 digests."""
+    n = len(ptrs)
+    p = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    out = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    check(lib.krk_sha256_dev_on_host(p.ctypes.data_as(C.POINTER(C.c_void_p)), ln.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                     n, int(threads), stream, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out[:n]
+
+
+def piece_sums_dev_arrays(ptrs, lens, piece_lengths, sums_offsets, sums_dev_ptr: int, stream=None):
+    """krk_piece_sums_dev over blobs given column-wise (device addresses, lengths, piece
+    lengths, offsets of their sums in the sums buffer at sums_dev_ptr)."""
+    n = len(ptrs)
+    a = np.zeros(max(n, 1), dtype=KRK_BLOB_DTYPE)
+    a["data"][:n], a["length"][:n] = ptrs, lens
+    a["piece_length"][:n], a["sums_offset"][:n] = piece_lengths, sums_offsets
+    check(lib.krk_piece_sums_dev(a.ctypes.data_as(C.POINTER(krk_blob)), n, sums_dev_ptr, stream))
+
+
 def metainfo_digest(arena: BlobArena, out: BatchOutputs, stream=None):
     check(lib.krk_metainfo_digest_dev(arena.blob_structs(), len(arena.lengths), out.sums.ptr,
                                       out.digests.ptr, stream))

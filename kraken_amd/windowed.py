@@ -84,26 +84,112 @@ def window_stream_cap(D, n):
     return max(1, min(n, cap))
 
 
+def stream_rate(rates, n_streams):
+    """One SHA-256 stream's rate (B/s) in a launch of n_streams: the planner rate of the
+    AUTO tier the launch falls in (eight lanes up to 16 x CUs streams, two lanes up to
+    64 x CUs, one lane beyond; krk_planner_rates)."""
+    cus = max(1, int(rates["cus"]))
+    return rates["sha_stream_bps"][0 if n_streams <= 16 * cus else 1 if n_streams <= 64 * cus else 2]
+
+
+def windows_seconds(rates, lens, W, cap, launch_s=0.0005):
+    """Modelled run time of the windows over `lens`: each window lasts its largest chunk
+    at the per-stream rate of its launch plan (the chain of the window's longest chunk
+    sets it), plus a launch overhead."""
+    t = 0.0
+    for blobs, _, take in window_plan(lens, W, cap):
+        t += float(take.max()) / stream_rate(rates, blobs.size) + launch_s
+    return t
+
+
+def host_lane_plan(D, lens, W, cap, threads, rates=None, min_gain=0.02):
+    """How many of the longest blobs the host lane takes: K (a multiple of `threads`, the
+    lane hashes one group of `threads` blobs at a time) minimising max(GPU windows over the
+    rest, host groups), from the planner rates (krk_planner_rates: per-stream rates
+    measured on the device, one host thread's SHA-256 rate, the D2H rate shared by the
+    threads).  0 unless it shortens the modelled run by min_gain.  Returns (K, modelled
+    seconds with it, modelled seconds without)."""
+    rates = rates or D.planner_rates()
+    T = max(1, int(threads))
+    L = np.asarray(lens, dtype=np.int64)
+    order = np.argsort(-L, kind="stable")
+    per_thread = min(rates["host_sha_bps"], rates["d2h_bps"] / T)
+
+    def cost(m):  # m groups of T on the host
+        k = min(m * T, L.size)
+        host = sum(float(L[order[g * T]]) / per_thread for g in range(m))  # a group lasts its longest blob
+        rest = L[order[k:]]
+        gpu = windows_seconds(rates, rest, W, min(cap, max(1, rest.size))) if rest.size else 0.0
+        return max(gpu, host), k
+
+    base, _ = cost(0)
+    lo, hi = 0, (L.size + T - 1) // T
+    while hi - lo > 2:  # max(decreasing, increasing): ternary search on the group count
+        m1, m2 = lo + (hi - lo) // 3, hi - (hi - lo) // 3
+        if cost(m1)[0] <= cost(m2)[0]:
+            hi = m2
+        else:
+            lo = m1
+    best, k = min(cost(m) for m in range(lo, hi + 1))
+    if best > base * (1 - min_gain):
+        return 0, base, base
+    return k, best, base
+
+
 class WindowedRun:
     """One batch of synthetic blobs (ids, lens, piece length P) streamed through two
     device windows of W bytes: window k+1 is generated on `gen` while window k's
     kernels run on `run`.  After run(): cb.sums / cb.digests hold every blob's piece
-    sums and digest (device)."""
+    sums and digest (device).
 
-    def __init__(self, D, ids, lens, P, W, cap=None):
+    host_lane=(K, threads): the K longest blobs skip the windows; a host-lane thread
+    generates them `threads` at a time into a device buffer of their own, queues their
+    piece CRCs on the GPU (krk_piece_sums_dev, into cb.sums) and hashes them on `threads`
+    host threads (krk_sha256_dev_on_host: each reads a blob out of HBM through pinned
+    double buffers), while the windows run the rest; their digests go into cb.digests at
+    the end of run()."""
+
+    def __init__(self, D, ids, lens, P, W, cap=None, host_lane=None, device=0, run_priority=0, lane_priority=0):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = list(lens)
         self.P = P
         self.W = int(W)
+        self.device = device
         n = len(self.lens)
-        self.cap = window_stream_cap(D, n) if cap is None else int(cap)
-        self.wins = window_plan(self.lens, self.W, self.cap)
-        self.bufs = [D.DeviceBuffer(self.W + 16 * n), D.DeviceBuffer(self.W + 16 * n)]
+        L = np.asarray(self.lens, dtype=np.int64)
+        k, self.lane_threads = (host_lane or (0, 0))
+        order = np.argsort(-L, kind="stable")
+        self.lane_blobs = np.sort(order[:k]) if k else np.zeros(0, dtype=np.int64)
+        self.lane_groups = [order[g:g + self.lane_threads] for g in range(0, k, max(1, self.lane_threads))]
+        gpu = np.setdiff1d(np.arange(n), self.lane_blobs) if k else np.arange(n)
+        self.cap = window_stream_cap(D, gpu.size) if cap is None else int(cap)
+        self.wins = [(gpu[b], o, t) for b, o, t in window_plan(L[gpu], self.W, self.cap)]
+        wb = self.W + 16 * max(gpu.size, 1)
+        self.bufs = [D.DeviceBuffer(wb), D.DeviceBuffer(wb)] if self.wins else []
+        self.lane_bufs, self.lane_ss = [], []
+        if k:  # two buffers of a group each (the first group holds the longest blobs)
+            nb = (int(L[order[0]]) + 256) * len(self.lane_groups[0])
+            self.lane_bufs = [D.DeviceBuffer(nb) for _ in range(min(2, len(self.lane_groups)))]
+        self.lane_digests = None
+        self.lane_seconds = 0.0
         self.cb = D.ChunkedBatch(self.lens, P)
+        # The windows' launches (a SHA-256 launch lasts up to ~0.6 s) go on a stream of
+        # their own priority -- hardware queues of their own -- unless run_priority=0:
+        # the generator's, the host lane's and its D2H copies' work would otherwise wait
+        # behind them in a shared queue (HIP maps streams onto GPU_MAX_HW_QUEUES queues).
         self.gen_s, self.run_s = C.c_void_p(), C.c_void_p()
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
-        D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
+        if run_priority:
+            D.check(D.lib.krk_stream_create_prio(int(run_priority), C.byref(self.run_s)))
+        else:
+            D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
+        for _ in self.lane_bufs:
+            self.lane_ss.append(C.c_void_p())
+            if lane_priority:
+                D.check(D.lib.krk_stream_create_prio(int(lane_priority), C.byref(self.lane_ss[-1])))
+            else:
+                D.check(D.lib.krk_stream_create(C.byref(self.lane_ss[-1])))
 
     def _items(self, k):
         blobs, offs, take = self.wins[k]
@@ -117,10 +203,72 @@ class WindowedRun:
         self.D.synth_fill_chunk_arrays(self.ids[blobs], dev, offs, take, stream=self.gen_s)
         self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
 
+    def _lane(self, err):
+        """The host lane's thread: group by group (longest first), generate the group's
+        blobs into one of two lane buffers and queue their piece CRCs on that buffer's
+        stream, then hash the previous group on the host threads -- group g+1 is
+        generated and CRC'd on the device while group g is hashed."""
+        D = self.D
+        try:
+            import time
+            t0 = time.perf_counter()
+            D.set_device(self.device)
+            dig = np.zeros((len(self.lens), 32), dtype=np.uint8)
+            L = np.asarray(self.lens, dtype=np.uint64)
+
+            def place(g, b):
+                ln = L[g]
+                dev = np.zeros(g.size, dtype=np.uint64)  # 256-byte aligned slots in lane buffer b
+                dev[1:] = np.cumsum((ln + np.uint64(255)) // np.uint64(256) * np.uint64(256))[:-1]
+                dev += np.uint64(self.lane_bufs[b].ptr)
+                s = self.lane_ss[b]
+                D.synth_fill_chunk_arrays(self.ids[g], dev, np.zeros(g.size, np.uint64), ln, stream=s)
+                for j in range(g.size):  # one call a blob: a call zeroes the whole sums span it covers
+                    D.piece_sums_dev_arrays(dev[j:j + 1], ln[j:j + 1], self.cb.piece_lengths[g[j:j + 1]],
+                                            self.cb.sums_off[g[j:j + 1]], self.cb.sums.ptr, stream=s)
+                return dev, ln
+
+            groups = self.lane_groups
+            cur = place(groups[0], 0)
+            for k, g in enumerate(groups):
+                # buffer (k+1)&1 last held group k-1: hashed (the call below is synchronous)
+                # and CRC'd (same stream, earlier) before the next fill is queued behind them
+                nxt = place(groups[k + 1], (k + 1) & 1) if k + 1 < len(groups) else None
+                dig[g] = D.sha256_dev_on_host(cur[0], cur[1], self.lane_threads, stream=self.lane_ss[k & 1])
+                cur = nxt
+            for s in self.lane_ss:  # the last groups' CRCs
+                D.check(D.lib.krk_stream_sync(s))
+            self.lane_digests = dig
+            self.lane_seconds = time.perf_counter() - t0
+        except BaseException as e:  # re-raised on the caller's thread
+            err.append(e)
+
     def run(self):
         """Window k's kernels are queued before the host waits for window k-1's (an
         event after each window), so the device goes from one window to the next with
-        no host round trip; window k+1 is generated into k-1's buffer once k-1 is done."""
+        no host round trip; window k+1 is generated into k-1's buffer once k-1 is done.
+        The host lane (if any) runs on its own thread meanwhile."""
+        lane, err = None, []
+        if self.lane_groups:
+            import threading
+            lane = threading.Thread(target=self._lane, args=(err,), name="krk-host-lane")
+            lane.start()
+        try:
+            if self.wins:
+                self._run_windows()
+        finally:
+            if lane is not None:
+                lane.join()
+        if err:
+            raise err[0]
+        if lane is not None:  # the lane's digests into the batch's digest rows
+            D = self.D
+            for i in self.lane_blobs:
+                row = np.ascontiguousarray(self.lane_digests[i])
+                D.check(D.lib.krk_memcpy_h2d(C.c_void_p(self.cb.digests.ptr + 32 * int(i)),
+                                             row.ctypes.data_as(C.c_void_p), 32))
+
+    def _run_windows(self):
         D = self.D
         cur = self._items(0)
         self._gen(cur)
@@ -142,13 +290,13 @@ class WindowedRun:
                 D.lib.krk_event_destroy(e)
 
     def close(self):
-        for b in self.bufs:
+        for b in self.bufs + self.lane_bufs:
             b.free()
-        self.bufs = []
-        for s in (self.gen_s, self.run_s):
+        self.bufs, self.lane_bufs = [], []
+        for s in [self.gen_s, self.run_s] + self.lane_ss:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s = self.run_s = C.c_void_p()
+        self.gen_s, self.run_s, self.lane_ss = C.c_void_p(), C.c_void_p(), []
 
     def __del__(self):
         try:

@@ -35,15 +35,23 @@ def one_shot(gpu):
     return lens, ids, dg, sums, offs, counts
 
 
-@pytest.mark.parametrize("window_gib,cap", [(4, None), (1, 200)])
-def test_windowed_c3_matches_one_shot_and_oracle(one_shot, orc, window_gib, cap):
+@pytest.mark.parametrize("window_gib,cap,lane", [(4, None, None), (1, 200, None), (1, 200, (100, 8))])
+def test_windowed_c3_matches_one_shot_and_oracle(one_shot, orc, window_gib, cap, lane):
+    """lane=(K, T): the K longest blobs go through the host lane (generated into their
+    own device buffer T at a time, piece CRCs on the GPU, SHA-256 on T host threads
+    reading HBM) while the windows run the rest; the last group is partial (100 = 12 x 8
+    + 4) and every result must still match."""
     lens, ids, dg1, sums1, offs1, counts1 = one_shot
-    wr = WindowedRun(D, ids, lens, P, window_gib << 30, cap=cap)
+    wr = WindowedRun(D, ids, lens, P, window_gib << 30, cap=cap, host_lane=lane)
+    if lane:
+        assert len(wr.lane_blobs) == lane[0] and len(wr.lane_groups) == 13
+        assert not set(wr.lane_blobs) & set(np.concatenate([w[0] for w in wr.wins]).tolist())
+        assert min(lens[i] for i in wr.lane_blobs) >= max(lens[int(i)] for w in wr.wins for i in w[0])
     if cap is None:
         assert wr.cap >= N  # production admission: the two-lane cap exceeds this batch
     else:
         live = max(len(w[0]) for w in wr.wins)
-        assert live <= cap < N and len(wr.wins) > 50
+        assert live <= cap < N and len(wr.wins) > (40 if lane else 50)
     wr.run()
     cb = wr.cb
     dg = cb.digests.to_host(np.uint8, 32 * N).reshape(-1, 32)

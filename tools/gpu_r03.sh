@@ -28,6 +28,9 @@ for s in "$@"; do
     bench) step bench 900 python bench.py ;;
     bench20) step bench20 900 python bench.py --steps 20 --warmup 5 ;;
     c3cap) for c in ${CAPS:-16384 13824 12288}; do step bench_c3_cap$c 600 python bench.py --workload c3 --no-cpu-baseline --no-ceiling --live-cap $c || exit 1; done ;;
+    lane) step pytest_lane 300 python -u -m pytest tests/test_gpu_windowed.py -q -rf -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    c3w8lane) step bench_c3_w8_lane 900 python bench.py --workload c3 --no-cpu-baseline --emulate-world 8 --host-lane ;;
+    c3lane) step bench_c3_lane 1100 python bench.py --workload c3 --no-cpu-baseline --host-lane ;;
     c3w8) step bench_c3_w8 600 python bench.py --workload c3 --no-cpu-baseline --emulate-world 8 ;;
     c4pipe) step bench_c4 600 python bench.py --workload c4 ;;
     e2ehyb) step e2e_hybrid 900 env KRK_BENCH_HYBRID=${HYB:-4,8,16} python bench.py --e2e-only --no-cpu-baseline ;;
