@@ -266,12 +266,13 @@ static void teardown_device(Device& D) {
         }
         D.cache.live.clear();
     }
-    for (auto& P : D.slots) {
-        if (P->ev) hipEventSynchronize(P->ev), hipEventDestroy(P->ev);
-        if (P->p) hipHostFree(P->p);
-    }
-    D.slots.clear();
-    D.next_slot = 0;
+    for (auto& R : D.rings)
+        for (PinnedSlot& P : R->slot) {
+            if (P.ev) hipEventSynchronize(P.ev), hipEventDestroy(P.ev);
+            if (P.p) hipHostFree(P.p);
+        }
+    D.rings.clear();
+    D.ring_of.clear();
     for (void* p : D.retired_pinned) hipHostFree(p);
     D.retired_pinned.clear();
     for (void* p : {(void*)D.shard_kb, (void*)D.shard_koff, (void*)D.shard_bad, (void*)D.d_tabs})

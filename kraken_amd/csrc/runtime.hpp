@@ -117,12 +117,24 @@ inline void drain_timing() {
 }
 
 // ------------------------------------------------------------------ device
-constexpr size_t kMaxUploadSlots = 64;
 struct PinnedSlot {
     void* p = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
     bool busy = false;
+};
+// upload()'s pinned slots, one ring per stream (at most kMaxUploadRings; more streams
+// share rings).  A slot's bytes are rewritten only after hipEventSynchronize on its last
+// copy -- never on hipEventQuery's word (skipping slots the query called busy let the C3
+// host-lane test see a CRC pack overwritten before its copy ran: piece sums XOR'd twice,
+// tools/micro/evq_probe.hip).  A ring waits only for its own stream's copies, so a stream
+// held behind a long kernel never holds another stream's uploads.
+constexpr int kRingSlots = 8;
+constexpr size_t kMaxUploadRings = 32;
+struct UploadRing {
+    std::mutex mu;
+    PinnedSlot slot[kRingSlots];
+    unsigned next = 0;
 };
 
 // Stream-ordered device scratch.  Blocks are power-of-two sized and stay with the
@@ -225,9 +237,9 @@ struct Device {
     hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;
     uint32_t* d_tabs = nullptr;
     int crc_variant = 0;
-    std::mutex mu;
-    std::vector<std::unique_ptr<PinnedSlot>> slots;  // upload(): grows while every slot is in flight
-    size_t next_slot = 0;
+    std::mutex mu;  // the ring table and the retired list
+    std::unordered_map<hipStream_t, UploadRing*> ring_of;
+    std::vector<std::unique_ptr<UploadRing>> rings;
     std::vector<void*> retired_pinned;  // grown-out upload buffers (freed at krk_shutdown)
 };
 
@@ -341,41 +353,38 @@ inline int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_
     *d_out = nullptr;
     if (!n) return KRK_OK;
     KRK_HIP(scratch_alloc(D, d_out, n, s));
-    std::lock_guard<std::mutex> g(D->mu);
-    // A slot whose last copy is done.  A copy queued behind a long kernel of its stream
-    // (a C3 window's chunk upload waits for the window before it, ~0.6 s of SHA-256) keeps
-    // its slot busy that long: such slots are skipped and the pool grows instead of
-    // waiting -- waiting here, under the device lock, held every other caller's upload
-    // (the C3 host lane's CRC launches) behind that kernel.
-    PinnedSlot* pick_slot = nullptr;
-    const size_t ns = D->slots.size();
-    for (size_t k = 0; k < ns && !pick_slot; ++k) {
-        PinnedSlot& c = *D->slots[(D->next_slot + k) % ns];
-        if (c.busy && hipEventQuery(c.ev) == hipSuccess) c.busy = false;
-        if (!c.busy) {
-            pick_slot = &c;
-            D->next_slot = (D->next_slot + k + 1) % ns;
+    UploadRing* R = nullptr;
+    {
+        std::lock_guard<std::mutex> g(D->mu);
+        auto it = D->ring_of.find(s);
+        if (it != D->ring_of.end()) {
+            R = it->second;
+        } else {
+            if (D->rings.size() < kMaxUploadRings) D->rings.push_back(std::make_unique<UploadRing>());
+            R = D->rings[D->ring_of.size() % D->rings.size()].get();  // beyond the cap: shared
+            D->ring_of.emplace(s, R);
         }
     }
-    if (!pick_slot && ns < kMaxUploadSlots) {
-        D->slots.push_back(std::make_unique<PinnedSlot>());
-        pick_slot = D->slots.back().get();
+    std::lock_guard<std::mutex> g(R->mu);
+    // The ring's next slot, once its last copy has run (this stream's upload kRingSlots
+    // calls ago, queued before everything this call is about to queue).
+    PinnedSlot& P = R->slot[R->next++ % kRingSlots];
+    if (P.busy) {
+        KRK_HIP(hipEventSynchronize(P.ev));
+        P.busy = false;
     }
-    if (!pick_slot) {  // every slot in flight: wait for the next in turn
-        pick_slot = D->slots[D->next_slot++ % ns].get();
-        KRK_HIP(hipEventSynchronize(pick_slot->ev));
-        pick_slot->busy = false;
-    }
-    PinnedSlot& P = *pick_slot;
     if (!P.ev) KRK_HIP(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming));
     if (P.cap < n) {
         // hipHostFree waits for the whole device (a kernel of another stream included), so
         // a grown slot's old buffer is kept until krk_shutdown: freeing it here held the C3
         // windows' CRC launch back until the window's SHA-256 kernel had ended.
-        if (P.p) D->retired_pinned.push_back(P.p);
+        if (P.p) {
+            std::lock_guard<std::mutex> gd(D->mu);
+            D->retired_pinned.push_back(P.p);
+        }
         P.p = nullptr;  // a failed grow leaves an empty slot, not a dangling one
         P.cap = 0;
-        size_t cap = 1 << 20;
+        size_t cap = 1 << 16;
         while (cap < n) cap <<= 1;
         KRK_HIP(hipHostMalloc(&P.p, cap, hipHostMallocDefault));
         P.cap = cap;
