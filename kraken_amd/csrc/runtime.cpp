@@ -1033,7 +1033,8 @@ static int validate_chunks(const krk_chunk* c, uint64_t n) {
 // One window step over device chunks: SHA jobs on D->s_a, CRC items on D->s_b,
 // both forked from and joined back into s.
 static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
-                       uint8_t* digests_dev, hipStream_t s, ItemBuilder& B) {
+                       uint8_t* digests_dev, hipStream_t s, ItemBuilder& B, hipStream_t ks = nullptr) {
+    if (!ks) ks = D->s_a;
     std::vector<ShaJob> jobs(n);
     CrcBatch items;
     for (uint64_t i = 0; i < n; ++i) {
@@ -1054,11 +1055,11 @@ static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* stat
     KRK_HIP(hipEventCreateWithFlags(&j1, hipEventDisableTiming));
     KRK_HIP(hipEventCreateWithFlags(&j2, hipEventDisableTiming));
     KRK_HIP(hipEventRecord(fork, s));
-    KRK_HIP(hipStreamWaitEvent(D->s_a, fork, 0));
+    KRK_HIP(hipStreamWaitEvent(ks, fork, 0));
     KRK_HIP(hipStreamWaitEvent(D->s_b, fork, 0));
-    int r = run_jobs(D, jobs, digests_dev, state_dev, D->s_a);
+    int r = run_jobs(D, jobs, digests_dev, state_dev, ks);
     if (!r) r = run_items(D, items, sums_dev, D->s_b);
-    hipEventRecord(j1, D->s_a);
+    hipEventRecord(j1, ks);
     hipEventRecord(j2, D->s_b);
     hipStreamWaitEvent(s, j1, 0);
     hipStreamWaitEvent(s, j2, 0);
@@ -1076,6 +1077,17 @@ int krk_metainfo_digest_chunks_dev(const krk_chunk* chunks, uint64_t n, uint32_t
     KRK_CHECK(state_dev && sums_dev && digests_dev, KRK_EINVAL, "chunks_dev: null output");
     ItemBuilder B;
     return chunks_step(D, chunks, n, state_dev, sums_dev, digests_dev, pick(D, stream), B);
+}
+
+int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
+                                      uint8_t* digests_dev, void* stream, void* sha_stream) {
+    KRK_DEVICE(D);
+    int r = validate_chunks(chunks, n);
+    if (r || !n) return r;
+    KRK_CHECK(state_dev && sums_dev && digests_dev, KRK_EINVAL, "chunks_dev: null output");
+    ItemBuilder B;
+    return chunks_step(D, chunks, n, state_dev, sums_dev, digests_dev, pick(D, stream), B,
+                       static_cast<hipStream_t>(sha_stream));
 }
 
 int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {

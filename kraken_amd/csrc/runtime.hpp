@@ -125,10 +125,10 @@ struct PinnedSlot {
 };
 // upload()'s pinned slots, one ring per stream (at most kMaxUploadRings; more streams
 // share rings).  A slot's bytes are rewritten only after hipEventSynchronize on its last
-// copy -- never on hipEventQuery's word (skipping slots the query called busy let the C3
-// host-lane test see a CRC pack overwritten before its copy ran: piece sums XOR'd twice,
-// tools/micro/evq_probe.hip).  A ring waits only for its own stream's copies, so a stream
-// held behind a long kernel never holds another stream's uploads.
+// copy, and a ring waits only for its own stream's copies, so a stream held behind a long
+// kernel (a C3 window's pack copy waits for the window before it, ~0.6 s) never holds
+// another stream's uploads -- the shared pool before it either waited under the device
+// lock or skipped busy slots (hipEventQuery) and grew without bound.
 constexpr int kRingSlots = 8;
 constexpr size_t kMaxUploadRings = 32;
 struct UploadRing {
@@ -277,7 +277,16 @@ inline int init_device(Device& D, int id) {
         const char* m = getenv("KRK_STREAM_MODE");
         const int mode = m ? atoi(m) : 0;
         std::vector<uint32_t> all((D.cus + 31) / 32, 0xFFFFFFFFu);
+        // KRK_SA_PRIO (experiment): s_a (the SHA-256 launches) at another priority, i.e. on
+        // hardware queues of its own: streams of one priority share GPU_MAX_HW_QUEUES queues,
+        // and a copy queued on a stream that shares s_a's queue waits behind its kernel.
+        const char* sp = getenv("KRK_SA_PRIO");
+        const int sa_prio = sp ? atoi(sp) : 0;
+        int least = 0, greatest = 0;
+        if (sa_prio) KRK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         if (mode == 1) KRK_HIP(hipExtStreamCreateWithCUMask(&D.s_a, (uint32_t)all.size(), all.data()));
+        else if (sa_prio)
+            KRK_HIP(hipStreamCreateWithPriority(&D.s_a, hipStreamNonBlocking, sa_prio < 0 ? greatest : least));
         else KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
         if (mode == 1 || mode == 2) KRK_HIP(hipExtStreamCreateWithCUMask(&D.s_b, (uint32_t)all.size(), all.data()));
         else KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));

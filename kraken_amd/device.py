@@ -384,12 +384,13 @@ class ChunkedBatch:
         self.sums.zero()
         self.digests = DeviceBuffer(max(n, 1) * 32)
 
-    def step_arrays(self, blob_idx, ptrs, offsets, lengths, stream=None):
-        """step() from numpy arrays (one window of thousands of chunks, no Python loop)."""
+    def step_arrays(self, blob_idx, ptrs, offsets, lengths, stream=None, sha_stream=None):
+        """step() from numpy arrays (one window of thousands of chunks, no Python loop);
+        sha_stream: the SHA-256 launch's stream (krk_metainfo_digest_chunks_dev_on)."""
         arr = chunk_array(ptrs, offsets, lengths, self.lengths[blob_idx], self.piece_lengths[blob_idx],
                           self.sums_off[blob_idx], blob_idx)
-        check(lib.krk_metainfo_digest_chunks_dev(arr.ctypes.data_as(C.POINTER(krk_chunk)), len(arr), self.state.ptr,
-                                                 self.sums.ptr, self.digests.ptr, stream))
+        check(lib.krk_metainfo_digest_chunks_dev_on(arr.ctypes.data_as(C.POINTER(krk_chunk)), len(arr), self.state.ptr,
+                                                    self.sums.ptr, self.digests.ptr, stream, sha_stream))
 
     def step(self, items, stream=None):
         """items: [(blob index, device address of the chunk, offset, length)]."""

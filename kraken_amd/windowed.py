@@ -136,6 +136,19 @@ def host_lane_plan(D, lens, W, cap, threads, rates=None, min_gain=0.02):
     return k, best, base
 
 
+def lane_groups(lens, k, threads):
+    """The host lane's blobs: the K longest (sorted indices) and the groups of `threads`
+    of them it hashes one after the other, longest first.  The last group stops at K (it
+    once ran on into the window blobs, hashing them too and zeroing the piece sums the
+    windows had accumulated for them)."""
+    L = np.asarray(lens, dtype=np.int64)
+    k = int(min(max(k, 0), L.size))
+    T = max(1, int(threads))
+    order = np.argsort(-L, kind="stable")
+    blobs = np.sort(order[:k]) if k else np.zeros(0, dtype=np.int64)
+    return blobs, [order[g:min(g + T, k)] for g in range(0, k, T)]
+
+
 class WindowedRun:
     """One batch of synthetic blobs (ids, lens, piece length P) streamed through two
     device windows of W bytes: window k+1 is generated on `gen` while window k's
@@ -149,7 +162,7 @@ class WindowedRun:
     double buffers), while the windows run the rest; their digests go into cb.digests at
     the end of run()."""
 
-    def __init__(self, D, ids, lens, P, W, cap=None, host_lane=None, device=0, run_priority=0, lane_priority=0):
+    def __init__(self, D, ids, lens, P, W, cap=None, host_lane=None, device=0, sha_priority=None):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = list(lens)
@@ -160,8 +173,7 @@ class WindowedRun:
         L = np.asarray(self.lens, dtype=np.int64)
         k, self.lane_threads = (host_lane or (0, 0))
         order = np.argsort(-L, kind="stable")
-        self.lane_blobs = np.sort(order[:k]) if k else np.zeros(0, dtype=np.int64)
-        self.lane_groups = [order[g:g + self.lane_threads] for g in range(0, k, max(1, self.lane_threads))]
+        self.lane_blobs, self.lane_groups = lane_groups(L, k, self.lane_threads)
         gpu = np.setdiff1d(np.arange(n), self.lane_blobs) if k else np.arange(n)
         self.cap = window_stream_cap(D, gpu.size) if cap is None else int(cap)
         self.wins = [(gpu[b], o, t) for b, o, t in window_plan(L[gpu], self.W, self.cap)]
@@ -174,22 +186,24 @@ class WindowedRun:
         self.lane_digests = None
         self.lane_seconds = 0.0
         self.cb = D.ChunkedBatch(self.lens, P)
-        # The windows' launches (a SHA-256 launch lasts up to ~0.6 s) go on a stream of
-        # their own priority -- hardware queues of their own -- unless run_priority=0:
-        # the generator's, the host lane's and its D2H copies' work would otherwise wait
-        # behind them in a shared queue (HIP maps streams onto GPU_MAX_HW_QUEUES queues).
-        self.gen_s, self.run_s = C.c_void_p(), C.c_void_p()
+        self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
-        if run_priority:
-            D.check(D.lib.krk_stream_create_prio(int(run_priority), C.byref(self.run_s)))
-        else:
-            D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
+        D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
+        # With the host lane, the windows' SHA-256 launches (up to ~0.6 s each) go on a
+        # high-priority stream, i.e. hardware queues of their own: normal-priority streams
+        # share GPU_MAX_HW_QUEUES queues, and the lane's D2H copies and generator / CRC
+        # launches queued on a stream sharing the SHA launch's queue wait behind it.  Rank
+        # 0's shard of an 8-GPU C3 (tools/lane_probe.py, 480 blobs on 15 threads): lane 24.3
+        # s on the shared queues, 15.75 s with the SHA launches apart.  Without the lane they
+        # stay on the library's stream (a C3 N=1 run measured 553 GB/s there, 499 with its
+        # SHA launches at high priority).
+        if sha_priority is None:
+            sha_priority = -1 if k else 0
+        if sha_priority:
+            D.check(D.lib.krk_stream_create_prio(int(sha_priority), C.byref(self.sha_s)))
         for _ in self.lane_bufs:
             self.lane_ss.append(C.c_void_p())
-            if lane_priority:
-                D.check(D.lib.krk_stream_create_prio(int(lane_priority), C.byref(self.lane_ss[-1])))
-            else:
-                D.check(D.lib.krk_stream_create(C.byref(self.lane_ss[-1])))
+            D.check(D.lib.krk_stream_create(C.byref(self.lane_ss[-1])))
 
     def _items(self, k):
         blobs, offs, take = self.wins[k]
@@ -277,7 +291,8 @@ class WindowedRun:
             D.check(D.lib.krk_event_create(C.byref(e)))
         try:
             for k in range(len(self.wins)):
-                self.cb.step_arrays(cur[0], cur[1], cur[2], cur[3], stream=self.run_s)
+                self.cb.step_arrays(cur[0], cur[1], cur[2], cur[3], stream=self.run_s,
+                                    sha_stream=self.sha_s if self.sha_s.value else None)
                 D.check(D.lib.krk_event_record(evs[k & 1], self.run_s))
                 if k + 1 < len(self.wins):
                     if k:  # window k-1 read buffer (k+1) & 1
@@ -293,10 +308,10 @@ class WindowedRun:
         for b in self.bufs + self.lane_bufs:
             b.free()
         self.bufs, self.lane_bufs = [], []
-        for s in [self.gen_s, self.run_s] + self.lane_ss:
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.lane_ss:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s, self.run_s, self.lane_ss = C.c_void_p(), C.c_void_p(), []
+        self.gen_s, self.run_s, self.sha_s, self.lane_ss = C.c_void_p(), C.c_void_p(), C.c_void_p(), []
 
     def __del__(self):
         try:

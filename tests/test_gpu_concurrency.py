@@ -89,6 +89,73 @@ def test_init_shutdown_reinit(gpu, orc):
     assert L.krk_init(1 << 63) == KRK_ENODEV
 
 
+def test_uploads_behind_a_long_kernel_on_many_streams(gpu):
+    """upload()'s pinned slots (runtime.hpp UploadRing) under the pattern that corrupted the
+    C3 host lane in round 3: a window step whose CRC pack copy waits (on another library
+    stream, behind an event) for a ~0.8 s SHA-256 kernel, while 40 threads on streams of
+    their own (more than the 32 rings: some share) upload piece-sum packs.  Every result
+    must equal the one-shot device run of the same bytes: a slot rewritten before its copy
+    ran would hand a launch another call's work items (piece sums XOR'd twice or missed)."""
+    import ctypes as C
+    import threading
+    P = 1 << 20
+    long_arena = D.BlobArena([48 << 20], P, blob_ids=[901])
+    long_out = D.BatchOutputs(long_arena)
+    # the window step's blobs and every thread's blobs, with their one-shot results
+    win_lens = [(k * 977_777) % (3 << 20) + 1 for k in range(1, 41)]
+    win = D.BlobArena(win_lens, P, blob_ids=range(1000, 1040))
+    wref = D.BatchOutputs(win)
+    D.metainfo_digest(win, wref)
+    thr = [D.BlobArena([(t * 7919 + k * 104_729) % (2 << 20) + 1 for k in range(3)], 1 << 18,
+                       blob_ids=[2000 + 3 * t + k for k in range(3)]) for t in range(40)]
+    tref = []
+    for a in thr:
+        o = D.BatchOutputs(a)
+        D.piece_sums(a, o)
+        tref.append(o)
+    D.synchronize()
+    wsums = wref.sums.to_host(np.uint32, win.total_pieces)
+    wdig = wref.digests.to_host(np.uint8, 32 * len(win_lens))
+    trefs = [o.sums.to_host(np.uint32, a.total_pieces) for a, o in zip(thr, tref)]
+
+    s = C.c_void_p()
+    D.check(D.lib.krk_stream_create(C.byref(s)))
+    cb = D.ChunkedBatch(win_lens, P)
+    errs = []
+
+    def worker(t):
+        try:
+            D.set_device(0)
+            st = C.c_void_p()
+            D.check(D.lib.krk_stream_create(C.byref(st)))
+            out = D.BatchOutputs(thr[t])
+            for _ in range(12):
+                D.piece_sums(thr[t], out, stream=st)
+                D.check(D.lib.krk_stream_sync(st))
+                got = out.sums.to_host(np.uint32, thr[t].total_pieces)
+                if not np.array_equal(got, trefs[t]):
+                    errs.append(f"thread {t}")
+            D.lib.krk_stream_destroy(st)
+        except Exception as e:  # re-raised below
+            errs.append(repr(e))
+
+    try:
+        D.sha256(long_arena, long_out, stream=s)  # ~0.8 s on one stream
+        ptrs = np.uint64(win.buf.ptr) + win.offsets
+        cb.step_arrays(np.arange(len(win_lens)), ptrs, np.zeros(len(win_lens), np.uint64), win.lengths, stream=s)
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(40)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        D.check(D.lib.krk_stream_sync(s))
+    finally:
+        D.lib.krk_stream_destroy(s)
+    assert not errs, errs[:5]
+    assert np.array_equal(cb.sums.to_host(np.uint32, cb.total_pieces), wsums)
+    assert np.array_equal(cb.digests.to_host(np.uint8, 32 * len(win_lens)), wdig)
+
+
 def test_async_d2h_on_two_streams(gpu):
     """krk_memcpy_d2h_async (the C4 back-to-back steps): copies queued on two library streams
     behind piece-sum launches land in pinned arrays once each stream is synchronised, and

@@ -43,3 +43,19 @@ def test_windows_model_is_the_sum_of_window_chains():
     wins = window_plan(L, 1 << 30, 100)
     want = sum(float(t.max()) / 58e6 + 0.0005 for _, _, t in wins)
     assert abs(windows_seconds(BOX, L, 1 << 30, 100) - want) < 1e-9
+
+
+def test_lane_groups_stop_at_k():
+    """The lane hashes groups of `threads` of the K longest blobs; a K that is not a multiple
+    of `threads` leaves a short last group, never blobs past K (the GPU lane test's 100 = 12 x
+    8 + 4 once took the four longest window blobs as well, and their piece sums broke)."""
+    from kraken_amd.windowed import lane_groups
+    L = c3_lengths(1500, scale=16)
+    order = np.argsort(-np.asarray(L), kind="stable")
+    for k, t in [(100, 8), (96, 8), (7, 8), (0, 8), (480, 15), (1500, 7), (2000, 7)]:
+        blobs, groups = lane_groups(L, k, t)
+        kk = min(k, len(L))
+        assert sorted(np.concatenate(groups).tolist() if groups else []) == sorted(order[:kk].tolist())
+        assert blobs.tolist() == sorted(order[:kk].tolist())
+        assert all(len(g) == t for g in groups[:-1]) and (not groups or 1 <= len(groups[-1]) <= t)
+        assert len(groups) == -(-kk // t)

@@ -24,8 +24,8 @@ def main():
     ap.add_argument("--threads", type=int, default=15)
     ap.add_argument("--mode", default="both")
     ap.add_argument("--window-gib", type=int, default=48)
-    ap.add_argument("--prio", type=int, default=0, help="the windows' stream priority (-1 high, 1 low, 0 normal)")
-    ap.add_argument("--lane-prio", type=int, default=0, help="the lane streams' priority")
+    ap.add_argument("--sha-prio", type=int, default=None,
+                    help="the windows' SHA-256 stream priority (-1 high, 1 low, 0 the library's; default: -1 with the lane)")
     a = ap.parse_args()
     D.set_device(0)
     L = c3_lengths(20000)
@@ -39,12 +39,12 @@ def main():
                              host_lane=(a.k, a.threads))
         else:
             wr = WindowedRun(D, ids, lens, 4 << 20, a.window_gib << 30, host_lane=(a.k, a.threads),
-                             run_priority=a.prio, lane_priority=a.lane_prio)
+                             sha_priority=a.sha_prio)
         t0 = time.perf_counter()
         wr.run()
         el = time.perf_counter() - t0
         hb = sum(wr.lens[i] for i in wr.lane_blobs)
-        print(f"{mode}: prio={a.prio} lane_prio={a.lane_prio} K={a.k} T={a.threads}: run {el:.2f} s, "
+        print(f"{mode}: sha_prio={a.sha_prio} K={a.k} T={a.threads}: run {el:.2f} s, "
               f"lane {wr.lane_seconds:.2f} s = "
               f"{hb / wr.lane_seconds / 1e9:.2f} GB/s ({hb / wr.lane_seconds / 1e9 / a.threads:.2f} a thread), "
               f"{len(wr.wins)} windows", flush=True)
