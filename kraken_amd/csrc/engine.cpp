@@ -254,7 +254,8 @@ struct Req {
     bool done = false;
 };
 
-constexpr int kMaxInflight = 3;           // launches per queue on the device at once
+constexpr int kMaxInflight = 8;           // result buffers per queue (launches on the device at once <= this)
+int g_inflight = 3;                       // launches per queue on the device at once (KRK_ENGINE_INFLIGHT)
 // Requests per digester / piece stream in flight (KRK_OWNER_INFLIGHT).  With 512 KiB
 // slots a launch of 256 streams is ~9 ms, so 8 in flight keep ~70 ms of each owner's
 // bytes ahead of the device: an owner whose writer thread was descheduled for a while
@@ -545,7 +546,7 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
         int64_t missing = 0;
         {
             std::unique_lock<std::mutex> lk(Q->mu);
-            Q->cv.wait(lk, [&] { return (Q->stop && Q->q.empty()) || (!Q->q.empty() && Q->inflight.size() < kMaxInflight); });
+            Q->cv.wait(lk, [&] { return (Q->stop && Q->q.empty()) || (!Q->q.empty() && Q->inflight.size() < (size_t)g_inflight); });
             if (Q->q.empty()) {  // stop requested and drained
                 delete f;
                 Q->disp_exited = true;
@@ -618,8 +619,9 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
         }
         f->t_launch = Clock::now();
         if (sha && E->trace)
-            fprintf(stderr, "krk_engine sha t=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
-                    std::chrono::duration<double, std::milli>(f->t_launch - E->t0).count(), f->batch.size(), reason,
+            fprintf(stderr, "krk_engine sha t=%.3fms abs=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
+                    std::chrono::duration<double, std::milli>(f->t_launch - E->t0).count(),
+                    std::chrono::duration<double, std::milli>(f->t_launch.time_since_epoch()).count(), f->batch.size(), reason,
                     depth, queued, (long long)missing, Q->ns_per_byte);
         if (!sha && ++E->crc_launches == E->fail_crc_at) {
             set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
@@ -669,6 +671,9 @@ void completer(Engine* E, Queue* Q, bool sha) {
             f->err = t_err;
         }
         const auto t_done = Clock::now();
+        if (sha && E->trace)
+            fprintf(stderr, "krk_engine sha_done abs=%.3fms n=%zu\n",
+                    std::chrono::duration<double, std::milli>(t_done.time_since_epoch()).count(), f->batch.size());
         if (sha) complete_sha(E, f);
         else complete_crc(E, f);
         {
@@ -707,6 +712,7 @@ int engine_start(Engine* E) {
                                               : getenv("KRK_SLOT_MB") ? (env_size("KRK_SLOT_MB", 2) << 20) : (512u << 10);
     E->pool.init((slot + 63) & ~size_t(63), env_size("KRK_SLOT_POOL_MB", 4096) << 20);
     g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 8));
+    g_inflight = (int)std::min<size_t>(kMaxInflight, std::max<size_t>(1, env_size("KRK_ENGINE_INFLIGHT", 3)));
     E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 30000);
     E->quiet_us = env_size("KRK_SHA_QUIET_US", 3000);
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);

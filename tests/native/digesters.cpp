@@ -93,10 +93,10 @@ int main(int argc, char** argv) {
         const double agg = (double)n * L / el;
         const bool ok = bad.load() == 0;
         all_ok = all_ok && ok;
-        printf("{\"round\": %d, \"digesters\": %d, \"bytes_each\": %zu, \"seconds\": %.4f, \"GBps\": %.3f, "
+        printf("{\"round\": %d, \"t_go_ms\": %.3f, \"digesters\": %d, \"bytes_each\": %zu, \"seconds\": %.4f, \"GBps\": %.3f, "
                "\"MBps_per_stream\": %.2f, \"sha_launches\": %llu, \"streams_per_launch\": %.1f, "
                "\"pinned_bytes\": %llu, \"digests_match\": %s}\n",
-               r, n, L, el, agg / 1e9, agg / n / 1e6, (unsigned long long)(b1[0] - b0[0]),
+               r, std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), n, L, el, agg / 1e9, agg / n / 1e6, (unsigned long long)(b1[0] - b0[0]),
                (double)(b1[1] - b0[1]) / (double)std::max<uint64_t>(1, b1[0] - b0[0]),
                (unsigned long long)b1[4], ok ? "true" : "false");
         fflush(stdout);
