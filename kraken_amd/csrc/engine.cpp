@@ -79,8 +79,11 @@ class SlotPool {
   public:
     size_t S = 0;  // bytes per slot (multiple of 64)
 
-    void init(size_t slot_bytes, size_t cap_bytes) {
+    int numa = -1;  // the node the slots' pinned pages come from (-1: wherever the growing thread runs)
+
+    void init(size_t slot_bytes, size_t cap_bytes, int numa_node = -1) {
         S = slot_bytes;
+        numa = numa_node;
         set_cap(cap_bytes);
     }
 
@@ -198,7 +201,10 @@ class SlotPool {
         void *h = nullptr, *d = nullptr, *hm = nullptr;
         // coherent: the SHA-256 kernel reads a slot straight over PCIe (no H2D copy), and a
         // reused slot must never be served from a stale GPU cache line
-        if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) h = nullptr;
+        on_numa_node(numa, [&] {
+            if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) h = nullptr;
+            else memset(h, 0, bytes);  // first touch on that node
+        });
         if (h && hipHostGetDevicePointer(&hm, h, 0) != hipSuccess) hm = nullptr;
         if (h && hm && hipMalloc(&d, bytes) != hipSuccess) d = nullptr;
         if (!h || !hm || !d) {
@@ -710,7 +716,10 @@ int engine_start(Engine* E) {
     // in flight 8.8-12.6 GB/s, 512 KiB with 8 in flight 11.1-14.2 GB/s (zero-copy).
     const size_t slot = getenv("KRK_SLOT_KB") ? (env_size("KRK_SLOT_KB", 512) << 10)
                                               : getenv("KRK_SLOT_MB") ? (env_size("KRK_SLOT_MB", 2) << 20) : (512u << 10);
-    E->pool.init((slot + 63) & ~size_t(63), env_size("KRK_SLOT_POOL_MB", 4096) << 20);
+    // KRK_SLOT_NUMA: "gpu" = the device's NUMA node, N = node N, unset = no binding
+    int numa = -1;
+    if (const char* nm = getenv("KRK_SLOT_NUMA")) numa = strcmp(nm, "gpu") == 0 ? device_numa_node(E->dev) : atoi(nm);
+    E->pool.init((slot + 63) & ~size_t(63), env_size("KRK_SLOT_POOL_MB", 4096) << 20, numa);
     g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 8));
     g_inflight = (int)std::min<size_t>(kMaxInflight, std::max<size_t>(1, env_size("KRK_ENGINE_INFLIGHT", 3)));
     E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 30000);

@@ -3,6 +3,7 @@
 // (runtime.cpp) and the submission engine (engine.cpp).  Not part of the ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -114,6 +115,58 @@ inline void drain_timing() {
     }
     g_pending.clear();
     hipSetDevice(cur);
+}
+
+// ------------------------------------------------------------------ NUMA
+// NUMA node of device `id` (its PCI function's sysfs entry); -1 if unknown.
+inline int device_numa_node(int id) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, id) != hipSuccess) return -1;
+    for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+    std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return -1;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    return node;
+}
+
+// The CPUs of NUMA node `node` this process may run on (empty if none / unknown).
+inline cpu_set_t numa_node_cpus(int node) {
+    cpu_set_t s, allowed;
+    CPU_ZERO(&s);
+    if (node < 0 || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return s;
+    std::string path = "/sys/devices/system/node/node" + std::to_string(node) + "/cpulist";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return s;
+    char buf[4096] = {0};
+    if (!fgets(buf, sizeof buf, f)) buf[0] = 0;
+    fclose(f);
+    for (char* p = strtok(buf, ",\n"); p; p = strtok(nullptr, ",\n")) {
+        int a = 0, b = 0;
+        const int k = sscanf(p, "%d-%d", &a, &b);
+        if (k < 1) continue;
+        if (k == 1) b = a;
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &allowed)) CPU_SET(c, &s);
+    }
+    return s;
+}
+
+// f() on the calling thread bound to the CPUs of NUMA node `node` (memory it allocates or
+// first touches comes from that node under the default local policy), then the thread's
+// affinity restored.  node < 0, or no allowed CPU there: f() as is.
+template <class F>
+inline void on_numa_node(int node, F&& f) {
+    cpu_set_t want = numa_node_cpus(node), old;
+    if (node < 0 || CPU_COUNT(&want) == 0 || pthread_getaffinity_np(pthread_self(), sizeof old, &old) != 0 ||
+        pthread_setaffinity_np(pthread_self(), sizeof want, &want) != 0) {
+        f();
+        return;
+    }
+    f();
+    pthread_setaffinity_np(pthread_self(), sizeof old, &old);
 }
 
 // ------------------------------------------------------------------ device

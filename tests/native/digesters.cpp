@@ -10,6 +10,7 @@
 // holds its digester until the last digest), streams per SHA launch, and whether every
 // digest equals krk_host_sha256 of the same bytes (the host SHA-NI path, itself checked
 // against hashlib by tests/test_capi_cpu.py).  Exit 1 on any mismatch or error.
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -85,9 +86,31 @@ int main(int argc, char** argv) {
                 krk_digester_free(d);
             });
         while (ready.load() < n) std::this_thread::yield();
+        // DIGESTERS_CLOCK=1: sample the shader clock every ~20 ms during the round
+        // (krk_device_clock_mhz on a stream of its own)
+        std::vector<double> clocks;
+        std::atomic<bool> done{false};
+        std::thread clk;
+        if (getenv("DIGESTERS_CLOCK"))
+            clk = std::thread([&] {
+                krk_set_device(0);
+                void* cs = nullptr;
+                krk_stream_create(&cs);
+                while (!done.load()) {
+                    double m = 0;
+                    if (krk_device_clock_mhz(cs, &m) == KRK_OK) clocks.push_back(m);
+                    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+                }
+                krk_stream_destroy(cs);
+            });
         const auto t0 = std::chrono::steady_clock::now();
         go.store(true, std::memory_order_release);
         for (auto& t : th) t.join();
+        done = true;
+        if (clk.joinable()) clk.join();
+        std::sort(clocks.begin(), clocks.end());
+        const double clk_med = clocks.empty() ? 0.0 : clocks[clocks.size() / 2];
+        const double clk_min = clocks.empty() ? 0.0 : clocks.front();
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         krk_engine_stats(&b1[0], &b1[1], &b1[2], &b1[3], &b1[4]);
         const double agg = (double)n * L / el;
@@ -95,10 +118,10 @@ int main(int argc, char** argv) {
         all_ok = all_ok && ok;
         printf("{\"round\": %d, \"t_go_ms\": %.3f, \"digesters\": %d, \"bytes_each\": %zu, \"seconds\": %.4f, \"GBps\": %.3f, "
                "\"MBps_per_stream\": %.2f, \"sha_launches\": %llu, \"streams_per_launch\": %.1f, "
-               "\"pinned_bytes\": %llu, \"digests_match\": %s}\n",
+               "\"pinned_bytes\": %llu, \"clock_mhz_median\": %.0f, \"clock_mhz_min\": %.0f, \"digests_match\": %s}\n",
                r, std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), n, L, el, agg / 1e9, agg / n / 1e6, (unsigned long long)(b1[0] - b0[0]),
                (double)(b1[1] - b0[1]) / (double)std::max<uint64_t>(1, b1[0] - b0[0]),
-               (unsigned long long)b1[4], ok ? "true" : "false");
+               (unsigned long long)b1[4], clk_med, clk_min, ok ? "true" : "false");
         fflush(stdout);
     }
     return all_ok ? 0 : 1;
