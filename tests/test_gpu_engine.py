@@ -155,23 +155,27 @@ def test_256_concurrent_gpu_digesters(gpu):
 
 def test_256_native_digesters():
     """256 GPU Digesters on 256 native threads (tests/native/
-    digesters.cpp, a C-ABI caller like the cgo layer), 16 MiB each in random writes of up
-    to 1 MiB, every digest equal to the host SHA-256 of the same bytes.  With midstates
-    in HBM rows, launches queued behind the running one and up to 4 requests of a digester
-    in flight, the aggregate reaches >= 13 GB/s (>= 50 MB/s a stream; the batch kernel's
-    per-stream rate is ~59 MB/s)."""
+    digesters.cpp, a C-ABI caller like the cgo layer), 16 MiB each in random writes of up to
+    1 MiB, every digest equal to the host SHA-256 of the same bytes.  With midstates in HBM
+    rows, launches queued behind the running one and up to 8 requests of a digester in
+    flight, a warm round reaches >= 13 GB/s (>= 50 MB/s a stream; the batch kernel's
+    per-stream rate is ~59 MB/s).  The rate is bimodal round to round on the same box
+    (~14.3 and ~11.2 GB/s: every launch of a slow round runs ~11 ms instead of 8.9 at the
+    same shader clock, tools/engine_trace.py), so the best of five warm
+    rounds is asserted, and every warm round above the slow mode's floor."""
     import json
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "digesters")
     assert os.path.exists(exe), "build() compiles tests/native"
-    r = subprocess.run([exe, "256", "16", "3"], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([exe, "256", "16", "6"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     rounds = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     print(rounds)
-    assert len(rounds) == 3 and all(x["digests_match"] for x in rounds)
-    best = max(x["GBps"] for x in rounds[1:])  # round 0 pins the slot pool
-    assert best >= 13.0, rounds
+    assert len(rounds) == 6 and all(x["digests_match"] for x in rounds)
+    warm = [x["GBps"] for x in rounds[1:]]  # round 0 pins the slot pool
+    assert max(warm) >= 13.0, rounds
+    assert min(warm) >= 9.5, rounds
 
 
 @pytest.mark.parametrize("P", [3, 1000, 65536, 3 << 20, 5 << 20, 8 << 20])
