@@ -278,6 +278,9 @@ struct Inflight {
     int out_i = -1;  // the queue's pinned result buffer this launch writes
     uint64_t max_len = 0;
     Clock::time_point t_launch;
+    char reason = '-';                    // trace: why the batch was formed
+    size_t depth = 0, left_queued = 0;    // trace: launches on the device, requests left
+    int64_t missing = 0;
     // SHA: digest rows [row0, row0 + nrows) copied back (final requests)
     uint32_t row0 = 0, nrows = 0;
     // CRC: request i's portion CRCs at base[i] .. base[i + 1] of the results
@@ -292,6 +295,7 @@ struct Queue {
     std::deque<Req*> q;
     std::deque<Inflight*> inflight;   // launch order
     bool stop = false, disp_exited = false;
+    bool dispatching = false;  // a batch is between take_batch and publish (one at a time: stream order = owner order)
     std::thread th, th_done;
     hipStream_t s = nullptr;
     uint8_t* out[kMaxInflight] = {};  // pinned result buffers, grown on demand
@@ -340,6 +344,7 @@ struct Engine {
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
     bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
     bool sha_zero_copy = true;    // SHA jobs read the pinned slots directly (KRK_SHA_ZERO_COPY=0: H2D first)
+    bool caller_runs = true;      // the submission completing a coalescing set launches it (KRK_ENGINE_CALLER_RUNS=0: off)
     Clock::time_point t0 = Clock::now();
     uint64_t crc_launches = 0;
     std::atomic<uint64_t> sha_batches{0}, sha_jobs{0}, crc_batches{0}, crc_reqs{0};
@@ -542,30 +547,111 @@ bool expected_present(const Queue& Q, int64_t live) {
     return Q.missing == 0;
 }
 
+// With Q->mu held and no dispatch in progress: the next batch (SHA: the oldest request of
+// each owner, FIFO -- its state row chains through the launches, which run one after the
+// other on the queue's stream; CRC: up to kMaxCrcBatchBytes), marked as being dispatched.
+Inflight* take_batch(Queue* Q, bool sha, char reason) {
+    auto* f = new Inflight();
+    if (sha) {
+        std::unordered_set<const void*> seen;
+        for (auto it = Q->q.begin(); it != Q->q.end() && f->batch.size() < kStateRows;) {
+            if (seen.insert((*it)->owner).second) {
+                Req* r = *it;
+                f->batch.push_back(r);
+                own_update(*Q, r->owner, [&](Queue::Own& w) {
+                    --w.queued;
+                    if (r->final) w.closed = true;
+                });
+                it = Q->q.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    } else {
+        uint64_t bytes = 0;
+        while (!Q->q.empty() && (f->batch.empty() || bytes + Q->q.front()->len <= kMaxCrcBatchBytes)) {
+            bytes += Q->q.front()->len;
+            f->batch.push_back(Q->q.front());
+            Q->q.pop_front();
+        }
+    }
+    f->reason = reason;
+    f->depth = Q->inflight.size();
+    f->left_queued = Q->q.size();
+    f->missing = Q->missing;
+    for (int i = 0; i < kMaxInflight; ++i)
+        if (!Q->out_busy[i]) {
+            Q->out_busy[i] = true;
+            f->out_i = i;
+            break;
+        }
+    Q->dispatching = true;
+    return f;
+}
+
+// Without the lock: launch f on the queue's stream and record its completion event.
+void launch_batch(Engine* E, Queue* Q, Inflight* f, bool sha) {
+    hipSetDevice(E->dev);  // a caller's thread may run this (submit)
+    f->t_launch = Clock::now();
+    if (sha && E->trace)
+        fprintf(stderr, "krk_engine sha t=%.3fms abs=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
+                std::chrono::duration<double, std::milli>(f->t_launch - E->t0).count(),
+                std::chrono::duration<double, std::milli>(f->t_launch.time_since_epoch()).count(), f->batch.size(),
+                f->reason, f->depth, f->left_queued, (long long)f->missing, Q->ns_per_byte);
+    if (!sha && ++E->crc_launches == E->fail_crc_at) {
+        set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
+                  (unsigned long long)E->crc_launches);
+        f->rc = KRK_EHIP;
+    } else {
+        f->rc = sha ? launch_sha(E, f) : launch_crc(E, f);
+    }
+    if (!f->rc) {
+        if (hipEventCreateWithFlags(&f->done, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(f->done, Q->s) != hipSuccess) {
+            set_error(KRK_EHIP, "engine: launch event");
+            f->rc = KRK_EHIP;
+        }
+    }
+    if (f->rc) f->err = t_err;
+}
+
+// With Q->mu held: f joins the launches on the device; the next dispatch may start.
+void publish(Queue* Q, Inflight* f, bool sha) {
+    if (sha) {
+        for (const Req* r : f->batch)
+            if (!r->final) own_update(*Q, r->owner, [](Queue::Own& w) { ++w.flying; });
+        const auto start = std::max(f->t_launch, Q->inflight.empty() ? f->t_launch : Q->due);
+        Q->due = start + std::chrono::nanoseconds((int64_t)(Q->ns_per_byte * (double)f->max_len));
+    }
+    Q->inflight.push_back(f);
+    Q->dispatching = false;
+}
+
 void dispatcher(Engine* E, Queue* Q, bool sha) {
     hipSetDevice(E->dev);
     t_dev = E->dev;
     for (;;) {
-        auto* f = new Inflight();
-        char reason = '-';
-        size_t depth = 0, queued = 0;
-        int64_t missing = 0;
+        Inflight* f = nullptr;
         {
             std::unique_lock<std::mutex> lk(Q->mu);
-            Q->cv.wait(lk, [&] { return (Q->stop && Q->q.empty()) || (!Q->q.empty() && Q->inflight.size() < (size_t)g_inflight); });
+            Q->cv.wait(lk, [&] {
+                return (Q->stop && Q->q.empty() && !Q->dispatching) ||
+                       (!Q->q.empty() && !Q->dispatching && Q->inflight.size() < (size_t)g_inflight);
+            });
             if (Q->q.empty()) {  // stop requested and drained
-                delete f;
                 Q->disp_exited = true;
                 Q->cv_done.notify_all();
                 return;
             }
+            char reason = '-';
             if (sha) {
                 // Coalesce: on an idle device the first request waits coalesce_us for
                 // company; behind running launches, the next batch is formed once every
                 // owner with requests on the device has its next request queued, or ~1 ms
                 // before the last launch is due to end.  (Forming it as soon as SOME owners
                 // are back splits the owners into groups that alternate between launches:
-                // each would then run at a fraction of the per-stream rate.)
+                // each would then run at a fraction of the per-stream rate.)  The submission
+                // that completes the set usually launches the batch itself (submit()).
                 reason = 'T';
                 for (;;) {
                     if (Q->stop || expected_present(*Q, E->live_digesters.load(std::memory_order_relaxed))) {  // every owner on the device is back
@@ -583,77 +669,19 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                             : Q->due - std::chrono::milliseconds(1);
                     if (Clock::now() >= until) break;
                     Q->cv.wait_until(lk, until);
-                    if (Q->q.empty()) break;
+                    if (Q->q.empty() || Q->dispatching) break;
                 }
-                if (Q->q.empty()) {
-                    delete f;
-                    continue;
-                }
-                // FIFO, the oldest request of each owner (its state row chains through
-                // the launches, which run one after the other on the queue's stream)
-                std::unordered_set<const void*> seen;
-                for (auto it = Q->q.begin(); it != Q->q.end() && f->batch.size() < kStateRows;) {
-                    if (seen.insert((*it)->owner).second) {
-                        Req* r = *it;
-                        f->batch.push_back(r);
-                        own_update(*Q, r->owner, [&](Queue::Own& w) {
-                            --w.queued;
-                            if (r->final) w.closed = true;
-                        });
-                        it = Q->q.erase(it);
-                    } else {
-                        ++it;
-                    }
-                }
-            } else {
-                uint64_t bytes = 0;
-                while (!Q->q.empty() && (f->batch.empty() || bytes + Q->q.front()->len <= kMaxCrcBatchBytes)) {
-                    bytes += Q->q.front()->len;
-                    f->batch.push_back(Q->q.front());
-                    Q->q.pop_front();
-                }
+                // a caller dispatched meanwhile, or took every request
+                if (Q->q.empty() || Q->dispatching || Q->inflight.size() >= (size_t)g_inflight) continue;
             }
-            depth = Q->inflight.size();
-            queued = Q->q.size();
-            missing = Q->missing;
-            for (int i = 0; i < kMaxInflight; ++i)
-                if (!Q->out_busy[i]) {
-                    Q->out_busy[i] = true;
-                    f->out_i = i;
-                    break;
-                }
+            f = take_batch(Q, sha, reason);
         }
-        f->t_launch = Clock::now();
-        if (sha && E->trace)
-            fprintf(stderr, "krk_engine sha t=%.3fms abs=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
-                    std::chrono::duration<double, std::milli>(f->t_launch - E->t0).count(),
-                    std::chrono::duration<double, std::milli>(f->t_launch.time_since_epoch()).count(), f->batch.size(), reason,
-                    depth, queued, (long long)missing, Q->ns_per_byte);
-        if (!sha && ++E->crc_launches == E->fail_crc_at) {
-            set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
-                      (unsigned long long)E->crc_launches);
-            f->rc = KRK_EHIP;
-        } else {
-            f->rc = sha ? launch_sha(E, f) : launch_crc(E, f);
-        }
-        if (!f->rc) {
-            if (hipEventCreateWithFlags(&f->done, hipEventDisableTiming) != hipSuccess ||
-                hipEventRecord(f->done, Q->s) != hipSuccess) {
-                set_error(KRK_EHIP, "engine: launch event");
-                f->rc = KRK_EHIP;
-            }
-        }
-        if (f->rc) f->err = t_err;
+        launch_batch(E, Q, f, sha);
         {
             std::lock_guard<std::mutex> g(Q->mu);
-            if (sha) {
-                for (const Req* r : f->batch)
-                    if (!r->final) own_update(*Q, r->owner, [](Queue::Own& w) { ++w.flying; });
-                const auto start = std::max(f->t_launch, Q->inflight.empty() ? f->t_launch : Q->due);
-                Q->due = start + std::chrono::nanoseconds((int64_t)(Q->ns_per_byte * (double)f->max_len));
-            }
-            Q->inflight.push_back(f);
+            publish(Q, f, sha);
         }
+        Q->cv.notify_all();
         Q->cv_done.notify_one();
     }
 }
@@ -727,6 +755,7 @@ int engine_start(Engine* E) {
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
     E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
     if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->sha_zero_copy = atoi(z) != 0;
+    if (const char* c = getenv("KRK_ENGINE_CALLER_RUNS")) E->caller_runs = atoi(c) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
     KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));
     KRK_HIP(hipStreamCreateWithFlags(&E->s_copy, hipStreamNonBlocking));
@@ -787,17 +816,39 @@ int stage(Engine* E, Req* r) {
     return KRK_OK;
 }
 
-void submit(Queue& Q, Req* r) {
+// Queue r.  On the SHA queue, the submission that completes the coalescing set (every
+// owner with requests on the device has its next one queued; on an idle device, every
+// live GPU digester has one) launches the batch on its own thread: with many writer
+// threads busy filling slots, the dispatcher thread could wait tens of milliseconds for a
+// CPU while the device idled (tools/engine_slow.py: slow rounds' first launch formed ~90
+// ms after their requests were all queued).  The dispatcher still forms the batches that
+// coalescing times out on.
+void submit(Engine* E, Queue& Q, Req* r) {
     r->t_submit = Clock::now();
+    Inflight* f = nullptr;
     {
         std::lock_guard<std::mutex> g(Q.mu);
         Q.q.push_back(r);
-        if (Q.coalesce)
+        if (Q.coalesce) {
             own_update(Q, r->owner, [&](Queue::Own& w) {
                 if (w.queued == 0 && w.flying == 0) Q.last_arrival = r->t_submit;
                 ++w.queued;
                 w.closed = false;
             });
+            if (E->caller_runs && !Q.dispatching && !Q.stop && Q.inflight.size() < (size_t)g_inflight &&
+                expected_present(Q, E->live_digesters.load(std::memory_order_relaxed)))
+                f = take_batch(&Q, true, 'C');
+        }
+    }
+    if (f) {
+        const std::string keep = t_err;  // the launch's error text belongs to its requests
+        launch_batch(E, &Q, f, true);
+        t_err = keep;
+        {
+            std::lock_guard<std::mutex> g(Q.mu);
+            publish(&Q, f, true);
+        }
+        Q.cv_done.notify_one();
     }
     Q.cv.notify_all();
 }
@@ -963,8 +1014,19 @@ int digester_drain(krk_digester* d, size_t keep) {
 
 // Submit `len` bytes: from the slot `sl` the digester filled in place (handed over to the
 // request), else copied from `src` into a fresh slot.
+// KRK_ENGINE_TRACE: one stderr line for a submission step that held its caller > 5 ms.
+void trace_slow(Engine* E, const char* what, Clock::time_point t0) {
+    const double ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    if (E->trace && ms > 5.0)
+        fprintf(stderr, "krk_engine slow %s %.2fms abs=%.3fms\n", what, ms,
+                std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count());
+}
+
 int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool final, Slot* sl = nullptr) {
+    auto t0 = Clock::now();
     int rc = digester_drain(d, g_owner_inflight - 1);
+    trace_slow(d->E, "drain", t0);
+    t0 = Clock::now();
     if (rc) {
         d->E->pool.release(sl);
         return rc;
@@ -985,13 +1047,14 @@ int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool fina
         rc = make_req(d->E, src, len, &r, h2d);
         if (rc) return rc;
     }
+    trace_slow(d->E, sl ? "stage" : "make_req", t0);
     r->owner = d;
     r->w = &d->w;
     r->row = d->row;
     r->prefix = d->submitted;
     r->final = final;
     d->inflight.push_back(r);
-    submit(d->E->sha, r);
+    submit(d->E, d->E->sha, r);
     if (!final) d->submitted += len;
     return KRK_OK;
 }
@@ -1070,7 +1133,11 @@ int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
             n -= S;
             continue;
         }
-        if (d->fill == 0 && !d->cur) d->cur = E->pool.try_acquire(E->pool.reserve());
+        if (d->fill == 0 && !d->cur) {
+            const auto t0 = Clock::now();
+            d->cur = E->pool.try_acquire(E->pool.reserve());
+            trace_slow(E, "try_acquire", t0);
+        }
         uint8_t* dst;
         if (d->cur) {
             dst = d->cur->host;
@@ -1079,7 +1146,9 @@ int krk_digester_write(krk_digester* d, const uint8_t* buf, uint64_t n) {
             dst = d->pend.get();
         }
         const size_t take = std::min<uint64_t>(n, S - d->fill);
+        const auto tc = Clock::now();
         memcpy(dst + d->fill, buf, take);
+        trace_slow(E, d->cur ? "memcpy_slot" : "memcpy_pend", tc);
         d->fill += take;
         buf += take;
         n -= take;
@@ -1221,7 +1290,7 @@ int stream_submit(krk_piece_stream* s, const uint8_t* src, uint64_t len) {
     r->on_done = stream_fold;
     r->ctx = s;
     s->inflight.push_back(r);
-    submit(s->E->crc, r);
+    submit(s->E, s->E->crc, r);
     s->submitted += len;
     return KRK_OK;
 }
@@ -1344,7 +1413,7 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
         r->off = off;
         r->P = 0;
         reqs.push_back(r);
-        submit(E->crc, r);
+        submit(E, E->crc, r);
     }
     for (Req* r : reqs) retire(r);
     if (!rc) *out = c;

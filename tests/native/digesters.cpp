@@ -17,6 +17,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <pthread.h>
+
 #include <random>
 #include <thread>
 #include <vector>
@@ -54,24 +56,25 @@ int main(int argc, char** argv) {
     for (int r = 0; r < rounds; ++r) {
         uint64_t b0[5], b1[5];
         krk_engine_stats(&b0[0], &b0[1], &b0[2], &b0[3], &b0[4]);
-        // start line: every thread holds its digester, then all are released at once
-        // (an atomic flag, not a condition variable: waking 256 waiters one mutex handoff
-        // at a time took ~15 ms, which the timed region would have charged to the engine)
-        std::atomic<int> ready{0};
-        std::atomic<bool> go{false};
+        // start line: every thread holds its digester, then all are released at once by a
+        // barrier (one futex wake for all; a condition variable woke 256 waiters one mutex
+        // handoff at a time, ~15 ms).  Not a spin on a flag: the GPU boxes grant a CPU
+        // QUOTA (16 CPUs' worth) over many more CPUs, and 256 threads spinning on yield()
+        // burnt it, so the whole process was throttled for the rest of the quota period
+        // (~90 ms stalls in a third of the rounds: tools/engine_slow.py).
+        pthread_barrier_t start;
+        pthread_barrier_init(&start, nullptr, (unsigned)n + 1);
         std::atomic<int> bad{0};
         std::vector<std::thread> th;
         for (int i = 0; i < n; ++i)
             th.emplace_back([&, i] {
                 krk_set_device(0);
                 krk_digester* d = nullptr;
-                if (krk_digester_new_on(KRK_PLACE_GPU, &d) != KRK_OK) {
-                    bad.fetch_add(1);
-                    return;
-                }
+                const bool made = krk_digester_new_on(KRK_PLACE_GPU, &d) == KRK_OK;
+                if (!made) bad.fetch_add(1);
                 std::mt19937_64 rg(i * 7919 + r);
-                ready.fetch_add(1);
-                while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+                pthread_barrier_wait(&start);  // every thread arrives, made or not
+                if (!made) return;
                 const uint8_t* p = base.data() + (size_t)i * 4096;
                 for (size_t pos = 0; pos < L;) {
                     const size_t k = std::min<size_t>(L - pos, 1 + rg() % maxw);
@@ -85,7 +88,7 @@ int main(int argc, char** argv) {
                 if (krk_digester_sum(d, out) != KRK_OK || memcmp(out, want[i].data(), 32) != 0) bad.fetch_add(1);
                 krk_digester_free(d);
             });
-        while (ready.load() < n) std::this_thread::yield();
+
         // DIGESTERS_CLOCK=1: sample the shader clock every ~20 ms during the round
         // (krk_device_clock_mhz on a stream of its own)
         std::vector<double> clocks;
@@ -104,8 +107,9 @@ int main(int argc, char** argv) {
                 krk_stream_destroy(cs);
             });
         const auto t0 = std::chrono::steady_clock::now();
-        go.store(true, std::memory_order_release);
+        pthread_barrier_wait(&start);  // the last arrival releases every thread
         for (auto& t : th) t.join();
+        pthread_barrier_destroy(&start);
         done = true;
         if (clk.joinable()) clk.join();
         std::sort(clocks.begin(), clocks.end());

@@ -159,10 +159,11 @@ def test_256_native_digesters():
     1 MiB, every digest equal to the host SHA-256 of the same bytes.  With midstates in HBM
     rows, launches queued behind the running one and up to 8 requests of a digester in
     flight, a warm round reaches >= 13 GB/s (>= 50 MB/s a stream; the batch kernel's
-    per-stream rate is ~59 MB/s).  The rate is bimodal round to round on the same box
-    (~14.3 and ~11.2 GB/s: every launch of a slow round runs ~11 ms instead of 8.9 at the
-    same shader clock, tools/engine_trace.py), so the best of five warm
-    rounds is asserted, and every warm round above the slow mode's floor."""
+    per-stream rate is ~59 MB/s).  Warm rounds measure 13.2-14.4 GB/s; before the harness
+    started its threads on a barrier (it spun them on yield(), which burnt the box's CPU
+    quota and throttled the process ~90 ms in a third of the rounds) they
+    were bimodal, so the best of five warm rounds is asserted, and every warm round well
+    above the throttled mode."""
     import json
     import os
     import subprocess
@@ -175,7 +176,7 @@ def test_256_native_digesters():
     assert len(rounds) == 6 and all(x["digests_match"] for x in rounds)
     warm = [x["GBps"] for x in rounds[1:]]  # round 0 pins the slot pool
     assert max(warm) >= 13.0, rounds
-    assert min(warm) >= 9.5, rounds
+    assert min(warm) >= 11.0, rounds
 
 
 @pytest.mark.parametrize("P", [3, 1000, 65536, 3 << 20, 5 << 20, 8 << 20])
