@@ -944,10 +944,10 @@ std::atomic<int64_t> g_live_digesters{0};
 std::atomic<int64_t> g_host_streams{-1};  // -1: default (host threads x per-stream rate ratio)
 
 unsigned host_threads() {
-    // the CPUs this process may use (affinity); the GPU boxes grant a 16-CPU share
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof set, &set) == 0) return std::max(1, CPU_COUNT(&set));
-    return std::max(1u, std::thread::hardware_concurrency());
+    // the CPUs this process may use: affinity AND the cgroup's CPU quota (the GPU boxes
+    // grant 16 CPUs' worth of quota over an affinity of 256 CPUs; counting the affinity
+    // alone kept AUTO digesters on the host up to 10,240 live instead of 640)
+    return (unsigned)std::max(1, host_cpu_budget());
 }
 
 // Live digesters up to which new ones run on their caller's thread: where the host's
