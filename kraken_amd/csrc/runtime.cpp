@@ -516,7 +516,14 @@ int krk_metainfo_batch_dev(const krk_blob* blobs, uint64_t n_blobs, const char* 
         ns[i] = krk_num_pieces(blobs[i].length, blobs[i].piece_length);
         total += blobs[i].length;
     }
-    const uint64_t G = std::min<uint64_t>(n_blobs, 8);
+    // Four groups (KRK_REGEN_GROUPS): C5 regen 9.84-9.90 ms a step against 10.14-10.16
+    // with eight (each launch's ramp and tail cost more than the InfoHash overlap buys) and
+    // 9.70-10.07 with one (profiles/r03/regen_groups_ab.txt).
+    static const uint64_t kGroups = [] {
+        const char* g = getenv("KRK_REGEN_GROUPS");
+        return (uint64_t)std::max(1, g ? atoi(g) : 4);
+    }();
+    const uint64_t G = std::min<uint64_t>(n_blobs, kGroups);
     std::vector<uint64_t> cut{0};
     for (uint64_t i = 0, acc = 0; i < n_blobs && cut.size() < G; ++i) {
         acc += blobs[i].length;
