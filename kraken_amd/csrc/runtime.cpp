@@ -1167,6 +1167,13 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
             if (t.joinable()) t.join();
         }
     } joiner{host_th};
+    // The copy threads and the offload's threads share the process's CPU budget: above it
+    // a CPU quota throttles the whole process.
+    struct ShareGuard {
+        int saved;
+        ~ShareGuard() { t_host_share = saved; }
+    } share_guard{t_host_share};
+    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - offload_threads());
     ItemBuilder B;
     uint64_t remaining = n_gpu;
     int k = 0;
