@@ -1733,6 +1733,8 @@ int krk_stream_create_prio(int priority, void** out) {
     return KRK_OK;
 }
 int krk_stream_destroy(void* s) {
+    int drc = KRK_OK;
+    if (Device* D = device(&drc)) forget_stream(D, static_cast<hipStream_t>(s));
     KRK_HIP(hipStreamDestroy(static_cast<hipStream_t>(s)));
     return KRK_OK;
 }

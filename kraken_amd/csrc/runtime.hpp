@@ -174,6 +174,7 @@ struct PinnedSlot {
     void* p = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
+    hipStream_t s_last = nullptr;  // the stream the last copy (and ev) went on
     bool busy = false;
 };
 // upload()'s pinned slots, one ring per stream (at most kMaxUploadRings; more streams
@@ -454,8 +455,48 @@ inline int upload(Device* D, const void* src, size_t n, void** d_out, hipStream_
     memcpy(P.p, src, n);
     KRK_HIP(hipMemcpyAsync(*d_out, P.p, n, hipMemcpyHostToDevice, s));
     KRK_HIP(hipEventRecord(P.ev, s));
+    P.s_last = s;
     P.busy = true;
     return KRK_OK;
+}
+
+// Before a stream the library has used is destroyed (krk_stream_destroy): its work is
+// waited for, and every library event last recorded on it -- upload slots, idle scratch
+// blocks -- is replaced by a fresh one.  HIP keeps a reference to the stream in an event
+// it recorded; a later hipEventSynchronize / hipStreamWaitEvent on such an event after the
+// stream was destroyed failed with "operation not permitted when stream is capturing"
+// (the GPU suite once the C3 windows' and the concurrency test's streams came and went).
+inline void forget_stream(Device* D, hipStream_t s) {
+    if (!s) return;
+    hipStreamSynchronize(s);
+    std::vector<UploadRing*> rings;
+    {
+        std::lock_guard<std::mutex> g(D->mu);
+        D->ring_of.erase(s);
+        for (auto& R : D->rings) rings.push_back(R.get());
+    }
+    for (UploadRing* R : rings) {
+        std::lock_guard<std::mutex> g(R->mu);
+        for (PinnedSlot& P : R->slot)
+            if (P.s_last == s) {
+                if (P.ev) hipEventDestroy(P.ev);
+                P.ev = nullptr;  // re-created at the slot's next use
+                P.s_last = nullptr;
+                P.busy = false;
+            }
+    }
+    std::lock_guard<std::mutex> g(D->cache.mu);
+    for (auto& kv : D->cache.idle) {
+        DevCache::Blk& b = kv.second;
+        if (b.s != s) continue;
+        hipEvent_t fresh = nullptr;
+        if (hipEventCreateWithFlags(&fresh, hipEventDisableTiming) == hipSuccess) {
+            hipEventDestroy(b.ev);
+            b.ev = fresh;
+        }
+        b.pending = false;  // its stream's work is done
+        b.s = nullptr;
+    }
 }
 
 // ------------------------------------------------------------------ CRC items

@@ -1533,6 +1533,7 @@ static hipError_t launch_w8(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_di
     });
     if (attr_err != hipSuccess) return attr_err;
     constexpr uint32_t per = 8u * kGroups;
+    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
     hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * kGroups), lds, s, jobs, n_jobs, out_digest,
                        out_state);
     return hipGetLastError();
@@ -1551,6 +1552,7 @@ static hipError_t launch_ws(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_di
     });
     if (attr_err != hipSuccess) return attr_err;
     constexpr uint32_t per = (kTwo ? 32u : 64u) * kGroups;
+    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
     hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * kGroups), lds, s, jobs, n_jobs, out_digest,
                        out_state);
     return hipGetLastError();
@@ -1578,6 +1580,7 @@ hipError_t launch_sha256_plan(int plan, const ShaJob* jobs, uint32_t n_jobs, uin
         // diagnostics (WRONG digests except 100): rounds-only consumer (102 one lane, 104 two
         // lanes), producer-only (105 / 106), producer without global loads (107)
         case 100:
+            (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
             hipLaunchKernelGGL(sha256_multi_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, s, jobs, n_jobs,
                                out_digest, out_state);
             return hipGetLastError();
@@ -1607,6 +1610,7 @@ __global__ void __launch_bounds__(256) digest_scatter_kernel(const uint8_t* __re
 
 hipError_t launch_digest_scatter(const uint8_t* rec, uint32_t n, uint8_t* digests, hipStream_t s) {
     if (!n) return hipSuccess;
+    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
     hipLaunchKernelGGL(digest_scatter_kernel, dim3((n * 32 + 255) / 256), dim3(256), 0, s, rec, n, digests);
     return hipGetLastError();
 }
