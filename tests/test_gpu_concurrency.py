@@ -90,10 +90,10 @@ def test_init_shutdown_reinit(gpu, orc):
 
 
 def test_uploads_behind_a_long_kernel_on_many_streams(gpu):
-    """upload()'s pinned slots (runtime.hpp UploadRing) under the pattern that corrupted the
-    C3 host lane in round 3: a window step whose CRC pack copy waits (on another library
-    stream, behind an event) for a ~0.8 s SHA-256 kernel, while 40 threads on streams of
-    their own (more than the 32 rings: some share) upload piece-sum packs.  Every result
+    """upload()'s pinned slots (runtime.hpp UploadRing) when one stream's copies wait: a
+    window step whose CRC pack copy waits (on another library stream, behind an event) for
+    a ~0.8 s SHA-256 kernel, while 40 threads on streams of their own (more than the 32
+    rings: some share) upload piece-sum packs, then destroy their streams.  Every result
     must equal the one-shot device run of the same bytes: a slot rewritten before its copy
     ran would hand a launch another call's work items (piece sums XOR'd twice or missed)."""
     import ctypes as C
@@ -180,3 +180,32 @@ def test_async_d2h_on_two_streams(gpu):
     finally:
         for st in streams:
             D.lib.krk_stream_destroy(st)
+
+
+def test_streams_come_and_go(gpu):
+    """Library streams created, used and destroyed one after another (what every
+    WindowedRun does): the library's events last recorded on a destroyed stream (upload
+    slots, idle scratch blocks) are replaced before it goes (krk_stream_destroy), so later
+    calls on other streams -- and a kernel launch on the default stream -- neither wait on
+    nor report the dead stream ("operation not permitted when stream is capturing" once)."""
+    import ctypes as C
+    from kraken_amd import hrw
+    arena = D.BlobArena([(1 << 20) + 17, 333, 5 << 18], 1 << 18, blob_ids=[41, 42, 43])
+    ref = D.BatchOutputs(arena)
+    D.piece_sums(arena, ref)
+    D.synchronize()
+    want = ref.sums.to_host(np.uint32, arena.total_pieces)
+    out = D.BatchOutputs(arena)
+    for k in range(60):
+        st = C.c_void_p()
+        D.check(D.lib.krk_stream_create(C.byref(st)) if k % 2 else D.lib.krk_stream_create_prio(-1, C.byref(st)))
+        D.piece_sums(arena, out, stream=st)
+        D.check(D.lib.krk_stream_destroy(st))  # no sync first: destroy waits for the stream's work
+        assert np.array_equal(out.sums.to_host(np.uint32, arena.total_pieces), want), k
+        D.piece_sums(arena, out)  # the default stream, reusing the dead stream's blocks
+        D.synchronize()
+        assert np.array_equal(out.sums.to_host(np.uint32, arena.total_pieces), want), k
+    rh = hrw.NewRendezvousHash()
+    for i in range(4):
+        rh.AddNode(f"n{i}", 100)
+    assert len(rh.GetOrderedNodes("abcd", 3)) == 3  # a launch after all of it reports no stale error
