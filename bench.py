@@ -844,7 +844,7 @@ def run_chunked(a, D, T, rank, world, res):
     ids, lens, P = workload_blobs(a.workload, rank, shard_world, a.blobs)
     n = len(lens)
     wr = WindowedRun(D, ids, lens, P, a.window_gib << 30,
-                     cap=n if a.no_admission else (a.live_cap or None))
+                     cap=n if a.no_admission else (a.live_cap or None), cu_split=a.cu_split)
     T.barrier()
     with D.KernelTimer():
         t0 = time.perf_counter()
@@ -1155,6 +1155,8 @@ def main():
                     help="C3: also run the batch with the host lane (the longest blobs hashed on host threads "
                          "while the windows run the rest), reported as host_offload beside the GPU-only value")
     ap.add_argument("--host-lane-k", type=int, default=-1, help="C3: blobs the host lane takes (-1 = the planner's)")
+    ap.add_argument("--cu-split", action="store_true",
+                    help="C3: the window generator on an eighth of the CUs, the SHA-256 launches on the rest")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
     ap.add_argument("--regen-serial", action="store_true",
                     help="c5regen: piece sums then InfoHashes (no krk_metainfo_batch_dev pipelining)")

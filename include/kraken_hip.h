@@ -398,6 +398,12 @@ int krk_stream_create(void** out);
  * long kernels (a C3 window's SHA-256 launch runs ~0.6 s) is kept off the queues the
  * short work shares, which would otherwise wait behind it. */
 int krk_stream_create_prio(int priority, void** out);
+/* A stream whose kernels run only on the CUs set in `mask` (bit i of word i/32 = CU i of
+ * the device; n_words 32-bit words).  A C3 window generator masked to the CUs the SHA-256
+ * launch leaves free no longer takes issue slots from the SHA waves. */
+int krk_stream_create_cu_mask(const uint32_t* mask, uint32_t n_words, void** out);
+/* CUs of the calling thread's device. */
+int krk_device_cus(int* out);
 int krk_stream_destroy(void* s);
 int krk_stream_sync(void* s);
 /* Events (a window loop waits for ONE earlier window's kernels while the next

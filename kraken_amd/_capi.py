@@ -139,6 +139,8 @@ def _load() -> C.CDLL:
         "krk_memcpy_d2h_async": (i, [vp, vp, C.c_uint64, vp]),
         "krk_stream_create": (i, [C.POINTER(vp)]),
         "krk_stream_create_prio": (i, [i, C.POINTER(vp)]),
+        "krk_stream_create_cu_mask": (i, [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(vp)]),
+        "krk_device_cus": (i, [C.POINTER(i)]),
         "krk_stream_destroy": (i, [vp]),
         "krk_stream_sync": (i, [vp]),
         "krk_event_create": (i, [C.POINTER(vp)]),

@@ -1720,6 +1720,21 @@ int krk_stream_create(void** out) {
     *out = s;
     return KRK_OK;
 }
+int krk_stream_create_cu_mask(const uint32_t* mask, uint32_t n_words, void** out) {
+    KRK_CHECK(out && mask && n_words, KRK_EINVAL, "stream_create_cu_mask: null argument");
+    KRK_DEVICE(D);
+    (void)D;
+    hipStream_t s;
+    KRK_HIP(hipExtStreamCreateWithCUMask(&s, n_words, mask));
+    *out = s;
+    return KRK_OK;
+}
+int krk_device_cus(int* out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    *out = D->cus;
+    return KRK_OK;
+}
 int krk_stream_create_prio(int priority, void** out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_DEVICE(D);
