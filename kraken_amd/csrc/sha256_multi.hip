@@ -170,8 +170,11 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
 // 4 slots) or kSlots2 slots (two lanes per stream, where each producer step
 // builds two blocks), see produce_step.
 constexpr int kSlots = 4;
-constexpr int kSlots2 = 6;           // two lanes: block positions in the ring ...
-constexpr int kRing2 = kSlots2 / 2;  // ... in 3 slots, two blocks per slot (A / E columns)
+#ifndef KRK_RING2
+#define KRK_RING2 3  // ring4 experiment build: 4 (80 KiB a pair, 160 KiB a two-pair workgroup)
+#endif
+constexpr int kSlots2 = 2 * KRK_RING2;  // two lanes: block positions in the ring ...
+constexpr int kRing2 = kSlots2 / 2;     // ... in 3 slots, two blocks per slot (A / E columns)
 constexpr int kSlotWords = 64 * 64;  // 64 rounds x 64 lanes
 // eight lanes: 1 KiB of 1s past the all-1 slot (the A lanes' column walks one block ahead)
 constexpr uint32_t kOnesPad8 = 256;
