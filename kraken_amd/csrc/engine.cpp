@@ -340,7 +340,7 @@ struct Engine {
     std::vector<std::unique_ptr<uint8_t[]>> pend_free;
     uint32_t next_row = 0;
     uint64_t coalesce_us = 30000;  // idle device: the longest the first request waits for company
-    uint64_t quiet_us = 3000;      // ... or this long with no new owner (KRK_SHA_QUIET_US)
+    uint64_t quiet_us = 10000;     // ... or this long with no new owner (KRK_SHA_QUIET_US)
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
     bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
     bool sha_zero_copy = true;    // SHA jobs read the pinned slots directly (KRK_SHA_ZERO_COPY=0: H2D first)
@@ -659,7 +659,7 @@ void dispatcher(Engine* E, Queue* Q, bool sha) {
                         break;
                     }
                     // idle device: wait until every live GPU digester has a request queued, or
-                    // 3 ms pass with no new owner, at most coalesce_us after the first request,
+                    // 10 ms pass with no new owner, at most coalesce_us after the first request,
                     // so that uploads that start together also start on the device together
                     // (a digester that misses the first launch runs a whole launch behind)
                     const auto until =
@@ -751,7 +751,11 @@ int engine_start(Engine* E) {
     g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 8));
     g_inflight = (int)std::min<size_t>(kMaxInflight, std::max<size_t>(1, env_size("KRK_ENGINE_INFLIGHT", 3)));
     E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 30000);
-    E->quiet_us = env_size("KRK_SHA_QUIET_US", 3000);
+    // 10 ms: 256 writers starting together reach their first full slot over 5-25 ms on a
+    // CPU-quota box; with 3 ms a third of the rounds launched before all were in and ran 3-4
+    // launches more (profiles/r03/engine_quiet_ab.jsonl: median 13.94 -> 14.16 GB/s, every
+    // round 33 launches).  A GPU Digester carries >= 512 KiB a request, ~9 ms of a stream.
+    E->quiet_us = env_size("KRK_SHA_QUIET_US", 10000);
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
     E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
     if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->sha_zero_copy = atoi(z) != 0;

@@ -159,7 +159,7 @@ def test_256_native_digesters():
     1 MiB, every digest equal to the host SHA-256 of the same bytes.  With midstates in HBM
     rows, launches queued behind the running one and up to 8 requests of a digester in
     flight, a warm round reaches >= 13 GB/s (>= 50 MB/s a stream; the batch kernel's
-    per-stream rate is ~59 MB/s).  Warm rounds measure 13.2-14.4 GB/s; before the harness
+    per-stream rate is ~59 MB/s).  Warm rounds measure 14.0-14.4 GB/s; before the harness
     started its threads on a barrier (it spun them on yield(), which burnt the box's CPU
     quota and throttled the process ~90 ms in a third of the rounds) they
     were bimodal, so the best of five warm rounds is asserted, and every warm round well
