@@ -281,6 +281,7 @@ struct Inflight {
     char reason = '-';                    // trace: why the batch was formed
     size_t depth = 0, left_queued = 0;    // trace: launches on the device, requests left
     int64_t missing = 0;
+    double est = 0;                       // trace: the per-byte time estimate when formed
     // SHA: digest rows [row0, row0 + nrows) copied back (final requests)
     uint32_t row0 = 0, nrows = 0;
     // CRC: request i's portion CRCs at base[i] .. base[i + 1] of the results
@@ -579,6 +580,7 @@ Inflight* take_batch(Queue* Q, bool sha, char reason) {
     f->depth = Q->inflight.size();
     f->left_queued = Q->q.size();
     f->missing = Q->missing;
+    f->est = Q->ns_per_byte;
     for (int i = 0; i < kMaxInflight; ++i)
         if (!Q->out_busy[i]) {
             Q->out_busy[i] = true;
@@ -597,7 +599,7 @@ void launch_batch(Engine* E, Queue* Q, Inflight* f, bool sha) {
         fprintf(stderr, "krk_engine sha t=%.3fms abs=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
                 std::chrono::duration<double, std::milli>(f->t_launch - E->t0).count(),
                 std::chrono::duration<double, std::milli>(f->t_launch.time_since_epoch()).count(), f->batch.size(),
-                f->reason, f->depth, f->left_queued, (long long)f->missing, Q->ns_per_byte);
+                f->reason, f->depth, f->left_queued, (long long)f->missing, f->est);
     if (!sha && ++E->crc_launches == E->fail_crc_at) {
         set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
                   (unsigned long long)E->crc_launches);
