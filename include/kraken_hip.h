@@ -404,6 +404,9 @@ int krk_stream_create_prio(int priority, void** out);
 int krk_stream_create_cu_mask(const uint32_t* mask, uint32_t n_words, void** out);
 /* CUs of the calling thread's device. */
 int krk_device_cus(int* out);
+/* Waits for the stream's work, retires the library's state tied to it (events of upload
+ * slots and scratch blocks last used on it), then destroys it.  Streams handed to the
+ * library must be destroyed here, not with hipStreamDestroy. */
 int krk_stream_destroy(void* s);
 int krk_stream_sync(void* s);
 /* Events (a window loop waits for ONE earlier window's kernels while the next
