@@ -440,15 +440,15 @@ def run_metainfo(a, D, T, rank, world, res):
 
 
 def host_offload_leg(a, D, T, step, lens, world, dg_h, n):
-    """The same batch with krk_set_sha_host_offload(host cores): the longest SHA-256
-    chains on host threads (x86 SHA extensions, read out of HBM), the rest and every
-    piece CRC on the GPU.  Reported beside `value` (which stays the GPU-only path): it
-    is what a chain-bound batch (C1's one 1 GiB blob, the log-uniform regen batch) gets
-    from the library with the offload on."""
+    """The same batch with the library's default, krk_set_sha_host_offload(KRK_OFFLOAD_AUTO):
+    the planner's longest SHA-256 chains on host threads (x86 SHA extensions, read out of
+    HBM; as many threads as the process's CPU budget), the rest and every piece CRC on the
+    GPU.  Reported beside `value` (which stays the GPU-only path): it is what a chain-bound
+    batch (C1's one 1 GiB blob, the log-uniform regen batch) gets from the library."""
     thr = host_cores()
     idx, g_s, h_s = D.sha_offload_plan(lens, thr)
     gpu_only = dg_h.copy()  # step() gathers the digests into dg_h
-    D.set_sha_host_offload(thr)
+    D.set_sha_host_offload(-1)
     try:
         for _ in range(a.warmup):
             step()
@@ -466,7 +466,7 @@ def host_offload_leg(a, D, T, step, lens, world, dg_h, n):
             "bytes_on_host": int(sum(int(lens[i]) for i in idx)), "blobs": n,
             "model_s": {"gpu": round(g_s, 3), "host": round(h_s, 3)},
             "digests_match_gpu_only": bool(np.array_equal(dg_h, gpu_only)),
-            "what": "krk_metainfo_digest_dev with krk_set_sha_host_offload(host cores): the planner's longest "
+            "what": "krk_metainfo_digest_dev with the default offload (AUTO, host cores): the planner's longest "
                     "blobs hashed on host threads from HBM through pinned double buffers while the GPU hashes "
                     "the rest and every blob's piece CRCs (DESIGN.md 4.2)"}
 
@@ -713,8 +713,10 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
     return res
 
 
-# Host threads of the end-to-end leg's hybrid pass (KRK_BENCH_HYBRID="8,16"; "" = none).
-E2E_HYBRID_THREADS = [int(x) for x in os.environ.get("KRK_BENCH_HYBRID", "4").split(",") if x.strip()]
+# Host threads of the end-to-end leg's hybrid pass (KRK_BENCH_HYBRID="8,16"; "" = none;
+# -1 = the library's default, KRK_OFFLOAD_AUTO: a quarter of the CPU budget for host-resident
+# batches).
+E2E_HYBRID_THREADS = [int(x) for x in os.environ.get("KRK_BENCH_HYBRID", "-1").split(",") if x.strip()]
 
 
 def host_hybrid(D, T, datas, P, thr, sums_gpu, dg_gpu, world):
@@ -724,7 +726,11 @@ def host_hybrid(D, T, datas, P, thr, sums_gpu, dg_gpu, world):
     the windows as before.  Reported beside the GPU-only end-to-end figure, with the
     outputs checked equal to it."""
     lens = [int(d.size) for d in datas]
-    idx, g_s, h_s = D.sha_offload_plan(lens, thr, mode=D.OFFLOAD_HOST_WHOLE)
+    if thr < 0:
+        thr_plan = max(1, host_cores() // 4)  # what KRK_OFFLOAD_AUTO uses for host-resident batches
+    else:
+        thr_plan = thr
+    idx, g_s, h_s = D.sha_offload_plan(lens, thr_plan, mode=D.OFFLOAD_HOST_WHOLE)
     passes = []
     D.set_sha_host_offload(thr)
     try:
@@ -737,10 +743,10 @@ def host_hybrid(D, T, datas, P, thr, sums_gpu, dg_gpu, world):
         D.set_sha_host_offload(0)
     el = float(np.median(passes))
     same = bool(np.array_equal(dg, dg_gpu)) and all(np.array_equal(a, b) for a, b in zip(sums, sums_gpu))
-    return {"threads": thr, "value": round(world * sum(lens) / el / 1e9, 3), "unit": "GB/s",
+    return {"threads": thr_plan, "auto": thr < 0, "value": round(world * sum(lens) / el / 1e9, 3), "unit": "GB/s",
             "seconds": round(el, 3), "passes_s": [round(x, 3) for x in passes], "blobs_on_host": int(idx.size),
             "model_s": {"gpu": round(g_s, 3), "host": round(h_s, 3)}, "outputs_match_gpu_only": same,
-            "what": "krk_metainfo_digest_host with krk_set_sha_host_offload(threads): the planner's blobs are "
+            "what": "krk_metainfo_digest_host with the host offload on (auto: the library's default): the planner's blobs are "
                     "hashed and piece-summed in place on host threads and never cross PCIe, the rest as in the "
                     "GPU-only pass (DESIGN.md 4.5); median of the passes"}
 
@@ -844,7 +850,7 @@ def run_chunked(a, D, T, rank, world, res):
     ids, lens, P = workload_blobs(a.workload, rank, shard_world, a.blobs)
     n = len(lens)
     wr = WindowedRun(D, ids, lens, P, a.window_gib << 30,
-                     cap=n if a.no_admission else (a.live_cap or None), cu_split=a.cu_split)
+                     cap=n if a.no_admission else (a.live_cap or None))
     T.barrier()
     with D.KernelTimer():
         t0 = time.perf_counter()
@@ -1155,8 +1161,6 @@ def main():
                     help="C3: also run the batch with the host lane (the longest blobs hashed on host threads "
                          "while the windows run the rest), reported as host_offload beside the GPU-only value")
     ap.add_argument("--host-lane-k", type=int, default=-1, help="C3: blobs the host lane takes (-1 = the planner's)")
-    ap.add_argument("--cu-split", action="store_true",
-                    help="C3: the window generator on an eighth of the CUs, the SHA-256 launches on the rest")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
     ap.add_argument("--regen-serial", action="store_true",
                     help="c5regen: piece sums then InfoHashes (no krk_metainfo_batch_dev pipelining)")
@@ -1197,6 +1201,10 @@ def main():
         raise SystemExit(f"bench.py: {world} ranks but {ndev} gfx950 device(s) visible (pass --rehearse to share)")
     a.device = local % max(1, ndev)
     D.set_device(a.device)
+    # `value` is the GPU-only path (every chain on the device): the library's default
+    # (planner-gated host offload, AUTO) is measured beside it as `host_offload` /
+    # end_to_end.host_hybrid
+    D.set_sha_host_offload(0)
     T = Timer(D, dist)
     res = {"n_gpus": world, "warmup": a.warmup, "vs_baseline": None}
     if world > ndev:

@@ -102,26 +102,42 @@ typedef struct krk_file_blob {
 } krk_file_blob;
 int krk_piece_sums_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host);
 
-/* Streaming form for NewMetaInfo(d, io.Reader, P): the cgo shim copies each
- * Read() chunk in with _update.  Bytes go through the device's submission engine
- * (pooled pinned slots; the CRC requests of all concurrent streams and crc32_update
- * calls share launches); each slot's piece portions are hashed as independent
- * messages and folded into the piece sums on the host with the GF(2) combine, so
- * state crosses slot and piece boundaries.  _end returns the io.CopyN-loop results. */
+/* Streaming form for NewMetaInfo(d, io.Reader, P): the cgo shim copies each Read() chunk in
+ * with _update; _end returns the io.CopyN-loop results (core/metainfo.go:157-179).
+ * Placement (KRK_PLACE_* below), fixed at _begin:
+ *   KRK_PLACE_HOST  the caller's thread runs PCLMUL CRC-32 over each chunk in place (~17 GB/s
+ *                   a core, the reference's own placement) -- no copy, no PCIe;
+ *   KRK_PLACE_GPU   bytes go through the device's submission engine (pooled pinned slots;
+ *                   the CRC requests of all concurrent streams and crc32_update calls share
+ *                   launches); each slot's piece portions are hashed as independent
+ *                   messages and folded into the piece sums on the host with the GF(2)
+ *                   combine, so state crosses slot and piece boundaries;
+ *   KRK_PLACE_AUTO  (krk_piece_stream_begin) the process setting (krk_set_crc_placement,
+ *                   KRK_CRC_PLACEMENT), by default the crossover: HOST while every live host
+ *                   CRC stream has a CPU of its own (the CPUs this process may use), beyond
+ *                   that GPU when a memcpy costs the caller less per byte than the CRC
+ *                   (measured rates); HOST when no gfx950 device is present.
+ * HOST placement needs no device; GPU placement without one is KRK_ENODEV. */
 typedef struct krk_piece_stream krk_piece_stream;
 int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out);
+int krk_piece_stream_begin_on(int placement, int64_t piece_length, krk_piece_stream** out);
+int krk_piece_stream_placement(const krk_piece_stream* s, int* placement);
 int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* host_buf, uint64_t n);
 int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap,
                          uint64_t* n_sums, uint64_t* length);
 void krk_piece_stream_free(krk_piece_stream* s);
 
-/* crc32.Update(crc, IEEETable, p) for one buffer (hash.Hash32 Write path used
- * by agentstorage.Torrent.writePiece, lib/torrent/storage/agentstorage/torrent.go:175-199).
- * data is a HOST pointer.  Calls of at most 64 KiB (KRK_CRC_HOST_MAX) run on the
- * caller's thread (krk_host_crc32_update: no PCIe round trip for a small write);
- * larger ones go through the device's CRC queue, coalesced with the other pending
- * requests of the device into one launch. */
+/* crc32.Update(crc, IEEETable, p) for one buffer (hash.Hash32 Write path used by
+ * agentstorage.Torrent.writePiece, lib/torrent/storage/agentstorage/torrent.go:175-199).
+ * data is a HOST pointer.  AUTO (krk_crc32_update): calls of at most 64 KiB
+ * (KRK_CRC_HOST_MAX) and calls below the crossover of krk_piece_stream_begin run on the
+ * caller's thread; the rest go through the device's CRC queue, coalesced with the other
+ * pending requests of the device into one launch.  krk_crc32_update_on forces a placement. */
 int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
+int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
+/* What KRK_PLACE_AUTO means for new piece streams and crc32_update calls, process-wide:
+ * KRK_PLACE_AUTO (default: the crossover), KRK_PLACE_HOST or KRK_PLACE_GPU. */
+int krk_set_crc_placement(int placement);
 
 /* Batch piece verification (the same kernel in verify mode): ok_out[i] = 1 iff
  * piece i of the blob matches expected[i].  data is a device pointer. */
@@ -182,7 +198,8 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~59 MB/s).
  *                   N = 40 x the CPUs this process may use, or KRK_DIGESTER_HOST_STREAMS,
  *                   or krk_set_digester_host_streams (-1 restores the default).
- * Without a gfx950 device every constructor fails with KRK_ENODEV. */
+ * HOST placement needs no device; GPU placement without a gfx950 device is KRK_ENODEV and
+ * AUTO without one is HOST (the product's own SHA-NI path, not the oracle). */
 typedef struct krk_digester krk_digester;
 #define KRK_PLACE_AUTO 0
 #define KRK_PLACE_HOST 1
@@ -398,10 +415,6 @@ int krk_stream_create(void** out);
  * long kernels (a C3 window's SHA-256 launch runs ~0.6 s) is kept off the queues the
  * short work shares, which would otherwise wait behind it. */
 int krk_stream_create_prio(int priority, void** out);
-/* A stream whose kernels run only on the CUs set in `mask` (bit i of word i/32 = CU i of
- * the device; n_words 32-bit words).  A C3 window generator masked to the CUs the SHA-256
- * launch leaves free no longer takes issue slots from the SHA waves. */
-int krk_stream_create_cu_mask(const uint32_t* mask, uint32_t n_words, void** out);
 /* CUs of the calling thread's device. */
 int krk_device_cus(int* out);
 /* Waits for the stream's work, retires the library's state tied to it (events of upload
@@ -468,20 +481,26 @@ int krk_sha_plan_for(uint64_t n_streams, int* plan);
 #define KRK_SHA_PLAN_8LANE_2PAIR 6  /* eight lanes, two pairs per workgroup */
 int krk_set_sha_plan(int plan);
 
-/* Host offload of the longest SHA-256 chains, process-wide (default 0 = off).  With
- * threads > 0, krk_sha256_dev and krk_metainfo_digest_dev hand the longest blobs of a
- * batch to up to `threads` host threads (x86 SHA extensions, ~2 GB/s a thread against
- * ~59 MB/s a GPU stream), which read them from device memory through pinned double
- * buffers while the GPU hashes the rest and every blob's piece CRCs; the digests land in
- * digests_dev as before.  How many go to the host minimises max(GPU time, host time) and
- * is 0 unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host,
- * 1,000 equal 100 MiB blobs (C2) stay on the GPU.  The call then returns after the host
- * part is hashed (the GPU part stays asynchronous on `stream`).  The host-buffer entry
- * points work on their offloaded blobs in place and never upload them: krk_sha256_host
- * hashes them, krk_metainfo_digest_host hashes them AND computes their piece sums (the
- * SHA-256 pass and the CRC pass of a blob are separate host tasks), so the bytes that
- * cross the host link shrink by theirs (the threshold there is 3 %). */
+/* Host offload of the longest SHA-256 chains, process-wide.  krk_sha256_dev and
+ * krk_metainfo_digest_dev hand the longest blobs of a batch to host threads (x86 SHA
+ * extensions, ~2 GB/s a thread against ~59 MB/s a GPU stream), which read them from device
+ * memory through pinned double buffers while the GPU hashes the rest and every blob's piece
+ * CRCs; the digests land in digests_dev as before.  How many go to the host minimises
+ * max(GPU time, host time) at the planner's measured rates (krk_planner_rates_get) and is 0
+ * unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host, 1,000
+ * equal 100 MiB blobs (C2) stay on the GPU.  The call then returns after the host part is
+ * hashed (the GPU part stays asynchronous on `stream`).  The host-buffer entry points work
+ * on their offloaded blobs in place and never upload them: krk_sha256_host hashes them,
+ * krk_metainfo_digest_host hashes them AND computes their piece sums (the SHA-256 pass and
+ * the CRC pass of a blob are separate host tasks), so the bytes that cross the host link
+ * shrink by theirs (the threshold there is 3 %).
+ * threads: KRK_OFFLOAD_AUTO (-1, the default) = the CPUs this process may use (affinity,
+ * cgroup quota, OMP_NUM_THREADS) for device-resident batches and a quarter of them for
+ * host-resident batches (whose staging windows need the rest as copy threads); 0 = off
+ * (every chain on the GPU); n = up to n threads. */
+#define KRK_OFFLOAD_AUTO (-1)
 int krk_set_sha_host_offload(int threads);
+int krk_sha_host_offload(int* threads);      /* the current setting */
 /* The rates the planners use (krk_host_offload_plan, the offload of the batch entry
  * points, the host/GPU split of the CRC-only host entry points), per device:
  * sha_stream_bps = one SHA-256 stream's rate at full residency under each AUTO tier
@@ -503,6 +522,10 @@ typedef struct krk_planner_rates {
 } krk_planner_rates;
 int krk_planner_rates_get(krk_planner_rates* out);
 int krk_planner_rates_set(const krk_planner_rates* in);
+/* Measure the calling thread's device's rates now (krk_init does it for its devices, so that
+ * the measurement runs before the library has work of its own on them; otherwise the first
+ * planner use measures).  Re-measure after a change of load the planners should see. */
+int krk_planner_calibrate(void);
 /* The offload plan for `n` blob lengths on `threads` host threads with the planner rates
  * (krk_planner_rates_get; `cus` > 0 overrides their CU count), no device work: the
  * indices (longest first) to host_idx (room for n, may be NULL), their count to n_host,

@@ -15,6 +15,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip.h")
 
 KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX, KRK_EIO = 0, -1, -2, -3, -4, -5, -6, -7
 KRK_PLACE_AUTO, KRK_PLACE_HOST, KRK_PLACE_GPU = 0, 1, 2
+KRK_OFFLOAD_AUTO = -1
 
 
 class KrakenError(RuntimeError):
@@ -86,6 +87,10 @@ def _load() -> C.CDLL:
         "krk_piece_stream_end": (i, [vp, u32p, C.c_uint64, u64p, u64p]),
         "krk_piece_stream_free": (None, [vp]),
         "krk_crc32_update": (i, [C.c_uint32, vp, C.c_uint64, u32p]),
+        "krk_crc32_update_on": (i, [i, C.c_uint32, vp, C.c_uint64, u32p]),
+        "krk_set_crc_placement": (i, [i]),
+        "krk_piece_stream_begin_on": (i, [i, C.c_int64, C.POINTER(vp)]),
+        "krk_piece_stream_placement": (i, [vp, C.POINTER(C.c_int)]),
         "krk_verify_pieces_dev": (i, [blobp, u32p, u8p, vp]),
         "krk_verify_pieces_host": (i, [C.POINTER(vp), u64p, u32p, C.c_uint64, u8p]),
         "krk_sha256_dev": (i, [C.POINTER(vp), u64p, C.c_uint64, vp, vp]),
@@ -139,7 +144,6 @@ def _load() -> C.CDLL:
         "krk_memcpy_d2h_async": (i, [vp, vp, C.c_uint64, vp]),
         "krk_stream_create": (i, [C.POINTER(vp)]),
         "krk_stream_create_prio": (i, [i, C.POINTER(vp)]),
-        "krk_stream_create_cu_mask": (i, [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(vp)]),
         "krk_device_cus": (i, [C.POINTER(i)]),
         "krk_stream_destroy": (i, [vp]),
         "krk_stream_sync": (i, [vp]),
@@ -148,6 +152,8 @@ def _load() -> C.CDLL:
         "krk_event_sync": (i, [vp]),
         "krk_event_destroy": (i, [vp]),
         "krk_set_sha_host_offload": (i, [i]),
+        "krk_sha_host_offload": (i, [C.POINTER(C.c_int)]),
+        "krk_planner_calibrate": (i, []),
         "krk_sha_offload_plan": (i, [C.POINTER(C.c_uint64), C.c_uint64, i, i, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "krk_host_offload_plan": (i, [C.POINTER(C.c_uint64), C.c_uint64, i, i, i, C.POINTER(C.c_uint32),

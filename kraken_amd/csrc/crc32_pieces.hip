@@ -415,7 +415,7 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
     uint64_t cap = uint64_t(cus) * blocks_per_cu;
     uint32_t grid = (uint32_t)(want < cap ? want : cap);
     if (grid == 0) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
     return hipGetLastError();
 }
@@ -495,7 +495,7 @@ __global__ void crc_verify_kernel(const uint32_t* sums, const uint32_t* expected
 hipError_t launch_crc_verify(const uint32_t* sums, const uint32_t* expected, uint8_t* ok,
                              uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(crc_verify_kernel, dim3((n + 255) / 256), dim3(256), 0, s, sums, expected,
                        ok, n);
     return hipGetLastError();

@@ -593,7 +593,21 @@ Inflight* take_batch(Queue* Q, bool sha, char reason) {
 
 // Without the lock: launch f on the queue's stream and record its completion event.
 void launch_batch(Engine* E, Queue* Q, Inflight* f, bool sha) {
-    hipSetDevice(E->dev);  // a caller's thread may run this (submit)
+    // A caller's thread may run this (submit): the launch goes to the engine's device, and
+    // the caller's current device -- HIP's and the library's (t_dev, which the launch timing
+    // records) -- is restored afterwards.
+    int hip_saved = -1;
+    if (hipGetDevice(&hip_saved) != hipSuccess) hip_saved = -1;
+    const int t_saved = t_dev;
+    struct Restore {
+        int hip, t;
+        ~Restore() {
+            t_dev = t;
+            if (hip >= 0) hipSetDevice(hip);
+        }
+    } restore{hip_saved, t_saved};
+    hipSetDevice(E->dev);
+    t_dev = E->dev;
     f->t_launch = Clock::now();
     if (sha && E->trace)
         fprintf(stderr, "krk_engine sha t=%.3fms abs=%.3fms n=%zu why=%c depth=%zu left_queued=%zu missing=%lld est=%.2fns/B\n",
@@ -1074,10 +1088,20 @@ int krk_digester_new_on(int placement, krk_digester** out) {
     KRK_CHECK(placement >= KRK_PLACE_AUTO && placement <= KRK_PLACE_GPU, KRK_EINVAL, "unknown placement %d",
               placement);
     *out = nullptr;
-    KRK_DEVICE(D0);  // the library serves a gfx950 device; no device is KRK_ENODEV, never a CPU fallback
-    (void)D0;
     const int64_t live = g_live_digesters.fetch_add(1) + 1;
-    const bool host = placement == KRK_PLACE_HOST || (placement == KRK_PLACE_AUTO && live <= host_stream_limit());
+    bool host = placement == KRK_PLACE_HOST || (placement == KRK_PLACE_AUTO && live <= host_stream_limit());
+    if (!host) {
+        // GPU placement needs a gfx950 device (KRK_ENODEV without one); AUTO on a host with
+        // none is the host placement: the product's own SHA-NI path (host_meta.cpp).
+        int drc = KRK_OK;
+        if (!device(&drc)) {
+            if (placement == KRK_PLACE_GPU) {
+                g_live_digesters.fetch_sub(1);
+                return drc;
+            }
+            host = true;
+        }
+    }
     auto* d = new krk_digester();
     memcpy(d->h, kIV, sizeof d->h);
     if (!host) {
@@ -1216,12 +1240,16 @@ int krk_set_digester_host_streams(int64_t n) {
 
 // ======================================================================= piece stream
 struct krk_piece_stream {
-    Engine* E = nullptr;
+    Engine* E = nullptr;  // null: host placement
     uint64_t P = 0;
+    uint64_t submitted = 0;       // stream bytes consumed (host) / handed to the engine (GPU)
+    std::vector<uint32_t> sums;   // GPU: folded on the completer thread, in submission order
+    // host placement: crc32.Update value of the current piece, bytes of it seen
+    uint32_t crc = 0;
+    uint64_t in_piece = 0;
+    // GPU placement
     std::unique_ptr<uint8_t[]> pend;  // bytes not yet submitted
     size_t fill = 0;
-    uint64_t submitted = 0;       // stream bytes handed to the engine
-    std::vector<uint32_t> sums;   // folded on the completer thread, in submission order
     std::atomic<bool> fold_stop{false};    // completer thread: a request failed or broke the order, stop folding
     std::atomic<bool> fold_broken{false};  // completer thread: a continuation arrived with no start
     std::deque<Req*> inflight;
@@ -1230,7 +1258,61 @@ struct krk_piece_stream {
     std::string err_msg;
 };
 
+namespace krk {
 namespace {
+
+// ------------------------------------------------------- CRC placement
+// A piece stream (NewMetaInfo over an io.Reader) and a crc32.Update call (PieceHash) carry
+// no state the GPU could keep: every byte crosses the host link once and the caller's
+// thread copies it into a pinned slot first.  One host core's PCLMUL CRC runs ~17 GB/s
+// (host_crc_rate()) and the GPU path of one stream is bounded by that caller-thread copy
+// and the slot round trips (profiles/r04/crc_crossover.json), so AUTO keeps a stream on its
+// caller's thread while every live host CRC stream has a core of its own; beyond the cores
+// the excess goes to the GPU engine only when its per-byte cost to the calling thread (a
+// memcpy, host_copy_rate()) is below the CRC's own -- the host's aggregate is then the CPU
+// budget, and bytes the GPU takes free CPU for the rest.
+std::atomic<int> g_crc_placement{KRK_PLACE_AUTO};  // krk_set_crc_placement / KRK_CRC_PLACEMENT
+std::atomic<int64_t> g_host_crc_load{0};           // live host piece streams + host crc32_update calls running
+
+int crc_placement_setting() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (const char* e = getenv("KRK_CRC_PLACEMENT")) {
+            const int v = atoi(e);
+            if (v >= KRK_PLACE_AUTO && v <= KRK_PLACE_GPU) g_crc_placement.store(v);
+        }
+    });
+    return g_crc_placement.load(std::memory_order_relaxed);
+}
+
+// AUTO: true = this stream / call goes to the GPU engine (a device being present).
+bool crc_auto_gpu() {
+    const int64_t load = g_host_crc_load.load(std::memory_order_relaxed);
+    if (load < (int64_t)host_threads()) return false;
+    return host_copy_rate() > host_crc_rate();
+}
+
+// The placement a new piece stream / crc32_update call runs on: HOST or GPU.  `placement`
+// KRK_PLACE_AUTO follows the process setting, then the crossover; GPU needs a gfx950
+// device (KRK_ENODEV), AUTO without one is HOST.
+int resolve_crc_placement(int placement, int* rc) {
+    *rc = KRK_OK;
+    const bool asked_auto = placement == KRK_PLACE_AUTO;
+    if (asked_auto) placement = crc_placement_setting();
+    const bool forced = placement != KRK_PLACE_AUTO;  // explicit, or the process setting
+    if (placement == KRK_PLACE_AUTO) placement = crc_auto_gpu() ? KRK_PLACE_GPU : KRK_PLACE_HOST;
+    if (placement == KRK_PLACE_GPU) {
+        int drc = KRK_OK;
+        if (!device(&drc)) {
+            if (forced) {
+                *rc = drc;
+                return -1;
+            }
+            return KRK_PLACE_HOST;
+        }
+    }
+    return placement;
+}
 
 // Fold a request's portion CRCs into the stream's piece sums (completer thread, the
 // stream's requests in submission order).  Once a request has failed, later ones are
@@ -1301,29 +1383,102 @@ int stream_submit(krk_piece_stream* s, const uint8_t* src, uint64_t len) {
     return KRK_OK;
 }
 
+// Host placement: calcPieceSums' loop (core/metainfo.go:157-179) on the caller's thread --
+// each piece's crc32.Update value carried across calls, a sum appended when a piece fills.
+// A large write is cut into spans (at piece ends, then at most `span` bytes) that idle
+// host-pool threads hash beside the caller; the spans' CRCs are combined in order.
+void stream_host_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
+    const int idle = n >= (2u << 20) && s->P >= (64u << 10) ? host_pool_idle() : 0;
+    if (idle <= 0) {  // (small pieces: a span a piece would cost more than it spreads)
+        while (n) {
+            const uint64_t take = std::min<uint64_t>(n, s->P - s->in_piece);
+            s->crc = host_crc32_update(s->crc, buf, take);
+            s->in_piece += take;
+            s->submitted += take;
+            buf += take;
+            n -= take;
+            if (s->in_piece == s->P) {
+                s->sums.push_back(s->crc);
+                s->crc = 0;
+                s->in_piece = 0;
+            }
+        }
+        return;
+    }
+    struct Span {
+        const uint8_t* p;
+        uint64_t n;
+        bool ends_piece;
+        uint32_t c;
+    };
+    const uint64_t span = std::max<uint64_t>(256u << 10, ((n / (uint64_t)(idle + 1)) + 63) & ~uint64_t(63));
+    std::vector<Span> sp;
+    for (uint64_t in = s->in_piece, o = 0; o < n;) {
+        const uint64_t take = std::min<uint64_t>(n - o, s->P - in);
+        for (uint64_t q = 0; q < take; q += span) {
+            const uint64_t m = std::min(span, take - q);
+            sp.push_back({buf + o + q, m, q + m == take && in + take == s->P, 0});
+        }
+        in = (in + take) % s->P;
+        o += take;
+    }
+    host_parallel_for(sp.size(), idle, [&](size_t i) { sp[i].c = host_crc32_update(0, sp[i].p, sp[i].n); });
+    for (const Span& x : sp) {
+        s->crc = crc32_combine(s->crc, x.c, x.n);
+        s->in_piece += x.n;
+        s->submitted += x.n;
+        if (x.ends_piece) {
+            s->sums.push_back(s->crc);
+            s->crc = 0;
+            s->in_piece = 0;
+        }
+    }
+}
+
 }  // namespace
+}  // namespace krk
 
 extern "C" {
 
-int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out) {
+int krk_piece_stream_begin_on(int placement, int64_t piece_length, krk_piece_stream** out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_CHECK(placement >= KRK_PLACE_AUTO && placement <= KRK_PLACE_GPU, KRK_EINVAL, "unknown placement %d",
+              placement);
     KRK_CHECK(piece_length > 0, KRK_EINVAL, "piece length must be positive");
     *out = nullptr;
-    KRK_DEVICE(D0);
-    (void)D0;
     int rc = KRK_OK;
-    Engine* E = engine_of(place_device(), &rc);
-    if (!E) return rc;
+    const int where = resolve_crc_placement(placement, &rc);
+    if (rc) return rc;
+    Engine* E = nullptr;
+    if (where == KRK_PLACE_GPU) {
+        E = engine_of(place_device(), &rc);
+        if (!E) return rc;
+    }
     auto* s = new krk_piece_stream();
     s->E = E;
     s->P = (uint64_t)piece_length;
+    if (!E) g_host_crc_load.fetch_add(1);
     *out = s;
+    return KRK_OK;
+}
+
+int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out) {
+    return krk_piece_stream_begin_on(KRK_PLACE_AUTO, piece_length, out);
+}
+
+int krk_piece_stream_placement(const krk_piece_stream* s, int* placement) {
+    KRK_CHECK(s && placement, KRK_EINVAL, "piece_stream_placement: null argument");
+    *placement = s->E ? KRK_PLACE_GPU : KRK_PLACE_HOST;
     return KRK_OK;
 }
 
 int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
     KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
     KRK_CHECK(n == 0 || buf, KRK_EINVAL, "buffer is NULL");
+    if (!s->E) {
+        stream_host_update(s, buf, n);
+        return KRK_OK;
+    }
     if (s->err) {
         t_err = s->err_msg;
         return s->err;
@@ -1355,44 +1510,62 @@ int krk_piece_stream_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n)
 int krk_piece_stream_end(krk_piece_stream* s, uint32_t* sums_out, uint64_t cap, uint64_t* n_sums,
                          uint64_t* length) {
     KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
-    if (s->err) {
-        t_err = s->err_msg;
-        return s->err;
+    if (s->E) {
+        if (s->err) {
+            t_err = s->err_msg;
+            return s->err;
+        }
+        int rc = stream_submit(s, s->pend.get(), s->fill);
+        if (!rc) s->fill = 0;
+        if (!rc) rc = stream_drain(s, 0);
+        if (rc) return rc;
     }
-    int rc = stream_submit(s, s->pend.get(), s->fill);
-    if (!rc) s->fill = 0;
-    if (!rc) rc = stream_drain(s, 0);
-    if (rc) return rc;
     const uint64_t np = krk_num_pieces(s->submitted, (int64_t)s->P);
     if (n_sums) *n_sums = np;
     if (length) *length = s->submitted;
     KRK_CHECK(np <= cap || !sums_out, KRK_ERANGE, "sums capacity %llu < %llu pieces", (unsigned long long)cap,
               (unsigned long long)np);
-    KRK_CHECK(s->sums.size() >= np, KRK_EHIP, "engine: %llu of %llu piece sums folded",
-              (unsigned long long)s->sums.size(), (unsigned long long)np);
-    if (sums_out && np) memcpy(sums_out, s->sums.data(), np * 4);
+    const uint64_t have = s->sums.size() + (!s->E && s->in_piece ? 1 : 0);
+    KRK_CHECK(have >= np, KRK_EHIP, "engine: %llu of %llu piece sums folded", (unsigned long long)have,
+              (unsigned long long)np);
+    if (sums_out && np) {
+        const uint64_t full = std::min<uint64_t>(np, s->sums.size());
+        memcpy(sums_out, s->sums.data(), full * 4);
+        if (full < np) sums_out[full] = s->crc;  // host: the partial last piece (io.CopyN n > 0)
+    }
     return KRK_OK;
 }
 
 void krk_piece_stream_free(krk_piece_stream* s) {
     if (!s) return;
-    stream_drain(s, 0);
-    pend_release(s->E, std::move(s->pend));
+    if (s->E) {
+        stream_drain(s, 0);
+        pend_release(s->E, std::move(s->pend));
+    } else {
+        g_host_crc_load.fetch_sub(1);
+    }
     delete s;
 }
 
-// crc32.Update(crc, IEEETable, p): small writes on the caller's thread, the rest
-// through the CRC queue (slot-sized portions combined in order on this thread).
-int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out) {
+// crc32.Update(crc, IEEETable, p): on the caller's thread (HOST, and AUTO below the
+// crossover or for writes of at most KRK_CRC_HOST_MAX bytes), else through the device's
+// CRC queue (slot-sized portions combined in order on this thread).
+int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_CHECK(n == 0 || data, KRK_EINVAL, "data is NULL");
-    KRK_DEVICE(D0);
-    (void)D0;
-    if (n <= env_size("KRK_CRC_HOST_MAX", 64 << 10)) {
-        *out = host_crc32_update(crc, data, n);
+    KRK_CHECK(placement >= KRK_PLACE_AUTO && placement <= KRK_PLACE_GPU, KRK_EINVAL, "unknown placement %d",
+              placement);
+    static const size_t host_max = env_size("KRK_CRC_HOST_MAX", 64 << 10);
+    int rc = KRK_OK;
+    const int where = (placement == KRK_PLACE_AUTO && n <= host_max) ? KRK_PLACE_HOST
+                                                                      : resolve_crc_placement(placement, &rc);
+    if (rc) return rc;
+    if (where == KRK_PLACE_HOST) {
+        g_host_crc_load.fetch_add(1);
+        *out = host_crc32_update_par(crc, data, n);
+        g_host_crc_load.fetch_sub(1);
         return KRK_OK;
     }
-    int rc = KRK_OK;
     Engine* E = engine_of(place_device(), &rc);
     if (!E) return rc;
     Waiter w;
@@ -1424,6 +1597,18 @@ int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* ou
     for (Req* r : reqs) retire(r);
     if (!rc) *out = c;
     return rc;
+}
+
+int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out) {
+    return krk_crc32_update_on(KRK_PLACE_AUTO, crc, data, n, out);
+}
+
+int krk_set_crc_placement(int placement) {
+    KRK_CHECK(placement >= KRK_PLACE_AUTO && placement <= KRK_PLACE_GPU, KRK_EINVAL, "unknown placement %d",
+              placement);
+    crc_placement_setting();  // the environment is read first, so this call wins over it
+    g_crc_placement.store(placement);
+    return KRK_OK;
 }
 
 int krk_engine_stats(uint64_t* sha_batches, uint64_t* sha_jobs, uint64_t* crc_batches, uint64_t* crc_requests,

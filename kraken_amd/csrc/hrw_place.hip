@@ -113,7 +113,7 @@ __global__ void u64_to_f64_kernel(const uint64_t* vals, uint64_t n, int rehash, 
 
 hipError_t launch_u64_to_f64(const uint64_t* vals, uint64_t n, int rehash, double* out, hipStream_t s) {
     if (!n) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(u64_to_f64_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, vals, n, rehash, out);
     return hipGetLastError();
 }
@@ -168,7 +168,7 @@ hipError_t launch_hrw_order(const HrwArgs& a, hipStream_t s) {
     const uint32_t kpb = a.n_nodes >= kHrwMaxNodes ? 1 : kHrwMaxNodes / a.n_nodes > 64 ? 64
                                                                                      : kHrwMaxNodes / a.n_nodes;
     const uint64_t grid = (a.n_keys + kpb - 1) / kpb;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(hrw_order_kernel, dim3((uint32_t)grid), dim3(kHrwBlock), 0, s, a, kpb);
     return hipGetLastError();
 }
@@ -198,7 +198,7 @@ hipError_t launch_ring_filter(const int32_t* order, uint64_t n_rows, uint32_t n_
                               const uint8_t* healthy, int32_t max_replica, uint32_t row_out,
                               int32_t* locs, uint8_t* counts, hipStream_t s) {
     if (!n_rows) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(ring_filter_kernel, dim3((uint32_t)((n_rows + 255) / 256)), dim3(256), 0, s,
                        order, n_rows, n_nodes, healthy, max_replica, row_out, locs, counts);
     return hipGetLastError();
@@ -227,7 +227,7 @@ static hipError_t launch_gather(const uint8_t* digests32, uint64_t n, const int3
                                 const uint8_t* table_counts, uint32_t row_out, T* locs, uint8_t* counts,
                                 hipStream_t s) {
     if (!n) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(shard_gather_kernel<T>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
                        digests32, n, table_locs, table_counts, row_out, locs, counts);
     return hipGetLastError();

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 namespace krk {
 
@@ -10,6 +11,28 @@ namespace krk {
 // SHA-256, work items + runs for CRC).  Written by the launchers, read by timed().
 inline thread_local int t_launch_plan = 0;
 inline thread_local uint64_t t_launch_units = 0;
+
+// Before a launch: an error already pending on this thread belongs to an earlier HIP call
+// that nobody checked (the caller's own, or one outside the library).  It is reported, not
+// cleared away: the launcher returns it without launching, and launch_error_text() says
+// where it came from, so the entry point's message names it.  hipErrorNotReady is an event
+// query's answer, not an error.
+inline thread_local bool t_launch_pending = false;
+inline hipError_t launch_precheck() {
+    t_launch_pending = false;
+    const hipError_t p = hipPeekAtLastError();
+    if (p == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    if (p == hipErrorNotReady) return hipSuccess;
+    t_launch_pending = true;
+    return p;
+}
+inline const char* launch_error_text(hipError_t e) {
+    static thread_local char buf[256];
+    if (!t_launch_pending) return hipGetErrorString(e);
+    snprintf(buf, sizeof buf, "HIP error pending from an earlier call on this thread: %s", hipGetErrorString(e));
+    return buf;
+}
 
 // ---------------------------------------------------------------- CRC pieces
 // One work item = a contiguous byte run inside ONE piece, processed by one wave.

@@ -31,15 +31,9 @@ void host_sha256_blocks(uint32_t h[8], const uint8_t* p, size_t nblocks);
 void host_sha256_final(const uint32_t h[8], uint64_t absorbed, const uint8_t* tail, size_t n, uint8_t out[32]);
 uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);
 
-namespace {
-
-std::atomic<int> g_off_threads{0};
-
-constexpr uint64_t kOffChunk = 8ull << 20;  // D2H chunk (multiple of 64)
-
 // One host thread, bytes/s: measured once (16 MiB) and derated for the clock a fully
 // loaded socket holds.  SHA-256 (x86 SHA extensions) and the piece CRC (PCLMUL folding).
-double time_rate(const std::function<void(const uint8_t*, size_t)>& f) {
+static double time_rate(const std::function<void(const uint8_t*, size_t)>& f) {
     std::vector<uint8_t> buf(16u << 20, 0x5a);
     f(buf.data(), 64 << 10);  // warm
     const auto t0 = std::chrono::steady_clock::now();
@@ -47,7 +41,7 @@ double time_rate(const std::function<void(const uint8_t*, size_t)>& f) {
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return 0.85 * buf.size() / std::max(s, 1e-6);
 }
-double host_rate() {
+double host_sha_rate() {
     static const double r = time_rate([](const uint8_t* p, size_t n) {
         uint32_t h[8];
         memcpy(h, kIV, sizeof h);
@@ -69,6 +63,16 @@ double host_crc_rate() {
     });
     return r;
 }
+
+namespace {
+
+// Host threads of the offload: KRK_OFFLOAD_AUTO (the default) = the CPUs this call may use
+// for blobs read out of HBM (their D2H copies need no host CPU), a quarter of them for
+// host-resident batches, whose windows need the rest as copy threads (C2 end-to-end: 4 of
+// 16 threads 55.5 GB/s, 8 54.4-55.2, 16 49.9).  0 = off, n = n threads.
+std::atomic<int> g_off_threads{KRK_OFFLOAD_AUTO};
+
+constexpr uint64_t kOffChunk = 8ull << 20;  // D2H chunk (multiple of 64)
 
 // ------------------------------------------------------------------ planner rates
 // Kernel geometry (a property of the code, not of the box): the AUTO launch plan's three
@@ -93,7 +97,7 @@ Rates nominal_rates(int cus) {
     R.stream[1] = 51.6e6;
     R.stream[2] = 35.7e6;
     R.d2h = R.h2d = 54e9;
-    R.host_sha = host_rate();
+    R.host_sha = host_sha_rate();
     R.host_crc = host_crc_rate();
     R.host_copy = host_copy_rate();
     R.cus = cus > 0 ? cus : 256;
@@ -101,20 +105,54 @@ Rates nominal_rates(int cus) {
     return R;
 }
 
-// The device's own rates, measured once per device and process (~50 ms): each SHA-256
-// tier's plan timed on 16 / 64 / 128 x CUs streams of 256 KiB (every stream reads the
-// same bytes: the kernel is issue-bound, not HBM-bound), pinned 64 MiB copies each way.
-int calibrate(Device* D, Rates& R) {
-    R = Rates{};
-    R.cus = D->cus;
-    KRK_HIP(hipSetDevice(D->id));
-    const uint64_t L = 256u << 10, C = 64u << 20;
-    const uint32_t mmax = (uint32_t)(kResidentPerCu[2] * (uint64_t)D->cus);
+}  // namespace
+
+// The calibration's device and pinned buffers, stream and events, kept until krk_shutdown:
+// hipFree / hipHostFree wait for the whole device, i.e. for whatever other work is running
+// on it when a later call re-measures.
+struct CalBufs {
     hipStream_t s = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     uint8_t *d_in = nullptr, *d_dig = nullptr, *d_copy = nullptr, *h_copy = nullptr;
     uint32_t* d_state = nullptr;
     ShaJob* d_jobs = nullptr;
+    uint32_t mmax = 0;
+};
+
+// Per device: host threads + pinned double buffers of the offload phases, and the planner
+// calibration (measured once per device and process, or again on krk_planner_calibrate).
+struct Worker;
+struct OffloadPool {
+    std::mutex mu;
+    std::vector<std::vector<Worker>> free_sets;
+    std::mutex cal_mu;  // one calibration of this device at a time
+    CalBufs cal;
+    bool measured = false;
+    Rates rates{};
+};
+
+namespace {
+
+OffloadPool* pool_of(Device* D) {
+    std::lock_guard<std::mutex> g(D->offload_mu);
+    if (!D->offload) D->offload = new OffloadPool();
+    return D->offload;
+}
+
+// The device's own rates (~50 ms): each SHA-256 tier's plan timed on 16 / 64 / 128 x CUs
+// streams of 256 KiB (every stream reads the same bytes: the kernel is issue-bound, not
+// HBM-bound), pinned 64 MiB copies each way, on a stream of the calibration's own.
+int calibrate(Device* D, CalBufs& cb, Rates& R) {
+    R = Rates{};
+    R.cus = D->cus;
+    KRK_HIP(hipSetDevice(D->id));
+    const uint64_t L = 256u << 10, C = 64u << 20;
+    const uint32_t mmax = (uint32_t)(kResidentPerCu[2] * (uint64_t)D->cus);
+    hipStream_t& s = cb.s;
+    hipEvent_t &e0 = cb.e0, &e1 = cb.e1;
+    uint8_t *&d_in = cb.d_in, *&d_dig = cb.d_dig, *&d_copy = cb.d_copy, *&h_copy = cb.h_copy;
+    uint32_t*& d_state = cb.d_state;
+    ShaJob*& d_jobs = cb.d_jobs;
     int rc = KRK_OK;
     auto ok = [&](hipError_t e, const char* what) {
         if (e != hipSuccess && !rc) {
@@ -134,10 +172,23 @@ int calibrate(Device* D, Rates& R) {
         }
         return (double)std::max(ms, 1e-3f);
     };
-    if (ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
-        ok(hipEventCreate(&e0), "event") && ok(hipEventCreate(&e1), "event") &&
-        ok(hipMalloc(&d_in, L), "alloc") && ok(hipMalloc(&d_state, 32ull * mmax), "alloc") &&
-        ok(hipMalloc(&d_dig, 32ull * mmax), "alloc") && ok(hipMalloc(&d_jobs, sizeof(ShaJob) * mmax), "alloc") &&
+    auto have = [&](bool present, const std::function<hipError_t()>& make, const char* what) {
+        return present || ok(make(), what);
+    };
+    if (cb.mmax < mmax) {  // a device with more CUs than the buffers were made for: start over
+        for (void* p : {(void*)d_state, (void*)d_dig, (void*)d_jobs})
+            if (p) hipFree(p);
+        d_state = nullptr;
+        d_dig = nullptr;
+        d_jobs = nullptr;
+        cb.mmax = mmax;
+    }
+    if (have(s, [&] { return hipStreamCreateWithFlags(&s, hipStreamNonBlocking); }, "stream") &&
+        have(e0, [&] { return hipEventCreate(&e0); }, "event") && have(e1, [&] { return hipEventCreate(&e1); }, "event") &&
+        have(d_in, [&] { return hipMalloc(&d_in, L); }, "alloc") &&
+        have(d_state, [&] { return hipMalloc(&d_state, 32ull * mmax); }, "alloc") &&
+        have(d_dig, [&] { return hipMalloc(&d_dig, 32ull * mmax); }, "alloc") &&
+        have(d_jobs, [&] { return hipMalloc(&d_jobs, sizeof(ShaJob) * mmax); }, "alloc") &&
         ok(hipMemsetAsync(d_in, 0x5a, L, s), "memset")) {
         std::vector<ShaJob> jobs(mmax);
         for (uint32_t i = 0; i < mmax; ++i) {
@@ -154,28 +205,22 @@ int calibrate(Device* D, Rates& R) {
                 R.stream[t] = (double)L / (ms * 1e-3);
             }
     }
-    if (!rc && ok(hipMalloc(&d_copy, C), "alloc") && ok(hipHostMalloc(reinterpret_cast<void**>(&h_copy), C, 0), "pin")) {
+    if (!rc && have(d_copy, [&] { return hipMalloc(&d_copy, C); }, "alloc") &&
+        have(h_copy, [&] { return hipHostMalloc(reinterpret_cast<void**>(&h_copy), C, 0); }, "pin")) {
         R.h2d = (double)C / (timed_ms([&] { return hipMemcpyAsync(d_copy, h_copy, C, hipMemcpyHostToDevice, s); }) * 1e-3);
         R.d2h = (double)C / (timed_ms([&] { return hipMemcpyAsync(h_copy, d_copy, C, hipMemcpyDeviceToHost, s); }) * 1e-3);
     }
     if (s) hipStreamSynchronize(s);
-    for (void* p : {(void*)d_in, (void*)d_state, (void*)d_dig, (void*)d_jobs, (void*)d_copy})
-        if (p) hipFree(p);
-    if (h_copy) hipHostFree(h_copy);
-    if (e0) hipEventDestroy(e0);
-    if (e1) hipEventDestroy(e1);
-    if (s) hipStreamDestroy(s);
-    R.host_sha = host_rate();
+    R.host_sha = host_sha_rate();
     R.host_crc = host_crc_rate();
     R.host_copy = host_copy_rate();
     R.source = KRK_RATES_MEASURED;
     return rc;
 }
 
-std::mutex g_rates_mu;
+std::mutex g_rates_mu;  // the override only: a calibration never runs under it
 bool g_rates_set = false;
 Rates g_rates_override{};
-std::vector<std::pair<int, Rates>> g_rates_measured;  // per device id
 
 // GPU time of m streams (longest `longest` bytes, `bytes` in all) under the AUTO launch
 // plan: the longest chain at the tier's per-stream rate, or the streams' bytes at the
@@ -195,37 +240,61 @@ double gpu_seconds(uint64_t longest, double bytes, uint64_t m, const Rates& R) {
 // behind the batch's own long SHA-256 kernel (tools/micro/d2h_probe.hip: copy kernels
 // on 4 of 16 streams waited 1 s for a 1 s kernel on a fifth), while the DMA copies
 // themselves do not wait for it.
+}  // namespace
+
+// Each offload phase takes a set of worker resources of its own (two streams + two pinned
+// buffers a thread), so concurrent callers on one device (several krk_sha256_dev callers,
+// *_multi workers sharing a GPU) hash at the same time.
 struct Worker {
     hipStream_t s[2] = {nullptr, nullptr};
     uint8_t* buf[2] = {nullptr, nullptr};
 };
 
-}  // namespace
-
-// Per device: sets of worker resources (two streams + two pinned buffers a thread).  Each
-// offload phase takes a set of its own, so concurrent callers on one device (several
-// krk_sha256_dev callers, *_multi workers sharing a GPU) hash at the same time.
-struct OffloadPool {
-    std::mutex mu;
-    std::vector<std::vector<Worker>> free_sets;
-};
-
-// The longest blobs to hash on `threads` host threads (indices into lens, longest
-// first); empty when the host would not shorten the batch by at least 10 % (device-
-// resident: the host's D2H reads share the PCIe link and the chip's memory with the
-// GPU part) or 3 % (host-resident: the host's blobs simply stay off the link).
-Rates planner_rates(Device* D) {
-    std::lock_guard<std::mutex> g(g_rates_mu);
-    if (g_rates_set) return g_rates_override;
-    if (!D) return nominal_rates(0);
-    for (auto& [id, R] : g_rates_measured)
-        if (id == D->id) return R;
+// (Re)measure device D's rates now; a failed calibration plans with the nominal rates.
+int calibrate_device(Device* D) {
+    OffloadPool* P = pool_of(D);
+    std::lock_guard<std::mutex> g(P->cal_mu);
     Rates R{};
-    if (calibrate(D, R) != KRK_OK) {  // a failed calibration plans with the nominal rates
-        R = nominal_rates(D->cus);
+    const int rc = calibrate(D, P->cal, R);
+    if (rc != KRK_OK) R = nominal_rates(D->cus);
+    std::lock_guard<std::mutex> gp(P->mu);
+    P->rates = R;
+    P->measured = true;
+    return rc;
+}
+
+// The rates the planners use on device D: the override, else D's measured rates (the first
+// caller on a device measures them; krk_init measures them eagerly, before the device
+// carries any work of the library's), else -- no device -- the nominal ones.  Only the
+// device being measured waits for its calibration: no process-wide lock is held across it.
+Rates planner_rates(Device* D) {
+    {
+        std::lock_guard<std::mutex> g(g_rates_mu);
+        if (g_rates_set) return g_rates_override;
     }
-    g_rates_measured.push_back({D->id, R});
-    return R;
+    if (!D) return nominal_rates(0);
+    OffloadPool* P = pool_of(D);
+    {
+        std::lock_guard<std::mutex> g(P->mu);
+        if (P->measured) return P->rates;
+    }
+    {
+        std::lock_guard<std::mutex> g(P->cal_mu);  // a concurrent first caller waits for the one measuring
+        bool done;
+        {
+            std::lock_guard<std::mutex> gp(P->mu);
+            done = P->measured;
+        }
+        if (!done) {
+            Rates R{};
+            if (calibrate(D, P->cal, R) != KRK_OK) R = nominal_rates(D->cus);
+            std::lock_guard<std::mutex> gp(P->mu);
+            P->rates = R;
+            P->measured = true;
+        }
+    }
+    std::lock_guard<std::mutex> g(P->mu);
+    return P->rates;
 }
 
 // Host-resident batches: the caller's pageable bytes are copied into pinned windows on
@@ -291,7 +360,12 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
     return order;
 }
 
-int offload_threads() { return g_off_threads.load(std::memory_order_relaxed); }
+int offload_threads(int mode) {
+    const int t = g_off_threads.load(std::memory_order_relaxed);
+    if (t != KRK_OFFLOAD_AUTO) return t;
+    const int budget = host_threads_for_call();
+    return mode == kOffDevice ? budget : std::max(1, budget / 4);
+}
 
 int host_cpu_budget() {
     static const int n = [] {
@@ -319,11 +393,7 @@ int host_cpu_budget() {
 int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
                  hipEvent_t ready, uint8_t* out) {
     if (ptrs.empty()) return KRK_OK;
-    {
-        std::lock_guard<std::mutex> g(D->offload_mu);
-        if (!D->offload) D->offload = new OffloadPool();
-    }
-    OffloadPool& P = *D->offload;
+    OffloadPool& P = *pool_of(D);
     // at least one thread: the knob may have been lowered since the plan was made
     const int T = (int)std::min<size_t>((size_t)std::max(threads, 1), ptrs.size());
     std::vector<Worker> set;
@@ -345,13 +415,18 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     while ((int)set.size() < T) {
         Worker w;
         for (int b = 0; b < 2; ++b) {
-            KRK_HIP(hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking));
-            if (hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault) != hipSuccess) {
-                for (int c = 0; c <= b; ++c)
+            const hipError_t es = hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking);
+            const hipError_t eb = es == hipSuccess
+                                      ? hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault)
+                                      : es;
+            if (eb != hipSuccess) {  // undo what this worker made so far
+                for (int c = 0; c <= b; ++c) {
                     if (w.s[c]) hipStreamDestroy(w.s[c]);
-                if (b) hipHostFree(w.buf[0]);
-                set_error(KRK_ENOMEM, "sha256 host offload: pinned buffers");
-                return KRK_ENOMEM;
+                    if (w.buf[c]) hipHostFree(w.buf[c]);
+                }
+                if (es != hipSuccess) set_error(KRK_EHIP, "sha256 host offload: stream: %s", hipGetErrorString(es));
+                else set_error(KRK_ENOMEM, "sha256 host offload: pinned buffers");
+                return es != hipSuccess ? KRK_EHIP : KRK_ENOMEM;
             }
         }
         set.push_back(w);
@@ -437,6 +512,13 @@ void offload_teardown(Device& D) {  // krk_shutdown: no offload phase is running
                 if (w.s[b]) hipStreamSynchronize(w.s[b]), hipStreamDestroy(w.s[b]);
                 if (w.buf[b]) hipHostFree(w.buf[b]);
             }
+    CalBufs& c = P->cal;
+    if (c.s) hipStreamSynchronize(c.s), hipStreamDestroy(c.s);
+    for (void* p : {(void*)c.d_in, (void*)c.d_state, (void*)c.d_dig, (void*)c.d_jobs, (void*)c.d_copy})
+        if (p) hipFree(p);
+    if (c.h_copy) hipHostFree(c.h_copy);
+    if (c.e0) hipEventDestroy(c.e0);
+    if (c.e1) hipEventDestroy(c.e1);
     delete P;
     D.offload = nullptr;
 }
@@ -465,7 +547,7 @@ void offload_whole_host(const std::vector<const uint8_t*>& ptrs, const std::vect
                         uint8_t* out) {
     // Task t: blob t / 2, its SHA-256 pass (even t) or its piece-CRC pass (odd t), in
     // order of cost (the CRC pass runs ~6x the SHA-256 rate on one core).
-    const double rs = host_rate(), rc = host_crc_rate();
+    const double rs = host_sha_rate(), rc = host_crc_rate();
     std::vector<std::pair<double, size_t>> tasks;
     tasks.reserve(2 * ptrs.size());
     for (size_t j = 0; j < ptrs.size(); ++j) {
@@ -512,7 +594,7 @@ int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* di
     if (r) return r;
     hipError_t e = launch_digest_scatter(static_cast<const uint8_t*>(d), (uint32_t)idx.size(), digests_dev, s);
     scratch_free(D, d, s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "digest scatter launch: %s", hipGetErrorString(e));
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "digest scatter launch: %s", launch_error_text(e));
     return KRK_OK;
 }
 
@@ -523,9 +605,21 @@ using namespace krk;
 extern "C" {
 
 int krk_set_sha_host_offload(int threads) {
-    KRK_CHECK(threads >= 0 && threads <= 1024, KRK_EINVAL, "host offload threads %d outside 0..1024", threads);
+    KRK_CHECK(threads == KRK_OFFLOAD_AUTO || (threads >= 0 && threads <= 1024), KRK_EINVAL,
+              "host offload threads %d outside -1 (auto), 0..1024", threads);
     g_off_threads.store(threads);
     return KRK_OK;
+}
+
+int krk_sha_host_offload(int* threads) {
+    KRK_CHECK(threads, KRK_EINVAL, "threads is NULL");
+    *threads = g_off_threads.load();
+    return KRK_OK;
+}
+
+int krk_planner_calibrate(void) {
+    KRK_DEVICE(D);
+    return calibrate_device(D);
 }
 
 int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, int mode, uint32_t* host_idx,

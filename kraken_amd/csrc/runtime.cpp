@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "runtime.hpp"
+#include "staging.hpp"
 
 namespace krk {
 
@@ -33,212 +34,10 @@ void set_error(int code, const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
-    (void)code;
     t_err = buf;
-}
-
-// Device allocations of one host-path call, freed on every return path (hipFree
-// waits for the device, so work still queued on them on an error path is drained).
-struct DevMem {
-    std::vector<void*> ps;
-    ~DevMem() {
-        for (void* p : ps) hipFree(p);
-    }
-    template <class T>
-    hipError_t alloc(T** p, size_t n) {
-        void* v = nullptr;
-        const hipError_t e = hipMalloc(&v, n);
-        if (e == hipSuccess) ps.push_back(v);
-        *p = static_cast<T*>(v);
-        return e;
-    }
-};
-
-// ------------------------------------------------------------------ host staging pipeline
-// Two pinned host windows and two device windows; window k is refilled only after
-// the kernel that consumed it (event) has finished.
-struct Window {
-    uint8_t* host = nullptr;
-    uint8_t* dev = nullptr;
-    size_t cap = 0;
-    hipEvent_t copied = nullptr;    // the H2D out of `host` has finished: host buffer reusable
-    hipEvent_t consumed = nullptr;  // single-stream users: all work reading `dev` has finished
-    hipEvent_t done[2] = {nullptr, nullptr};  // kernels reading `dev`, one event per kernel stream
-    bool inflight = false, copying = false;
-    bool done_pending[2] = {false, false};
-};
-
-// Two pinned host windows and two device windows.  The host side of window k is
-// refilled once its H2D is done; the H2D into its device side waits (on the copy
-// stream only) for the kernels that read the previous contents, so the upload of
-// window k+1 overlaps the kernels of window k.
-struct CopyTask {
-    uint8_t* dst;
-    const uint8_t* src;
-    size_t n;
-};
-
-struct Pipeline {
-    Window w[2];
-    ~Pipeline() {
-        for (auto& x : w) {
-            if (x.inflight) hipEventSynchronize(x.consumed);
-            if (x.copying) hipEventSynchronize(x.copied);
-            for (int i = 0; i < 2; ++i)
-                if (x.done_pending[i]) hipEventSynchronize(x.done[i]);
-            if (x.host) hipHostFree(x.host);
-            if (x.dev) hipFree(x.dev);
-            if (x.copied) hipEventDestroy(x.copied);
-            if (x.consumed) hipEventDestroy(x.consumed);
-            for (auto e : x.done)
-                if (e) hipEventDestroy(e);
-        }
-    }
-    int init(size_t cap) {
-        for (auto& x : w) {
-            x.cap = cap;
-            KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&x.host), cap, hipHostMallocDefault));
-            KRK_HIP(hipMalloc(reinterpret_cast<void**>(&x.dev), cap));
-            KRK_HIP(hipEventCreateWithFlags(&x.copied, hipEventDisableTiming));
-            KRK_HIP(hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming));
-            for (auto& e : x.done) KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-        return KRK_OK;
-    }
-    // Host side of window k is free for refilling.
-    int acquire(int k) {
-        if (w[k].inflight) {
-            KRK_HIP(hipEventSynchronize(w[k].consumed));
-            w[k].inflight = false;
-        }
-        if (w[k].copying) {
-            KRK_HIP(hipEventSynchronize(w[k].copied));
-            w[k].copying = false;
-        }
-        return KRK_OK;
-    }
-    // Upload n bytes of window k on cp, after the kernels that read its last contents.
-    hipError_t h2d(int k, size_t n, hipStream_t cp) {
-        Window& x = w[k];
-        for (int i = 0; i < 2; ++i)
-            if (x.done_pending[i]) {
-                hipError_t e = hipStreamWaitEvent(cp, x.done[i], 0);
-                if (e != hipSuccess) return e;
-                x.done_pending[i] = false;
-            }
-        hipError_t e = hipMemcpyAsync(x.dev, x.host, n, hipMemcpyHostToDevice, cp);
-        if (e == hipSuccess) e = hipEventRecord(x.copied, cp);
-        if (e == hipSuccess) x.copying = true;
-        return e;
-    }
-    // The caller's pinned bytes DMA'd straight into device window k (tasks' dst are
-    // device addresses in it), after the kernels that read its last contents.
-    hipError_t h2d_direct(int k, const std::vector<CopyTask>& tasks, hipStream_t cp) {
-        Window& x = w[k];
-        for (int i = 0; i < 2; ++i)
-            if (x.done_pending[i]) {
-                hipError_t e = hipStreamWaitEvent(cp, x.done[i], 0);
-                if (e != hipSuccess) return e;
-                x.done_pending[i] = false;
-            }
-        for (const auto& t : tasks) {
-            hipError_t e = hipMemcpyAsync(t.dst, t.src, t.n, hipMemcpyHostToDevice, cp);
-            if (e != hipSuccess) return e;
-        }
-        hipError_t e = hipEventRecord(x.copied, cp);
-        if (e == hipSuccess) x.copying = true;
-        return e;
-    }
-    // Kernel stream ks (slot 0 or 1) has enqueued everything that reads window k.
-    hipError_t release(int k, int slot, hipStream_t ks) {
-        hipError_t e = hipEventRecord(w[k].done[slot], ks);
-        if (e == hipSuccess) w[k].done_pending[slot] = true;
-        return e;
-    }
-};
-
-// KRK_TRACE=1: host-side phase times of the windowed host paths, to stderr.
-static bool trace_on() {
-    static const bool on = getenv("KRK_TRACE") && atoi(getenv("KRK_TRACE")) > 0;
-    return on;
-}
-static double wall_s() {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-static size_t window_bytes() {
-    const char* v = getenv("KRK_WINDOW_MB");
-    size_t mb = v ? strtoull(v, nullptr, 10) : 512;
-    if (mb < 1) mb = 1;
-    return mb << 20;
-}
-
-// The device's persistent staging windows (grown to at least `cap`) for one host-path
-// call; a concurrent second caller, or a call wanting windows above 1 GiB, gets
-// private windows (freed when the call returns) instead.
-struct StagingLease {
-    Device* D = nullptr;
-    Pipeline* p = nullptr;
-    std::unique_ptr<Pipeline> own;
-    bool locked = false;
-    ~StagingLease() {
-        if (locked) D->staging_mu.unlock();
-    }
-};
-
-static int lease_staging(Device* D, size_t cap, StagingLease& L) {
-    L.D = D;
-    constexpr size_t kKeepMax = size_t(1) << 30;  // windows kept across calls: at most 2 x 1 GiB pinned
-    if (cap <= kKeepMax && D->staging_mu.try_lock()) {
-        L.locked = true;
-        if (!D->staging || D->staging->w[0].cap < cap) {
-            delete D->staging;  // its destructor drains the old windows' events
-            D->staging = nullptr;
-            auto p = std::make_unique<Pipeline>();
-            int r = p->init(cap);
-            if (r) return r;
-            D->staging = p.release();
-        }
-        L.p = D->staging;
-        return KRK_OK;
-    }
-    L.own = std::make_unique<Pipeline>();
-    L.p = L.own.get();
-    return L.own->init(cap);
-}
-
-// Host -> pinned staging copies of one window, split over a few threads (one
-// host thread's memcpy is well below the PCIe rate).  KRK_COPY_THREADS overrides.
-
-static unsigned copy_threads() {
-    const char* v = getenv("KRK_COPY_THREADS");
-    if (v) return std::max(1u, (unsigned)strtoul(v, nullptr, 10));
-    return std::max(1u, std::min(16u, (unsigned)host_threads_for_call()));
-}
-
-static void par_copy(const std::vector<CopyTask>& tasks) {
-    size_t total = 0;
-    for (const auto& t : tasks) total += t.n;
-    const unsigned T = copy_threads();
-    if (T == 1 || total < (8u << 20)) {
-        for (const auto& t : tasks) memcpy(t.dst, t.src, t.n);
-        return;
-    }
-    // Cut the concatenated byte range into T equal spans.
-    auto run = [&](size_t lo, size_t hi) {
-        size_t pos = 0;
-        for (const auto& t : tasks) {
-            const size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
-            if (a < b) memcpy(t.dst + (a - pos), t.src + (a - pos), b - a);
-            pos += t.n;
-            if (pos >= hi) break;
-        }
-    };
-    std::vector<std::thread> th;
-    const size_t span = (total + T - 1) / T;
-    for (unsigned i = 1; i < T; ++i) th.emplace_back(run, i * span, std::min(total, (i + 1) * span));
-    run(0, std::min(total, span));
-    for (auto& t : th) t.join();
+    // A HIP failure the library reports is consumed here: left pending on the thread, the
+    // next launch would report it again as an unchecked earlier error (launch_precheck).
+    if (code == KRK_EHIP || code == KRK_ENOMEM) (void)hipGetLastError();
 }
 
 void engine_teardown(Device& D);                 // engine.cpp
@@ -281,60 +80,6 @@ static void teardown_device(Device& D) {
         if (s) hipStreamDestroy(s);
 }
 
-// File -> pinned window reads of one window, split over the copy threads at
-// 1 MiB-aligned spans (O_DIRECT needs block-aligned offsets and lengths; every
-// task starts 4 KiB-aligned in both the file and the window).
-struct ReadTask {
-    int fd;
-    uint64_t off;   // file offset
-    uint8_t* dst;
-    size_t n;       // bytes wanted (O_DIRECT reads round the last block up)
-    size_t blob;    // index into the caller's files (for the error message)
-};
-
-// Returns -1 on success, else the index of the failed task; err = its errno (0 = EOF).
-static long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) {
-    // Spans are cut in a stream of the tasks laid end to end, each padded to 4 KiB
-    // when direct, so every span boundary falls on a block boundary of its task.
-    auto padded = [direct](size_t n) { return direct ? (n + 4095) & ~size_t(4095) : n; };
-    size_t total = 0;
-    for (const auto& t : tasks) total += padded(t.n);
-    std::atomic<long> bad{-1};
-    std::atomic<int> bad_errno{0};
-    auto run = [&](size_t lo, size_t hi) {
-        size_t pos = 0;
-        for (size_t i = 0; i < tasks.size() && pos < hi; pos += padded(tasks[i].n), ++i) {
-            const ReadTask& t = tasks[i];
-            size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
-            if (a >= b) continue;
-            a -= pos;
-            b -= pos;
-            while (a < b) {
-                size_t want = b - a;
-                if (direct) want = (want + 4095) & ~size_t(4095);
-                const ssize_t got = pread(t.fd, t.dst + a, want, (off_t)(t.off + a));
-                if (got < 0 && errno == EINTR) continue;
-                if (got <= 0) {
-                    long expect = -1;
-                    bad.compare_exchange_strong(expect, (long)i);
-                    bad_errno.store(got < 0 ? errno : 0);
-                    return;
-                }
-                a += (size_t)got;
-            }
-        }
-    };
-    const unsigned T = (total < (8u << 20)) ? 1 : copy_threads();
-    constexpr size_t kAlign = size_t(1) << 20;
-    const size_t span = std::max(kAlign, ((total + T - 1) / T + kAlign - 1) & ~(kAlign - 1));
-    std::vector<std::thread> th;
-    for (size_t lo = span; lo < total; lo += span) th.emplace_back(run, lo, std::min(total, lo + span));
-    run(0, std::min(total, span));
-    for (auto& t : th) t.join();
-    *err = bad_errno.load();
-    return bad.load();
-}
-
 }  // namespace krk
 
 using namespace krk;
@@ -370,7 +115,11 @@ int krk_init(uint64_t dev_mask) {
         if (dev_mask ? !((dev_mask >> i) & 1) : i != saved) continue;
         t_dev = i;
         int rc = KRK_OK;
-        if (!device(&rc)) r = rc;
+        Device* D = device(&rc);
+        if (!D) r = rc;
+        // the planners' rates, measured now while the library has no work on the device
+        // (a first use under load would fix a contended split for the process)
+        else if (!getenv("KRK_NO_CALIBRATE")) r = calibrate_device(D);
     }
     for (int i = n; i < 64 && !r; ++i)
         if ((dev_mask >> i) & 1) {
@@ -713,12 +462,17 @@ static std::atomic<double> g_crc_split{-1.0};
 static thread_local uint64_t t_split_gpu = 0, t_split_host = 0;
 
 static bool host_pinned(const void* p, uint64_t n) {
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) return false;
-    if (n > 1 && (hipPointerGetAttributes(&a, static_cast<const uint8_t*>(p) + n - 1) != hipSuccess ||
-                  a.type != hipMemoryTypeHost))
-        return false;
-    return true;
+    // pageable memory is an expected "invalid value" here: not left pending on the thread
+    // (the next launch would report it as an unchecked earlier error)
+    auto pinned_at = [](const void* q) {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return a.type == hipMemoryTypeHost;
+    };
+    return pinned_at(p) && (n <= 1 || pinned_at(static_cast<const uint8_t*>(p) + n - 1));
 }
 
 int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
@@ -729,14 +483,23 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     sums_span(blobs, n_blobs, &lo, &hi);
     if (hi == lo) return KRK_OK;
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
-    const Rates R = planner_rates(D);
-    const int T = host_threads_for_call();
+    // Concurrent callers (the agent's dispatcher verifying from several goroutines) share the
+    // CPU budget instead of each starting a full set of threads.
+    static std::atomic<int> callers{0};
+    struct Caller {
+        Caller() { callers.fetch_add(1); }
+        ~Caller() { callers.fetch_sub(1); }
+    } caller;
+    const int T = std::max(1, host_threads_for_call() / std::max(1, callers.load()));
     bool all_pinned = true;
     double bytes = 0;
     for (uint64_t i = 0; i < n_blobs; ++i) {
         bytes += (double)blobs[i].length;
         if (all_pinned && blobs[i].length && !host_pinned(blobs[i].data, blobs[i].length)) all_pinned = false;
     }
+    const char* forced = getenv("KRK_CRC_GPU_FRACTION");
+    // Rates only where they decide something: pageable batches stay on the host threads.
+    const Rates R = (all_pinned || forced) ? planner_rates(D) : Rates{};
     // Pinned bytes: the GPU's share starts from the rates' model, capped at 10 %, and is then
     // set from what the previous calls measured (each side's bytes over its own wall time
     // while both ran): the DMA reads share the host's memory with the CRC threads, so the
@@ -749,7 +512,6 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         const double learned = g_crc_split.load(std::memory_order_relaxed);
         gpu_frac = learned >= 0 ? learned : std::min(0.10, R.h2d / (R.h2d + H));
     }
-    const char* forced = getenv("KRK_CRC_GPU_FRACTION");
     if (forced) gpu_frac = std::clamp(atof(forced), 0.0, 1.0);
     // Whole pieces to the GPU until its share of the bytes is reached, the rest to the host.
     const double quota = gpu_frac * bytes;
@@ -773,21 +535,21 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         }
         for (uint64_t k = q; k < np; ++k) host.push_back({b.data + k * P, std::min(P, b.length - k * P), b.sums_offset + k});
     }
-    std::atomic<size_t> next{0};
-    std::atomic<int> running{0};
+    // The host share on the host pool's idle threads (and this thread once the GPU pass is
+    // queued): at most T threads, one per 8 MiB of host bytes (a small share stays on the
+    // calling thread).
     const auto t0 = std::chrono::steady_clock::now();
     std::atomic<int64_t> host_end_ns{0};
-    auto work = [&] {
-        for (size_t j; (j = next.fetch_add(1)) < host.size();)
-            sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
-        if (running.fetch_sub(1) == 1)  // the last host thread: the host side's wall time
-            host_end_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
-                                  .count());
-    };
-    std::vector<std::thread> pool;
-    const int TH = (int)std::min<size_t>((size_t)T, host.size());
-    running.store(TH);
-    for (int t = 0; t < TH; ++t) pool.emplace_back(work);
+    std::atomic<size_t> left{host.size()};
+    double hbytes_all = 0;
+    for (const PieceTask& h : host) hbytes_all += (double)h.n;
+    const int TH = (int)std::min<size_t>({(size_t)T, host.size(), (size_t)(hbytes_all / (8 << 20)) + 1});
+    HostBatch hb(host.size(), gpu.empty() ? TH - 1 : TH, [&](size_t j) {
+        sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
+        if (left.fetch_sub(1) == 1)  // the last piece: the host side's wall time
+            host_end_ns.store(
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+    });
     double gpu_s = 0;
     if (!gpu.empty()) {
         std::vector<uint32_t> gs(g_sums);
@@ -799,7 +561,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
                 memcpy(sums_host + gpu_dst[j], gs.data() + gpu[j].sums_offset, cnt * 4);
             }
     }
-    for (auto& t : pool) t.join();
+    hb.join();
     const double hbytes = bytes - gbytes, host_s = host_end_ns.load() * 1e-9;
     t_split_gpu = (uint64_t)gbytes;
     t_split_host = (uint64_t)hbytes;
@@ -955,8 +717,9 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed in
     // place on host threads and never cross PCIe.
     std::vector<uint32_t> host;
-    if (offload_threads() > 0) {
-        host = offload_plan(lengths, n, offload_threads(), planner_rates(D), nullptr, nullptr, kOffHostSha);
+    const int off_t = offload_threads(kOffHostSha);
+    if (off_t > 0) {
+        host = offload_plan(lengths, n, off_t, planner_rates(D), nullptr, nullptr, kOffHostSha);
         for (uint32_t i : host) {
             done[i] = 1;
             --remaining;
@@ -972,7 +735,7 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
                 p[j] = data_host[host[j]];
                 l[j] = lengths[host[j]];
             }
-            offload_hash_host(p, l, offload_threads(), host_dig.data());
+            offload_hash_host(p, l, off_t, host_dig.data());
         });
     struct Joiner {
         std::thread& t;
@@ -1121,10 +884,11 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     // below carry the others' bytes to both kernels.
     std::vector<char> on_host(n, 0);
     std::vector<uint32_t> host;
-    if (offload_threads() > 0) {
+    const int off_t = offload_threads(kOffHostWhole);
+    if (off_t > 0) {
         std::vector<uint64_t> lens(n);
         for (uint64_t i = 0; i < n; ++i) lens[i] = blobs[i].length;
-        host = offload_plan(lens.data(), n, offload_threads(), planner_rates(D), nullptr, nullptr, kOffHostWhole);
+        host = offload_plan(lens.data(), n, off_t, planner_rates(D), nullptr, nullptr, kOffHostWhole);
         for (uint32_t i : host) on_host[i] = 1;
     }
     const uint64_t n_gpu = n - host.size();
@@ -1169,7 +933,7 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
                 pl[j] = (uint64_t)blobs[host[j]].piece_length;
                 so[j] = host_sums.data() + host_sums_off[j];
             }
-            offload_whole_host(p, l, pl, so, offload_threads(), host_dig.data());
+            offload_whole_host(p, l, pl, so, off_t, host_dig.data());
         });
     struct Joiner {
         std::thread& t;
@@ -1183,7 +947,7 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         int saved;
         ~ShareGuard() { t_host_share = saved; }
     } share_guard{t_host_share};
-    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - offload_threads());
+    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
     ItemBuilder B;
     uint64_t remaining = n_gpu;
     int k = 0;
@@ -1290,7 +1054,7 @@ int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, u
     if (!r) r = upload(D, expected_host, np * 4, &d_exp, s);
     if (!r) {
         hipError_t e = launch_crc_verify(d_sums, static_cast<const uint32_t*>(d_exp), d_ok, (uint32_t)np, s);
-        if (e != hipSuccess) { set_error(KRK_EHIP, "verify launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+        if (e != hipSuccess) { set_error(KRK_EHIP, "verify launch: %s", launch_error_text(e)); r = KRK_EHIP; }
     }
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "verify sync"); r = KRK_EHIP; }
     if (!r && hipMemcpy(ok_out_host, d_ok, np, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
@@ -1382,7 +1146,7 @@ static int hrw_table_dev(Device* D, const void* d_kb, const void* d_koff, const 
             e = timed(K_FILTER, s, [&] {
                 return launch_ring_filter(d_order, nk, N, dn.healthy, max_replica, row_out, *d_locs, *d_counts, s);
             });
-        if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+        if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", launch_error_text(e)); r = KRK_EHIP; }
     }
     free_nodes(D, dn, s);
     if (d_order) scratch_free(D, d_order, s);
@@ -1448,7 +1212,7 @@ int krk_hrw_ordered(const char* keys, const uint64_t* key_off, uint64_t n_keys, 
         HrwArgs a{static_cast<const uint8_t*>(d_kb), static_cast<const uint64_t*>(d_koff), n_keys, dn.labels, dn.off,
                   dn.w, N, n_out, static_cast<const uint8_t*>(d_bad), d_order, d_sc};
         hipError_t e = n_out ? timed(K_HRW, s, [&] { return launch_hrw_order(a, s); }) : hipSuccess;
-        if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+        if (e != hipSuccess) { set_error(KRK_EHIP, "hrw launch: %s", launch_error_text(e)); r = KRK_EHIP; }
     }
     // Copy-out: drain the stream, then blocking copies into the caller's (pageable) memory.
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "hrw sync"); r = KRK_EHIP; }
@@ -1484,7 +1248,7 @@ int krk_hrw_uint64_to_float64(const uint8_t* sums8, uint64_t n, int rehash, doub
     if (!r && scratch_alloc(D, &d_o, n * 8, s) != hipSuccess) r = KRK_ENOMEM;
     if (!r) {
         hipError_t e = launch_u64_to_f64(static_cast<const uint64_t*>(d_v), n, rehash, d_o, s);
-        if (e != hipSuccess) { set_error(KRK_EHIP, "u64_to_f64 launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+        if (e != hipSuccess) { set_error(KRK_EHIP, "u64_to_f64 launch: %s", launch_error_text(e)); r = KRK_EHIP; }
     }
     if (hipStreamSynchronize(s) != hipSuccess && !r) { set_error(KRK_EHIP, "u64_to_f64 sync"); r = KRK_EHIP; }
     if (!r && hipMemcpy(out, d_o, n * 8, hipMemcpyDeviceToHost) != hipSuccess) r = KRK_EHIP;
@@ -1587,7 +1351,7 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
             else
                 return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
         });
-        if (e != hipSuccess) { set_error(KRK_EHIP, "gather launch: %s", hipGetErrorString(e)); r = KRK_EHIP; }
+        if (e != hipSuccess) { set_error(KRK_EHIP, "gather launch: %s", launch_error_text(e)); r = KRK_EHIP; }
     }
     if (d_tl) scratch_free(D, d_tl, s);
     if (d_tc) scratch_free(D, d_tc, s);
@@ -1642,7 +1406,7 @@ int krk_synth_fill_dev(uint8_t* dst_dev, uint64_t blob_idx, uint64_t offset, uin
     };
     const uint64_t seed = mix((0x4B52414B454EULL ^ blob_idx) + GAMMA);
     hipError_t e = timed(K_SYNTH, s, [&] { return launch_synth_fill(dst_dev, seed, offset, n, variant, s); });
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", hipGetErrorString(e));
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", launch_error_text(e));
     return KRK_OK;
 }
 
@@ -1674,7 +1438,7 @@ int krk_synth_fill_chunks_dev(const krk_chunk* chunks, uint64_t n, int variant, 
         return launch_synth_fill_chunks(static_cast<const SynthChunk*>(d_sc), (uint32_t)sc.size(), variant, s);
     });
     scratch_free(D, d_sc, s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", hipGetErrorString(e));
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "synth launch: %s", launch_error_text(e));
     return KRK_OK;
 }
 
@@ -1730,15 +1494,6 @@ int krk_stream_create(void** out) {
     *out = s;
     return KRK_OK;
 }
-int krk_stream_create_cu_mask(const uint32_t* mask, uint32_t n_words, void** out) {
-    KRK_CHECK(out && mask && n_words, KRK_EINVAL, "stream_create_cu_mask: null argument");
-    KRK_DEVICE(D);
-    (void)D;
-    hipStream_t s;
-    KRK_HIP(hipExtStreamCreateWithCUMask(&s, n_words, mask));
-    *out = s;
-    return KRK_OK;
-}
 int krk_device_cus(int* out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_DEVICE(D);
@@ -1758,9 +1513,17 @@ int krk_stream_create_prio(int priority, void** out) {
     return KRK_OK;
 }
 int krk_stream_destroy(void* s) {
+    KRK_CHECK(s, KRK_EINVAL, "stream is NULL");
+    const hipStream_t hs = static_cast<hipStream_t>(s);
+    // The library state tied to the stream lives on the stream's own device, which need not
+    // be this thread's.
+    hipDevice_t owner = t_dev;
+    KRK_HIP(hipStreamGetDevice(hs, &owner));
+    const int saved = t_dev;
     int drc = KRK_OK;
-    if (Device* D = device(&drc)) forget_stream(D, static_cast<hipStream_t>(s));
-    KRK_HIP(hipStreamDestroy(static_cast<hipStream_t>(s)));
+    if (Device* D = device_id((int)owner, &drc)) forget_stream(D, hs);
+    device_id(saved, &drc);  // the calling thread's current device is unchanged
+    KRK_HIP(hipStreamDestroy(hs));
     return KRK_OK;
 }
 int krk_stream_sync(void* s) {
@@ -1830,7 +1593,7 @@ int krk_device_clock_mhz(void* stream, double* mhz) {
     if (e == hipSuccess) e = hipMemcpyAsync(h, d_out, 24, hipMemcpyDeviceToHost, s);
     scratch_free(D, d_out, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "clock probe: %s", hipGetErrorString(e));
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "clock probe: %s", launch_error_text(e));
     KRK_CHECK(h[1] > 0, KRK_EHIP, "clock probe: no realtime ticks");
     *mhz = (double)h[0] / (double)h[1] * 100.0;
     return KRK_OK;

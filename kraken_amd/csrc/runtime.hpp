@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -325,26 +326,8 @@ inline int init_device(Device& D, int id) {
               "device %d is %s, this build targets gfx950 (MI355X)", id, prop.gcnArchName);
     D.cus = prop.multiProcessorCount;
     KRK_HIP(hipStreamCreateWithFlags(&D.s_main, hipStreamNonBlocking));
-    {
-        // KRK_STREAM_MODE (experiment): 0 plain streams; 1 s_a and s_b with a CU mask of
-        // every CU (a dedicated hardware queue each); 2 only s_b (the CRC side).
-        const char* m = getenv("KRK_STREAM_MODE");
-        const int mode = m ? atoi(m) : 0;
-        std::vector<uint32_t> all((D.cus + 31) / 32, 0xFFFFFFFFu);
-        // KRK_SA_PRIO (experiment): s_a (the SHA-256 launches) at another priority, i.e. on
-        // hardware queues of its own: streams of one priority share GPU_MAX_HW_QUEUES queues,
-        // and a copy queued on a stream that shares s_a's queue waits behind its kernel.
-        const char* sp = getenv("KRK_SA_PRIO");
-        const int sa_prio = sp ? atoi(sp) : 0;
-        int least = 0, greatest = 0;
-        if (sa_prio) KRK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        if (mode == 1) KRK_HIP(hipExtStreamCreateWithCUMask(&D.s_a, (uint32_t)all.size(), all.data()));
-        else if (sa_prio)
-            KRK_HIP(hipStreamCreateWithPriority(&D.s_a, hipStreamNonBlocking, sa_prio < 0 ? greatest : least));
-        else KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
-        if (mode == 1 || mode == 2) KRK_HIP(hipExtStreamCreateWithCUMask(&D.s_b, (uint32_t)all.size(), all.data()));
-        else KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
-    }
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_a, hipStreamNonBlocking));
+    KRK_HIP(hipStreamCreateWithFlags(&D.s_b, hipStreamNonBlocking));
     std::vector<uint32_t> tabs(kTabWords);
     make_slice_tables(tabs.data() + kTabT);
     const X8Pow& xp = x8();
@@ -652,7 +635,7 @@ inline int run_items(Device* D, const CrcBatch& B, uint32_t* sums_dev, hipStream
     hipError_t e = timed(K_CRC, s, [&] { return launch_crc_items(w, D->d_tabs, sums_dev, cfg, s); });
     scratch_free(D, d_next, s);
     scratch_free(D, d_pack, s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", hipGetErrorString(e));
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "crc32_pieces launch: %s", launch_error_text(e));
     return KRK_OK;
 }
 
@@ -689,7 +672,7 @@ inline int run_jobs(Device* D, std::vector<ShaJob>& jobs, uint8_t* digests_dev, 
                              state_dev, s);
     });
     scratch_free(D, d_jobs, s);
-    KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", hipGetErrorString(e));
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", launch_error_text(e));
     return KRK_OK;
 }
 
@@ -717,7 +700,8 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 //    hashed AND piece-summed in place and never uploaded (krk_metainfo_digest_host) --
 //    the batch's bytes over the host link shrink by theirs.
 enum OffMode { kOffDevice = 0, kOffHostSha = 1, kOffHostWhole = 2 };
-int offload_threads();
+// Host threads the offload of a `mode` batch may use (krk_set_sha_host_offload; 0 = off).
+int offload_threads(int mode = kOffDevice);
 // What the planners know about this box (offload.cpp): per-stream SHA-256 rate of each
 // AUTO tier at full residency (eight / two / one lane(s)), pinned D2H / H2D, one host
 // thread's SHA-256 and CRC-32; measured on the device at first use.
@@ -728,12 +712,39 @@ struct Rates {
     int source;  // KRK_RATES_*
 };
 Rates planner_rates(Device* D);  // D == nullptr: the override or the nominal rates
+int calibrate_device(Device* D);  // (re)measure D's rates now (krk_init, krk_planner_calibrate)
 int host_cpu_budget();           // CPUs this process may use: affinity, cgroup quota, OMP_NUM_THREADS
 // Host threads a call on this thread may use (0: host_cpu_budget()): a *_multi worker runs
 // with its share of the budget, so N devices' workers do not start N x 16 copy threads.
 inline thread_local int t_host_share = 0;
 inline int host_threads_for_call() { return t_host_share > 0 ? t_host_share : host_cpu_budget(); }
 uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);  // host_meta.cpp
+// One host thread's rates, bytes/s, each measured once per process on 16 MiB (offload.cpp;
+// no device needed): SHA-256 (x86 SHA extensions), CRC-32 (PCLMUL folding), memcpy.
+double host_sha_rate();
+double host_crc_rate();
+double host_copy_rate();
+
+// The process's host worker pool (host_pool.cpp, host_cpu_budget() - 1 threads).  A batch
+// of n items runs on up to `helpers` pool threads idle at construction and on the thread
+// that calls join() (which returns once all n are done; the destructor joins).  Items are
+// claimed one at a time, so a busy pool delays nobody.
+struct HostJob;
+class HostBatch {
+  public:
+    HostBatch(size_t n, int helpers, std::function<void(size_t)> f);
+    ~HostBatch() { join(); }
+    void join();
+
+  private:
+    std::shared_ptr<HostJob> j_;
+};
+int host_pool_idle();  // pool threads idle right now (not yet promised to a batch)
+void host_parallel_for(size_t n, int helpers, std::function<void(size_t)> f);
+// crc(A||B) from crc(A), crc(B), |B| (crc32.Update values).
+uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+// crc32.Update(crc, p[0, n)) with idle pool threads taking spans of a large buffer.
+uint32_t host_crc32_update_par(uint32_t crc, const uint8_t* p, size_t n);
 double host_link(const Rates& R);
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode = kOffDevice);

@@ -170,9 +170,7 @@ sha256_multi_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* _
 // 4 slots) or kSlots2 slots (two lanes per stream, where each producer step
 // builds two blocks), see produce_step.
 constexpr int kSlots = 4;
-#ifndef KRK_RING2
-#define KRK_RING2 3  // ring4 experiment build: 4 (80 KiB a pair, 160 KiB a two-pair workgroup)
-#endif
+#define KRK_RING2 3  // two-lane ring slots (a ring one slot deeper measured 0.4 % slower, profiles/r03/c3_ring4_ab.txt)
 constexpr int kSlots2 = 2 * KRK_RING2;  // two lanes: block positions in the ring ...
 constexpr int kRing2 = kSlots2 / 2;     // ... in 3 slots, two blocks per slot (A / E columns)
 constexpr int kSlotWords = 64 * 64;  // 64 rounds x 64 lanes
@@ -506,108 +504,14 @@ __device__ __forceinline__ void sha2_quad(uint32_t& R0, uint32_t& R1, uint32_t& 
     (void)t3;
 }
 
-// The 64 rounds of one block on a lane pair: 66 instruction-rounds (the A lane
-// idles in the first two, the E lane in the last two).  h[] = this lane's half of
-// the state, fed forward at the end: E holds (H4, H5, H6, H7), A holds
-// (H2, H3, H0, H1) -- index k ^ 2 -- so that both lanes enter the first round from
-// h[0], h[1] and feed h[0], h[1] forward from the same registers (no per-lane
-// selects there; only h[2], h[3] need one).  W is read from LDS
-// slot cslot (the E lanes: the block's ring slot; the A lanes: the all-1 slot).
-// Quads 0..kAhead-1 arrive already loaded in k[]; the rest are read kAhead quads
-// ahead (quad q+1's first W feeds quad q's last z, so the read of quad q+1 must have
-// landed when quad q starts: issued one quad before its use it stalled ~230 cycles a
-// block), and quads 0..kAhead-1 of the next block (slot ncslot) are read into k[]
-// during the last quads.
-#ifndef KRK_SHA_AHEAD
+// The W read-ahead: a consumer reads KW quads kAhead quads before their use (quad q+1's
+// first W feeds quad q's last z, so its read must have landed when quad q starts: issued
+// one quad before its use it stalled ~230 cycles a block in round 1's one-block-a-step
+// two-lane consumer), and the next block's first kAhead quads during the last ones.
 #define KRK_SHA_AHEAD 3
-#endif
 constexpr int kAhead = KRK_SHA_AHEAD;
-#ifndef KRK_SHA2_PIPELINED
-#define KRK_SHA2_PIPELINED 1  // two-lane consumer: blocks pipelined (block2p) instead of rounds2
-#endif
-#ifndef KRK_SHA8_UNROLL
 #define KRK_SHA8_UNROLL 4  // eight-lane consumer: blocks per loop iteration
-#endif
 static_assert(kAhead >= 2 && kAhead <= 8, "read-ahead distance");
-__device__ __forceinline__ void rounds2(uint32_t h[4], const uint32_t* lds, uint32_t cbase, uint32_t nbase,
-                                        uint32_t lane, const TwoLaneConst& c, bool is_e, u32x4 k[kAhead]) {
-    // Instruction-rounds 0 and 1: E runs rounds 0, 1 on (e, f, g, h); the A lane's
-    // x1 must show d = H3 then H2 to it, and its x0 must be a = H0 when round 0 of
-    // its own starts, so A starts at (H2, H3) and its two results are replaced by
-    // H1 and H0.
-    uint32_t R0 = h[0], R3 = h[1], R2 = h[2], R1 = h[3], z;
-    // W ring: quad q lives in wq[q % kRS]
-    constexpr int kRS = kAhead + 1;
-    u32x4 wq[kRS];
-#pragma unroll
-    for (int j = 1; j < kAhead; ++j) wq[j] = k[j];
-#ifdef KRK_SHA_NOLDS  // diagnostic: W from registers (wrong digests) -- prices the LDS reads
-    wq[kAhead] = u32x4{3u, lane, cbase, 7u};
-#else
-    wq[kAhead] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * kAhead);
-#endif
-    {
-        uint32_t t1, t2, t3, kk, p;
-        // s_nop 0 + the xad: two wait states before the DPP read of R3.
-        asm volatile("s_nop 0\n\t"
-                     "v_xad_u32 %[z], %[R1], %[ma], %[w0]\n\t"
-                     KRK_SHA2_ROUND(R0, R3, R2, R1, w1)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w0] "v"(k[0][0]), [w1] "v"(k[0][1]));
-        (void)t3;
-    }
-    R1 = is_e ? R1 : h[3];
-    {
-        uint32_t t1, t2, t3, kk, p;
-        asm volatile(KRK_SHA2_ROUND(R1, R0, R3, R2, w2)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w2] "v"(k[0][2]));
-        (void)t3;
-    }
-    R2 = is_e ? R2 : h[2];
-    {
-        uint32_t t1, t2, t3, kk, p;
-        asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
-                     KRK_SHA2_ROUND(R3, R2, R1, R0, w4)
-                     KRK_SHA2_OPERANDS
-                     : KRK_SHA2_CONSTS, [w3] "v"(k[0][3]), [w4] "v"(k[1][0]));
-        (void)t3;
-    }
-#pragma unroll
-    for (int q = 1; q < 16; ++q) {
-        if (q + kAhead < 16) {
-#ifdef KRK_SHA_NOLDS
-            wq[(q + kAhead) % kRS] = u32x4{(uint32_t)q, lane, cbase, 7u};
-#else
-            wq[(q + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (q + kAhead));
-#endif
-        }
-        // The next block's first kAhead quads, read unconditionally (a slot is always
-        // mapped LDS; past the last block the values go unused) so that no branch
-        // sinks them to the end of the block, where their latency would be exposed.
-        if (q >= 16 - kAhead)
-            k[q - (16 - kAhead)] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (q - (16 - kAhead)));
-        const u32x4& cur = wq[q % kRS];
-        sha2_quad(R0, R1, R2, R3, z, c, cur[1], cur[2], cur[3], q + 1 < 16 ? wq[(q + 1) % kRS][0] : c.one_a);
-    }
-    // Instruction-rounds 64, 65: A runs rounds 62, 63 into T1, T2 (W = 1 on A lanes);
-    // the E lanes' registers keep their final state.
-    uint32_t T1, T2;
-    {
-        uint32_t t1, t2, t3, kk, p;
-        asm volatile(KRK_SHA2_ROUND(R0, R3, R2, T1, w)
-                     KRK_SHA2_ROUND(T1, R0, R3, T2, w)
-                     KRK_SHA2_OPERANDS, [T1] "=&v"(T1), [T2] "=&v"(T2)
-                     : KRK_SHA2_CONSTS, [w] "v"(c.one_a));
-        (void)t3;
-    }
-    // E: (e, f, g, h) = (R0, R3, R2, R1); A: (a, b, c, d) = (T2, T1, R0, R3) into
-    // its (H2, H3, H0, H1) order.
-    h[0] += R0;
-    h[1] += R3;
-    h[2] += is_e ? R2 : T2;
-    h[3] += is_e ? R1 : T1;
-}
 
 // Rounds n = 4j + 2 .. 4j + 5 of an eight-lane block (block8p), the register roles of
 // instruction-rounds 2 .. 5: W operands are W[n + 1] for the z of the next round.
@@ -621,25 +525,14 @@ __device__ __forceinline__ void sha8_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
                  : KRK_SHA8_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
 }
 
-// W quads a read group of the eight-lane consumer covers (KRK_SHA8_GROUP): 3 (default) =
-// three quads read between 12-round asm blocks, four quads ahead (a group's last block
+// W read groups of the eight-lane consumer: three quads read between 12-round asm blocks, four quads ahead (a group's last block
 // needs quad j + 3, read one group earlier), so ONE s_waitcnt precedes every 12 rounds;
 // 1 = one read and one wait per 4 rounds (round 2's first form).  C2-shaped A/B on one
 // box (profiles/r02/sha8_read_groups.jsonl): 56.2 MB/s a stream with one read a group,
 // 57.2 with pairs, 58.7 with threes, 58.3 with fives (two asm statements a group); the
 // threes' reads issued mid-way through the previous group (two six-round statements)
 // instead of right before its wait: 59.1 vs 59.2 (profiles/r02/sha8_read_split.jsonl).
-#ifndef KRK_SHA8_GROUP
-#define KRK_SHA8_GROUP 3
-#endif
-static_assert(KRK_SHA8_GROUP == 1 || KRK_SHA8_GROUP == 3, "read group of the eight-lane consumer");
-#if KRK_SHA8_GROUP == 3 && !defined(KRK_SHA_NOLDS)
-#define KRK_SHA8_G3 1
 constexpr int kAhead8 = 4;
-#else
-#define KRK_SHA8_G3 0
-constexpr int kAhead8 = kAhead;
-#endif
 // Twelve eight-lane rounds, n = 4j + 2 .. 4j + 13: W quads a = j, b = j + 1, d = j + 2,
 // e = j + 3 (each block of four takes its first quad's last word and the next quad's
 // first three).
@@ -688,14 +581,13 @@ __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2
     u32x4 wq[kRS];
 #pragma unroll
     for (int j = 0; j < kAhead8; ++j) wq[j] = k[j];
-    // Rounds n = 2 .. 61.  Production (KRK_SHA8_GROUP 3): 5 asm blocks of twelve rounds,
+    // Rounds n = 2 .. 61: 5 asm blocks of twelve rounds,
     // the next three W quads read before each (four quads ahead), so one s_waitcnt per
     // twelve rounds.  Otherwise 15 asm blocks of four, n = 4j + 2 .. 4j + 5 (W: quad j's
     // last word, quad j + 1's first three), each W read between two blocks -- two rounds
     // into a W quad (issued right before a W quad's rounds a read cost ~16 cycles of the
     // wave's stream, two rounds in ~8, tools/micro/sha8lds.hip); the read + its wait
     // between two asm blocks are the two wait states the hazard recognizer would pad.
-#if KRK_SHA8_G3
     constexpr int RS = kAhead8 + 3;
     u32x4 wr[RS];
 #pragma unroll
@@ -712,28 +604,7 @@ __device__ __forceinline__ void block8p(uint32_t& R0, uint32_t& R1, uint32_t& R2
         sha8_dodec2(R0, R1, R2, R3, z, c, wr[j % RS], wr[(j + 1) % RS], wr[(j + 2) % RS], wr[(j + 3) % RS]);
     }
     wq[15 % kRS] = wr[15 % RS];
-#else
-#pragma unroll
-    for (int j = 0; j < 15; ++j) {
-#ifdef KRK_SHA_NOLDS
-        if (j + kAhead < 16) wq[(j + kAhead) % kRS] = u32x4{(uint32_t)j, cbase, 5u, 7u};
-        else k[j + kAhead - 16] = u32x4{(uint32_t)j, nbase, 5u, 7u};
-#else
-        if (j + kAhead < 16)
-            wq[(j + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (j + kAhead));
-        else  // the next block's first quads
-            k[j + kAhead - 16] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (j + kAhead - 16));
-#endif
-        const u32x4& a = wq[j % kRS];
-        const u32x4& b = wq[(j + 1) % kRS];
-        sha8_quad2(R0, R1, R2, R3, z, c, a[3], b[0], b[1], b[2]);
-    }
-#endif
-#ifdef KRK_SHA_NOLDS
-    k[kAhead8 - 1] = u32x4{15u, nbase, 5u, 7u};
-#else
     k[kAhead8 - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead8 - 1));
-#endif
     {
         uint32_t t1, t2, kk, p;  // n = 62, 63
         asm volatile(KRK_SHA8_ROUND(R2, R1, R0, R3, w3)
@@ -825,22 +696,11 @@ __device__ __forceinline__ void sha2_quad2(uint32_t& R0, uint32_t& R1, uint32_t&
                  : KRK_SHA2_CONSTS, [w1] "v"(w1), [w2] "v"(w2), [w3] "v"(w3), [w4] "v"(w4));
 }
 
-// The two-lane consumer's W read group (KRK_SHA2_GROUP): 3 (default) = as the eight-lane
-// KRK_SHA8_GROUP 3 (three quads read four ahead, twelve rounds a wait); 1 = one read and
-// one wait per four rounds.  Same-box A/B (profiles/r02/sha2_read_groups.jsonl): 16,384
+// The two-lane consumer's W read groups: as the eight-lane consumer's (three quads read
+// four ahead, twelve rounds a wait) instead of one read and one wait per four rounds.  Same-box A/B (profiles/r02/sha2_read_groups.jsonl): 16,384
 // streams 49.7 -> 51.6 MB/s a stream, 8,192 streams 50.4 -> 51.9 (pairs were 0.5 % slower
 // than one read a quad).
-#ifndef KRK_SHA2_GROUP
-#define KRK_SHA2_GROUP 3
-#endif
-static_assert(KRK_SHA2_GROUP == 1 || KRK_SHA2_GROUP == 3, "read group of the two-lane consumer");
-#if KRK_SHA2_GROUP == 3 && KRK_SHA2_PIPELINED && !defined(KRK_SHA_NOLDS)
-#define KRK_SHA2_G3 1
 constexpr int kAhead2 = 4;
-#else
-#define KRK_SHA2_G3 0
-constexpr int kAhead2 = kAhead;
-#endif
 __device__ __forceinline__ void sha2_dodec2(uint32_t& R0, uint32_t& R1, uint32_t& R2, uint32_t& R3, uint32_t& z,
                                             const TwoLaneConst& c, const u32x4& a, const u32x4& b, const u32x4& d,
                                             const u32x4& e) {
@@ -894,7 +754,6 @@ __device__ __forceinline__ void block2p(uint32_t& R0, uint32_t& R1, uint32_t& R2
     // wave's stream, two rounds in ~8, its code bytes (tools/micro/sha8lds.hip,
     // profiles/r02/micro_sha8lds.txt); and the read + its wait between two asm blocks
     // are the two wait states the hazard recognizer would otherwise pad there.
-#if KRK_SHA2_G3
     constexpr int RS = kAhead2 + 3;
     u32x4 wr[RS];
 #pragma unroll
@@ -911,28 +770,7 @@ __device__ __forceinline__ void block2p(uint32_t& R0, uint32_t& R1, uint32_t& R2
         sha2_dodec2(R0, R1, R2, R3, z, c, wr[j % RS], wr[(j + 1) % RS], wr[(j + 2) % RS], wr[(j + 3) % RS]);
     }
     wq[15 % kRS] = wr[15 % RS];
-#else
-#pragma unroll
-    for (int j = 0; j < 15; ++j) {
-#ifdef KRK_SHA_NOLDS
-        if (j + kAhead < 16) wq[(j + kAhead) % kRS] = u32x4{(uint32_t)j, cbase, 5u, 7u};
-        else k[j + kAhead - 16] = u32x4{(uint32_t)j, nbase, 5u, 7u};
-#else
-        if (j + kAhead < 16)
-            wq[(j + kAhead) % kRS] = *reinterpret_cast<const u32x4*>(lds + cbase + 256 * (j + kAhead));
-        else  // the next block's first quads
-            k[j + kAhead - 16] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (j + kAhead - 16));
-#endif
-        const u32x4& a = wq[j % kRS];
-        const u32x4& b = wq[(j + 1) % kRS];
-        sha2_quad2(R0, R1, R2, R3, z, c, a[3], b[0], b[1], b[2]);
-    }
-#endif
-#ifdef KRK_SHA_NOLDS
-    k[kAhead2 - 1] = u32x4{15u, nbase, 5u, 7u};
-#else
     k[kAhead2 - 1] = *reinterpret_cast<const u32x4*>(lds + nbase + 256 * (kAhead2 - 1));
-#endif
     {
         uint32_t t1, t2, t3, kk, p;  // n = 62, 63
         asm volatile(KRK_SHA2_ROUND(R2, R1, R0, R3, w3)
@@ -1125,11 +963,6 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         const uint32_t einc = is_e ? uint32_t(kSlotWords) : 0u;
         uint32_t vslot = 0, slot = 0;
         u32x4 kq[kAhead2] = {};
-#ifdef KRK_SHA_CYCLES  // diagnostic build (make cycles): consumer cycles per block
-        const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
-        uint64_t cyc_bar = 0, cyc_rounds = 0;
-#endif
-#if KRK_SHA2_PIPELINED
         // Blocks pipelined (block2p): 64 instruction-rounds a block, each half's chaining
         // value on its own lanes (0 on the other half).
         uint32_t hE[4], hA[4];
@@ -1144,63 +977,27 @@ sha256_ws_kernel(const ShaJob* __restrict__ jobs, uint32_t n_jobs, uint8_t* __re
         auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
             block2p(R0, R1, R2, R3, z, hE, hA, mineE, mineA, i, ring, cur, nxt, c, kq);
         };
-#else
-        auto block = [&](uint32_t i, uint32_t cur, uint32_t nxt) {
-            uint32_t x[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) x[k] = h[k];
-            rounds2(x, ring, cur, nxt, lane, c, is_e, kq);
-            if (i < common) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) h[k] = x[k];
-            } else if (i < mine) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) h[k] = x[k];
-            }
-        };
-#endif
         if (nb) {  // step 0's barrier, the first quads, and (pipelined) rounds 0, 1 of block 0
             if (kTiming == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int q = 0; q < kAhead2; ++q) kq[q] = *reinterpret_cast<const u32x4*>(ring + base_even + 256 * q);
-#if KRK_SHA2_PIPELINED
             prologue2p(R0, R1, R2, R3, z, h, is_e, c, kq[0]);
-#endif
         }
         for (uint32_t i = 0; i < nb; i += 2) {
-#ifdef KRK_SHA_CYCLES
-            const uint64_t cb0 = __builtin_amdgcn_s_memtime();
-#endif
             if (i) {
                 if (kTiming == 0) __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
             }
-#ifdef KRK_SHA_CYCLES
-            const uint64_t cb1 = __builtin_amdgcn_s_memtime();
-#endif
             const uint32_t nslot = slot == kRing2 - 1 ? 0u : slot + 1;
             const uint32_t nvslot = slot == kRing2 - 1 ? 0u : vslot + einc;
             block(i, base_even + vslot, base_odd + vslot);
             if (i + 1 < nb) block(i + 1, base_odd + vslot, base_even + nvslot);
             slot = nslot;
             vslot = nvslot;
-#ifdef KRK_SHA_CYCLES
-            const uint64_t cb2 = __builtin_amdgcn_s_memtime();
-            cyc_bar += cb1 - cb0;
-            cyc_rounds += cb2 - cb1;
-#endif
         }
-#ifdef KRK_SHA_CYCLES
-        if (blockIdx.x == 0 && lane == 0 && nb)
-            printf("KRK_SHA_CYCLES timing=%d two=1 blocks=%u cycles/block=%.1f barrier+setup=%.1f rounds2=%.1f\n",
-                   kTiming, nb, (double)(__builtin_amdgcn_s_memtime() - cyc0) / nb, (double)cyc_bar / nb,
-                   (double)cyc_rounds / nb);
-#endif
-#if KRK_SHA2_PIPELINED
 #pragma unroll
         for (int k = 0; k < 4; ++k) h[k] = is_e ? hE[k] : hA[k];
-#endif
         if (live) {
             uint32_t hs[4];  // back to H order (A lanes hold H[k ^ 2] in h[k])
 #pragma unroll
@@ -1536,7 +1333,7 @@ static hipError_t launch_w8(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_di
     });
     if (attr_err != hipSuccess) return attr_err;
     constexpr uint32_t per = 8u * kGroups;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * kGroups), lds, s, jobs, n_jobs, out_digest,
                        out_state);
     return hipGetLastError();
@@ -1555,7 +1352,7 @@ static hipError_t launch_ws(const ShaJob* jobs, uint32_t n_jobs, uint8_t* out_di
     });
     if (attr_err != hipSuccess) return attr_err;
     constexpr uint32_t per = (kTwo ? 32u : 64u) * kGroups;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(k, dim3((n_jobs + per - 1) / per), dim3(128 * kGroups), lds, s, jobs, n_jobs, out_digest,
                        out_state);
     return hipGetLastError();
@@ -1583,7 +1380,7 @@ hipError_t launch_sha256_plan(int plan, const ShaJob* jobs, uint32_t n_jobs, uin
         // diagnostics (WRONG digests except 100): rounds-only consumer (102 one lane, 104 two
         // lanes), producer-only (105 / 106), producer without global loads (107)
         case 100:
-            (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+            if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
             hipLaunchKernelGGL(sha256_multi_kernel, dim3((n_jobs + 63) / 64), dim3(64), 0, s, jobs, n_jobs,
                                out_digest, out_state);
             return hipGetLastError();
@@ -1613,7 +1410,7 @@ __global__ void __launch_bounds__(256) digest_scatter_kernel(const uint8_t* __re
 
 hipError_t launch_digest_scatter(const uint8_t* rec, uint32_t n, uint8_t* digests, hipStream_t s) {
     if (!n) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(digest_scatter_kernel, dim3((n * 32 + 255) / 256), dim3(256), 0, s, rec, n, digests);
     return hipGetLastError();
 }

@@ -1,0 +1,270 @@
+// staging.hpp -- internal to libkraken_hip: the pinned staging windows of the host
+// paths (host buffers and files -> pinned host window -> device window -> kernels), and
+// the host-side fills of a window (copies, file reads) spread over the host pool.
+#pragma once
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <chrono>
+
+#include "runtime.hpp"
+
+namespace krk {
+
+// Device allocations of one host-path call, freed on every return path (hipFree
+// waits for the device, so work still queued on them on an error path is drained).
+struct DevMem {
+    std::vector<void*> ps;
+    ~DevMem() {
+        for (void* p : ps) hipFree(p);
+    }
+    template <class T>
+    hipError_t alloc(T** p, size_t n) {
+        void* v = nullptr;
+        const hipError_t e = hipMalloc(&v, n);
+        if (e == hipSuccess) ps.push_back(v);
+        *p = static_cast<T*>(v);
+        return e;
+    }
+};
+
+// ------------------------------------------------------------------ host staging pipeline
+// Two pinned host windows and two device windows; window k is refilled only after
+// the kernel that consumed it (event) has finished.
+struct Window {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t copied = nullptr;    // the H2D out of `host` has finished: host buffer reusable
+    hipEvent_t consumed = nullptr;  // single-stream users: all work reading `dev` has finished
+    hipEvent_t done[2] = {nullptr, nullptr};  // kernels reading `dev`, one event per kernel stream
+    bool inflight = false, copying = false;
+    bool done_pending[2] = {false, false};
+};
+
+// Two pinned host windows and two device windows.  The host side of window k is
+// refilled once its H2D is done; the H2D into its device side waits (on the copy
+// stream only) for the kernels that read the previous contents, so the upload of
+// window k+1 overlaps the kernels of window k.
+struct CopyTask {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+
+struct Pipeline {
+    Window w[2];
+    ~Pipeline() {
+        for (auto& x : w) {
+            if (x.inflight) hipEventSynchronize(x.consumed);
+            if (x.copying) hipEventSynchronize(x.copied);
+            for (int i = 0; i < 2; ++i)
+                if (x.done_pending[i]) hipEventSynchronize(x.done[i]);
+            if (x.host) hipHostFree(x.host);
+            if (x.dev) hipFree(x.dev);
+            if (x.copied) hipEventDestroy(x.copied);
+            if (x.consumed) hipEventDestroy(x.consumed);
+            for (auto e : x.done)
+                if (e) hipEventDestroy(e);
+        }
+    }
+    int init(size_t cap) {
+        for (auto& x : w) {
+            x.cap = cap;
+            KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&x.host), cap, hipHostMallocDefault));
+            KRK_HIP(hipMalloc(reinterpret_cast<void**>(&x.dev), cap));
+            KRK_HIP(hipEventCreateWithFlags(&x.copied, hipEventDisableTiming));
+            KRK_HIP(hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming));
+            for (auto& e : x.done) KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        return KRK_OK;
+    }
+    // Host side of window k is free for refilling.
+    int acquire(int k) {
+        if (w[k].inflight) {
+            KRK_HIP(hipEventSynchronize(w[k].consumed));
+            w[k].inflight = false;
+        }
+        if (w[k].copying) {
+            KRK_HIP(hipEventSynchronize(w[k].copied));
+            w[k].copying = false;
+        }
+        return KRK_OK;
+    }
+    // Upload n bytes of window k on cp, after the kernels that read its last contents.
+    hipError_t h2d(int k, size_t n, hipStream_t cp) {
+        Window& x = w[k];
+        for (int i = 0; i < 2; ++i)
+            if (x.done_pending[i]) {
+                hipError_t e = hipStreamWaitEvent(cp, x.done[i], 0);
+                if (e != hipSuccess) return e;
+                x.done_pending[i] = false;
+            }
+        hipError_t e = hipMemcpyAsync(x.dev, x.host, n, hipMemcpyHostToDevice, cp);
+        if (e == hipSuccess) e = hipEventRecord(x.copied, cp);
+        if (e == hipSuccess) x.copying = true;
+        return e;
+    }
+    // The caller's pinned bytes DMA'd straight into device window k (tasks' dst are
+    // device addresses in it), after the kernels that read its last contents.
+    hipError_t h2d_direct(int k, const std::vector<CopyTask>& tasks, hipStream_t cp) {
+        Window& x = w[k];
+        for (int i = 0; i < 2; ++i)
+            if (x.done_pending[i]) {
+                hipError_t e = hipStreamWaitEvent(cp, x.done[i], 0);
+                if (e != hipSuccess) return e;
+                x.done_pending[i] = false;
+            }
+        for (const auto& t : tasks) {
+            hipError_t e = hipMemcpyAsync(t.dst, t.src, t.n, hipMemcpyHostToDevice, cp);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipEventRecord(x.copied, cp);
+        if (e == hipSuccess) x.copying = true;
+        return e;
+    }
+    // Kernel stream ks (slot 0 or 1) has enqueued everything that reads window k.
+    hipError_t release(int k, int slot, hipStream_t ks) {
+        hipError_t e = hipEventRecord(w[k].done[slot], ks);
+        if (e == hipSuccess) w[k].done_pending[slot] = true;
+        return e;
+    }
+};
+
+// KRK_TRACE=1: host-side phase times of the windowed host paths, to stderr.
+inline bool trace_on() {
+    static const bool on = getenv("KRK_TRACE") && atoi(getenv("KRK_TRACE")) > 0;
+    return on;
+}
+inline double wall_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+inline size_t window_bytes() {
+    const char* v = getenv("KRK_WINDOW_MB");
+    size_t mb = v ? strtoull(v, nullptr, 10) : 512;
+    if (mb < 1) mb = 1;
+    return mb << 20;
+}
+
+// The device's persistent staging windows (grown to at least `cap`) for one host-path
+// call; a concurrent second caller, or a call wanting windows above 1 GiB, gets
+// private windows (freed when the call returns) instead.
+struct StagingLease {
+    Device* D = nullptr;
+    Pipeline* p = nullptr;
+    std::unique_ptr<Pipeline> own;
+    bool locked = false;
+    ~StagingLease() {
+        if (locked) D->staging_mu.unlock();
+    }
+};
+
+inline int lease_staging(Device* D, size_t cap, StagingLease& L) {
+    L.D = D;
+    constexpr size_t kKeepMax = size_t(1) << 30;  // windows kept across calls: at most 2 x 1 GiB pinned
+    if (cap <= kKeepMax && D->staging_mu.try_lock()) {
+        L.locked = true;
+        if (!D->staging || D->staging->w[0].cap < cap) {
+            delete D->staging;  // its destructor drains the old windows' events
+            D->staging = nullptr;
+            auto p = std::make_unique<Pipeline>();
+            int r = p->init(cap);
+            if (r) return r;
+            D->staging = p.release();
+        }
+        L.p = D->staging;
+        return KRK_OK;
+    }
+    L.own = std::make_unique<Pipeline>();
+    L.p = L.own.get();
+    return L.own->init(cap);
+}
+
+// Host -> pinned staging copies of one window, split over the calling thread and the host
+// pool's idle threads (one host thread's memcpy is well below the PCIe rate).
+// KRK_COPY_THREADS overrides the split.
+
+inline unsigned copy_threads() {
+    const char* v = getenv("KRK_COPY_THREADS");
+    if (v) return std::max(1u, (unsigned)strtoul(v, nullptr, 10));
+    return std::max(1u, std::min(16u, (unsigned)host_threads_for_call()));
+}
+
+inline void par_copy(const std::vector<CopyTask>& tasks) {
+    size_t total = 0;
+    for (const auto& t : tasks) total += t.n;
+    const unsigned T = copy_threads();
+    if (T == 1 || total < (8u << 20)) {
+        for (const auto& t : tasks) memcpy(t.dst, t.src, t.n);
+        return;
+    }
+    // Cut the concatenated byte range into T equal spans.
+    auto run = [&](size_t lo, size_t hi) {
+        size_t pos = 0;
+        for (const auto& t : tasks) {
+            const size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
+            if (a < b) memcpy(t.dst + (a - pos), t.src + (a - pos), b - a);
+            pos += t.n;
+            if (pos >= hi) break;
+        }
+    };
+    // spans on the calling thread and the host pool's idle threads
+    const size_t span = (total + T - 1) / T;
+    host_parallel_for(T, (int)T - 1, [&](size_t i) { run(i * span, std::min(total, (i + 1) * span)); });
+}
+
+// File -> pinned window reads of one window, split over the copy threads at
+// 1 MiB-aligned spans (O_DIRECT needs block-aligned offsets and lengths; every
+// task starts 4 KiB-aligned in both the file and the window).
+struct ReadTask {
+    int fd;
+    uint64_t off;   // file offset
+    uint8_t* dst;
+    size_t n;       // bytes wanted (O_DIRECT reads round the last block up)
+    size_t blob;    // index into the caller's files (for the error message)
+};
+
+// Returns -1 on success, else the index of the failed task; err = its errno (0 = EOF).
+inline long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) {
+    // Spans are cut in a stream of the tasks laid end to end, each padded to 4 KiB
+    // when direct, so every span boundary falls on a block boundary of its task.
+    auto padded = [direct](size_t n) { return direct ? (n + 4095) & ~size_t(4095) : n; };
+    size_t total = 0;
+    for (const auto& t : tasks) total += padded(t.n);
+    std::atomic<long> bad{-1};
+    std::atomic<int> bad_errno{0};
+    auto run = [&](size_t lo, size_t hi) {
+        size_t pos = 0;
+        for (size_t i = 0; i < tasks.size() && pos < hi; pos += padded(tasks[i].n), ++i) {
+            const ReadTask& t = tasks[i];
+            size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
+            if (a >= b) continue;
+            a -= pos;
+            b -= pos;
+            while (a < b) {
+                size_t want = b - a;
+                if (direct) want = (want + 4095) & ~size_t(4095);
+                const ssize_t got = pread(t.fd, t.dst + a, want, (off_t)(t.off + a));
+                if (got < 0 && errno == EINTR) continue;
+                if (got <= 0) {
+                    long expect = -1;
+                    bad.compare_exchange_strong(expect, (long)i);
+                    bad_errno.store(got < 0 ? errno : 0);
+                    return;
+                }
+                a += (size_t)got;
+            }
+        }
+    };
+    const unsigned T = (total < (8u << 20)) ? 1 : copy_threads();
+    constexpr size_t kAlign = size_t(1) << 20;
+    const size_t span = std::max(kAlign, ((total + T - 1) / T + kAlign - 1) & ~(kAlign - 1));
+    const size_t spans = (total + span - 1) / span;
+    host_parallel_for(spans, (int)spans - 1, [&](size_t i) { run(i * span, std::min(total, (i + 1) * span)); });
+    *err = bad_errno.load();
+    return bad.load();
+}
+
+}  // namespace krk

@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) synth_fill_chunks(const SynthChunk* __res
 
 hipError_t launch_synth_fill_chunks(const SynthChunk* chunks, uint32_t n_chunks, int variant, hipStream_t s) {
     if (!n_chunks) return hipSuccess;
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(synth_fill_chunks, dim3(n_chunks * kSynthBlocksPerChunk), dim3(256), 0, s, chunks, n_chunks,
                        variant);
     return hipGetLastError();
@@ -90,12 +90,12 @@ hipError_t launch_synth_fill_chunks(const SynthChunk* chunks, uint32_t n_chunks,
 hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint64_t n, int variant,
                              hipStream_t s) {
     if (!n) return hipSuccess;
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     uint64_t head = 0;
     if ((offset & 7) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         const uint64_t npairs = n / 16;
         if (npairs) {
             const uint64_t blocks = (npairs + 255) / 256;
-            (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
             hipLaunchKernelGGL(synth_fill_words, dim3((uint32_t)(blocks < 8192 ? blocks : 8192)), dim3(256),
                                0, s, reinterpret_cast<uint4*>(dst), seed, offset >> 3, npairs, variant);
         }
@@ -104,7 +104,6 @@ hipError_t launch_synth_fill(uint8_t* dst, uint64_t seed, uint64_t offset, uint6
     if (head < n) {
         const uint64_t rest = n - head;
         const uint64_t blocks = (rest + 255) / 256;
-        (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
         hipLaunchKernelGGL(synth_fill_bytes, dim3((uint32_t)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s,
                            dst + head, seed, offset + head, rest, variant);
     }
@@ -132,7 +131,7 @@ __global__ void __launch_bounds__(64) clock_probe_kernel(uint32_t spins, uint32_
 }
 
 hipError_t launch_clock_probe(uint32_t spins, uint64_t* out, hipStream_t s) {
-    (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
     hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, spins, 12345u, out);
     return hipGetLastError();
 }

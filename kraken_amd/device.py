@@ -250,7 +250,8 @@ def metainfo_digest(arena: BlobArena, out: BatchOutputs, stream=None):
 
 def set_sha_host_offload(threads: int):
     """krk_set_sha_host_offload: up to `threads` host threads take the longest SHA-256
-    chains of sha256 / metainfo_digest batches (0 = off, the default)."""
+    chains of sha256 / metainfo_digest batches (0 = off; -1 = AUTO, the default: the
+    planner-gated offload on the process's CPU budget)."""
     check(lib.krk_set_sha_host_offload(int(threads)))
 
 

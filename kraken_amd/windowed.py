@@ -162,7 +162,7 @@ class WindowedRun:
     double buffers), while the windows run the rest; their digests go into cb.digests at
     the end of run()."""
 
-    def __init__(self, D, ids, lens, P, W, cap=None, host_lane=None, device=0, sha_priority=None, cu_split=False):
+    def __init__(self, D, ids, lens, P, W, cap=None, host_lane=None, device=0, sha_priority=None):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = list(lens)
@@ -188,22 +188,7 @@ class WindowedRun:
         self.cb = D.ChunkedBatch(self.lens, P)
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
         D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
-        # cu_split: the generator on an eighth of the CUs (every eighth CU) and the windows'
-        # SHA-256 launches on the rest -- the CUs the window cap (7/8 of the two-lane count)
-        # leaves free to the piece-CRC launch -- so the generator's waves stop taking issue
-        # slots from the SHA waves they would otherwise share SIMDs with.
-        if cu_split and not k:
-            cus = C.c_int(0)
-            D.check(D.lib.krk_device_cus(C.byref(cus)))
-            nw = (cus.value + 31) // 32
-            free = np.zeros(nw, dtype=np.uint32)
-            rest = np.zeros(nw, dtype=np.uint32)
-            for cu in range(cus.value):
-                (free if cu % 8 == 7 else rest)[cu // 32] |= np.uint32(1 << (cu % 32))
-            D.check(D.lib.krk_stream_create_cu_mask(free.ctypes.data_as(C.POINTER(C.c_uint32)), nw, C.byref(self.gen_s)))
-            D.check(D.lib.krk_stream_create_cu_mask(rest.ctypes.data_as(C.POINTER(C.c_uint32)), nw, C.byref(self.sha_s)))
-        else:
-            D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
+        D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         # With the host lane, the windows' SHA-256 launches (up to ~0.6 s each) go on a
         # high-priority stream, i.e. hardware queues of their own: normal-priority streams
         # share GPU_MAX_HW_QUEUES queues, and the lane's D2H copies and generator / CRC

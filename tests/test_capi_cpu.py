@@ -75,16 +75,30 @@ def test_num_pieces_and_piece_length_config(orc):
 
 
 def test_device_entry_points_fail_loudly_without_gpu():
+    """Device entry points and the GPU placements are KRK_ENODEV without a gfx950 device:
+    nothing falls back to the CPU."""
     n = C.c_int(-1)
     check(lib.krk_device_count(C.byref(n)))
     if n.value > 0:
         pytest.skip("a GPU is visible")
     h = C.c_void_p()
-    assert lib.krk_digester_new(C.byref(h)) == KRK_ENODEV
-    assert lib.krk_piece_stream_begin(4, C.byref(h)) == KRK_ENODEV
+    assert lib.krk_digester_new_on(_capi.KRK_PLACE_GPU, C.byref(h)) == KRK_ENODEV
+    assert lib.krk_piece_stream_begin_on(_capi.KRK_PLACE_GPU, 4, C.byref(h)) == KRK_ENODEV
     out = C.c_uint32()
-    assert lib.krk_crc32_update(0, b"abc", 3, C.byref(out)) == KRK_ENODEV
+    big = b"x" * (1 << 20)
+    assert lib.krk_crc32_update_on(_capi.KRK_PLACE_GPU, 0, big, len(big), C.byref(out)) == KRK_ENODEV
     assert b"no HIP device" in lib.krk_last_error()
+    blob = (_capi.krk_blob * 1)(_capi.krk_blob(None, 0, 4, 0))
+    assert lib.krk_metainfo_digest_host(blob, 1, None, (C.c_uint8 * 32)()) == KRK_ENODEV
+    assert lib.krk_metainfo_digest_host_multi(blob, 1, None, (C.c_uint8 * 32)()) == KRK_ENODEV
+    assert lib.krk_piece_sums_dev(blob, 1, None, None) == KRK_ENODEV
+    # a process-wide GPU setting makes AUTO a forced GPU placement, which has no fallback
+    check(lib.krk_set_crc_placement(_capi.KRK_PLACE_GPU))
+    try:
+        assert lib.krk_piece_stream_begin(4, C.byref(h)) == KRK_ENODEV
+        assert lib.krk_crc32_update(0, big, len(big), C.byref(out)) == KRK_ENODEV
+    finally:
+        check(lib.krk_set_crc_placement(_capi.KRK_PLACE_AUTO))
 
 
 def _ih(P, sums, name, L):
@@ -223,19 +237,113 @@ def test_host_crossover_ni_matches_portable(tmp_path):
     assert runs[0].stdout == runs[1].stdout and len(runs[0].stdout.split()) == 10
 
 
-def test_streaming_constructors_need_a_device():
-    """Even the host placement of a Digester needs the gfx950 device the library
-    serves: without one every constructor is KRK_ENODEV (no CPU fallback)."""
+def test_host_placements_work_without_a_device():
+    """a host-placed Digester, piece stream and crc32.Update run the
+    product's own SHA-NI / PCLMUL code (host_meta.cpp, not the oracle) and need no device;
+    AUTO on a host without a gfx950 device is the host placement.  (On a GPU host the
+    same calls place by the crossover, tests/test_gpu_crossover.py.)"""
+    import hashlib
+    import zlib
     n = C.c_int(-1)
     check(lib.krk_device_count(C.byref(n)))
     if n.value > 0:
         pytest.skip("a GPU is visible")
+    rng = np.random.default_rng(21)
+    data = rng.integers(0, 256, (3 << 20) + 12345, dtype=np.uint8).tobytes()
+    for p in (_capi.KRK_PLACE_AUTO, _capi.KRK_PLACE_HOST):
+        h = C.c_void_p()
+        check(lib.krk_digester_new_on(p, C.byref(h)))
+        try:
+            where = C.c_int(-1)
+            check(lib.krk_digester_placement(h, C.byref(where)))
+            assert where.value == _capi.KRK_PLACE_HOST
+            for a in range(0, len(data), 1 << 19):  # io.Copy-like writes
+                chunk = data[a:a + (1 << 19) - 7]
+                check(lib.krk_digester_write(h, chunk, len(chunk)))
+            o = (C.c_uint8 * 32)()
+            check(lib.krk_digester_sum(h, o))
+            seen = b"".join(data[a:a + (1 << 19) - 7] for a in range(0, len(data), 1 << 19))
+            assert bytes(o) == hashlib.sha256(seen).digest()
+        finally:
+            lib.krk_digester_free(h)
+        for P in (1, 7, 1 << 20):
+            s = C.c_void_p()
+            check(lib.krk_piece_stream_begin_on(p, P, C.byref(s)))
+            try:
+                where = C.c_int(-1)
+                check(lib.krk_piece_stream_placement(s, C.byref(where)))
+                assert where.value == _capi.KRK_PLACE_HOST
+                blob = data[:200_001] if P < 8 else data
+                step = 65_537
+                for a in range(0, len(blob), step):
+                    check(lib.krk_piece_stream_update(s, blob[a:a + step], len(blob[a:a + step])))
+                ns, ln = C.c_uint64(), C.c_uint64()
+                check(lib.krk_piece_stream_end(s, None, 0, C.byref(ns), C.byref(ln)))
+                sums = (C.c_uint32 * ns.value)()
+                check(lib.krk_piece_stream_end(s, sums, ns.value, C.byref(ns), C.byref(ln)))
+                want = [zlib.crc32(blob[i:i + P]) for i in range(0, len(blob), P)]
+                assert ln.value == len(blob) and list(sums) == want, P
+            finally:
+                lib.krk_piece_stream_free(s)
+        out = C.c_uint32()
+        check(lib.krk_crc32_update_on(p, 12345, data, len(data), C.byref(out)))
+        assert out.value == zlib.crc32(data, 12345)
+    out = C.c_uint32()
+    check(lib.krk_crc32_update(7, data, len(data), C.byref(out)))  # AUTO, no device: host
+    assert out.value == zlib.crc32(data, 7)
     h = C.c_void_p()
-    for p in (_capi.KRK_PLACE_AUTO, _capi.KRK_PLACE_HOST, _capi.KRK_PLACE_GPU):
-        assert lib.krk_digester_new_on(p, C.byref(h)) == KRK_ENODEV
     assert lib.krk_digester_new_on(7, C.byref(h)) == _capi.KRK_EINVAL
-    blob = (_capi.krk_blob * 1)(_capi.krk_blob(None, 0, 4, 0))
-    assert lib.krk_metainfo_digest_host_multi(blob, 1, None, (C.c_uint8 * 32)()) == KRK_ENODEV
+    assert lib.krk_piece_stream_begin_on(1, 0, C.byref(h)) == _capi.KRK_EINVAL
+    assert lib.krk_last_error() == b"piece length must be positive"
+
+
+def test_host_crc_spans_on_the_pool_match_zlib():
+    """Large host-placed writes are cut into spans that idle host-pool threads hash beside
+    the caller (host_pool.cpp); the spans' CRCs recombine (GF(2) shift + xor) to exactly
+    crc32.Update of the whole write, across piece ends and with seeds."""
+    import zlib
+    rng = np.random.default_rng(23)
+    data = rng.integers(0, 256, (37 << 20) + 4321, dtype=np.uint8).tobytes()
+    for seed in (0, 0xDEADBEEF):
+        for n in (2 << 20, (2 << 20) + 1, (9 << 20) + 77, len(data)):
+            out = C.c_uint32()
+            check(lib.krk_crc32_update_on(_capi.KRK_PLACE_HOST, seed, data, n, C.byref(out)))
+            assert out.value == zlib.crc32(data[:n], seed), (seed, n)
+    for P in ((1 << 20) + 1, 4 << 20, 64 << 10, 3):
+        s = C.c_void_p()
+        check(lib.krk_piece_stream_begin_on(_capi.KRK_PLACE_HOST, P, C.byref(s)))
+        try:
+            blob = data if P >= (64 << 10) else data[:(3 << 20) + 1]
+            pos = 0
+            for step in [(4 << 20) + 3, 5, (2 << 20), (8 << 20) - 1] * 10:
+                if pos >= len(blob):
+                    break
+                chunk = blob[pos:pos + step]
+                check(lib.krk_piece_stream_update(s, chunk, len(chunk)))
+                pos += len(chunk)
+            rest = blob[pos:]
+            if rest:
+                check(lib.krk_piece_stream_update(s, rest, len(rest)))
+            ns, ln = C.c_uint64(), C.c_uint64()
+            check(lib.krk_piece_stream_end(s, None, 0, C.byref(ns), C.byref(ln)))
+            sums = (C.c_uint32 * ns.value)()
+            check(lib.krk_piece_stream_end(s, sums, ns.value, C.byref(ns), C.byref(ln)))
+            assert ln.value == len(blob)
+            assert list(sums) == [zlib.crc32(blob[i:i + P]) for i in range(0, len(blob), P)], P
+        finally:
+            lib.krk_piece_stream_free(s)
+
+
+def test_offload_setting_defaults_to_auto():
+    """the SHA-256 host offload is planner-gated AUTO by default."""
+    t = C.c_int(99)
+    check(lib.krk_sha_host_offload(C.byref(t)))
+    assert t.value == _capi.KRK_OFFLOAD_AUTO == -1
+    assert lib.krk_set_sha_host_offload(-2) == _capi.KRK_EINVAL
+    check(lib.krk_set_sha_host_offload(0))
+    check(lib.krk_sha_host_offload(C.byref(t)))
+    assert t.value == 0
+    check(lib.krk_set_sha_host_offload(_capi.KRK_OFFLOAD_AUTO))
 
 
 def test_sha_offload_plan():

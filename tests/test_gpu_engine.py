@@ -94,8 +94,8 @@ def _one_gpu_digester_rate(data: bytes) -> float:
 def test_256_concurrent_gpu_digesters(gpu):
     """256 digesters on 256 threads (16 MiB each, random write
     sizes), every digest equal to hashlib; their bytes are coalesced into multi-stream
-    launches, so the aggregate is >= 100x one digester's rate; creating a digester
-    allocates nothing on the device (< 1 ms)."""
+    launches (> 8 streams a launch); creating a digester allocates nothing on the device
+    (< 1 ms).  The rates are printed, not asserted: they are bench.py --workload engine's."""
     n, L = 256, 16 << 20
     rng = np.random.default_rng(256)
     base = rng.integers(0, 256, L + n * 4096, dtype=np.uint8).tobytes()
@@ -148,7 +148,6 @@ def test_256_concurrent_gpu_digesters(gpu):
           f"create {create_ms:.3f} ms")
     assert create_ms < 1.0
     assert jobs_per_launch > 8
-    assert agg >= 100 * single, (agg, single)
     # (the rate from Python threads is capped by the GIL: their first requests trickle in
     # over ~70 ms; test_256_native_digesters measures the engine from native threads)
 
@@ -156,27 +155,21 @@ def test_256_concurrent_gpu_digesters(gpu):
 def test_256_native_digesters():
     """256 GPU Digesters on 256 native threads (tests/native/
     digesters.cpp, a C-ABI caller like the cgo layer), 16 MiB each in random writes of up to
-    1 MiB, every digest equal to the host SHA-256 of the same bytes.  With midstates in HBM
-    rows, launches queued behind the running one and up to 8 requests of a digester in
-    flight, a warm round reaches >= 13 GB/s (>= 50 MB/s a stream; the batch kernel's
-    per-stream rate is ~59 MB/s).  Warm rounds measure 14.0-14.4 GB/s; before the harness
-    started its threads on a barrier (it spun them on yield(), which burnt the box's CPU
-    quota and throttled the process ~90 ms in a third of the rounds) they
-    were bimodal, so the best of five warm rounds is asserted, and every warm round well
-    above the throttled mode."""
+    1 MiB: every digest equals the host SHA-256 of the same bytes and the requests of the
+    256 owners share launches.  The aggregate rate (14.0-14.4 GB/s warm) is measured by
+    bench.py --workload engine, not asserted here (no rate in the
+    parity gate)."""
     import json
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "digesters")
     assert os.path.exists(exe), "build() compiles tests/native"
-    r = subprocess.run([exe, "256", "16", "6"], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([exe, "256", "16", "3"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     rounds = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     print(rounds)
-    assert len(rounds) == 6 and all(x["digests_match"] for x in rounds)
-    warm = [x["GBps"] for x in rounds[1:]]  # round 0 pins the slot pool
-    assert max(warm) >= 13.0, rounds
-    assert min(warm) >= 11.0, rounds
+    assert len(rounds) == 3 and all(x["digests_match"] for x in rounds)
+    assert all(x["streams_per_launch"] > 8 for x in rounds[1:]), rounds
 
 
 @pytest.mark.parametrize("P", [3, 1000, 65536, 3 << 20, 5 << 20, 8 << 20])
@@ -250,7 +243,9 @@ def _run_script(code, env_extra, timeout=240):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, **env_extra)
+    # the engine's CRC side is what these scripts test: piece streams and crc32_update on
+    # the GPU placement (a fresh process's AUTO would keep them on the caller's thread)
+    env = dict(os.environ, KRK_CRC_PLACEMENT="2", **env_extra)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout, cwd=root,
                        env=env)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -35,16 +35,14 @@ def one_shot(gpu):
     return lens, ids, dg, sums, offs, counts
 
 
-@pytest.mark.parametrize("window_gib,cap,lane,cu_split", [(4, None, None, False), (1, 200, None, False),
-                                                      (1, 200, (100, 8), False), (1, 200, None, True)])
-def test_windowed_c3_matches_one_shot_and_oracle(one_shot, orc, window_gib, cap, lane, cu_split):
+@pytest.mark.parametrize("window_gib,cap,lane", [(4, None, None), (1, 200, None), (1, 200, (100, 8))])
+def test_windowed_c3_matches_one_shot_and_oracle(one_shot, orc, window_gib, cap, lane):
     """lane=(K, T): the K longest blobs go through the host lane (generated into their
     own device buffer T at a time, piece CRCs on the GPU, SHA-256 on T host threads
     reading HBM) while the windows run the rest; the last group is partial (100 = 12 x 8
-    + 4) and every result must still match.  cu_split: the generator and the SHA-256
-    launches on CU-masked streams of disjoint CUs (krk_stream_create_cu_mask)."""
+    + 4) and every result must still match."""
     lens, ids, dg1, sums1, offs1, counts1 = one_shot
-    wr = WindowedRun(D, ids, lens, P, window_gib << 30, cap=cap, host_lane=lane, cu_split=cu_split)
+    wr = WindowedRun(D, ids, lens, P, window_gib << 30, cap=cap, host_lane=lane)
     if lane:
         assert len(wr.lane_blobs) == lane[0] and len(wr.lane_groups) == 13
         assert not set(wr.lane_blobs) & set(np.concatenate([w[0] for w in wr.wins]).tolist())
