@@ -264,6 +264,26 @@ def cpu_baseline_hrw(digests, labels, healthy, max_replica, target_s):
 class Timer:
     def __init__(self, D, dist):
         self.D, self.dist = D, dist
+        self.rank_s = None  # every rank's own time of the leg's timed region
+
+    def timed_region(self, x):
+        """The leg's timed region: every rank's own seconds (kept for the line's rank_ms),
+        the max over ranks returned."""
+        if self.dist is None:
+            self.rank_s = [x]
+            return x
+        import torch
+        parts = [torch.zeros(1, dtype=torch.float64) for _ in range(self.dist.get_world_size())]
+        self.dist.all_gather(parts, torch.tensor([x], dtype=torch.float64))
+        self.rank_s = [float(p.item()) for p in parts]
+        return max(self.rank_s)
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.dist.get_world_size()
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def barrier(self):
         self.D.synchronize()
@@ -383,7 +403,7 @@ def run_metainfo(a, D, T, rank, world, res):
         t1 = time.perf_counter()
         crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
         sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
-    elapsed = T.max_over_ranks(t1 - t0)
+    elapsed = T.timed_region(t1 - t0)
     bytes_rank = int(sum(lens))
     value = world * bytes_rank * a.steps / elapsed / 1e9
     crc_avg, sha_avg = crc_ms / max(crc_n, 1), sha_ms / max(sha_n, 1)
@@ -427,7 +447,7 @@ def run_metainfo(a, D, T, rank, world, res):
         if ev:
             res["end_to_end"]["valu"] = {"sha256_multi": ev.get("sha256_multi"), "crc32_pieces": ev.get("crc32_pieces"),
                                          "source": valu_src, "measured_in_this_run": False, "note": VALU_NOTE}
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         m = min(n, 2 * host_cores())  # bounded sample: the first blobs of this workload
         cb, dg, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds)
         ok = all(bytes(dg[k]) == bytes(dg_h[32 * k:32 * k + 32]) for k in range(m))
@@ -507,7 +527,7 @@ def run_regen(a, D, T, rank, world, res):
         crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
     if "ih" in raw:
         ihs[:] = [core.InfoHash(bytes(r)) for r in raw["ih"]]
-    elapsed = T.max_over_ranks(t1 - t0)
+    elapsed = T.timed_region(t1 - t0)
     bytes_rank = int(sum(lens))
     crc_avg = crc_ms / max(crc_n, 1)
     per_step = max(1, round(crc_n / max(a.steps, 1)))
@@ -536,7 +556,7 @@ def run_regen(a, D, T, rank, world, res):
             o, c = int(arena.sums_off[k]), int(arena.n_pieces[k])
             ok = ok and bytes(ihs[k]) == O.info_hash(P, pin_s.a[o:o + c], names[k], lens[k])
         res["info_hash_matches_oracle"] = bool(ok)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         m = min(n, 2 * host_cores())
         cb, _, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds, passes=2)
         s_, off = sums
@@ -591,7 +611,7 @@ def run_verify(a, D, T, rank, world, res):
         T.barrier()
         t1 = time.perf_counter()
         crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
-    elapsed = T.max_over_ranks(t1 - t0)
+    elapsed = T.timed_region(t1 - t0)
     bytes_rank = n * P
     rates = D.planner_rates()
     g_bytes, h_bytes, frac_next = D.crc_host_split()  # the last step's split
@@ -632,7 +652,7 @@ def run_verify(a, D, T, rank, world, res):
                        "verdicts_match": bool(np.array_equal(pv, want)),
                        "what": "the same batch from pageable host memory (numpy)"}
     del pg, pdatas
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         # 512 pieces = 2 GiB of distinct bytes: a sample of a few hundred MiB would sit in the
         # host's last-level cache across the repeated passes and overstate the CPU rate
         m = min(n, 512)
@@ -804,7 +824,7 @@ def run_pieces(a, D, T, rank, world, res):
     same = all(np.array_equal(p.a, want) for p in pins)
     for st in streams:
         D.lib.krk_stream_destroy(st)
-    elapsed = T.max_over_ranks(t1 - t0)
+    elapsed = T.timed_region(t1 - t0)
     bytes_rank = int(sum(lens))
     crc_avg = crc_ms / max(crc_n, 1)
     crc_gbps = bytes_rank / (crc_avg / 1e3) / 1e9
@@ -827,7 +847,7 @@ def run_pieces(a, D, T, rank, world, res):
     t0 = time.perf_counter()
     core._info_hash(P, sums_h[:arena.total_pieces], "0" * 64, lens[0])
     res["info_hash_host_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         m = 2 * host_cores()
         cb, _, sums = cpu_baseline_metainfo([256 << 20] * m, [ids[0]] * m, P, a.cpu_seconds, passes=2)
         s, off = sums
@@ -860,7 +880,7 @@ def run_chunked(a, D, T, rank, world, res):
         sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
         crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
         gen_n, gen_ms = D.KernelTimer.stats("synth_fill")
-    elapsed = T.max_over_ranks(t1 - t0)
+    elapsed = T.timed_region(t1 - t0)
     bytes_rank = int(sum(lens))
     total_bytes = int(sum(c3_lengths(a.blobs or 20000)))
     cb = wr.cb
@@ -913,7 +933,7 @@ def run_chunked(a, D, T, rank, world, res):
         res["roofline"] = roof
     dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
     sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_c3(ids, lens, P, dg, sums, cb.sums_off)
     if rank == 0:  # spot-check three blobs against the one-shot device path
         pick = sorted({0, n // 2, n - 1})
@@ -1011,7 +1031,7 @@ def run_hrw(a, D, T, rank, world, res):
         t1 = time.perf_counter()
         hn, hms = D.KernelTimer.stats("hrw_order")
         gn, gms = D.KernelTimer.stats("hrw_gather")
-    elapsed = T.max_over_ranks(t1 - t0)
+    elapsed = T.timed_region(t1 - t0)
     res.update({"metric": "hashring placement digests/s (C5)", "value": round(world * n * a.steps / elapsed, 1),
                 "unit": "digests/s", "steps": a.steps, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "weak", "dtype": "u64+f64",
@@ -1032,7 +1052,7 @@ def run_hrw(a, D, T, rank, world, res):
                     "indices + 1-B count); the hrw_order kernel (65,536-shard table, "
                     f"{round(hms / max(hn, 1), 3)} ms) is VALU-bound and independent of the digest count")
     res["roofline"] = roof
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         cbl, cl, cc = cpu_baseline_hrw(dig, labels, healthy, R, a.cpu_seconds)
         got = locs_h[:cl.shape[0]].astype(np.int32)
         if compact:
@@ -1213,6 +1233,17 @@ def main():
     {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen,
      "verify": run_verify}[kind](
         a, D, T, rank, world, res)
+    # rank 0's CPU baseline (if any) ran after the timed region, behind this barrier the
+    # other ranks wait at; then every rank's device and time go into the line, so an N-GPU
+    # line shows it ran on N distinct GPUs
+    T.barrier()
+    devs = T.gather(D.device_pci_bus_id())
+    if world > 1 or T.rank_s:
+        res["rank_devices"] = devs
+        if T.rank_s:
+            res["rank_ms"] = [round(x * 1e3, 3) for x in T.rank_s]
+        if world > 1 and len(set(devs)) < world and "rehearsal" not in res:
+            raise SystemExit(f"bench.py: {world} ranks on {len(set(devs))} distinct device(s): {devs}")
     order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
              "vs_baseline", "dtype", "data", "config"]
     line = {k: res[k] for k in order if k in res}

@@ -273,6 +273,42 @@ int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n_chunks
 int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host,
                              uint8_t* digests_host);
 
+/* The same from the CAS files themselves: the upload verify of uploader.verify
+ * (origin/blobserver/uploader.go:74-94) or the cache-fill digest of CAStore.WriteCacheFile
+ * (lib/store/ca_store.go:99-135) fused with the metainfo Generator.Generate computes from the
+ * cache file (lib/metainfogen/generator.go:41-58): each file is read ONCE (pread on the host
+ * pool into the pinned windows; O_DIRECT with KRK_FILE_DIRECT=1) and that read feeds both
+ * the SHA-256 digest and the piece CRCs -- the reference reads it twice.  files[i].length is
+ * the size the caller stat-ed; a shorter file is KRK_EIO "read blob: <path>: unexpected EOF",
+ * an unopenable one KRK_EIO "open <path>: <errno text>".  Live blobs per window are also
+ * capped by the file descriptors the process may still open (RLIMIT_NOFILE).  With the host
+ * offload (KRK_OFFLOAD_AUTO) the planner's files are read, hashed and piece-summed on host
+ * threads in one pass each.  Synchronous. */
+int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host,
+                              uint8_t* digests_host);
+
+/* The window schedule of the host-resident batch calls (and of kraken_amd/windowed.py's
+ * larger-than-HBM device batches): every live blob advances by the same chunk (a multiple of
+ * 64 bytes but each blob's last, about window_bytes / live a window); at most live_cap blobs
+ * are live, admitted longest first; a finished blob's place goes to the next-longest.  _next
+ * writes the next window's chunks (blob index, offset, length; admission order) and their
+ * count to *n_out, 0 once every blob is done (KRK_ERANGE if cap is too small: the window
+ * has *n_out <= live_cap chunks). */
+typedef struct krk_window_sched krk_window_sched;
+int krk_window_sched_new(const uint64_t* lengths, uint64_t n, uint64_t window_bytes, uint64_t live_cap,
+                         krk_window_sched** out);
+int krk_window_sched_next(krk_window_sched* s, uint32_t* blobs, uint64_t* offsets, uint64_t* lengths, uint64_t cap,
+                          uint64_t* n_out);
+void krk_window_sched_free(krk_window_sched* s);
+/* The live-stream cap of the windows on the calling thread's device: 7/8 of the largest
+ * stream count whose SHA-256 launch runs more than one lane a stream (14,336 on 256 CUs),
+ * so each window's CRC launch has the CUs the SHA workgroups leave free.  KRK_LIVE_CAP
+ * overrides it for the host-resident calls. */
+int krk_window_stream_cap(uint64_t* cap);
+/* The calling thread's last krk_metainfo_digest_host / _files call: the most live blobs in
+ * one window, the windows, and the blobs the host offload took. */
+int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs);
+
 /* ------------------------------------------------------- multi-device
  * One process, several GPUs (the origin is one process,
  * origin/cmd/cmd.go:164).  The device set -- the devices of the last krk_init mask,
@@ -289,6 +325,8 @@ int krk_metainfo_digest_host_multi(const krk_blob* blobs, uint64_t n_blobs, uint
                                    uint8_t* digests_host);
 int krk_piece_sums_host_multi(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host);
 int krk_piece_sums_files_multi(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host);
+int krk_metainfo_digest_files_multi(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host,
+                                    uint8_t* digests_host);
 int krk_sha256_host_multi(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
                           uint8_t* digests_host);
 
@@ -415,6 +453,9 @@ int krk_stream_create(void** out);
  * long kernels (a C3 window's SHA-256 launch runs ~0.6 s) is kept off the queues the
  * short work shares, which would otherwise wait behind it. */
 int krk_stream_create_prio(int priority, void** out);
+/* PCI bus id of the calling thread's device ("0000:05:00.0"; cap >= 16): an N-rank run
+ * reports every rank's, so a scaling line shows it ran on N distinct GPUs. */
+int krk_device_pci_bus_id(char* out, uint32_t cap);
 /* CUs of the calling thread's device. */
 int krk_device_cus(int* out);
 /* Waits for the stream's work, retires the library's state tied to it (events of upload
@@ -532,11 +573,13 @@ int krk_planner_calibrate(void);
  * and the modelled GPU / host seconds (may be NULL).
  * krk_sha_offload_plan plans a device-resident batch (krk_sha256_dev,
  * krk_metainfo_digest_dev); krk_host_offload_plan plans for `mode`
- * KRK_OFFLOAD_DEVICE (the same), KRK_OFFLOAD_HOST_SHA (krk_sha256_host) or
- * KRK_OFFLOAD_HOST_WHOLE (krk_metainfo_digest_host). */
+ * KRK_OFFLOAD_DEVICE (the same), KRK_OFFLOAD_HOST_SHA (krk_sha256_host),
+ * KRK_OFFLOAD_HOST_WHOLE (krk_metainfo_digest_host) or KRK_OFFLOAD_HOST_FILES
+ * (krk_metainfo_digest_files). */
 #define KRK_OFFLOAD_DEVICE 0
 #define KRK_OFFLOAD_HOST_SHA 1
 #define KRK_OFFLOAD_HOST_WHOLE 2
+#define KRK_OFFLOAD_HOST_FILES 3  /* krk_metainfo_digest_files: one read, SHA-256 + CRC per host blob */
 int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
                          uint64_t* n_host, double* gpu_seconds, double* host_seconds);
 int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, int mode, uint32_t* host_idx,

@@ -120,6 +120,13 @@ def _load() -> C.CDLL:
         "krk_digester_free": (None, [vp]),
         "krk_metainfo_digest_dev": (i, [blobp, C.c_uint64, vp, vp, vp]),
         "krk_metainfo_digest_host": (i, [blobp, C.c_uint64, u32p, u8p]),
+        "krk_metainfo_digest_files": (i, [C.POINTER(krk_file_blob), C.c_uint64, u32p, u8p]),
+        "krk_metainfo_digest_files_multi": (i, [C.POINTER(krk_file_blob), C.c_uint64, u32p, u8p]),
+        "krk_window_sched_new": (i, [u64p, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(vp)]),
+        "krk_window_sched_next": (i, [vp, u32p, u64p, u64p, C.c_uint64, u64p]),
+        "krk_window_sched_free": (None, [vp]),
+        "krk_window_stream_cap": (i, [u64p]),
+        "krk_windows_last_call": (i, [u64p, C.POINTER(C.c_int), u64p]),
         "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_metainfo_digest_chunks_dev_on": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp, vp]),
         "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),
@@ -145,6 +152,7 @@ def _load() -> C.CDLL:
         "krk_stream_create": (i, [C.POINTER(vp)]),
         "krk_stream_create_prio": (i, [i, C.POINTER(vp)]),
         "krk_device_cus": (i, [C.POINTER(i)]),
+        "krk_device_pci_bus_id": (i, [C.c_char_p, C.c_uint32]),
         "krk_stream_destroy": (i, [vp]),
         "krk_stream_sync": (i, [vp]),
         "krk_event_create": (i, [C.POINTER(vp)]),

@@ -213,6 +213,29 @@ int krk_piece_sums_files_multi(const krk_file_blob* files, uint64_t n, uint32_t*
     });
 }
 
+int krk_metainfo_digest_files_multi(const krk_file_blob* files, uint64_t n, uint32_t* sums_host,
+                                    uint8_t* digests_host) {
+    int r = check_batch(files, n);
+    if (r || !n) return r;
+    KRK_CHECK(digests_host, KRK_EINVAL, "digests_host is NULL");
+    std::vector<uint64_t> bytes(n);
+    bool any_sums = false;
+    for (uint64_t i = 0; i < n; ++i) {
+        bytes[i] = files[i].length;
+        any_sums |= files[i].length > 0;
+    }
+    KRK_CHECK(!any_sums || sums_host, KRK_EINVAL, "sums_host is NULL");
+    return shard_run(bytes, [&](size_t, const std::vector<uint64_t>& idx) {
+        SubBatch<krk_file_blob> sb(files, idx);
+        std::vector<uint8_t> dg(idx.size() * 32);
+        int rc = krk_metainfo_digest_files(sb.blobs.data(), idx.size(), sb.sums.data(), dg.data());
+        if (rc) return rc;
+        sb.scatter(files, idx, sums_host);
+        for (size_t k = 0; k < idx.size(); ++k) memcpy(digests_host + 32 * idx[k], dg.data() + 32 * k, 32);
+        return KRK_OK;
+    });
+}
+
 int krk_sha256_host_multi(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
                           uint8_t* digests_host) {
     if (!n) return KRK_OK;

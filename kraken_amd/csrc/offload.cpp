@@ -14,7 +14,9 @@
 // host blobs get their piece sums on the host too, which takes their bytes off the host
 // link -- C2 end-to-end, link-bound, then hands the host the blobs the link would carry
 // past the GPU's own chain time.
+#include <fcntl.h>
 #include <sched.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -335,8 +337,12 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
         for (uint64_t k = 1; k <= n; ++k) {
             const double L = (double)lens[order[k - 1]];
             if (L == 0) break;  // empty blobs are not worth a thread
-            put(L / rs);
-            if (mode == kOffHostWhole) put(L / rc);
+            if (mode == kOffHostFiles) {
+                put(L / rs + L / R.host_crc + L / R.host_copy);  // one read, SHA-256 and CRC per chunk
+            } else {
+                put(L / rs);
+                if (mode == kOffHostWhole) put(L / rc);
+            }
             hbytes += L;
             const double h = mode == kOffDevice ? std::max(maxload, hbytes / R.d2h) : maxload;
             const double g = gpu_side(k);
@@ -579,6 +585,83 @@ void offload_whole_host(const std::vector<const uint8_t*>& ptrs, const std::vect
     for (auto& th : pool) th.join();
 }
 
+// kOffHostFiles: file j read once in 1 MiB chunks, each chunk hashed (SHA-256) and its
+// piece portions CRC'd while it is in the cache; digest to out + 32 j, sums to sums[j].
+// Errors keep the reference's texts ("open <path>: ...", "read blob: <path>: ...").
+int offload_whole_files(const std::vector<const char*>& paths, const std::vector<uint64_t>& lens,
+                        const std::vector<uint64_t>& plen, const std::vector<uint32_t*>& sums, int threads,
+                        uint8_t* out) {
+    constexpr size_t kChunk = size_t(1) << 20;  // a multiple of 64: only the last chunk is partial
+    std::atomic<size_t> next{0};
+    std::atomic<bool> failed{false};
+    std::mutex emu;
+    int rc = KRK_OK;
+    std::string msg;
+    auto fail = [&](int code, const std::string& m) {
+        std::lock_guard<std::mutex> g(emu);
+        if (!rc) {
+            rc = code;
+            msg = m;
+        }
+        failed = true;
+    };
+    auto work = [&] {
+        std::vector<uint8_t> buf(kChunk);
+        for (size_t j; !failed && (j = next.fetch_add(1)) < paths.size();) {
+            const int fd = open(paths[j], O_RDONLY | O_CLOEXEC);
+            if (fd < 0) {
+                fail(KRK_EIO, std::string("open ") + paths[j] + ": " + strerror(errno));
+                return;
+            }
+            const uint64_t L = lens[j], P = plen[j];
+            uint32_t h[8];
+            memcpy(h, kIV, sizeof h);
+            uint32_t crc = 0;
+            uint64_t pos = 0, in_piece = 0, piece = 0;
+            bool ok = true;
+            do {
+                const size_t m = (size_t)std::min<uint64_t>(kChunk, L - pos);
+                for (size_t got = 0; got < m;) {
+                    const ssize_t g = pread(fd, buf.data() + got, m - got, (off_t)(pos + got));
+                    if (g < 0 && errno == EINTR) continue;
+                    if (g <= 0) {
+                        fail(KRK_EIO, std::string("read blob: ") + paths[j] + ": " +
+                                          (g < 0 ? strerror(errno) : "unexpected EOF"));
+                        ok = false;
+                        break;
+                    }
+                    got += (size_t)g;
+                }
+                if (!ok) break;
+                for (size_t q = 0; q < m;) {  // core/metainfo.go:157-179 over this chunk
+                    const size_t take = (size_t)std::min<uint64_t>(m - q, P - in_piece);
+                    crc = host_crc32_update(crc, buf.data() + q, take);
+                    q += take;
+                    in_piece += take;
+                    if (in_piece == P) {
+                        sums[j][piece++] = crc;
+                        crc = 0;
+                        in_piece = 0;
+                    }
+                }
+                if (pos + m < L) host_sha256_blocks(h, buf.data(), m / 64);
+                else host_sha256_final(h, pos, buf.data(), m, out + 32 * j);
+                pos += m;
+            } while (pos < L);
+            if (ok && in_piece) sums[j][piece] = crc;
+            close(fd);
+            if (!ok) return;
+        }
+    };
+    const int T = (int)std::min<size_t>((size_t)std::max(threads, 1), paths.size());
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    if (rc) set_error(rc, "%s", msg.c_str());
+    return rc;
+}
+
 // Write host-computed digests into digests_dev (record j: 4-byte blob index, 32-byte
 // digest) on stream s: one upload + one scatter launch.
 int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,
@@ -628,9 +711,9 @@ int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int 
     KRK_CHECK(n_host, KRK_EINVAL, "n_host is NULL");
     KRK_CHECK(threads >= 0 && cus >= 0, KRK_EINVAL, "threads and cus must be >= 0");
     static_assert(KRK_OFFLOAD_DEVICE == kOffDevice && KRK_OFFLOAD_HOST_SHA == kOffHostSha &&
-                      KRK_OFFLOAD_HOST_WHOLE == kOffHostWhole,
+                      KRK_OFFLOAD_HOST_WHOLE == kOffHostWhole && KRK_OFFLOAD_HOST_FILES == kOffHostFiles,
                   "offload modes");
-    KRK_CHECK(mode >= KRK_OFFLOAD_DEVICE && mode <= KRK_OFFLOAD_HOST_WHOLE, KRK_EINVAL, "offload mode %d", mode);
+    KRK_CHECK(mode >= KRK_OFFLOAD_DEVICE && mode <= KRK_OFFLOAD_HOST_FILES, KRK_EINVAL, "offload mode %d", mode);
     int drc = KRK_OK;
     Device* D = device(&drc);  // none: the override or the nominal rates
     Rates R = planner_rates(D);

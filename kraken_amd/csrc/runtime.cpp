@@ -870,171 +870,7 @@ int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n, uint3
                        static_cast<hipStream_t>(sha_stream));
 }
 
-int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {
-    KRK_DEVICE(D);
-    int r = validate_blobs(blobs, n);
-    if (r) return r;
-    if (!n) return KRK_OK;
-    KRK_CHECK(digests_host, KRK_EINVAL, "digests_host is NULL");
-    uint64_t lo, hi;
-    sums_span(blobs, n, &lo, &hi);
-    KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
-    // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed and
-    // piece-summed in place on host threads and never cross the host link; the windows
-    // below carry the others' bytes to both kernels.
-    std::vector<char> on_host(n, 0);
-    std::vector<uint32_t> host;
-    const int off_t = offload_threads(kOffHostWhole);
-    if (off_t > 0) {
-        std::vector<uint64_t> lens(n);
-        for (uint64_t i = 0; i < n; ++i) lens[i] = blobs[i].length;
-        host = offload_plan(lens.data(), n, off_t, planner_rates(D), nullptr, nullptr, kOffHostWhole);
-        for (uint32_t i : host) on_host[i] = 1;
-    }
-    const uint64_t n_gpu = n - host.size();
-    const size_t W = window_bytes();
-    // Every unfinished blob contributes up to C bytes per window, so the SHA
-    // streams all advance together (multiple of 64: only final chunks are partial).
-    uint64_t C = (W / std::max<uint64_t>(n_gpu, 1)) & ~uint64_t(63);
-    if (C < 64) C = 64;
-    const size_t cap = std::max<size_t>(W, C * n_gpu + 16 * n_gpu);
-    StagingLease lease;
-    r = lease_staging(D, cap, lease);
-    if (r) return r;
-    Pipeline& pl = *lease.p;
-    uint8_t* d_dig = nullptr;
-    uint32_t *d_state = nullptr, *d_sums = nullptr;
-    DevMem mem;
-    KRK_HIP(mem.alloc(&d_dig, n * 32));
-    KRK_HIP(mem.alloc(&d_state, n * 32));
-    KRK_HIP(mem.alloc(&d_sums, std::max<uint64_t>(hi, 1) * 4));
-    KRK_HIP(hipMemset(d_sums, 0, std::max<uint64_t>(hi, 1) * 4));
-    std::vector<uint64_t> off(n, 0);
-    std::vector<char> done(on_host);
-    hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
-    // The host blobs' digests and piece sums land in host_dig / host_sums (host_sums_off[j]
-    // = where blob host[j]'s first sum sits there) and go to the caller's arrays after the
-    // device results are copied out.
-    std::vector<uint8_t> host_dig(32 * host.size());
-    std::vector<uint64_t> host_sums_off(host.size() + 1, 0);
-    for (size_t j = 0; j < host.size(); ++j)
-        host_sums_off[j + 1] =
-            host_sums_off[j] + krk_num_pieces(blobs[host[j]].length, blobs[host[j]].piece_length);
-    std::vector<uint32_t> host_sums(host_sums_off.back());
-    std::thread host_th;
-    if (!host.empty())
-        host_th = std::thread([&] {
-            std::vector<const uint8_t*> p(host.size());
-            std::vector<uint64_t> l(host.size()), pl(host.size());
-            std::vector<uint32_t*> so(host.size());
-            for (size_t j = 0; j < host.size(); ++j) {
-                p[j] = blobs[host[j]].data;
-                l[j] = blobs[host[j]].length;
-                pl[j] = (uint64_t)blobs[host[j]].piece_length;
-                so[j] = host_sums.data() + host_sums_off[j];
-            }
-            offload_whole_host(p, l, pl, so, off_t, host_dig.data());
-        });
-    struct Joiner {
-        std::thread& t;
-        ~Joiner() {
-            if (t.joinable()) t.join();
-        }
-    } joiner{host_th};
-    // The copy threads and the offload's threads share the process's CPU budget: above it
-    // a CPU quota throttles the whole process.
-    struct ShareGuard {
-        int saved;
-        ~ShareGuard() { t_host_share = saved; }
-    } share_guard{t_host_share};
-    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
-    ItemBuilder B;
-    uint64_t remaining = n_gpu;
-    int k = 0;
-    double t_acq = 0, t_build = 0, t_copy = 0, t_enq = 0, t0 = wall_s();
-    int n_win = 0;
-    while (!r && remaining) {
-        double ta = wall_s();
-        r = pl.acquire(k);
-        if (r) break;
-        double tb = wall_s();
-        t_acq += tb - ta;
-        Window& w = pl.w[k];
-        std::vector<ShaJob> jobs;
-        CrcBatch items;
-        std::vector<CopyTask> copies;
-        size_t fill = 0;
-        for (uint64_t i = 0; i < n; ++i) {
-            if (done[i]) continue;
-            const krk_blob& b = blobs[i];
-            const uint64_t left = b.length - off[i];
-            const bool fin = left <= C;
-            const uint64_t take = fin ? left : C;
-            const uint64_t dev = reinterpret_cast<uint64_t>(w.dev + fill);
-            if (take) {
-                copies.push_back({w.host + fill, b.data + off[i], take});
-                B.add(items, dev, off[i], off[i] + take, b.length, (uint64_t)b.piece_length, b.sums_offset);
-            }
-            ShaJob j{};
-            j.ptr = dev;
-            j.len = take;
-            j.prefix = off[i];
-            j.out = (uint32_t)i;
-            j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
-            memcpy(j.h, kIV, sizeof kIV);
-            jobs.push_back(j);
-            off[i] += take;
-            fill += (take + 15) & ~uint64_t(15);
-            if (fin) { done[i] = 1; --remaining; }
-        }
-        double tc = wall_s();
-        t_build += tc - tb;
-        par_copy(copies);
-        double td = wall_s();
-        t_copy += td - tc;
-        ++n_win;
-        if (pl.h2d(k, fill, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
-            hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess) {
-            set_error(KRK_EHIP, "metainfo_digest_host: staging copy failed");
-            r = KRK_EHIP;
-            break;
-        }
-        r = run_jobs(D, jobs, d_dig, d_state, ks);
-        if (!r) r = run_items(D, items, d_sums, kc);
-        if (r) break;
-        // the device window is free again once both kernels have read it
-        pl.release(k, 0, ks);
-        pl.release(k, 1, kc);
-        t_enq += wall_s() - td;
-        k ^= 1;
-    }
-    const double t_loop = wall_s() - t0;
-    if (!r && (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(kc) != hipSuccess ||
-               hipStreamSynchronize(cp) != hipSuccess)) {
-        set_error(KRK_EHIP, "sync failed");
-        r = KRK_EHIP;
-    }
-    if (trace_on())
-        fprintf(stderr,
-                "krk_trace metainfo_digest_host: windows=%d W=%zu C=%llu loop=%.3fs acquire=%.3fs build=%.3fs "
-                "copy=%.3fs enqueue=%.3fs drain=%.3fs\n",
-                n_win, W, (unsigned long long)C, t_loop, t_acq, t_build, t_copy, t_enq, wall_s() - t0 - t_loop);
-    if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error(KRK_EHIP, "digest copy-out failed");
-        r = KRK_EHIP;
-    }
-    if (host_th.joinable()) host_th.join();
-    for (size_t q = 0; q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
-    if (!r && hi > lo && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error(KRK_EHIP, "sums copy-out failed");
-        r = KRK_EHIP;
-    }
-    for (size_t q = 0; !r && q < host.size(); ++q)
-        if (host_sums_off[q + 1] > host_sums_off[q])
-            memcpy(sums_host + blobs[host[q]].sums_offset, &host_sums[host_sums_off[q]],
-                   (host_sums_off[q + 1] - host_sums_off[q]) * 4);
-    return r;
-}
+// krk_metainfo_digest_host: windows.cpp
 
 int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, uint8_t* ok_out_host, void* stream) {
     KRK_CHECK(blob && expected_host && ok_out_host, KRK_EINVAL, "verify: null argument");
@@ -1492,6 +1328,12 @@ int krk_stream_create(void** out) {
     hipStream_t s;
     KRK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     *out = s;
+    return KRK_OK;
+}
+int krk_device_pci_bus_id(char* out, uint32_t cap) {
+    KRK_CHECK(out && cap >= 16, KRK_EINVAL, "device_pci_bus_id: a buffer of at least 16 bytes");
+    KRK_DEVICE(D);
+    KRK_HIP(hipDeviceGetPCIBusId(out, (int)cap, D->id));
     return KRK_OK;
 }
 int krk_device_cus(int* out) {

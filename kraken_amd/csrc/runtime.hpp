@@ -699,7 +699,9 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 //  * kOffHostWhole: blobs in host memory, digests and piece sums; the host's blobs are
 //    hashed AND piece-summed in place and never uploaded (krk_metainfo_digest_host) --
 //    the batch's bytes over the host link shrink by theirs.
-enum OffMode { kOffDevice = 0, kOffHostSha = 1, kOffHostWhole = 2 };
+//  * kOffHostFiles: cache files (krk_metainfo_digest_files): a host blob is read once and
+//    hashed and piece-summed chunk by chunk on one host thread.
+enum OffMode { kOffDevice = 0, kOffHostSha = 1, kOffHostWhole = 2, kOffHostFiles = 3 };
 // Host threads the offload of a `mode` batch may use (krk_set_sha_host_offload; 0 = off).
 int offload_threads(int mode = kOffDevice);
 // What the planners know about this box (offload.cpp): per-stream SHA-256 rate of each
@@ -755,6 +757,9 @@ void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vecto
 // to sums[j][0 .. ceil(len / plen)), on up to `threads` threads; the SHA-256 pass and the
 // CRC pass of a blob are separate tasks, longest first.
 void offload_whole_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens,
+                        const std::vector<uint64_t>& plen, const std::vector<uint32_t*>& sums, int threads,
+                        uint8_t* out);
+int offload_whole_files(const std::vector<const char*>& paths, const std::vector<uint64_t>& lens,
                         const std::vector<uint64_t>& plen, const std::vector<uint32_t*>& sums, int threads,
                         uint8_t* out);
 int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,

@@ -1,0 +1,551 @@
+// windows.cpp -- host-resident batches through the pinned staging windows:
+// the upload / cache-fill verify of origin/blobserver/uploader.go:74-94 and
+// lib/store/ca_store.go:99-135 (Digester over the bytes) fused with the metainfo of
+// lib/metainfogen/generator.go:41-58 (piece CRCs of the same bytes), so each byte is read
+// once -- from the caller's buffers (krk_metainfo_digest_host) or from the cache files
+// themselves (krk_metainfo_digest_files) -- and crosses PCIe once, where the reference
+// reads every upload twice.
+//
+// The window schedule (the C3 machinery of kraken_amd/windowed.py, here in C++): every live
+// blob advances by the same chunk per window (about W bytes a window), SHA-256 chained
+// through per-blob midstates in HBM and the chunk's piece CRCs XOR-accumulated into its
+// pieces (CRC-32 is linear, so any cut is legal).  At most `cap` blobs are live, admitted
+// longest first so the longest chain starts in window 0: by default 7/8 of the largest
+// stream count the SHA-256 launch plan still runs on two lanes a stream (14,336 on 256
+// CUs), which keeps every window on a multi-lane plan and leaves an eighth of the CUs free
+// of SHA workgroups for the window's CRC launch, queued beside it on another stream
+// (profiles/r02/c3_live_cap.jsonl).  The host's work per window is O(live).
+#include <dirent.h>
+#include <sys/resource.h>
+
+#include <deque>
+#include <thread>
+
+#include "runtime.hpp"
+#include "staging.hpp"
+
+namespace krk {
+
+// ----------------------------------------------------------------- the window schedule
+struct WinChunk {
+    uint32_t blob;
+    uint64_t off, len;
+};
+
+class WindowSched {
+  public:
+    // blobs: the windowed blobs' indices into lens; chunks a multiple of `align` bytes
+    // (64: SHA-256 blocks; 4 KiB for O_DIRECT file reads) except each blob's last.
+    WindowSched(const uint64_t* lens, std::vector<uint32_t> blobs, uint64_t W, uint64_t cap, uint64_t align = 64)
+        : L_(lens), W_(W), cap_(std::max<uint64_t>(cap, 1)), align_(std::max<uint64_t>(align, 64)), queue_(std::move(blobs)) {
+        std::stable_sort(queue_.begin(), queue_.end(), [&](uint32_t a, uint32_t b) { return L_[a] > L_[b]; });
+    }
+    // The next window's chunks (in admission order); false once every blob is done.
+    bool next(std::vector<WinChunk>& out) {
+        out.clear();
+        while (live_.size() < cap_ && q_ < queue_.size()) live_.push_back({queue_[q_++], 0});
+        if (live_.empty()) return false;
+        max_live_ = std::max<uint64_t>(max_live_, live_.size());
+        const uint64_t c = std::max(align_, W_ / live_.size() / align_ * align_);
+        size_t keep = 0;
+        for (size_t k = 0; k < live_.size(); ++k) {
+            auto [b, pos] = live_[k];
+            const uint64_t take = std::min(c, L_[b] - pos);
+            out.push_back({b, pos, take});
+            pos += take;
+            if (pos < L_[b]) live_[keep++] = {b, pos};
+        }
+        live_.resize(keep);
+        return true;
+    }
+    uint64_t max_live() const { return max_live_; }
+
+  private:
+    const uint64_t* L_;
+    uint64_t W_, cap_, align_;
+    std::vector<uint32_t> queue_;
+    size_t q_ = 0;
+    std::vector<std::pair<uint32_t, uint64_t>> live_;  // blob, bytes done
+    uint64_t max_live_ = 0;
+};
+
+// Live streams per window on device D: 7/8 of the largest stream count whose SHA-256 launch
+// still runs two (or eight) lanes a stream, a multiple of the two-pair workgroup's 64.
+uint64_t window_stream_cap(Device* D) {
+    (void)D;  // the plan reads the current device's CU count
+    uint64_t lo = 1, hi = uint64_t(1) << 30;
+    if (sha_lanes_for((uint32_t)hi) >= 2) return (hi * 7 / 8) / 64 * 64;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) / 2;
+        (sha_lanes_for((uint32_t)mid) >= 2 ? lo : hi) = mid;
+    }
+    return std::max<uint64_t>(64, (lo * 7 / 8) / 64 * 64);
+}
+
+namespace {
+
+// Where a window's bytes come from: the caller's buffers or the cache files.
+struct Filler {
+    virtual ~Filler() = default;
+    // bytes [off, off + len) of blob b into dst (host, pinned); the whole window at once
+    struct Task {
+        uint32_t b;
+        uint64_t off, len;
+        uint8_t* dst;
+    };
+    virtual int fill(const std::vector<Task>& tasks) = 0;
+};
+
+struct MemFiller : Filler {
+    const krk_blob* blobs;
+    explicit MemFiller(const krk_blob* b) : blobs(b) {}
+    int fill(const std::vector<Task>& tasks) override {
+        std::vector<CopyTask> c;
+        c.reserve(tasks.size());
+        for (const Task& t : tasks)
+            if (t.len) c.push_back({t.dst, blobs[t.b].data + t.off, (size_t)t.len});
+        par_copy(c);
+        return KRK_OK;
+    }
+};
+
+// A blob's file is opened at its first chunk and closed after its last; live blobs <= the
+// descriptor budget (the window cap is capped by it), so no descriptor is reopened.
+struct FileFiller : Filler {
+    const krk_file_blob* files;
+    bool direct;
+    std::vector<int> fd;
+    std::vector<char> is_direct;
+    FileFiller(const krk_file_blob* f, uint64_t n, bool want_direct) : files(f), direct(want_direct), fd(n, -1), is_direct(n, 0) {}
+    ~FileFiller() override {
+        for (int x : fd)
+            if (x >= 0) close(x);
+    }
+    int open_file(uint32_t i) {
+        if (fd[i] >= 0) return KRK_OK;
+        int x = -1;
+        if (direct) {
+            x = open(files[i].path, O_RDONLY | O_DIRECT | O_CLOEXEC);
+            is_direct[i] = x >= 0;
+        }
+        if (x < 0) x = open(files[i].path, O_RDONLY | O_CLOEXEC);
+        KRK_CHECK(x >= 0, KRK_EIO, "open %s: %s", files[i].path, strerror(errno));
+        fd[i] = x;
+        return KRK_OK;
+    }
+    int fill(const std::vector<Task>& tasks) override {
+        std::vector<ReadTask> plain, odirect;
+        for (const Task& t : tasks) {
+            if (!t.len) continue;
+            int r = open_file(t.b);
+            if (r) return r;
+            (is_direct[t.b] ? odirect : plain).push_back({fd[t.b], t.off, t.dst, (size_t)t.len, (size_t)t.b});
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            const auto& rt = pass ? odirect : plain;
+            if (rt.empty()) continue;
+            int e = 0;
+            const long bad = par_read(rt, pass == 1, &e);
+            if (bad >= 0) {
+                const char* path = files[rt[bad].blob].path;
+                if (e) set_error(KRK_EIO, "read blob: %s: %s", path, strerror(e));
+                else set_error(KRK_EIO, "read blob: %s: unexpected EOF", path);
+                return KRK_EIO;
+            }
+        }
+        for (const Task& t : tasks)  // a blob's last chunk: its file is done
+            if (t.off + t.len == files[t.b].length && fd[t.b] >= 0) {
+                close(fd[t.b]);
+                fd[t.b] = -1;
+            }
+        return KRK_OK;
+    }
+};
+
+// File descriptors this call may hold open at once: the soft RLIMIT_NOFILE less those
+// already open and a reserve for the rest of the process.
+uint64_t fd_budget() {
+    struct rlimit rl {};
+    if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return uint64_t(1) << 20;
+    uint64_t open_now = 0;
+    if (DIR* d = opendir("/proc/self/fd")) {
+        while (readdir(d)) ++open_now;
+        closedir(d);
+    }
+    const uint64_t reserve = 64 + open_now;
+    return rl.rlim_cur > reserve + 16 ? rl.rlim_cur - reserve : 16;
+}
+
+// The windows of one host-resident batch: the blobs not in `skip`, chunk by chunk, into the
+// device's staging windows and through both kernels.  d_sums / d_dig / d_state indexed like
+// the caller's blobs (sums by sums_off).  Asynchronous on the device's streams; returns once
+// the last window is queued (the caller synchronises s_main / s_a / s_b).
+int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* plens, const uint64_t* soff,
+                 const std::vector<char>& skip, Filler& filler, uint64_t align, uint64_t cap, uint32_t* d_sums,
+                 uint8_t* d_dig, uint32_t* d_state, uint64_t* max_live, int* n_windows) {
+    std::vector<uint32_t> blobs;
+    for (uint64_t i = 0; i < n; ++i)
+        if (!skip[i]) blobs.push_back((uint32_t)i);
+    *max_live = 0;
+    *n_windows = 0;
+    if (blobs.empty()) return KRK_OK;
+    const size_t W = window_bytes();
+    const uint64_t live_cap = std::min<uint64_t>(cap, blobs.size());
+    WindowSched sched(lens, blobs, W, live_cap, align);
+    const size_t place = std::max<uint64_t>(align == 64 ? 16 : align, 16);  // chunk start alignment in the window
+    StagingLease lease;
+    int r = lease_staging(D, W + place * live_cap, lease);
+    if (r) return r;
+    Pipeline& pl = *lease.p;
+    hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
+    ItemBuilder B;
+    std::vector<WinChunk> win;
+    std::vector<Filler::Task> tasks;
+    int k = 0;
+    double t_acq = 0, t_build = 0, t_fill = 0, t_enq = 0;
+    const double t0 = wall_s();
+    while (!r && sched.next(win)) {
+        const double ta = wall_s();
+        r = pl.acquire(k);
+        if (r) break;
+        const double tb = wall_s();
+        t_acq += tb - ta;
+        Window& w = pl.w[k];
+        std::vector<ShaJob> jobs;
+        jobs.reserve(win.size());
+        CrcBatch items;
+        tasks.clear();
+        size_t fill = 0;
+        for (const WinChunk& c : win) {
+            const uint64_t L = lens[c.blob];
+            const uint64_t dev = reinterpret_cast<uint64_t>(w.dev + fill);
+            if (c.len) {
+                tasks.push_back({c.blob, c.off, c.len, w.host + fill});
+                B.add(items, dev, c.off, c.off + c.len, L, (uint64_t)plens[c.blob], soff[c.blob]);
+            }
+            ShaJob j{};
+            j.ptr = dev;
+            j.len = c.len;
+            j.prefix = c.off;
+            j.out = c.blob;
+            j.flags = (c.off + c.len == L ? kShaFinal : 0) | (c.off ? kShaFromState : 0);
+            memcpy(j.h, kIV, sizeof kIV);
+            jobs.push_back(j);
+            fill += (c.len + place - 1) / place * place;
+        }
+        const double tc = wall_s();
+        t_build += tc - tb;
+        r = filler.fill(tasks);
+        if (r) break;
+        const double td = wall_s();
+        t_fill += td - tc;
+        ++*n_windows;
+        if (pl.h2d(k, std::min(fill, pl.w[k].cap), cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
+            hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess) {
+            set_error(KRK_EHIP, "metainfo windows: staging copy failed");
+            r = KRK_EHIP;
+            break;
+        }
+        r = run_jobs(D, jobs, d_dig, d_state, ks);
+        if (!r) r = run_items(D, items, d_sums, kc);
+        if (r) break;
+        // the device window is free again once both kernels have read it
+        pl.release(k, 0, ks);
+        pl.release(k, 1, kc);
+        t_enq += wall_s() - td;
+        k ^= 1;
+    }
+    *max_live = sched.max_live();
+    if (trace_on())
+        fprintf(stderr,
+                "krk_trace windows: windows=%d W=%zu max_live=%llu loop=%.3fs acquire=%.3fs build=%.3fs fill=%.3fs "
+                "enqueue=%.3fs\n",
+                *n_windows, W, (unsigned long long)*max_live, wall_s() - t0, t_acq, t_build, t_fill, t_enq);
+    return r;
+}
+
+// KRK_LIVE_CAP: overrides the window's live-stream cap (tests, sweeps).
+uint64_t live_cap_for(Device* D) {
+    const char* e = getenv("KRK_LIVE_CAP");
+    const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return v ? v : window_stream_cap(D);
+}
+
+struct CallStats {
+    uint64_t max_live = 0;
+    int windows = 0;
+    uint64_t host_blobs = 0;
+};
+thread_local CallStats t_last_call;
+
+}  // namespace
+
+}  // namespace krk
+
+using namespace krk;
+
+// The device results, the host offload's results and the caller's arrays of one call.
+namespace {
+struct Outputs {
+    uint8_t* d_dig = nullptr;
+    uint32_t *d_state = nullptr, *d_sums = nullptr;
+    DevMem mem;
+    int alloc(uint64_t n, uint64_t hi) {
+        KRK_HIP(mem.alloc(&d_dig, n * 32));
+        KRK_HIP(mem.alloc(&d_state, n * 32));
+        KRK_HIP(mem.alloc(&d_sums, std::max<uint64_t>(hi, 1) * 4));
+        KRK_HIP(hipMemset(d_sums, 0, std::max<uint64_t>(hi, 1) * 4));
+        return KRK_OK;
+    }
+};
+}  // namespace
+
+extern "C" {
+
+int krk_window_stream_cap(uint64_t* cap) {
+    KRK_CHECK(cap, KRK_EINVAL, "cap is NULL");
+    KRK_DEVICE(D);
+    *cap = window_stream_cap(D);
+    return KRK_OK;
+}
+
+struct krk_window_sched {
+    std::vector<uint64_t> lens;
+    std::unique_ptr<WindowSched> s;
+    std::vector<WinChunk> win;
+};
+
+int krk_window_sched_new(const uint64_t* lengths, uint64_t n, uint64_t window_bytes, uint64_t live_cap,
+                         krk_window_sched** out) {
+    KRK_CHECK(out && (n == 0 || lengths), KRK_EINVAL, "window_sched_new: null argument");
+    KRK_CHECK(window_bytes >= 64 && live_cap >= 1, KRK_EINVAL, "window bytes >= 64 and live cap >= 1");
+    KRK_CHECK(n <= 0xFFFFFFFFull, KRK_EINVAL, "more than 2^32 blobs");
+    auto* w = new krk_window_sched();
+    w->lens.assign(lengths, lengths + n);
+    std::vector<uint32_t> all(n);
+    for (uint64_t i = 0; i < n; ++i) all[i] = (uint32_t)i;
+    w->s = std::make_unique<WindowSched>(w->lens.data(), std::move(all), window_bytes, live_cap);
+    *out = w;
+    return KRK_OK;
+}
+
+int krk_window_sched_next(krk_window_sched* w, uint32_t* blobs, uint64_t* offsets, uint64_t* lengths, uint64_t cap,
+                          uint64_t* n_out) {
+    KRK_CHECK(w && n_out, KRK_EINVAL, "window_sched_next: null argument");
+    if (!w->s->next(w->win)) {
+        *n_out = 0;
+        return KRK_OK;
+    }
+    *n_out = w->win.size();
+    KRK_CHECK(w->win.size() <= cap, KRK_ERANGE, "window has %zu chunks, capacity %llu", w->win.size(),
+              (unsigned long long)cap);
+    for (size_t k = 0; k < w->win.size(); ++k) {
+        if (blobs) blobs[k] = w->win[k].blob;
+        if (offsets) offsets[k] = w->win[k].off;
+        if (lengths) lengths[k] = w->win[k].len;
+    }
+    return KRK_OK;
+}
+
+void krk_window_sched_free(krk_window_sched* w) { delete w; }
+
+int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {
+    KRK_DEVICE(D);
+    int r = validate_blobs(blobs, n);
+    if (r) return r;
+    if (!n) return KRK_OK;
+    KRK_CHECK(digests_host, KRK_EINVAL, "digests_host is NULL");
+    uint64_t lo, hi;
+    sums_span(blobs, n, &lo, &hi);
+    KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
+    std::vector<uint64_t> lens(n), soff(n);
+    std::vector<int64_t> plens(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        lens[i] = blobs[i].length;
+        plens[i] = blobs[i].piece_length;
+        soff[i] = blobs[i].sums_offset;
+    }
+    // SHA-256 host offload (KRK_OFFLOAD_AUTO by default): the planner's blobs are hashed and
+    // piece-summed in place on host threads and never cross the host link.
+    std::vector<char> on_host(n, 0);
+    std::vector<uint32_t> host;
+    const int off_t = offload_threads(kOffHostWhole);
+    if (off_t > 0) {
+        host = offload_plan(lens.data(), n, off_t, planner_rates(D), nullptr, nullptr, kOffHostWhole);
+        for (uint32_t i : host) on_host[i] = 1;
+    }
+    Outputs o;
+    r = o.alloc(n, hi);
+    if (r) return r;
+    std::vector<uint8_t> host_dig(32 * host.size());
+    std::vector<uint64_t> host_sums_off(host.size() + 1, 0);
+    for (size_t j = 0; j < host.size(); ++j)
+        host_sums_off[j + 1] = host_sums_off[j] + krk_num_pieces(lens[host[j]], plens[host[j]]);
+    std::vector<uint32_t> host_sums(host_sums_off.back());
+    std::thread host_th;
+    if (!host.empty())
+        host_th = std::thread([&] {
+            std::vector<const uint8_t*> p(host.size());
+            std::vector<uint64_t> l(host.size()), pl(host.size());
+            std::vector<uint32_t*> so(host.size());
+            for (size_t j = 0; j < host.size(); ++j) {
+                p[j] = blobs[host[j]].data;
+                l[j] = lens[host[j]];
+                pl[j] = (uint64_t)plens[host[j]];
+                so[j] = host_sums.data() + host_sums_off[j];
+            }
+            offload_whole_host(p, l, pl, so, off_t, host_dig.data());
+        });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{host_th};
+    // The copy threads and the offload's threads share the process's CPU budget: above it
+    // a CPU quota throttles the whole process.
+    struct ShareGuard {
+        int saved;
+        ~ShareGuard() { t_host_share = saved; }
+    } share_guard{t_host_share};
+    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
+    MemFiller filler(blobs);
+    CallStats st;
+    r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, 64, live_cap_for(D), o.d_sums,
+                     o.d_dig, o.d_state, &st.max_live, &st.windows);
+    if (!r && (hipStreamSynchronize(D->s_a) != hipSuccess || hipStreamSynchronize(D->s_b) != hipSuccess ||
+               hipStreamSynchronize(D->s_main) != hipSuccess)) {
+        set_error(KRK_EHIP, "metainfo_digest_host: sync failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hipMemcpy(digests_host, o.d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "digest copy-out failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hi > lo && hipMemcpy(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "sums copy-out failed");
+        r = KRK_EHIP;
+    }
+    if (host_th.joinable()) host_th.join();
+    for (size_t q = 0; !r && q < host.size(); ++q) {
+        memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
+        if (host_sums_off[q + 1] > host_sums_off[q])
+            memcpy(sums_host + soff[host[q]], &host_sums[host_sums_off[q]], (host_sums_off[q + 1] - host_sums_off[q]) * 4);
+    }
+    st.host_blobs = host.size();
+    t_last_call = st;
+    return r;
+}
+
+int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {
+    KRK_DEVICE(D);
+    if (!n) return KRK_OK;
+    KRK_CHECK(files && digests_host, KRK_EINVAL, "metainfo_digest_files: null argument");
+    std::vector<uint64_t> lens(n), soff(n);
+    std::vector<int64_t> plens(n);
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        KRK_CHECK(files[i].path, KRK_EINVAL, "file %llu: path is NULL", (unsigned long long)i);
+        KRK_CHECK(files[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
+        lens[i] = files[i].length;
+        plens[i] = files[i].piece_length;
+        soff[i] = files[i].sums_offset;
+        const uint64_t np = krk_num_pieces(lens[i], plens[i]);
+        KRK_CHECK(soff[i] + np <= 0xFFFFFFFFull, KRK_EINVAL, "sums index exceeds 2^32 in one call");
+        if (np) {
+            lo = std::min(lo, soff[i]);
+            hi = std::max(hi, soff[i] + np);
+        }
+    }
+    if (lo > hi) lo = hi = 0;
+    KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
+    // Host offload (AUTO by default): the planner's files are read, hashed and piece-summed
+    // by host threads in one pass each and never cross the host link.
+    std::vector<char> on_host(n, 0);
+    std::vector<uint32_t> host;
+    const int off_t = offload_threads(kOffHostWhole);
+    if (off_t > 0) {
+        host = offload_plan(lens.data(), n, off_t, planner_rates(D), nullptr, nullptr, kOffHostFiles);
+        for (uint32_t i : host) on_host[i] = 1;
+    }
+    Outputs o;
+    int r = o.alloc(n, hi);
+    if (r) return r;
+    std::vector<uint8_t> host_dig(32 * host.size());
+    std::vector<uint64_t> host_sums_off(host.size() + 1, 0);
+    for (size_t j = 0; j < host.size(); ++j)
+        host_sums_off[j + 1] = host_sums_off[j] + krk_num_pieces(lens[host[j]], plens[host[j]]);
+    std::vector<uint32_t> host_sums(host_sums_off.back());
+    int host_rc = KRK_OK;
+    std::string host_err;
+    std::thread host_th;
+    if (!host.empty())
+        host_th = std::thread([&] {
+            std::vector<const char*> p(host.size());
+            std::vector<uint64_t> l(host.size()), pl(host.size());
+            std::vector<uint32_t*> so(host.size());
+            for (size_t j = 0; j < host.size(); ++j) {
+                p[j] = files[host[j]].path;
+                l[j] = lens[host[j]];
+                pl[j] = (uint64_t)plens[host[j]];
+                so[j] = host_sums.data() + host_sums_off[j];
+            }
+            host_rc = offload_whole_files(p, l, pl, so, off_t, host_dig.data());
+            if (host_rc) host_err = t_err;
+        });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{host_th};
+    struct ShareGuard {
+        int saved;
+        ~ShareGuard() { t_host_share = saved; }
+    } share_guard{t_host_share};
+    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
+    const bool direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
+    FileFiller filler(files, n, direct);
+    CallStats st;
+    // at most as many live blobs as this call may hold files open
+    const uint64_t cap = std::min(live_cap_for(D), fd_budget());
+    r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, cap,
+                     o.d_sums, o.d_dig, o.d_state, &st.max_live, &st.windows);
+    // drain what was queued even after a read error (the windows' kernels read the buffers)
+    const bool synced = hipStreamSynchronize(D->s_a) == hipSuccess && hipStreamSynchronize(D->s_b) == hipSuccess &&
+                        hipStreamSynchronize(D->s_main) == hipSuccess;
+    if (!r && !synced) {
+        set_error(KRK_EHIP, "metainfo_digest_files: sync failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hipMemcpy(digests_host, o.d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "digest copy-out failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hi > lo && hipMemcpy(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "sums copy-out failed");
+        r = KRK_EHIP;
+    }
+    if (host_th.joinable()) host_th.join();
+    if (!r && host_rc) {
+        t_err = host_err;
+        r = host_rc;
+    }
+    for (size_t q = 0; !r && q < host.size(); ++q) {
+        memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
+        if (host_sums_off[q + 1] > host_sums_off[q])
+            memcpy(sums_host + soff[host[q]], &host_sums[host_sums_off[q]], (host_sums_off[q + 1] - host_sums_off[q]) * 4);
+    }
+    st.host_blobs = host.size();
+    t_last_call = st;
+    return r;
+}
+
+int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs) {
+    if (max_live) *max_live = t_last_call.max_live;
+    if (windows) *windows = t_last_call.windows;
+    if (host_blobs) *host_blobs = t_last_call.host_blobs;
+    return KRK_OK;
+}
+
+}  // extern "C"

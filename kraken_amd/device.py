@@ -6,7 +6,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._capi import check, krk_blob, krk_chunk, krk_launch_rec, krk_nodes, krk_planner_rates, lib
+from ._capi import check, krk_blob, krk_file_blob, krk_chunk, krk_launch_rec, krk_nodes, krk_planner_rates, lib
 
 ALIGN = 256  # every blob starts 256-byte aligned in the arena
 
@@ -255,7 +255,7 @@ def set_sha_host_offload(threads: int):
     check(lib.krk_set_sha_host_offload(int(threads)))
 
 
-OFFLOAD_DEVICE, OFFLOAD_HOST_SHA, OFFLOAD_HOST_WHOLE = 0, 1, 2
+OFFLOAD_DEVICE, OFFLOAD_HOST_SHA, OFFLOAD_HOST_WHOLE, OFFLOAD_HOST_FILES = 0, 1, 2, 3
 
 
 def piece_sums_host(datas, piece_length: int):
@@ -364,6 +364,54 @@ def metainfo_digest_host(datas, piece_lengths, multi: bool = False):
     fn = lib.krk_metainfo_digest_host_multi if multi else lib.krk_metainfo_digest_host
     check(fn(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)), dg.ctypes.data_as(C.POINTER(C.c_uint8))))
     return [sums[int(offs[i]):int(offs[i + 1])] for i in range(n)], dg[:n]
+
+
+def metainfo_digest_files(paths, lengths, piece_lengths, multi: bool = False):
+    """krk_metainfo_digest_files: the digests and piece sums of CAS files, each read once
+    (pinned windows -> both kernels; the planner's files on host threads).  lengths: the
+    sizes the caller stat-ed.  Returns (sums per file, digests).  multi: the _multi form
+    (LPT over the device set)."""
+    n = len(paths)
+    L = np.asarray(lengths, dtype=np.uint64)
+    pls = np.broadcast_to(np.asarray(piece_lengths, dtype=np.int64), (n,))
+    counts = [int(lib.krk_num_pieces(int(l), int(p))) for l, p in zip(L, pls)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(counts) if n else []
+    enc = [p.encode() if isinstance(p, str) else bytes(p) for p in paths]
+    arr = (krk_file_blob * max(n, 1))()
+    for i in range(n):
+        arr[i] = krk_file_blob(enc[i], int(L[i]), int(pls[i]), int(offs[i]))
+    sums = np.zeros(max(int(offs[-1]), 1), dtype=np.uint32)
+    dg = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    fn = lib.krk_metainfo_digest_files_multi if multi else lib.krk_metainfo_digest_files
+    check(fn(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)), dg.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return [sums[int(offs[i]):int(offs[i + 1])] for i in range(n)], dg[:n]
+
+
+def windows_last_call() -> dict:
+    """The calling thread's last krk_metainfo_digest_host / _files call: the most live blobs
+    in a window, the windows, the blobs the host offload took (krk_windows_last_call)."""
+    m, w, h = C.c_uint64(), C.c_int(), C.c_uint64()
+    check(lib.krk_windows_last_call(C.byref(m), C.byref(w), C.byref(h)))
+    return {"max_live": m.value, "windows": w.value, "host_blobs": h.value}
+
+
+def device_pci_bus_id() -> str:
+    b = C.create_string_buffer(64)
+    check(lib.krk_device_pci_bus_id(b, 64))
+    return b.value.decode()
+
+
+def device_cus() -> int:
+    v = C.c_int(0)
+    check(lib.krk_device_cus(C.byref(v)))
+    return v.value
+
+
+def window_stream_cap() -> int:
+    v = C.c_uint64(0)
+    check(lib.krk_window_stream_cap(C.byref(v)))
+    return v.value
 
 
 class ChunkedBatch:

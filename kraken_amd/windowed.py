@@ -30,30 +30,38 @@ def c3_lengths(n_total=20000, scale: int = 1):
 
 
 def window_plan(lens, W, cap):
-    """Windows: [(blob indices, offsets, chunk lengths)].  Every live blob advances by
-    the same 64-multiple chunk per window (about W bytes a window).  Admission: at most
-    `cap` blobs are live, admitted longest first, so the longest chain starts in window 0
-    and every window stays on a multi-lane SHA plan (eight lanes a stream up to 16 x CUs
-    live streams, two up to 64 x CUs; a launch of more streams falls back to one lane per
-    stream, ~0.7x per stream); a finished blob's slot goes to the
-    next-longest waiting blob."""
-    L = np.asarray(lens, dtype=np.uint64)
+    """Windows: [(blob indices, offsets, chunk lengths)] -- the library's window schedule
+    (krk_window_sched_*, kraken_amd/csrc/windows.cpp; the same one its host-resident batch
+    calls run).  Every live blob advances by the same 64-multiple chunk per window (about W
+    bytes a window).  Admission: at most `cap` blobs are live, admitted longest first, so the
+    longest chain starts in window 0 and every window stays on a multi-lane SHA plan (eight
+    lanes a stream up to 16 x CUs live streams, two up to 64 x CUs; a launch of more streams
+    falls back to one lane per stream, ~0.7x per stream); a finished blob's
+    slot goes to the next-longest waiting blob."""
+    from ._capi import check, lib
+    L = np.ascontiguousarray(lens, dtype=np.uint64)
     n = L.size
-    cap = max(1, min(int(cap), n)) if n else 1
-    queue = list(np.argsort(-L.astype(np.int64), kind="stable"))
-    wins, pos = [], np.zeros(n, dtype=np.uint64)
-    live = np.asarray(sorted(queue[:cap]), dtype=np.int64)
-    queue = queue[cap:]
-    while live.size:
-        c = max(64, (W // live.size) // 64 * 64)
-        take = np.minimum(np.uint64(c), L[live] - pos[live])
-        wins.append((live, pos[live].copy(), take))
-        pos[live] += take
-        live = live[pos[live] < L[live]]
-        if queue and live.size < cap:
-            k = cap - live.size
-            live = np.sort(np.concatenate([live, np.asarray(queue[:k], dtype=np.int64)]))
-            queue = queue[k:]
+    if n == 0:
+        return []
+    cap = max(1, min(int(cap), n))
+    h = C.c_void_p()
+    check(lib.krk_window_sched_new(L.ctypes.data_as(C.POINTER(C.c_uint64)), n, int(W), cap, C.byref(h)))
+    wins = []
+    try:
+        b = np.zeros(cap, dtype=np.uint32)
+        o = np.zeros(cap, dtype=np.uint64)
+        t = np.zeros(cap, dtype=np.uint64)
+        k = C.c_uint64(0)
+        while True:
+            check(lib.krk_window_sched_next(h, b.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                            o.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            t.ctypes.data_as(C.POINTER(C.c_uint64)), cap, C.byref(k)))
+            if not k.value:
+                break
+            m = k.value
+            wins.append((b[:m].astype(np.int64), o[:m].copy(), t[:m].copy()))
+    finally:
+        lib.krk_window_sched_free(h)
     return wins
 
 
@@ -73,15 +81,16 @@ def two_lane_stream_cap(D, n):
 
 def window_stream_cap(D, n):
     """Live streams per window: at most 7/8 of the largest multi-lane stream count (a
-    multiple of the two-pair workgroup's 64 streams).  At the full two-lane count
-    (64 x CUs) every CU holds a 128 KiB SHA workgroup and the window's piece-CRC launch
-    (144 KiB workgroups) waits for the SHA launch to end; with an eighth of the CUs left
-    free it runs inside it, and the chain of the longest blob -- not the live count --
-    still sets the run time.  C3 on one MI355X (bench --live-cap): 16,384 live 494 GB/s,
-    15,360 522, 14,336 524, 13,824 523, 13,312 522, 12,288 509 (profiles/r02/c3_live_cap.jsonl)."""
-    full = two_lane_stream_cap(D, 1 << 30) if n else 1
-    cap = max(64, (full * 7 // 8) // 64 * 64)
-    return max(1, min(n, cap))
+    multiple of the two-pair workgroup's 64; krk_window_stream_cap, the cap the library's
+    host-resident windows use too).  At the full two-lane count (64 x CUs) every CU holds a
+    128 KiB SHA workgroup and the window's piece-CRC launch (144 KiB workgroups) waits for
+    the SHA launch to end; with an eighth of the CUs left free it runs inside it, and the
+    chain of the longest blob -- not the live count -- still sets the run time.  C3 on one
+    MI355X (bench --live-cap): 16,384 live 494 GB/s, 15,360 522, 14,336 524, 13,824 523,
+    13,312 522, 12,288 509 (profiles/r02/c3_live_cap.jsonl)."""
+    v = C.c_uint64(0)
+    D.check(D.lib.krk_window_stream_cap(C.byref(v)))
+    return max(1, min(n, v.value))
 
 
 def stream_rate(rates, n_streams):

@@ -50,3 +50,32 @@ def test_fewer_devices_refused_unless_rehearse(child, tmp_path):
 def test_failed_rank_fails_the_run(child, tmp_path, monkeypatch):
     monkeypatch.setenv("FAIL_RANK", "1")
     assert bench.spawn_ranks(2, [str(tmp_path)], devices=2, script=child) == 3
+
+
+TIMER_CHILD = r'''
+import json, os, sys
+sys.path.insert(0, sys.argv[2])
+import torch.distributed as dist
+import bench
+dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+T = bench.Timer(None, dist)
+r = int(os.environ["RANK"])
+mx = T.timed_region(0.5 + r)
+devs = T.gather("0000:%02x:00.0" % (r + 3))
+with open(os.path.join(sys.argv[1], "t%d.json" % r), "w") as f:
+    json.dump({"max": mx, "rank_s": T.rank_s, "devs": devs}, f)
+dist.destroy_process_group()
+'''
+
+
+def test_timer_gathers_every_ranks_time_and_device(tmp_path):
+    """VERDICT r03 item 4 (CPU, gloo, world 2): the timed region's max over ranks, every
+    rank's own time and every rank's device id reach every rank (rank 0 prints them as
+    rank_ms / rank_devices)."""
+    script = tmp_path / "timer_child.py"
+    script.write_text(TIMER_CHILD)
+    assert bench.spawn_ranks(2, [str(tmp_path), ROOT], devices=2, script=str(script)) == 0
+    for r in range(2):
+        d = json.load(open(tmp_path / f"t{r}.json"))
+        assert d["max"] == 1.5 and d["rank_s"] == [0.5, 1.5]
+        assert d["devs"] == ["0000:03:00.0", "0000:04:00.0"]

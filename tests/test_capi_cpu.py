@@ -388,8 +388,12 @@ def test_host_offload_plan_modes():
     assert D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_DEVICE)[0].size == 0
     idx, g, h = D.sha_offload_plan([1 << 30], 4, mode=D.OFFLOAD_HOST_SHA)  # C1 from host memory
     assert list(idx) == [0] and g == 0.0 and h > 0
+    # cache files (one read, SHA-256 + CRC a chunk on one thread): fewer blobs than the
+    # whole-blob mode, whose two passes run on two threads
+    idx_f, gf, hf = D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_HOST_FILES)
+    assert max(gf, hf) <= g0 and idx_f.size <= D.sha_offload_plan(c2, 16, mode=D.OFFLOAD_HOST_WHOLE)[0].size
     with pytest.raises(Exception):
-        D.sha_offload_plan(c2, 4, mode=3)
+        D.sha_offload_plan(c2, 4, mode=4)
 
 
 def test_planner_moves_with_injected_rates():

@@ -39,9 +39,12 @@ def test_bench_json_line_contract(gpu):
 def test_bench_gpus_2_spawns_two_ranks(gpu):
     """`bench.py --gpus 2` with no launcher spawns two rank processes (here sharing the
     one GPU: --rehearse) and reports the whole job: n_gpus == 2 and value == both
-    ranks' bytes over the max-over-ranks time."""
+    ranks' bytes over the max-over-ranks time.  VERDICT r03 item 4: the N-rank line is
+    self-verifying -- rank 0's CPU baseline (timed after the GPU region while the other
+    ranks wait), every rank's device PCI bus id and own time; here both ranks share the
+    one GPU, which only a rehearsal may."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse", "--blobs", "20",
-                        "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-e2e", "--no-ceiling"],
+                        "--steps", "1", "--warmup", "1", "--cpu-seconds", "1", "--no-e2e", "--no-ceiling"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -51,6 +54,10 @@ def test_bench_gpus_2_spawns_two_ranks(gpu):
     assert d["config"]["blobs_per_gpu"] == 20 and d["config"]["parallelism"].startswith("blob-sharded x2")
     want = 2 * d["config"]["bytes_per_gpu"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3) / 1e9
     assert abs(d["value"] - want) / want < 1e-3, (d["value"], want)
+    assert len(d["rank_devices"]) == 2 and len(set(d["rank_devices"])) == 1  # one GPU, two ranks
+    assert len(d["rank_ms"]) == 2 and abs(max(d["rank_ms"]) - d["ms_per_step"] * d["steps"]) < 1e-2
+    cb = d["cpu_baseline"]
+    assert cb["cores"] >= 1 and cb["value"] > 0 and cb["outputs_match_gpu"] is True
 
 
 def test_bench_gpus_more_than_visible_refused(gpu):

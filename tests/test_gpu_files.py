@@ -1,0 +1,181 @@
+"""VERDICT r03 item 2 / SURVEY 8(f) row 3: upload and cache-fill verification fused with the
+metainfo, from the CAS files themselves -- krk_metainfo_digest_files (+ _multi): each file is
+read once (pread into the pinned windows, on the host pool) and that read feeds the
+SHA-256 digest of uploader.verify / CAStore.WriteCacheFile (origin/blobserver/uploader.go:
+74-94, lib/store/ca_store.go:99-135) AND the piece CRCs of Generator.Generate
+(lib/metainfogen/generator.go:41-58), where the reference reads the file twice.
+
+* Edge lengths x piece lengths against the oracle, with the host offload off and on (the
+  planner's files then read, hashed and piece-summed in one pass on host threads) and with a
+  small live cap (admission), plus the reference's error texts.
+* The production window shape: 16,384 blobs of the C3 length law / 64 (1.6-16.8 MB) from
+  files and from pinned host memory (krk_metainfo_digest_host) through the C++ window
+  schedule -- 14,336 live streams (7/8 of the two-lane count) on the two-lane two-pair plan
+  (KRK_SHA_PLAN_2LANE_2PAIR = 4, krk_kernel_timeline), late admission of the other 2,048 --
+  every blob equal to the one-shot device path, the shortest, longest, a partial and a late
+  blob equal to the oracle."""
+import hashlib
+import os
+import resource
+
+import numpy as np
+import pytest
+
+from kraken_amd import device as D
+from kraken_amd._capi import KRK_EIO, KrakenError, check, krk_blob, lib
+from kraken_amd.windowed import c3_lengths
+
+pytestmark = pytest.mark.gpu
+
+EDGE = [0, 1, 63, 64, 65, 4095, 4096, 4097, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, 3 * (1 << 20) + 5, 9_999_999]
+
+
+def _write(tmp_path, name, data):
+    p = str(tmp_path / name)
+    with open(p, "wb") as f:
+        f.write(memoryview(data))
+    return p
+
+
+@pytest.mark.parametrize("P", [1 << 20, 3, 4 << 20])
+@pytest.mark.parametrize("mode", ["gpu", "offload", "cap3"])
+def test_files_edge_lengths_match_oracle(gpu, orc, tmp_path, P, mode, monkeypatch):
+    lens = EDGE if P != 3 else [0, 1, 2, 3, 4, 64, 65, 100_001]
+    datas = [orc.synth(50 + i, L) for i, L in enumerate(lens)]
+    paths = [_write(tmp_path, f"b{i}", d) for i, d in enumerate(datas)]
+    if mode == "cap3":
+        monkeypatch.setenv("KRK_LIVE_CAP", "3")
+    if mode == "offload":
+        D.set_sha_host_offload(8)
+        D.set_planner_rates(dict(D.planner_rates(), sha_stream_bps=[1e6, 1e6, 1e6]))  # the host takes files
+    try:
+        sums, dg = D.metainfo_digest_files(paths, lens, P)
+        st = D.windows_last_call()
+    finally:
+        D.set_sha_host_offload(0)
+        D.set_planner_rates(None)
+    for i, d in enumerate(datas):
+        assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), (i, lens[i])
+        assert np.array_equal(sums[i], orc.calc_piece_sums(d, P)[1]), (i, lens[i])
+    if mode == "offload":
+        assert st["host_blobs"] > 0
+    if mode == "cap3":
+        assert st["max_live"] == 3 and st["windows"] >= len(lens) // 3
+
+
+def test_files_errors_keep_reference_texts(gpu, orc, tmp_path):
+    d = orc.synth(1, 1 << 20)
+    p = _write(tmp_path, "short", d)
+    with pytest.raises(KrakenError) as e:
+        D.metainfo_digest_files([p], [(1 << 20) + 10], 1 << 20)  # stat said longer: EOF
+    assert e.value.code == KRK_EIO and str(e.value).endswith(f"read blob: {p}: unexpected EOF")
+    missing = str(tmp_path / "nope")
+    with pytest.raises(KrakenError) as e:
+        D.metainfo_digest_files([p, missing], [1 << 20, 5], 1 << 20)
+    assert e.value.code == KRK_EIO and f"open {missing}: No such file or directory" in str(e.value)
+    with pytest.raises(KrakenError, match="piece length must be positive"):
+        D.metainfo_digest_files([p], [1 << 20], 0)
+    # the library is usable after the failures
+    sums, dg = D.metainfo_digest_files([p], [1 << 20], 1 << 20)
+    assert bytes(dg[0]) == hashlib.sha256(d.tobytes()).digest()
+
+
+def test_files_multi_equals_single(gpu, orc, tmp_path):
+    lens = [int(x) for x in np.random.default_rng(5).integers(0, 6 << 20, 40)]
+    datas = [orc.synth(900 + i, L) for i, L in enumerate(lens)]
+    paths = [_write(tmp_path, f"m{i}", d) for i, d in enumerate(datas)]
+    s1, d1 = D.metainfo_digest_files(paths, lens, 1 << 20)
+    check(lib.krk_set_devices((C_int * 2)(0, 0), 2))
+    try:
+        s2, d2 = D.metainfo_digest_files(paths, lens, 1 << 20, multi=True)
+    finally:
+        check(lib.krk_set_devices(None, 0))
+    assert np.array_equal(d1, d2) and all(np.array_equal(a, b) for a, b in zip(s1, s2))
+    for i in (0, 17, 39):
+        assert bytes(d1[i]) == hashlib.sha256(datas[i].tobytes()).digest()
+
+
+from ctypes import c_int as C_int  # noqa: E402
+
+N, SCALE, P4 = 16384, 64, 4 << 20
+SOURCES = 64  # blob i = a prefix of source i % 64 (1 GB of distinct bytes for 151 GB of blobs)
+
+
+@pytest.fixture(scope="module")
+def c3_law(gpu, orc, tmp_path_factory):
+    lens = c3_lengths(N, scale=SCALE)
+    top = max(lens)
+    srcs = [orc.synth((3 << 40) + s, top) for s in range(SOURCES)]
+    d = tmp_path_factory.mktemp("c3files")
+    paths = []
+    for s, x in enumerate(srcs):
+        p = str(d / f"src{s}")
+        with open(p, "wb") as f:
+            f.write(memoryview(x))
+        paths.append(p)
+    # one-shot device reference: every blob a prefix of its source in HBM
+    dev = D.DeviceBuffer(SOURCES * top)
+    for s, x in enumerate(srcs):
+        dev.from_host(x, s * top)
+    n_p = [int(lib.krk_num_pieces(L, P4)) for L in lens]
+    offs = np.zeros(N + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(n_p)
+    arr = (krk_blob * N)()
+    for i, L in enumerate(lens):
+        arr[i] = krk_blob(dev.ptr + (i % SOURCES) * top, L, P4, int(offs[i]))
+    sums_d = D.DeviceBuffer(int(offs[-1]) * 4)
+    dg_d = D.DeviceBuffer(N * 32)
+    check(lib.krk_metainfo_digest_dev(arr, N, sums_d.ptr, dg_d.ptr, None))
+    D.synchronize()
+    one = (sums_d.to_host(np.uint32, int(offs[-1])), dg_d.to_host(np.uint8, N * 32).reshape(N, 32))
+    del dev, sums_d, dg_d
+    return lens, srcs, paths, offs, one
+
+
+def _check_against_one_shot_and_oracle(lens, srcs, offs, one, sums, dg, orc):
+    s1, d1 = one
+    assert np.array_equal(dg, d1)
+    for i in range(N):
+        assert np.array_equal(sums[i], s1[int(offs[i]):int(offs[i + 1])]), i
+    L = np.asarray(lens)
+    order = np.argsort(-L, kind="stable")
+    late = int(order[14336])  # the first blob admitted after the initial 14,336
+    partial = int(np.flatnonzero(L % P4)[0])
+    for i in sorted({int(L.argmin()), int(L.argmax()), partial, late}):
+        data = srcs[i % SOURCES][:lens[i]]
+        assert bytes(dg[i]) == hashlib.sha256(data.tobytes()).digest(), i
+        assert np.array_equal(sums[i], orc.calc_piece_sums(data, P4)[1]), i
+
+
+@pytest.mark.parametrize("source", ["files", "pinned"])
+def test_c3_law_16384_blobs_production_windows(gpu, orc, c3_law, source):
+    lens, srcs, paths, offs, one = c3_law
+    cap = D.window_stream_cap()
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if source == "files" and soft < cap + 1024:  # what Go's runtime does at start-up (os package)
+        resource.setrlimit(resource.RLIMIT_NOFILE, (min(hard, 1 << 20), hard))
+    bufs = []
+    try:
+        with D.KernelTimer():
+            if source == "files":
+                sums, dg = D.metainfo_digest_files([paths[i % SOURCES] for i in range(N)], lens, P4)
+            else:
+                for x in srcs:  # the sources in pinned host memory (krk_host_alloc)
+                    pa = D.PinnedArray((x.size,), np.uint8)
+                    pa.a[:] = x
+                    bufs.append(pa)
+                datas = [bufs[i % SOURCES].a[:lens[i]] for i in range(N)]
+                sums, dg = D.metainfo_digest_host(datas, P4)
+            st = D.windows_last_call()
+            tl = [(p, u) for p, u, _, _ in D.KernelTimer.timeline("sha256_multi")]
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+        bufs.clear()
+    print(source, st, cap, tl[:3], len(tl))
+    assert cap % 64 == 0 and cap == 14336 * D.device_cus() // 256  # 7/8 of the two-lane count
+    want_live = cap if source == "pinned" or min(hard, 1 << 20) >= cap + 1024 else st["max_live"]
+    assert st["max_live"] == want_live and st["host_blobs"] == 0
+    if want_live == 14336:
+        assert tl[0] == (4, 14336), tl[:3]  # KRK_SHA_PLAN_2LANE_2PAIR at the cap
+    assert st["windows"] > 100  # late admission: live shrinks below the cap only at the end
+    _check_against_one_shot_and_oracle(lens, srcs, offs, one, sums, dg, orc)
