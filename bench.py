@@ -113,6 +113,14 @@ WORKLOADS = {
                desc="C4: one 20 GiB blob per GPU, 256 KiB pieces (81,920), piece sums only"),
     "c3": dict(kind="chunked", desc="C3: 20k blobs of 100 MiB + (rng mod 968,884,225) B, 4 MiB pieces, "
                                     "LPT-sharded by blob, streamed through HBM in windows"),
+    "engine": dict(kind="engine", steps=3, warmup=1,
+                   desc="256 concurrent GPU Digesters (core.Digester per upload / cache fill, "
+                        "origin/blobserver/uploader.go:75) on 256 native threads, 16 MiB each in random writes of "
+                        "up to 1 MiB (tests/native/digesters.cpp, a C-ABI caller like the cgo layer)"),
+    "files": dict(kind="files", steps=3, warmup=1,
+                  desc="upload / cache-fill verify + metainfo from CAS files (uploader.go:74-94 + generator.go:41-58):"
+                       " 16,384 blobs of the C3 length law / 64 (1.6-16.8 MB, 151 GB a pass), each a prefix of one of"
+                       " 64 source files, 4 MiB pieces; every byte read once (pread -> pinned windows -> PCIe)"),
     "c5": dict(kind="hrw", steps=50, warmup=5,  # 0.4 ms steps: a few would time launch jitter
                desc="C5: 1M seeded 32-B digests -> hashring.Locations (ShardID key), "
                     "16 origins weight 100, MaxReplica 3, all healthy"),
@@ -683,6 +691,15 @@ def host_mem_budget():
 E2E_PASSES = 3
 
 
+def link_roofline(D, gbps):
+    """An end-to-end pass is bounded by the host link: every byte crosses PCIe once.  Peak =
+    the pinned H2D rate the planner measured on this device (krk_planner_rates_get)."""
+    h2d = D.planner_rates()["h2d_bps"] / 1e9
+    return {"bound": "host link (PCIe H2D)", "achieved": round(gbps, 3), "peak": round(h2d, 3), "unit": "GB/s",
+            "frac": round(gbps / h2d, 4) if h2d else None,
+            "peak_source": "pinned 64 MiB H2D measured on this device (krk_planner_rates_get: h2d_bps)"}
+
+
 def end_to_end(D, T, arena, n, Le, P, out, world):
     """End-to-end leg (reported beside `value`, never as it): the same blobs' first
     Le bytes in pageable host memory, through krk_metainfo_digest_host (pinned
@@ -722,7 +739,8 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
            "seconds": round(el, 3), "passes_s": [round(x, 3) for x in passes],
            "source": "pageable host memory (numpy), copied into pinned windows; median of the passes",
            "bound": "PCIe H2D (one pass per byte) and the per-blob SHA-256 chain (blob_bytes / per-stream rate)",
-           "sums_match_device_run": ok}
+           "sums_match_device_run": ok,
+           "roofline": link_roofline(D, world * n * Le / el / 1e9)}
     if out is not None and Le == int(arena.lengths[0]) and (arena.lengths == Le).all():  # whole blobs
         dev_dg = out.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
         res["digests_match_device_run"] = bool(np.array_equal(dg, dev_dg))
@@ -1106,6 +1124,134 @@ def hrw_sweep(D, dbuf, dig, n, steps):
     return out
 
 
+def run_files(a, D, T, rank, world, res):
+    """The f3 file leg (krk_metainfo_digest_files): the C3 length law / 64 from
+    files on the box's disk (page cache warm after the first pass).  value = blob bytes / time
+    of one call, every byte read once and over PCIe once (GPU only: the host offload off);
+    beside it the same batch from pinned host memory (krk_metainfo_digest_host) and the
+    library's default (AUTO offload).  Digests and piece sums of the three runs are equal and
+    sampled blobs equal the oracle."""
+    import resource
+    import shutil
+    import tempfile
+    n, SRC, P = a.blobs or 16384, 64, 4 << 20
+    lens = c3_lengths(n, scale=64)
+    top = max(lens)
+    d = tempfile.mkdtemp(prefix=f"krk_files_r{rank}_")
+    try:
+        srcs = []
+        for k in range(SRC):  # device-generated content, copied down and written once
+            buf = D.DeviceBuffer(top)
+            D.check(D.lib.krk_synth_fill_dev(buf.ptr, (3 << 40) + rank * SRC + k, 0, top, 0, None))
+            D.synchronize()
+            x = buf.to_host(np.uint8, top)
+            buf.free()
+            with open(os.path.join(d, f"src{k}"), "wb") as f:
+                f.write(memoryview(x))
+            srcs.append(x)
+        paths = [os.path.join(d, f"src{i % SRC}") for i in range(n)]
+        soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+        resource.setrlimit(resource.RLIMIT_NOFILE, (min(hard, 1 << 20), hard))  # as Go's runtime does
+        total = int(sum(lens))
+        for _ in range(a.warmup):
+            D.metainfo_digest_files(paths, lens, P)
+        T.barrier()
+        with D.KernelTimer():
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                sums_f, dg_f = D.metainfo_digest_files(paths, lens, P)
+            T.barrier()
+            t1 = time.perf_counter()
+            st = D.windows_last_call()
+            sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
+            crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
+        elapsed = T.timed_region(t1 - t0)
+        value = world * total * a.steps / elapsed / 1e9
+        # the same bytes from pinned host memory, and the library's default (AUTO offload)
+        pins = []
+        for x in srcs:
+            pa = D.PinnedArray((x.size,), np.uint8)
+            pa.a[:] = x
+            pins.append(pa)
+        datas = [pins[i % SRC].a[:lens[i]] for i in range(n)]
+        D.metainfo_digest_host(datas, P)
+        T.barrier()
+        t0 = time.perf_counter()
+        sums_p, dg_p = D.metainfo_digest_host(datas, P)
+        T.barrier()
+        el_p = T.max_over_ranks(time.perf_counter() - t0)
+        D.set_sha_host_offload(-1)
+        try:
+            T.barrier()
+            t0 = time.perf_counter()
+            sums_a, dg_a = D.metainfo_digest_files(paths, lens, P)
+            T.barrier()
+            el_a = T.max_over_ranks(time.perf_counter() - t0)
+            st_a = D.windows_last_call()
+        finally:
+            D.set_sha_host_offload(0)
+        same = (np.array_equal(dg_f, dg_p) and np.array_equal(dg_f, dg_a) and
+                all(np.array_equal(x, y) and np.array_equal(x, z) for x, y, z in zip(sums_f, sums_p, sums_a)))
+        from oracle import oracle as O  # checker only
+        O.build()
+        import hashlib
+        L = np.asarray(lens)
+        ok = True
+        for i in sorted({int(L.argmin()), int(L.argmax()), n // 2}):
+            x = srcs[i % SRC][:lens[i]]
+            ok = ok and bytes(dg_f[i]) == hashlib.sha256(x.tobytes()).digest() and np.array_equal(
+                sums_f[i], O.calc_piece_sums(x, P)[1])
+        del pins, datas
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    res.update({"metric": "upload verify + metainfo from files, GB/s (end-to-end, host link)",
+                "value": round(value, 3), "unit": "GB/s", "steps": a.steps,
+                "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+                "dtype": "u8", "data": "synthetic (device-generated splitmix64 sources written to local files)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "blobs_per_gpu": n, "bytes_per_gpu": total,
+                           "piece_length": P, "mode": "files -> pinned windows -> GPU (offload off)",
+                           "parallelism": f"blob-sharded x{world}, no collective"},
+                "roofline": link_roofline(D, value),
+                "windows": st, "kernels": {"sha256_multi": {"launches": sha_n, "avg_ms": round(sha_ms / max(sha_n, 1), 3)},
+                                           "crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_ms / max(crc_n, 1), 3)}},
+                "pinned_host_memory": {"value": round(world * total / el_p / 1e9, 3), "unit": "GB/s",
+                                       "roofline": link_roofline(D, world * total / el_p / 1e9),
+                                       "what": "the same blobs from pinned host memory (krk_metainfo_digest_host)"},
+                "default_offload": {"value": round(world * total / el_a / 1e9, 3), "unit": "GB/s",
+                                    "host_blobs": st_a["host_blobs"],
+                                    "what": "krk_metainfo_digest_files with the library's default host offload (AUTO)"},
+                "outputs_equal_across_paths": bool(same), "oracle_sampled_match": bool(ok)})
+
+
+def run_engine(a, D, T, rank, world, res):
+    """The submission engine under concurrent Digesters: tests/native/digesters
+    runs warmup + steps rounds of 256 GPU-placed digesters (a round = every digester's 16 MiB
+    and its digest); value = the timed rounds' bytes over their summed seconds.  Every digest
+    is checked against the host SHA-256 of the same bytes in the child (digests_match).  The
+    rate lives here, not in the parity tests."""
+    exe = os.path.join(ROOT, "tests", "native", "digesters")
+    n, mib = 256, 16
+    r = subprocess.run([exe, str(n), str(mib), str(a.warmup + a.steps)], capture_output=True, text=True, timeout=900)
+    rounds = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or len(rounds) != a.warmup + a.steps:
+        raise SystemExit(f"bench.py: digesters failed (rc {r.returncode}): {r.stderr[-2000:]}")
+    timed = rounds[a.warmup:]
+    secs = sum(x["seconds"] for x in timed)
+    el = T.timed_region(secs)
+    total = n * (mib << 20) * len(timed)
+    res.update({"metric": "concurrent GPU Digester GB/s (256 uploads)", "value": round(world * total / el / 1e9, 3),
+                "unit": "GB/s", "steps": a.steps, "ms_per_step": round(el / a.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "weak", "dtype": "u8",
+                "data": "synthetic (seeded random bytes, host memory of the native caller)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "digesters": n, "bytes_each": mib << 20,
+                           "placement": "KRK_PLACE_GPU (the submission engine)"},
+                "rounds": [{k: x[k] for k in ("round", "seconds", "GBps", "MBps_per_stream", "sha_launches",
+                                              "streams_per_launch", "digests_match")} for x in rounds],
+                "digests_match": all(x["digests_match"] for x in rounds),
+                "per_stream_ceiling_MBps": "~59 (the eight-lane batch kernel, DESIGN.md 4.2): 256 x 59 MB/s = "
+                                           "15.1 GB/s"})
+
+
 def visible_devices() -> int:
     """gfx950 devices a rank would see, counted in a child process so that the parent
     (which only spawns and waits) never initialises the GPU itself."""
@@ -1231,7 +1377,7 @@ def main():
         res["rehearsal"] = f"{world} ranks on {ndev} device(s): not an N-GPU measurement"
     kind = WORKLOADS[a.workload]["kind"]
     {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen,
-     "verify": run_verify}[kind](
+     "verify": run_verify, "engine": run_engine, "files": run_files}[kind](
         a, D, T, rank, world, res)
     # rank 0's CPU baseline (if any) ran after the timed region, behind this barrier the
     # other ranks wait at; then every rank's device and time go into the line, so an N-GPU

@@ -1,13 +1,18 @@
 """GPU parity at BASELINE.json's full sizes, where the oracle cannot recompute
 everything in seconds: sampled oracle checks plus size-independent properties.
 
-* C2 (configs[1]: 1,000 x 100 MiB, 4 MiB pieces, 105 GB in HBM): sampled blobs
-  against hashlib / the oracle, and decomposition invariance over ALL blobs --
+* C2 (configs[1]: 1,000 x 100 MiB, 4 MiB pieces, 105 GB in HBM): ALL 1,000 digests and
+  25,000 piece sums against the oracle's threaded runner (each blob regenerated on the
+  host, ~7 s on 16 threads), and decomposition invariance over all blobs --
   the chunked path (SHA-256 from per-blob midstates, CRC items cut at chunk edges
   that split pieces) must give the same 1,000 digests and 25,000 sums as the
   one-shot path (two different work decompositions of the same bytes).
 * C1 (configs[0]: one 1 GiB blob): the whole SHA-256 chain on one stream and the
   256 piece sums against hashlib / the oracle.
+* C3 (configs[2]'s blob law, unscaled): 256 seeded blobs of 100 MiB - 1 GiB (151.7 GB,
+  the bench's CPU-baseline sample, its longest 1.07 GB) through the production window
+  machinery (kraken_amd.windowed.WindowedRun, 48 GiB windows), every digest and piece sum
+  against the oracle.
 * C4 (configs[3]: one 20 GiB blob, 256 KiB pieces): sampled pieces against the
   oracle (content regenerated at the piece's offset), and CRC linearity -- the
   81,920 piece sums combined with crc(A||B) = shift(crc(A), |B|) ^ crc(B) equal the
@@ -78,6 +83,11 @@ def test_c2_full_size_decomposition_invariance(gpu, orc):
         assert bytes(dg[i]) == hashlib.sha256(data).digest(), i
         o = int(arena.sums_off[i])
         assert np.array_equal(sums[o:o + 25], orc.calc_piece_sums(data, P)[1]), i
+    # every blob against the oracle: its threaded runner regenerates each
+    # blob on the host and runs the reference's two passes, outputs kept
+    _, dgo, (so, offo) = orc.baseline_run_lazy(list(range(n)), [L] * n, P, _threads(), passes=3)
+    assert np.array_equal(dgo, dg)
+    assert np.array_equal(so[:int(offo[-1])], sums)  # the arena's sums are laid out blob by blob
     cb = D.ChunkedBatch([L] * n, P)
     chunk = 3 * P + 64 * 1001  # a multiple of 64 that cuts pieces at varying offsets
     pos = 0
@@ -88,6 +98,44 @@ def test_c2_full_size_decomposition_invariance(gpu, orc):
     D.synchronize()
     assert np.array_equal(cb.sums.to_host(np.uint32, arena.total_pieces), sums)
     assert np.array_equal(cb.digests.to_host(np.uint8, 32 * n).reshape(n, 32), dg)
+
+
+def _threads():
+    import os
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 32))
+
+
+def test_c3_unscaled_sample_windows_match_oracle(gpu, orc):
+    """C3 at unscaled lengths under a -m gpu test (it was only inside
+    bench.py's cpu_baseline_c3): the bench's seeded 256-blob sample of the 20,000-blob law."""
+    from kraken_amd.windowed import WindowedRun, c3_lengths
+    lens_all = c3_lengths(20000)
+    pick = np.sort(np.random.default_rng(0xC3).choice(20000, 256, replace=False))
+    lens = [int(lens_all[i]) for i in pick]
+    ids = [(2 << 40) + int(i) for i in pick]
+    assert max(lens) >= 1_070_000_000 and sum(lens) > 150e9
+    P = 4 << 20
+    wr = WindowedRun(D, ids, lens, P, 48 << 30)
+    try:
+        wr.run()
+        cb = wr.cb
+        dg = cb.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+        sums = cb.sums.to_host(np.uint32, cb.total_pieces)
+        offs = cb.sums_off.copy()
+    finally:
+        wr.close()
+    _, dgo, (so, offo) = orc.baseline_run_lazy(ids, lens, P, _threads(), passes=3)
+    assert np.array_equal(dgo, dg)
+    for k in range(len(lens)):
+        a, m = int(offs[k]), int(offo[k + 1] - offo[k])
+        assert np.array_equal(sums[a:a + m], so[int(offo[k]):int(offo[k + 1])]), k
 
 
 def test_c1_full_size_one_stream(gpu, orc):
