@@ -82,7 +82,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
  * share learned from the previous calls' measured rates of both sides (first call: the
  * planner rates' model, at most 10 %); pageable bytes stay on the host (a staging copy per
  * byte costs more than the GPU saves).  KRK_CRC_GPU_FRACTION forces the share.  This
- * returns the calling thread's last split in bytes and the share the next pinned batch
+ * returns the calling thread's last split in bytes and the share the next pinned batch of its device
  * will use (-1 until learned). */
 int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction);
 

@@ -458,7 +458,15 @@ struct PieceTask {
 
 // GPU share of pinned CRC batches learned from earlier calls (-1: none yet), and the
 // calling thread's last split (krk_crc_host_split).
-static std::atomic<double> g_crc_split{-1.0};
+// Per device (one process-wide share fitted every device and batch alike).
+static std::atomic<double> g_crc_split[kMaxDevs];
+static std::once_flag g_crc_split_once;
+static std::atomic<double>& crc_split_of(int dev) {
+    std::call_once(g_crc_split_once, [] {
+        for (auto& x : g_crc_split) x.store(-1.0);
+    });
+    return g_crc_split[(dev >= 0 && dev < kMaxDevs) ? dev : 0];
+}
 static thread_local uint64_t t_split_gpu = 0, t_split_host = 0;
 
 static bool host_pinned(const void* p, uint64_t n) {
@@ -509,7 +517,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     const double c = R.host_crc, H = T * c;
     double gpu_frac = 0.0;
     if (all_pinned) {
-        const double learned = g_crc_split.load(std::memory_order_relaxed);
+        const double learned = crc_split_of(D->id).load(std::memory_order_relaxed);
         gpu_frac = learned >= 0 ? learned : std::min(0.10, R.h2d / (R.h2d + H));
     }
     if (forced) gpu_frac = std::clamp(atof(forced), 0.0, 1.0);
@@ -568,8 +576,9 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     if (!r && all_pinned && !forced && gbytes >= (64u << 20) && hbytes >= (64u << 20) && gpu_s > 0 && host_s > 0) {
         // the split where both sides would have ended together at the rates just measured
         const double rg = gbytes / gpu_s, rh = hbytes / host_s, want = rg / (rg + rh);
-        const double cur = g_crc_split.load(std::memory_order_relaxed);
-        g_crc_split.store(cur >= 0 ? 0.5 * cur + 0.5 * want : want, std::memory_order_relaxed);
+        std::atomic<double>& split = crc_split_of(D->id);
+        const double cur = split.load(std::memory_order_relaxed);
+        split.store(cur >= 0 ? 0.5 * cur + 0.5 * want : want, std::memory_order_relaxed);
     }
     return r;
 }
@@ -577,7 +586,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
 int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction) {
     if (gpu_bytes) *gpu_bytes = t_split_gpu;
     if (host_bytes) *host_bytes = t_split_host;
-    if (gpu_fraction) *gpu_fraction = g_crc_split.load(std::memory_order_relaxed);
+    if (gpu_fraction) *gpu_fraction = crc_split_of(t_dev).load(std::memory_order_relaxed);
     return KRK_OK;
 }
 

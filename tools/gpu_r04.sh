@@ -23,6 +23,22 @@ for step in "$@"; do
     all) run pytest_all 900 $PYT tests -m gpu ;;
     crossover) run crc_crossover 200 tests/native/crc_crossover ;;
     bench) run bench_c2 300 python bench.py ;;
+    bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
+    bench_files) run bench_files 600 python bench.py --workload files --steps 2 --warmup 1 ;;
+    bench_engine) run bench_engine 300 python bench.py --workload engine ;;
+    # rocprofv3 on the end-to-end legs (kernel trace + copy trace; PMC passes on their own runs)
+    prof_e2e) run prof_e2e 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+                  -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
+    prof_files) run prof_files 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+                  -d gpurun_out/prof_files -- python3 bench.py --workload files --steps 1 --warmup 1 --no-cpu-baseline ;;
+    pmc_e2e)
+        B="python3 bench.py --e2e-only --no-cpu-baseline"
+        run pmc_e2e_valu 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+            SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv -d gpurun_out/pmc_e2e_valu -- $B
+        run pmc_e2e_wait 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmc_e2e_wait -- $B
+        run pmc_e2e_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_e2e_fetch -- $B
+        run pmc_e2e_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_e2e_write -- $B ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
