@@ -430,7 +430,7 @@ static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blob
         r = run_items(D, items, d_sums, ks);
         if (r) break;
         pl.release(k, 0, ks);
-        k ^= 1;
+        k = pl.next(k);
     }
     if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
     if (!r && hipMemcpy(sums_host + lo, d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
@@ -689,7 +689,7 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
         r = run_items(D, items, d_sums, ks);
         if (r) break;
         pl->release(k, 0, ks);
-        k ^= 1;
+        k = pl->next(k);
     }
     for (int fd : fds)
         if (fd >= 0) close(fd);
@@ -785,7 +785,7 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
         r = run_jobs(D, jobs, d_dig, d_state, ks);
         if (r) break;
         pl.release(k, 0, ks);
-        k ^= 1;
+        k = pl.next(k);
     }
     if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
     if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {

@@ -53,8 +53,22 @@ struct CopyTask {
     size_t n;
 };
 
+// KRK_STAGING_WINDOWS (2..4, default 2): windows in the ring; with more, a window's host copy
+// or file reads may run further ahead of the upload and kernels of the earlier ones.
+constexpr int kMaxWindows = 4;
+inline int staging_windows() {
+    static const int n = [] {
+        const char* v = getenv("KRK_STAGING_WINDOWS");
+        const int x = v ? atoi(v) : 2;
+        return std::min(kMaxWindows, std::max(2, x));
+    }();
+    return n;
+}
+
 struct Pipeline {
-    Window w[2];
+    Window w[kMaxWindows];
+    int n = 2;  // windows in use
+    int next(int k) const { return (k + 1) % n; }
     ~Pipeline() {
         for (auto& x : w) {
             if (x.inflight) hipEventSynchronize(x.consumed);
@@ -70,7 +84,9 @@ struct Pipeline {
         }
     }
     int init(size_t cap) {
-        for (auto& x : w) {
+        n = staging_windows();
+        for (int i = 0; i < n; ++i) {
+            Window& x = w[i];
             x.cap = cap;
             KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(&x.host), cap, hipHostMallocDefault));
             KRK_HIP(hipMalloc(reinterpret_cast<void**>(&x.dev), cap));

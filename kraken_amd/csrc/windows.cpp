@@ -253,7 +253,7 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         pl.release(k, 0, ks);
         pl.release(k, 1, kc);
         t_enq += wall_s() - td;
-        k ^= 1;
+        k = pl.next(k);
     }
     *max_live = sched.max_live();
     if (trace_on())
