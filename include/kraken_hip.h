@@ -113,10 +113,12 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n_files, uint32_t*
  *                   messages and folded into the piece sums on the host with the GF(2)
  *                   combine, so state crosses slot and piece boundaries;
  *   KRK_PLACE_AUTO  (krk_piece_stream_begin) the process setting (krk_set_crc_placement,
- *                   KRK_CRC_PLACEMENT), by default the crossover: HOST while every live host
- *                   CRC stream has a CPU of its own (the CPUs this process may use), beyond
- *                   that GPU when a memcpy costs the caller less per byte than the CRC
- *                   (measured rates); HOST when no gfx950 device is present.
+ *                   KRK_CRC_PLACEMENT), by default the crossover: HOST unless the host's CRC
+ *                   capacity (the CPUs this process may use x one thread's measured PCLMUL
+ *                   rate) is below what the host link could carry to the GPU (0.85 x the
+ *                   measured pinned H2D rate) -- on MI355X hosts the host side carries
+ *                   60-80 GB/s for one stream and > 100 GB/s for several against ~20 GB/s
+ *                   through the engine; HOST when no gfx950 device is present.
  * HOST placement needs no device; GPU placement without one is KRK_ENODEV. */
 typedef struct krk_piece_stream krk_piece_stream;
 int krk_piece_stream_begin(int64_t piece_length, krk_piece_stream** out);
@@ -130,9 +132,10 @@ void krk_piece_stream_free(krk_piece_stream* s);
 /* crc32.Update(crc, IEEETable, p) for one buffer (hash.Hash32 Write path used by
  * agentstorage.Torrent.writePiece, lib/torrent/storage/agentstorage/torrent.go:175-199).
  * data is a HOST pointer.  AUTO (krk_crc32_update): calls of at most 64 KiB
- * (KRK_CRC_HOST_MAX) and calls below the crossover of krk_piece_stream_begin run on the
- * caller's thread; the rest go through the device's CRC queue, coalesced with the other
- * pending requests of the device into one launch.  krk_crc32_update_on forces a placement. */
+ * (KRK_CRC_HOST_MAX) and every call while the crossover of krk_piece_stream_begin says HOST
+ * run on the caller's thread (large ones shared with idle host-pool threads); the rest go
+ * through the device's CRC queue, coalesced with the other pending requests of the device
+ * into one launch.  krk_crc32_update_on forces a placement. */
 int krk_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
 int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
 /* What KRK_PLACE_AUTO means for new piece streams and crc32_update calls, process-wide:

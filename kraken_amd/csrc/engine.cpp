@@ -1263,16 +1263,16 @@ namespace {
 
 // ------------------------------------------------------- CRC placement
 // A piece stream (NewMetaInfo over an io.Reader) and a crc32.Update call (PieceHash) carry
-// no state the GPU could keep: every byte crosses the host link once and the caller's
-// thread copies it into a pinned slot first.  One host core's PCLMUL CRC runs ~17 GB/s
-// (host_crc_rate()) and the GPU path of one stream is bounded by that caller-thread copy
-// and the slot round trips (profiles/r04/crc_crossover.json), so AUTO keeps a stream on its
-// caller's thread while every live host CRC stream has a core of its own; beyond the cores
-// the excess goes to the GPU engine only when its per-byte cost to the calling thread (a
-// memcpy, host_copy_rate()) is below the CRC's own -- the host's aggregate is then the CPU
-// budget, and bytes the GPU takes free CPU for the rest.
+// no state the GPU could keep: every byte crosses the host link once, copied into a pinned
+// slot by the caller's thread first.  Measured on MI355X (tests/native/crc_crossover.cpp,
+// profiles/r04/crc_crossover.jsonl): the engine's CRC side carries 10 GB/s for one stream
+// and ~20 GB/s for 4 to 64 (slot copies and per-slot H2D), where the host placement --
+// PCLMUL on the caller's thread, large writes shared with idle host-pool threads -- carries
+// 60-80 GB/s for one stream and well over 100 GB/s for several.  So AUTO keeps CRC work on
+// the host unless the host's whole CRC capacity (the CPUs this process may use x one thread's
+// PCLMUL rate) is below what the host link could carry to the GPU at best (0.85 x the
+// measured pinned H2D rate): a box with few or slow cores.
 std::atomic<int> g_crc_placement{KRK_PLACE_AUTO};  // krk_set_crc_placement / KRK_CRC_PLACEMENT
-std::atomic<int64_t> g_host_crc_load{0};           // live host piece streams + host crc32_update calls running
 
 int crc_placement_setting() {
     static std::once_flag once;
@@ -1287,9 +1287,11 @@ int crc_placement_setting() {
 
 // AUTO: true = this stream / call goes to the GPU engine (a device being present).
 bool crc_auto_gpu() {
-    const int64_t load = g_host_crc_load.load(std::memory_order_relaxed);
-    if (load < (int64_t)host_threads()) return false;
-    return host_copy_rate() > host_crc_rate();
+    int drc = KRK_OK;
+    Device* D = device(&drc);
+    if (!D) return false;
+    const Rates R = planner_rates(D);
+    return (double)host_threads() * R.host_crc < host_link(R);
 }
 
 // The placement a new piece stream / crc32_update call runs on: HOST or GPU.  `placement`
@@ -1457,7 +1459,6 @@ int krk_piece_stream_begin_on(int placement, int64_t piece_length, krk_piece_str
     auto* s = new krk_piece_stream();
     s->E = E;
     s->P = (uint64_t)piece_length;
-    if (!E) g_host_crc_load.fetch_add(1);
     *out = s;
     return KRK_OK;
 }
@@ -1541,8 +1542,6 @@ void krk_piece_stream_free(krk_piece_stream* s) {
     if (s->E) {
         stream_drain(s, 0);
         pend_release(s->E, std::move(s->pend));
-    } else {
-        g_host_crc_load.fetch_sub(1);
     }
     delete s;
 }
@@ -1561,9 +1560,7 @@ int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64
                                                                       : resolve_crc_placement(placement, &rc);
     if (rc) return rc;
     if (where == KRK_PLACE_HOST) {
-        g_host_crc_load.fetch_add(1);
         *out = host_crc32_update_par(crc, data, n);
-        g_host_crc_load.fetch_sub(1);
         return KRK_OK;
     }
     Engine* E = engine_of(place_device(), &rc);

@@ -4,17 +4,21 @@
 // cgo layer's goroutines drive them, on each placement:
 //
 //   * one stream over 1 GiB in 4 MiB writes (HOST / GPU / AUTO);
-//   * N concurrent streams (N = 4, 16, 64), 256 MiB each in 4 MiB writes;
+//   * N concurrent streams (N = 4, 16, 64), 128 MiB each in 4 MiB writes;
 //   * one thread's crc32_update calls of 64 KiB .. 256 MiB;
 //   * 64 threads' crc32_update calls of 4 MiB (an agent verifying received pieces).
 //
-// Every result is compared with krk_host_crc32_update over the same bytes (itself checked
-// against zlib by tests/test_capi_cpu.py).  One JSON line per case; exit 1 on a mismatch.
+// Every stream / thread reads bytes of its own (no two share cache lines), and every case
+// repeats its work until it has run for at least ~0.4 s, so neither the host's caches nor a
+// CPU quota's first-period burst inflates a rate.  Every result is compared with
+// krk_host_crc32_update over the same bytes (itself checked against zlib by
+// tests/test_capi_cpu.py).  One JSON line per case; exit 1 on a mismatch.
 //
 //   crc_crossover [scale]   (scale < 1 shrinks every size, for a quick run)
 #include <pthread.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -34,6 +38,7 @@ double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::n
 const char* pname(int p) { return p == KRK_PLACE_HOST ? "host" : p == KRK_PLACE_GPU ? "gpu" : "auto"; }
 
 std::vector<uint8_t> g_buf;
+uint64_t g_region = 0;  // bytes of g_buf each thread of the update cases owns
 bool g_ok = true;
 
 // One piece stream over [p, p + L) in `w`-byte writes; returns its sums (placement to *where).
@@ -71,12 +76,15 @@ std::vector<uint32_t> host_sums(const uint8_t* p, uint64_t L, uint64_t P) {
     return s;
 }
 
+constexpr double kMinSeconds = 0.4;
+
 void run_streams(int placement, int n, uint64_t L, uint64_t P, uint64_t w, int reps) {
     std::vector<std::vector<uint32_t>> want(n);
-    for (int i = 0; i < n; ++i) want[i] = host_sums(g_buf.data() + (size_t)i * 4096, L, P);
+    for (int i = 0; i < n; ++i) want[i] = host_sums(g_buf.data() + (size_t)i * L, L, P);
     double best = 1e30;
     int where_host = 0, where_gpu = 0;
     bool ok = true;
+    int loops = 1;
     for (int r = 0; r < reps; ++r) {
         pthread_barrier_t start;
         pthread_barrier_init(&start, nullptr, (unsigned)n + 1);
@@ -87,12 +95,20 @@ void run_streams(int placement, int n, uint64_t L, uint64_t P, uint64_t w, int r
             th.emplace_back([&, i] {
                 krk_set_device(0);
                 pthread_barrier_wait(&start);
-                good[i] = stream(placement, g_buf.data() + (size_t)i * 4096, L, P, w, &where[i]) == want[i];
+                bool g = true;
+                for (int l = 0; l < loops; ++l)
+                    g = stream(placement, g_buf.data() + (size_t)i * L, L, P, w, &where[i]) == want[i] && g;
+                good[i] = g;
             });
         const auto t0 = Clock::now();
         pthread_barrier_wait(&start);
         for (auto& t : th) t.join();
-        best = std::min(best, secs(t0));
+        const double el = secs(t0);
+        best = std::min(best, el / loops);
+        if (r == 0 && el < kMinSeconds) {  // the timed reps run long enough
+            loops = (int)std::min(1000.0, std::ceil(kMinSeconds / std::max(el, 1e-4)));
+            best = 1e30;
+        }
         pthread_barrier_destroy(&start);
         where_host = (int)std::count(where.begin(), where.end(), KRK_PLACE_HOST);
         where_gpu = (int)std::count(where.begin(), where.end(), KRK_PLACE_GPU);
@@ -100,17 +116,22 @@ void run_streams(int placement, int n, uint64_t L, uint64_t P, uint64_t w, int r
     }
     g_ok = g_ok && ok;
     printf("{\"case\": \"piece_streams\", \"placement\": \"%s\", \"streams\": %d, \"bytes_each\": %llu, \"write\": %llu, "
-           "\"piece_length\": %llu, \"seconds\": %.4f, \"GBps\": %.3f, \"placed_host\": %d, \"placed_gpu\": %d, "
-           "\"sums_match\": %s}\n",
-           pname(placement), n, (unsigned long long)L, (unsigned long long)w, (unsigned long long)P, best,
+           "\"piece_length\": %llu, \"seconds\": %.4f, \"loops\": %d, \"GBps\": %.3f, \"placed_host\": %d, "
+           "\"placed_gpu\": %d, \"sums_match\": %s}\n",
+           pname(placement), n, (unsigned long long)L, (unsigned long long)w, (unsigned long long)P, best, loops,
            (double)n * L / best / 1e9, where_host, where_gpu, ok ? "true" : "false");
     fflush(stdout);
 }
 
+// Thread t's calls walk `span` bytes of its own region (call c at offset (c * size) % span).
 void run_updates(int placement, int threads, uint64_t size, uint64_t total_each, int reps) {
-    const uint64_t calls = std::max<uint64_t>(1, total_each / size);
-    std::vector<uint32_t> want(threads);
-    for (int t = 0; t < threads; ++t) krk_host_crc32_update((uint32_t)t, g_buf.data() + (size_t)t * 4096, size, &want[t]);
+    const uint64_t span = std::max<uint64_t>(size, std::min<uint64_t>(g_region, 64ull << 20) / size * size);
+    const uint64_t per = std::max<uint64_t>(1, span / size);
+    uint64_t calls = std::max<uint64_t>(1, total_each / size);
+    std::vector<std::vector<uint32_t>> want(threads, std::vector<uint32_t>(per));
+    for (int t = 0; t < threads; ++t)
+        for (uint64_t c = 0; c < per; ++c)
+            krk_host_crc32_update((uint32_t)t, g_buf.data() + (size_t)t * g_region + c * size, size, &want[t][c]);
     double best = 1e30;
     bool ok = true;
     for (int r = 0; r < reps; ++r) {
@@ -124,16 +145,23 @@ void run_updates(int placement, int threads, uint64_t size, uint64_t total_each,
                 pthread_barrier_wait(&start);
                 for (uint64_t c = 0; c < calls; ++c) {
                     uint32_t out = 0;
-                    if (krk_crc32_update_on(placement, (uint32_t)t, g_buf.data() + (size_t)t * 4096, size, &out) !=
-                            KRK_OK ||
-                        out != want[t])
+                    const uint64_t k = c % per;
+                    if (krk_crc32_update_on(placement, (uint32_t)t, g_buf.data() + (size_t)t * g_region + k * size, size,
+                                            &out) != KRK_OK ||
+                        out != want[t][k])
                         bad.fetch_add(1);
                 }
             });
         const auto t0 = Clock::now();
         pthread_barrier_wait(&start);
         for (auto& t : th) t.join();
-        best = std::min(best, secs(t0));
+        const double el = secs(t0);
+        best = std::min(best, el);
+        if (r == 0 && el < kMinSeconds) {  // the timed reps run long enough
+            calls = (uint64_t)std::ceil(calls * std::min(1000.0, kMinSeconds / std::max(el, 1e-4)));
+            best = 1e30;
+            ++reps;
+        }
         pthread_barrier_destroy(&start);
         ok = ok && bad.load() == 0;
     }
@@ -154,12 +182,23 @@ int main(int argc, char** argv) {
         fprintf(stderr, "no device: %s\n", krk_last_error());
         return 1;
     }
-    const uint64_t L1 = sz(1ull << 30), LN = sz(256ull << 20), P = 4 << 20, W = 4 << 20;
-    g_buf.resize(std::max<uint64_t>(L1, LN) + 64 * 4096 + (256ull << 20));
-    std::mt19937_64 g(4242);
-    for (size_t k = 0; k + 8 <= g_buf.size(); k += 8) {
-        const uint64_t v = g();
-        memcpy(&g_buf[k], &v, 8);
+    const uint64_t L1 = sz(1ull << 30), LN = sz(128ull << 20), P = 4 << 20, W = 4 << 20;
+    g_region = std::max<uint64_t>(sz(64ull << 20), 4u << 20);
+    g_buf.resize(std::max({L1, 64 * LN, 64 * g_region, sz(256ull << 20)}));
+    {  // splitmix64 bytes, filled on 16 threads
+        std::vector<std::thread> th;
+        const size_t words = g_buf.size() / 8, per = (words + 15) / 16;
+        for (int t = 0; t < 16; ++t)
+            th.emplace_back([&, t] {
+                for (size_t k = t * per; k < std::min(words, (t + 1) * per); ++k) {
+                    uint64_t z = (k + 1) * 0x9E3779B97F4A7C15ull;
+                    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+                    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+                    z ^= z >> 31;
+                    memcpy(&g_buf[8 * k], &z, 8);
+                }
+            });
+        for (auto& t : th) t.join();
     }
     for (int p : {KRK_PLACE_HOST, KRK_PLACE_GPU, KRK_PLACE_AUTO}) run_streams(p, 1, L1, P, W, 3);
     for (int n : {4, 16, 64})

@@ -21,7 +21,8 @@ for step in "$@"; do
     new) run pytest_new 420 $PYT tests/test_gpu_errors.py tests/test_gpu_defaults.py tests/test_gpu_files.py ;;
     rest) run pytest_rest 600 $PYT tests -m gpu --deselect tests/test_gpu_files.py --deselect tests/test_gpu_defaults.py --deselect tests/test_gpu_errors.py ;;
     all) run pytest_all 900 $PYT tests -m gpu ;;
-    crossover) run crc_crossover 200 tests/native/crc_crossover ;;
+    crossover) run crc_crossover 300 tests/native/crc_crossover ;;
+    defaults) run pytest_defaults 300 $PYT tests/test_gpu_defaults.py tests/test_gpu_bindings.py ;;
     bench) run bench_c2 300 python bench.py ;;
     bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
     bench_files) run bench_files 600 python bench.py --workload files --steps 2 --warmup 1 ;;
