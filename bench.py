@@ -80,7 +80,7 @@ def load_valu(workload):
     (tools/pmc_valu.py -> profiles/r03/valu_<workload>.json); the raw counters stay in
     that file, the derived fractions go into the bench line."""
     d, path = None, None
-    for rnd in ("r03", "r02"):  # the newest round's passes
+    for rnd in ("r04", "r03", "r02"):  # the newest round's passes
         path = os.path.join(ROOT, "profiles", rnd, f"valu_{workload}.json")
         try:
             d = json.load(open(path))
@@ -367,16 +367,20 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
 
 
 def load_traffic(path, workload, n):
-    """Per-launch HBM bytes from the PMC passes: profiles/pmc_traffic.json (C2) or
-    profiles/pmc_traffic_<workload>.json (tools/pmc_traffic.py)."""
-    if workload != "c2" and os.path.basename(path) == "pmc_traffic.json":
-        path = os.path.join(os.path.dirname(path), f"pmc_traffic_{workload}.json")
-    try:
-        pm = json.load(open(path))
+    """Per-launch HBM bytes from the PMC passes (tools/pmc_traffic.py): `path` if given, else
+    the newest of profiles/r04/pmc_traffic_<workload>.json, profiles/pmc_traffic_<workload>.json
+    and (C2) profiles/pmc_traffic.json -- the first whose workload and blob count match."""
+    cands = [path] if path else []
+    cands += [os.path.join(ROOT, "profiles", "r04", f"pmc_traffic_{workload}.json"),
+              os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json"),
+              os.path.join(ROOT, "profiles", "pmc_traffic.json")]
+    for c in cands:
+        try:
+            pm = json.load(open(c))
+        except (ValueError, OSError):
+            continue
         if pm.get("workload") == workload and pm.get("blobs") == n:
             return pm.get("bytes_per_launch", {})
-    except (ValueError, OSError):
-        pass
     return {}
 
 
@@ -691,13 +695,32 @@ def host_mem_budget():
 E2E_PASSES = 3
 
 
-def link_roofline(D, gbps):
+def link_roofline(D, gbps, traffic_workload=None, n=None):
     """An end-to-end pass is bounded by the host link: every byte crosses PCIe once.  Peak =
-    the pinned H2D rate the planner measured on this device (krk_planner_rates_get)."""
+    the pinned H2D rate the planner measured on this device (krk_planner_rates_get).  With
+    `traffic_workload`, the kernels' HBM bytes per window launch from the committed PMC
+    passes of that leg (tools/pmc_traffic.py) ride along: the windows' kernels read each
+    staged byte once (traffic over the 512 MiB window ~1.00)."""
     h2d = D.planner_rates()["h2d_bps"] / 1e9
-    return {"bound": "host link (PCIe H2D)", "achieved": round(gbps, 3), "peak": round(h2d, 3), "unit": "GB/s",
-            "frac": round(gbps / h2d, 4) if h2d else None,
-            "peak_source": "pinned 64 MiB H2D measured on this device (krk_planner_rates_get: h2d_bps)"}
+    r = {"bound": "host link (PCIe H2D)", "achieved": round(gbps, 3), "peak": round(h2d, 3), "unit": "GB/s",
+         "frac": round(gbps / h2d, 4) if h2d else None,
+         "peak_source": "pinned 64 MiB H2D measured on this device (krk_planner_rates_get: h2d_bps)", "traffic": None}
+    if traffic_workload:
+        t = load_traffic(None, traffic_workload, n)
+        if t:
+            win = window_bytes_default()
+            r["traffic"] = {"per_window_launch": {k: t[k] for k in ("crc32_pieces", "sha256_multi") if k in t},
+                            "window_bytes": win,
+                            "over_algorithmic": {k: round(t[k] / win, 4) for k in ("crc32_pieces", "sha256_multi")
+                                                 if k in t},
+                            "source": f"profiles/r04/pmc_traffic_{traffic_workload}.json (FETCH_SIZE/WRITE_SIZE "
+                                      "passes, gfx950 correction)"}
+    return r
+
+
+def window_bytes_default():
+    """Bytes of one staging window (KRK_WINDOW_MB, default 512 MiB: staging.hpp window_bytes)."""
+    return int(os.environ.get("KRK_WINDOW_MB", "512")) << 20
 
 
 def end_to_end(D, T, arena, n, Le, P, out, world):
@@ -740,7 +763,7 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
            "source": "pageable host memory (numpy), copied into pinned windows; median of the passes",
            "bound": "PCIe H2D (one pass per byte) and the per-blob SHA-256 chain (blob_bytes / per-stream rate)",
            "sums_match_device_run": ok,
-           "roofline": link_roofline(D, world * n * Le / el / 1e9)}
+           "roofline": link_roofline(D, world * n * Le / el / 1e9, "c2_end_to_end", n)}
     if out is not None and Le == int(arena.lengths[0]) and (arena.lengths == Le).all():  # whole blobs
         dev_dg = out.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
         res["digests_match_device_run"] = bool(np.array_equal(dg, dev_dg))
@@ -1180,6 +1203,7 @@ def run_files(a, D, T, rank, world, res):
         sums_p, dg_p = D.metainfo_digest_host(datas, P)
         T.barrier()
         el_p = T.max_over_ranks(time.perf_counter() - t0)
+        st_p = D.windows_last_call()
         D.set_sha_host_offload(-1)
         try:
             T.barrier()
@@ -1211,12 +1235,14 @@ def run_files(a, D, T, rank, world, res):
                 "config": {"workload": WORKLOADS[a.workload]["desc"], "blobs_per_gpu": n, "bytes_per_gpu": total,
                            "piece_length": P, "mode": "files -> pinned windows -> GPU (offload off)",
                            "parallelism": f"blob-sharded x{world}, no collective"},
-                "roofline": link_roofline(D, value),
+                "roofline": link_roofline(D, value, "files", n),
                 "windows": st, "kernels": {"sha256_multi": {"launches": sha_n, "avg_ms": round(sha_ms / max(sha_n, 1), 3)},
                                            "crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_ms / max(crc_n, 1), 3)}},
                 "pinned_host_memory": {"value": round(world * total / el_p / 1e9, 3), "unit": "GB/s",
                                        "roofline": link_roofline(D, world * total / el_p / 1e9),
-                                       "what": "the same blobs from pinned host memory (krk_metainfo_digest_host)"},
+                                       "windows": st_p,
+                                       "what": "the same blobs from pinned host memory (krk_metainfo_digest_host; "
+                                               "direct_windows: windows DMA'd from the caller's pages)"},
                 "default_offload": {"value": round(world * total / el_a / 1e9, 3), "unit": "GB/s",
                                     "host_blobs": st_a["host_blobs"],
                                     "what": "krk_metainfo_digest_files with the library's default host offload (AUTO)"},
@@ -1332,7 +1358,7 @@ def main():
                     help="c5regen: piece sums then InfoHashes (no krk_metainfo_batch_dev pipelining)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-json", default=None, help="PMC traffic JSON (default: the newest committed for the workload)")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the live SHA issue-ceiling run (profiler passes: keeps its launches out of the trace)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers, PCIe) leg")

@@ -469,20 +469,6 @@ static std::atomic<double>& crc_split_of(int dev) {
 }
 static thread_local uint64_t t_split_gpu = 0, t_split_host = 0;
 
-static bool host_pinned(const void* p, uint64_t n) {
-    // pageable memory is an expected "invalid value" here: not left pending on the thread
-    // (the next launch would report it as an unchecked earlier error)
-    auto pinned_at = [](const void* q) {
-        hipPointerAttribute_t a{};
-        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        return a.type == hipMemoryTypeHost;
-    };
-    return pinned_at(p) && (n <= 1 || pinned_at(static_cast<const uint8_t*>(p) + n - 1));
-}
-
 int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
     KRK_DEVICE(D);
     int r = validate_blobs(blobs, n_blobs);

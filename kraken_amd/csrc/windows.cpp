@@ -94,11 +94,15 @@ struct Filler {
         uint8_t* dst;
     };
     virtual int fill(const std::vector<Task>& tasks) = 0;
+    // The source is page-locked: its chunks can be DMA'd straight into the device window.
+    virtual const uint8_t* pinned_src(uint32_t /*blob*/, uint64_t /*off*/) const { return nullptr; }
 };
 
 struct MemFiller : Filler {
     const krk_blob* blobs;
+    bool pinned = false;  // every windowed blob page-locked (krk_host_alloc): no staging copy
     explicit MemFiller(const krk_blob* b) : blobs(b) {}
+    const uint8_t* pinned_src(uint32_t b, uint64_t off) const override { return pinned ? blobs[b].data + off : nullptr; }
     int fill(const std::vector<Task>& tasks) override {
         std::vector<CopyTask> c;
         c.reserve(tasks.size());
@@ -176,18 +180,31 @@ uint64_t fd_budget() {
     return rl.rlim_cur > reserve + 16 ? rl.rlim_cur - reserve : 16;
 }
 
+struct CallStats {
+    uint64_t max_live = 0;
+    int windows = 0;
+    int direct_windows = 0;  // windows DMA'd straight from the caller's page-locked memory
+    uint64_t host_blobs = 0;
+};
+thread_local CallStats t_last_call;
+
+// A window of page-locked chunks goes to the device as one hipMemcpyBatchAsync, or -- where
+// the HIP runtime in the process predates it -- as one hipMemcpyAsync a chunk when it has few
+// enough chunks that the calls' cost (a few us each) stays well under the window's transfer.
+constexpr size_t kDirectMaxCalls = 64;
+
 // The windows of one host-resident batch: the blobs not in `skip`, chunk by chunk, into the
 // device's staging windows and through both kernels.  d_sums / d_dig / d_state indexed like
 // the caller's blobs (sums by sums_off).  Asynchronous on the device's streams; returns once
 // the last window is queued (the caller synchronises s_main / s_a / s_b).
 int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* plens, const uint64_t* soff,
                  const std::vector<char>& skip, Filler& filler, uint64_t align, uint64_t cap, uint32_t* d_sums,
-                 uint8_t* d_dig, uint32_t* d_state, uint64_t* max_live, int* n_windows) {
+                 uint8_t* d_dig, uint32_t* d_state, CallStats* st) {
     std::vector<uint32_t> blobs;
     for (uint64_t i = 0; i < n; ++i)
         if (!skip[i]) blobs.push_back((uint32_t)i);
-    *max_live = 0;
-    *n_windows = 0;
+    st->max_live = 0;
+    st->windows = st->direct_windows = 0;
     if (blobs.empty()) return KRK_OK;
     const size_t W = window_bytes();
     const uint64_t live_cap = std::min<uint64_t>(cap, blobs.size());
@@ -235,12 +252,25 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         }
         const double tc = wall_s();
         t_build += tc - tb;
-        r = filler.fill(tasks);
-        if (r) break;
+        // page-locked sources are DMA'd straight from the caller's memory into the device
+        // window; the others go through the pinned host window
+        const bool direct = !tasks.empty() && filler.pinned_src(tasks[0].b, tasks[0].off) != nullptr &&
+                            (memcpy_batch() != nullptr || tasks.size() <= kDirectMaxCalls);
+        std::vector<CopyTask> dma;
+        if (direct) {
+            dma.reserve(tasks.size());
+            for (const Filler::Task& t : tasks)
+                dma.push_back({w.dev + (t.dst - w.host), filler.pinned_src(t.b, t.off), (size_t)t.len});
+        } else {
+            r = filler.fill(tasks);
+            if (r) break;
+        }
         const double td = wall_s();
         t_fill += td - tc;
-        ++*n_windows;
-        if (pl.h2d(k, std::min(fill, pl.w[k].cap), cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
+        ++st->windows;
+        st->direct_windows += direct;
+        const hipError_t up = direct ? pl.h2d_direct(k, dma, cp) : pl.h2d(k, std::min(fill, pl.w[k].cap), cp);
+        if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
             hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "metainfo windows: staging copy failed");
             r = KRK_EHIP;
@@ -255,12 +285,12 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         t_enq += wall_s() - td;
         k = pl.next(k);
     }
-    *max_live = sched.max_live();
+    st->max_live = sched.max_live();
     if (trace_on())
         fprintf(stderr,
                 "krk_trace windows: windows=%d W=%zu max_live=%llu loop=%.3fs acquire=%.3fs build=%.3fs fill=%.3fs "
                 "enqueue=%.3fs\n",
-                *n_windows, W, (unsigned long long)*max_live, wall_s() - t0, t_acq, t_build, t_fill, t_enq);
+                st->windows, W, (unsigned long long)st->max_live, wall_s() - t0, t_acq, t_build, t_fill, t_enq);
     return r;
 }
 
@@ -271,12 +301,6 @@ uint64_t live_cap_for(Device* D) {
     return v ? v : window_stream_cap(D);
 }
 
-struct CallStats {
-    uint64_t max_live = 0;
-    int windows = 0;
-    uint64_t host_blobs = 0;
-};
-thread_local CallStats t_last_call;
 
 }  // namespace
 
@@ -410,9 +434,14 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     } share_guard{t_host_share};
     if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
     MemFiller filler(blobs);
+    // KRK_PINNED_DIRECT=0 stages pinned sources too (A/B)
+    static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
+    filler.pinned = allow_direct;
+    for (uint64_t i = 0; i < n && filler.pinned; ++i)
+        if (!on_host[i] && lens[i] && !host_pinned(blobs[i].data, lens[i])) filler.pinned = false;
     CallStats st;
     r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, 64, live_cap_for(D), o.d_sums,
-                     o.d_dig, o.d_state, &st.max_live, &st.windows);
+                     o.d_dig, o.d_state, &st);
     if (!r && (hipStreamSynchronize(D->s_a) != hipSuccess || hipStreamSynchronize(D->s_b) != hipSuccess ||
                hipStreamSynchronize(D->s_main) != hipSuccess)) {
         set_error(KRK_EHIP, "metainfo_digest_host: sync failed");
@@ -510,7 +539,7 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     // at most as many live blobs as this call may hold files open
     const uint64_t cap = std::min(live_cap_for(D), fd_budget());
     r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, cap,
-                     o.d_sums, o.d_dig, o.d_state, &st.max_live, &st.windows);
+                     o.d_sums, o.d_dig, o.d_state, &st);
     // drain what was queued even after a read error (the windows' kernels read the buffers)
     const bool synced = hipStreamSynchronize(D->s_a) == hipSuccess && hipStreamSynchronize(D->s_b) == hipSuccess &&
                         hipStreamSynchronize(D->s_main) == hipSuccess;
@@ -545,6 +574,12 @@ int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs
     if (max_live) *max_live = t_last_call.max_live;
     if (windows) *windows = t_last_call.windows;
     if (host_blobs) *host_blobs = t_last_call.host_blobs;
+    return KRK_OK;
+}
+
+int krk_windows_last_direct(int* direct_windows) {
+    KRK_CHECK(direct_windows, KRK_EINVAL, "direct_windows is NULL");
+    *direct_windows = t_last_call.direct_windows;
     return KRK_OK;
 }
 

@@ -391,9 +391,10 @@ def metainfo_digest_files(paths, lengths, piece_lengths, multi: bool = False):
 def windows_last_call() -> dict:
     """The calling thread's last krk_metainfo_digest_host / _files call: the most live blobs
     in a window, the windows, the blobs the host offload took (krk_windows_last_call)."""
-    m, w, h = C.c_uint64(), C.c_int(), C.c_uint64()
+    m, w, h, d = C.c_uint64(), C.c_int(), C.c_uint64(), C.c_int()
     check(lib.krk_windows_last_call(C.byref(m), C.byref(w), C.byref(h)))
-    return {"max_live": m.value, "windows": w.value, "host_blobs": h.value}
+    check(lib.krk_windows_last_direct(C.byref(d)))
+    return {"max_live": m.value, "windows": w.value, "host_blobs": h.value, "direct_windows": d.value}
 
 
 def device_pci_bus_id() -> str:

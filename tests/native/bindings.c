@@ -148,6 +148,45 @@ int main(int argc, char** argv) {
         free(all);
         free(all2);
     }
+    /* Generate over pinned receive buffers: 100 page-locked blobs in one window of 100
+     * chunks go up as one batched DMA (hipMemcpyBatchAsync of this process's HIP runtime) */
+    {
+        enum { NB = 100 };
+        void* pc[NB];
+        krk_blob bl[NB];
+        uint64_t so = 0;
+        for (int i = 0; i < NB; ++i) {
+            const uint64_t len = (1u << 20) + (uint64_t)i * 4097;
+            CHECK(krk_host_alloc(len, &pc[i]) == KRK_OK, "host_alloc");
+            memcpy(pc[i], blob + i * 977, len);
+            bl[i].data = (const uint8_t*)pc[i];
+            bl[i].length = len;
+            bl[i].piece_length = 1 << 20;
+            bl[i].sums_offset = so;
+            so += krk_num_pieces(len, 1 << 20);
+        }
+        uint32_t* sums = calloc(so, 4);
+        uint8_t* dg = malloc(32 * NB);
+        CHECK(krk_set_sha_host_offload(0) == KRK_OK, "offload off"); /* every blob through the windows */
+        CHECK(krk_metainfo_digest_host(bl, NB, sums, dg) == KRK_OK, "metainfo_digest_host (pinned)");
+        CHECK(krk_set_sha_host_offload(KRK_OFFLOAD_AUTO) == KRK_OK, "offload default");
+        int windows = 0, direct = 0;
+        CHECK(krk_windows_last_call(NULL, &windows, NULL) == KRK_OK && krk_windows_last_direct(&direct) == KRK_OK &&
+                  windows >= 1 && direct == windows,
+              "direct windows %d of %d", direct, windows);
+        for (int i = 0; i < NB; ++i) {
+            uint8_t want[32];
+            krk_host_sha256(bl[i].data, bl[i].length, want);
+            CHECK(memcmp(dg + 32 * i, want, 32) == 0, "pinned digest %d", i);
+            CHECK(sums[bl[i].sums_offset] == host_crc(0, bl[i].data, 1 << 20), "pinned piece %d", i);
+            CHECK(sums[bl[i].sums_offset + 1] == host_crc(0, bl[i].data + (1 << 20), bl[i].length - (1 << 20)) ||
+                      bl[i].length == (1u << 20),
+                  "pinned tail piece %d", i);
+        }
+        for (int i = 0; i < NB; ++i) krk_host_free(pc[i]);
+        free(sums);
+        free(dg);
+    }
     /* core/digester_krkgpu.go: AUTO digester, io.Copy-sized writes, Digest() without reset */
     {
         krk_digester* d = NULL;

@@ -427,3 +427,16 @@ def test_planner_moves_with_injected_rates():
     finally:
         D.set_planner_rates(None)
     assert D.planner_rates()["source"] == "nominal"
+
+
+def test_library_loads_after_torch(tmp_path):
+    """bench.py and the gloo tests import torch before the library; a PyTorch wheel brings
+    its own (older) libamdhip64, so the library must not need a newer HIP symbol version at
+    load time (hipMemcpyBatchAsync, HIP 7.1, is looked up at run time instead)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import torch; from kraken_amd import _capi; "
+            "print(_capi.lib.krk_version().decode())" % root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("kraken_amd"), r.stderr[-2000:]

@@ -179,3 +179,33 @@ def test_c3_law_16384_blobs_production_windows(gpu, orc, c3_law, source):
         assert tl[0] == (4, 14336), tl[:3]  # KRK_SHA_PLAN_2LANE_2PAIR at the cap
     assert st["windows"] > 100  # late admission: live shrinks below the cap only at the end
     _check_against_one_shot_and_oracle(lens, srcs, offs, one, sums, dg, orc)
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_pinned_blobs_go_direct(gpu, orc, mixed):
+    """krk_metainfo_digest_host over page-locked blobs (krk_host_alloc): windows of few chunks
+    are DMA'd from the caller's memory straight into the device window (no staging copy:
+    krk_windows_last_direct); one pageable blob in the batch stages every window.  Outputs
+    equal the oracle either way."""
+    lens = [0, 5, (64 << 20) + 1, (100 << 20) + 7, 3 << 20, (300 << 20) + 3]
+    datas, bufs = [], []
+    for i, L in enumerate(lens):
+        x = orc.synth(7000 + i, L)
+        if mixed and i == 2:
+            datas.append(x)
+            continue
+        pa = D.PinnedArray((max(L, 1),), np.uint8)
+        pa.a[:L] = x
+        bufs.append(pa)
+        datas.append(pa.a[:L])
+    try:
+        sums, dg = D.metainfo_digest_host(datas, P4)
+        st = D.windows_last_call()
+        for i, L in enumerate(lens):
+            x = np.asarray(datas[i])
+            assert bytes(dg[i]) == hashlib.sha256(x.tobytes()).digest(), i
+            assert np.array_equal(sums[i], orc.calc_piece_sums(x, P4)[1]), i
+    finally:
+        bufs.clear()
+    assert st["windows"] >= 2 and st["host_blobs"] == 0
+    assert st["direct_windows"] == (0 if mixed else st["windows"]), st
