@@ -312,9 +312,8 @@ int krk_window_stream_cap(uint64_t* cap);
  * one window, the windows, and the blobs the host offload took. */
 int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs);
 /* ... and how many of its windows went to the device straight from the caller's
- * page-locked blobs (krk_host_alloc memory: no pinned staging copy; one
- * hipMemcpyBatchAsync a window, or one copy a chunk for windows of <= 64 chunks where the
- * process's HIP runtime predates that call).  KRK_PINNED_DIRECT=0 stages them instead. */
+ * page-locked blobs (krk_host_alloc memory, windows of <= 64 chunks: no pinned staging
+ * copy, one DMA a chunk).  KRK_PINNED_DIRECT=0 stages them instead. */
 int krk_windows_last_direct(int* direct_windows);
 
 /* ------------------------------------------------------- multi-device

@@ -2,7 +2,6 @@
 // paths (host buffers and files -> pinned host window -> device window -> kernels), and
 // the host-side fills of a window (copies, file reads) spread over the host pool.
 #pragma once
-#include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <unistd.h>
@@ -64,16 +63,6 @@ inline int staging_windows() {
         return std::min(kMaxWindows, std::max(2, x));
     }();
     return n;
-}
-
-// hipMemcpyBatchAsync (HIP 7.1), looked up at run time: the process may run an older HIP
-// runtime (a PyTorch wheel brings its own libamdhip64), and a link-time reference to the
-// versioned symbol would keep the library from loading there.  nullptr: not available.
-using MemcpyBatchFn = hipError_t (*)(void**, void**, size_t*, size_t, hipMemcpyAttributes*, size_t*, size_t,
-                                     size_t*, hipStream_t);
-inline MemcpyBatchFn memcpy_batch() {
-    static const MemcpyBatchFn f = reinterpret_cast<MemcpyBatchFn>(dlsym(RTLD_DEFAULT, "hipMemcpyBatchAsync"));
-    return f;
 }
 
 struct Pipeline {
@@ -143,22 +132,9 @@ struct Pipeline {
                 if (e != hipSuccess) return e;
                 x.done_pending[i] = false;
             }
-        if (tasks.size() > 1 && memcpy_batch()) {  // a window of many chunks is one API call
-            std::vector<void*> d(tasks.size()), s(tasks.size());
-            std::vector<size_t> n(tasks.size());
-            for (size_t i = 0; i < tasks.size(); ++i) {
-                d[i] = tasks[i].dst;
-                s[i] = const_cast<uint8_t*>(tasks[i].src);
-                n[i] = tasks[i].n;
-            }
-            size_t fail = 0;
-            hipError_t e = memcpy_batch()(d.data(), s.data(), n.data(), tasks.size(), nullptr, nullptr, 0, &fail, cp);
+        for (const auto& t : tasks) {
+            hipError_t e = hipMemcpyAsync(t.dst, t.src, t.n, hipMemcpyHostToDevice, cp);
             if (e != hipSuccess) return e;
-        } else {
-            for (const auto& t : tasks) {
-                hipError_t e = hipMemcpyAsync(t.dst, t.src, t.n, hipMemcpyHostToDevice, cp);
-                if (e != hipSuccess) return e;
-            }
         }
         hipError_t e = hipEventRecord(x.copied, cp);
         if (e == hipSuccess) x.copying = true;

@@ -148,10 +148,10 @@ int main(int argc, char** argv) {
         free(all);
         free(all2);
     }
-    /* Generate over pinned receive buffers: 100 page-locked blobs in one window of 100
-     * chunks go up as one batched DMA (hipMemcpyBatchAsync of this process's HIP runtime) */
+    /* Generate over pinned receive buffers: 48 page-locked blobs in windows of <= 64 chunks
+     * go up straight from the caller's pages (one DMA a chunk, no staging copy) */
     {
-        enum { NB = 100 };
+        enum { NB = 48 };
         void* pc[NB];
         krk_blob bl[NB];
         uint64_t so = 0;

@@ -432,7 +432,7 @@ def test_planner_moves_with_injected_rates():
 def test_library_loads_after_torch(tmp_path):
     """bench.py and the gloo tests import torch before the library; a PyTorch wheel brings
     its own (older) libamdhip64, so the library must not need a newer HIP symbol version at
-    load time (hipMemcpyBatchAsync, HIP 7.1, is looked up at run time instead)."""
+    load time (no HIP 7.1-only call such as hipMemcpyBatchAsync is linked)."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -27,6 +27,8 @@ for step in "$@"; do
     bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
     bench_files) run bench_files 600 python bench.py --workload files --steps 2 --warmup 1 ;;
     bench_engine) run bench_engine 300 python bench.py --workload engine ;;
+    pinned_ab) run pinned_ab 400 python tools/pinned_ab.py 48 192 ;;
+    e2e_w2 | e2e_w3 | e2e_w4) run $step 300 env KRK_STAGING_WINDOWS=${step#e2e_w} python bench.py --e2e-only --no-cpu-baseline ;;
     # rocprofv3 on the end-to-end legs (kernel trace + copy trace; PMC passes on their own runs)
     prof_e2e) run prof_e2e 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
                   -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
