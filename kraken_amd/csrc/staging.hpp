@@ -30,8 +30,8 @@ struct DevMem {
 };
 
 // ------------------------------------------------------------------ host staging pipeline
-// Two pinned host windows and two device windows; window k is refilled only after
-// the kernel that consumed it (event) has finished.
+// One pinned host window and one device window of the ring; window k is refilled only
+// after the kernels that consumed it (events) have finished.
 struct Window {
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
@@ -43,7 +43,7 @@ struct Window {
     bool done_pending[2] = {false, false};
 };
 
-// Two pinned host windows and two device windows.  The host side of window k is
+// A ring of pinned host windows and device windows.  The host side of window k is
 // refilled once its H2D is done; the H2D into its device side waits (on the copy
 // stream only) for the kernels that read the previous contents, so the upload of
 // window k+1 overlaps the kernels of window k.
@@ -53,13 +53,15 @@ struct CopyTask {
     size_t n;
 };
 
-// KRK_STAGING_WINDOWS (2..4, default 2): windows in the ring; with more, a window's host copy
-// or file reads may run further ahead of the upload and kernels of the earlier ones.
+// KRK_STAGING_WINDOWS (2..4, default 3): windows in the ring; with more, a window's host copy
+// or file reads may run further ahead of the upload and kernels of the earlier ones.  C2's
+// end-to-end leg on MI355X: 47.4 GB/s with 2, 54.3 with 3, 53.1 with 4 (H2D 56.5 / 56.5 /
+// 53.5 measured beside each; profiles/r04/e2e_staging_windows_*.json).
 constexpr int kMaxWindows = 4;
 inline int staging_windows() {
     static const int n = [] {
         const char* v = getenv("KRK_STAGING_WINDOWS");
-        const int x = v ? atoi(v) : 2;
+        const int x = v ? atoi(v) : 3;
         return std::min(kMaxWindows, std::max(2, x));
     }();
     return n;
@@ -179,7 +181,7 @@ struct StagingLease {
 
 inline int lease_staging(Device* D, size_t cap, StagingLease& L) {
     L.D = D;
-    constexpr size_t kKeepMax = size_t(1) << 30;  // windows kept across calls: at most 2 x 1 GiB pinned
+    constexpr size_t kKeepMax = size_t(1) << 30;  // windows kept across calls: at most 4 x 1 GiB pinned
     if (cap <= kKeepMax && D->staging_mu.try_lock()) {
         L.locked = true;
         if (!D->staging || D->staging->w[0].cap < cap) {
