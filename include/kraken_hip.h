@@ -88,10 +88,13 @@ int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fr
 
 /* Piece sums of cache FILES: the batch form of Generator.Generate reading the
  * CAS cache file itself (lib/metainfogen/generator.go:41-58: GetCacheFileReader
- * -> NewMetaInfo).  Each file's bytes are read (pread on a pool of host
- * threads, or O_DIRECT when KRK_FILE_DIRECT=1 and the filesystem allows it)
- * straight into the pinned staging windows -- no pageable copy -- and the
- * windows feed the CRC kernel as in krk_piece_sums_host.  length is the size
+ * -> NewMetaInfo).  Placement as krk_crc32_update (krk_set_crc_placement; AUTO =
+ * the measured crossover, HOST without a device): HOST reads each file once in
+ * 512 KiB preads on the host pool and CRCs each chunk in cache; GPU reads the
+ * bytes (pread on a pool of host threads, or O_DIRECT when KRK_FILE_DIRECT=1 and
+ * the filesystem allows it) straight into the pinned staging windows -- no
+ * pageable copy -- and the windows feed the CRC kernel as in krk_piece_sums_host.
+ * krk_crc_host_split reports the call's bytes on each side.  length is the size
  * the caller stat-ed (Generate picks the piece length from it); a file shorter
  * than that is KRK_EIO "read blob: <path>: unexpected EOF".  Synchronous. */
 typedef struct krk_file_blob {

@@ -1297,7 +1297,7 @@ bool crc_auto_gpu() {
 // The placement a new piece stream / crc32_update call runs on: HOST or GPU.  `placement`
 // KRK_PLACE_AUTO follows the process setting, then the crossover; GPU needs a gfx950
 // device (KRK_ENODEV), AUTO without one is HOST.
-int resolve_crc_placement(int placement, int* rc) {
+int resolve_placement(int placement, int* rc) {
     *rc = KRK_OK;
     const bool asked_auto = placement == KRK_PLACE_AUTO;
     if (asked_auto) placement = crc_placement_setting();
@@ -1315,6 +1315,13 @@ int resolve_crc_placement(int placement, int* rc) {
     }
     return placement;
 }
+
+}  // namespace
+
+// runtime.hpp: the file and host-buffer CRC calls resolve their placement the same way.
+int resolve_crc_placement(int placement, int* rc) { return resolve_placement(placement, rc); }
+
+namespace {
 
 // Fold a request's portion CRCs into the stream's piece sums (completer thread, the
 // stream's requests in submission order).  Once a request has failed, later ones are
@@ -1449,7 +1456,7 @@ int krk_piece_stream_begin_on(int placement, int64_t piece_length, krk_piece_str
     KRK_CHECK(piece_length > 0, KRK_EINVAL, "piece length must be positive");
     *out = nullptr;
     int rc = KRK_OK;
-    const int where = resolve_crc_placement(placement, &rc);
+    const int where = resolve_placement(placement, &rc);
     if (rc) return rc;
     Engine* E = nullptr;
     if (where == KRK_PLACE_GPU) {
@@ -1557,7 +1564,7 @@ int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64
     static const size_t host_max = env_size("KRK_CRC_HOST_MAX", 64 << 10);
     int rc = KRK_OK;
     const int where = (placement == KRK_PLACE_AUTO && n <= host_max) ? KRK_PLACE_HOST
-                                                                      : resolve_crc_placement(placement, &rc);
+                                                                      : resolve_placement(placement, &rc);
     if (rc) return rc;
     if (where == KRK_PLACE_HOST) {
         *out = host_crc32_update_par(crc, data, n);

@@ -203,6 +203,10 @@ int krk_piece_sums_files_multi(const krk_file_blob* files, uint64_t n, uint32_t*
     int r = check_batch(files, n);
     if (r || !n) return r;
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
+    int prc = KRK_OK;  // host placement: one pass on the host pool, nothing to shard
+    const int where = resolve_crc_placement(KRK_PLACE_AUTO, &prc);
+    if (where < 0) return prc;
+    if (where != KRK_PLACE_GPU) return krk_piece_sums_files(files, n, sums_host);
     std::vector<uint64_t> bytes(n);
     for (uint64_t i = 0; i < n; ++i) bytes[i] = files[i].length;
     return shard_run(bytes, [&](size_t, const std::vector<uint64_t>& idx) {

@@ -576,15 +576,81 @@ int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fr
     return KRK_OK;
 }
 
+// The host placement of krk_piece_sums_files: what the reference's Generate does with a
+// cache file (lib/metainfogen/generator.go:41-58 -> core.NewMetaInfo over the file reader,
+// core/metainfo.go:157-179), spread over the host pool.  Each file is cut into spans of
+// whole pieces (~16 MiB); a span's thread preads it in 512 KiB chunks into a buffer of its
+// own and folds each chunk into the piece's CRC while the chunk is in cache.  The same
+// bytes through the GPU cost the same pread (into a pinned window) plus the host link, so
+// where the host's CRC capacity exceeds the link this placement is faster.
+static int piece_sums_files_host(const krk_file_blob* files, uint64_t n, uint32_t* sums_host) {
+    struct Span {
+        uint64_t file, first, pieces;
+    };
+    std::vector<Span> spans;
+    constexpr uint64_t kSpan = 16ull << 20;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t P = (uint64_t)files[i].piece_length, np = krk_num_pieces(files[i].length, files[i].piece_length);
+        const uint64_t per = std::max<uint64_t>(1, kSpan / P);
+        for (uint64_t k = 0; k < np; k += per) spans.push_back({i, k, std::min(per, np - k)});
+    }
+    std::mutex emu;
+    std::string emsg;
+    std::atomic<bool> failed{false};
+    auto fail = [&](const std::string& m) {
+        std::lock_guard<std::mutex> g(emu);
+        if (emsg.empty()) emsg = m;
+        failed.store(true);
+    };
+    const int T = std::max(1, host_threads_for_call());
+    host_parallel_for(spans.size(), T - 1, [&](size_t s) {
+        if (failed.load(std::memory_order_relaxed)) return;
+        constexpr size_t kChunk = 512u << 10;
+        thread_local std::vector<uint8_t> buf;
+        if (buf.size() < kChunk) buf.resize(kChunk);
+        const Span& sp = spans[s];
+        const krk_file_blob& f = files[sp.file];
+        const int fd = open(f.path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+            fail(std::string("open ") + f.path + ": " + strerror(errno));
+            return;
+        }
+        const uint64_t P = (uint64_t)f.piece_length;
+        for (uint64_t k = sp.first; k < sp.first + sp.pieces; ++k) {
+            uint64_t a = k * P;
+            const uint64_t e = std::min(f.length, a + P);
+            uint32_t c = 0;
+            while (a < e) {
+                const ssize_t got = pread(fd, buf.data(), std::min<uint64_t>(kChunk, e - a), (off_t)a);
+                if (got < 0 && errno == EINTR) continue;
+                if (got <= 0) {
+                    fail(std::string("read blob: ") + f.path + ": " + (got < 0 ? strerror(errno) : "unexpected EOF"));
+                    close(fd);
+                    return;
+                }
+                c = host_crc32_update(c, buf.data(), (size_t)got);
+                a += (uint64_t)got;
+            }
+            sums_host[f.sums_offset + k] = c;
+        }
+        close(fd);
+    });
+    if (failed.load()) {
+        set_error(KRK_EIO, "%s", emsg.c_str());
+        return KRK_EIO;
+    }
+    return KRK_OK;
+}
+
 int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_host) {
-    KRK_DEVICE(D);
     if (!n) return KRK_OK;
     KRK_CHECK(files, KRK_EINVAL, "files is NULL");
-    uint64_t lo = ~0ull, hi = 0;
+    uint64_t lo = ~0ull, hi = 0, bytes = 0;
     for (uint64_t i = 0; i < n; ++i) {
         KRK_CHECK(files[i].path, KRK_EINVAL, "file %llu: path is NULL", (unsigned long long)i);
         KRK_CHECK(files[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
         const uint64_t np = krk_num_pieces(files[i].length, files[i].piece_length);
+        bytes += files[i].length;
         if (np) {
             lo = std::min(lo, files[i].sums_offset);
             hi = std::max(hi, files[i].sums_offset + np);
@@ -592,6 +658,14 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
     }
     if (hi == 0) return KRK_OK;
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
+    // CRC placement (krk_set_crc_placement, else the measured crossover; HOST without a device)
+    int prc = KRK_OK;
+    const int where = resolve_crc_placement(KRK_PLACE_AUTO, &prc);
+    if (where < 0) return prc;
+    t_split_gpu = where == KRK_PLACE_GPU ? bytes : 0;
+    t_split_host = where == KRK_PLACE_GPU ? 0 : bytes;
+    if (where != KRK_PLACE_GPU) return piece_sums_files_host(files, n, sums_host);
+    KRK_DEVICE(D);
     const bool want_direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
     uint32_t* d_sums = nullptr;
     DevMem mem;

@@ -747,6 +747,10 @@ void host_parallel_for(size_t n, int helpers, std::function<void(size_t)> f);
 uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 // crc32.Update(crc, p[0, n)) with idle pool threads taking spans of a large buffer.
 uint32_t host_crc32_update_par(uint32_t crc, const uint8_t* p, size_t n);
+// The placement (KRK_PLACE_HOST / KRK_PLACE_GPU) of a CRC-only call asked for `placement`
+// (engine.cpp): AUTO follows krk_set_crc_placement, then the measured host-vs-link
+// crossover; -1 with *rc set when GPU is forced and no device is usable.
+int resolve_crc_placement(int placement, int* rc);
 double host_link(const Rates& R);
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode = kOffDevice);

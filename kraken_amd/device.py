@@ -388,6 +388,34 @@ def metainfo_digest_files(paths, lengths, piece_lengths, multi: bool = False):
     return [sums[int(offs[i]):int(offs[i + 1])] for i in range(n)], dg[:n]
 
 
+def piece_sums_files(paths, lengths, piece_lengths, multi: bool = False):
+    """krk_piece_sums_files: the piece sums of CAS files (Generate over cache files), on the
+    CRC placement (krk_set_crc_placement; AUTO = the measured crossover).  Returns the sums
+    per file as one array (offsets from the counts) and the per-file views."""
+    n = len(paths)
+    L = np.asarray(lengths, dtype=np.uint64)
+    pls = np.broadcast_to(np.asarray(piece_lengths, dtype=np.int64), (n,))
+    counts = [int(lib.krk_num_pieces(int(l), int(p))) for l, p in zip(L, pls)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(counts) if n else []
+    enc = [p.encode() if isinstance(p, str) else bytes(p) for p in paths]
+    arr = (krk_file_blob * max(n, 1))()
+    for i in range(n):
+        arr[i] = krk_file_blob(enc[i], int(L[i]), int(pls[i]), int(offs[i]))
+    sums = np.zeros(max(int(offs[-1]), 1), dtype=np.uint32)
+    fn = lib.krk_piece_sums_files_multi if multi else lib.krk_piece_sums_files
+    check(fn(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32))))
+    return sums, offs
+
+
+PLACE_AUTO, PLACE_HOST, PLACE_GPU = 0, 1, 2
+
+
+def set_crc_placement(placement: int):
+    """krk_set_crc_placement: the process-wide placement of CRC-only host calls."""
+    check(lib.krk_set_crc_placement(int(placement)))
+
+
 def windows_last_call() -> dict:
     """The calling thread's last krk_metainfo_digest_host / _files call: the most live blobs
     in a window, the windows, the blobs the host offload took (krk_windows_last_call)."""

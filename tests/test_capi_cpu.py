@@ -440,3 +440,52 @@ def test_library_loads_after_torch(tmp_path):
             "print(_capi.lib.krk_version().decode())" % root)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("kraken_amd"), r.stderr[-2000:]
+
+
+def test_piece_sums_files_host_placement(tmp_path):
+    """krk_piece_sums_files (+ _multi) on the host placement -- Generate over cache files
+    (generator.go:41-58) read once in preads on the host pool, no device needed: every
+    piece sum equals zlib over the file's bytes, and the reference's error texts hold."""
+    import zlib
+    from kraken_amd._capi import krk_file_blob
+    rng = np.random.default_rng(31)
+    lens = [0, 1, 63, 4096, (1 << 20) - 1, (1 << 20) + 1, (17 << 20) + 3, 40 << 20]
+    datas = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    paths = []
+    for i, d in enumerate(datas):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(d)
+        paths.append(str(p).encode())
+    check(lib.krk_set_crc_placement(_capi.KRK_PLACE_HOST))
+    try:
+        for P in (1, 4097, 1 << 20, 4 << 20):
+            if P == 1:
+                use = [i for i, L in enumerate(lens) if L <= 4096]
+            else:
+                use = list(range(len(lens)))
+            arr = (krk_file_blob * len(use))()
+            off = 0
+            for k, i in enumerate(use):
+                arr[k] = krk_file_blob(paths[i], lens[i], P, off)
+                off += int(lib.krk_num_pieces(lens[i], P))
+            for fn in (lib.krk_piece_sums_files, lib.krk_piece_sums_files_multi):
+                sums = np.zeros(max(off, 1), dtype=np.uint32)
+                check(fn(arr, len(use), sums.ctypes.data_as(C.POINTER(C.c_uint32))))
+                for k, i in enumerate(use):
+                    d = datas[i]
+                    want = [zlib.crc32(d[a:a + P]) for a in range(0, len(d), P)]
+                    got = sums[arr[k].sums_offset:arr[k].sums_offset + len(want)]
+                    assert list(got) == want, (P, i)
+            g, h, _ = C.c_uint64(), C.c_uint64(), C.c_double()
+            check(lib.krk_crc_host_split(C.byref(g), C.byref(h), C.byref(_)))
+            assert g.value == 0 and h.value == sum(lens[i] for i in use)
+        sums = np.zeros(64, dtype=np.uint32)
+        bad = (krk_file_blob * 1)(krk_file_blob(paths[5], lens[5] + 10, 1 << 20, 0))
+        assert lib.krk_piece_sums_files(bad, 1, sums.ctypes.data_as(C.POINTER(C.c_uint32))) == _capi.KRK_EIO
+        assert lib.krk_last_error() == b"read blob: " + paths[5] + b": unexpected EOF"
+        missing = str(tmp_path / "nope").encode()
+        bad = (krk_file_blob * 1)(krk_file_blob(missing, 5, 1 << 20, 0))
+        assert lib.krk_piece_sums_files(bad, 1, sums.ctypes.data_as(C.POINTER(C.c_uint32))) == _capi.KRK_EIO
+        assert lib.krk_last_error() == b"open " + missing + b": No such file or directory"
+    finally:
+        check(lib.krk_set_crc_placement(_capi.KRK_PLACE_AUTO))

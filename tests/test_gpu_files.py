@@ -209,3 +209,27 @@ def test_pinned_blobs_go_direct(gpu, orc, mixed):
         bufs.clear()
     assert st["windows"] >= 2 and st["host_blobs"] == 0
     assert st["direct_windows"] == (0 if mixed else st["windows"]), st
+
+
+def test_piece_sums_files_placements_agree(gpu, orc, tmp_path):
+    """krk_piece_sums_files on each CRC placement (host preads + PCLMUL on the host pool, GPU
+    windows + CRC kernel, and AUTO = the measured crossover) gives the oracle's sums; the
+    split report names the side that ran."""
+    lens = EDGE + [(40 << 20) + 3]
+    datas = [orc.synth(4000 + i, L) for i, L in enumerate(lens)]
+    paths = [_write(tmp_path, f"p{i}", d) for i, d in enumerate(datas)]
+    got = {}
+    try:
+        for name, place in (("host", D.PLACE_HOST), ("gpu", D.PLACE_GPU), ("auto", D.PLACE_AUTO)):
+            D.set_crc_placement(place)
+            got[name] = D.piece_sums_files(paths, lens, 1 << 20)
+            g, h, _ = D.crc_host_split()
+            if name != "auto":
+                assert (g > 0) == (name == "gpu") and g + h == sum(lens), (name, g, h)
+    finally:
+        D.set_crc_placement(D.PLACE_GPU)  # the suite's setting (conftest)
+    sums, offs = got["host"]
+    for name in ("gpu", "auto"):
+        assert np.array_equal(got[name][0], sums), name
+    for i, d in enumerate(datas):
+        assert np.array_equal(sums[int(offs[i]):int(offs[i + 1])], orc.calc_piece_sums(d, 1 << 20)[1]), i

@@ -27,6 +27,9 @@ for step in "$@"; do
     bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
     bench_files) run bench_files 600 python bench.py --workload files --steps 2 --warmup 1 ;;
     bench_engine) run bench_engine 300 python bench.py --workload engine ;;
+    bench_c4) run bench_c4 600 python bench.py --workload c4 ;;
+    bench_c5regen) run bench_c5regen 600 python bench.py --workload c5regen ;;
+    bench_c3) run bench_c3 900 python bench.py --workload c3 ;;
     pinned_ab) run pinned_ab 400 python tools/pinned_ab.py 48 192 ;;
     e2e_w2 | e2e_w3 | e2e_w4) run $step 300 env KRK_STAGING_WINDOWS=${step#e2e_w} python bench.py --e2e-only --no-cpu-baseline ;;
     # rocprofv3 on the end-to-end legs (kernel trace + copy trace; PMC passes on their own runs)
