@@ -80,10 +80,12 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
  * lib/torrent/storage/agentstorage/torrent.go:182-193) and the GPU pass.  Pinned caller
  * bytes (krk_host_alloc) are DMA'd straight into the device windows and the GPU takes a
  * share learned from the previous calls' measured rates of both sides (first call: the
- * planner rates' model, at most 10 %); pageable bytes stay on the host (a staging copy per
- * byte costs more than the GPU saves).  KRK_CRC_GPU_FRACTION forces the share.  This
- * returns the calling thread's last split in bytes and the share the next pinned batch of its device
- * will use (-1 until learned). */
+ * planner rates' model, at most 10 %) -- or none, when host-only calls measured faster
+ * than split ones (the second call runs host-only to find out; every 16th call re-measures
+ * the other choice).  Pageable bytes stay on the host (a staging copy per byte costs more
+ * than the GPU saves).  KRK_CRC_GPU_FRACTION forces the share.  This returns the calling
+ * thread's last split in bytes and the share the next pinned batch of its device will use
+ * (0 while host-only wins, -1 until learned). */
 int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction);
 
 /* Piece sums of cache FILES: the batch form of Generator.Generate reading the

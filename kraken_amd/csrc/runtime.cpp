@@ -456,17 +456,23 @@ struct PieceTask {
     uint64_t out;
 };
 
-// GPU share of pinned CRC batches learned from earlier calls (-1: none yet), and the
-// calling thread's last split (krk_crc_host_split).
-// Per device (one process-wide share fitted every device and batch alike).
-static std::atomic<double> g_crc_split[kMaxDevs];
-static std::once_flag g_crc_split_once;
-static std::atomic<double>& crc_split_of(int dev) {
-    std::call_once(g_crc_split_once, [] {
-        for (auto& x : g_crc_split) x.store(-1.0);
-    });
-    return g_crc_split[(dev >= 0 && dev < kMaxDevs) ? dev : 0];
-}
+// The pinned-batch split of each device, learned from earlier calls (per device).
+//  * frac: the balanced GPU share -- where both sides would have ended together at the
+//    rates the last split call measured (-1: none yet; first call: the rates' model, <= 10 %);
+//  * r_split / r_host: whole-call throughput (bytes / wall time) of calls at that split and
+//    of host-only calls.  The DMA reads share host memory with the CRC threads, so a balanced
+//    split can still lose to the host alone (C4's 20 GiB pinned blob on one box: 131 GB/s at
+//    the balanced 27 % against 260 host-only; f1verify on another: 282 at 10 % against 228).
+//    So the second call runs host-only, later calls take whichever measured faster, and
+//    every 16th call re-measures the other one.
+struct CrcSplit {
+    std::mutex mu;
+    double frac = -1, r_split = 0, r_host = 0;
+    uint64_t calls = 0;
+    bool use_split() const { return r_host <= 0 || r_split >= r_host; }
+};
+static CrcSplit g_crc_split[kMaxDevs];
+static CrcSplit& crc_split_of(int dev) { return g_crc_split[(dev >= 0 && dev < kMaxDevs) ? dev : 0]; }
 static thread_local uint64_t t_split_gpu = 0, t_split_host = 0;
 
 int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
@@ -502,9 +508,14 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     // cost more than the GPU saved (host only 241 GB/s, the model's split 202).
     const double c = R.host_crc, H = T * c;
     double gpu_frac = 0.0;
-    if (all_pinned) {
-        const double learned = crc_split_of(D->id).load(std::memory_order_relaxed);
-        gpu_frac = learned >= 0 ? learned : std::min(0.10, R.h2d / (R.h2d + H));
+    CrcSplit& cs = crc_split_of(D->id);
+    if (all_pinned && !forced) {
+        std::lock_guard<std::mutex> g(cs.mu);
+        const uint64_t k = ++cs.calls;
+        bool split = cs.r_split <= 0 || (cs.r_host > 0 && cs.use_split());
+        if (cs.r_split > 0 && cs.r_host <= 0) split = false;  // the second call: host only
+        else if (k % 16 == 0) split = !split;                    // re-measure the other side
+        gpu_frac = split ? (cs.frac >= 0 ? cs.frac : std::min(0.10, R.h2d / (R.h2d + H))) : 0.0;
     }
     if (forced) gpu_frac = std::clamp(atof(forced), 0.0, 1.0);
     // Whole pieces to the GPU until its share of the bytes is reached, the rest to the host.
@@ -559,12 +570,20 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     const double hbytes = bytes - gbytes, host_s = host_end_ns.load() * 1e-9;
     t_split_gpu = (uint64_t)gbytes;
     t_split_host = (uint64_t)hbytes;
-    if (!r && all_pinned && !forced && gbytes >= (64u << 20) && hbytes >= (64u << 20) && gpu_s > 0 && host_s > 0) {
-        // the split where both sides would have ended together at the rates just measured
-        const double rg = gbytes / gpu_s, rh = hbytes / host_s, want = rg / (rg + rh);
-        std::atomic<double>& split = crc_split_of(D->id);
-        const double cur = split.load(std::memory_order_relaxed);
-        split.store(cur >= 0 ? 0.5 * cur + 0.5 * want : want, std::memory_order_relaxed);
+    const double call_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!r && all_pinned && !forced && bytes >= (128u << 20) && call_s > 0) {
+        std::lock_guard<std::mutex> g(cs.mu);
+        auto ema = [](double& x, double v) { x = x > 0 ? 0.5 * x + 0.5 * v : v; };
+        if (gbytes > 0) {
+            ema(cs.r_split, bytes / call_s);
+            if (gbytes >= (64u << 20) && hbytes >= (64u << 20) && gpu_s > 0 && host_s > 0) {
+                // the split where both sides would have ended together at the rates just measured
+                const double rg = gbytes / gpu_s, rh = hbytes / host_s, want = rg / (rg + rh);
+                cs.frac = cs.frac >= 0 ? 0.5 * cs.frac + 0.5 * want : want;
+            }
+        } else {
+            ema(cs.r_host, bytes / call_s);
+        }
     }
     return r;
 }
@@ -572,7 +591,11 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
 int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction) {
     if (gpu_bytes) *gpu_bytes = t_split_gpu;
     if (host_bytes) *host_bytes = t_split_host;
-    if (gpu_fraction) *gpu_fraction = crc_split_of(t_dev).load(std::memory_order_relaxed);
+    if (gpu_fraction) {
+        CrcSplit& cs = crc_split_of(t_dev);
+        std::lock_guard<std::mutex> g(cs.mu);
+        *gpu_fraction = cs.r_host > 0 && !cs.use_split() ? 0.0 : cs.frac;
+    }
     return KRK_OK;
 }
 
