@@ -476,7 +476,6 @@ static CrcSplit& crc_split_of(int dev) { return g_crc_split[(dev >= 0 && dev < k
 static thread_local uint64_t t_split_gpu = 0, t_split_host = 0;
 
 int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host) {
-    KRK_DEVICE(D);
     int r = validate_blobs(blobs, n_blobs);
     if (r) return r;
     uint64_t lo, hi;
@@ -498,8 +497,15 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         if (all_pinned && blobs[i].length && !host_pinned(blobs[i].data, blobs[i].length)) all_pinned = false;
     }
     const char* forced = getenv("KRK_CRC_GPU_FRACTION");
-    // Rates only where they decide something: pageable batches stay on the host threads.
-    const Rates R = (all_pinned || forced) ? planner_rates(D) : Rates{};
+    // Pageable batches stay on the host threads and need no device; pinned (or forced) ones
+    // split by the device's rates.
+    Device* D = nullptr;
+    if (all_pinned || forced) {
+        int drc = KRK_OK;
+        D = device(&drc);
+        if (!D) return drc;
+    }
+    const Rates R = D ? planner_rates(D) : Rates{};
     // Pinned bytes: the GPU's share starts from the rates' model, capped at 10 %, and is then
     // set from what the previous calls measured (each side's bytes over its own wall time
     // while both ran): the DMA reads share the host's memory with the CRC threads, so the
@@ -508,7 +514,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     // cost more than the GPU saved (host only 241 GB/s, the model's split 202).
     const double c = R.host_crc, H = T * c;
     double gpu_frac = 0.0;
-    CrcSplit& cs = crc_split_of(D->id);
+    CrcSplit& cs = crc_split_of(D ? D->id : 0);
     if (all_pinned && !forced) {
         std::lock_guard<std::mutex> g(cs.mu);
         const uint64_t k = ++cs.calls;

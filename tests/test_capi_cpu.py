@@ -489,3 +489,20 @@ def test_piece_sums_files_host_placement(tmp_path):
         assert lib.krk_last_error() == b"open " + missing + b": No such file or directory"
     finally:
         check(lib.krk_set_crc_placement(_capi.KRK_PLACE_AUTO))
+
+
+def test_piece_sums_host_pageable_needs_no_device():
+    """Pageable host buffers stay on host threads (krk_piece_sums_host / verify_pieces_host),
+    so those calls run without a gfx950 device: sums equal zlib, verdicts follow them."""
+    import zlib
+    from kraken_amd import agentstorage
+    from kraken_amd import device as D
+    rng = np.random.default_rng(41)
+    datas = [rng.integers(0, 256, L, dtype=np.uint8) for L in (0, 1, 4097, (3 << 20) + 5, 9 << 20)]
+    for P in (1 << 20, 4097):
+        for d, s in zip(datas, D.piece_sums_host(datas, P)):
+            b = d.tobytes()
+            assert [int(x) for x in s] == [zlib.crc32(b[k:k + P]) for k in range(0, len(b), P)]
+    exp = np.array([zlib.crc32(d.tobytes()) for d in datas], dtype=np.uint32)
+    exp[2] ^= 1
+    assert list(agentstorage.verify_pieces(datas, exp)) == [True, True, False, True, True]
