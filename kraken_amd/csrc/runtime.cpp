@@ -4,6 +4,8 @@
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1389,16 +1391,84 @@ int krk_dev_free(void* p) {
     KRK_HIP(hipFree(p));
     return KRK_OK;
 }
+// Page-locked host memory for receive buffers and staged results.  Large buffers are
+// anonymous mappings in transparent huge pages, interleaved over the host's NUMA nodes and
+// then registered with HIP: the GPU's DMA reads them at the same rate as hipHostMalloc
+// memory (57.3 vs 57.5 GB/s), while host threads reading them -- the host share of a CRC
+// split, an agent's own checks -- are no longer held to one node's bandwidth (hipHostMalloc
+// places every page on one node: 16 threads' CRC 194 GB/s there against 284-304 spread;
+// tools/micro/host_mem_probe.cpp, profiles/r04/host_mem_probe.jsonl).  Small buffers stay
+// hipHostMalloc (one registration per call costs more than it saves).
+namespace {
+std::mutex g_host_mu;
+std::unordered_map<void*, size_t> g_host_maps;  // registered mappings: address -> length
+
+unsigned long online_nodes_mask() {
+    FILE* f = fopen("/sys/devices/system/node/online", "r");
+    if (!f) return 0;
+    char buf[256] = {0};
+    const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+    fclose(f);
+    if (!ok) return 0;
+    unsigned long m = 0;
+    for (char* q = buf; *q && *q != '\n';) {
+        char* e = nullptr;
+        long a = strtol(q, &e, 10), b = a;
+        if (e == q) break;
+        if (*e == '-') b = strtol(e + 1, &e, 10);
+        for (long x = a; x <= b && x < 64; ++x) m |= 1ul << x;
+        q = *e == ',' ? e + 1 : e;
+    }
+    return m;
+}
+}  // namespace
+
 int krk_host_alloc(uint64_t bytes, void** out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_DEVICE(D);
     (void)D;
+    constexpr uint64_t kLarge = 2ull << 20;
+    if (bytes >= kLarge) {
+        const size_t len = (bytes + kLarge - 1) & ~(kLarge - 1);
+        void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p != MAP_FAILED) {
+            madvise(p, len, MADV_HUGEPAGE);
+            static const unsigned long nodes = online_nodes_mask();
+            if (nodes & (nodes - 1)) {  // more than one node: interleave (refused by a cpuset: default policy)
+                unsigned long mask[2] = {nodes, 0};
+                (void)syscall(SYS_mbind, p, len, 3 /* MPOL_INTERLEAVE */, mask, 65, 0);
+            }
+            if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+                std::lock_guard<std::mutex> g(g_host_mu);
+                g_host_maps[p] = len;
+                *out = p;
+                return KRK_OK;
+            }
+            (void)hipGetLastError();
+            munmap(p, len);
+        }
+    }
     hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
     KRK_CHECK(e == hipSuccess, KRK_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
               hipGetErrorString(e));
     return KRK_OK;
 }
 int krk_host_free(void* p) {
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        auto it = g_host_maps.find(p);
+        if (it != g_host_maps.end()) {
+            len = it->second;
+            g_host_maps.erase(it);
+        }
+    }
+    if (len) {
+        const hipError_t e = hipHostUnregister(p);
+        munmap(p, len);
+        KRK_HIP(e);
+        return KRK_OK;
+    }
     KRK_HIP(hipHostFree(p));
     return KRK_OK;
 }
