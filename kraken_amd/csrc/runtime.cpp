@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -1402,6 +1403,7 @@ int krk_dev_free(void* p) {
 namespace {
 std::mutex g_host_mu;
 std::unordered_map<void*, size_t> g_host_maps;  // registered mappings: address -> length
+std::map<uintptr_t, size_t> g_host_ranges;      // every live krk_host_alloc block: start -> length
 
 unsigned long online_nodes_mask() {
     FILE* f = fopen("/sys/devices/system/node/online", "r");
@@ -1423,6 +1425,18 @@ unsigned long online_nodes_mask() {
 }
 }  // namespace
 
+extern "C++" {
+namespace krk {
+bool lib_pinned_range(const void* p, uint64_t n) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(g_host_mu);
+    auto it = g_host_ranges.upper_bound(a);
+    if (it == g_host_ranges.begin()) return false;
+    --it;
+    return a >= it->first && a + n <= it->first + it->second;
+}
+}  // namespace krk
+}
 int krk_host_alloc(uint64_t bytes, void** out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_DEVICE(D);
@@ -1441,6 +1455,7 @@ int krk_host_alloc(uint64_t bytes, void** out) {
             if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
                 std::lock_guard<std::mutex> g(g_host_mu);
                 g_host_maps[p] = len;
+                g_host_ranges[reinterpret_cast<uintptr_t>(p)] = len;
                 *out = p;
                 return KRK_OK;
             }
@@ -1451,12 +1466,15 @@ int krk_host_alloc(uint64_t bytes, void** out) {
     hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
     KRK_CHECK(e == hipSuccess, KRK_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
               hipGetErrorString(e));
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host_ranges[reinterpret_cast<uintptr_t>(*out)] = bytes ? bytes : 1;
     return KRK_OK;
 }
 int krk_host_free(void* p) {
     size_t len = 0;
     {
         std::lock_guard<std::mutex> g(g_host_mu);
+        g_host_ranges.erase(reinterpret_cast<uintptr_t>(p));
         auto it = g_host_maps.find(p);
         if (it != g_host_maps.end()) {
             len = it->second;

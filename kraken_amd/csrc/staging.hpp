@@ -200,10 +200,15 @@ inline int lease_staging(Device* D, size_t cap, StagingLease& L) {
     return L.own->init(cap);
 }
 
-// Whether [p, p + n) is page-locked host memory (krk_host_alloc / hipHostMalloc).  Pageable
+// Whether [p, p + n) is page-locked host memory (krk_host_alloc / hipHostMalloc).  A range
+// inside a krk_host_alloc block is answered from the library's own table (thousands of
+// receive-buffer pieces a batch: a HIP pointer query each cost ~3 us).  Pageable
 // memory is an expected "invalid value" here: not left pending on the thread (the next
 // launch would report it as an unchecked earlier error).
+bool lib_pinned_range(const void* p, uint64_t n);  // runtime.cpp: inside one live krk_host_alloc block
+
 inline bool host_pinned(const void* p, uint64_t n) {
+    if (lib_pinned_range(p, n)) return true;  // the library's own blocks: no HIP query
     auto pinned_at = [](const void* q) {
         hipPointerAttribute_t a{};
         if (hipPointerGetAttributes(&a, q) != hipSuccess) {

@@ -95,7 +95,16 @@ int main(int argc, char** argv) {
     void* dev = nullptr;
     hipStream_t s = nullptr;
     if (hipMalloc(&dev, n) != hipSuccess || hipStreamCreate(&s) != hipSuccess) return 1;
-    for (const char* kind : {"hipHostMalloc", "malloc", "mmap_thp", "mmap_thp_registered", "hipHostMalloc_numauser"}) {
+    {
+        std::ifstream on("/sys/devices/system/node/online"), st("/proc/self/status");
+        std::string online, line, mems;
+        std::getline(on, online);
+        while (std::getline(st, line))
+            if (line.rfind("Mems_allowed_list:", 0) == 0) mems = line.substr(18);
+        printf("{\"nodes_online\": \"%s\", \"mems_allowed\": \"%s\"}\n", online.c_str(), mems.c_str());
+    }
+    for (const char* kind : {"hipHostMalloc", "malloc", "mmap_thp", "mmap_thp_registered", "mmap_thp_interleave_registered",
+                             "hipHostMalloc_numauser"}) {
         const long huge0 = anon_huge_kb();
         uint8_t* p = nullptr;
         bool pinned = false, mapped = false;
@@ -113,6 +122,11 @@ int main(int argc, char** argv) {
             if (p == MAP_FAILED) return 1;
             madvise(p, n, MADV_HUGEPAGE);
             mapped = true;
+            if (!strcmp(kind, "mmap_thp_interleave_registered")) {
+                unsigned long mask[2] = {3, 0};
+                const long rc = syscall(SYS_mbind, p, n, 3 /* MPOL_INTERLEAVE */, mask, 65, 0);
+                printf("{\"mbind_rc\": %ld, \"errno\": %d}\n", rc, rc ? errno : 0);
+            }
         }
         // first touch on T threads (spans), as a filling receive path would
         {
@@ -127,7 +141,7 @@ int main(int argc, char** argv) {
                 });
             for (auto& x : th) x.join();
         }
-        if (!strcmp(kind, "mmap_thp_registered")) {
+        if (!strncmp(kind, "mmap_thp_", 9)) {
             if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) return 1;
             pinned = true;
         }
@@ -140,7 +154,7 @@ int main(int argc, char** argv) {
                kind, n / double(1ull << 30), T, alloc_s, crc, h2d, nodes_of(p, n).c_str(),
                huge1 >= 0 ? (huge1 - huge0) * 1024.0 / n : -1.0);
         fflush(stdout);
-        if (!strcmp(kind, "mmap_thp_registered")) hipHostUnregister(p);
+        if (!strncmp(kind, "mmap_thp_", 9)) hipHostUnregister(p);
         if (!strcmp(kind, "hipHostMalloc") || !strcmp(kind, "hipHostMalloc_numauser")) hipHostFree(p);
         else if (mapped) munmap(p, n);
         else free(p);
