@@ -558,9 +558,17 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     double hbytes_all = 0;
     for (const PieceTask& h : host) hbytes_all += (double)h.n;
     const int TH = (int)std::min<size_t>({(size_t)T, host.size(), (size_t)(hbytes_all / (8 << 20)) + 1});
-    HostBatch hb(host.size(), gpu.empty() ? TH - 1 : TH, [&](size_t j) {
-        sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
-        if (left.fetch_sub(1) == 1)  // the last piece: the host side's wall time
+    // A task is a run of consecutive pieces (~8 MiB): one thread streams through adjacent
+    // bytes, which the hardware prefetchers follow (256 KiB tasks handed out one at a time ran
+    // C4's host side ~30 % below contiguous spans, profiles/r04/host_mem_probe_lib.jsonl).
+    const size_t G = host.empty() ? 1
+                                  : std::max<size_t>(1, (size_t)((8u << 20) / std::max(1.0, hbytes_all / host.size())));
+    const size_t n_tasks = (host.size() + G - 1) / G;
+    left.store(n_tasks);
+    HostBatch hb(n_tasks, gpu.empty() ? TH - 1 : TH, [&](size_t t) {
+        for (size_t j = t * G; j < std::min(host.size(), (t + 1) * G); ++j)
+            sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
+        if (left.fetch_sub(1) == 1)  // the last task: the host side's wall time
             host_end_ns.store(
                 std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
     });
@@ -1393,36 +1401,18 @@ int krk_dev_free(void* p) {
     return KRK_OK;
 }
 // Page-locked host memory for receive buffers and staged results.  Large buffers are
-// anonymous mappings in transparent huge pages, interleaved over the host's NUMA nodes and
-// then registered with HIP: the GPU's DMA reads them at the same rate as hipHostMalloc
-// memory (57.3 vs 57.5 GB/s), while host threads reading them -- the host share of a CRC
-// split, an agent's own checks -- are no longer held to one node's bandwidth (hipHostMalloc
-// places every page on one node: 16 threads' CRC 194 GB/s there against 284-304 spread;
-// tools/micro/host_mem_probe.cpp, profiles/r04/host_mem_probe.jsonl).  Small buffers stay
-// hipHostMalloc (one registration per call costs more than it saves).
+// anonymous mappings in transparent huge pages registered with HIP (pages placed by the
+// default policy as the registration faults them in): the GPU's DMA reads them at the same
+// rate as hipHostMalloc memory (57.2-57.6 GB/s) and host threads read them as fast as
+// pageable memory (the library's host CRC: 216 vs 218 GB/s pageable, against 166 for
+// hipHostMalloc blocks on the same box; interleaving the pages over the NUMA nodes cost as
+// much, 165; tools/micro/host_mem_probe.cpp, profiles/r04/host_mem_probe*.jsonl).  Small
+// buffers stay hipHostMalloc (one registration per call costs more than it saves).
 namespace {
 std::mutex g_host_mu;
 std::unordered_map<void*, size_t> g_host_maps;  // registered mappings: address -> length
 std::map<uintptr_t, size_t> g_host_ranges;      // every live krk_host_alloc block: start -> length
 
-unsigned long online_nodes_mask() {
-    FILE* f = fopen("/sys/devices/system/node/online", "r");
-    if (!f) return 0;
-    char buf[256] = {0};
-    const bool ok = fgets(buf, sizeof buf, f) != nullptr;
-    fclose(f);
-    if (!ok) return 0;
-    unsigned long m = 0;
-    for (char* q = buf; *q && *q != '\n';) {
-        char* e = nullptr;
-        long a = strtol(q, &e, 10), b = a;
-        if (e == q) break;
-        if (*e == '-') b = strtol(e + 1, &e, 10);
-        for (long x = a; x <= b && x < 64; ++x) m |= 1ul << x;
-        q = *e == ',' ? e + 1 : e;
-    }
-    return m;
-}
 }  // namespace
 
 extern "C++" {
@@ -1447,11 +1437,6 @@ int krk_host_alloc(uint64_t bytes, void** out) {
         void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (p != MAP_FAILED) {
             madvise(p, len, MADV_HUGEPAGE);
-            static const unsigned long nodes = online_nodes_mask();
-            if (nodes & (nodes - 1)) {  // more than one node: interleave (refused by a cpuset: default policy)
-                unsigned long mask[2] = {nodes, 0};
-                (void)syscall(SYS_mbind, p, len, 3 /* MPOL_INTERLEAVE */, mask, 65, 0);
-            }
             if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
                 std::lock_guard<std::mutex> g(g_host_mu);
                 g_host_maps[p] = len;

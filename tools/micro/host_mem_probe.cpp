@@ -12,6 +12,7 @@
 //
 //   host_mem_probe [GiB] [threads]      one JSON line per kind
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -162,11 +163,34 @@ int main(int argc, char** argv) {
     // The library's own host CRC path (krk_piece_sums_host, C4 shape: one blob, 256 KiB
     // pieces) over a hipHostMalloc buffer filled by the CPU, the same filled by D2H DMA, and
     // a pageable buffer.
-    for (const char* kind : {"lib_pinned_cpu_filled", "lib_pinned_dma_filled", "lib_pageable"}) {
+    {  // the CPUs this process may run on, and their NUMA nodes
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        sched_getaffinity(0, sizeof cs, &cs);
+        int per_node[8] = {0};
+        for (int c = 0; c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &cs))
+                for (int nd = 0; nd < 8; ++nd)
+                    if (access(("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/node" + std::to_string(nd)).c_str(),
+                               F_OK) == 0)
+                        ++per_node[nd];
+        printf("{\"affinity_cpus\": %d, \"cpus_per_node\": [%d,%d,%d,%d]}\n", CPU_COUNT(&cs), per_node[0], per_node[1],
+               per_node[2], per_node[3]);
+    }
+    for (const char* kind : {"lib_pinned_cpu_filled", "lib_pinned_dma_filled", "lib_pageable", "lib_thp_interleave_pageable",
+                             "lib_thp_local_registered", "lib_thp_local_pageable"}) {
         uint8_t* p = nullptr;
         const bool pinned = strncmp(kind, "lib_pinned", 10) == 0;
+        const bool thp = strncmp(kind, "lib_thp", 7) == 0;
         if (pinned) {
             if (krk_host_alloc(n, (void**)&p) != KRK_OK) return 1;
+        } else if (thp) {
+            p = (uint8_t*)mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            madvise(p, n, MADV_HUGEPAGE);
+            if (strstr(kind, "interleave")) {
+                unsigned long mask[2] = {3, 0};
+                syscall(SYS_mbind, p, n, 3, mask, 65, 0);
+            }
         } else {
             p = (uint8_t*)malloc(n);
         }
@@ -178,6 +202,8 @@ int main(int argc, char** argv) {
                 memcpy(p + i, &z, 8);
             }
         }
+        if (!strcmp(kind, "lib_thp_local_registered") && hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess)
+            return 1;
         const uint64_t P = 256 << 10, np = n / P;
         std::vector<uint32_t> sums(np);
         krk_blob b{p, n, (int64_t)P, 0};
@@ -198,7 +224,10 @@ int main(int argc, char** argv) {
                kind, n / double(1ull << 30), best, (unsigned long long)g, (unsigned long long)h, nodes_of(p, n).c_str());
         fflush(stdout);
         if (pinned) krk_host_free(p);
-        else free(p);
+        else if (thp) {
+            if (!strcmp(kind, "lib_thp_local_registered")) hipHostUnregister(p);
+            munmap(p, n);
+        } else free(p);
     }
     hipFree(dev);
     return 0;
