@@ -561,8 +561,12 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     // A task is a run of consecutive pieces (~8 MiB): one thread streams through adjacent
     // bytes, which the hardware prefetchers follow (256 KiB tasks handed out one at a time ran
     // C4's host side ~30 % below contiguous spans, profiles/r04/host_mem_probe_lib.jsonl).
+    static const double task_bytes = [] {  // KRK_CRC_TASK_KB overrides the run length (A/B)
+        const char* v = getenv("KRK_CRC_TASK_KB");
+        return v ? atof(v) * 1024.0 : double(8u << 20);
+    }();
     const size_t G = host.empty() ? 1
-                                  : std::max<size_t>(1, (size_t)((8u << 20) / std::max(1.0, hbytes_all / host.size())));
+                                  : std::max<size_t>(1, (size_t)(task_bytes / std::max(1.0, hbytes_all / host.size())));
     const size_t n_tasks = (host.size() + G - 1) / G;
     left.store(n_tasks);
     HostBatch hb(n_tasks, gpu.empty() ? TH - 1 : TH, [&](size_t t) {

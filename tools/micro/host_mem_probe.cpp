@@ -229,6 +229,38 @@ int main(int argc, char** argv) {
             munmap(p, n);
         } else free(p);
     }
+    // The agent's verify shape: 2,048 received 4 MiB pieces in one krk_host_alloc block (and
+    // in malloc memory), each its own blob, through krk_verify_pieces_host.
+    for (const char* kind : {"verify_pinned", "verify_pageable"}) {
+        uint8_t* p = nullptr;
+        const bool pinned = !strcmp(kind, "verify_pinned");
+        if (pinned) {
+            if (krk_host_alloc(n, (void**)&p) != KRK_OK) return 1;
+        } else {
+            p = (uint8_t*)malloc(n);
+        }
+        for (size_t i = 0; i < n; i += 8) {
+            uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+            memcpy(p + i, &z, 8);
+        }
+        const uint64_t P = 4 << 20, np = n / P;
+        std::vector<const uint8_t*> ptr(np);
+        std::vector<uint64_t> len(np, P);
+        std::vector<uint32_t> exp(np, 0);
+        std::vector<uint8_t> ok(np);
+        for (uint64_t i = 0; i < np; ++i) ptr[i] = p + i * P;
+        double best = 0;
+        for (int rep = 0; rep < 4; ++rep) {
+            const double t0 = now();
+            if (krk_verify_pieces_host(ptr.data(), len.data(), exp.data(), np, ok.data()) != KRK_OK) return 1;
+            best = std::max(best, n / (now() - t0) / 1e9);
+        }
+        printf("{\"kind\": \"%s\", \"GiB\": %.2f, \"pieces\": %llu, \"lib_GBps\": %.2f}\n", kind,
+               n / double(1ull << 30), (unsigned long long)np, best);
+        fflush(stdout);
+        if (pinned) krk_host_free(p);
+        else free(p);
+    }
     hipFree(dev);
     return 0;
 }
