@@ -783,7 +783,7 @@ def c4_end_to_end(D, T, arena, want_sums, P, world):
            **({"blob_bytes_requested": L, "capped_by": "host memory per rank"} if Le < L else {}),
            "ceiling": host_crc_ceiling(D)}
     for name, buf in (("pinned", pin.a), ("pageable", pg)):
-        for _ in range(2):  # warm: a pinned call splits, the next runs host-only, then the faster one
+        for _ in range(3):  # warm: two pinned calls split (the first sets up), one runs host-only, then the faster
             D.piece_sums_host([buf], P)
         el, ts, r = timed_passes(T, lambda: D.piece_sums_host([buf], P))
         g, h, frac = D.crc_host_split()

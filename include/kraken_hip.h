@@ -81,8 +81,8 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
  * bytes (krk_host_alloc) are DMA'd straight into the device windows and the GPU takes a
  * share learned from the previous calls' measured rates of both sides (first call: the
  * planner rates' model, at most 10 %) -- or none, when host-only calls measured faster
- * than split ones (the second call runs host-only to find out; every 16th call re-measures
- * the other choice).  Pageable bytes stay on the host (a staging copy per byte costs more
+ * than split ones (after two split calls -- the first sets up the staging windows -- one
+ * runs host-only to find out; every 16th call re-measures the other choice).  Pageable bytes stay on the host (a staging copy per byte costs more
  * than the GPU saves).  KRK_CRC_GPU_FRACTION forces the share.  This returns the calling
  * thread's last split in bytes and the share the next pinned batch of its device will use
  * (0 while host-only wins, -1 until learned). */

@@ -466,12 +466,14 @@ struct PieceTask {
 //    of host-only calls.  The DMA reads share host memory with the CRC threads, so a balanced
 //    split can still lose to the host alone (C4's 20 GiB pinned blob on one box: 131 GB/s at
 //    the balanced 27 % against 260 host-only; f1verify on another: 282 at 10 % against 228).
-//    So the second call runs host-only, later calls take whichever measured faster, and
-//    every 16th call re-measures the other one.
+//    So the first split call sets up the windows (not a sample), the second measures the
+//    split, the next runs host-only, later calls take whichever measured faster, and every
+//    16th call re-measures the other one.
 struct CrcSplit {
     std::mutex mu;
     double frac = -1, r_split = 0, r_host = 0;
     uint64_t calls = 0;
+    bool warm = false;  // a split call has run: the staging windows exist (the first pays their set-up)
     bool use_split() const { return r_host <= 0 || r_split >= r_host; }
 };
 static CrcSplit g_crc_split[kMaxDevs];
@@ -595,7 +597,9 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     if (!r && all_pinned && !forced && bytes >= (128u << 20) && call_s > 0) {
         std::lock_guard<std::mutex> g(cs.mu);
         auto ema = [](double& x, double v) { x = x > 0 ? 0.5 * x + 0.5 * v : v; };
-        if (gbytes > 0) {
+        if (gbytes > 0 && !cs.warm) {
+            cs.warm = true;  // not a sample: this call allocated and pinned the windows
+        } else if (gbytes > 0) {
             ema(cs.r_split, bytes / call_s);
             if (gbytes >= (64u << 20) && hbytes >= (64u << 20) && gpu_s > 0 && host_s > 0) {
                 // the split where both sides would have ended together at the rates just measured

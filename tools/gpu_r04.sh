@@ -32,6 +32,8 @@ for step in "$@"; do
     bench_f1) run bench_f1verify 600 python bench.py --workload f1verify ;;
     verify_tests) run pytest_verify 400 $PYT tests/test_gpu_agent_verify.py tests/test_gpu_files.py -k "split or placements or verify" ;;
     bench_c3) run bench_c3 900 python bench.py --workload c3 ;;
+    bench_c5) run bench_c5 300 python bench.py --workload c5 ;;
+    bench_c5regen_digest) run bench_c5regen_digest 400 python bench.py --workload c5regen_digest ;;
     pinned_ab) run pinned_ab 400 python tools/pinned_ab.py 48 192 ;;
     e2e_w2 | e2e_w3 | e2e_w4) run $step 300 env KRK_STAGING_WINDOWS=${step#e2e_w} python bench.py --e2e-only --no-cpu-baseline ;;
     # rocprofv3 on the end-to-end legs (kernel trace + copy trace; PMC passes on their own runs)

@@ -89,6 +89,24 @@ double h2d_rate(const uint8_t* p, size_t n, void* dev, hipStream_t s) {
 int main(int argc, char** argv) {
     const size_t n = (size_t)(argc > 1 ? atof(argv[1]) : 4.0) * (1ull << 30);
     const int T = argc > 2 ? atoi(argv[2]) : 16;
+    if (argc > 3 && !strncmp(argv[3], "bind", 4)) {  // "bindN": every thread on node N's CPUs
+        std::ifstream f("/sys/devices/system/node/node" + std::string(argv[3] + 4) + "/cpulist");
+        std::string list;
+        std::getline(f, list);
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        for (size_t q = 0; q < list.size();) {
+            size_t e = list.find(',', q);
+            if (e == std::string::npos) e = list.size();
+            const std::string r = list.substr(q, e - q);
+            const size_t d = r.find('-');
+            const int a = atoi(r.c_str()), b = d == std::string::npos ? a : atoi(r.c_str() + d + 1);
+            for (int c = a; c <= b; ++c) CPU_SET(c, &cs);
+            q = e + 1;
+        }
+        sched_setaffinity(0, sizeof cs, &cs);
+        printf("{\"bound_to\": \"%s\", \"cpus\": %d}\n", list.c_str(), CPU_COUNT(&cs));
+    }
     if (krk_set_device(0) != KRK_OK) {
         fprintf(stderr, "no device: %s\n", krk_last_error());
         return 1;
