@@ -636,6 +636,13 @@ def run_verify(a, D, T, rank, world, res):
     roof["note"] = ("achieved = the GPU's share of a step's bytes (split.gpu_bytes) per launch / average launch time; "
                     "that share goes up by DMA in pinned windows, one CRC launch per window, so the call is bounded "
                     "by the host link and the host threads' PCLMUL rate, not by the kernel")
+    if not crc_n:  # the split measured host-only faster: the host threads are the whole call
+        cap = host_cores() * rates["host_crc_bps"] / 1e9
+        v = world * bytes_rank * a.steps / elapsed / 1e9
+        roof = {"kernel": None, "bound": "host PCLMUL threads", "achieved": round(v, 3), "peak": round(cap, 3),
+                "unit": "GB/s", "frac": round(v / cap, 4) if cap else None, "traffic": None,
+                "note": "no byte went to the GPU in the timed steps (the learned split measured host-only faster, "
+                        "DESIGN.md 4.5); peak = the CPU budget's threads x one thread's measured PCLMUL rate"}
     res.update({"metric": "agent piece-verify GB/s (host pieces, end to end)",
                 "value": round(world * bytes_rank * a.steps / elapsed / 1e9, 3), "unit": "GB/s", "steps": a.steps,
                 "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
