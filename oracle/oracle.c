@@ -11,7 +11,9 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <fcntl.h>
 #include <pthread.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -778,6 +780,65 @@ double orc_baseline_run_lazy(const uint64_t* blob_idx, const uint64_t* lengths, 
     for (int i = 0; i < n_threads; i++) { pthread_join(th[i], NULL); busy += la[i].busy; }
     free(la); free(th); free(J.bufs);
     return busy;
+}
+
+/* The reference's Generate over cache FILES (lib/metainfogen/generator.go:41-58 ->
+ * core.NewMetaInfo(d, blob, P) -> calcPieceSums, core/metainfo.go:157-179): per piece,
+ * io.CopyN(crc32 hasher, file, P), i.e. io.Copy through a LimitReader with its 32 KiB
+ * buffer -- read(2) calls of at most 32 KiB, each folded into the piece's CRC (PCLMUL).
+ * n_threads workers take whole files in turn (the origin regenerates many blobs at once).
+ * Returns wall seconds; -1 on an open/read failure (a short file: the reference's
+ * "unexpected EOF"). */
+typedef struct {
+    const char* const* paths; const uint64_t* lengths; uint64_t n; int64_t piece_len;
+    uint32_t* sums; const uint64_t* sums_off; uint64_t next; int failed;
+} files_job;
+
+static void* files_worker(void* a) {
+    files_job* F = (files_job*)a;
+    const uint64_t CH = 32768; /* io.Copy's 32 KiB buffer */
+    uint8_t* buf = (uint8_t*)malloc(CH);
+    for (;;) {
+        uint64_t b = __atomic_fetch_add(&F->next, 1, __ATOMIC_RELAXED);
+        if (b >= F->n) break;
+        int fd = open(F->paths[b], O_RDONLY);
+        if (fd < 0) { F->failed = 1; continue; }
+        uint64_t L = F->lengths[b], P = (uint64_t)F->piece_len, off = 0, k = 0;
+        while (off < L) {
+            uint64_t n = L - off < P ? L - off : P, got = 0;
+            uint32_t crc = 0;
+            while (got < n) {
+                uint64_t want = n - got < CH ? n - got : CH;
+                ssize_t r = read(fd, buf, want);
+                if (r <= 0) { F->failed = 1; break; }
+                crc = orc_crc32_update_clmul(crc, buf, (uint64_t)r);
+                got += (uint64_t)r;
+            }
+            if (got < n) break;
+            if (F->sums) F->sums[F->sums_off[b] + k] = crc;
+            k++;
+            off += n;
+        }
+        close(fd);
+    }
+    free(buf);
+    return NULL;
+}
+
+double orc_baseline_files(const char* const* paths, const uint64_t* lengths, uint64_t n, int64_t piece_len,
+                          int n_threads, uint32_t* sums_out, const uint64_t* sums_off) {
+    if (n_threads < 1) n_threads = 1;
+    files_job F;
+    memset(&F, 0, sizeof F);
+    F.paths = paths; F.lengths = lengths; F.n = n; F.piece_len = piece_len;
+    F.sums = sums_out; F.sums_off = sums_off;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    double t0 = now_s();
+    for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, files_worker, &F);
+    for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
+    double t1 = now_s();
+    free(th);
+    return F.failed ? -1.0 : t1 - t0;
 }
 
 typedef struct {

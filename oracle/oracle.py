@@ -54,6 +54,7 @@ def _load() -> C.CDLL:
         "orc_synth_fill": (None, [C.c_uint64, C.c_uint64, u8p, C.c_uint64, C.c_int]),
         "orc_baseline_run": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_uint64, u8p, u32p, u64p]),
+        "orc_baseline_files": (C.c_double, [C.POINTER(C.c_char_p), u64p, C.c_uint64, C.c_int64, C.c_int, u32p, u64p]),
         "orc_baseline_run_lazy": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
                                                u8p, u32p, u64p]),
         "orc_baseline_hrw": (C.c_double, [u8p, C.c_uint64, C.c_char_p, u64p, C.c_uint32, u8p,
@@ -265,6 +266,23 @@ def baseline_run_lazy(blob_idx, lengths, piece_length: int, threads: int, passes
     busy = lib().orc_baseline_run_lazy(_ptr(bi, C.c_uint64), _ptr(ln, C.c_uint64), len(bi), piece_length, threads,
                                        passes, _ptr(dg, C.c_uint8), _ptr(sums, C.c_uint32), _ptr(off, C.c_uint64))
     return busy, dg, (sums, off)
+
+
+def baseline_files(paths, lengths, piece_length: int, threads: int):
+    """orc_baseline_files: the reference's Generate over cache files (calcPieceSums over
+    the file reader, 32 KiB reads) on `threads` threads.  Returns (seconds, sums, offsets)."""
+    n = len(paths)
+    enc = (C.c_char_p * max(n, 1))(*[p.encode() if isinstance(p, str) else p for p in paths])
+    ln = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+    npieces = [(int(l) + piece_length - 1) // piece_length for l in ln]
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(npieces)
+    sums = np.zeros(max(int(off[-1]), 1), dtype=np.uint32)
+    t = lib().orc_baseline_files(enc, _ptr(ln, C.c_uint64), n, piece_length, threads, _ptr(sums, C.c_uint32),
+                                 _ptr(off, C.c_uint64))
+    if t < 0:
+        raise OSError("orc_baseline_files: a file could not be read to its length")
+    return t, sums, off
 
 
 def baseline_hrw(digests: np.ndarray, labels, healthy, max_replica: int, threads: int):

@@ -134,3 +134,22 @@ def test_baseline_runner_outputs(orc):
         assert bytes(dg[i]) == hashlib.sha256(data.tobytes()).digest()
         ref = orc.calc_piece_sums(data, 1 << 20)[1]
         assert sums[int(off[i]):int(off[i]) + len(ref)].tolist() == ref.tolist()
+
+
+def test_baseline_files_matches_zlib(orc, tmp_path):
+    """The files CPU baseline (the reference's Generate over cache files: calcPieceSums over
+    the file reader in 32 KiB reads) gives zlib's piece sums, and fails on a short file."""
+    import zlib
+    rng = np.random.default_rng(5)
+    datas = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in (0, 1, 32769, (1 << 20) + 3, 5 << 20)]
+    paths = []
+    for i, x in enumerate(datas):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(x)
+        paths.append(str(p))
+    P = 1 << 20
+    _, sums, off = orc.baseline_files(paths, [len(x) for x in datas], P, 3)
+    for i, x in enumerate(datas):
+        assert list(sums[int(off[i]):int(off[i + 1])]) == [zlib.crc32(x[k:k + P]) for k in range(0, len(x), P)]
+    with pytest.raises(OSError):
+        orc.baseline_files(paths[-1:], [len(datas[-1]) + 1], P, 1)
