@@ -4,7 +4,9 @@
 * ``Generator.Generate``: lib/metainfogen/generator.go:40-58 (stat -> piece length
   -> NewMetaInfo over the cache file -> persist the _torrentmeta sidecar)
 * ``Generator.GenerateBatch``: the batch form used for whole-CAS regeneration
-  (SURVEY.md §8(f) row 2): one GPU pass over many cache files.
+  (SURVEY.md §8(f) row 2): one pass over many cache files (krk_piece_sums_files).
+* ``Generator.VerifyAndGenerateBatch`` / ``VerifyAndGenerateUploads``: upload verification
+  fused with Generate, over upload bytes or the upload files.
 
 The CAS store itself (lib/store) is out of scope; ``DirCAS`` is a minimal
 stand-in exposing the three calls Generate makes.
@@ -90,6 +92,16 @@ class DirCAS:
         with open(os.path.join(self._dir(d.Hex()), "data"), "wb") as f:
             f.write(memoryview(data))
         return d
+
+    def MoveUploadFileToCache(self, upload_path: str, hex_: str) -> None:
+        """CAStore.MoveUploadFileToCache (origin/blobserver/uploader.go:98 commit): the
+        verified upload file renamed into the cache; FileExistsError when the blob is
+        already cached (the uploader's 409)."""
+        dst = os.path.join(self._dir(hex_), "data")
+        os.makedirs(self._dir(hex_), exist_ok=True)
+        if os.path.exists(dst):
+            raise FileExistsError(dst)
+        os.replace(upload_path, dst)
 
     def WriteCacheFile(self, data: bytes) -> core.Digest:
         d = core.NewDigester().FromBytes(data)
@@ -226,7 +238,44 @@ class Generator:
                 continue
             d = self.cas.WriteCacheFileAs(want, x)
             out.append((d, pl, s.copy() if s.size else None, int(x.size)))
-        # the verified blobs' InfoHashes in one batched call
+        return self._commit_metainfo(out)
+
+    def VerifyAndGenerateUploads(self, uploads):
+        """The same from the upload FILES, as the origin holds them (uploader.verify reads
+        the upload file, origin/blobserver/uploader.go:74-94; commit moves it into the
+        cache, :96-105; Generate re-reads the cache file, generator.go:41-58): each file is
+        read once by krk_metainfo_digest_files and that read yields the digest AND the piece
+        sums.  uploads: [(core.Digest expected, upload file path)].  A file that cannot be
+        read fails the batch with uploader.verify's prefixes ("get upload file: ...",
+        "calculate digest: read blob: <path>: ..."); a digest mismatch is that upload's
+        ValueError; verified files are moved into the CAS with their _torrentmeta.  Returns
+        [MetaInfo | ValueError] in input order."""
+        from . import device as D
+        from ._capi import KrakenError
+        paths, sizes = [], []
+        for _, p in uploads:
+            try:
+                sizes.append(os.stat(p).st_size)
+            except OSError as e:
+                raise IOError(f"get upload file: {e}") from None
+            paths.append(p)
+        pls = [self.pieceLengthConfig.get(n) for n in sizes]
+        try:
+            sums, dg = D.metainfo_digest_files(paths, sizes, pls)
+        except KrakenError as e:
+            raise IOError(f"calculate digest: {e}") from None
+        out = []
+        for (want, p), n, pl, s, g in zip(uploads, sizes, pls, sums, dg):
+            got = core.NewSHA256DigestFromHex(bytes(g).hex())
+            if got != want:
+                out.append(ValueError(f"computed digest {got.String()} doesn't match parameter {want.String()}"))
+                continue
+            self.cas.MoveUploadFileToCache(p, want.Hex())
+            out.append((want, pl, s.copy() if s.size else None, int(n)))
+        return self._commit_metainfo(out)
+
+    def _commit_metainfo(self, out):
+        """The verified uploads' InfoHashes in one batched call and their sidecars."""
         ok = [k for k, o in enumerate(out) if not isinstance(o, ValueError)]
         if ok:
             flat = [out[k][2] for k in ok if out[k][2] is not None]

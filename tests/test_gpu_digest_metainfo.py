@@ -270,6 +270,38 @@ def test_verify_and_generate_batch(gpu, orc, tmp_path):
         assert open(os.path.join(cas._dir(d.Hex()), "data"), "rb").read() == b
 
 
+def test_verify_and_generate_uploads_from_files(gpu, orc, tmp_path):
+    """The files form (krk_metainfo_digest_files: one read of each upload file feeds the
+    digest and the piece sums): a corrupted upload is rejected with uploader.verify's
+    message and stays in the upload dir, the others are moved into the CAS with
+    _torrentmeta byte-identical to the two-pass path; an unreadable upload fails the batch
+    with the reference's prefixes."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path / "cas"))
+    up = tmp_path / "upload"
+    up.mkdir()
+    g = metainfogen.New({0: 1 << 20, 4 << 20: 4 << 20}, cas)
+    blobs = [os.urandom(n) for n in (0, 5, 1 << 20, (4 << 20) + 7, 3_000_001)]
+    want = [core.NewSHA256DigestFromHex(hashlib.sha256(b).hexdigest()) for b in blobs]
+    bad = bytearray(blobs[3])
+    bad[777] ^= 4
+    ups = []
+    for i, b in enumerate(blobs + [bytes(bad)]):
+        p = up / f"u{i}"
+        p.write_bytes(b)
+        ups.append((want[i] if i < len(blobs) else want[3], str(p)))
+    res = g.VerifyAndGenerateUploads(ups)
+    assert isinstance(res[-1], ValueError) and "doesn't match parameter" in str(res[-1])
+    assert os.path.exists(ups[-1][1])  # the rejected upload is not committed
+    for mi, d, b, (_, p) in zip(res[:-1], want, blobs, ups):
+        pl = 1 << 20 if len(b) < 4 << 20 else 4 << 20
+        assert bytes(mi.InfoHash()) == orc.info_hash(pl, orc.calc_piece_sums(b, pl)[1], d.Hex(), len(b))
+        assert open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read() == core.NewMetaInfo(d, b, pl).Serialize()
+        assert open(os.path.join(cas._dir(d.Hex()), "data"), "rb").read() == b and not os.path.exists(p)
+    with pytest.raises(IOError, match="get upload file: "):
+        g.VerifyAndGenerateUploads([(want[1], str(up / "missing"))])
+
+
 def _go_json(pl, sums, name, length):
     """encoding/json of metaInfoJSON{info} (core/metainfo.go:125-134), written out
     independently of core.MetaInfo.Serialize: declared field order, compact, nil
