@@ -1439,6 +1439,18 @@ def run_files(a, D, T, rank, world, res):
             ok = ok and bytes(dg_f[i]) == hashlib.sha256(x.tobytes()).digest() and np.array_equal(
                 sums_f[i], O.calc_piece_sums(x, P)[1])
         del pins, datas
+        cb = None
+        if rank == 0 and not a.no_cpu_baseline:
+            # the reference's two reads of every file on the CPU budget: uploader.verify's
+            # Digester over the upload file, then Generate's calcPieceSums over the cache file
+            t_c, s_c, off_c, dg_c = O.baseline_files(paths, lens, P, host_cores(), passes=3)
+            same_c = bool(np.array_equal(dg_c, dg_f)) and all(
+                np.array_equal(s_c[int(off_c[i]):int(off_c[i + 1])], sums_f[i]) for i in range(n))
+            cb = {"value": round(total / t_c / 1e9, 3), "unit": "GB/s", "cores": host_cores(), "kind": "port",
+                  "seconds": round(t_c, 3), "outputs_match_gpu": same_c,
+                  "sample": f"all {n} files of the pass (page cache warm): Digester.FromReader then calcPieceSums "
+                            "over each file, 32 KiB reads, SHA-NI and PCLMUL, one file per thread "
+                            "(oracle/oracle.c orc_baseline_files)"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
     res.update({"metric": "upload verify + metainfo from files, GB/s (end-to-end, host link)",
@@ -1460,6 +1472,8 @@ def run_files(a, D, T, rank, world, res):
                                     "host_blobs": st_a["host_blobs"],
                                     "what": "krk_metainfo_digest_files with the library's default host offload (AUTO)"},
                 "outputs_equal_across_paths": bool(same), "oracle_sampled_match": bool(ok)})
+    if cb:
+        res["cpu_baseline"] = cb
 
 
 def run_engine(a, D, T, rank, world, res):

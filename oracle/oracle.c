@@ -782,17 +782,42 @@ double orc_baseline_run_lazy(const uint64_t* blob_idx, const uint64_t* lengths, 
     return busy;
 }
 
-/* The reference's Generate over cache FILES (lib/metainfogen/generator.go:41-58 ->
- * core.NewMetaInfo(d, blob, P) -> calcPieceSums, core/metainfo.go:157-179): per piece,
- * io.CopyN(crc32 hasher, file, P), i.e. io.Copy through a LimitReader with its 32 KiB
- * buffer -- read(2) calls of at most 32 KiB, each folded into the piece's CRC (PCLMUL).
- * n_threads workers take whole files in turn (the origin regenerates many blobs at once).
- * Returns wall seconds; -1 on an open/read failure (a short file: the reference's
- * "unexpected EOF"). */
+/* The reference's passes over CAS FILES, n_threads workers taking whole files in turn (the
+ * origin verifies and regenerates many blobs at once).  passes & 2 -- Generate over the
+ * cache file (lib/metainfogen/generator.go:41-58 -> core.NewMetaInfo(d, blob, P) ->
+ * calcPieceSums, core/metainfo.go:157-179): per piece, io.CopyN(crc32 hasher, file, P), i.e.
+ * io.Copy through a LimitReader with its 32 KiB buffer -- read(2) calls of at most 32 KiB,
+ * each folded into the piece's CRC (PCLMUL).  passes & 1 -- the upload verify before it
+ * (files_sha).  Returns wall seconds; -1 on an open/read failure (a short file: the
+ * reference's "unexpected EOF"). */
 typedef struct {
     const char* const* paths; const uint64_t* lengths; uint64_t n; int64_t piece_len;
-    uint32_t* sums; const uint64_t* sums_off; uint64_t next; int failed;
+    uint32_t* sums; const uint64_t* sums_off; uint8_t* digests; int passes; uint64_t next; int failed;
 } files_job;
+
+/* Pass 1 (passes & 1): the upload verify -- Digester.FromReader over the upload file
+ * (origin/blobserver/uploader.go:74-94 -> core/digester.go: io.Copy into sha256), 32 KiB
+ * reads, whole reads through the SHA-NI block function. */
+static int files_sha(int fd, uint64_t L, uint8_t* buf, uint64_t CH, uint8_t out[32]) {
+    orc_sha256_ctx c;
+    orc_sha256_init(&c);
+    uint64_t got = 0;
+    const int ni = orc_have_shani();
+    while (got < L) {
+        uint64_t want = L - got < CH ? L - got : CH;
+        ssize_t r = read(fd, buf, want);
+        if (r <= 0) return -1;
+        if (ni && c.nbuf == 0 && r % 64 == 0) {
+            sha256_blocks_shani(c.h, buf, (uint64_t)r / 64);
+            c.nbytes += (uint64_t)r;
+        } else {
+            orc_sha256_update(&c, buf, (uint64_t)r);
+        }
+        got += (uint64_t)r;
+    }
+    orc_sha256_sum(&c, out);
+    return 0;
+}
 
 static void* files_worker(void* a) {
     files_job* F = (files_job*)a;
@@ -801,6 +826,15 @@ static void* files_worker(void* a) {
     for (;;) {
         uint64_t b = __atomic_fetch_add(&F->next, 1, __ATOMIC_RELAXED);
         if (b >= F->n) break;
+        if (F->passes & 1) {
+            int fd = open(F->paths[b], O_RDONLY);
+            uint8_t dg[32];
+            if (fd < 0 || files_sha(fd, F->lengths[b], buf, CH, dg) != 0) F->failed = 1;
+            else if (F->digests) memcpy(F->digests + 32 * b, dg, 32);
+            if (fd >= 0) close(fd);
+        }
+        if (!(F->passes & 2)) continue;
+        /* pass 2: Generate re-reads the committed cache file for the piece sums */
         int fd = open(F->paths[b], O_RDONLY);
         if (fd < 0) { F->failed = 1; continue; }
         uint64_t L = F->lengths[b], P = (uint64_t)F->piece_len, off = 0, k = 0;
@@ -826,12 +860,13 @@ static void* files_worker(void* a) {
 }
 
 double orc_baseline_files(const char* const* paths, const uint64_t* lengths, uint64_t n, int64_t piece_len,
-                          int n_threads, uint32_t* sums_out, const uint64_t* sums_off) {
+                          int n_threads, int passes, uint32_t* sums_out, const uint64_t* sums_off,
+                          uint8_t* digests_out) {
     if (n_threads < 1) n_threads = 1;
     files_job F;
     memset(&F, 0, sizeof F);
     F.paths = paths; F.lengths = lengths; F.n = n; F.piece_len = piece_len;
-    F.sums = sums_out; F.sums_off = sums_off;
+    F.sums = sums_out; F.sums_off = sums_off; F.digests = digests_out; F.passes = passes ? passes : 2;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)n_threads);
     double t0 = now_s();
     for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, files_worker, &F);

@@ -100,9 +100,10 @@ double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint6
 /* Bounded-memory form (one buffer per thread; each blob materialised untimed just
  * before its passes): returns the SUMMED busy seconds of the threads, so the
  * sustained rate is bytes / (busy / n_threads).  Always the fast (SHA-NI/PCLMUL) path. */
-/* Generate over cache files, the reference's way: 32 KiB reads per piece (io.CopyN). */
+/* Upload verify (passes & 1) and Generate (passes & 2) over files, the reference's way (32 KiB reads). */
 double orc_baseline_files(const char* const* paths, const uint64_t* lengths, uint64_t n, int64_t piece_len,
-                          int n_threads, uint32_t* sums_out, const uint64_t* sums_off);
+                          int n_threads, int passes, uint32_t* sums_out, const uint64_t* sums_off,
+                          uint8_t* digests_out);
 double orc_baseline_run_lazy(const uint64_t* blob_idx, const uint64_t* lengths, uint64_t n_blobs,
                              int64_t piece_len, int n_threads, int passes, uint8_t* digests_out,
                              uint32_t* sums_out, const uint64_t* sums_off);

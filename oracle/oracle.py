@@ -54,7 +54,8 @@ def _load() -> C.CDLL:
         "orc_synth_fill": (None, [C.c_uint64, C.c_uint64, u8p, C.c_uint64, C.c_int]),
         "orc_baseline_run": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_uint64, u8p, u32p, u64p]),
-        "orc_baseline_files": (C.c_double, [C.POINTER(C.c_char_p), u64p, C.c_uint64, C.c_int64, C.c_int, u32p, u64p]),
+        "orc_baseline_files": (C.c_double, [C.POINTER(C.c_char_p), u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
+                                            u32p, u64p, u8p]),
         "orc_baseline_run_lazy": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
                                                u8p, u32p, u64p]),
         "orc_baseline_hrw": (C.c_double, [u8p, C.c_uint64, C.c_char_p, u64p, C.c_uint32, u8p,
@@ -268,9 +269,11 @@ def baseline_run_lazy(blob_idx, lengths, piece_length: int, threads: int, passes
     return busy, dg, (sums, off)
 
 
-def baseline_files(paths, lengths, piece_length: int, threads: int):
-    """orc_baseline_files: the reference's Generate over cache files (calcPieceSums over
-    the file reader, 32 KiB reads) on `threads` threads.  Returns (seconds, sums, offsets)."""
+def baseline_files(paths, lengths, piece_length: int, threads: int, passes: int = 2):
+    """orc_baseline_files: the reference's passes over CAS files on `threads` threads --
+    passes & 1 the upload verify (Digester over the file, 32 KiB reads), passes & 2 Generate
+    (calcPieceSums over the file reader).  Returns (seconds, sums, offsets), plus the
+    digests when passes & 1."""
     n = len(paths)
     enc = (C.c_char_p * max(n, 1))(*[p.encode() if isinstance(p, str) else p for p in paths])
     ln = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
@@ -278,11 +281,12 @@ def baseline_files(paths, lengths, piece_length: int, threads: int):
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(npieces)
     sums = np.zeros(max(int(off[-1]), 1), dtype=np.uint32)
-    t = lib().orc_baseline_files(enc, _ptr(ln, C.c_uint64), n, piece_length, threads, _ptr(sums, C.c_uint32),
-                                 _ptr(off, C.c_uint64))
+    dg = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    t = lib().orc_baseline_files(enc, _ptr(ln, C.c_uint64), n, piece_length, threads, passes,
+                                 _ptr(sums, C.c_uint32), _ptr(off, C.c_uint64), _ptr(dg, C.c_uint8))
     if t < 0:
         raise OSError("orc_baseline_files: a file could not be read to its length")
-    return t, sums, off
+    return (t, sums, off, dg[:n]) if passes & 1 else (t, sums, off)
 
 
 def baseline_hrw(digests: np.ndarray, labels, healthy, max_replica: int, threads: int):

@@ -153,3 +153,7 @@ def test_baseline_files_matches_zlib(orc, tmp_path):
         assert list(sums[int(off[i]):int(off[i + 1])]) == [zlib.crc32(x[k:k + P]) for k in range(0, len(x), P)]
     with pytest.raises(OSError):
         orc.baseline_files(paths[-1:], [len(datas[-1]) + 1], P, 1)
+    # with the upload verify pass: the digests are hashlib's
+    _, sums2, _, dg = orc.baseline_files(paths, [len(x) for x in datas], P, 2, passes=3)
+    assert np.array_equal(sums2, sums)
+    assert [bytes(d) for d in dg] == [hashlib.sha256(x).digest() for x in datas]
