@@ -8,6 +8,7 @@ import pytest
 
 from kraken_amd import hashring, hrw
 from kraken_amd import device as D
+from kraken_amd._capi import check, lib
 
 pytestmark = pytest.mark.gpu
 
@@ -175,6 +176,37 @@ def test_ring_locations_u8_dev_equals_int32_path(gpu, orc, n_nodes, max_replica)
         key = bytes(digests[i, :2]).hex()
         want = orc.ring_locations(orc.hrw_ordered(key, labels, [100] * n_nodes), healthy, max_replica)
         assert a8[i, : len(want)].tolist() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_replica", [1, 3, 5])
+def test_ring_locations_u8_dev_offsets_and_tails(gpu, max_replica):
+    """The compact gather runs four digests a thread over dword-aligned outputs and the
+    tail (n % 4) one a thread; outputs at odd addresses take the one-a-thread kernel.
+    Every layout gives the int32 path's lists."""
+    import ctypes as C
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(16)]
+    healthy = np.ones(16, dtype=np.uint8)
+    healthy[[2, 9]] = 0
+    rng = np.random.default_rng(77 + max_replica)
+    for n in (1, 3, 4, 5, 1023, 4097):
+        digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        dbuf = D.DeviceBuffer(n * 32)
+        dbuf.from_host(digests.reshape(-1))
+        l32, c32 = D.DeviceBuffer(n * max_replica * 4), D.DeviceBuffer(n)
+        D.ring_locations_dev(dbuf, n, labels, healthy, max_replica, l32, c32)
+        D.synchronize()
+        want = np.where(l32.to_host(np.int32, n * max_replica) < 0, 255,
+                        l32.to_host(np.int32, n * max_replica)).astype(np.uint8)
+        wc = c32.to_host(np.uint8, n)
+        for shift in (0, 1, 3):
+            lb, cb = D.DeviceBuffer(n * max_replica + 8), D.DeviceBuffer(n + 8)
+            s, keep = D.nodes_struct(labels, [100] * 16)
+            check(lib.krk_ring_locations_u8_dev(dbuf.ptr, n, C.byref(s), healthy.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                 max_replica, lb.ptr + shift, cb.ptr + shift, None))
+            D.synchronize()
+            assert np.array_equal(lb.to_host(np.uint8, n * max_replica, shift), want), (n, shift)
+            assert np.array_equal(cb.to_host(np.uint8, n, shift), wc), (n, shift)
 
 
 @pytest.mark.gpu
