@@ -222,63 +222,14 @@ __global__ void shard_gather_kernel(const uint8_t* digests32, uint64_t n, const 
     counts[i] = tc[shard];
 }
 
-// Compact owner lists, four digests a thread: the four ShardIDs (two bytes of each 32-byte
-// record), their rows of the L2-resident table, and the outputs written as whole dwords --
-// 4 x row_out owner bytes (row_out dword stores) and the 4 counts (one).  The one-digest
-// kernel above spends a byte store per owner and a wave per 64 digests; this one a quarter
-// of the waves and dword stores.  Needs dword-aligned outputs and n % 4 == 0 (the caller
-// runs the tail through the one-digest kernel).
-__global__ void shard_gather_u8x4_kernel(const uint8_t* digests32, uint64_t n4, const int32_t* tl,
-                                         const uint8_t* tc, uint32_t row_out, uint32_t* locs, uint32_t* counts) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n4) return;
-    const uint8_t* d = digests32 + 128 * t;
-    uint32_t shard[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint16_t v = *reinterpret_cast<const uint16_t*>(d + 32 * j);  // bytes 0, 1 of record j
-        shard[j] = (uint32_t)(v & 0xFF) << 8 | (v >> 8);
-    }
-    // owner bytes of the 4 digests in output order, packed 4 to a dword
-    uint32_t w = 0;
-    uint32_t* out = locs + t * row_out;
-    uint32_t k = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        for (uint32_t q = 0; q < row_out; ++q) {
-            const int32_t v = tl[(uint64_t)shard[j] * row_out + q];
-            w |= (uint32_t)(v < 0 ? 0xFF : (uint8_t)v) << (8 * (k & 3));
-            if ((++k & 3) == 0) {
-                out[k / 4 - 1] = w;
-                w = 0;
-            }
-        }
-    counts[t] = (uint32_t)tc[shard[0]] | (uint32_t)tc[shard[1]] << 8 | (uint32_t)tc[shard[2]] << 16 |
-                (uint32_t)tc[shard[3]] << 24;
-}
-
 template <typename T>
 static hipError_t launch_gather(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
                                 const uint8_t* table_counts, uint32_t row_out, T* locs, uint8_t* counts,
                                 hipStream_t s) {
     if (!n) return hipSuccess;
     if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
-    uint64_t done = 0;
-    if constexpr (sizeof(T) == 1) {
-        const bool aligned = reinterpret_cast<uintptr_t>(locs) % 4 == 0 && reinterpret_cast<uintptr_t>(counts) % 4 == 0 &&
-                             reinterpret_cast<uintptr_t>(digests32) % 2 == 0;
-        const uint64_t n4 = aligned ? n / 4 : 0;
-        if (n4) {
-            hipLaunchKernelGGL(shard_gather_u8x4_kernel, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, s, digests32,
-                               n4, table_locs, table_counts, row_out, reinterpret_cast<uint32_t*>(locs),
-                               reinterpret_cast<uint32_t*>(counts));
-            done = 4 * n4;
-        }
-    }
-    if (done < n)  // the tail (or every digest, for int32 rows or unaligned outputs)
-        hipLaunchKernelGGL(shard_gather_kernel<T>, dim3((uint32_t)((n - done + 255) / 256)), dim3(256), 0, s,
-                           digests32 + 32 * done, n - done, table_locs, table_counts, row_out, locs + done * row_out,
-                           counts + done);
+    hipLaunchKernelGGL(shard_gather_kernel<T>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       digests32, n, table_locs, table_counts, row_out, locs, counts);
     return hipGetLastError();
 }
 

@@ -181,9 +181,8 @@ def test_ring_locations_u8_dev_equals_int32_path(gpu, orc, n_nodes, max_replica)
 @pytest.mark.gpu
 @pytest.mark.parametrize("max_replica", [1, 3, 5])
 def test_ring_locations_u8_dev_offsets_and_tails(gpu, max_replica):
-    """The compact gather runs four digests a thread over dword-aligned outputs and the
-    tail (n % 4) one a thread; outputs at odd addresses take the one-a-thread kernel.
-    Every layout gives the int32 path's lists."""
+    """Compact owner lists at any output address and count (byte stores, tails of every
+    length): every layout gives the int32 path's lists."""
     import ctypes as C
     labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(16)]
     healthy = np.ones(16, dtype=np.uint8)
