@@ -1399,6 +1399,7 @@ int stream_submit(krk_piece_stream* s, const uint8_t* src, uint64_t len) {
 void stream_host_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
     const int idle = n >= (2u << 20) && s->P >= (64u << 10) ? host_pool_idle() : 0;
     if (idle <= 0) {  // (small pieces: a span a piece would cost more than it spreads)
+        HostCpuToken tok;
         while (n) {
             const uint64_t take = std::min<uint64_t>(n, s->P - s->in_piece);
             s->crc = host_crc32_update(s->crc, buf, take);

@@ -742,6 +742,14 @@ class HostBatch {
     std::shared_ptr<HostJob> j_;
 };
 int host_pool_idle();  // pool threads idle right now (not yet promised to a batch)
+// Held while a thread runs host hash work: at most host_cpu_budget() such threads at once
+// (host_pool.cpp); re-entrant on one thread.  Pool items take one themselves.
+struct HostCpuToken {
+    HostCpuToken();
+    ~HostCpuToken();
+    HostCpuToken(const HostCpuToken&) = delete;
+    HostCpuToken& operator=(const HostCpuToken&) = delete;
+};
 void host_parallel_for(size_t n, int helpers, std::function<void(size_t)> f);
 // crc(A||B) from crc(A), crc(B), |B| (crc32.Update values).
 uint32_t crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
