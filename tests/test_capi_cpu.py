@@ -506,3 +506,63 @@ def test_piece_sums_host_pageable_needs_no_device():
     exp = np.array([zlib.crc32(d.tobytes()) for d in datas], dtype=np.uint32)
     exp[2] ^= 1
     assert list(agentstorage.verify_pieces(datas, exp)) == [True, True, False, True, True]
+
+
+def test_host_hash_work_concurrent_callers_under_cpu_tokens():
+    """Many concurrent host-placed callers (piece streams, crc32.Update, piece_sums_host)
+    share the CPU tokens (at most the CPU budget hashing at once, host_pool.cpp): no caller
+    deadlocks or starves, every result equals zlib."""
+    import threading
+    import zlib
+    from kraken_amd import device as D
+    rng = np.random.default_rng(61)
+    blob = rng.integers(0, 256, (9 << 20) + 77, dtype=np.uint8)
+    data = blob.tobytes()
+    P = 2 << 20
+    want = [zlib.crc32(data[i:i + P]) for i in range(0, len(data), P)]
+    errors = []
+
+    def stream_worker():
+        try:
+            for _ in range(3):
+                s = C.c_void_p()
+                check(lib.krk_piece_stream_begin_on(_capi.KRK_PLACE_HOST, P, C.byref(s)))
+                try:
+                    for a in range(0, len(data), 1 << 20):
+                        chunk = data[a:a + (1 << 20)]
+                        check(lib.krk_piece_stream_update(s, chunk, len(chunk)))
+                    ns, ln = C.c_uint64(), C.c_uint64()
+                    sums = (C.c_uint32 * len(want))()
+                    check(lib.krk_piece_stream_end(s, sums, len(want), C.byref(ns), C.byref(ln)))
+                    assert list(sums) == want
+                finally:
+                    lib.krk_piece_stream_free(s)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    def update_worker():
+        try:
+            for _ in range(3):
+                out = C.c_uint32()
+                check(lib.krk_crc32_update_on(_capi.KRK_PLACE_HOST, 0, data, len(data), C.byref(out)))
+                assert out.value == zlib.crc32(data)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def batch_worker():
+        try:
+            for _ in range(2):
+                got = D.piece_sums_host([blob, blob[:P + 1]], P)
+                assert [int(x) for x in got[0]] == want
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = ([threading.Thread(target=stream_worker) for _ in range(24)] +
+          [threading.Thread(target=update_worker) for _ in range(8)] +
+          [threading.Thread(target=batch_worker) for _ in range(4)])
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a caller did not finish"
+    assert not errors, errors[:3]
