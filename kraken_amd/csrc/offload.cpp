@@ -536,6 +536,7 @@ void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vecto
     std::atomic<size_t> next{0};
     auto work = [&] {
         for (size_t j; (j = next.fetch_add(1)) < ptrs.size();) {
+            HostCpuToken tok;  // a blob at a time under the process's CPU tokens
             uint32_t h[8];
             memcpy(h, kIV, sizeof h);
             host_sha256_final(h, 0, ptrs[j], lens[j], out + 32 * j);
@@ -564,6 +565,7 @@ void offload_whole_host(const std::vector<const uint8_t*>& ptrs, const std::vect
     std::atomic<size_t> next{0};
     auto work = [&] {
         for (size_t q; (q = next.fetch_add(1)) < tasks.size();) {
+            HostCpuToken tok;  // a task at a time under the process's CPU tokens
             const size_t j = tasks[q].second / 2;
             const uint8_t* p = ptrs[j];
             const uint64_t L = lens[j];
@@ -608,6 +610,7 @@ int offload_whole_files(const std::vector<const char*>& paths, const std::vector
     auto work = [&] {
         std::vector<uint8_t> buf(kChunk);
         for (size_t j; !failed && (j = next.fetch_add(1)) < paths.size();) {
+            HostCpuToken tok;  // a file at a time under the process's CPU tokens
             const int fd = open(paths[j], O_RDONLY | O_CLOEXEC);
             if (fd < 0) {
                 fail(KRK_EIO, std::string("open ") + paths[j] + ": " + strerror(errno));
