@@ -179,7 +179,11 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
 int krk_sha256_dev_on_host(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n, int threads,
                            void* stream, uint8_t* digests_host);
 
-/* Host batch: HOST data pointers; digests_host n*32 bytes.  Synchronous. */
+/* Host batch: HOST data pointers; digests_host n*32 bytes.  Synchronous.  The window
+ * schedule of krk_metainfo_digest_host without the piece CRCs (at most
+ * krk_window_stream_cap blobs live, admitted longest first; page-locked blobs DMA'd
+ * directly), and the planner's blobs hashed in place on host threads under the default
+ * AUTO host offload; krk_windows_last_call reports the call. */
 int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
                     uint8_t* digests_host);
 

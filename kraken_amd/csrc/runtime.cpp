@@ -809,102 +809,6 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
     return r;
 }
 
-int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n, uint8_t* digests_host) {
-    KRK_DEVICE(D);
-    if (!n) return KRK_OK;
-    KRK_CHECK(data_host && lengths && digests_host, KRK_EINVAL, "sha256_host: null argument");
-    const size_t W = window_bytes();
-    // Per-stream chunk per round: the window split over the streams (multiple of 64).
-    uint64_t C = (W / n) & ~uint64_t(63);
-    if (C < 64) C = 64;
-    const size_t cap = std::max<size_t>(W, C * n + 16 * n);
-    StagingLease lease;
-    int r = lease_staging(D, cap, lease);
-    if (r) return r;
-    Pipeline& pl = *lease.p;
-    uint8_t* d_dig = nullptr;
-    uint32_t* d_state = nullptr;
-    DevMem mem;
-    KRK_HIP(mem.alloc(&d_dig, n * 32));
-    KRK_HIP(mem.alloc(&d_state, n * 32));
-    std::vector<uint64_t> off(n, 0);
-    std::vector<char> done(n, 0);
-    hipStream_t cp = D->s_a, ks = D->s_b;
-    uint64_t remaining = n;
-    // SHA-256 host offload (krk_set_sha_host_offload): the longest blobs are hashed in
-    // place on host threads and never cross PCIe.
-    std::vector<uint32_t> host;
-    const int off_t = offload_threads(kOffHostSha);
-    if (off_t > 0) {
-        host = offload_plan(lengths, n, off_t, planner_rates(D), nullptr, nullptr, kOffHostSha);
-        for (uint32_t i : host) {
-            done[i] = 1;
-            --remaining;
-        }
-    }
-    std::vector<uint8_t> host_dig(32 * host.size());
-    std::thread host_th;
-    if (!host.empty())
-        host_th = std::thread([&] {
-            std::vector<const uint8_t*> p(host.size());
-            std::vector<uint64_t> l(host.size());
-            for (size_t j = 0; j < host.size(); ++j) {
-                p[j] = data_host[host[j]];
-                l[j] = lengths[host[j]];
-            }
-            offload_hash_host(p, l, off_t, host_dig.data());
-        });
-    struct Joiner {
-        std::thread& t;
-        ~Joiner() {
-            if (t.joinable()) t.join();
-        }
-    } joiner{host_th};
-    int k = 0;
-    while (!r && remaining) {
-        r = pl.acquire(k);
-        if (r) break;
-        Window& w = pl.w[k];
-        std::vector<ShaJob> jobs;
-        size_t fill = 0;
-        for (uint64_t i = 0; i < n; ++i) {
-            if (done[i]) continue;
-            const uint64_t left = lengths[i] - off[i];
-            const bool fin = left <= C;
-            const uint64_t take = fin ? left : C;
-            if (take) memcpy(w.host + fill, data_host[i] + off[i], take);
-            ShaJob j{};
-            j.ptr = reinterpret_cast<uint64_t>(w.dev + fill);
-            j.len = take;
-            j.prefix = off[i];
-            j.out = (uint32_t)i;
-            j.flags = (fin ? kShaFinal : 0) | (off[i] ? kShaFromState : 0);
-            memcpy(j.h, kIV, sizeof kIV);
-            jobs.push_back(j);
-            off[i] += take;
-            fill += (take + 15) & ~uint64_t(15);
-            if (fin) { done[i] = 1; --remaining; }
-        }
-        if (pl.h2d(k, fill, cp) != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
-            set_error(KRK_EHIP, "sha256_host: staging copy failed");
-            r = KRK_EHIP;
-            break;
-        }
-        r = run_jobs(D, jobs, d_dig, d_state, ks);
-        if (r) break;
-        pl.release(k, 0, ks);
-        k = pl.next(k);
-    }
-    if (!r && hipStreamSynchronize(ks) != hipSuccess) { set_error(KRK_EHIP, "sync failed"); r = KRK_EHIP; }
-    if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error(KRK_EHIP, "digest copy-out failed");
-        r = KRK_EHIP;
-    }
-    if (host_th.joinable()) host_th.join();
-    for (size_t q = 0; q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
-    return r;
-}
-
 static int validate_chunks(const krk_chunk* c, uint64_t n) {
     KRK_CHECK(n == 0 || c, KRK_EINVAL, "chunks is NULL");
     std::unordered_map<uint64_t, uint64_t> seen;

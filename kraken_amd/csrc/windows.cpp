@@ -200,7 +200,7 @@ constexpr size_t kDirectMaxCalls = 64;
 // the last window is queued (the caller synchronises s_main / s_a / s_b).
 int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* plens, const uint64_t* soff,
                  const std::vector<char>& skip, Filler& filler, uint64_t align, uint64_t cap, uint32_t* d_sums,
-                 uint8_t* d_dig, uint32_t* d_state, CallStats* st) {
+                 uint8_t* d_dig, uint32_t* d_state, CallStats* st, bool crc = true) {
     std::vector<uint32_t> blobs;
     for (uint64_t i = 0; i < n; ++i)
         if (!skip[i]) blobs.push_back((uint32_t)i);
@@ -239,7 +239,7 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
             const uint64_t dev = reinterpret_cast<uint64_t>(w.dev + fill);
             if (c.len) {
                 tasks.push_back({c.blob, c.off, c.len, w.host + fill});
-                B.add(items, dev, c.off, c.off + c.len, L, (uint64_t)plens[c.blob], soff[c.blob]);
+                if (crc) B.add(items, dev, c.off, c.off + c.len, L, (uint64_t)plens[c.blob], soff[c.blob]);
             }
             ShaJob j{};
             j.ptr = dev;
@@ -272,17 +272,17 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         st->direct_windows += direct;
         const hipError_t up = direct ? pl.h2d_direct(k, dma, cp) : pl.h2d(k, std::min(fill, pl.w[k].cap), cp);
         if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
-            hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess) {
+            (crc && hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess)) {
             set_error(KRK_EHIP, "metainfo windows: staging copy failed");
             r = KRK_EHIP;
             break;
         }
         r = run_jobs(D, jobs, d_dig, d_state, ks);
-        if (!r) r = run_items(D, items, d_sums, kc);
+        if (!r && crc) r = run_items(D, items, d_sums, kc);
         if (r) break;
         // the device window is free again once both kernels have read it
         pl.release(k, 0, ks);
-        pl.release(k, 1, kc);
+        if (crc) pl.release(k, 1, kc);
         t_enq += wall_s() - td;
         k = pl.next(k);
     }
@@ -462,6 +462,77 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         if (host_sums_off[q + 1] > host_sums_off[q])
             memcpy(sums_host + soff[host[q]], &host_sums[host_sums_off[q]], (host_sums_off[q + 1] - host_sums_off[q]) * 4);
     }
+    st.host_blobs = host.size();
+    t_last_call = st;
+    return r;
+}
+
+// Whole-blob SHA-256 of host buffers (the Digester over many uploads at once): the same
+// windows and schedule as krk_metainfo_digest_host without the CRC launches, and the
+// planner's blobs hashed in place on host threads (KRK_OFFLOAD_HOST_SHA).
+int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n, uint8_t* digests_host) {
+    KRK_DEVICE(D);
+    if (!n) return KRK_OK;
+    KRK_CHECK(data_host && lengths && digests_host, KRK_EINVAL, "sha256_host: null argument");
+    for (uint64_t i = 0; i < n; ++i)
+        KRK_CHECK(lengths[i] == 0 || data_host[i], KRK_EINVAL, "blob %llu: data is NULL", (unsigned long long)i);
+    std::vector<krk_blob> blobs(n);
+    std::vector<int64_t> plens(n, 1);
+    std::vector<uint64_t> soff(n, 0);
+    for (uint64_t i = 0; i < n; ++i) blobs[i] = krk_blob{data_host[i], lengths[i], 1, 0};
+    std::vector<char> on_host(n, 0);
+    std::vector<uint32_t> host;
+    const int off_t = offload_threads(kOffHostSha);
+    if (off_t > 0) {
+        host = offload_plan(lengths, n, off_t, planner_rates(D), nullptr, nullptr, kOffHostSha);
+        for (uint32_t i : host) on_host[i] = 1;
+    }
+    uint8_t* d_dig = nullptr;
+    uint32_t* d_state = nullptr;
+    DevMem mem;
+    KRK_HIP(mem.alloc(&d_dig, n * 32));
+    KRK_HIP(mem.alloc(&d_state, n * 32));
+    std::vector<uint8_t> host_dig(32 * host.size());
+    std::thread host_th;
+    if (!host.empty())
+        host_th = std::thread([&] {
+            std::vector<const uint8_t*> p(host.size());
+            std::vector<uint64_t> l(host.size());
+            for (size_t j = 0; j < host.size(); ++j) {
+                p[j] = data_host[host[j]];
+                l[j] = lengths[host[j]];
+            }
+            offload_hash_host(p, l, off_t, host_dig.data());
+        });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{host_th};
+    struct ShareGuard {
+        int saved;
+        ~ShareGuard() { t_host_share = saved; }
+    } share_guard{t_host_share};
+    if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
+    MemFiller filler(blobs.data());
+    static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
+    filler.pinned = allow_direct;
+    for (uint64_t i = 0; i < n && filler.pinned; ++i)
+        if (!on_host[i] && lengths[i] && !host_pinned(data_host[i], lengths[i])) filler.pinned = false;
+    CallStats st;
+    int r = windows_pass(D, n, lengths, plens.data(), soff.data(), on_host, filler, 64, live_cap_for(D), nullptr,
+                         d_dig, d_state, &st, /*crc=*/false);
+    if (!r && (hipStreamSynchronize(D->s_a) != hipSuccess || hipStreamSynchronize(D->s_main) != hipSuccess)) {
+        set_error(KRK_EHIP, "sha256_host: sync failed");
+        r = KRK_EHIP;
+    }
+    if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(KRK_EHIP, "digest copy-out failed");
+        r = KRK_EHIP;
+    }
+    if (host_th.joinable()) host_th.join();
+    for (size_t q = 0; !r && q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
     st.host_blobs = host.size();
     t_last_call = st;
     return r;

@@ -233,3 +233,27 @@ def test_piece_sums_files_placements_agree(gpu, orc, tmp_path):
         assert np.array_equal(got[name][0], sums), name
     for i, d in enumerate(datas):
         assert np.array_equal(sums[int(offs[i]):int(offs[i + 1])], orc.calc_piece_sums(d, 1 << 20)[1]), i
+
+
+def test_sha256_host_window_schedule(gpu, orc):
+    """krk_sha256_host runs the C++ window schedule (no CRC): 20,000 blobs -- more than the
+    live cap -- from pageable memory, every digest equal to hashlib, at most the cap live,
+    late admission over several windows; empty and one-byte blobs included."""
+    import ctypes as C
+    n = 20000
+    rng = np.random.default_rng(2024)
+    lens = [int(x) for x in rng.integers(0, 300_000, n)]
+    lens[0], lens[1], lens[-1] = 0, 1, 1 << 20
+    src = orc.synth(99, max(lens) + 4096)
+    offs = [int(x) for x in rng.integers(0, 4096, n)]
+    datas = [src[o:o + L] for o, L in zip(offs, lens)]
+    ptrs = (C.c_void_p * n)(*[d.ctypes.data if d.size else None for d in datas])
+    ln = np.asarray(lens, dtype=np.uint64)
+    out = np.zeros((n, 32), dtype=np.uint8)
+    check(lib.krk_sha256_host(ptrs, ln.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                              out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    st = D.windows_last_call()
+    cap = D.window_stream_cap()
+    assert st["max_live"] == cap and st["windows"] >= 2 and st["host_blobs"] == 0, st
+    for i in range(n):
+        assert bytes(out[i]) == hashlib.sha256(datas[i].tobytes()).digest(), (i, lens[i])
