@@ -39,6 +39,8 @@ for step in "$@"; do
     # rocprofv3 on the end-to-end legs (kernel trace + copy trace; PMC passes on their own runs)
     prof_e2e) run prof_e2e 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
                   -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
+    prof_c2) run prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
     prof_files) run prof_files 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
                   -d gpurun_out/prof_files -- python3 bench.py --workload files --steps 1 --warmup 1 --no-cpu-baseline ;;
     pmc_c2 | pmc_e2e | pmc_files)
