@@ -212,7 +212,15 @@ int calibrate(Device* D, CalBufs& cb, Rates& R) {
         R.h2d = (double)C / (timed_ms([&] { return hipMemcpyAsync(d_copy, h_copy, C, hipMemcpyHostToDevice, s); }) * 1e-3);
         R.d2h = (double)C / (timed_ms([&] { return hipMemcpyAsync(h_copy, d_copy, C, hipMemcpyDeviceToHost, s); }) * 1e-3);
     }
-    if (s) hipStreamSynchronize(s);
+    if (s) {
+        // The buffers stay (freeing waits for the device); the stream does not: a stream
+        // kept alive takes a turn in the round-robin of normal-priority streams over the
+        // hardware queues, and moved the C3 host lane's D2H copies onto a queue behind the
+        // windows' kernels (rank 0's shard of 8 GPUs: lane 16.5 -> 18-20 s).
+        hipStreamSynchronize(s);
+        hipStreamDestroy(s);
+        s = nullptr;
+    }
     R.host_sha = host_sha_rate();
     R.host_crc = host_crc_rate();
     R.host_copy = host_copy_rate();
