@@ -257,3 +257,74 @@ def test_sha256_host_window_schedule(gpu, orc):
     assert st["max_live"] == cap and st["windows"] >= 2 and st["host_blobs"] == 0, st
     for i in range(n):
         assert bytes(out[i]) == hashlib.sha256(datas[i].tobytes()).digest(), (i, lens[i])
+
+
+def test_concurrent_host_paths_under_cpu_tokens(gpu, orc, tmp_path):
+    """Host paths that share the CPU tokens, at once from several threads: end-to-end batches
+    with the host offload on (offload threads + pool copies), files on the host CRC
+    placement (pool preads), host piece streams and crc32.Update calls.  No caller stalls;
+    every result equals hashlib / zlib / the oracle."""
+    import threading
+    import zlib
+    from ctypes import c_uint32, c_uint64, c_void_p, byref
+    from kraken_amd import _capi
+    rng = np.random.default_rng(404)
+    blobs = [orc.synth(6000 + i, int(n)) for i, n in enumerate(rng.integers(1, 12 << 20, 24))]
+    paths = [_write(tmp_path, f"t{i}", b) for i, b in enumerate(blobs)]
+    lens = [int(b.size) for b in blobs]
+    P = 1 << 20
+    want_dg = [hashlib.sha256(b.tobytes()).digest() for b in blobs]
+    errors = []
+
+    def e2e():
+        try:
+            for _ in range(2):
+                sums, dg = D.metainfo_digest_host(blobs, P)
+                assert [bytes(x) for x in dg] == want_dg
+                assert np.array_equal(sums[5], orc.calc_piece_sums(blobs[5], P)[1])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def files():
+        try:
+            for _ in range(2):
+                sums, offs = D.piece_sums_files(paths, lens, P)
+                for i in (0, 7, 23):
+                    assert np.array_equal(sums[int(offs[i]):int(offs[i + 1])], orc.calc_piece_sums(blobs[i], P)[1])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def streams(i):
+        try:
+            data = blobs[i].tobytes()
+            s = c_void_p()
+            check(lib.krk_piece_stream_begin_on(_capi.KRK_PLACE_HOST, P, byref(s)))
+            try:
+                for a in range(0, len(data), 3 << 20):
+                    check(lib.krk_piece_stream_update(s, data[a:a + (3 << 20)], len(data[a:a + (3 << 20)])))
+                n, ln = c_uint64(), c_uint64()
+                out = (c_uint32 * ((len(data) + P - 1) // P))()
+                check(lib.krk_piece_stream_end(s, out, len(out), byref(n), byref(ln)))
+                assert list(out) == [zlib.crc32(data[k:k + P]) for k in range(0, len(data), P)]
+            finally:
+                lib.krk_piece_stream_free(s)
+            o = c_uint32()
+            check(lib.krk_crc32_update_on(_capi.KRK_PLACE_HOST, 0, data, len(data), byref(o)))
+            assert o.value == zlib.crc32(data)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    D.set_sha_host_offload(-1)
+    D.set_crc_placement(D.PLACE_HOST)
+    try:
+        th = ([threading.Thread(target=e2e) for _ in range(2)] + [threading.Thread(target=files) for _ in range(2)] +
+              [threading.Thread(target=streams, args=(i,)) for i in range(12)])
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=240)
+        assert not any(t.is_alive() for t in th), "a caller did not finish"
+    finally:
+        D.set_sha_host_offload(0)
+        D.set_crc_placement(D.PLACE_GPU)
+    assert not errors, errors[:3]
