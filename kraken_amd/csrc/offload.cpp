@@ -124,15 +124,9 @@ struct CalBufs {
 // Per device: host threads + pinned double buffers of the offload phases, and the planner
 // calibration (measured once per device and process, or again on krk_planner_calibrate).
 struct Worker;
-constexpr int kCopyQueues = 4;
 struct OffloadPool {
     std::mutex mu;
     std::vector<std::vector<Worker>> free_sets;
-    // D2H copy streams on hardware queues of their own (CU-masked streams get a queue each),
-    // shared by the offload threads; nullptr until first use or when not available.
-    std::once_flag copy_once;
-    hipStream_t copy_s[kCopyQueues] = {};
-    bool copy_ok = false;
     std::mutex cal_mu;  // one calibration of this device at a time
     CalBufs cal;
     bool measured = false;
@@ -264,32 +258,7 @@ double gpu_seconds(uint64_t longest, double bytes, uint64_t m, const Rates& R) {
 struct Worker {
     hipStream_t s[2] = {nullptr, nullptr};
     uint8_t* buf[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};  // the copy into buf[b] is done (dedicated copy queues)
 };
-
-// The offload's copy queues (KRK_OFFLOAD_COPY_QUEUES=0: each thread's own normal streams).
-// A normal-priority stream shares one of HIP's hardware queues with other streams in
-// creation order, and its copies' completion then waits behind whatever kernels another
-// stream queued there first (the C3 host lane beside the windows' ~80 ms CRC launches: its
-// threads waited 0.8-15 s a group).  Streams with a CU mask get queues of their own.
-bool copy_queues(Device* D, OffloadPool& P) {
-    static const bool want = !getenv("KRK_OFFLOAD_COPY_QUEUES") || atoi(getenv("KRK_OFFLOAD_COPY_QUEUES")) != 0;
-    if (!want) return false;
-    std::call_once(P.copy_once, [&] {
-        std::vector<uint32_t> mask((D->cus + 31) / 32, 0xFFFFFFFFu);
-        if (D->cus % 32) mask.back() = (1u << (D->cus % 32)) - 1;
-        bool ok = true;
-        for (int q = 0; q < kCopyQueues && ok; ++q)
-            ok = hipExtStreamCreateWithCUMask(&P.copy_s[q], (uint32_t)mask.size(), mask.data()) == hipSuccess;
-        if (!ok) {
-            (void)hipGetLastError();
-            for (auto& q : P.copy_s)
-                if (q) hipStreamDestroy(q), q = nullptr;
-        }
-        P.copy_ok = ok;
-    });
-    return P.copy_ok;
-}
 
 // (Re)measure device D's rates now; a failed calibration plans with the nominal rates.
 int calibrate_device(Device* D) {
@@ -460,15 +429,13 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     while ((int)set.size() < T) {
         Worker w;
         for (int b = 0; b < 2; ++b) {
-            hipError_t es = hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking);
-            if (es == hipSuccess) es = hipEventCreateWithFlags(&w.ev[b], hipEventDisableTiming);
+            const hipError_t es = hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking);
             const hipError_t eb = es == hipSuccess
                                       ? hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault)
                                       : es;
             if (eb != hipSuccess) {  // undo what this worker made so far
                 for (int c = 0; c <= b; ++c) {
                     if (w.s[c]) hipStreamDestroy(w.s[c]);
-                    if (w.ev[c]) hipEventDestroy(w.ev[c]);
                     if (w.buf[c]) hipHostFree(w.buf[c]);
                 }
                 if (es != hipSuccess) set_error(KRK_EHIP, "sha256 host offload: stream: %s", hipGetErrorString(es));
@@ -486,12 +453,10 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     auto secs = [](std::chrono::steady_clock::time_point a) {
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     };
-    const bool own_queues = copy_queues(D, P);
     std::vector<std::thread> pool;
     for (int t = 0; t < T; ++t)
         pool.emplace_back([&, t] {
             Worker& W = set[t];
-            hipStream_t cs = own_queues ? P.copy_s[t % kCopyQueues] : nullptr;
             // The host waits for `ready` (the caller's stream up to the call; the batch's own
             // kernels come after it): a stream wait packet could queue behind those kernels.
             if (hipSetDevice(D->id) != hipSuccess || hipEventSynchronize(ready) != hipSuccess) {
@@ -504,18 +469,8 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
                 const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
                 auto issue = [&](uint64_t c) {
                     const uint64_t o = c * kOffChunk, m = std::min(kOffChunk, L - o);
-                    if (cs)  // a shared copy queue: each copy's own event marks its completion
-                        return m == 0 ||
-                               (hipMemcpyAsync(W.buf[c & 1], src + o, m, hipMemcpyDeviceToHost, cs) == hipSuccess &&
-                                hipEventRecord(W.ev[c & 1], cs) == hipSuccess);
                     return m == 0 ||
                            hipMemcpyAsync(W.buf[c & 1], src + o, m, hipMemcpyDeviceToHost, W.s[c & 1]) == hipSuccess;
-                };
-                auto wait = [&](uint64_t c) {
-                    const uint64_t o = c * kOffChunk;
-                    if (o >= L) return true;  // an empty blob: nothing was copied
-                    return cs ? hipEventSynchronize(W.ev[c & 1]) == hipSuccess
-                              : hipStreamSynchronize(W.s[c & 1]) == hipSuccess;
                 };
                 uint32_t h[8];
                 memcpy(h, kIV, sizeof h);
@@ -524,7 +479,7 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
                 for (uint64_t c = 0; ok && c < nch; ++c) {
                     if (c + 1 < nch) ok = issue(c + 1);  // into the other buffer, hashed at c - 1
                     const auto tw = std::chrono::steady_clock::now();
-                    if (!ok || !wait(c)) {
+                    if (!ok || hipStreamSynchronize(W.s[c & 1]) != hipSuccess) {
                         ok = false;
                         break;
                     }
@@ -539,9 +494,8 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
                     }
                     t_hash[t] += secs(th);
                 }
-                if (!ok) {  // leave no copy in flight into the buffers
-                    if (cs) hipStreamSynchronize(cs);
-                    hipStreamSynchronize(W.s[0]);
+                if (!ok) {
+                    hipStreamSynchronize(W.s[0]);  // leave no copy in flight into the buffers
                     hipStreamSynchronize(W.s[1]);
                     err.store(1);
                 }
@@ -570,11 +524,8 @@ void offload_teardown(Device& D) {  // krk_shutdown: no offload phase is running
         for (Worker& w : set)
             for (int b = 0; b < 2; ++b) {
                 if (w.s[b]) hipStreamSynchronize(w.s[b]), hipStreamDestroy(w.s[b]);
-                if (w.ev[b]) hipEventDestroy(w.ev[b]);
                 if (w.buf[b]) hipHostFree(w.buf[b]);
             }
-    for (auto& q : P->copy_s)
-        if (q) hipStreamSynchronize(q), hipStreamDestroy(q), q = nullptr;
     CalBufs& c = P->cal;
     if (c.s) hipStreamSynchronize(c.s), hipStreamDestroy(c.s);
     for (void* p : {(void*)c.d_in, (void*)c.d_state, (void*)c.d_dig, (void*)c.d_jobs, (void*)c.d_copy})
