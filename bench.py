@@ -140,21 +140,35 @@ def mix64(z: int) -> int:
     return z ^ (z >> 31)
 
 
+def host_budget():
+    """(this rank's host CPU budget, the node's CPUs, where the budget came from), from the
+    library itself (krk_host_cpu_budget: KRK_HOST_CPUS, else the node's CPUs -- affinity
+    capped by the cgroup quota -- divided among LOCAL_WORLD_SIZE ranks, else capped by
+    OMP_NUM_THREADS), so the bench's host legs size themselves as the library does."""
+    from kraken_amd import _capi
+    return _capi.host_cpu_budget()
+
+
 def host_cores() -> int:
-    """CPUs this process may actually use: the affinity mask capped by the cgroup
-    CPU quota and by OMP_NUM_THREADS (GPU boxes expose the whole machine in the
-    mask but grant a 16-CPU share)."""
-    n = len(os.sched_getaffinity(0))
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
-        if q != "max":
-            n = min(n, max(1, int(q) // int(per)))
-    except (OSError, ValueError):
-        pass
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        n = min(n, int(env))
-    return n
+    """CPUs this rank's host legs may use: the library's per-process budget."""
+    return host_budget()[0]
+
+
+def node_cores() -> int:
+    """All of the node's host cores (GOMAXPROCS = every core, BASELINE.json north_star):
+    what rank 0's cpu_baseline runs on at every N, whatever a launcher put in
+    OMP_NUM_THREADS.  The other ranks wait at a barrier meanwhile."""
+    return host_budget()[1]
+
+
+def baseline_sample_blobs() -> int:
+    """Blobs in a CPU baseline sample: one per core at least (one goroutine a blob, every
+    core busy), two per core up to 32 (load balance on small nodes)."""
+    return max(node_cores(), min(2 * node_cores(), 32))
+
+
+CORES_SOURCE = ("the node's host cores: affinity capped by the cgroup cpu.max quota (krk_host_cpu_budget "
+                "node_cpus; OMP_NUM_THREADS and LOCAL_WORLD_SIZE not applied)")
 
 
 # ----------------------------------------------------------------- workloads
@@ -200,7 +214,7 @@ def cpu_baseline_metainfo(lens_sample, ids_sample, piece, target_s, passes=3):
     from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
     O.build()
     # one blob per worker, as the reference (one goroutine per blob): C1's single blob is one core
-    threads = min(host_cores(), len(lens_sample))
+    threads = min(node_cores(), len(lens_sample))
     t1, dg, sums = O.baseline_run(ids_sample, lens_sample, piece, threads, fast=True, want_outputs=True,
                                   passes=passes)
     reps = max(1, int(round(target_s / max(t1, 1e-3))))
@@ -208,10 +222,11 @@ def cpu_baseline_metainfo(lens_sample, ids_sample, piece, target_s, passes=3):
     total = sum(lens_sample) * reps
     what = {3: "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL)", 2: "CRC-32 piece pass (PCLMUL) only",
             1: "SHA-256 pass (SHA-NI) only"}[passes]
-    info = {"value": round(total / t / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+    info = {"value": round(total / t / 1e9, 3), "unit": "GB/s", "cores": threads, "cores_source": CORES_SOURCE,
+            "kind": "port",
             "sample": (f"{len(lens_sample)} synthetic blobs ({sum(lens_sample) / 2**20:.0f} MiB) x {reps} passes "
                        f"({t:.1f} s): {what}, 32 KiB chunks, one blob per thread, {threads} threads (the host "
-                       "CPU share of this GPU), oracle/oracle.c"),
+                       "node's cores), oracle/oracle.c"),
             "seconds": round(t, 2), "have_shani": bool(O.lib().orc_have_shani()),
             "have_clmul": bool(O.lib().orc_have_clmul())}
     return info, dg, sums
@@ -233,7 +248,7 @@ def cpu_baseline_c3(ids, lens, P, dg_gpu, sums_gpu, sums_off_gpu):
     n = len(lens)
     m = min(n, C3_CPU_SAMPLE)
     pick = np.sort(np.random.default_rng(0xC3).choice(n, m, replace=False))
-    threads = min(host_cores(), m)
+    threads = min(node_cores(), m)
     lens_s = [int(lens[i]) for i in pick]
     busy, dgc, (s, off) = O.baseline_run_lazy([ids[i] for i in pick], lens_s, P, threads)
     ok = True
@@ -243,7 +258,8 @@ def cpu_baseline_c3(ids, lens, P, dg_gpu, sums_gpu, sums_off_gpu):
                                                                          sums_gpu[o:o + cnt])
     total = sum(lens_s)
     wall = busy / threads
-    return {"value": round(total / wall / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+    return {"value": round(total / wall / 1e9, 3), "unit": "GB/s", "cores": threads, "cores_source": CORES_SOURCE,
+            "kind": "port",
             "sample": (f"{m} seeded C3 blobs ({total / 1e9:.1f} GB, {min(lens_s) >> 20}-{max(lens_s) >> 20} MiB): "
                        "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL), 32 KiB chunks, one blob per thread, "
                        f"{threads} threads; each blob generated untimed into its thread's buffer, rate = bytes / "
@@ -256,14 +272,15 @@ def cpu_baseline_c3(ids, lens, P, dg_gpu, sums_gpu, sums_off_gpu):
 def cpu_baseline_hrw(digests, labels, healthy, max_replica, target_s):
     from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
     O.build()
-    threads = host_cores()
+    threads = node_cores()
     m = min(len(digests), 100_000)
     t1, locs, counts = O.baseline_hrw(digests[:m], labels, healthy, max_replica, threads)
     reps = max(1, int(round(target_s / max(t1, 1e-3))))
     t = 0.0
     for _ in range(reps):
         t += O.baseline_hrw(digests[:m], labels, healthy, max_replica, threads)[0]
-    return ({"value": round(m * reps / t, 1), "unit": "digests/s", "cores": threads, "kind": "port",
+    return ({"value": round(m * reps / t, 1), "unit": "digests/s", "cores": threads, "cores_source": CORES_SOURCE,
+             "kind": "port",
              "sample": f"{m} digests x {reps} passes ({t:.1f} s): GetOrderedNodes(ShardID) + Locations filter "
                        f"per digest, {threads} threads, oracle/oracle.c"}, locs, counts)
 
@@ -460,7 +477,7 @@ def run_metainfo(a, D, T, rank, world, res):
             res["end_to_end"]["valu"] = {"sha256_multi": ev.get("sha256_multi"), "crc32_pieces": ev.get("crc32_pieces"),
                                          "source": valu_src, "measured_in_this_run": False, "note": VALU_NOTE}
     if rank == 0 and not a.no_cpu_baseline:
-        m = min(n, 2 * host_cores())  # bounded sample: the first blobs of this workload
+        m = min(n, baseline_sample_blobs())  # bounded sample: the first blobs of this workload
         cb, dg, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds)
         ok = all(bytes(dg[k]) == bytes(dg_h[32 * k:32 * k + 32]) for k in range(m))
         s, off = sums
@@ -571,7 +588,7 @@ def run_regen(a, D, T, rank, world, res):
     if a.workload == "c5regen" and not a.no_e2e:
         res["end_to_end"] = regen_end_to_end(D, T, lens, P, names, world, rank, cpu=not a.no_cpu_baseline)
     if rank == 0 and not a.no_cpu_baseline:
-        m = min(n, 2 * host_cores())
+        m = min(n, baseline_sample_blobs())
         cb, _, sums = cpu_baseline_metainfo(lens[:m], ids[:m], P, a.cpu_seconds, passes=2)
         s_, off = sums
         ok = all(np.array_equal(s_[int(off[k]):int(off[k + 1])],
@@ -858,9 +875,10 @@ def regen_end_to_end(D, T, lens, P, names, world, rank, cpu=True):
         if cpu and rank == 0:  # the reference's own Generate over the same files on the CPU budget
             from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
             O.build()
-            runs = [O.baseline_files(paths, lens, P, host_cores()) for _ in range(3)]
+            runs = [O.baseline_files(paths, lens, P, node_cores()) for _ in range(3)]
             t_c = float(np.median([r[0] for r in runs]))
-            cpu_files = {"value": round(total / t_c / 1e9, 3), "unit": "GB/s", "cores": host_cores(), "kind": "port",
+            cpu_files = {"value": round(total / t_c / 1e9, 3), "unit": "GB/s", "cores": node_cores(),
+                         "cores_source": CORES_SOURCE, "kind": "port",
                          "seconds": round(t_c, 3),
                          "sums_match": bool(np.array_equal(runs[0][1][:int(counts.sum())],
                                                            legs["default"]["result"][0][:int(counts.sum())])),
@@ -1100,7 +1118,7 @@ def run_pieces(a, D, T, rank, world, res):
     if a.workload == "c4" and not a.no_e2e:
         res["end_to_end"] = c4_end_to_end(D, T, arena, sums_h, P, world)
     if rank == 0 and not a.no_cpu_baseline:
-        m = 2 * host_cores()
+        m = 2 * node_cores()
         cb, _, sums = cpu_baseline_metainfo([256 << 20] * m, [ids[0]] * m, P, a.cpu_seconds, passes=2)
         s, off = sums
         cnt = int(off[1] - off[0])
@@ -1443,10 +1461,11 @@ def run_files(a, D, T, rank, world, res):
         if rank == 0 and not a.no_cpu_baseline:
             # the reference's two reads of every file on the CPU budget: uploader.verify's
             # Digester over the upload file, then Generate's calcPieceSums over the cache file
-            t_c, s_c, off_c, dg_c = O.baseline_files(paths, lens, P, host_cores(), passes=3)
+            t_c, s_c, off_c, dg_c = O.baseline_files(paths, lens, P, node_cores(), passes=3)
             same_c = bool(np.array_equal(dg_c, dg_f)) and all(
                 np.array_equal(s_c[int(off_c[i]):int(off_c[i + 1])], sums_f[i]) for i in range(n))
-            cb = {"value": round(total / t_c / 1e9, 3), "unit": "GB/s", "cores": host_cores(), "kind": "port",
+            cb = {"value": round(total / t_c / 1e9, 3), "unit": "GB/s", "cores": node_cores(),
+                  "cores_source": CORES_SOURCE, "kind": "port",
                   "seconds": round(t_c, 3), "outputs_match_gpu": same_c,
                   "sample": f"all {n} files of the pass (page cache warm): Digester.FromReader then calcPieceSums "
                             "over each file, 32 KiB reads, SHA-NI and PCLMUL, one file per thread "
@@ -1637,6 +1656,10 @@ def main():
     # line shows it ran on N distinct GPUs
     T.barrier()
     devs = T.gather(D.device_pci_bus_id())
+    cpus, node, src = host_budget()
+    res["host_budget"] = {"rank_cpus": T.gather(cpus), "node_cpus": node, "source": src,
+                          "local_world_size": _env_int("LOCAL_WORLD_SIZE", 1),
+                          "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
     if world > 1 or T.rank_s:
         res["rank_devices"] = devs
         if T.rank_s:

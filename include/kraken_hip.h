@@ -82,11 +82,9 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
  * share learned from the previous calls' measured rates of both sides (first call: the
  * planner rates' model, at most 10 %) -- or none, when host-only calls measured faster
  * than split ones (after two split calls -- the first sets up the staging windows -- one
- * runs host-only to find out; every 16th call re-measures the other choice).  Pageable bytes stay on the host (a staging copy per byte costs more
- * than the GPU saves).  KRK_CRC_GPU_FRACTION forces the share.  This returns the calling
- * thread's last split in bytes and the share the next pinned batch of its device will use
- * (0 while host-only wins, -1 until learned). */
-int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fraction);
+ * runs host-only to find out; every 16th call re-measures the other choice).  Pageable
+ * bytes stay on the host (a staging copy per byte costs more than the GPU saves).
+ * KRK_CRC_GPU_FRACTION forces the share. */
 
 /* Piece sums of cache FILES: the batch form of Generator.Generate reading the
  * CAS cache file itself (lib/metainfogen/generator.go:41-58: GetCacheFileReader
@@ -96,7 +94,8 @@ int krk_crc_host_split(uint64_t* gpu_bytes, uint64_t* host_bytes, double* gpu_fr
  * bytes (pread on a pool of host threads, or O_DIRECT when KRK_FILE_DIRECT=1 and
  * the filesystem allows it) straight into the pinned staging windows -- no
  * pageable copy -- and the windows feed the CRC kernel as in krk_piece_sums_host.
- * krk_crc_host_split reports the call's bytes on each side.  length is the size
+ * The call's bytes on each side are reported by
+ * krk_crc_host_split (kraken_hip_internal.h).  length is the size
  * the caller stat-ed (Generate picks the piece length from it); a file shorter
  * than that is KRK_EIO "read blob: <path>: unexpected EOF".  Synchronous. */
 typedef struct krk_file_blob {
@@ -180,10 +179,10 @@ int krk_sha256_dev_on_host(const uint8_t* const* data_dev, const uint64_t* lengt
                            void* stream, uint8_t* digests_host);
 
 /* Host batch: HOST data pointers; digests_host n*32 bytes.  Synchronous.  The window
- * schedule of krk_metainfo_digest_host without the piece CRCs (at most
- * krk_window_stream_cap blobs live, admitted longest first; page-locked blobs DMA'd
- * directly), and the planner's blobs hashed in place on host threads under the default
- * AUTO host offload; krk_windows_last_call reports the call. */
+ * schedule of krk_metainfo_digest_host without the piece CRCs (at most the window
+ * stream cap of blobs live, admitted longest first; page-locked blobs DMA'd directly),
+ * and the planner's blobs hashed in place on host threads under the default AUTO host
+ * offload. */
 int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, uint64_t n,
                     uint8_t* digests_host);
 
@@ -224,11 +223,6 @@ int krk_digester_sum(krk_digester* d, uint8_t out32[32]);
 void krk_digester_free(krk_digester* d);
 int krk_set_digester_host_streams(int64_t n);
 
-/* Submission-engine counters of the calling thread's device: SHA launches and the
- * jobs they carried (jobs / batches = streams coalesced per launch), CRC launches and
- * requests, pinned staging bytes held by the slot pool. */
-int krk_engine_stats(uint64_t* sha_batches, uint64_t* sha_jobs, uint64_t* crc_batches,
-                     uint64_t* crc_requests, uint64_t* pinned_bytes);
 /* The slot pool's HARD cap on pinned staging bytes for the calling thread's device
  * (default KRK_SLOT_POOL_MB = 4096 MiB; at least one 16-slot chunk).  At the cap a
  * writer waits for a slot to come back (backpressure) instead of pinning more: slots
@@ -299,32 +293,6 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* 
 int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host,
                               uint8_t* digests_host);
 
-/* The window schedule of the host-resident batch calls (and of kraken_amd/windowed.py's
- * larger-than-HBM device batches): every live blob advances by the same chunk (a multiple of
- * 64 bytes but each blob's last, about window_bytes / live a window); at most live_cap blobs
- * are live, admitted longest first; a finished blob's place goes to the next-longest.  _next
- * writes the next window's chunks (blob index, offset, length; admission order) and their
- * count to *n_out, 0 once every blob is done (KRK_ERANGE if cap is too small: the window
- * has *n_out <= live_cap chunks). */
-typedef struct krk_window_sched krk_window_sched;
-int krk_window_sched_new(const uint64_t* lengths, uint64_t n, uint64_t window_bytes, uint64_t live_cap,
-                         krk_window_sched** out);
-int krk_window_sched_next(krk_window_sched* s, uint32_t* blobs, uint64_t* offsets, uint64_t* lengths, uint64_t cap,
-                          uint64_t* n_out);
-void krk_window_sched_free(krk_window_sched* s);
-/* The live-stream cap of the windows on the calling thread's device: 7/8 of the largest
- * stream count whose SHA-256 launch runs more than one lane a stream (14,336 on 256 CUs),
- * so each window's CRC launch has the CUs the SHA workgroups leave free.  KRK_LIVE_CAP
- * overrides it for the host-resident calls. */
-int krk_window_stream_cap(uint64_t* cap);
-/* The calling thread's last krk_metainfo_digest_host / _files call: the most live blobs in
- * one window, the windows, and the blobs the host offload took. */
-int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs);
-/* ... and how many of its windows went to the device straight from the caller's
- * page-locked blobs (krk_host_alloc memory, windows of <= 64 chunks: no pinned staging
- * copy, one DMA a chunk).  KRK_PINNED_DIRECT=0 stages them instead. */
-int krk_windows_last_direct(int* direct_windows);
-
 /* ------------------------------------------------------- multi-device
  * One process, several GPUs (the origin is one process,
  * origin/cmd/cmd.go:164).  The device set -- the devices of the last krk_init mask,
@@ -369,16 +337,6 @@ int krk_info_hash_batch(const int64_t* piece_lengths, const uint32_t* sums, cons
 int krk_bencode_info(int64_t piece_length, const uint32_t* sums, uint64_t n_sums,
                      const char* name, uint64_t name_len, int64_t length,
                      uint8_t* out, uint64_t cap, uint64_t* written);
-
-/* --------------------------------------- host crossover primitives (CPU)
- * The host side of the Digester / PieceHash crossovers: a single
- * SHA-256 stream digests ~2 GB/s on one SHA-NI core vs ~59 MB/s on one GPU stream,
- * and a small crc32.Update is cheaper on the calling thread than a PCIe round trip,
- * so a krk_digester with few concurrent peers and a small krk_crc32_update write
- * run these on the caller's thread.  x86 SHA-NI / PCLMULQDQ when the CPU has them,
- * portable code otherwise; sha256.Sum256 and crc32.Update(crc, IEEETable, p). */
-int krk_host_sha256(const uint8_t* data, uint64_t n, uint8_t out32[32]);
-int krk_host_crc32_update(uint32_t crc, const uint8_t* data, uint64_t n, uint32_t* out);
 
 /* pieceLengthConfig.get (lib/metainfogen/config.go:71-80); thresholds ascending. */
 int64_t krk_piece_length_for_size(const int64_t* thresholds, const int64_t* lengths,
@@ -438,17 +396,6 @@ int krk_ring_locations_u8_dev(const uint8_t* digests32_dev, uint64_t n, const kr
                               const uint8_t* healthy, int32_t max_replica,
                               uint8_t* locs_dev, uint8_t* counts_dev, void* stream);
 
-/* ----------------------------------------------------- synthetic blobs
- * Fills a device buffer with bytes [offset, offset+n) of synthetic blob
- * blob_idx (splitmix64 counter stream, variant 0 = uniform bytes, 1 = alnum;
- * spec in DESIGN.md).  Benchmark/test data generator. */
-int krk_synth_fill_dev(uint8_t* dst_dev, uint64_t blob_idx, uint64_t offset, uint64_t n,
-                       int variant, void* stream);
-/* Batched form for window generation: chunk i fills chunks[i].data (device)
- * with bytes [offset, offset+length) of synthetic blob chunks[i].blob (the
- * other krk_chunk fields are ignored).  One launch. */
-int krk_synth_fill_chunks_dev(const krk_chunk* chunks, uint64_t n, int variant, void* stream);
-
 /* ------------------------------------------------ device memory helpers
  * For callers (benchmarks, cgo) that do not own a device allocator. */
 int krk_dev_alloc(uint64_t bytes, void** out);
@@ -469,11 +416,6 @@ int krk_stream_create(void** out);
  * long kernels (a C3 window's SHA-256 launch runs ~0.6 s) is kept off the queues the
  * short work shares, which would otherwise wait behind it. */
 int krk_stream_create_prio(int priority, void** out);
-/* PCI bus id of the calling thread's device ("0000:05:00.0"; cap >= 16): an N-rank run
- * reports every rank's, so a scaling line shows it ran on N distinct GPUs. */
-int krk_device_pci_bus_id(char* out, uint32_t cap);
-/* CUs of the calling thread's device. */
-int krk_device_cus(int* out);
 /* Waits for the stream's work, retires the library's state tied to it (events of upload
  * slots and scratch blocks last used on it), then destroys it.  Streams handed to the
  * library must be destroyed here, not with hipStreamDestroy. */
@@ -485,58 +427,6 @@ int krk_event_create(void** out);
 int krk_event_record(void* ev, void* stream);
 int krk_event_sync(void* ev);
 int krk_event_destroy(void* ev);
-
-/* Kernel timing: when enabled, every kernel launch is bracketed by hipEvents
- * recorded on the stream the kernel runs on; krk_kernel_stats returns the
- * number of launches and their summed device time (ms) since the last reset
- * for kernel name "crc32_pieces", "sha256_multi", "hrw_shard_table",
- * "hrw_gather" or "synth_fill" (timed launches are synchronised lazily). */
-int krk_set_timing(int on);
-/* Shader clock of the calling thread's device, measured by a one-wave probe kernel on
- * `stream` (NULL = the library's stream): s_memtime cycles over s_memrealtime (100 MHz)
- * ticks of a ~2 ms spin.  Launched while another kernel runs it reads the clock the chip
- * holds under that load (bench.py prices the SHA-256 issue ceiling with it). */
-int krk_device_clock_mhz(void* stream, double* mhz);
-int krk_kernel_stats(const char* kernel, uint64_t* launches, double* total_ms);
-/* Every timed launch of `kernel` since the last reset, in the order the host issued
- * them: device, SHA-256 plan (KRK_SHA_PLAN_*; 0 for other kernels), work units
- * (streams for sha256_multi, work items + runs for crc32_pieces, else 0) and the
- * launch's start / end in ms after the device's first timed launch (hipEvents on the
- * launch's own stream, so launches on different streams of one device share the
- * clock).  Up to `cap` records to out (may be NULL), the total count to *n; the
- * library keeps the first 2^20 launches.  Lets a test check which plan a launch ran
- * and whether two launches overlapped on the device. */
-typedef struct krk_launch_rec {
-    int32_t device;
-    int32_t plan;
-    uint64_t units;
-    double start_ms;
-    double end_ms;
-} krk_launch_rec;
-int krk_kernel_timeline(const char* kernel, krk_launch_rec* out, uint64_t cap, uint64_t* n);
-int krk_reset_kernel_stats(void);
-
-/* SHA-256 launch plan: lanes per stream (1, 2 or 8) the library uses for a batch of
- * n_streams streams on the current device (more lanes a stream -- a shorter chain a
- * block -- while the batch leaves SIMDs idle).  Diagnostic; bench.py prices the
- * per-stream issue ceiling of that plan. */
-int krk_sha_lanes_per_stream(uint64_t n_streams, int* lanes);
-/* The launch plan itself (KRK_SHA_PLAN_1LANE .. KRK_SHA_PLAN_8LANE_2PAIR below) for a
- * batch of n_streams streams on the current device under the current plan setting. */
-int krk_sha_plan_for(uint64_t n_streams, int* plan);
-
-/* SHA-256 launch plan, process-wide (default AUTO: eight lanes per stream while the
- * batch leaves SIMDs idle, then two lanes, then two producer/consumer pairs per
- * workgroup, then one lane).  Every plan is bit-exact; the knob exists for tests and tuning.  The
- * environment variable KRK_SHA_PLAN, read once at the first launch, sets the same. */
-#define KRK_SHA_PLAN_AUTO 0
-#define KRK_SHA_PLAN_1LANE 1        /* one lane per stream, one pair per workgroup */
-#define KRK_SHA_PLAN_2LANE 2        /* two lanes per stream, one pair per workgroup */
-#define KRK_SHA_PLAN_1LANE_2PAIR 3  /* one lane, two pairs per 4-wave workgroup */
-#define KRK_SHA_PLAN_2LANE_2PAIR 4  /* two lanes, two pairs per workgroup */
-#define KRK_SHA_PLAN_8LANE 5        /* eight lanes per stream, one pair per workgroup */
-#define KRK_SHA_PLAN_8LANE_2PAIR 6  /* eight lanes, two pairs per workgroup */
-int krk_set_sha_plan(int plan);
 
 /* Host offload of the longest SHA-256 chains, process-wide.  krk_sha256_dev and
  * krk_metainfo_digest_dev hand the longest blobs of a batch to host threads (x86 SHA
@@ -551,22 +441,23 @@ int krk_set_sha_plan(int plan);
  * krk_metainfo_digest_host hashes them AND computes their piece sums (the SHA-256 pass and
  * the CRC pass of a blob are separate host tasks), so the bytes that cross the host link
  * shrink by theirs (the threshold there is 3 %).
- * threads: KRK_OFFLOAD_AUTO (-1, the default) = the CPUs this process may use (affinity,
- * cgroup quota, OMP_NUM_THREADS) for device-resident batches and a quarter of them for
+ * threads: KRK_OFFLOAD_AUTO (-1, the default) = the process's host CPU budget (the node's
+ * CPUs -- affinity capped by the cgroup quota -- divided among the LOCAL_WORLD_SIZE ranks of
+ * a node, or KRK_HOST_CPUS) for device-resident batches and a quarter of them for
  * host-resident batches (whose staging windows need the rest as copy threads); 0 = off
  * (every chain on the GPU); n = up to n threads. */
 #define KRK_OFFLOAD_AUTO (-1)
 int krk_set_sha_host_offload(int threads);
 int krk_sha_host_offload(int* threads);      /* the current setting */
-/* The rates the planners use (krk_host_offload_plan, the offload of the batch entry
+/* The rates the planners use (the offload of the batch entry
  * points, the host/GPU split of the CRC-only host entry points), per device:
  * sha_stream_bps = one SHA-256 stream's rate at full residency under each AUTO tier
  * (eight lanes up to 16 x CUs streams, two lanes up to 64 x CUs, one lane beyond),
  * pinned D2H / H2D copy rates, one host thread's SHA-256, CRC-32 and memcpy rates.  Measured on
  * the calling thread's device at first use (~50 ms: each tier's launch plan timed on
  * 16 / 64 / 128 x CUs streams, a 64 MiB pinned copy each way); without a device the
- * nominal MI355X figures (source 0).  krk_planner_rates_set overrides them process-wide
- * (NULL restores the measured ones): tests inject rates, an operator pins them. */
+ * nominal MI355X figures (source 0).  (kraken_hip_internal.h: krk_planner_rates_set
+ * overrides them for tests, krk_host_offload_plan shows a plan without device work.) */
 #define KRK_RATES_NOMINAL 0
 #define KRK_RATES_MEASURED 1
 #define KRK_RATES_SET 2
@@ -578,28 +469,10 @@ typedef struct krk_planner_rates {
     int32_t source;
 } krk_planner_rates;
 int krk_planner_rates_get(krk_planner_rates* out);
-int krk_planner_rates_set(const krk_planner_rates* in);
 /* Measure the calling thread's device's rates now (krk_init does it for its devices, so that
  * the measurement runs before the library has work of its own on them; otherwise the first
  * planner use measures).  Re-measure after a change of load the planners should see. */
 int krk_planner_calibrate(void);
-/* The offload plan for `n` blob lengths on `threads` host threads with the planner rates
- * (krk_planner_rates_get; `cus` > 0 overrides their CU count), no device work: the
- * indices (longest first) to host_idx (room for n, may be NULL), their count to n_host,
- * and the modelled GPU / host seconds (may be NULL).
- * krk_sha_offload_plan plans a device-resident batch (krk_sha256_dev,
- * krk_metainfo_digest_dev); krk_host_offload_plan plans for `mode`
- * KRK_OFFLOAD_DEVICE (the same), KRK_OFFLOAD_HOST_SHA (krk_sha256_host),
- * KRK_OFFLOAD_HOST_WHOLE (krk_metainfo_digest_host) or KRK_OFFLOAD_HOST_FILES
- * (krk_metainfo_digest_files). */
-#define KRK_OFFLOAD_DEVICE 0
-#define KRK_OFFLOAD_HOST_SHA 1
-#define KRK_OFFLOAD_HOST_WHOLE 2
-#define KRK_OFFLOAD_HOST_FILES 3  /* krk_metainfo_digest_files: one read, SHA-256 + CRC per host blob */
-int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, uint32_t* host_idx,
-                         uint64_t* n_host, double* gpu_seconds, double* host_seconds);
-int krk_host_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int cus, int mode, uint32_t* host_idx,
-                          uint64_t* n_host, double* gpu_seconds, double* host_seconds);
 
 #ifdef __cplusplus
 }

@@ -1,4 +1,5 @@
-"""ctypes binding of libkraken_hip.so (include/kraken_hip.h).
+"""ctypes binding of libkraken_hip.so (include/kraken_hip.h, and the benchmark / test
+hooks of include/kraken_hip_internal.h).
 
 This is the Python-side FFI stub over the C ABI -- the same role the cgo stubs in
 INTEGRATION.md play for the reference's Go code.  There is no fallback: if the
@@ -12,6 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KRK_LIB_PATH") or os.path.join(_HERE, "lib", "libkraken_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip.h")
+INTERNAL_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kraken_hip_internal.h")
 
 KRK_OK, KRK_EINVAL, KRK_EHIP, KRK_ENOMEM, KRK_ENODEV, KRK_ERANGE, KRK_EHEX, KRK_EIO = 0, -1, -2, -3, -4, -5, -6, -7
 KRK_PLACE_AUTO, KRK_PLACE_HOST, KRK_PLACE_GPU = 0, 1, 2
@@ -173,6 +175,8 @@ def _load() -> C.CDLL:
         "krk_reset_kernel_stats": (i, []),
         "krk_kernel_timeline": (i, [C.c_char_p, C.POINTER(krk_launch_rec), C.c_uint64, u64p]),
         "krk_sha_plan_for": (i, [C.c_uint64, C.POINTER(C.c_int)]),
+        "krk_host_cpu_budget": (i, [C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
+        "krk_digester_host_streams": (i, [i64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -191,8 +195,31 @@ def check(rc: int) -> int:
     return rc
 
 
-def declared_symbols() -> list[str]:
-    """Every krk_* function declared in include/kraken_hip.h."""
+def _declared(path) -> set[str]:
     import re
-    src = open(HEADER_PATH).read()
-    return sorted(set(re.findall(r"\b(krk_[a-z0-9_]+)\s*\(", src)))
+    src = open(path).read()
+    return set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(krk_[a-z0-9_]+)\s*\(", src, re.M))
+
+
+def public_symbols() -> list[str]:
+    """The drop-in boundary: every krk_* function declared in include/kraken_hip.h."""
+    return sorted(_declared(HEADER_PATH))
+
+
+def internal_symbols() -> list[str]:
+    """Benchmark / test / diagnostic hooks declared in include/kraken_hip_internal.h."""
+    return sorted(_declared(INTERNAL_HEADER_PATH))
+
+
+def declared_symbols() -> list[str]:
+    """Every krk_* function either header declares."""
+    return sorted(set(public_symbols()) | set(internal_symbols()))
+
+
+def host_cpu_budget() -> tuple[int, int, str]:
+    """(this process's host CPU budget, the node's CPUs, where the budget came from):
+    krk_host_cpu_budget, no device needed."""
+    cpus, node = C.c_int(), C.c_int()
+    src = C.create_string_buffer(64)
+    check(lib.krk_host_cpu_budget(C.byref(cpus), C.byref(node), src, 64))
+    return cpus.value, node.value, src.value.decode()

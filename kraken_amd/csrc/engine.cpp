@@ -970,17 +970,23 @@ unsigned host_threads() {
     return (unsigned)std::max(1, host_cpu_budget());
 }
 
-// Live digesters up to which new ones run on their caller's thread: where the host's
-// aggregate (threads x ~2 GB/s SHA-NI) still beats the GPU's (streams x ~59 MB/s),
-// i.e. 40 streams per host thread.  KRK_DIGESTER_HOST_STREAMS / krk_set_digester_host_streams.
+// Live digesters up to which new ones run on their caller's thread: below the crossover
+// where the GPU engine's aggregate (live streams x the planner's per-stream rate, capped by
+// the host link) overtakes the host's (the CPU budget x one thread's SHA-NI rate), both
+// from the calling thread's device's planner rates (offload.cpp digester_crossover; the
+// nominal ones without a device).  KRK_DIGESTER_HOST_STREAMS / krk_set_digester_host_streams
+// pin it.
 int64_t host_stream_limit() {
-    int64_t v = g_host_streams.load(std::memory_order_relaxed);
+    const int64_t v = g_host_streams.load(std::memory_order_relaxed);
     if (v >= 0) return v;
-    const char* e = getenv("KRK_DIGESTER_HOST_STREAMS");
-    v = e && *e ? strtoll(e, nullptr, 10) : int64_t(40) * host_threads();
-    int64_t expect = -1;
-    g_host_streams.compare_exchange_strong(expect, v);
-    return g_host_streams.load(std::memory_order_relaxed);
+    static const int64_t env = [] {
+        const char* e = getenv("KRK_DIGESTER_HOST_STREAMS");
+        return e && *e ? std::max<int64_t>(0, strtoll(e, nullptr, 10)) : int64_t(-1);
+    }();
+    if (env >= 0) return env;
+    int drc = KRK_OK;
+    const int64_t x = digester_crossover(planner_rates(device(&drc)), (int)host_threads());
+    return x == INT64_MAX ? x : x - 1;
 }
 
 }  // namespace
@@ -1233,6 +1239,12 @@ void krk_digester_free(krk_digester* d) {
 
 int krk_set_digester_host_streams(int64_t n) {
     g_host_streams.store(n < 0 ? -1 : n);
+    return KRK_OK;
+}
+
+int krk_digester_host_streams(int64_t* n) {
+    KRK_CHECK(n, KRK_EINVAL, "n is NULL");
+    *n = host_stream_limit();
     return KRK_OK;
 }
 

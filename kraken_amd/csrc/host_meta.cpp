@@ -18,7 +18,7 @@
 #include <immintrin.h>
 #endif
 
-#include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h"
 
 namespace krk {
 void set_error(int code, const char* fmt, ...);

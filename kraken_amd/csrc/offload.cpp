@@ -312,6 +312,33 @@ Rates planner_rates(Device* D) {
 // pinned H2D rate (C2 end-to-end 45.7-54.4 GB/s against 54 GB/s pinned).
 double host_link(const Rates& R) { return 0.85 * R.h2d; }
 
+// The AUTO Digester crossover (engine.cpp host_stream_limit): m live digesters on the
+// host run SHA-NI on their writers' threads, min(m, threads) x one thread's rate; on the
+// GPU their pending slots are coalesced into multi-stream launches that read the pinned
+// slots in place, m x the tier's per-stream rate (x kEngineEff: the engine's launches
+// start and end with the writers, measured 0.93 of the batch kernel's rate at 256
+// digesters, profiles/r04/bench_engine.json) up to the tier's residency, capped by the
+// host link.  The crossover is the smallest m whose GPU aggregate beats the host's; none
+// (the host out-hashes the link) is INT64_MAX: every AUTO digester stays on the host.
+constexpr double kEngineEff = 0.93;
+double engine_gpu_bps(uint64_t m, const Rates& R) {
+    if (!m) return 0;
+    const int t = tier_of(m, R.cus);
+    const double r = R.stream[t] * kEngineEff;
+    return std::min({(double)m * r, (double)kResidentPerCu[t] * R.cus * r, host_link(R)});
+}
+int64_t digester_crossover(const Rates& R, int threads) {
+    const double host = std::max(1, threads) * R.host_sha;
+    for (int t = 0; t < 3; ++t) {  // the first m (tier by tier) with m x r > host
+        const uint64_t lo = t == 0 ? 1 : kTierMaxPerCu[t - 1] * (uint64_t)R.cus + 1;
+        const uint64_t hi = t < 2 ? kTierMaxPerCu[t] * (uint64_t)R.cus : UINT64_MAX / 2;
+        const double r = R.stream[t] * kEngineEff;
+        const uint64_t m = std::max<uint64_t>(lo, (uint64_t)(host / r) + 1);
+        if (m <= hi && engine_gpu_bps(m, R) > host) return (int64_t)m;
+    }
+    return INT64_MAX;
+}
+
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode) {
     std::vector<uint32_t> order(n);
@@ -381,25 +408,53 @@ int offload_threads(int mode) {
     return mode == kOffDevice ? budget : std::max(1, budget / 4);
 }
 
-int host_cpu_budget() {
-    static const int n = [] {
-        int c = 1;
-        cpu_set_t set;
-        c = sched_getaffinity(0, sizeof set, &set) == 0 ? std::max(1, CPU_COUNT(&set))
+// The node's CPUs as this process sees them: its affinity mask capped by the cgroup v2 CPU
+// quota (the GPU boxes expose the whole machine in the mask but grant a share of it).
+static int node_cpu_count() {
+    cpu_set_t set;
+    int c = sched_getaffinity(0, sizeof set, &set) == 0 ? std::max(1, CPU_COUNT(&set))
                                                         : (int)std::max(1u, std::thread::hardware_concurrency());
-        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota> <period>" or "max <period>"
-            char q[32] = {0};
-            long long per = 0;
-            if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
-                c = std::min<int>(c, std::max<long long>(1, atoll(q) / per));
-            fclose(f);
-        }
-        if (const char* e = getenv("OMP_NUM_THREADS"))
-            if (atoi(e) > 0) c = std::min(c, atoi(e));
-        return c;
-    }();
-    return n;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // "<quota> <period>" or "max <period>"
+        char q[32] = {0};
+        long long per = 0;
+        if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+            c = std::min<int>(c, std::max<long long>(1, atoll(q) / per));
+        fclose(f);
+    }
+    return c;
 }
+
+static int env_pos(const char* k) {
+    const char* e = getenv(k);
+    return e && atoi(e) > 0 ? atoi(e) : 0;
+}
+
+struct CpuBudget {
+    int cpus, node;
+    const char* source;
+};
+
+// One process per GPU (origin/cmd/cmd.go:164 runs one origin a host; bench.py and
+// torch.distributed.run start one rank a GPU): the ranks of a node share its CPUs.
+//   KRK_HOST_CPUS            an operator's explicit per-process budget;
+//   LOCAL_WORLD_SIZE > 1     the node's CPUs / the ranks on it -- a launcher's
+//                            OMP_NUM_THREADS (torch.distributed.run sets 1 a rank) is
+//                            about OpenMP pools, not this library's hash threads;
+//   otherwise                the node's CPUs, capped by OMP_NUM_THREADS when set.
+static const CpuBudget& cpu_budget() {
+    static const CpuBudget b = [] {
+        const int node = node_cpu_count();
+        if (int x = env_pos("KRK_HOST_CPUS")) return CpuBudget{x, node, "KRK_HOST_CPUS"};
+        if (int w = env_pos("LOCAL_WORLD_SIZE"); w > 1)
+            return CpuBudget{std::max(1, node / w), node, "node/LOCAL_WORLD_SIZE"};
+        if (int o = env_pos("OMP_NUM_THREADS"); o > 0 && o < node)
+            return CpuBudget{o, node, "OMP_NUM_THREADS"};
+        return CpuBudget{node, node, "node"};
+    }();
+    return b;
+}
+
+int host_cpu_budget() { return cpu_budget().cpus; }
 
 // Hash blobs (device pointers, lengths) on up to `threads` host threads; digest j to
 // out + 32 j.  The D2H copies start once `ready` (recorded on the caller's stream: the
@@ -777,6 +832,14 @@ int krk_sha_offload_plan(const uint64_t* lengths, uint64_t n, int threads, int c
                          uint64_t* n_host, double* gpu_seconds_out, double* host_seconds_out) {
     return krk_host_offload_plan(lengths, n, threads, cus, KRK_OFFLOAD_DEVICE, host_idx, n_host, gpu_seconds_out,
                                  host_seconds_out);
+}
+
+int krk_host_cpu_budget(int* cpus, int* node_cpus, char* source, uint32_t cap) {
+    const CpuBudget& b = cpu_budget();
+    if (cpus) *cpus = b.cpus;
+    if (node_cpus) *node_cpus = b.node;
+    if (source && cap) snprintf(source, cap, "%s", b.source);
+    return KRK_OK;
 }
 
 }  // extern "C"

@@ -18,7 +18,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h"
 #include "crc_math.hpp"
 #include "kernels.hpp"
 
@@ -715,7 +715,10 @@ struct Rates {
 };
 Rates planner_rates(Device* D);  // D == nullptr: the override or the nominal rates
 int calibrate_device(Device* D);  // (re)measure D's rates now (krk_init, krk_planner_calibrate)
-int host_cpu_budget();           // CPUs this process may use: affinity, cgroup quota, OMP_NUM_THREADS
+// Host CPUs this process may use (offload.cpp): KRK_HOST_CPUS, else the node's CPUs
+// (affinity capped by the cgroup quota) / LOCAL_WORLD_SIZE under a launcher, else the
+// node's capped by OMP_NUM_THREADS.
+int host_cpu_budget();
 // Host threads a call on this thread may use (0: host_cpu_budget()): a *_multi worker runs
 // with its share of the budget, so N devices' workers do not start N x 16 copy threads.
 inline thread_local int t_host_share = 0;
@@ -760,6 +763,11 @@ uint32_t host_crc32_update_par(uint32_t crc, const uint8_t* p, size_t n);
 // crossover; -1 with *rc set when GPU is forced and no device is usable.
 int resolve_crc_placement(int placement, int* rc);
 double host_link(const Rates& R);
+// GPU-placed digesters' modelled aggregate for m live streams, and the AUTO Digester
+// crossover: the fewest live digesters whose GPU aggregate beats `threads` host SHA-NI
+// threads (INT64_MAX: never) -- offload.cpp.
+double engine_gpu_bps(uint64_t m, const Rates& R);
+int64_t digester_crossover(const Rates& R, int threads);
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode = kOffDevice);
 void offload_teardown(Device& D);  // krk_shutdown: the offload threads' streams and pinned buffers

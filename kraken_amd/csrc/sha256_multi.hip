@@ -22,7 +22,7 @@
 #include <atomic>
 #include <mutex>
 
-#include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h"
 #include "kernels.hpp"
 #include "device_util.hpp"
 

@@ -3,9 +3,11 @@
  * No Go toolchain exists in this image, so the Go files there cannot be compiled; this
  * program makes exactly the C calls they make, with the same argument shapes (C-allocated
  * arrays, pinned receive buffers, the two-phase krk_piece_stream_end, a failing write that
- * must surface from crc32_update), and checks every result against the library's host
- * primitives (krk_host_sha256 / krk_host_crc32_update, themselves checked against
- * hashlib / zlib by tests/test_capi_cpu.py).
+ * must surface from crc32_update), and checks every result against the CPU oracle
+ * (oracle/oracle.c, linked as the checker only: orc_sha256 / orc_crc32_update, pinned by
+ * the reference's KATs and zlib / hashlib in tests/test_oracle_golden.py).  The binding
+ * calls use include/kraken_hip.h only; kraken_hip_internal.h is included for one
+ * test-side check (which windows went up straight from the caller's pages).
  *
  *   bindings <scratch dir>      exit 0 = every binding shape worked and agreed */
 #include <stdint.h>
@@ -14,6 +16,8 @@
 #include <string.h>
 
 #include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h" /* krk_windows_last_*: test-side check only */
+#include "../../oracle/oracle.h"               /* the checker */
 
 static int fails = 0;
 #define CHECK(cond, ...)                                        \
@@ -34,11 +38,7 @@ static uint8_t next_byte(void) {
     return (uint8_t)rng;
 }
 
-static uint32_t host_crc(uint32_t c, const uint8_t* p, uint64_t n) {
-    uint32_t o = 0;
-    krk_host_crc32_update(c, p, n, &o);
-    return o;
-}
+static uint32_t host_crc(uint32_t c, const uint8_t* p, uint64_t n) { return orc_crc32_update(c, p, n); }
 
 int main(int argc, char** argv) {
     const char* dir = argc > 1 ? argv[1] : "/tmp";
@@ -132,7 +132,7 @@ int main(int argc, char** argv) {
         CHECK(krk_piece_sums_files(fb, NF, all2) == KRK_OK, "piece_sums_files");
         for (int i = 0; i < NF; ++i) {
             uint8_t want[32];
-            krk_host_sha256(blob, flen[i], want);
+            orc_sha256(blob, flen[i], want);
             CHECK(memcmp(dg + 32 * i, want, 32) == 0, "file digest %d", i);
             const uint64_t np = krk_num_pieces(flen[i], (int64_t)P);
             for (uint64_t k = 0; k < np; ++k) {
@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
               "direct windows %d of %d", direct, windows);
         for (int i = 0; i < NB; ++i) {
             uint8_t want[32];
-            krk_host_sha256(bl[i].data, bl[i].length, want);
+            orc_sha256(bl[i].data, bl[i].length, want);
             CHECK(memcmp(dg + 32 * i, want, 32) == 0, "pinned digest %d", i);
             CHECK(sums[bl[i].sums_offset] == host_crc(0, bl[i].data, 1 << 20), "pinned piece %d", i);
             CHECK(sums[bl[i].sums_offset + 1] == host_crc(0, bl[i].data + (1 << 20), bl[i].length - (1 << 20)) ||
@@ -194,11 +194,11 @@ int main(int argc, char** argv) {
         CHECK(krk_digester_write(d, blob, 32768) == KRK_OK, "write");
         uint8_t a[32], b[32], w[32];
         CHECK(krk_digester_sum(d, a) == KRK_OK, "sum");
-        krk_host_sha256(blob, 32768, w);
+        orc_sha256(blob, 32768, w);
         CHECK(memcmp(a, w, 32) == 0, "digest");
         CHECK(krk_digester_write(d, blob + 32768, L - 32768) == KRK_OK, "write after Digest()");
         CHECK(krk_digester_sum(d, b) == KRK_OK, "sum 2");
-        krk_host_sha256(blob, L, w);
+        orc_sha256(blob, L, w);
         CHECK(memcmp(b, w, 32) == 0, "digest continues");
         krk_digester_free(d);
     }

@@ -29,7 +29,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h"
 
 namespace {
 

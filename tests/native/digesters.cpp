@@ -23,7 +23,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h"
 
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 256;

@@ -43,9 +43,11 @@ def test_bench_gpus_2_spawns_two_ranks(gpu):
     self-verifying -- rank 0's CPU baseline (timed after the GPU region while the other
     ranks wait), every rank's device PCI bus id and own time; here both ranks share the
     one GPU, which only a rehearsal may."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")  # what torch.distributed.run gives each rank of a node
+    env.pop("KRK_HOST_CPUS", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse", "--blobs", "20",
                         "--steps", "1", "--warmup", "1", "--cpu-seconds", "1", "--no-e2e", "--no-ceiling"],
-                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # only rank 0 prints
@@ -58,6 +60,12 @@ def test_bench_gpus_2_spawns_two_ranks(gpu):
     assert len(d["rank_ms"]) == 2 and abs(max(d["rank_ms"]) - d["ms_per_step"] * d["steps"]) < 1e-2
     cb = d["cpu_baseline"]
     assert cb["cores"] >= 1 and cb["value"] > 0 and cb["outputs_match_gpu"] is True
+    # each rank's library budget is the node's CPUs / LOCAL_WORLD_SIZE
+    # (a launcher's OMP_NUM_THREADS=1 does not shrink it); rank 0's baseline runs on the node
+    hb = d["host_budget"]
+    node = hb["node_cpus"]
+    assert hb["rank_cpus"] == [max(1, node // 2)] * 2 and hb["source"] == "node/LOCAL_WORLD_SIZE", hb
+    assert cb["cores"] == min(node, 20), (cb["cores"], node)
 
 
 def test_bench_gpus_more_than_visible_refused(gpu):

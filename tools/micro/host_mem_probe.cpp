@@ -27,7 +27,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/kraken_hip.h"
+#include "../../include/kraken_hip_internal.h"
 
 namespace {
 double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
