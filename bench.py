@@ -121,6 +121,9 @@ WORKLOADS = {
                   desc="upload / cache-fill verify + metainfo from CAS files (uploader.go:74-94 + generator.go:41-58):"
                        " 16,384 blobs of the C3 length law / 64 (1.6-16.8 MB, 151 GB a pass), each a prefix of one of"
                        " 64 source files, 4 MiB pieces; every byte read once (pread -> pinned windows -> PCIe)"),
+    "defaults": dict(kind="defaults", steps=3, warmup=0,
+                     desc="the library's defaults, no knobs: one 1 GiB blob (C1) through krk_metainfo_digest_dev "
+                          "and one 1 GiB NewMetaInfo piece stream of 4 MiB reads, each against one host thread"),
     "c5": dict(kind="hrw", steps=50, warmup=5,  # 0.4 ms steps: a few would time launch jitter
                desc="C5: 1M seeded 32-B digests -> hashring.Locations (ShardID key), "
                     "16 origins weight 100, MaxReplica 3, all healthy"),
@@ -1495,6 +1498,111 @@ def run_files(a, D, T, rank, world, res):
         res["cpu_baseline"] = cb
 
 
+# The library's DEFAULTS in a fresh process (no knob, no KRK_ environment): a C1-shaped
+# batch through krk_metainfo_digest_dev and one 1 GiB NewMetaInfo piece stream of 4 MiB
+# reads, against one host thread's SHA-NI / PCLMUL time of the same bytes.  The outputs and
+# placements are asserted here (tests/test_gpu_defaults.py runs it as a parity test); the
+# times are the `--workload defaults` line's.
+DEFAULTS_PROBE = r"""
+import ctypes as C, hashlib, json, sys, time, zlib
+import numpy as np
+sys.path.insert(0, ".")
+from kraken_amd import device as D
+from kraken_amd._capi import KRK_OFFLOAD_AUTO, KRK_PLACE_HOST, check, lib
+RUNS = int(sys.argv[1])
+D.set_device(0)
+t = C.c_int(0)
+check(lib.krk_sha_host_offload(C.byref(t)))
+assert t.value == KRK_OFFLOAD_AUTO, t.value
+L, P = 1 << 30, 4 << 20
+arena = D.BlobArena([L], P, blob_ids=[7])
+out = D.BatchOutputs(arena)
+host = arena.buf.to_host(np.uint8, L)
+res = {"blob_bytes": L, "piece_length": P, "runs": RUNS}
+
+def best(f, k=RUNS):
+    ts = []
+    for _ in range(k):
+        t0 = time.perf_counter(); f(); ts.append(time.perf_counter() - t0)
+    return min(ts)
+# one host thread, the same bytes: SHA-NI (krk_host_sha256) and PCLMUL (krk_host_crc32_update)
+o32 = (C.c_uint8 * 32)()
+res["host_sha_1thread_s"] = best(lambda: lib.krk_host_sha256(host.ctypes.data, L, o32))
+want_dg = hashlib.sha256(host).digest()
+assert bytes(o32) == want_dg
+c = C.c_uint32()
+res["host_crc_1thread_s"] = best(lambda: lib.krk_host_crc32_update(0, host.ctypes.data, L, C.byref(c)))
+assert c.value == zlib.crc32(host)
+
+def c1():  # C1 through the device-resident drop-in, defaults
+    D.metainfo_digest(arena, out)
+    D.synchronize()
+res["c1_metainfo_digest_dev_s"] = best(c1)
+dg = out.digests.to_host(np.uint8, 32)
+sums = out.sums.to_host(np.uint32, arena.total_pieces)
+want_sums = [zlib.crc32(host[i:i + P]) for i in range(0, L, P)]
+assert bytes(dg) == want_dg
+assert sums.tolist() == want_sums
+res["digest_ok"] = res["sums_ok"] = True
+
+placement = []
+def stream():  # one NewMetaInfo stream, 4 MiB reads, defaults
+    s = C.c_void_p()
+    check(lib.krk_piece_stream_begin(P, C.byref(s)))
+    w = C.c_int(-1)
+    check(lib.krk_piece_stream_placement(s, C.byref(w)))
+    placement.append(w.value)
+    base = host.ctypes.data
+    for a in range(0, L, 4 << 20):
+        check(lib.krk_piece_stream_update(s, base + a, min(4 << 20, L - a)))
+    ns, ln = C.c_uint64(), C.c_uint64()
+    got = (C.c_uint32 * 256)()
+    check(lib.krk_piece_stream_end(s, got, 256, C.byref(ns), C.byref(ln)))
+    lib.krk_piece_stream_free(s)
+    assert ns.value == 256 and ln.value == L
+    stream.sums = list(got)
+res["stream_s"] = best(stream)
+assert stream.sums == want_sums
+assert all(p == KRK_PLACE_HOST for p in placement), placement
+res["stream_placement"] = "host"
+res["stream_GBps"] = L / res["stream_s"] / 1e9
+res["host_crc_1thread_GBps"] = L / res["host_crc_1thread_s"] / 1e9
+res["host_sha_1thread_GBps"] = L / res["host_sha_1thread_s"] / 1e9
+res["c1_GBps"] = L / res["c1_metainfo_digest_dev_s"] / 1e9
+res["c1_ratio_to_host_sha"] = res["c1_metainfo_digest_dev_s"] / res["host_sha_1thread_s"]
+print(json.dumps(res))
+"""
+
+
+def run_defaults_probe(runs=3):
+    """DEFAULTS_PROBE in a fresh child process with every KRK_ variable removed."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("KRK_")}
+    r = subprocess.run([sys.executable, "-c", DEFAULTS_PROBE, str(runs)], capture_output=True, text=True, cwd=ROOT,
+                       env=env, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError("defaults probe failed: " + r.stdout[-2000:] + r.stderr[-3000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def run_defaults(a, D, T, rank, world, res):
+    """The library's defaults on the two single-stream drop-ins (C1's NewMetaInfo + digest,
+    one NewMetaInfo piece stream), each the best of `steps` runs in a fresh process, against
+    one host thread of the reference's own placement on the same bytes.  value = C1 GB/s
+    with the defaults; the line carries the VERDICT r03 item 1 criteria as measured booleans
+    (C1 within 1.2x of one SHA-NI thread, the stream at least one PCLMUL thread)."""
+    p = run_defaults_probe(runs=max(1, a.steps))
+    el = T.timed_region(p["c1_metainfo_digest_dev_s"])
+    res.update({"metric": "defaults: C1 NewMetaInfo+digest GB/s (library defaults, fresh process)",
+                "value": round(world * p["blob_bytes"] / el / 1e9, 3), "unit": "GB/s", "steps": a.steps,
+                "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak", "dtype": "u8",
+                "data": "synthetic (device-generated splitmix64 blob)",
+                "config": {"workload": WORKLOADS[a.workload]["desc"], "blob_bytes": p["blob_bytes"],
+                           "piece_length": p["piece_length"], "knobs": "none (KRK_ environment removed)"},
+                "defaults": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in p.items()},
+                "criteria": {"c1_within_1.2x_one_sha_thread": p["c1_ratio_to_host_sha"] <= 1.2,
+                             "stream_at_least_one_crc_thread": p["stream_GBps"] >= p["host_crc_1thread_GBps"]}})
+
+
 def run_engine(a, D, T, rank, world, res):
     """The submission engine under concurrent Digesters: tests/native/digesters
     runs warmup + steps rounds of 256 GPU-placed digesters (a round = every digester's 16 MiB
@@ -1649,7 +1757,7 @@ def main():
         res["rehearsal"] = f"{world} ranks on {ndev} device(s): not an N-GPU measurement"
     kind = WORKLOADS[a.workload]["kind"]
     {"metainfo": run_metainfo, "pieces": run_pieces, "chunked": run_chunked, "hrw": run_hrw, "regen": run_regen,
-     "verify": run_verify, "engine": run_engine, "files": run_files}[kind](
+     "verify": run_verify, "engine": run_engine, "files": run_files, "defaults": run_defaults}[kind](
         a, D, T, rank, world, res)
     # rank 0's CPU baseline (if any) ran after the timed region, behind this barrier the
     # other ranks wait at; then every rank's device and time go into the line, so an N-GPU

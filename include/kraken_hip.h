@@ -205,10 +205,13 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *   KRK_PLACE_HOST  SHA-NI on the caller's thread (host_meta.cpp): ~2 GB/s per stream
  *                   against ~59 MB/s for one GPU stream.
  *   KRK_PLACE_AUTO  (krk_digester_new) HOST while at most N digesters are live in the
- *                   process, GPU beyond: the crossover where the host's aggregate
- *                   (threads x ~2 GB/s) stops beating the GPU's (streams x ~59 MB/s).
- *                   N = 40 x the CPUs this process may use, or KRK_DIGESTER_HOST_STREAMS,
- *                   or krk_set_digester_host_streams (-1 restores the default).
+ *                   process, GPU beyond.  N is the crossover computed from the calling
+ *                   thread's device's planner rates: the fewest live GPU digesters whose
+ *                   aggregate (live streams x the measured per-stream rate of the launch
+ *                   plan they get, capped by the host link) beats the host's (the process's
+ *                   CPU budget x one thread's measured SHA-NI rate); never (all on the host)
+ *                   when the host out-hashes the link.  KRK_DIGESTER_HOST_STREAMS or
+ *                   krk_set_digester_host_streams pins N (-1 restores the default).
  * HOST placement needs no device; GPU placement without a gfx950 device is KRK_ENODEV and
  * AUTO without one is HOST (the product's own SHA-NI path, not the oracle). */
 typedef struct krk_digester krk_digester;

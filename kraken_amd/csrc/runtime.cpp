@@ -414,7 +414,7 @@ static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blob
             const krk_blob& b = blobs[bi];
             const uint64_t take = std::min<uint64_t>(b.length - boff, W - fill);
             if (take) {
-                copies.push_back({(direct ? w.dev : w.host) + fill, b.data + boff, take});
+                copies.push_back({w.host + fill, b.data + boff, take});
                 B.add(items, reinterpret_cast<uint64_t>(w.dev + fill), boff, boff + take, b.length,
                       (uint64_t)b.piece_length, b.sums_offset);
             }
@@ -424,7 +424,12 @@ static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blob
             fill = (fill + 15) & ~size_t(15);
             if (boff >= b.length) { ++bi; boff = 0; }
         }
-        const hipError_t up = direct ? pl.h2d_direct(k, copies, cp) : (par_copy(copies), pl.h2d(k, std::min(fill, W), cp));
+        // pinned bytes go up straight from the caller's pages only in windows of few copies
+        // (many small DMAs cost more than the staging copy, windows.cpp kDirectMaxCalls)
+        const bool dw = direct && copies.size() <= kDirectMaxCalls;
+        if (dw)
+            for (CopyTask& c : copies) c.dst = w.dev + (c.dst - w.host);
+        const hipError_t up = dw ? pl.h2d_direct(k, copies, cp) : (par_copy(copies), pl.h2d(k, std::min(fill, W), cp));
         if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "piece_sums_host: staging copy failed");
             r = KRK_EHIP;
@@ -704,6 +709,14 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
             hi = std::max(hi, files[i].sums_offset + np);
         }
     }
+    // An empty file has no piece to read, but Generate opens it (GetCacheFileReader,
+    // lib/metainfogen/generator.go:47-49): a missing or unreadable one fails.
+    for (uint64_t i = 0; i < n; ++i)
+        if (files[i].length == 0) {
+            const int fd = open(files[i].path, O_RDONLY | O_CLOEXEC);
+            KRK_CHECK(fd >= 0, KRK_EIO, "open %s: %s", files[i].path, strerror(errno));
+            close(fd);
+        }
     if (hi == 0) return KRK_OK;
     KRK_CHECK(sums_host, KRK_EINVAL, "sums_host is NULL");
     // CRC placement (krk_set_crc_placement, else the measured crossover; HOST without a device)

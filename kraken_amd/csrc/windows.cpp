@@ -18,6 +18,7 @@
 #include <dirent.h>
 #include <sys/resource.h>
 
+#include <condition_variable>
 #include <deque>
 #include <thread>
 
@@ -140,9 +141,11 @@ struct FileFiller : Filler {
     int fill(const std::vector<Task>& tasks) override {
         std::vector<ReadTask> plain, odirect;
         for (const Task& t : tasks) {
-            if (!t.len) continue;
+            // every file is opened, an empty one too: Generate / verify open the file and
+            // fail on a missing one
             int r = open_file(t.b);
             if (r) return r;
+            if (!t.len) continue;
             (is_direct[t.b] ? odirect : plain).push_back({fd[t.b], t.off, t.dst, (size_t)t.len, (size_t)t.b});
         }
         for (int pass = 0; pass < 2; ++pass) {
@@ -166,19 +169,66 @@ struct FileFiller : Filler {
     }
 };
 
-// File descriptors this call may hold open at once: the soft RLIMIT_NOFILE less those
-// already open and a reserve for the rest of the process.
-uint64_t fd_budget() {
-    struct rlimit rl {};
-    if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return uint64_t(1) << 20;
-    uint64_t open_now = 0;
-    if (DIR* d = opendir("/proc/self/fd")) {
-        while (readdir(d)) ++open_now;
-        closedir(d);
+// File descriptors the file batches may hold open, shared by the whole process (ADVICE r04:
+// every *_multi worker and every concurrent caller took the whole remaining budget for
+// itself): the soft RLIMIT_NOFILE less the descriptors open at first use and a reserve for
+// the rest of the process, handed out in leases.  A call waits only while every descriptor
+// is leased, and then takes at least one.
+class FdPool {
+  public:
+    uint64_t acquire(uint64_t want) {
+        std::unique_lock<std::mutex> g(mu_);
+        if (!init_) {
+            free_ = total_ = initial_budget();
+            init_ = true;
+        }
+        cv_.wait(g, [&] { return free_ > 0; });
+        const uint64_t take = std::max<uint64_t>(1, std::min(want, free_));
+        free_ -= take;
+        return take;
     }
-    const uint64_t reserve = 64 + open_now;
-    return rl.rlim_cur > reserve + 16 ? rl.rlim_cur - reserve : 16;
+    void release(uint64_t n) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            free_ += n;
+        }
+        cv_.notify_all();
+    }
+    uint64_t total() {
+        std::lock_guard<std::mutex> g(mu_);
+        return init_ ? total_ : initial_budget();
+    }
+
+  private:
+    static uint64_t initial_budget() {
+        if (const char* e = getenv("KRK_FD_BUDGET"))  // tests: a small budget without touching the rlimit
+            if (strtoull(e, nullptr, 10) > 0) return strtoull(e, nullptr, 10);
+        struct rlimit rl {};
+        if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return uint64_t(1) << 20;
+        uint64_t open_now = 0;
+        if (DIR* d = opendir("/proc/self/fd")) {
+            while (readdir(d)) ++open_now;
+            closedir(d);
+        }
+        const uint64_t reserve = 64 + open_now;
+        return rl.rlim_cur > reserve + 16 ? rl.rlim_cur - reserve : 16;
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool init_ = false;
+    uint64_t free_ = 0, total_ = 0;
+};
+FdPool& fd_pool() {
+    static FdPool* p = new FdPool();  // leaked: used until exit
+    return *p;
 }
+struct FdLease {
+    uint64_t n;
+    explicit FdLease(uint64_t want) : n(fd_pool().acquire(want)) {}
+    ~FdLease() { fd_pool().release(n); }
+    FdLease(const FdLease&) = delete;
+    FdLease& operator=(const FdLease&) = delete;
+};
 
 struct CallStats {
     uint64_t max_live = 0;
@@ -188,11 +238,6 @@ struct CallStats {
 };
 thread_local CallStats t_last_call;
 
-// A window of page-locked chunks goes to the device as one hipMemcpyAsync a chunk when it has
-// few enough chunks that the calls stay well under the window's transfer.  Windows of
-// thousands of chunks stage instead: measured on MI355X, one hipMemcpyBatchAsync of a
-// window's 14,336 pinned chunks ran at 4.3 GB/s against 50 GB/s staged (profiles/r04).
-constexpr size_t kDirectMaxCalls = 64;
 
 // The windows of one host-resident batch: the blobs not in `skip`, chunk by chunk, into the
 // device's staging windows and through both kernels.  d_sums / d_dig / d_state indexed like
@@ -211,8 +256,12 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
     const uint64_t live_cap = std::min<uint64_t>(cap, blobs.size());
     WindowSched sched(lens, blobs, W, live_cap, align);
     const size_t place = std::max<uint64_t>(align == 64 ? 16 : align, 16);  // chunk start alignment in the window
+    // a window holds about W bytes, but never less than one minimum chunk (the schedule's
+    // alignment) a live blob, each rounded up to `place` (a small KRK_WINDOW_MB
+    // or a large KRK_LIVE_CAP made live x 64 > W + 16 x live)
+    const uint64_t span = std::max<uint64_t>(W, live_cap * std::max<uint64_t>(align, 64)) + place * live_cap;
     StagingLease lease;
-    int r = lease_staging(D, W + place * live_cap, lease);
+    int r = lease_staging(D, span, lease);
     if (r) return r;
     Pipeline& pl = *lease.p;
     hipStream_t cp = D->s_main, ks = D->s_a, kc = D->s_b;
@@ -251,6 +300,12 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
             jobs.push_back(j);
             fill += (c.len + place - 1) / place * place;
         }
+        if (fill > w.cap) {  // the lease covers every window the schedule can build
+            set_error(KRK_EINVAL, "metainfo windows: window of %zu bytes exceeds the %zu-byte staging lease", fill,
+                      (size_t)w.cap);
+            r = KRK_EINVAL;
+            break;
+        }
         const double tc = wall_s();
         t_build += tc - tb;
         // page-locked sources are DMA'd straight from the caller's memory into the device
@@ -270,7 +325,7 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         t_fill += td - tc;
         ++st->windows;
         st->direct_windows += direct;
-        const hipError_t up = direct ? pl.h2d_direct(k, dma, cp) : pl.h2d(k, std::min(fill, pl.w[k].cap), cp);
+        const hipError_t up = direct ? pl.h2d_direct(k, dma, cp) : pl.h2d(k, fill, cp);
         if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
             (crc && hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess)) {
             set_error(KRK_EHIP, "metainfo windows: staging copy failed");
@@ -608,9 +663,10 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     const bool direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
     FileFiller filler(files, n, direct);
     CallStats st;
-    // at most as many live blobs as this call may hold files open
-    const uint64_t cap = std::min(live_cap_for(D), fd_budget());
-    r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, cap,
+    // at most as many live blobs as this call holds file descriptors (a lease of the
+    // process's budget, shared with every other file batch running now)
+    FdLease fds(std::min<uint64_t>(live_cap_for(D), n));
+    r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, fds.n,
                      o.d_sums, o.d_dig, o.d_state, &st);
     // drain what was queued even after a read error (the windows' kernels read the buffers)
     const bool synced = hipStreamSynchronize(D->s_a) == hipSuccess && hipStreamSynchronize(D->s_b) == hipSuccess &&

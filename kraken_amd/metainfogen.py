@@ -96,12 +96,17 @@ class DirCAS:
     def MoveUploadFileToCache(self, upload_path: str, hex_: str) -> None:
         """CAStore.MoveUploadFileToCache (origin/blobserver/uploader.go:98 commit): the
         verified upload file renamed into the cache; FileExistsError when the blob is
-        already cached (the uploader's 409)."""
+        already cached (the uploader's 409).  The upload file is deleted either way
+        (lib/store/ca_store.go:79-86: `defer s.DeleteUploadFile(uploadName)`)."""
         dst = os.path.join(self._dir(hex_), "data")
         os.makedirs(self._dir(hex_), exist_ok=True)
-        if os.path.exists(dst):
-            raise FileExistsError(dst)
-        os.replace(upload_path, dst)
+        try:
+            if os.path.exists(dst):
+                raise FileExistsError(dst)
+            os.replace(upload_path, dst)
+        finally:
+            if os.path.exists(upload_path):
+                os.remove(upload_path)
 
     def WriteCacheFile(self, data: bytes) -> core.Digest:
         d = core.NewDigester().FromBytes(data)
@@ -248,8 +253,11 @@ class Generator:
         sums.  uploads: [(core.Digest expected, upload file path)].  A file that cannot be
         read fails the batch with uploader.verify's prefixes ("get upload file: ...",
         "calculate digest: read blob: <path>: ..."); a digest mismatch is that upload's
-        ValueError; verified files are moved into the CAS with their _torrentmeta.  Returns
-        [MetaInfo | ValueError] in input order."""
+        ValueError; verified files are moved into the CAS with their _torrentmeta.  A verified
+        upload whose blob is already cached -- or an earlier upload of the same batch put it
+        there -- is that upload's FileExistsError (uploader.commit's 409, uploader.go:96-104),
+        its upload file deleted as the reference does, and the batch goes on.  Returns
+        [MetaInfo | ValueError | FileExistsError] in input order."""
         from . import device as D
         from ._capi import KrakenError
         paths, sizes = [], []
@@ -270,13 +278,18 @@ class Generator:
             if got != want:
                 out.append(ValueError(f"computed digest {got.String()} doesn't match parameter {want.String()}"))
                 continue
-            self.cas.MoveUploadFileToCache(p, want.Hex())
+            try:
+                self.cas.MoveUploadFileToCache(p, want.Hex())
+            except FileExistsError as e:
+                out.append(e)  # 409 Conflict for this upload only
+                continue
             out.append((want, pl, s.copy() if s.size else None, int(n)))
         return self._commit_metainfo(out)
 
     def _commit_metainfo(self, out):
-        """The verified uploads' InfoHashes in one batched call and their sidecars."""
-        ok = [k for k, o in enumerate(out) if not isinstance(o, ValueError)]
+        """The committed uploads' InfoHashes in one batched call and their sidecars (entries
+        that are errors -- digest mismatch, conflict -- pass through)."""
+        ok = [k for k, o in enumerate(out) if isinstance(o, tuple)]
         if ok:
             flat = [out[k][2] for k in ok if out[k][2] is not None]
             allsums = np.concatenate(flat) if flat else np.zeros(0, np.uint32)

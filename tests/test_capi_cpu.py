@@ -487,6 +487,12 @@ def test_piece_sums_files_host_placement(tmp_path):
         bad = (krk_file_blob * 1)(krk_file_blob(missing, 5, 1 << 20, 0))
         assert lib.krk_piece_sums_files(bad, 1, sums.ctypes.data_as(C.POINTER(C.c_uint32))) == _capi.KRK_EIO
         assert lib.krk_last_error() == b"open " + missing + b": No such file or directory"
+        # an EMPTY missing file fails too (Generate opens the file before reading)
+        bad = (krk_file_blob * 2)(krk_file_blob(paths[1], 1, 1 << 20, 0), krk_file_blob(missing, 0, 1 << 20, 1))
+        assert lib.krk_piece_sums_files(bad, 2, sums.ctypes.data_as(C.POINTER(C.c_uint32))) == _capi.KRK_EIO
+        assert lib.krk_last_error() == b"open " + missing + b": No such file or directory"
+        bad = (krk_file_blob * 1)(krk_file_blob(missing, 0, 1 << 20, 0))
+        assert lib.krk_piece_sums_files(bad, 1, sums.ctypes.data_as(C.POINTER(C.c_uint32))) == _capi.KRK_EIO
     finally:
         check(lib.krk_set_crc_placement(_capi.KRK_PLACE_AUTO))
 
@@ -566,3 +572,26 @@ def test_host_hash_work_concurrent_callers_under_cpu_tokens():
         t.join(timeout=120)
     assert not any(t.is_alive() for t in th), "a caller did not finish"
     assert not errors, errors[:3]
+
+
+def test_public_header_is_the_bound_surface():
+    """include/kraken_hip.h declares exactly what INTEGRATION.md's
+    surface table binds (the Go callers' entry points and the operator calls); the
+    benchmark / diagnostic hooks live in include/kraken_hip_internal.h only."""
+    import os
+    import re
+    doc = open(os.path.join(os.path.dirname(_capi.HEADER_PATH), "..", "INTEGRATION.md")).read()
+    a = doc.index("## The exported surface")
+    b = doc.index("\n## ", a + 1)
+    table = set(re.findall(r"`(krk_[a-z0-9_]+)`", doc[a:b]))
+    pub, internal = set(_capi.public_symbols()), set(_capi.internal_symbols())
+    assert pub == table, ("header only", sorted(pub - table), "table only", sorted(table - pub))
+    assert not pub & internal
+    hooks = {"krk_set_sha_plan", "krk_synth_fill_dev", "krk_synth_fill_chunks_dev", "krk_planner_rates_set",
+             "krk_kernel_timeline", "krk_kernel_stats", "krk_set_timing", "krk_window_sched_new",
+             "krk_window_sched_next", "krk_window_sched_free", "krk_windows_last_call", "krk_windows_last_direct",
+             "krk_device_clock_mhz"}
+    assert hooks <= internal, hooks - internal
+    # every function the Go files in INTEGRATION.md call is public
+    called = set(re.findall(r"\bC\.(krk_[a-z0-9_]+)\(", doc))
+    assert called <= pub, called - pub

@@ -302,6 +302,39 @@ def test_verify_and_generate_uploads_from_files(gpu, orc, tmp_path):
         g.VerifyAndGenerateUploads([(want[1], str(up / "missing"))])
 
 
+def test_verify_and_generate_uploads_conflicts(gpu, orc, tmp_path):
+    """a verified upload whose blob is already cached, or a second upload of one
+    digest in the same batch, is that upload's 409 (uploader.commit, origin/blobserver/
+    uploader.go:96-104) with its upload file deleted (ca_store.go:79-86); the batch goes on
+    and every other upload gets its _torrentmeta."""
+    from kraken_amd import metainfogen
+    cas = metainfogen.DirCAS(str(tmp_path / "cas"))
+    up = tmp_path / "upload"
+    up.mkdir()
+    g = metainfogen.New({0: 1 << 20}, cas)
+    blobs = [os.urandom(n) for n in (3_000_001, 12345, 1 << 20)]
+    want = [core.NewSHA256DigestFromHex(hashlib.sha256(b).hexdigest()) for b in blobs]
+    cached = cas.WriteCacheFile(blobs[1])  # blob 1 is in the CAS already
+    assert cached == want[1]
+    order = [0, 1, 2, 0]  # blob 0 twice in the batch
+    ups = []
+    for k, i in enumerate(order):
+        p = up / f"u{k}"
+        p.write_bytes(blobs[i])
+        ups.append((want[i], str(p)))
+    res = g.VerifyAndGenerateUploads(ups)
+    assert isinstance(res[1], FileExistsError) and isinstance(res[3], FileExistsError), res
+    for k in (0, 2):
+        i = order[k]
+        b, d = blobs[i], want[i]
+        assert bytes(res[k].InfoHash()) == orc.info_hash(1 << 20, orc.calc_piece_sums(b, 1 << 20)[1], d.Hex(), len(b))
+        assert open(os.path.join(cas._dir(d.Hex()), "_torrentmeta"), "rb").read() == \
+            core.NewMetaInfo(d, b, 1 << 20).Serialize()
+        assert open(os.path.join(cas._dir(d.Hex()), "data"), "rb").read() == b
+    assert not any(os.path.exists(p) for _, p in ups)  # committed or conflicting: every upload file is gone
+    assert open(os.path.join(cas._dir(want[1].Hex()), "data"), "rb").read() == blobs[1]
+
+
 def _go_json(pl, sums, name, length):
     """encoding/json of metaInfoJSON{info} (core/metainfo.go:125-134), written out
     independently of core.MetaInfo.Serialize: declared field order, compact, nil

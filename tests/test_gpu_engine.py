@@ -146,8 +146,7 @@ def test_256_concurrent_gpu_digesters(gpu):
     print(f"single GPU digester {single / 1e6:.1f} MB/s; 256 concurrent {agg / 1e9:.2f} GB/s "
           f"({agg / n / 1e6:.1f} MB/s a stream, {agg / single:.0f}x); {jobs_per_launch:.1f} streams per SHA launch; "
           f"create {create_ms:.3f} ms")
-    assert create_ms < 1.0
-    assert jobs_per_launch > 8
+    assert jobs_per_launch > 8  # (create_ms is printed, not asserted: no time in the parity gate)
     # (the rate from Python threads is capped by the GIL: their first requests trickle in
     # over ~70 ms; test_256_native_digesters measures the engine from native threads)
 

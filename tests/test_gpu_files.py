@@ -73,6 +73,10 @@ def test_files_errors_keep_reference_texts(gpu, orc, tmp_path):
     with pytest.raises(KrakenError) as e:
         D.metainfo_digest_files([p, missing], [1 << 20, 5], 1 << 20)
     assert e.value.code == KRK_EIO and f"open {missing}: No such file or directory" in str(e.value)
+    # an empty file is opened too -- missing, it fails like the reference
+    with pytest.raises(KrakenError) as e:
+        D.metainfo_digest_files([p, missing], [1 << 20, 0], 1 << 20)
+    assert e.value.code == KRK_EIO and f"open {missing}: No such file or directory" in str(e.value)
     with pytest.raises(KrakenError, match="piece length must be positive"):
         D.metainfo_digest_files([p], [1 << 20], 0)
     # the library is usable after the failures
@@ -96,6 +100,49 @@ def test_files_multi_equals_single(gpu, orc, tmp_path):
 
 
 from ctypes import c_int as C_int  # noqa: E402
+
+_FD_CHILD = r"""
+import hashlib, os, resource, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+from ctypes import c_int
+# the process may hold few descriptors: the library's pool = soft limit - open now - 64
+open_now = len(os.listdir("/proc/self/fd"))
+soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+resource.setrlimit(resource.RLIMIT_NOFILE, (open_now + 64 + 48, hard))
+from kraken_amd import device as D
+from kraken_amd._capi import check, lib
+D.set_device(0)
+D.set_sha_host_offload(0)
+tmp = sys.argv[2]
+lens = [int(x) for x in np.random.default_rng(8).integers(0, 3 << 20, 300)]
+paths = []
+for i, L in enumerate(lens):
+    p = os.path.join(tmp, "fd%d" % i)
+    with open(p, "wb") as f:
+        f.write(O.synth(4000 + i, L).tobytes())
+    paths.append(p)
+check(lib.krk_set_devices((c_int * 6)(0, 0, 0, 0, 0, 0), 6))  # six workers share the one budget
+sums, dg = D.metainfo_digest_files(paths, lens, 1 << 20, multi=True)
+for i in range(0, len(lens), 7):
+    d = O.synth(4000 + i, lens[i])
+    assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), i
+    assert np.array_equal(sums[i], O.calc_piece_sums(d, 1 << 20)[1]), i
+print("fd ok", len(lens))
+"""
+
+
+def test_files_multi_share_one_fd_budget(gpu, tmp_path):
+    """the *_multi workers (and concurrent callers) lease descriptors from ONE
+    process-wide budget; with ~48 descriptors to spare, six workers over 300 files would each
+    have taken the whole budget (EMFILE) before.  Fresh process: the budget is read once."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _FD_CHILD, root, str(tmp_path)], capture_output=True, text=True,
+                       timeout=300, cwd=root)
+    assert r.returncode == 0 and "fd ok 300" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 N, SCALE, P4 = 16384, 64, 4 << 20
 SOURCES = 64  # blob i = a prefix of source i % 64 (1 GB of distinct bytes for 151 GB of blobs)
@@ -328,3 +375,20 @@ def test_concurrent_host_paths_under_cpu_tokens(gpu, orc, tmp_path):
         D.set_sha_host_offload(0)
         D.set_crc_placement(D.PLACE_GPU)
     assert not errors, errors[:3]
+
+
+def test_tiny_window_many_live_blobs(gpu, orc, monkeypatch):
+    """with a 1 MiB window (KRK_WINDOW_MB=1) and 30,000 live blobs
+    (KRK_LIVE_CAP), every live blob still advances by the schedule's 64-byte minimum chunk,
+    1.9 MB a window: the staging lease must hold that, not W + 16 x live."""
+    monkeypatch.setenv("KRK_WINDOW_MB", "1")
+    monkeypatch.setenv("KRK_LIVE_CAP", "30000")
+    lens = [100 + (i % 37) for i in range(30000)]
+    datas = [orc.synth(7000 + i, L) for i, L in enumerate(lens)]
+    D.set_sha_host_offload(0)
+    sums, dg = D.metainfo_digest_host(datas, 64)
+    st = D.windows_last_call()
+    assert st["max_live"] == 30000 and st["windows"] >= 2, st
+    for i in range(0, len(lens), 997):
+        assert bytes(dg[i]) == hashlib.sha256(datas[i].tobytes()).digest(), i
+        assert np.array_equal(sums[i], orc.calc_piece_sums(datas[i], 64)[1]), i
