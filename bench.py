@@ -1608,7 +1608,8 @@ def run_engine(a, D, T, rank, world, res):
     runs warmup + steps rounds of 256 GPU-placed digesters (a round = every digester's 16 MiB
     and its digest); value = the timed rounds' bytes over their summed seconds.  Every digest
     is checked against the host SHA-256 of the same bytes in the child (digests_match).  The
-    rate lives here, not in the parity tests."""
+    rate lives here, not in the parity tests.  Then (unless --no-sweep)
+    the crossover sweep of VERDICT r04 item 4: N concurrent digesters on each placement."""
     exe = os.path.join(ROOT, "tests", "native", "digesters")
     n, mib = 256, 16
     r = subprocess.run([exe, str(n), str(mib), str(a.warmup + a.steps)], capture_output=True, text=True, timeout=900)
@@ -1630,6 +1631,63 @@ def run_engine(a, D, T, rank, world, res):
                 "digests_match": all(x["digests_match"] for x in rounds),
                 "per_stream_ceiling_MBps": "~59 (the eight-lane batch kernel, DESIGN.md 4.2): 256 x 59 MB/s = "
                                            "15.1 GB/s"})
+    if not a.no_sweep:
+        res["crossover"] = digester_crossover_sweep(exe, mib)
+
+
+ENGINE_SWEEP = (256, 640, 1024, 2048, 4096)
+
+
+def digester_crossover_sweep(exe, mib, sizes=ENGINE_SWEEP, threads=256):
+    """N concurrent Digesters (one per upload / cache fill,
+    origin/blobserver/uploader.go:75, lib/store/ca_store.go:119) driven from `threads` native
+    threads (each owns N / threads digesters and writes them round-robin), on the GPU engine
+    and on the host (SHA-NI on the writers' threads under the CPU tokens): aggregate GB/s and
+    per-stream MB/s, the measured crossover (linear interpolation of the first N where the GPU
+    overtakes), and AUTO's switch point from the planner rates (krk_digester_host_streams)."""
+    import ctypes as C
+    from kraken_amd._capi import check, lib
+    rows = []
+    for m in sizes:
+        row = {"digesters": m, "threads": min(m, threads)}
+        for pl in ("gpu", "host"):
+            r = subprocess.run([exe, str(m), str(mib), "2", str(1 << 20), pl, str(threads)], capture_output=True,
+                               text=True, timeout=900)
+            rr = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+            if r.returncode != 0 or len(rr) != 2:
+                raise SystemExit(f"bench.py: digesters {m} {pl} failed (rc {r.returncode}): {r.stderr[-2000:]}")
+            x = rr[-1]  # the second round: slot pool grown, threads warm
+            row[pl] = {"GBps": x["GBps"], "MBps_per_stream": x["MBps_per_stream"], "on_gpu": x["on_gpu"],
+                       "digests_match": x["digests_match"]}
+        rows.append(row)
+    cross = None
+    for lo, hi in zip(rows, rows[1:]):
+        d_lo = lo["gpu"]["GBps"] - lo["host"]["GBps"]
+        d_hi = hi["gpu"]["GBps"] - hi["host"]["GBps"]
+        if d_lo <= 0 < d_hi:
+            cross = lo["digesters"] + (hi["digesters"] - lo["digesters"]) * (-d_lo) / (d_hi - d_lo)
+            break
+    if cross is None and rows and rows[0]["gpu"]["GBps"] > rows[0]["host"]["GBps"]:
+        cross = float(rows[0]["digesters"])  # the GPU already wins at the smallest N
+    auto = C.c_int64()
+    check(lib.krk_digester_host_streams(C.byref(auto)))
+    a_n = auto.value if auto.value < (1 << 62) else None
+    within = (a_n is not None and cross is not None and abs(a_n + 1 - cross) <= 0.2 * cross) or \
+        (a_n is None and cross is None)
+    return {"rows": rows, "measured_crossover": None if cross is None else round(cross, 1),
+            "auto_host_streams": a_n, "auto_within_20pct": bool(within),
+            "rates": D_rates_brief(),
+            "what": f"{mib} MiB a digester, writes of 1 B - 1 MiB, {threads} native threads (tests/native/digesters); "
+                    "measured_crossover: N where the GPU engine's aggregate overtakes the host's (interpolated); "
+                    "auto_host_streams: krk_digester_host_streams, AUTO keeps digesters on the host up to it"}
+
+
+def D_rates_brief():
+    from kraken_amd import device as D
+    r = D.planner_rates()
+    return {"sha_stream_MBps": [round(x / 1e6, 2) for x in r["sha_stream_bps"]], "h2d_GBps": round(r["h2d_bps"] / 1e9, 2),
+            "host_sha_GBps_per_thread": round(r["host_sha_bps"] / 1e9, 3), "source": r["source"],
+            "host_cpus": host_cores()}
 
 
 def visible_devices() -> int:

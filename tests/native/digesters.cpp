@@ -4,7 +4,11 @@
 // random-sized chunks (io.Copy-like), then asks for the digest.  Links the product
 // library through its C ABI only (include/kraken_hip.h), as a cgo caller would.
 //
-//   digesters <n_threads> <MiB per digester> <rounds> [max write bytes]
+//   digesters <n_digesters> <MiB per digester> <rounds> [max write bytes] [gpu|host|auto] [threads]
+//
+// With fewer threads than digesters (the crossover sweep: thousands of uploads, few OS
+// threads, like goroutines on GOMAXPROCS threads), each thread drives its digesters
+// round-robin, one write each in turn.  placement: KRK_PLACE_GPU (default), HOST or AUTO.
 //
 // Prints one JSON line per round: aggregate GB/s (timed from the moment every thread
 // holds its digester until the last digest), streams per SHA launch, and whether every
@@ -30,7 +34,10 @@ int main(int argc, char** argv) {
     const size_t L = (size_t)(argc > 2 ? atoi(argv[2]) : 16) << 20;
     const int rounds = argc > 3 ? atoi(argv[3]) : 2;
     const size_t maxw = argc > 4 ? strtoull(argv[4], nullptr, 10) : (1u << 20);
-    if (n < 1 || L == 0 || maxw == 0) return 2;
+    const char* pl = argc > 5 ? argv[5] : "gpu";
+    const int place = !strcmp(pl, "host") ? KRK_PLACE_HOST : !strcmp(pl, "auto") ? KRK_PLACE_AUTO : KRK_PLACE_GPU;
+    const int nt = std::min(n, argc > 6 ? atoi(argv[6]) : n);
+    if (n < 1 || L == 0 || maxw == 0 || nt < 1) return 2;
     if (krk_set_device(0) != KRK_OK) {
         fprintf(stderr, "no device: %s\n", krk_last_error());
         return 1;
@@ -63,30 +70,51 @@ int main(int argc, char** argv) {
         // burnt it, so the whole process was throttled for the rest of the quota period
         // (~90 ms stalls in a third of the rounds: tools/engine_slow.py).
         pthread_barrier_t start;
-        pthread_barrier_init(&start, nullptr, (unsigned)n + 1);
-        std::atomic<int> bad{0};
+        pthread_barrier_init(&start, nullptr, (unsigned)nt + 1);
+        std::atomic<int> bad{0}, on_gpu{0};
         std::vector<std::thread> th;
-        for (int i = 0; i < n; ++i)
-            th.emplace_back([&, i] {
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
                 krk_set_device(0);
-                krk_digester* d = nullptr;
-                const bool made = krk_digester_new_on(KRK_PLACE_GPU, &d) == KRK_OK;
-                if (!made) bad.fetch_add(1);
-                std::mt19937_64 rg(i * 7919 + r);
-                pthread_barrier_wait(&start);  // every thread arrives, made or not
-                if (!made) return;
-                const uint8_t* p = base.data() + (size_t)i * 4096;
-                for (size_t pos = 0; pos < L;) {
-                    const size_t k = std::min<size_t>(L - pos, 1 + rg() % maxw);
-                    if (krk_digester_write(d, p + pos, k) != KRK_OK) {
+                struct Own {
+                    int i;
+                    krk_digester* d;
+                    std::mt19937_64 rg;
+                    size_t pos;
+                };
+                std::vector<Own> own;
+                for (int i = t; i < n; i += nt) {
+                    krk_digester* d = nullptr;
+                    if (krk_digester_new_on(place, &d) != KRK_OK) {
                         bad.fetch_add(1);
-                        break;
+                        continue;
                     }
-                    pos += k;
+                    int where = 0;
+                    krk_digester_placement(d, &where);
+                    if (where == KRK_PLACE_GPU) on_gpu.fetch_add(1);
+                    own.push_back({i, d, std::mt19937_64((uint64_t)i * 7919 + r), 0});
                 }
-                uint8_t out[32];
-                if (krk_digester_sum(d, out) != KRK_OK || memcmp(out, want[i].data(), 32) != 0) bad.fetch_add(1);
-                krk_digester_free(d);
+                pthread_barrier_wait(&start);  // every thread arrives, made or not
+                for (size_t live = own.size(); live;) {
+                    live = 0;
+                    for (Own& o : own) {  // one write per digester in turn
+                        if (!o.d || o.pos >= L) continue;
+                        const uint8_t* p = base.data() + (size_t)o.i * 4096;
+                        const size_t k = std::min<size_t>(L - o.pos, 1 + o.rg() % maxw);
+                        if (krk_digester_write(o.d, p + o.pos, k) != KRK_OK) {
+                            bad.fetch_add(1);
+                            o.pos = L;
+                            continue;
+                        }
+                        o.pos += k;
+                        live += o.pos < L;
+                    }
+                }
+                for (Own& o : own) {
+                    uint8_t out[32];
+                    if (krk_digester_sum(o.d, out) != KRK_OK || memcmp(out, want[o.i].data(), 32) != 0) bad.fetch_add(1);
+                    krk_digester_free(o.d);
+                }
             });
 
         // DIGESTERS_CLOCK=1: sample the shader clock every ~20 ms during the round
@@ -120,10 +148,12 @@ int main(int argc, char** argv) {
         const double agg = (double)n * L / el;
         const bool ok = bad.load() == 0;
         all_ok = all_ok && ok;
-        printf("{\"round\": %d, \"t_go_ms\": %.3f, \"digesters\": %d, \"bytes_each\": %zu, \"seconds\": %.4f, \"GBps\": %.3f, "
+        printf("{\"round\": %d, \"t_go_ms\": %.3f, \"digesters\": %d, \"threads\": %d, \"placement\": \"%s\", "
+               "\"on_gpu\": %d, \"bytes_each\": %zu, \"seconds\": %.4f, \"GBps\": %.3f, "
                "\"MBps_per_stream\": %.2f, \"sha_launches\": %llu, \"streams_per_launch\": %.1f, "
                "\"pinned_bytes\": %llu, \"clock_mhz_median\": %.0f, \"clock_mhz_min\": %.0f, \"digests_match\": %s}\n",
-               r, std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), n, L, el, agg / 1e9, agg / n / 1e6, (unsigned long long)(b1[0] - b0[0]),
+               r, std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), n, nt, pl, on_gpu.load(), L, el,
+               agg / 1e9, agg / n / 1e6, (unsigned long long)(b1[0] - b0[0]),
                (double)(b1[1] - b0[1]) / (double)std::max<uint64_t>(1, b1[0] - b0[0]),
                (unsigned long long)b1[4], clk_med, clk_min, ok ? "true" : "false");
         fflush(stdout);

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-5 GPU steps: gpurun --timeout T -- 'bash tools/gpu_r05.sh <step>...'
+# Each step runs under its own time limit; a step that ends in a fault, abort, crash or
+# time limit (rc >= 2 other than pytest's 1 = test failures) ends the script: nothing more
+# runs on the GPU in that call.
+mkdir -p gpurun_out
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -3 "gpurun_out/$name.log"
+    if [ $rc -ge 2 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+for step in "$@"; do
+    case $step in
+    all) run pytest_all 1000 $PYT tests -m gpu ;;
+    new) run pytest_new 600 $PYT tests/test_gpu_files.py tests/test_gpu_digest_metainfo.py tests/test_gpu_bench_contract.py tests/test_gpu_defaults.py tests/test_gpu_bindings.py tests/test_gpu_engine.py ;;
+    gather) run gather_probe 240 tools/micro/gather_probe 8 16 ;;
+    disk) run disk_info 60 bash -c 'df -h . /tmp /dev/shm; lsblk -o NAME,SIZE,ROTA,TYPE,MOUNTPOINT 2>/dev/null | head -30; free -g; nproc; cat /sys/fs/cgroup/cpu.max; cat /sys/fs/cgroup/memory.max; mount | grep -E " / | /tmp " ; echo; ls -la /mnt /scratch /local 2>/dev/null | head' ;;
+    ddtest) run dd_test 300 bash -c 'd=$(mktemp -d -p .); dd if=/dev/zero of=$d/f bs=64M count=96 oflag=direct conv=fsync 2>&1 | tail -1; sync; dd if=$d/f of=/dev/null bs=64M iflag=direct 2>&1 | tail -1; rm -rf $d' ;;
+    bench) run bench_c2 300 python bench.py ;;
+    bench_engine) run bench_engine 900 python bench.py --workload engine ;;
+    bench_defaults) run bench_defaults 300 python bench.py --workload defaults ;;
+    bench_files) run bench_files 900 python bench.py --workload files --steps 2 --warmup 1 ;;
+    bench_c4) run bench_c4 600 python bench.py --workload c4 ;;
+    bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
