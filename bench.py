@@ -1658,7 +1658,8 @@ def digester_crossover_sweep(exe, mib, sizes=ENGINE_SWEEP, threads=256):
                 raise SystemExit(f"bench.py: digesters {m} {pl} failed (rc {r.returncode}): {r.stderr[-2000:]}")
             x = rr[-1]  # the second round: slot pool grown, threads warm
             row[pl] = {"GBps": x["GBps"], "MBps_per_stream": x["MBps_per_stream"], "on_gpu": x["on_gpu"],
-                       "digests_match": x["digests_match"]}
+                       "sha_launches": x["sha_launches"], "streams_per_launch": x["streams_per_launch"],
+                       "pinned_bytes": x["pinned_bytes"], "digests_match": x["digests_match"]}
         rows.append(row)
     cross = None
     for lo, hi in zip(rows, rows[1:]):
@@ -1675,6 +1676,7 @@ def digester_crossover_sweep(exe, mib, sizes=ENGINE_SWEEP, threads=256):
     within = (a_n is not None and cross is not None and abs(a_n + 1 - cross) <= 0.2 * cross) or \
         (a_n is None and cross is None)
     return {"rows": rows, "measured_crossover": None if cross is None else round(cross, 1),
+            "engine_slot_src": os.environ.get("KRK_ENGINE_SLOT_SRC", "gather"),
             "auto_host_streams": a_n, "auto_within_20pct": bool(within),
             "rates": D_rates_brief(),
             "what": f"{mib} MiB a digester, writes of 1 B - 1 MiB, {threads} native threads (tests/native/digesters); "

@@ -276,6 +276,7 @@ struct Inflight {
     int rc = KRK_OK;
     std::string err;
     int out_i = -1;  // the queue's pinned result buffer this launch writes
+    hipEvent_t gathered = nullptr;  // kSrcGather: the batch's slots are in their device mirrors
     uint64_t max_len = 0;
     Clock::time_point t_launch;
     char reason = '-';                    // trace: why the batch was formed
@@ -344,7 +345,18 @@ struct Engine {
     uint64_t quiet_us = 10000;     // ... or this long with no new owner (KRK_SHA_QUIET_US)
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
     bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
-    bool sha_zero_copy = true;    // SHA jobs read the pinned slots directly (KRK_SHA_ZERO_COPY=0: H2D first)
+    // Where the kernels read a request's slot (KRK_ENGINE_SLOT_SRC):
+    //  kSrcGather (default): one gather launch per batch copies every slot of the batch into
+    //    its device mirror over PCIe (gather.hip), on the engine's gather stream, so the next
+    //    batch's gather runs beside this batch's kernel;
+    //  kSrcZeroCopy: the SHA-256 kernel loads the pinned slot itself over PCIe (CRC: DMA);
+    //  kSrcDma: one H2D DMA per slot on the copy stream at submission.
+    // Measured on MI355X (bench.py --workload engine, the crossover sweep): zero-copy SHA
+    // streams stall beyond ~640 concurrent digesters (29 GB/s at 640, 22 at 1,024: the
+    // kernel's 64-byte zero-copy loads), where the gathered slots feed the kernel from HBM.
+    int src = 0;
+    hipStream_t s_gather = nullptr;
+    std::mutex gather_mu;
     bool caller_runs = true;      // the submission completing a coalescing set launches it (KRK_ENGINE_CALLER_RUNS=0: off)
     Clock::time_point t0 = Clock::now();
     uint64_t crc_launches = 0;
@@ -353,6 +365,29 @@ struct Engine {
 };
 
 namespace {
+
+constexpr int kSrcGather = 0, kSrcZeroCopy = 1, kSrcDma = 2;
+
+// Whether a request's slot is DMA'd to its device mirror at submission (stage()).
+bool stages_on_submit(const Engine* E, bool sha) {
+    return E->src == kSrcDma || (!sha && E->src == kSrcZeroCopy);
+}
+
+// kSrcGather: every slot of the batch into its device mirror in ONE gather launch on the
+// engine's gather stream; the queue's stream waits for it (f->gathered).
+int gather_batch(Engine* E, Queue& Q, Inflight* f) {
+    std::vector<GatherSpan> spans;
+    for (const Req* r : f->batch)
+        if (r->slot && r->len) spans.push_back({r->slot->dev, r->slot->mapped, r->len});
+    if (spans.empty()) return KRK_OK;
+    std::lock_guard<std::mutex> g(E->gather_mu);
+    int rc = run_gather(E->D, spans, E->s_gather);
+    if (rc) return rc;
+    KRK_HIP(hipEventCreateWithFlags(&f->gathered, hipEventDisableTiming));
+    KRK_HIP(hipEventRecord(f->gathered, E->s_gather));
+    KRK_HIP(hipStreamWaitEvent(Q.s, f->gathered, 0));
+    return KRK_OK;
+}
 
 void finish(Req* r, int rc, const std::string& err) {
     r->rc = rc;
@@ -398,9 +433,9 @@ int launch_sha(Engine* E, Inflight* f) {
         Req* r = f->batch[i];
         ShaJob& j = jobs[i];
         j = ShaJob{};
-        // zero-copy: the producer waves load the pinned slot over PCIe (59 MB/s a stream is
-        // far below the link; its loads run two steps ahead of the rounds)
-        j.ptr = reinterpret_cast<uint64_t>(r->slot ? (E->sha_zero_copy ? r->slot->mapped : r->slot->dev)
+        // zero-copy: the producer waves load the pinned slot over PCIe; otherwise the slot's
+        // device mirror (gathered in this batch's gather launch, or DMA'd at submission)
+        j.ptr = reinterpret_cast<uint64_t>(r->slot ? (E->src == kSrcZeroCopy ? r->slot->mapped : r->slot->dev)
                                                    : reinterpret_cast<const uint8_t*>(E->d_state));
         j.len = r->len;
         j.prefix = r->prefix;
@@ -410,7 +445,7 @@ int launch_sha(Engine* E, Inflight* f) {
         f->max_len = std::max<uint64_t>(f->max_len, r->len);
         if (r->final) lo = std::min(lo, r->row), hi = std::max(hi, r->row);
     }
-    int rc = E->sha_zero_copy ? KRK_OK : wait_staged(Q, f->batch);
+    int rc = E->src == kSrcGather ? gather_batch(E, Q, f) : E->src == kSrcDma ? wait_staged(Q, f->batch) : KRK_OK;
     if (!rc) rc = run_jobs(D, jobs, E->d_digest, E->d_state, Q.s);
     if (!rc && lo <= hi) {
         f->row0 = lo;
@@ -502,7 +537,7 @@ int launch_crc(Engine* E, Inflight* f) {
         return KRK_EINVAL;
     }
     if (!total) return KRK_OK;
-    int rc = wait_staged(Q, batch);
+    int rc = E->src == kSrcGather ? gather_batch(E, Q, f) : wait_staged(Q, batch);
     if (rc) return rc;
     uint32_t* d_sums = nullptr;
     KRK_HIP(scratch_alloc(D, &d_sums, total * 4, Q.s));
@@ -748,6 +783,7 @@ void completer(Engine* E, Queue* Q, bool sha) {
             finish(r, f->rc, f->err);
         }
         if (f->done) hipEventDestroy(f->done);
+        if (f->gathered) hipEventDestroy(f->gathered);
         Q->cv.notify_all();
         delete f;
     }
@@ -774,11 +810,14 @@ int engine_start(Engine* E) {
     E->quiet_us = env_size("KRK_SHA_QUIET_US", 10000);
     E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
     E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
-    if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->sha_zero_copy = atoi(z) != 0;
+    if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->src = atoi(z) ? kSrcZeroCopy : kSrcDma;  // round-4 knob
+    if (const char* m = getenv("KRK_ENGINE_SLOT_SRC"))
+        E->src = !strcmp(m, "zerocopy") ? kSrcZeroCopy : !strcmp(m, "dma") ? kSrcDma : kSrcGather;
     if (const char* c = getenv("KRK_ENGINE_CALLER_RUNS")) E->caller_runs = atoi(c) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
     KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));
     KRK_HIP(hipStreamCreateWithFlags(&E->s_copy, hipStreamNonBlocking));
+    KRK_HIP(hipStreamCreateWithFlags(&E->s_gather, hipStreamNonBlocking));
     KRK_HIP(hipStreamCreateWithFlags(&E->sha.s, hipStreamNonBlocking));
     KRK_HIP(hipStreamCreateWithFlags(&E->crc.s, hipStreamNonBlocking));
     E->sha.last_done = E->crc.last_done = Clock::now();
@@ -792,7 +831,7 @@ int engine_start(Engine* E) {
 
 void engine_free_resources(Engine* E) {
     hipSetDevice(E->dev);
-    for (hipStream_t s : {E->s_copy, E->sha.s, E->crc.s})
+    for (hipStream_t s : {E->s_copy, E->s_gather, E->sha.s, E->crc.s})
         if (s) hipStreamSynchronize(s), hipStreamDestroy(s);
     for (Queue* Q : {&E->sha, &E->crc}) {
         for (auto& p : Q->out)
@@ -1058,7 +1097,7 @@ int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool fina
         return rc;
     }
     Req* r = nullptr;
-    const bool h2d = !d->E->sha_zero_copy;
+    const bool h2d = stages_on_submit(d->E, true);
     if (sl) {
         r = new Req();
         r->slot = sl;
@@ -1390,7 +1429,7 @@ int stream_submit(krk_piece_stream* s, const uint8_t* src, uint64_t len) {
     int rc = stream_drain(s, g_owner_inflight - 1);
     if (rc) return rc;
     Req* r = nullptr;
-    rc = make_req(s->E, src, len, &r);
+    rc = make_req(s->E, src, len, &r, stages_on_submit(s->E, false));
     if (rc) return rc;
     r->owner = s;
     r->w = &s->w;
@@ -1602,7 +1641,7 @@ int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64
             if (rc) break;
         }
         Req* r = nullptr;
-        rc = make_req(E, data + off, std::min<uint64_t>(S, n - off), &r);
+        rc = make_req(E, data + off, std::min<uint64_t>(S, n - off), &r, stages_on_submit(E, false));
         if (rc) break;
         r->owner = &w;
         r->w = &w;

@@ -145,6 +145,20 @@ hipError_t launch_sha256_plan(int plan, const ShaJob* jobs, uint32_t n_jobs, uin
 bool sha_plan_valid(int plan);
 void set_sha_plan(int plan);
 
+// ---------------------------------------------------------------- host gather
+// One tile of a host -> device gather (gather.hip): n <= kGatherTile bytes from src (a
+// device-visible address of page-locked host memory: a hipHostMalloc'd or registered
+// mapping; any alignment) to dst (device, 16-B aligned, room for n rounded up to 16).
+constexpr uint64_t kGatherTile = 64 << 10;
+struct alignas(32) GatherTile {
+    uint64_t src;
+    uint64_t dst;
+    uint64_t n;
+    uint64_t pad;
+};
+static_assert(sizeof(GatherTile) == 32, "GatherTile layout");
+hipError_t launch_gather(const GatherTile* tiles, uint32_t n_tiles, int cus, hipStream_t s);
+
 // ---------------------------------------------------------------- HRW
 // Scores for (key, node) pairs and the per-key descending order.
 struct HrwArgs {

@@ -48,9 +48,9 @@ void set_error(int code, const char* fmt, ...);
     } while (0)
 
 // ------------------------------------------------------------------ timing
-enum Kern { K_CRC, K_SHA, K_HRW, K_FILTER, K_GATHER, K_SYNTH, K_N };
-inline const char* kKernNames[K_N] = {"crc32_pieces", "sha256_multi", "hrw_order",
-                                      "ring_filter",  "hrw_gather",   "synth_fill"};
+enum Kern { K_CRC, K_SHA, K_HRW, K_FILTER, K_GATHER, K_SYNTH, K_HOSTG, K_N };
+inline const char* kKernNames[K_N] = {"crc32_pieces", "sha256_multi", "hrw_order",   "ring_filter",
+                                      "hrw_gather",   "synth_fill",   "host_gather"};
 inline std::atomic<bool> g_timing{false};
 struct Pending {
     hipEvent_t a, b;
@@ -673,6 +673,35 @@ inline int run_jobs(Device* D, std::vector<ShaJob>& jobs, uint8_t* digests_dev, 
     });
     scratch_free(D, d_jobs, s);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "sha256_multi launch: %s", launch_error_text(e));
+    return KRK_OK;
+}
+
+// ------------------------------------------------------------------ host gather
+// Spans of page-locked host bytes (src: the device-visible address of a hipHostMalloc'd or
+// registered mapping, any alignment) into device memory (dst: 16-B aligned, room for n
+// rounded up to 16): ONE gather launch (gather.hip) on s, the bytes read over PCIe by the
+// kernel -- no host thread copies them and no DMA descriptor is built per span.
+struct GatherSpan {
+    uint8_t* dst;
+    const uint8_t* src;
+    uint64_t n;
+};
+inline int run_gather(Device* D, const std::vector<GatherSpan>& spans, hipStream_t s) {
+    std::vector<GatherTile> tiles;
+    for (const GatherSpan& g : spans)
+        for (uint64_t o = 0; o < g.n; o += kGatherTile)
+            tiles.push_back({reinterpret_cast<uint64_t>(g.src + o), reinterpret_cast<uint64_t>(g.dst + o),
+                             std::min<uint64_t>(kGatherTile, g.n - o), 0});
+    if (tiles.empty()) return KRK_OK;
+    KRK_CHECK(tiles.size() < (1ull << 32), KRK_EINVAL, "more than 2^32 gather tiles in one call");
+    void* d_tiles = nullptr;
+    int r = upload(D, tiles.data(), tiles.size() * sizeof(GatherTile), &d_tiles, s);
+    if (r) return r;
+    hipError_t e = timed(K_HOSTG, s, [&] {
+        return launch_gather(static_cast<const GatherTile*>(d_tiles), (uint32_t)tiles.size(), D->cus, s);
+    });
+    scratch_free(D, d_tiles, s);
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "host_gather launch: %s", launch_error_text(e));
     return KRK_OK;
 }
 

@@ -97,6 +97,7 @@ struct Filler {
     virtual int fill(const std::vector<Task>& tasks) = 0;
     // The source is page-locked: its chunks can be DMA'd straight into the device window.
     virtual const uint8_t* pinned_src(uint32_t /*blob*/, uint64_t /*off*/) const { return nullptr; }
+    virtual bool pinned_all() const { return false; }
 };
 
 struct MemFiller : Filler {
@@ -104,6 +105,7 @@ struct MemFiller : Filler {
     bool pinned = false;  // every windowed blob page-locked (krk_host_alloc): no staging copy
     explicit MemFiller(const krk_blob* b) : blobs(b) {}
     const uint8_t* pinned_src(uint32_t b, uint64_t off) const override { return pinned ? blobs[b].data + off : nullptr; }
+    bool pinned_all() const override { return pinned; }
     int fill(const std::vector<Task>& tasks) override {
         std::vector<CopyTask> c;
         c.reserve(tasks.size());
@@ -286,10 +288,8 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         for (const WinChunk& c : win) {
             const uint64_t L = lens[c.blob];
             const uint64_t dev = reinterpret_cast<uint64_t>(w.dev + fill);
-            if (c.len) {
-                tasks.push_back({c.blob, c.off, c.len, w.host + fill});
-                if (crc) B.add(items, dev, c.off, c.off + c.len, L, (uint64_t)plens[c.blob], soff[c.blob]);
-            }
+            tasks.push_back({c.blob, c.off, c.len, w.host + fill});  // an empty blob too (its file is opened)
+            if (c.len && crc) B.add(items, dev, c.off, c.off + c.len, L, (uint64_t)plens[c.blob], soff[c.blob]);
             ShaJob j{};
             j.ptr = dev;
             j.len = c.len;
@@ -310,13 +310,13 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         t_build += tc - tb;
         // page-locked sources are DMA'd straight from the caller's memory into the device
         // window; the others go through the pinned host window
-        const bool direct = !tasks.empty() && filler.pinned_src(tasks[0].b, tasks[0].off) != nullptr &&
+        const bool direct = !tasks.empty() && filler.pinned_all() &&
                             tasks.size() <= kDirectMaxCalls;
         std::vector<CopyTask> dma;
         if (direct) {
             dma.reserve(tasks.size());
             for (const Filler::Task& t : tasks)
-                dma.push_back({w.dev + (t.dst - w.host), filler.pinned_src(t.b, t.off), (size_t)t.len});
+                if (t.len) dma.push_back({w.dev + (t.dst - w.host), filler.pinned_src(t.b, t.off), (size_t)t.len});
         } else {
             r = filler.fill(tasks);
             if (r) break;

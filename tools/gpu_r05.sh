@@ -24,6 +24,9 @@ for step in "$@"; do
     ddtest) run dd_test 300 bash -c 'd=$(mktemp -d -p .); dd if=/dev/zero of=$d/f bs=64M count=96 oflag=direct conv=fsync 2>&1 | tail -1; sync; dd if=$d/f of=/dev/null bs=64M iflag=direct 2>&1 | tail -1; rm -rf $d' ;;
     bench) run bench_c2 300 python bench.py ;;
     bench_engine) run bench_engine 900 python bench.py --workload engine ;;
+    bench_engine_zc) run bench_engine_zc 900 env KRK_ENGINE_SLOT_SRC=zerocopy python bench.py --workload engine ;;
+    regprobe) run reg_probe 300 tools/micro/reg_probe 16 ;;
+    engine_tests) run pytest_engine 600 $PYT tests/test_gpu_engine.py tests/test_gpu_concurrency.py tests/test_gpu_bindings.py tests/test_gpu_digest_metainfo.py ;;
     bench_defaults) run bench_defaults 300 python bench.py --workload defaults ;;
     bench_files) run bench_files 900 python bench.py --workload files --steps 2 --warmup 1 ;;
     bench_c4) run bench_c4 600 python bench.py --workload c4 ;;
