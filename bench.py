@@ -973,13 +973,41 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
     for i, d in enumerate(datas):  # the device blobs' prefixes (device-generated content)
         D.check(D.lib.krk_memcpy_d2h(d.ctypes.data_as(C.c_void_p), arena.buf.ptr + int(arena.offsets[i]), Le))
     D.metainfo_digest_host([d[:1 << 20] for d in datas[:2]], P)  # warm the staging windows (short chains)
-    passes = []
-    for _ in range(E2E_PASSES):  # the host side of a box varies pass to pass: the median is reported
-        T.barrier()
-        t0 = time.perf_counter()
-        sums, dg = D.metainfo_digest_host(datas, P)
-        passes.append(T.max_over_ranks(time.perf_counter() - t0))
-    el = float(np.median(passes))
+    paths = {}
+    # the staged path (pageable -> pinned window copies on host threads,
+    # then the DMA: three host-DRAM touches a byte) against the gather (the pages registered,
+    # each window read over PCIe by one gather launch: one touch), same batch, same box
+    for name, mode in (("staged", 0), ("gather", 1)):
+        D.set_host_gather(mode)
+        passes, cpu = [], []
+        try:
+            for _ in range(E2E_PASSES):  # the host side of a box varies pass to pass: the median is reported
+                T.barrier()
+                c0, t0 = cpu_seconds(), time.perf_counter()
+                sums, dg = D.metainfo_digest_host(datas, P)
+                cpu.append(cpu_seconds() - c0)
+                passes.append(T.max_over_ranks(time.perf_counter() - t0))
+            st = D.windows_last_call()
+        finally:
+            D.set_host_gather(-1)
+        el_p = float(np.median(passes))
+        gbps = world * n * Le / el_p / 1e9
+        paths[name] = {"GBps": round(gbps, 3), "passes_s": [round(x, 3) for x in passes],
+                       "host_cpu_s_per_GB": round(float(np.median(cpu)) / (n * Le / 1e9), 4),
+                       "h2d_frac": None, "windows": st["windows"], "gather_windows": st["gather_windows"],
+                       "registered_bytes": st["registered_bytes"], "register_s": round(st["register_s"], 3)}
+        paths[name]["_sums_dg"] = (sums, dg)
+    h2d = D.planner_rates()["h2d_bps"] / 1e9
+    for v in paths.values():
+        v["h2d_frac"] = round(v["GBps"] / world / h2d, 4) if h2d else None
+    best = max(paths, key=lambda k: paths[k]["GBps"])
+    same_paths = bool(np.array_equal(paths["staged"]["_sums_dg"][1], paths["gather"]["_sums_dg"][1]) and all(
+        np.array_equal(a, b) for a, b in zip(paths["staged"]["_sums_dg"][0], paths["gather"]["_sums_dg"][0])))
+    sums, dg = paths["gather"]["_sums_dg"]
+    for v in paths.values():
+        del v["_sums_dg"]
+    el = world * n * Le / (paths[DEFAULT_HOST_PATH]["GBps"] * 1e9)
+    passes = paths[DEFAULT_HOST_PATH]["passes_s"]
     k = Le // P
     ok = None
     if out is not None and k:
@@ -990,7 +1018,9 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
            **({"blob_bytes_requested": want, "capped_by": "host memory per rank (40 % / ranks, <= 24 GiB with "
                                                           "several ranks)"} if Le < want else {}),
            "seconds": round(el, 3), "passes_s": [round(x, 3) for x in passes],
-           "source": "pageable host memory (numpy), copied into pinned windows; median of the passes",
+           "source": f"pageable host memory (numpy), the library's default path ({DEFAULT_HOST_PATH}); median of "
+                     "the passes",
+           "paths": paths, "faster_path": best, "paths_outputs_equal": same_paths,
            "bound": "PCIe H2D (one pass per byte) and the per-blob SHA-256 chain (blob_bytes / per-stream rate)",
            "sums_match_device_run": ok,
            "roofline": link_roofline(D, world * n * Le / el / 1e9, "c2_end_to_end", n)}
@@ -1002,6 +1032,18 @@ def end_to_end(D, T, arena, n, Le, P, out, world):
         res["host_hybrid"] = hyb[0] if len(hyb) == 1 else hyb
     del datas
     return res
+
+
+# The library's default for a large pageable host batch (krk_set_host_gather AUTO): the
+# gather; the leg measures both and reports which was faster.
+DEFAULT_HOST_PATH = "gather"
+
+
+def cpu_seconds() -> float:
+    """This process's user + system CPU seconds (every thread)."""
+    import resource
+    u = resource.getrusage(resource.RUSAGE_SELF)
+    return u.ru_utime + u.ru_stime
 
 
 # Host threads of the end-to-end leg's hybrid pass (KRK_BENCH_HYBRID="8,16"; "" = none;
@@ -1475,6 +1517,8 @@ def run_files(a, D, T, rank, world, res):
                             "(oracle/oracle.c orc_baseline_files)"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
+    if a.cold_gib > 0:
+        res["cold"] = files_cold_leg(a, D, T, rank, world, P)
     res.update({"metric": "upload verify + metainfo from files, GB/s (end-to-end, host link)",
                 "value": round(value, 3), "unit": "GB/s", "steps": a.steps,
                 "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -1603,6 +1647,185 @@ def run_defaults(a, D, T, rank, world, res):
                              "stream_at_least_one_crc_thread": p["stream_GBps"] >= p["host_crc_1thread_GBps"]}})
 
 
+def drop_cache(paths):
+    """Evict every file's pages from the page cache (posix_fadvise DONTNEED; the files were
+    fsync'ed when written, so their pages are clean and can go)."""
+    for p in paths:
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        finally:
+            os.close(fd)
+
+
+def resident_fraction(paths):
+    """Share of the files' pages in the page cache (mincore over a read-only mapping)."""
+    import ctypes as C
+    libc = C.CDLL(None, use_errno=True)
+    libc.mmap.restype = C.c_void_p
+    libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+    libc.munmap.argtypes = [C.c_void_p, C.c_size_t]
+    libc.mincore.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+    pages = res = 0
+    for p in paths:
+        n = os.path.getsize(p)
+        if not n:
+            continue
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            addr = libc.mmap(None, n, 1, 1, fd, 0)  # PROT_READ, MAP_SHARED
+            if addr in (None, C.c_void_p(-1).value):
+                continue
+            k = (n + 4095) // 4096
+            vec = (C.c_ubyte * k)()
+            if libc.mincore(addr, n, vec) == 0:
+                pages += k
+                res += sum(v & 1 for v in vec)
+            libc.munmap(addr, n)
+        finally:
+            os.close(fd)
+    return res / pages if pages else 0.0
+
+
+def disk_read_rate(paths, threads=16, chunk=8 << 20):
+    """GB/s of plain large reads of the files (no compute), `threads` at a time: the disk
+    roofline of the cold leg."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def rd(p):
+        buf = bytearray(chunk)
+        mv = memoryview(buf)
+        got = 0
+        with open(p, "rb", buffering=0) as f:
+            while True:
+                k = f.readinto(mv)
+                if not k:
+                    return got
+                got += k
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(rd, paths))
+    return total / (time.perf_counter() - t0) / 1e9, total
+
+
+def files_cold_leg(a, D, T, rank, world, P):
+    """f3 (upload verify + metainfo from the files themselves) on DISK, not
+    page cache.  >= a.cold_gib GiB of DISTINCT files (the C3 length law / 64, every file its
+    own synthetic content), fsync'ed, and the page cache dropped for every file before every
+    pass (posix_fadvise DONTNEED; the resident share measured by mincore).  Passes: the
+    library's GPU-only path (offload off), its default (AUTO offload), O_DIRECT reads
+    (KRK_FILE_DIRECT=1), plain reads of the files on 16 threads (the disk roofline), and the
+    reference's two reads on the CPU (origin/blobserver/uploader.go:74-94 digest, then
+    lib/metainfogen/generator.go:41-58 piece sums): per file back to back (the second read
+    from the page cache the first filled, as on an origin with memory to spare) and the two
+    passes over the whole set with the cache dropped between them (both reads from disk).
+    Every pass's digests and sums are compared; sampled files against the oracle."""
+    import shutil
+    import tempfile
+    from kraken_amd.windowed import c3_lengths
+    d = tempfile.mkdtemp(prefix=f"krk_cold_r{rank}_")
+    try:
+        free = shutil.disk_usage(d).free
+        want = min(int(a.cold_gib * (1 << 30)), int(0.6 * free / max(1, world)))
+        law = c3_lengths(200_000, scale=64)
+        lens, tot = [], 0
+        for L in law:
+            if tot >= want:
+                break
+            lens.append(L)
+            tot += L
+        n = len(lens)
+        ids = [(4 << 40) + rank * 1_000_000 + i for i in range(n)]
+        top = max(lens)
+        buf = D.DeviceBuffer(top)
+        pin = D.PinnedArray((top,), np.uint8)
+        paths = []
+        t_w = time.perf_counter()
+        for i, L in enumerate(lens):
+            D.check(D.lib.krk_synth_fill_dev(buf.ptr, ids[i], 0, L, 0, None))
+            D.synchronize()
+            pin.fill_from(buf)
+            p = os.path.join(d, f"c{i}")
+            fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            try:
+                mv = memoryview(pin.a)[:L]
+                off = 0
+                while off < L:
+                    off += os.write(fd, mv[off:])
+                os.fsync(fd)
+            finally:
+                os.close(fd)
+            paths.append(p)
+        t_w = time.perf_counter() - t_w
+        buf.free()
+        del pin
+        legs = {}
+
+        def leg(name, fn):
+            drop_cache(paths)
+            cold = resident_fraction(paths[::max(1, n // 64)])
+            T.barrier()
+            t0 = time.perf_counter()
+            out = fn()
+            el = T.max_over_ranks(time.perf_counter() - t0)
+            legs[name] = {"GBps": round(world * tot / el / 1e9, 3), "seconds": round(el, 3),
+                          "resident_before": round(cold, 4)}
+            return out
+
+        D.set_sha_host_offload(0)
+        s_g, d_g = leg("gpu_only", lambda: D.metainfo_digest_files(paths, lens, P))
+        legs["gpu_only"].update({k: v for k, v in D.windows_last_call().items() if k in ("windows", "max_live")})
+        D.set_sha_host_offload(-1)
+        try:
+            s_a, d_a = leg("default", lambda: D.metainfo_digest_files(paths, lens, P))
+            legs["default"]["host_blobs"] = D.windows_last_call()["host_blobs"]
+        finally:
+            D.set_sha_host_offload(0)
+        os.environ["KRK_FILE_DIRECT"] = "1"
+        try:
+            s_d, d_d = leg("o_direct", lambda: D.metainfo_digest_files(paths, lens, P))
+        finally:
+            os.environ.pop("KRK_FILE_DIRECT", None)
+        rate, got = leg("disk_read", lambda: disk_read_rate(paths))
+        legs["disk_read"]["what"] = "plain 8 MiB reads of every file on 16 threads, no compute (the disk roofline)"
+        same = all(np.array_equal(x, y) for x, y in ((d_g, d_a), (d_g, d_d))) and all(
+            np.array_equal(x, y) and np.array_equal(x, z) for x, y, z in zip(s_g, s_a, s_d))
+        from oracle import oracle as O  # checker and CPU baseline only
+        O.build()
+        import hashlib
+        ok = True
+        for i in sorted({0, n // 2, n - 1, int(np.argmax(lens))}):
+            x = O.synth(ids[i], lens[i])
+            ok = ok and bytes(d_g[i]) == hashlib.sha256(x.tobytes()).digest() and np.array_equal(
+                s_g[i], O.calc_piece_sums(x, P)[1])
+        cpu = None
+        if rank == 0 and not a.no_cpu_baseline:
+            drop_cache(paths)
+            t_c, s_c, off_c, dg_c = O.baseline_files(paths, lens, P, node_cores(), passes=3)
+            drop_cache(paths)
+            t_1 = O.baseline_files(paths, lens, P, node_cores(), passes=1)[0]
+            drop_cache(paths)
+            t_2 = O.baseline_files(paths, lens, P, node_cores(), passes=2)[0]
+            same_c = bool(np.array_equal(dg_c, d_g)) and all(
+                np.array_equal(s_c[int(off_c[i]):int(off_c[i + 1])], s_g[i]) for i in range(n))
+            cpu = {"value": round(tot / t_c / 1e9, 3), "unit": "GB/s", "cores": node_cores(),
+                   "cores_source": CORES_SOURCE, "kind": "port", "seconds": round(t_c, 3),
+                   "two_disk_reads_GBps": round(tot / (t_1 + t_2) / 1e9, 3),
+                   "two_disk_reads_seconds": [round(t_1, 3), round(t_2, 3)], "outputs_match_gpu": same_c,
+                   "sample": f"all {n} cold files: Digester.FromReader then calcPieceSums over each file, 32 KiB "
+                             "reads, SHA-NI and PCLMUL, one file per thread (oracle/oracle.c orc_baseline_files); "
+                             "value = the two reads back to back per file (the second from the page cache), "
+                             "two_disk_reads = the two passes over the set with the cache dropped between"}
+        return {"files": n, "bytes": tot, "GiB": round(tot / (1 << 30), 2), "dir_free_GB": round(free / 1e9, 1),
+                "write_s": round(t_w, 2), "legs": legs, "outputs_equal": bool(same), "sampled_equal_oracle": bool(ok),
+                "cpu_baseline": cpu,
+                "roofline": {"bound": "disk", "peak": legs["disk_read"]["GBps"], "unit": "GB/s",
+                             "achieved": legs["gpu_only"]["GBps"],
+                             "frac": round(legs["gpu_only"]["GBps"] / max(legs["disk_read"]["GBps"], 1e-9), 4)}}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def run_engine(a, D, T, rank, world, res):
     """The submission engine under concurrent Digesters: tests/native/digesters
     runs warmup + steps rounds of 256 GPU-placed digesters (a round = every digester's 16 MiB
@@ -1650,14 +1873,16 @@ def digester_crossover_sweep(exe, mib, sizes=ENGINE_SWEEP, threads=256):
     rows = []
     for m in sizes:
         row = {"digesters": m, "threads": min(m, threads)}
-        for pl in ("gpu", "host"):
-            r = subprocess.run([exe, str(m), str(mib), "2", str(1 << 20), pl, str(threads)], capture_output=True,
+        for pl in ("gpu", "host", "auto"):
+            r = subprocess.run([exe, str(m), str(mib), "4", str(1 << 20), pl, str(threads)], capture_output=True,
                                text=True, timeout=900)
             rr = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-            if r.returncode != 0 or len(rr) != 2:
+            if r.returncode != 0 or len(rr) != 4:
                 raise SystemExit(f"bench.py: digesters {m} {pl} failed (rc {r.returncode}): {r.stderr[-2000:]}")
-            x = rr[-1]  # the second round: slot pool grown, threads warm
-            row[pl] = {"GBps": x["GBps"], "MBps_per_stream": x["MBps_per_stream"], "on_gpu": x["on_gpu"],
+            # rounds 1-3 (round 0 grows the slot pool): the median round
+            x = sorted(rr[1:], key=lambda q: q["GBps"])[1]
+            row[pl] = {"GBps": x["GBps"], "rounds_GBps": [q["GBps"] for q in rr[1:]],
+                       "MBps_per_stream": x["MBps_per_stream"], "on_gpu": x["on_gpu"],
                        "sha_launches": x["sha_launches"], "streams_per_launch": x["streams_per_launch"],
                        "pinned_bytes": x["pinned_bytes"], "digests_match": x["digests_match"]}
         rows.append(row)
@@ -1676,10 +1901,12 @@ def digester_crossover_sweep(exe, mib, sizes=ENGINE_SWEEP, threads=256):
     within = (a_n is not None and cross is not None and abs(a_n + 1 - cross) <= 0.2 * cross) or \
         (a_n is None and cross is None)
     return {"rows": rows, "measured_crossover": None if cross is None else round(cross, 1),
-            "engine_slot_src": os.environ.get("KRK_ENGINE_SLOT_SRC", "gather"),
+            "engine_slot_src": os.environ.get("KRK_ENGINE_SLOT_SRC", "zerocopy"),
             "auto_host_streams": a_n, "auto_within_20pct": bool(within),
             "rates": D_rates_brief(),
-            "what": f"{mib} MiB a digester, writes of 1 B - 1 MiB, {threads} native threads (tests/native/digesters); "
+            "what": f"{mib} MiB a digester, writes of 1 B - 1 MiB, {threads} native threads (tests/native/digesters), "
+                    "median of 3 rounds after a warm one; gpu / host: every digester on that placement, auto: the "
+                    "library's default (the first auto_host_streams live ones on the host, the rest on the GPU); "
                     "measured_crossover: N where the GPU engine's aggregate overtakes the host's (interpolated); "
                     "auto_host_streams: krk_digester_host_streams, AUTO keeps digesters on the host up to it"}
 
@@ -1780,6 +2007,8 @@ def main():
                     help="C1 / c5regen_digest: skip the SHA-256 host-offload leg")
     ap.add_argument("--no-sweep", action="store_true", help="C5: skip the N x MaxReplica x healthy grid")
     ap.add_argument("--e2e-mb", type=int, default=100, help="bytes per blob for the end-to-end leg (MiB; C2: 100)")
+    ap.add_argument("--cold-gib", type=float, default=32.0,
+                    help="files: GiB of distinct files for the cold (page cache dropped) leg; 0 = skip it")
     ap.add_argument("--e2e-only", action="store_true",
                     help="C2: only the end-to-end leg (profiler passes of the host path)")
     a = ap.parse_args()

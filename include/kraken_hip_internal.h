@@ -64,6 +64,17 @@ int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs
  * page-locked blobs (krk_host_alloc memory, windows of <= 64 chunks: no pinned staging
  * copy, one DMA a chunk).  KRK_PINNED_DIRECT=0 stages them instead. */
 int krk_windows_last_direct(int* direct_windows);
+/* ... and how many of its windows the GPU gathered from the caller's page-locked memory
+ * (gather.hip: one launch a window reading the pages over PCIe -- krk_host_alloc blobs in
+ * wide windows, or pageable blobs the call registered with hipHostRegister; KRK_HOST_GATHER
+ * 0 / 1 forces off / on), the caller bytes it registered and the helper threads' seconds
+ * spent registering them. */
+int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, double* register_seconds);
+/* The gather of host-buffer calls, process-wide: -1 AUTO (the default: page-locked blobs
+ * gathered in wide windows, pageable ones registered and gathered when a call windows at
+ * least 256 MiB), 0 off (stage every window through the pinned host windows), 1 on (any
+ * size).  KRK_HOST_GATHER sets the same at the first call.  For A/B runs (bench.py). */
+int krk_set_host_gather(int mode);
 
 /* --------------------------------------- host crossover primitives (CPU)
  * The host side of the Digester / PieceHash crossovers, exported so the

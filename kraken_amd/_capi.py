@@ -130,6 +130,8 @@ def _load() -> C.CDLL:
         "krk_window_stream_cap": (i, [u64p]),
         "krk_windows_last_call": (i, [u64p, C.POINTER(C.c_int), u64p]),
         "krk_windows_last_direct": (i, [C.POINTER(C.c_int)]),
+        "krk_windows_last_gather": (i, [C.POINTER(C.c_int), u64p, f64p]),
+        "krk_set_host_gather": (i, [i]),
         "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_metainfo_digest_chunks_dev_on": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp, vp]),
         "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),

@@ -346,15 +346,16 @@ struct Engine {
     uint64_t fail_crc_at = 0;     // fault injection for tests: the n-th CRC launch fails (0 = never)
     bool trace = false;           // KRK_ENGINE_TRACE: one stderr line per SHA launch
     // Where the kernels read a request's slot (KRK_ENGINE_SLOT_SRC):
-    //  kSrcGather (default): one gather launch per batch copies every slot of the batch into
-    //    its device mirror over PCIe (gather.hip), on the engine's gather stream, so the next
-    //    batch's gather runs beside this batch's kernel;
-    //  kSrcZeroCopy: the SHA-256 kernel loads the pinned slot itself over PCIe (CRC: DMA);
+    //  kSrcZeroCopy (default): the SHA-256 kernel loads the pinned slot itself over PCIe
+    //    (CRC requests: DMA'd at submission);
+    //  kSrcGather: one gather launch per batch copies every slot of the batch into its device
+    //    mirror (gather.hip) on the engine's gather stream, and the kernels read HBM;
     //  kSrcDma: one H2D DMA per slot on the copy stream at submission.
-    // Measured on MI355X (bench.py --workload engine, the crossover sweep): zero-copy SHA
-    // streams stall beyond ~640 concurrent digesters (29 GB/s at 640, 22 at 1,024: the
-    // kernel's 64-byte zero-copy loads), where the gathered slots feed the kernel from HBM.
-    int src = 0;
+    // Measured on MI355X, same box, bench.py --workload engine (profiles/r05/bench_engine_*.json):
+    // zero-copy 14.1 / 29.6 / 21.6 GB/s at 256 / 640 / 1,024 digesters, gather 12.0 / 20.6 /
+    // 20.4 -- a batch is formed only when its owners are back, just before the running one
+    // ends, so its gather cannot overlap the previous kernel and adds its time to every batch.
+    int src = 1;
     hipStream_t s_gather = nullptr;
     std::mutex gather_mu;
     bool caller_runs = true;      // the submission completing a coalescing set launches it (KRK_ENGINE_CALLER_RUNS=0: off)
@@ -367,6 +368,7 @@ struct Engine {
 namespace {
 
 constexpr int kSrcGather = 0, kSrcZeroCopy = 1, kSrcDma = 2;
+static_assert(kSrcZeroCopy == 1, "Engine::src default");
 
 // Whether a request's slot is DMA'd to its device mirror at submission (stage()).
 bool stages_on_submit(const Engine* E, bool sha) {
@@ -812,7 +814,7 @@ int engine_start(Engine* E) {
     E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
     if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->src = atoi(z) ? kSrcZeroCopy : kSrcDma;  // round-4 knob
     if (const char* m = getenv("KRK_ENGINE_SLOT_SRC"))
-        E->src = !strcmp(m, "zerocopy") ? kSrcZeroCopy : !strcmp(m, "dma") ? kSrcDma : kSrcGather;
+        E->src = !strcmp(m, "gather") ? kSrcGather : !strcmp(m, "dma") ? kSrcDma : kSrcZeroCopy;
     if (const char* c = getenv("KRK_ENGINE_CALLER_RUNS")) E->caller_runs = atoi(c) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
     KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));

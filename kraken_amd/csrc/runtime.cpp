@@ -403,6 +403,9 @@ static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blob
     ItemBuilder B;
     int k = 0;
     uint64_t bi = 0, boff = 0;
+    uint64_t first = 0;
+    while (first < n_blobs && !blobs[first].length) ++first;
+    const bool gather_ok = direct && first < n_blobs && mapped_at_host_address(blobs[first].data);
     while (!r && bi < n_blobs) {
         r = pl.acquire(k);
         if (r) break;
@@ -424,12 +427,23 @@ static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blob
             fill = (fill + 15) & ~size_t(15);
             if (boff >= b.length) { ++bi; boff = 0; }
         }
-        // pinned bytes go up straight from the caller's pages only in windows of few copies
-        // (many small DMAs cost more than the staging copy, windows.cpp kDirectMaxCalls)
+        // pinned bytes go up straight from the caller's pages: a DMA a copy in windows of few
+        // copies (many small DMAs cost more than the staging copy, staging.hpp
+        // kDirectMaxCalls), else one gather launch that reads them over PCIe (gather.hip)
         const bool dw = direct && copies.size() <= kDirectMaxCalls;
-        if (dw)
+        const bool gw = direct && !dw && gather_ok;
+        hipError_t up = hipSuccess;
+        if (dw || gw)
             for (CopyTask& c : copies) c.dst = w.dev + (c.dst - w.host);
-        const hipError_t up = dw ? pl.h2d_direct(k, copies, cp) : (par_copy(copies), pl.h2d(k, std::min(fill, W), cp));
+        if (gw) {
+            std::vector<GatherSpan> spans;
+            spans.reserve(copies.size());
+            for (const CopyTask& c : copies) spans.push_back({c.dst, c.src, c.n});
+            r = pl.h2d_gather(D, k, spans, cp);
+            if (r) break;
+        } else {
+            up = dw ? pl.h2d_direct(k, copies, cp) : (par_copy(copies), pl.h2d(k, std::min(fill, W), cp));
+        }
         if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess) {
             set_error(KRK_EHIP, "piece_sums_host: staging copy failed");
             r = KRK_EHIP;

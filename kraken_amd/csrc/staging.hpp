@@ -148,6 +148,22 @@ struct Pipeline {
         if (e == hipSuccess) x.copying = true;
         return e;
     }
+    // The caller's page-locked bytes gathered into device window k by ONE gather launch on
+    // cp (spans' dst are device addresses in it), after the kernels that read its last
+    // contents.
+    int h2d_gather(Device* D, int k, const std::vector<GatherSpan>& spans, hipStream_t cp) {
+        Window& x = w[k];
+        for (int i = 0; i < 2; ++i)
+            if (x.done_pending[i]) {
+                KRK_HIP(hipStreamWaitEvent(cp, x.done[i], 0));
+                x.done_pending[i] = false;
+            }
+        const int r = run_gather(D, spans, cp);
+        if (r) return r;
+        KRK_HIP(hipEventRecord(x.copied, cp));
+        x.copying = true;
+        return KRK_OK;
+    }
     // Kernel stream ks (slot 0 or 1) has enqueued everything that reads window k.
     hipError_t release(int k, int slot, hipStream_t ks) {
         hipError_t e = hipEventRecord(w[k].done[slot], ks);
@@ -224,6 +240,17 @@ inline bool host_pinned(const void* p, uint64_t n) {
         return a.type == hipMemoryTypeHost;
     };
     return pinned_at(p) && (n <= 1 || pinned_at(static_cast<const uint8_t*>(p) + n - 1));
+}
+
+// Whether the GPU addresses page-locked host memory at p at the host address itself (the
+// gather kernel reads it there).
+inline bool mapped_at_host_address(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.devicePointer == p;
 }
 
 // Host -> pinned staging copies of one window, split over the calling thread and the host

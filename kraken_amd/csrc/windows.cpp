@@ -22,6 +22,7 @@
 #include <deque>
 #include <thread>
 
+#include "host_register.hpp"
 #include "runtime.hpp"
 #include "staging.hpp"
 
@@ -98,14 +99,28 @@ struct Filler {
     // The source is page-locked: its chunks can be DMA'd straight into the device window.
     virtual const uint8_t* pinned_src(uint32_t /*blob*/, uint64_t /*off*/) const { return nullptr; }
     virtual bool pinned_all() const { return false; }
+    // ... and the GPU addresses it at the host address (the gather reads it there)
+    virtual bool pinned_mapped() const { return false; }
+    // The caller's pageable bytes made page-locked for the gather (host_register.hpp), or null.
+    virtual HostRegistry* registry() { return nullptr; }
+    virtual const uint8_t* src(uint32_t /*blob*/, uint64_t /*off*/) const { return nullptr; }
 };
 
 struct MemFiller : Filler {
     const krk_blob* blobs;
     bool pinned = false;  // every windowed blob page-locked (krk_host_alloc): no staging copy
+    bool mapped = false;  // ... at device addresses equal to the host ones
+    std::unique_ptr<HostRegistry> reg;  // pageable blobs registered for the gather
+    hipStream_t gather_stream = nullptr;  // where the gathers ran (drained before unregistering)
     explicit MemFiller(const krk_blob* b) : blobs(b) {}
+    ~MemFiller() override {
+        if (reg) reg->finish(gather_stream);
+    }
     const uint8_t* pinned_src(uint32_t b, uint64_t off) const override { return pinned ? blobs[b].data + off : nullptr; }
     bool pinned_all() const override { return pinned; }
+    bool pinned_mapped() const override { return mapped; }
+    HostRegistry* registry() override { return reg.get(); }
+    const uint8_t* src(uint32_t b, uint64_t off) const override { return blobs[b].data + off; }
     int fill(const std::vector<Task>& tasks) override {
         std::vector<CopyTask> c;
         c.reserve(tasks.size());
@@ -236,7 +251,10 @@ struct CallStats {
     uint64_t max_live = 0;
     int windows = 0;
     int direct_windows = 0;  // windows DMA'd straight from the caller's page-locked memory
+    int gather_windows = 0;  // windows gathered by the GPU from page-locked / registered caller memory
     uint64_t host_blobs = 0;
+    uint64_t registered_bytes = 0;  // caller bytes registered for the gather
+    double register_s = 0;          // helper-thread seconds spent registering them
 };
 thread_local CallStats t_last_call;
 
@@ -252,7 +270,7 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
     for (uint64_t i = 0; i < n; ++i)
         if (!skip[i]) blobs.push_back((uint32_t)i);
     st->max_live = 0;
-    st->windows = st->direct_windows = 0;
+    st->windows = st->direct_windows = st->gather_windows = 0;
     if (blobs.empty()) return KRK_OK;
     const size_t W = window_bytes();
     const uint64_t live_cap = std::min<uint64_t>(cap, blobs.size());
@@ -270,13 +288,25 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
     ItemBuilder B;
     std::vector<WinChunk> win;
     std::vector<Filler::Task> tasks;
-    int k = 0;
+    // the gather (gather.hip): page-locked caller memory goes up in one launch a window, read
+    // by the GPU -- pinned blobs as they are, pageable ones once the registry has registered
+    // the pages the window reads (a dry run of the same schedule tells it which, when)
+    HostRegistry* reg = filler.registry();
+    if (reg) {
+        WindowSched dry(lens, blobs, W, live_cap, align);
+        for (int w = 0; dry.next(win); ++w)
+            for (const WinChunk& c : win) reg->need(w, filler.src(c.blob, c.off), c.len);
+        reg->start(std::min(4, std::max(1, host_threads_for_call() / 4)));
+    }
+    bool gather_ok = reg != nullptr || (filler.pinned_all() && filler.pinned_mapped());
+    int k = 0, wi = 0;
     double t_acq = 0, t_build = 0, t_fill = 0, t_enq = 0;
     const double t0 = wall_s();
     while (!r && sched.next(win)) {
         const double ta = wall_s();
         r = pl.acquire(k);
         if (r) break;
+        if (reg && wi >= pl.n) reg->copied(wi - pl.n);  // acquire waited for that window's copy
         const double tb = wall_s();
         t_acq += tb - ta;
         Window& w = pl.w[k];
@@ -308,15 +338,21 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         }
         const double tc = wall_s();
         t_build += tc - tb;
-        // page-locked sources are DMA'd straight from the caller's memory into the device
-        // window; the others go through the pinned host window
-        const bool direct = !tasks.empty() && filler.pinned_all() &&
-                            tasks.size() <= kDirectMaxCalls;
+        // page-locked sources go straight from the caller's memory into the device window: a
+        // DMA a chunk for a few wide chunks, else one gather launch (pinned blobs, or pageable
+        // ones once registered); the others through the pinned host window
+        const bool direct = !tasks.empty() && filler.pinned_all() && tasks.size() <= kDirectMaxCalls;
+        const bool gather = !direct && !tasks.empty() && gather_ok && (!reg || (gather_ok = reg->ready(wi)));
         std::vector<CopyTask> dma;
+        std::vector<GatherSpan> spans;
         if (direct) {
             dma.reserve(tasks.size());
             for (const Filler::Task& t : tasks)
                 if (t.len) dma.push_back({w.dev + (t.dst - w.host), filler.pinned_src(t.b, t.off), (size_t)t.len});
+        } else if (gather) {
+            spans.reserve(tasks.size());
+            for (const Filler::Task& t : tasks)
+                if (t.len) spans.push_back({w.dev + (t.dst - w.host), filler.src(t.b, t.off), t.len});
         } else {
             r = filler.fill(tasks);
             if (r) break;
@@ -325,7 +361,14 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         t_fill += td - tc;
         ++st->windows;
         st->direct_windows += direct;
-        const hipError_t up = direct ? pl.h2d_direct(k, dma, cp) : pl.h2d(k, fill, cp);
+        st->gather_windows += gather;
+        hipError_t up = hipSuccess;
+        if (gather) {
+            r = pl.h2d_gather(D, k, spans, cp);
+            if (r) break;
+        } else {
+            up = direct ? pl.h2d_direct(k, dma, cp) : pl.h2d(k, fill, cp);
+        }
         if (up != hipSuccess || hipStreamWaitEvent(ks, w.copied, 0) != hipSuccess ||
             (crc && hipStreamWaitEvent(kc, w.copied, 0) != hipSuccess)) {
             set_error(KRK_EHIP, "metainfo windows: staging copy failed");
@@ -340,14 +383,61 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         if (crc) pl.release(k, 1, kc);
         t_enq += wall_s() - td;
         k = pl.next(k);
+        ++wi;
     }
     st->max_live = sched.max_live();
+    if (reg) {
+        st->registered_bytes = reg->registered_bytes();
+        st->register_s = reg->register_seconds();
+    }
     if (trace_on())
         fprintf(stderr,
                 "krk_trace windows: windows=%d W=%zu max_live=%llu loop=%.3fs acquire=%.3fs build=%.3fs fill=%.3fs "
                 "enqueue=%.3fs\n",
                 st->windows, W, (unsigned long long)st->max_live, wall_s() - t0, t_acq, t_build, t_fill, t_enq);
     return r;
+}
+
+// KRK_HOST_GATHER: 0 = host-buffer calls always stage; 1 = gather whatever the size; unset
+// (AUTO) = gather page-locked blobs, and register pageable ones when the call windows at
+// least kGatherMinBytes (registration has a fixed cost a call).
+constexpr uint64_t kGatherMinBytes = 256ull << 20;
+std::atomic<int> g_host_gather{-2};  // -2: not read yet; krk_set_host_gather
+int host_gather_mode() {
+    int m = g_host_gather.load(std::memory_order_relaxed);
+    if (m != -2) return m;
+    const char* e = getenv("KRK_HOST_GATHER");
+    int expect = -2;
+    g_host_gather.compare_exchange_strong(expect, e ? (atoi(e) > 0 ? 1 : 0) : -1);
+    return g_host_gather.load();
+}
+
+// The MemFiller of a host-buffer call: page-locked blobs DMA'd or gathered as they are,
+// pageable ones registered for the gather (KRK_HOST_GATHER) or staged.
+void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std::vector<char>& on_host, Device* D) {
+    // KRK_PINNED_DIRECT=0 stages pinned sources too (A/B)
+    static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
+    const int gm = host_gather_mode();
+    f.pinned = allow_direct;
+    uint64_t bytes = 0, first = n;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (on_host[i] || !blobs[i].length) continue;
+        bytes += blobs[i].length;
+        if (first == n) first = i;
+        if (f.pinned && !host_pinned(blobs[i].data, blobs[i].length)) f.pinned = false;
+    }
+    if (first == n) return;
+    f.mapped = f.pinned && gm != 0 && mapped_at_host_address(blobs[first].data);
+    if (!f.pinned && gm != 0 && (gm == 1 || bytes >= kGatherMinBytes)) {
+        std::vector<std::pair<uintptr_t, uintptr_t>> ranges;
+        for (uint64_t i = 0; i < n; ++i)
+            if (!on_host[i] && blobs[i].length) {
+                const uintptr_t a = reinterpret_cast<uintptr_t>(blobs[i].data);
+                ranges.push_back({a, a + blobs[i].length});
+            }
+        f.reg = std::make_unique<HostRegistry>(std::move(ranges));
+        f.gather_stream = D->s_main;  // windows_pass's copy stream
+    }
 }
 
 // KRK_LIVE_CAP: overrides the window's live-stream cap (tests, sweeps).
@@ -490,11 +580,7 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
     } share_guard{t_host_share};
     if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
     MemFiller filler(blobs);
-    // KRK_PINNED_DIRECT=0 stages pinned sources too (A/B)
-    static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
-    filler.pinned = allow_direct;
-    for (uint64_t i = 0; i < n && filler.pinned; ++i)
-        if (!on_host[i] && lens[i] && !host_pinned(blobs[i].data, lens[i])) filler.pinned = false;
+    setup_mem_filler(filler, blobs, n, on_host, D);
     CallStats st;
     r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, 64, live_cap_for(D), o.d_sums,
                      o.d_dig, o.d_state, &st);
@@ -571,10 +657,7 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     } share_guard{t_host_share};
     if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
     MemFiller filler(blobs.data());
-    static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
-    filler.pinned = allow_direct;
-    for (uint64_t i = 0; i < n && filler.pinned; ++i)
-        if (!on_host[i] && lengths[i] && !host_pinned(data_host[i], lengths[i])) filler.pinned = false;
+    setup_mem_filler(filler, blobs.data(), n, on_host, D);
     CallStats st;
     int r = windows_pass(D, n, lengths, plens.data(), soff.data(), on_host, filler, 64, live_cap_for(D), nullptr,
                          d_dig, d_state, &st, /*crc=*/false);
@@ -708,6 +791,19 @@ int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs
 int krk_windows_last_direct(int* direct_windows) {
     KRK_CHECK(direct_windows, KRK_EINVAL, "direct_windows is NULL");
     *direct_windows = t_last_call.direct_windows;
+    return KRK_OK;
+}
+
+int krk_set_host_gather(int mode) {
+    KRK_CHECK(mode >= -1 && mode <= 1, KRK_EINVAL, "host gather mode %d outside -1 (auto), 0, 1", mode);
+    g_host_gather.store(mode);
+    return KRK_OK;
+}
+
+int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, double* register_seconds) {
+    if (gather_windows) *gather_windows = t_last_call.gather_windows;
+    if (registered_bytes) *registered_bytes = t_last_call.registered_bytes;
+    if (register_seconds) *register_seconds = t_last_call.register_s;
     return KRK_OK;
 }
 

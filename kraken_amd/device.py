@@ -420,9 +420,17 @@ def windows_last_call() -> dict:
     """The calling thread's last krk_metainfo_digest_host / _files call: the most live blobs
     in a window, the windows, the blobs the host offload took (krk_windows_last_call)."""
     m, w, h, d = C.c_uint64(), C.c_int(), C.c_uint64(), C.c_int()
+    g, rb, rs = C.c_int(), C.c_uint64(), C.c_double()
     check(lib.krk_windows_last_call(C.byref(m), C.byref(w), C.byref(h)))
     check(lib.krk_windows_last_direct(C.byref(d)))
-    return {"max_live": m.value, "windows": w.value, "host_blobs": h.value, "direct_windows": d.value}
+    check(lib.krk_windows_last_gather(C.byref(g), C.byref(rb), C.byref(rs)))
+    return {"max_live": m.value, "windows": w.value, "host_blobs": h.value, "direct_windows": d.value,
+            "gather_windows": g.value, "registered_bytes": rb.value, "register_s": rs.value}
+
+
+def set_host_gather(mode: int):
+    """krk_set_host_gather: -1 AUTO (default), 0 stage every window, 1 gather any size."""
+    check(lib.krk_set_host_gather(int(mode)))
 
 
 def device_pci_bus_id() -> str:

@@ -595,3 +595,41 @@ def test_public_header_is_the_bound_surface():
     # every function the Go files in INTEGRATION.md call is public
     called = set(re.findall(r"\bC\.(krk_[a-z0-9_]+)\(", doc))
     assert called <= pub, called - pub
+
+
+def _set_rates(stream, host_sha, h2d, cus=256):
+    r = _capi.krk_planner_rates()
+    for k, v in enumerate(stream):
+        r.sha_stream_bps[k] = v
+    r.d2h_bps = r.h2d_bps = h2d
+    r.host_sha_bps, r.host_crc_bps, r.host_copy_bps = host_sha, 10e9, 10e9
+    r.cus = cus
+    check(lib.krk_planner_rates_set(C.byref(r)))
+
+
+def test_digester_crossover_follows_injected_rates():
+    """AUTO's Digester switch point comes from the planner rates: the
+    fewest live GPU digesters whose aggregate (streams x per-stream rate x 0.93, capped by
+    0.85 x the host link) beats the CPU budget x one thread's SHA-NI rate; none when the host
+    out-hashes the link.  (Measured on MI355X: 636 vs AUTO's 626, bench --workload engine.)"""
+    import math
+    cpus = _capi.host_cpu_budget()[0]
+    n = C.c_int64()
+    check(lib.krk_set_digester_host_streams(-1))
+    try:
+        for host_sha, stream in ((2e9, 57e6), (4e9, 57e6), (2e9, 30e6)):
+            _set_rates([stream, 50e6, 35e6], host_sha, 56e9)
+            check(lib.krk_digester_host_streams(C.byref(n)))
+            want = math.floor(cpus * host_sha / (stream * 0.93)) + 1  # the first m that beats the host
+            assert n.value == want - 1, (host_sha, stream, n.value, want)
+        # a host that out-hashes the link: every AUTO digester stays on the host
+        _set_rates([57e6, 50e6, 35e6], 2e9, 1e9)
+        check(lib.krk_digester_host_streams(C.byref(n)))
+        assert n.value >= (1 << 62)
+        # an operator's pin wins over the rates
+        check(lib.krk_set_digester_host_streams(123))
+        check(lib.krk_digester_host_streams(C.byref(n)))
+        assert n.value == 123
+    finally:
+        check(lib.krk_set_digester_host_streams(-1))
+        check(lib.krk_planner_rates_set(None))
