@@ -140,15 +140,46 @@ __device__ __forceinline__ u32x4 ld16(gptr<u32x4> p) {
     else return *p;
 }
 
+typedef __attribute__((address_space(3))) uint32_t* lds_u32w;
+
+// LDS-DMA ring of one wave (variant 20): step s's 4 KiB land in slot
+// s & 1 by four global_load_lds_dwordx4 (1 KiB each; lane l's source is its own 16 bytes k of
+// the step, so slot word [k][l] is what the register path loads into v_k of lane l and the
+// consumer's ds_read_b128 are bank-conflict free); the next step's four are in flight while
+// this one's lookups run.  NT: nontemporal (aux bit 1).
+template <bool NT>
+__device__ __forceinline__ void glds_issue(uint64_t src, lds_u32w slot) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 16 * k), (__attribute__((address_space(3))) void*)(slot + 256 * k),
+                                         16, 0, NT ? 2 : 0);
+}
+
 template <class TT, int RG, bool LOADONLY = false, bool NT = false, bool DEEP = false>
 __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                      const uint32_t* G, uint32_t lane_mul,
-                                                     const uint32_t* x8pow) {
+                                                     const uint32_t* x8pow, lds_u32w ring = nullptr) {
     uint32_t c = 0;
     uint32_t end = 0;  // end offset (in item) of this lane's last processed byte + 1
     const uint32_t nfull = len / kStep;
     if ((base & 15) == 0) {
-        if (nfull > 0) {
+        if (nfull > 0 && ring) {
+            const uint64_t src = base + lane * kSeg;
+            glds_issue<NT>(src, ring);
+            for (uint32_t s = 0; s < nfull; ++s) {
+                if (s + 1 < nfull) {
+                    glds_issue<NT>(src + uint64_t(s + 1) * kStep, ring + ((s + 1) & 1) * 1024);
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // step s has landed
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                const __attribute__((address_space(3))) u32x4* q =
+                    (const __attribute__((address_space(3))) u32x4*)(ring + (s & 1) * 1024) + lane;
+                const u32x4 v0 = q[0], v1 = q[64], v2 = q[128], v3 = q[192];
+                c = step64<TT, RG, LOADONLY>(c, v0, v1, v2, v3, T, G);
+            }
+            end = (nfull - 1) * kStep + (lane + 1) * kSeg;
+        } else if (nfull > 0) {
             gptr<u32x4> p = as_global<u32x4>(base + lane * kSeg);
             constexpr uint32_t S = kStep / 16;
             if constexpr (DEEP) {
@@ -337,14 +368,14 @@ __device__ __forceinline__ uint32_t next_item(const CrcWork& w, uint32_t it, uin
 template <class TT, int RG, bool COAL, bool LOADONLY, bool NT, bool DEEP, bool QUEUE = false>
 __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const uint32_t* G, const uint32_t lm[4],
                                           const uint32_t* x8pow, uint32_t lane, uint32_t wave0, uint32_t n_waves,
-                                          uint32_t* sums) {
+                                          uint32_t* sums, lds_u32w ring = nullptr) {
     const uint32_t n_items = w.run_items + w.n_items;
     // every wave leaves once the queue head passes n_items (no wave waits on another)
     for (uint32_t it = QUEUE ? next_item<true>(w, 0, 0, lane) : wave0; it < n_items;
          it = next_item<QUEUE>(w, it, n_waves, lane)) {
         const ItemRef ci = fetch_item(w, it);
         uint32_t c = COAL ? lane_crc_coal<TT, RG, LOADONLY>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
-                          : lane_crc_strided<TT, RG, LOADONLY, NT, DEEP>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow);
+                          : lane_crc_strided<TT, RG, LOADONLY, NT, DEEP>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow, ring);
         // Wave XOR-reduction.
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c ^= __shfl_xor(c, off, 64);
@@ -356,7 +387,7 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
 }
 
 template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false, bool DEEP = false,
-          bool QUEUE = false>
+          bool QUEUE = false, bool GLDS = false>
 __global__ void __launch_bounds__(BLOCK)
 crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -388,7 +419,9 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
         if ((uint32_t)(size_t)(lds_u32p)lds != 0) __builtin_trap();
         TabP<PERM> T;
         T.loff = (1u << 16) | ((lane % PERM) << 2);
-        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT, DEEP, QUEUE>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums);
+        // GLDS: the wave's two-step ring after the tables (8 KiB a wave)
+        lds_u32w ring = GLDS ? (lds_u32w)(lds + TW + GW) + (threadIdx.x / 64) * 2048 : nullptr;
+        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT, DEEP, QUEUE>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums, ring);
     } else {
         Tab<R> T;
         T.lo = lds + (lane % R);
@@ -398,14 +431,14 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
 }
 
 template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false,
-          bool DEEP = false, bool QUEUE = false>
+          bool DEEP = false, bool QUEUE = false, bool GLDS = false>
 static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
                                  int blocks_per_cu, hipStream_t s) {
-    constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4;
+    constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4 + (GLDS ? size_t(BLOCK / 64) * 8192 : 0);
     static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE>),
+        attr_err = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE, GLDS>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (attr_err != hipSuccess) return attr_err;
@@ -416,7 +449,7 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
     uint32_t grid = (uint32_t)(want < cap ? want : cap);
     if (grid == 0) return hipSuccess;
     if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
-    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
+    hipLaunchKernelGGL((crc_items_kernel<R, RG, BLOCK, COAL, LOADONLY, PERM, NT, DEEP, QUEUE, GLDS>), dim3(grid), dim3(BLOCK), lds, s, w, tabs, sums);
     return hipGetLastError();
 }
 
@@ -430,9 +463,9 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
 // sums -- is compiled only into the diagnostic build (make diag, -DKRK_DIAG).
 bool crc_variant_valid(int v) {
 #ifdef KRK_DIAG
-    return v >= 0 && v <= 17;
+    return v >= 0 && v <= 21;
 #else
-    return v == 7 || v == 8 || v == 14 || v == 15 || v == 16 || v == 17;
+    return v == 7 || v == 8 || v == 14 || v == 15 || v == 16 || v == 17 || v == 20 || v == 21;
 #endif
 }
 
@@ -454,6 +487,14 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
                           : hipErrorInvalidValue;
         case 17:  // 14 with the work queue
             return w.next ? launch_variant<32, 4, 1024, false, false, 32, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
+                          : hipErrorInvalidValue;
+        // LDS-DMA: R16 byte-addressable tables (64 KiB) + 4 gap replicas
+        // (16 KiB) + a two-step ring per wave (8 KiB), 10 waves (160 KiB), work queue; 21 = nt
+        case 20:
+            return w.next ? launch_variant<16, 4, 640, false, false, 16, false, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
+                          : hipErrorInvalidValue;
+        case 21:
+            return w.next ? launch_variant<16, 4, 640, false, false, 16, true, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
                           : hipErrorInvalidValue;
 #ifdef KRK_DIAG
         case 0:  // strided, interleaved R16 tables, 80 KiB LDS: two 512-thread blocks per CU

@@ -32,6 +32,8 @@ for step in "$@"; do
     bench_files) run bench_files 900 python bench.py --workload files --steps 2 --warmup 1 ;;
     bench_c4) run bench_c4 600 python bench.py --workload c4 ;;
     bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
+    crc_parity) run crc_parity 600 env KRK_CRC_VARIANT=20 $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py tests/test_gpu_digest_metainfo.py ;;
+    crc_ab) for v in 16 20 21 16 20 21; do run crc_c4_v$v.$RANDOM 300 env KRK_CRC_VARIANT=$v python bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
