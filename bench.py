@@ -1456,11 +1456,13 @@ def run_files(a, D, T, rank, world, res):
             D.metainfo_digest_files(paths, lens, P)
         T.barrier()
         with D.KernelTimer():
+            c_f = cpu_seconds()
             t0 = time.perf_counter()
             for _ in range(a.steps):
                 sums_f, dg_f = D.metainfo_digest_files(paths, lens, P)
             T.barrier()
             t1 = time.perf_counter()
+            c_f = cpu_seconds() - c_f
             st = D.windows_last_call()
             sha_n, sha_ms = D.KernelTimer.stats("sha256_multi")
             crc_n, crc_ms = D.KernelTimer.stats("crc32_pieces")
@@ -1474,12 +1476,24 @@ def run_files(a, D, T, rank, world, res):
             pins.append(pa)
         datas = [pins[i % SRC].a[:lens[i]] for i in range(n)]
         D.metainfo_digest_host(datas, P)
-        T.barrier()
-        t0 = time.perf_counter()
-        sums_p, dg_p = D.metainfo_digest_host(datas, P)
-        T.barrier()
-        el_p = T.max_over_ranks(time.perf_counter() - t0)
-        st_p = D.windows_last_call()
+        # pinned blobs: the library's default gathers the wide windows from the caller's pages
+        # (one launch a window); KRK_HOST_GATHER=0's staging copy beside it
+        pinned_paths = {}
+        for name, mode in (("staged", 0), ("gather", -1)):
+            D.set_host_gather(mode)
+            try:
+                T.barrier()
+                c0, t0 = cpu_seconds(), time.perf_counter()
+                sums_p, dg_p = D.metainfo_digest_host(datas, P)
+                cpu_p = cpu_seconds() - c0
+                T.barrier()
+                el_p = T.max_over_ranks(time.perf_counter() - t0)
+                st_p = D.windows_last_call()
+            finally:
+                D.set_host_gather(-1)
+            pinned_paths[name] = {"GBps": round(world * total / el_p / 1e9, 3),
+                                  "host_cpu_s_per_GB": round(cpu_p / (total / 1e9), 4),
+                                  "windows": st_p["windows"], "gather_windows": st_p["gather_windows"]}
         D.set_sha_host_offload(-1)
         try:
             T.barrier()
@@ -1529,11 +1543,14 @@ def run_files(a, D, T, rank, world, res):
                 "roofline": link_roofline(D, value, "files", n),
                 "windows": st, "kernels": {"sha256_multi": {"launches": sha_n, "avg_ms": round(sha_ms / max(sha_n, 1), 3)},
                                            "crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_ms / max(crc_n, 1), 3)}},
+                "host_cpu_s_per_GB": round(c_f / a.steps / (total / 1e9), 4),
                 "pinned_host_memory": {"value": round(world * total / el_p / 1e9, 3), "unit": "GB/s",
                                        "roofline": link_roofline(D, world * total / el_p / 1e9),
-                                       "windows": st_p,
-                                       "what": "the same blobs from pinned host memory (krk_metainfo_digest_host; "
-                                               "direct_windows: windows DMA'd from the caller's pages)"},
+                                       "windows": st_p, "paths": pinned_paths,
+                                       "what": "the same blobs from pinned host memory (krk_metainfo_digest_host): "
+                                               "value = the library's default (wide windows gathered from the "
+                                               "caller's pages, gather.hip); paths.staged = KRK_HOST_GATHER=0 "
+                                               "(pinned -> pinned window copies, then the DMA)"},
                 "default_offload": {"value": round(world * total / el_a / 1e9, 3), "unit": "GB/s",
                                     "host_blobs": st_a["host_blobs"],
                                     "what": "krk_metainfo_digest_files with the library's default host offload (AUTO)"},
