@@ -1089,9 +1089,20 @@ void trace_slow(Engine* E, const char* what, Clock::time_point t0) {
                 std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count());
 }
 
+// Requests a digester may keep in flight: KRK_OWNER_INFLIGHT (8), but no more than its share
+// of the slot pool beyond the submissions' reserve, so that many live digesters (the
+// crossover sweep: 1,024+) do not fill the hard pinned cap with the few that got there first
+// while the others' writers wait at it (then fewer streams make each launch).
+size_t owner_inflight(Engine* E) {
+    const size_t slots = E->pool.cap() / E->pool.S, reserve = E->pool.reserve();
+    const int64_t live = std::max<int64_t>(1, E->live_digesters.load(std::memory_order_relaxed));
+    const size_t share = slots > reserve ? (slots - reserve) / (size_t)live : 0;
+    return std::max<size_t>(2, std::min(g_owner_inflight, share));
+}
+
 int digester_submit(krk_digester* d, const uint8_t* src, uint64_t len, bool final, Slot* sl = nullptr) {
     auto t0 = Clock::now();
-    int rc = digester_drain(d, g_owner_inflight - 1);
+    int rc = digester_drain(d, owner_inflight(d->E) - 1);
     trace_slow(d->E, "drain", t0);
     t0 = Clock::now();
     if (rc) {
