@@ -465,7 +465,7 @@ bool crc_variant_valid(int v) {
 #ifdef KRK_DIAG
     return v >= 0 && v <= 21;
 #else
-    return v == 7 || v == 8 || v == 14 || v == 15 || v == 16 || v == 17 || v == 20 || v == 21;
+    return v == 7 || v == 8 || v == 14 || v == 15 || v == 16 || v == 17;
 #endif
 }
 
@@ -488,15 +488,16 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
         case 17:  // 14 with the work queue
             return w.next ? launch_variant<32, 4, 1024, false, false, 32, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
                           : hipErrorInvalidValue;
-        // LDS-DMA: R16 byte-addressable tables (64 KiB) + 4 gap replicas
-        // (16 KiB) + a two-step ring per wave (8 KiB), 10 waves (160 KiB), work queue; 21 = nt
+#ifdef KRK_DIAG
+        // LDS-DMA (bit-exact, measured in DESIGN.md 4.1): R16 byte-addressable
+        // tables (64 KiB) + 4 gap replicas (16 KiB) + a two-step ring per wave (8 KiB), 10 waves
+        // (160 KiB), work queue; 21 = the same with nt loads
         case 20:
             return w.next ? launch_variant<16, 4, 640, false, false, 16, false, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
                           : hipErrorInvalidValue;
         case 21:
             return w.next ? launch_variant<16, 4, 640, false, false, 16, true, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
                           : hipErrorInvalidValue;
-#ifdef KRK_DIAG
         case 0:  // strided, interleaved R16 tables, 80 KiB LDS: two 512-thread blocks per CU
             return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);
         case 1:  // 144 KiB LDS: one 1024-thread block per CU

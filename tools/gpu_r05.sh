@@ -32,21 +32,22 @@ for step in "$@"; do
     bench_files) run bench_files 900 python bench.py --workload files --steps 2 --warmup 1 ;;
     bench_c4) run bench_c4 600 python bench.py --workload c4 ;;
     bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
-    crc_parity) run crc_parity 600 env KRK_CRC_VARIANT=20 $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py tests/test_gpu_digest_metainfo.py ;;
-    crc_ab) for v in 16 20 21 16 20 21; do run crc_c4_v$v.$RANDOM 300 env KRK_CRC_VARIANT=$v python bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
+    # the LDS-DMA CRC variants live in the diagnostic build (make -C kraken_amd/csrc diag)
+    crc_parity) run crc_parity 600 env KRK_CRC_VARIANT=20 KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py tests/test_gpu_digest_metainfo.py ;;
+    crc_ab) for v in 16 20 21 16 20 21; do run crc_c4_v$v.$RANDOM 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so python bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
     # rocprofv3 summaries (kernel trace + copy trace; PMC passes on their own runs)
     prof_c2) run prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
     prof_e2e) run prof_e2e 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
                   -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
-    prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v rocprofv3 --kernel-trace --stats --output-format csv \
+    prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c4_v$v -- python3 bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
     pmc_c4_v16 | pmc_c4_v20 | pmc_c4_v21)
         v=${step#pmc_c4_v}
         B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
-        run ${step}_valu 300 env KRK_CRC_VARIANT=$v rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        run ${step}_valu 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
             SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv -d gpurun_out/${step}_valu -- $B
-        run ${step}_wait 300 env KRK_CRC_VARIANT=$v rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        run ${step}_wait 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
             SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/${step}_wait -- $B ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
