@@ -164,6 +164,17 @@ def test_c4_full_size_sampled_and_linear(gpu, orc):
     rng = np.random.default_rng(4)
     for pi in [0, 1, n // 2, n - 1] + rng.choice(n, 12, replace=False).tolist():
         assert int(sums[pi]) == orc.crc32_clmul(orc.synth(0, P, offset=pi * P)), pi
+    # every one of the 81,920 pieces against the oracle: the arena's
+    # bytes copied down 1 GiB at a time, each piece CRC'd by the oracle's PCLMUL restatement
+    chunk = 1 << 30
+    bad = []
+    for c0 in range(0, L, chunk):
+        h = arena.buf.to_host(np.uint8, chunk, offset=int(arena.offsets[0]) + c0)
+        for k in range(chunk // P):
+            if int(sums[c0 // P + k]) != orc.crc32_clmul(h[k * P:(k + 1) * P]):
+                bad.append(c0 // P + k)
+        del h
+    assert not bad, bad[:10]
     # the same 20 GiB as ONE piece
     from kraken_amd._capi import check, krk_blob, lib
     one = (krk_blob * 1)(krk_blob(arena.buf.ptr + int(arena.offsets[0]), L, L, 0))
