@@ -208,9 +208,11 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
  *                   process, GPU beyond.  N is the crossover computed from the calling
  *                   thread's device's planner rates: the fewest live GPU digesters whose
  *                   aggregate (live streams x the measured per-stream rate of the launch
- *                   plan they get, capped by the host link) beats the host's (the process's
- *                   CPU budget x one thread's measured SHA-NI rate); never (all on the host)
- *                   when the host out-hashes the link.  KRK_DIGESTER_HOST_STREAMS or
+ *                   plan they get, capped by what the engine's zero-copy slot reads carry:
+ *                   0.58 x the measured pinned H2D rate) beats the host's (the process's CPU
+ *                   budget x one thread's measured SHA-NI rate); never (all on the host) when
+ *                   the host out-hashes that -- the case on MI355X boxes' 16-CPU shares
+ *                   (measured: 32.7 GB/s at best on the GPU against 34-37 on the host).  KRK_DIGESTER_HOST_STREAMS or
  *                   krk_set_digester_host_streams pins N (-1 restores the default).
  * HOST placement needs no device; GPU placement without a gfx950 device is KRK_ENODEV and
  * AUTO without one is HOST (the product's own SHA-NI path, not the oracle). */

@@ -317,15 +317,18 @@ double host_link(const Rates& R) { return 0.85 * R.h2d; }
 // GPU their pending slots are coalesced into multi-stream launches that read the pinned
 // slots in place, m x the tier's per-stream rate (x kEngineEff: the engine's launches
 // start and end with the writers, measured 0.93 of the batch kernel's rate at 256
-// digesters, profiles/r04/bench_engine.json) up to the tier's residency, capped by the
-// host link.  The crossover is the smallest m whose GPU aggregate beats the host's; none
-// (the host out-hashes the link) is INT64_MAX: every AUTO digester stays on the host.
+// digesters, profiles/r04/bench_engine.json) up to the tier's residency, capped by what the
+// engine's zero-copy slot reads carry over the link (kEngineLinkFrac of the pinned H2D
+// rate: at most 32.7 GB/s of 56.6 measured, at 2,048 digesters, profiles/r05/
+// bench_engine.json).  The crossover is the smallest m whose GPU aggregate beats the host's;
+// none (the host out-hashes the engine) is INT64_MAX: every AUTO digester stays on the host.
 constexpr double kEngineEff = 0.93;
+constexpr double kEngineLinkFrac = 0.58;
 double engine_gpu_bps(uint64_t m, const Rates& R) {
     if (!m) return 0;
     const int t = tier_of(m, R.cus);
     const double r = R.stream[t] * kEngineEff;
-    return std::min({(double)m * r, (double)kResidentPerCu[t] * R.cus * r, host_link(R)});
+    return std::min({(double)m * r, (double)kResidentPerCu[t] * R.cus * r, kEngineLinkFrac * R.h2d});
 }
 int64_t digester_crossover(const Rates& R, int threads) {
     const double host = std::max(1, threads) * R.host_sha;

@@ -398,10 +398,15 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
     return r;
 }
 
-// KRK_HOST_GATHER: 0 = host-buffer calls always stage; 1 = gather whatever the size; unset
-// (AUTO) = gather page-locked blobs, and register pageable ones when the call windows at
-// least kGatherMinBytes (registration has a fixed cost a call).
-constexpr uint64_t kGatherMinBytes = 256ull << 20;
+// KRK_HOST_GATHER: 0 = host-buffer calls always stage; 1 = gather pageable blobs too
+// (registered for the call: host_register.hpp); unset (AUTO) = gather page-locked blobs'
+// wide windows, stage pageable ones.  Measured on MI355X, C2 end to end
+// (profiles/r05/bench_c2.json): pageable 100 MiB blobs registered and gathered 27.3 GB/s
+// (3.8 s a pass with the registrations already made, 8.2 s registering 100 GB of fresh 4 KiB
+// pages at ~20 GB/s -- registration does not scale with threads), staged 52.3 GB/s; pinned
+// blobs (the files leg's krk_host_alloc sources) gathered 58.0 GB/s at 0.034 CPU-s/GB,
+// staged 54.9 at 0.134.  The GPU reads 4 KiB-page registrations far slower than the
+// library's huge-page pinned blocks, so AUTO registers nothing.
 std::atomic<int> g_host_gather{-2};  // -2: not read yet; krk_set_host_gather
 int host_gather_mode() {
     int m = g_host_gather.load(std::memory_order_relaxed);
@@ -428,7 +433,7 @@ void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std
     }
     if (first == n) return;
     f.mapped = f.pinned && gm != 0 && mapped_at_host_address(blobs[first].data);
-    if (!f.pinned && gm != 0 && (gm == 1 || bytes >= kGatherMinBytes)) {
+    if (!f.pinned && gm == 1) {
         std::vector<std::pair<uintptr_t, uintptr_t>> ranges;
         for (uint64_t i = 0; i < n; ++i)
             if (!on_host[i] && blobs[i].length) {
@@ -438,6 +443,23 @@ void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std
         f.reg = std::make_unique<HostRegistry>(std::move(ranges));
         f.gather_stream = D->s_main;  // windows_pass's copy stream
     }
+}
+
+// A call's results to the caller's host memory.  `bounce`: through a private pageable
+// buffer -- the call registered pages of the caller's memory (KRK_HOST_GATHER=1), and a
+// HIP copy whose destination starts in a registered page and runs past it is refused.
+int copy_out(void* dst, const void* src_dev, size_t n, bool bounce, const char* what) {
+    if (!n) return KRK_OK;
+    hipError_t e;
+    if (bounce) {
+        std::vector<uint8_t> b(n);
+        e = hipMemcpy(b.data(), src_dev, n, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) memcpy(dst, b.data(), n);
+    } else {
+        e = hipMemcpy(dst, src_dev, n, hipMemcpyDeviceToHost);
+    }
+    KRK_CHECK(e == hipSuccess, KRK_EHIP, "%s copy-out failed: %s", what, hipGetErrorString(e));
+    return KRK_OK;
 }
 
 // KRK_LIVE_CAP: overrides the window's live-stream cap (tests, sweeps).
@@ -589,14 +611,9 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         set_error(KRK_EHIP, "metainfo_digest_host: sync failed");
         r = KRK_EHIP;
     }
-    if (!r && hipMemcpy(digests_host, o.d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error(KRK_EHIP, "digest copy-out failed");
-        r = KRK_EHIP;
-    }
-    if (!r && hi > lo && hipMemcpy(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error(KRK_EHIP, "sums copy-out failed");
-        r = KRK_EHIP;
-    }
+    const bool bounce = filler.reg != nullptr;
+    if (!r) r = copy_out(digests_host, o.d_dig, n * 32, bounce, "digest");
+    if (!r && hi > lo) r = copy_out(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, bounce, "sums");
     if (host_th.joinable()) host_th.join();
     for (size_t q = 0; !r && q < host.size(); ++q) {
         memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
@@ -665,10 +682,7 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
         set_error(KRK_EHIP, "sha256_host: sync failed");
         r = KRK_EHIP;
     }
-    if (!r && hipMemcpy(digests_host, d_dig, n * 32, hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error(KRK_EHIP, "digest copy-out failed");
-        r = KRK_EHIP;
-    }
+    if (!r) r = copy_out(digests_host, d_dig, n * 32, filler.reg != nullptr, "digest");
     if (host_th.joinable()) host_th.join();
     for (size_t q = 0; !r && q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
     st.host_blobs = host.size();

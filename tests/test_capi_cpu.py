@@ -610,20 +610,22 @@ def _set_rates(stream, host_sha, h2d, cus=256):
 def test_digester_crossover_follows_injected_rates():
     """AUTO's Digester switch point comes from the planner rates: the
     fewest live GPU digesters whose aggregate (streams x per-stream rate x 0.93, capped by
-    0.85 x the host link) beats the CPU budget x one thread's SHA-NI rate; none when the host
-    out-hashes the link.  (Measured on MI355X: 636 vs AUTO's 626, bench --workload engine.)"""
+    what the engine's zero-copy reads carry, 0.58 x the pinned H2D rate) beats the CPU budget
+    x one thread's SHA-NI rate; none when the host out-hashes that (the MI355X box, measured:
+    bench --workload engine's sweep never has the GPU ahead of 16 SHA-NI threads)."""
     import math
     cpus = _capi.host_cpu_budget()[0]
     n = C.c_int64()
     check(lib.krk_set_digester_host_streams(-1))
     try:
-        for host_sha, stream in ((2e9, 57e6), (4e9, 57e6), (2e9, 30e6)):
-            _set_rates([stream, 50e6, 35e6], host_sha, 56e9)
+        for host_sha, stream in ((1e9, 57e6), (2e9, 57e6), (1e9, 30e6)):
+            _set_rates([stream, 50e6, 35e6], host_sha, 200e9)  # a link wide enough not to cap
             check(lib.krk_digester_host_streams(C.byref(n)))
             want = math.floor(cpus * host_sha / (stream * 0.93)) + 1  # the first m that beats the host
             assert n.value == want - 1, (host_sha, stream, n.value, want)
-        # a host that out-hashes the link: every AUTO digester stays on the host
-        _set_rates([57e6, 50e6, 35e6], 2e9, 1e9)
+        # a host that out-hashes what the engine carries over the link (0.58 x H2D): every AUTO
+        # digester stays on the host (the MI355X box: 16 x 2.1 GB/s against 0.58 x 56.6)
+        _set_rates([57e6, 50e6, 35e6], 2e9, cpus * 2e9 / 0.58 * 0.99)
         check(lib.krk_digester_host_streams(C.byref(n)))
         assert n.value >= (1 << 62)
         # an operator's pin wins over the rates

@@ -104,15 +104,16 @@ def test_gather_edges_bit_exact(gpu, mode):
 
 
 def test_gather_default_large_pageable_and_pinned_wide(gpu, orc):
-    """The defaults (KRK_HOST_GATHER unset): a 320 MiB pageable batch is registered and
-    gathered; 200 pinned blobs (krk_host_alloc) in windows of more than 64 chunks are
-    gathered without registration; both bit-exact."""
+    """The defaults (KRK_HOST_GATHER unset): a 320 MiB pageable batch stages (registering
+    4 KiB pages measured slower than the staging copy); 200 pinned blobs
+    (krk_host_alloc) in windows of more than 64 chunks are gathered without registration;
+    both bit-exact."""
     D.set_sha_host_offload(0)
     lens = [(1 << 20) + 13 * i for i in range(320)]
     datas = [orc.synth(3000 + i, L) for i, L in enumerate(lens)]
     sums, dg = D.metainfo_digest_host(datas, 4 << 20)
     st = D.windows_last_call()
-    assert st["gather_windows"] == st["windows"] > 0 and st["registered_bytes"] >= sum(lens), st
+    assert st["gather_windows"] == 0 and st["registered_bytes"] == 0 and st["windows"] > 0, st
     for i in range(0, len(lens), 37):
         assert bytes(dg[i]) == hashlib.sha256(datas[i].tobytes()).digest(), i
         assert np.array_equal(sums[i], orc.calc_piece_sums(datas[i], 4 << 20)[1]), i
