@@ -155,7 +155,7 @@ __device__ __forceinline__ void glds_issue(uint64_t src, lds_u32w slot) {
                                          16, 0, NT ? 2 : 0);
 }
 
-template <class TT, int RG, bool LOADONLY = false, bool NT = false, bool DEEP = false>
+template <class TT, int RG, bool LOADONLY = false, bool NT = false, bool DEEP = false, int RING = 2>
 __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len, uint32_t lane, const TT& T,
                                                      const uint32_t* G, uint32_t lane_mul,
                                                      const uint32_t* x8pow, lds_u32w ring = nullptr) {
@@ -164,17 +164,21 @@ __device__ __forceinline__ uint32_t lane_crc_strided(uint64_t base, uint32_t len
     const uint32_t nfull = len / kStep;
     if ((base & 15) == 0) {
         if (nfull > 0 && ring) {
+            // RING - 1 steps in flight: steps s+1 .. s+RING-1 are loading while step s computes
             const uint64_t src = base + lane * kSeg;
-            glds_issue<NT>(src, ring);
+            for (uint32_t k = 0; k + 1 < (uint32_t)RING && k < nfull; ++k)
+                glds_issue<NT>(src + uint64_t(k) * kStep, ring + k * 1024);
             for (uint32_t s = 0; s < nfull; ++s) {
-                if (s + 1 < nfull) {
-                    glds_issue<NT>(src + uint64_t(s + 1) * kStep, ring + ((s + 1) & 1) * 1024);
-                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // step s has landed
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
+                const uint32_t nx = s + RING - 1;  // the step whose loads go out now
+                if (nx < nfull) glds_issue<NT>(src + uint64_t(nx) * kStep, ring + (nx % RING) * 1024);
+                // wait for step s: the loads issued after it may stay in flight
+                const uint32_t after = min(nfull - 1, nx) - s;
+                if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const __attribute__((address_space(3))) u32x4* q =
-                    (const __attribute__((address_space(3))) u32x4*)(ring + (s & 1) * 1024) + lane;
+                    (const __attribute__((address_space(3))) u32x4*)(ring + (s % RING) * 1024) + lane;
                 const u32x4 v0 = q[0], v1 = q[64], v2 = q[128], v3 = q[192];
                 c = step64<TT, RG, LOADONLY>(c, v0, v1, v2, v3, T, G);
             }
@@ -365,7 +369,7 @@ __device__ __forceinline__ uint32_t next_item(const CrcWork& w, uint32_t it, uin
     }
 }
 
-template <class TT, int RG, bool COAL, bool LOADONLY, bool NT, bool DEEP, bool QUEUE = false>
+template <class TT, int RG, bool COAL, bool LOADONLY, bool NT, bool DEEP, bool QUEUE = false, int RING = 2>
 __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const uint32_t* G, const uint32_t lm[4],
                                           const uint32_t* x8pow, uint32_t lane, uint32_t wave0, uint32_t n_waves,
                                           uint32_t* sums, lds_u32w ring = nullptr) {
@@ -375,7 +379,7 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
          it = next_item<QUEUE>(w, it, n_waves, lane)) {
         const ItemRef ci = fetch_item(w, it);
         uint32_t c = COAL ? lane_crc_coal<TT, RG, LOADONLY>(ci.ptr, ci.len, lane, T, G, lm, x8pow)
-                          : lane_crc_strided<TT, RG, LOADONLY, NT, DEEP>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow, ring);
+                          : lane_crc_strided<TT, RG, LOADONLY, NT, DEEP, RING>(ci.ptr, ci.len, lane, T, G, lm[0], x8pow, ring);
         // Wave XOR-reduction.
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c ^= __shfl_xor(c, off, 64);
@@ -387,7 +391,7 @@ __device__ __forceinline__ void item_loop(const CrcWork& w, const TT& T, const u
 }
 
 template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false, bool DEEP = false,
-          bool QUEUE = false, bool GLDS = false>
+          bool QUEUE = false, int GLDS = 0>
 __global__ void __launch_bounds__(BLOCK)
 crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restrict__ sums) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -419,9 +423,10 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
         if ((uint32_t)(size_t)(lds_u32p)lds != 0) __builtin_trap();
         TabP<PERM> T;
         T.loff = (1u << 16) | ((lane % PERM) << 2);
-        // GLDS: the wave's two-step ring after the tables (8 KiB a wave)
-        lds_u32w ring = GLDS ? (lds_u32w)(lds + TW + GW) + (threadIdx.x / 64) * 2048 : nullptr;
-        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT, DEEP, QUEUE>(w, T, G, lm, x8pow, lane, wave0, n_waves, sums, ring);
+        // GLDS: the wave's ring of GLDS 4 KiB steps after the tables
+        lds_u32w ring = GLDS ? (lds_u32w)(lds + TW + GW) + (threadIdx.x / 64) * (GLDS * 1024) : nullptr;
+        item_loop<TabP<PERM>, RG, COAL, LOADONLY, NT, DEEP, QUEUE, (GLDS ? GLDS : 2)>(w, T, G, lm, x8pow, lane, wave0,
+                                                                                 n_waves, sums, ring);
     } else {
         Tab<R> T;
         T.lo = lds + (lane % R);
@@ -431,10 +436,10 @@ crc_items_kernel(CrcWork w, const uint32_t* __restrict__ tabs, uint32_t* __restr
 }
 
 template <int R, int RG, int BLOCK, bool COAL, bool LOADONLY = false, int PERM = 0, bool NT = false,
-          bool DEEP = false, bool QUEUE = false, bool GLDS = false>
+          bool DEEP = false, bool QUEUE = false, int GLDS = 0>
 static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_t* sums, int cus,
                                  int blocks_per_cu, hipStream_t s) {
-    constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4 + (GLDS ? size_t(BLOCK / 64) * 8192 : 0);
+    constexpr size_t lds = size_t(1024) * ((PERM ? PERM : R) + RG) * 4 + size_t(BLOCK / 64) * GLDS * 4096;
     static std::once_flag once;  // host threads may launch concurrently (re-entrant C ABI)
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
@@ -463,7 +468,7 @@ static hipError_t launch_variant(const CrcWork& w, const uint32_t* tabs, uint32_
 // sums -- is compiled only into the diagnostic build (make diag, -DKRK_DIAG).
 bool crc_variant_valid(int v) {
 #ifdef KRK_DIAG
-    return v >= 0 && v <= 21;
+    return v >= 0 && v <= 23;
 #else
     return v == 7 || v == 8 || v == 14 || v == 15 || v == 16 || v == 17;
 #endif
@@ -493,10 +498,16 @@ hipError_t launch_crc_items(const CrcWork& w, const uint32_t* tabs, uint32_t* su
         // tables (64 KiB) + 4 gap replicas (16 KiB) + a two-step ring per wave (8 KiB), 10 waves
         // (160 KiB), work queue; 21 = the same with nt loads
         case 20:
-            return w.next ? launch_variant<16, 4, 640, false, false, 16, false, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
+            return w.next ? launch_variant<16, 4, 640, false, false, 16, false, false, true, 2>(w, tabs, sums, cfg.cus, 1, s)
                           : hipErrorInvalidValue;
         case 21:
-            return w.next ? launch_variant<16, 4, 640, false, false, 16, true, false, true, true>(w, tabs, sums, cfg.cus, 1, s)
+            return w.next ? launch_variant<16, 4, 640, false, false, 16, true, false, true, 2>(w, tabs, sums, cfg.cus, 1, s)
+                          : hipErrorInvalidValue;
+        case 22:  // 6 waves x a three-step ring (two steps in flight a wave, 48 KiB a CU; 152 KiB)
+            return w.next ? launch_variant<16, 4, 384, false, false, 16, false, false, true, 3>(w, tabs, sums, cfg.cus, 1, s)
+                          : hipErrorInvalidValue;
+        case 23:  // 5 waves x a four-step ring (three in flight a wave, 60 KiB a CU; 160 KiB)
+            return w.next ? launch_variant<16, 4, 320, false, false, 16, false, false, true, 4>(w, tabs, sums, cfg.cus, 1, s)
                           : hipErrorInvalidValue;
         case 0:  // strided, interleaved R16 tables, 80 KiB LDS: two 512-thread blocks per CU
             return launch_variant<16, 4, 512, false>(w, tabs, sums, cfg.cus, 2, s);

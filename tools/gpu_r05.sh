@@ -36,6 +36,9 @@ for step in "$@"; do
     # the LDS-DMA CRC variants live in the diagnostic build (make -C kraken_amd/csrc diag)
     crc_parity) run crc_parity 600 env KRK_CRC_VARIANT=20 KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py tests/test_gpu_digest_metainfo.py ;;
     crc_ab) for v in 16 20 21 16 20 21; do run crc_c4_v$v.$RANDOM 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so python bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
+    crc_ab2) for v in 16 22 23 16 22 23; do run crc_c4_v$v.$RANDOM 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so python bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
+    crc_parity22 | crc_parity23) v=${step#crc_parity}
+        run crc_parity$v 600 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py ;;
     # rocprofv3 summaries (kernel trace + copy trace; PMC passes on their own runs)
     prof_c2) run prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
@@ -43,7 +46,7 @@ for step in "$@"; do
                   -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
     prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c4_v$v -- python3 bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
-    pmc_c4_v16 | pmc_c4_v20 | pmc_c4_v21)
+    pmc_c4_v16 | pmc_c4_v20 | pmc_c4_v21 | pmc_c4_v22 | pmc_c4_v23)
         v=${step#pmc_c4_v}
         B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
         run ${step}_valu 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
