@@ -297,6 +297,17 @@ struct ReadTask {
     size_t blob;    // index into the caller's files (for the error message)
 };
 
+// Page-cache reads: before a thread reads its span it hands the kernel the whole span as
+// POSIX_FADV_WILLNEED, so the disk sees every chunk of the span at once (queue depth = the
+// span's chunks) instead of one synchronous chunk read a thread behind 128 KiB readahead.
+// A window holds a chunk of every live file (~140 KiB each at 3,734 live files), which is
+// what kept cold file batches at 0.80 of the disk's large-read rate.  KRK_FILE_WILLNEED=0
+// turns it off (the A/B leg of `bench.py --workload files`).
+inline bool file_willneed() {
+    const char* v = getenv("KRK_FILE_WILLNEED");
+    return !(v && v[0] == '0');
+}
+
 // Returns -1 on success, else the index of the failed task; err = its errno (0 = EOF).
 inline long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) {
     // Spans are cut in a stream of the tasks laid end to end, each padded to 4 KiB
@@ -306,7 +317,16 @@ inline long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) 
     for (const auto& t : tasks) total += padded(t.n);
     std::atomic<long> bad{-1};
     std::atomic<int> bad_errno{0};
+    const bool hint = !direct && file_willneed();
     auto run = [&](size_t lo, size_t hi) {
+        if (hint) {
+            size_t pos = 0;
+            for (size_t i = 0; i < tasks.size() && pos < hi; pos += tasks[i].n, ++i) {
+                const ReadTask& t = tasks[i];
+                const size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
+                if (a < b) posix_fadvise(t.fd, (off_t)(t.off + a - pos), (off_t)(b - a), POSIX_FADV_WILLNEED);
+            }
+        }
         size_t pos = 0;
         for (size_t i = 0; i < tasks.size() && pos < hi; pos += padded(tasks[i].n), ++i) {
             const ReadTask& t = tasks[i];

@@ -424,10 +424,9 @@ void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std
     static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
     const int gm = host_gather_mode();
     f.pinned = allow_direct;
-    uint64_t bytes = 0, first = n;
+    uint64_t first = n;
     for (uint64_t i = 0; i < n; ++i) {
         if (on_host[i] || !blobs[i].length) continue;
-        bytes += blobs[i].length;
         if (first == n) first = i;
         if (f.pinned && !host_pinned(blobs[i].data, blobs[i].length)) f.pinned = false;
     }
