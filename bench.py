@@ -225,11 +225,15 @@ def cpu_baseline_metainfo(lens_sample, ids_sample, piece, target_s, passes=3):
     total = sum(lens_sample) * reps
     what = {3: "SHA-256 pass (SHA-NI) then CRC-32 piece pass (PCLMUL)", 2: "CRC-32 piece pass (PCLMUL) only",
             1: "SHA-256 pass (SHA-NI) only"}[passes]
-    info = {"value": round(total / t / 1e9, 3), "unit": "GB/s", "cores": threads, "cores_source": CORES_SOURCE,
+    src = CORES_SOURCE if threads == node_cores() else (
+        f"one thread per blob, as the reference's one goroutine per blob: min({node_cores()} node cores "
+        f"({CORES_SOURCE}), {len(lens_sample)} blobs)")
+    info = {"value": round(total / t / 1e9, 3), "unit": "GB/s", "cores": threads, "cores_source": src,
             "kind": "port",
             "sample": (f"{len(lens_sample)} synthetic blobs ({sum(lens_sample) / 2**20:.0f} MiB) x {reps} passes "
-                       f"({t:.1f} s): {what}, 32 KiB chunks, one blob per thread, {threads} threads (the host "
-                       "node's cores), oracle/oracle.c"),
+                       f"({t:.1f} s): {what}, 32 KiB chunks, one blob per thread, {threads} threads "
+                       f"({'the host node' if threads == node_cores() else 'of the host node'}'s cores), "
+                       "oracle/oracle.c"),
             "seconds": round(t, 2), "have_shani": bool(O.lib().orc_have_shani()),
             "have_clmul": bool(O.lib().orc_have_clmul())}
     return info, dg, sums
