@@ -1736,8 +1736,8 @@ def files_cold_leg(a, D, T, rank, world, P):
     own synthetic content), fsync'ed, and the page cache dropped for every file before every
     pass (posix_fadvise DONTNEED; the resident share measured by mincore).  Passes: the
     library's GPU-only path (offload off), its default (AUTO offload), O_DIRECT reads
-    (KRK_FILE_DIRECT=1), fewer live files (KRK_LIVE_CAP=2048), the reads without their WILLNEED
-    hint (KRK_FILE_WILLNEED=0), plain reads of the files on 16 threads (the disk roofline), and the
+    (KRK_FILE_DIRECT=1), fewer live files (KRK_LIVE_CAP=2048), the per-file readahead off and at
+    8 MiB (KRK_FILE_READAHEAD_MB), plain reads of the files on 16 threads (the disk roofline), and the
     reference's two reads on the CPU (origin/blobserver/uploader.go:74-94 digest, then
     lib/metainfogen/generator.go:41-58 piece sums): per file back to back (the second read
     from the page cache the first filled, as on an origin with memory to spare) and the two
@@ -1816,17 +1816,19 @@ def files_cold_leg(a, D, T, rank, world, P):
             legs["gpu_only_live2048"]["max_live"] = D.windows_last_call()["max_live"]
         finally:
             os.environ.pop("KRK_LIVE_CAP", None)
-        # the reads without the span-wide WILLNEED hint (staging.hpp par_read): one synchronous
-        # chunk read a thread behind the kernel's readahead
-        os.environ["KRK_FILE_WILLNEED"] = "0"
-        try:
-            s_n, d_n = leg("gpu_only_no_willneed", lambda: D.metainfo_digest_files(paths, lens, P))
-        finally:
-            os.environ.pop("KRK_FILE_WILLNEED", None)
+        # the per-file readahead (staging.hpp par_read; default 2 MiB ahead): off, and 8 MiB
+        ra_out = []
+        for mb in (0, 8):
+            os.environ["KRK_FILE_READAHEAD_MB"] = str(mb)
+            try:
+                ra_out.append(leg(f"gpu_only_readahead{mb}", lambda: D.metainfo_digest_files(paths, lens, P)))
+            finally:
+                os.environ.pop("KRK_FILE_READAHEAD_MB", None)
         rate, got = leg("disk_read", lambda: disk_read_rate(paths))
         legs["disk_read"]["what"] = "plain 8 MiB reads of every file on 16 threads, no compute (the disk roofline)"
-        same = all(np.array_equal(x, y) for x, y in ((d_g, d_a), (d_g, d_d), (d_g, d_l), (d_g, d_n))) and all(
-            all(np.array_equal(x, y) for y in ys) for x, *ys in zip(s_g, s_a, s_d, s_l, s_n))
+        (s_n, d_n), (s_8, d_8) = ra_out
+        same = all(np.array_equal(d_g, y) for y in (d_a, d_d, d_l, d_n, d_8)) and all(
+            all(np.array_equal(x, y) for y in ys) for x, *ys in zip(s_g, s_a, s_d, s_l, s_n, s_8))
         from oracle import oracle as O  # checker and CPU baseline only
         O.build()
         import hashlib

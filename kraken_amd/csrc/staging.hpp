@@ -295,17 +295,22 @@ struct ReadTask {
     uint8_t* dst;
     size_t n;       // bytes wanted (O_DIRECT reads round the last block up)
     size_t blob;    // index into the caller's files (for the error message)
+    std::atomic<uint64_t>* ra = nullptr;  // the file's readahead mark (hinted up to), or null
+    uint64_t flen = 0;                    // the file's length (readahead stops there)
 };
 
-// Page-cache reads: before a thread reads its span it hands the kernel the whole span as
-// POSIX_FADV_WILLNEED, so the disk sees every chunk of the span at once (queue depth = the
-// span's chunks) instead of one synchronous chunk read a thread behind 128 KiB readahead.
-// A window holds a chunk of every live file (~140 KiB each at 3,734 live files), which is
-// what kept cold file batches at 0.80 of the disk's large-read rate.  KRK_FILE_WILLNEED=0
-// turns it off (the A/B leg of `bench.py --workload files`).
-inline bool file_willneed() {
-    const char* v = getenv("KRK_FILE_WILLNEED");
-    return !(v && v[0] == '0');
+// Per-file readahead of the page-cache reads (KRK_FILE_READAHEAD_MB, default 2; 0 = off).
+// A window holds one chunk of every live file -- ~136 KiB each at 3,826 live files -- and the
+// kernel's readahead turns that into ~128 KiB disk requests; the box's disk reads 13.9 GB/s at
+// 128 KiB requests, 18.0 at 1 MiB and 21.9 at 8 MiB (16 threads, tools/micro/disk_probe,
+// profiles/r05/disk_probe.jsonl), and neither more threads nor per-chunk WILLNEED hints
+// move it.  So each file's reads run R bytes ahead of its chunks as POSIX_FADV_WILLNEED in
+// R-sized pieces: one large request a file every R bytes, landing in the page cache while the
+// windows before it are read, and the chunk reads copy from the cache.  Cached files cost a
+// page-cache lookup a hint.
+inline uint64_t file_readahead_bytes() {
+    const char* v = getenv("KRK_FILE_READAHEAD_MB");
+    return (v ? strtoull(v, nullptr, 10) : 2) << 20;
 }
 
 // Returns -1 on success, else the index of the failed task; err = its errno (0 = EOF).
@@ -317,16 +322,8 @@ inline long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) 
     for (const auto& t : tasks) total += padded(t.n);
     std::atomic<long> bad{-1};
     std::atomic<int> bad_errno{0};
-    const bool hint = !direct && file_willneed();
+    const uint64_t R = direct ? 0 : file_readahead_bytes();
     auto run = [&](size_t lo, size_t hi) {
-        if (hint) {
-            size_t pos = 0;
-            for (size_t i = 0; i < tasks.size() && pos < hi; pos += tasks[i].n, ++i) {
-                const ReadTask& t = tasks[i];
-                const size_t a = std::max(lo, pos), b = std::min(hi, pos + t.n);
-                if (a < b) posix_fadvise(t.fd, (off_t)(t.off + a - pos), (off_t)(b - a), POSIX_FADV_WILLNEED);
-            }
-        }
         size_t pos = 0;
         for (size_t i = 0; i < tasks.size() && pos < hi; pos += padded(tasks[i].n), ++i) {
             const ReadTask& t = tasks[i];
@@ -334,6 +331,17 @@ inline long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) 
             if (a >= b) continue;
             a -= pos;
             b -= pos;
+            if (R && t.ra) {  // keep the file hinted R bytes past this read, R bytes a hint
+                const uint64_t want = std::min(t.flen, t.off + b + R);
+                uint64_t mark = t.ra->load(std::memory_order_relaxed);
+                while (mark < want) {
+                    const uint64_t to = std::min(t.flen, mark + R);
+                    if (t.ra->compare_exchange_weak(mark, to)) {
+                        posix_fadvise(t.fd, (off_t)mark, (off_t)(to - mark), POSIX_FADV_WILLNEED);
+                        mark = to;
+                    }
+                }
+            }
             while (a < b) {
                 size_t want = b - a;
                 if (direct) want = (want + 4095) & ~size_t(4095);

@@ -138,7 +138,9 @@ struct FileFiller : Filler {
     bool direct;
     std::vector<int> fd;
     std::vector<char> is_direct;
-    FileFiller(const krk_file_blob* f, uint64_t n, bool want_direct) : files(f), direct(want_direct), fd(n, -1), is_direct(n, 0) {}
+    std::unique_ptr<std::atomic<uint64_t>[]> ra;  // each file's readahead mark (par_read)
+    FileFiller(const krk_file_blob* f, uint64_t n, bool want_direct)
+        : files(f), direct(want_direct), fd(n, -1), is_direct(n, 0), ra(new std::atomic<uint64_t>[n]()) {}
     ~FileFiller() override {
         for (int x : fd)
             if (x >= 0) close(x);
@@ -163,7 +165,8 @@ struct FileFiller : Filler {
             int r = open_file(t.b);
             if (r) return r;
             if (!t.len) continue;
-            (is_direct[t.b] ? odirect : plain).push_back({fd[t.b], t.off, t.dst, (size_t)t.len, (size_t)t.b});
+            (is_direct[t.b] ? odirect : plain)
+                .push_back({fd[t.b], t.off, t.dst, (size_t)t.len, (size_t)t.b, &ra[t.b], files[t.b].length});
         }
         for (int pass = 0; pass < 2; ++pass) {
             const auto& rt = pass ? odirect : plain;
