@@ -1797,7 +1797,8 @@ def files_cold_leg(a, D, T, rank, world, P):
 
         D.set_sha_host_offload(0)
         s_g, d_g = leg("gpu_only", lambda: D.metainfo_digest_files(paths, lens, P))
-        legs["gpu_only"].update({k: v for k, v in D.windows_last_call().items() if k in ("windows", "max_live")})
+        legs["gpu_only"].update({k: v for k, v in D.windows_last_call().items()
+                                 if k in ("windows", "max_live", "phases_s")})
         D.set_sha_host_offload(-1)
         try:
             s_a, d_a = leg("default", lambda: D.metainfo_digest_files(paths, lens, P))
@@ -1822,6 +1823,7 @@ def files_cold_leg(a, D, T, rank, world, P):
             os.environ["KRK_FILE_READAHEAD_MB"] = str(mb)
             try:
                 ra_out.append(leg(f"gpu_only_readahead{mb}", lambda: D.metainfo_digest_files(paths, lens, P)))
+                legs[f"gpu_only_readahead{mb}"]["phases_s"] = D.windows_last_call()["phases_s"]
             finally:
                 os.environ.pop("KRK_FILE_READAHEAD_MB", None)
         rate, got = leg("disk_read", lambda: disk_read_rate(paths))

@@ -70,10 +70,14 @@ int krk_windows_last_direct(int* direct_windows);
  * 0 / 1 forces off / on), the caller bytes it registered and the helper threads' seconds
  * spent registering them. */
 int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, double* register_seconds);
+/* ... and its window loop's wall seconds, split into waiting for a free staging window,
+ * filling windows (staging copies or file reads) and enqueueing copies and kernels. */
+int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s);
 /* The gather of host-buffer calls, process-wide: -1 AUTO (the default: page-locked blobs
- * gathered in wide windows, pageable ones registered and gathered when a call windows at
- * least 256 MiB), 0 off (stage every window through the pinned host windows), 1 on (any
- * size).  KRK_HOST_GATHER sets the same at the first call.  For A/B runs (bench.py). */
+ * gathered in wide windows, pageable ones staged -- measured faster), 0 off
+ * (stage every window through the pinned host windows), 1 on (pageable blobs registered for
+ * the call with hipHostRegister and gathered too).  KRK_HOST_GATHER sets the same at the
+ * first call.  For A/B runs (bench.py). */
 int krk_set_host_gather(int mode);
 
 /* --------------------------------------- host crossover primitives (CPU)

@@ -258,6 +258,9 @@ struct CallStats {
     uint64_t host_blobs = 0;
     uint64_t registered_bytes = 0;  // caller bytes registered for the gather
     double register_s = 0;          // helper-thread seconds spent registering them
+    // the window loop's wall seconds and where it waited: for a free window (acquire), filling
+    // windows from the source (fill: staging copies or file reads), enqueueing copies + kernels
+    double loop_s = 0, acquire_s = 0, fill_s = 0, enqueue_s = 0;
 };
 thread_local CallStats t_last_call;
 
@@ -274,6 +277,7 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         if (!skip[i]) blobs.push_back((uint32_t)i);
     st->max_live = 0;
     st->windows = st->direct_windows = st->gather_windows = 0;
+    st->loop_s = st->acquire_s = st->fill_s = st->enqueue_s = 0;
     if (blobs.empty()) return KRK_OK;
     const size_t W = window_bytes();
     const uint64_t live_cap = std::min<uint64_t>(cap, blobs.size());
@@ -389,6 +393,10 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
         ++wi;
     }
     st->max_live = sched.max_live();
+    st->loop_s = wall_s() - t0;
+    st->acquire_s = t_acq;
+    st->fill_s = t_fill;
+    st->enqueue_s = t_enq;
     if (reg) {
         st->registered_bytes = reg->registered_bytes();
         st->register_s = reg->register_seconds();
@@ -820,6 +828,14 @@ int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, dou
     if (gather_windows) *gather_windows = t_last_call.gather_windows;
     if (registered_bytes) *registered_bytes = t_last_call.registered_bytes;
     if (register_seconds) *register_seconds = t_last_call.register_s;
+    return KRK_OK;
+}
+
+int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s) {
+    if (loop_s) *loop_s = t_last_call.loop_s;
+    if (acquire_s) *acquire_s = t_last_call.acquire_s;
+    if (fill_s) *fill_s = t_last_call.fill_s;
+    if (enqueue_s) *enqueue_s = t_last_call.enqueue_s;
     return KRK_OK;
 }
 

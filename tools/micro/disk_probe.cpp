@@ -190,6 +190,59 @@ int main(int argc, char** argv) {
             report(mode == 0 ? "windows" : mode == 1 ? "windows+willneed_next" : "stream", T, c, now() - t0, extra);
             close_all(fs);
         }
+    // the window schedule with the library's per-file readahead marks (staging.hpp par_read):
+    // each file kept hinted R bytes past its reads, R bytes a WILLNEED
+    for (uint64_t R : {2ull << 20, 8ull << 20})
+        for (int barrier = 1; barrier >= 0; --barrier) {
+            const int T = 16;
+            drop(fs);
+            open_all(fs);
+            const uint64_t c = std::max<uint64_t>(4096, W / fs.size() / 4096 * 4096);
+            std::vector<std::vector<size_t>> wins;  // file index per chunk
+            for (uint64_t off = 0; off < maxlen; off += c) {
+                std::vector<size_t> w;
+                for (size_t i = 0; i < fs.size(); ++i)
+                    if (off < fs[i].len) w.push_back(i);
+                wins.push_back(std::move(w));
+            }
+            std::vector<uint64_t> mark(fs.size(), 0);
+            std::vector<uint8_t> win(W + (64ull << 20));
+            auto read_chunk = [&](size_t f, uint64_t off, uint8_t* dst) {
+                const uint64_t len = std::min(c, fs[f].len - off);
+                const uint64_t want = std::min(fs[f].len, off + len + R);
+                while (mark[f] < want) {  // one thread a file a window: no race
+                    const uint64_t to = std::min(fs[f].len, mark[f] + R);
+                    posix_fadvise(fs[f].fd, (off_t)mark[f], (off_t)(to - mark[f]), POSIX_FADV_WILLNEED);
+                    mark[f] = to;
+                }
+                return pread(fs[f].fd, dst, len, (off_t)off) > 0;
+            };
+            const double t0 = now();
+            if (barrier) {
+                for (size_t wi = 0; wi < wins.size(); ++wi) {
+                    std::atomic<size_t> next{0};
+                    run_threads(T, [&](int) {
+                        for (size_t i; (i = next.fetch_add(1)) < wins[wi].size();)
+                            if (!read_chunk(wins[wi][i], wi * c, win.data() + i * c % W)) break;
+                    });
+                }
+            } else {
+                std::vector<std::pair<size_t, uint64_t>> all;
+                for (size_t wi = 0; wi < wins.size(); ++wi)
+                    for (size_t f : wins[wi]) all.push_back({f, wi * c});
+                std::atomic<size_t> next{0};
+                run_threads(T, [&](int t) {
+                    uint8_t* dst = win.data() + (uint64_t)t * (c + 4096) % W;
+                    for (size_t i; (i = next.fetch_add(1)) < all.size();)
+                        if (!read_chunk(all[i].first, all[i].second, dst)) break;
+                });
+            }
+            char extra[128];
+            snprintf(extra, sizeof extra, ", \"live\": %zu, \"windows\": %zu, \"readahead_MiB\": %llu", fs.size(),
+                     wins.size(), (unsigned long long)(R >> 20));
+            report(barrier ? "windows+readahead" : "stream+readahead", T, c, now() - t0, extra);
+            close_all(fs);
+        }
     for (auto& f : fs) unlink(f.path.c_str());
     return 0;
 }
