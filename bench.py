@@ -1802,7 +1802,8 @@ def files_cold_leg(a, D, T, rank, world, P):
         D.set_sha_host_offload(-1)
         try:
             s_a, d_a = leg("default", lambda: D.metainfo_digest_files(paths, lens, P))
-            legs["default"]["host_blobs"] = D.windows_last_call()["host_blobs"]
+            wl = D.windows_last_call()
+            legs["default"].update({"host_blobs": wl["host_blobs"], "resident_sample": wl["resident_sample"]})
         finally:
             D.set_sha_host_offload(0)
         os.environ["KRK_FILE_DIRECT"] = "1"

@@ -71,8 +71,11 @@ int krk_windows_last_direct(int* direct_windows);
  * spent registering them. */
 int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, double* register_seconds);
 /* ... and its window loop's wall seconds, split into waiting for a free staging window,
- * filling windows (staging copies or file reads) and enqueueing copies and kernels. */
-int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s);
+ * filling windows (staging copies or file reads) and enqueueing copies and kernels; for a
+ * krk_metainfo_digest_files call under AUTO offload, the page-cache resident share of its
+ * sampled files (below 0.5 the batch is treated as disk-bound: no host offload), else -1. */
+int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s,
+                            double* resident);
 /* The gather of host-buffer calls, process-wide: -1 AUTO (the default: page-locked blobs
  * gathered in wide windows, pageable ones staged -- measured faster), 0 off
  * (stage every window through the pinned host windows), 1 on (pageable blobs registered for

@@ -131,7 +131,7 @@ def _load() -> C.CDLL:
         "krk_windows_last_call": (i, [u64p, C.POINTER(C.c_int), u64p]),
         "krk_windows_last_direct": (i, [C.POINTER(C.c_int)]),
         "krk_windows_last_gather": (i, [C.POINTER(C.c_int), u64p, f64p]),
-        "krk_windows_last_phases": (i, [f64p, f64p, f64p, f64p]),
+        "krk_windows_last_phases": (i, [f64p, f64p, f64p, f64p, f64p]),
         "krk_set_host_gather": (i, [i]),
         "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_metainfo_digest_chunks_dev_on": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp, vp]),

@@ -404,6 +404,8 @@ std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads
     return order;
 }
 
+bool offload_auto() { return g_off_threads.load(std::memory_order_relaxed) == KRK_OFFLOAD_AUTO; }
+
 int offload_threads(int mode) {
     const int t = g_off_threads.load(std::memory_order_relaxed);
     if (t != KRK_OFFLOAD_AUTO) return t;

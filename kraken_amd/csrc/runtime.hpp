@@ -733,6 +733,7 @@ inline ShaJob full_job(const void* p, uint64_t len, uint32_t out) {
 enum OffMode { kOffDevice = 0, kOffHostSha = 1, kOffHostWhole = 2, kOffHostFiles = 3 };
 // Host threads the offload of a `mode` batch may use (krk_set_sha_host_offload; 0 = off).
 int offload_threads(int mode = kOffDevice);
+bool offload_auto();  // the offload's threads are KRK_OFFLOAD_AUTO (not set by the caller)
 // What the planners know about this box (offload.cpp): per-stream SHA-256 rate of each
 // AUTO tier at full residency (eight / two / one lane(s)), pinned D2H / H2D, one host
 // thread's SHA-256 and CRC-32; measured on the device at first use.

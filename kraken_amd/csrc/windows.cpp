@@ -16,6 +16,7 @@
 // of SHA workgroups for the window's CRC launch, queued beside it on another stream
 // (profiles/r02/c3_live_cap.jsonl).  The host's work per window is O(live).
 #include <dirent.h>
+#include <sys/mman.h>
 #include <sys/resource.h>
 
 #include <condition_variable>
@@ -261,6 +262,7 @@ struct CallStats {
     // the window loop's wall seconds and where it waited: for a free window (acquire), filling
     // windows from the source (fill: staging copies or file reads), enqueueing copies + kernels
     double loop_s = 0, acquire_s = 0, fill_s = 0, enqueue_s = 0;
+    double resident = -1;  // file batches: the page-cache resident share of the sampled files
 };
 thread_local CallStats t_last_call;
 
@@ -700,6 +702,31 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
     return r;
 }
 
+// The page-cache resident share of a file batch, from up to 64 evenly spaced files' first
+// 16 MiB (mmap + mincore: no page is read).  -1 when none could be sampled.
+static double files_resident_fraction(const krk_file_blob* files, uint64_t n) {
+    const uint64_t step = std::max<uint64_t>(1, n / 64);
+    const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+    uint64_t in = 0, all = 0;
+    std::vector<unsigned char> vec;
+    for (uint64_t i = 0; i < n; i += step) {
+        const size_t len = (size_t)std::min<uint64_t>(files[i].length, 16ull << 20);
+        if (!len) continue;
+        const int fd = open(files[i].path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) continue;  // the pass reports it
+        void* m = mmap(nullptr, len, PROT_READ, MAP_SHARED, fd, 0);
+        close(fd);
+        if (m == MAP_FAILED) continue;
+        vec.assign((len + pg - 1) / pg, 0);
+        if (mincore(m, len, vec.data()) == 0) {
+            for (unsigned char c : vec) in += c & 1;
+            all += vec.size();
+        }
+        munmap(m, len);
+    }
+    return all ? (double)in / (double)all : -1.0;
+}
+
 int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_host, uint8_t* digests_host) {
     KRK_DEVICE(D);
     if (!n) return KRK_OK;
@@ -724,9 +751,15 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
     // Host offload (AUTO by default): the planner's files are read, hashed and piece-summed
     // by host threads in one pass each and never cross the host link.
+    // Under AUTO, a batch mostly out of the page cache is bound by the disk, wherever its bytes
+    // are hashed: host threads would read the same disk and take CPU from the window readers
+    // (cold 32 GiB leg: AUTO 13.4 GB/s against 14.8 GPU-only, profiles/r05/bench_files.json),
+    // so such a batch stays on the windows.
     std::vector<char> on_host(n, 0);
     std::vector<uint32_t> host;
-    const int off_t = offload_threads(kOffHostWhole);
+    int off_t = offload_threads(kOffHostWhole);
+    const double resident = off_t > 0 && offload_auto() ? files_resident_fraction(files, n) : -1.0;
+    if (resident >= 0 && resident < 0.5) off_t = 0;
     if (off_t > 0) {
         host = offload_plan(lens.data(), n, off_t, planner_rates(D), nullptr, nullptr, kOffHostFiles);
         for (uint32_t i : host) on_host[i] = 1;
@@ -775,6 +808,7 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     FdLease fds(std::min<uint64_t>(live_cap_for(D), n));
     r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, fds.n,
                      o.d_sums, o.d_dig, o.d_state, &st);
+    st.resident = resident;
     // drain what was queued even after a read error (the windows' kernels read the buffers)
     const bool synced = hipStreamSynchronize(D->s_a) == hipSuccess && hipStreamSynchronize(D->s_b) == hipSuccess &&
                         hipStreamSynchronize(D->s_main) == hipSuccess;
@@ -831,7 +865,9 @@ int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, dou
     return KRK_OK;
 }
 
-int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s) {
+int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s,
+                            double* resident) {
+    if (resident) *resident = t_last_call.resident;
     if (loop_s) *loop_s = t_last_call.loop_s;
     if (acquire_s) *acquire_s = t_last_call.acquire_s;
     if (fill_s) *fill_s = t_last_call.fill_s;

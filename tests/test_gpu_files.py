@@ -63,6 +63,46 @@ def test_files_edge_lengths_match_oracle(gpu, orc, tmp_path, P, mode, monkeypatc
         assert st["max_live"] == 3 and st["windows"] >= len(lens) // 3
 
 
+def test_files_cold_batch_stays_on_windows_under_auto(gpu, orc, tmp_path):
+    """AUTO offload samples the batch's page-cache residency (mmap + mincore): files out of the
+    cache are disk-bound wherever they are hashed, so none go to host threads; the same files
+    cached do (with rates that make the host worth it).  Outputs equal the oracle both ways."""
+    lens = [4 << 20] * 6 + [3 << 20, 1]
+    datas = [orc.synth(700 + i, L) for i, L in enumerate(lens)]
+    paths = [_write(tmp_path, f"c{i}", d) for i, d in enumerate(datas)]
+
+    def drop():
+        for p in paths:
+            fd = os.open(p, os.O_RDONLY)
+            try:
+                os.fsync(fd)
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            finally:
+                os.close(fd)
+
+    D.set_sha_host_offload(-1)
+    D.set_planner_rates(dict(D.planner_rates(), sha_stream_bps=[1e6, 1e6, 1e6]))  # the host takes files
+    try:
+        drop()
+        sums_c, dg_c = D.metainfo_digest_files(paths, lens, 1 << 20)
+        cold = D.windows_last_call()
+        for p in paths:  # into the page cache
+            with open(p, "rb") as f:
+                f.read()
+        sums_w, dg_w = D.metainfo_digest_files(paths, lens, 1 << 20)
+        warm = D.windows_last_call()
+    finally:
+        D.set_sha_host_offload(0)
+        D.set_planner_rates(None)
+    assert 0 <= cold["resident_sample"] < 0.5 and cold["host_blobs"] == 0, cold
+    assert warm["resident_sample"] >= 0.5 and warm["host_blobs"] > 0, warm
+    for i, d in enumerate(datas):
+        want = hashlib.sha256(d.tobytes()).digest()
+        assert bytes(dg_c[i]) == want and bytes(dg_w[i]) == want, i
+        ref = orc.calc_piece_sums(d, 1 << 20)[1]
+        assert np.array_equal(sums_c[i], ref) and np.array_equal(sums_w[i], ref), i
+
+
 def test_files_errors_keep_reference_texts(gpu, orc, tmp_path):
     d = orc.synth(1, 1 << 20)
     p = _write(tmp_path, "short", d)
