@@ -319,8 +319,8 @@ double host_link(const Rates& R) { return 0.85 * R.h2d; }
 // start and end with the writers, measured 0.93 of the batch kernel's rate at 256
 // digesters, profiles/r04/bench_engine.json) up to the tier's residency, capped by what the
 // engine's zero-copy slot reads carry over the link (kEngineLinkFrac of the pinned H2D
-// rate: at most 32.7 GB/s of 56.6 measured, at 2,048 digesters, profiles/r05/
-// bench_engine.json).  The crossover is the smallest m whose GPU aggregate beats the host's;
+// rate: at most 32.7 GB/s of 56.3 measured, at 2,048 digesters, profiles/r05/
+// bench_engine_inflight_cap.json).  The crossover is the smallest m whose GPU aggregate beats the host's;
 // none (the host out-hashes the engine) is INT64_MAX: every AUTO digester stays on the host.
 constexpr double kEngineEff = 0.93;
 constexpr double kEngineLinkFrac = 0.58;
