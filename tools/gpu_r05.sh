@@ -33,6 +33,11 @@ for step in "$@"; do
     bench_defaults) run bench_defaults 300 python bench.py --workload defaults ;;
     bench_files) run bench_files 900 python bench.py --workload files --steps 2 --warmup 1 ;;
     bench_c4) run bench_c4 600 python bench.py --workload c4 ;;
+    bench_c3) run bench_c3 900 python bench.py --workload c3 ;;
+    bench_c5) run bench_c5 300 python bench.py --workload c5 ;;
+    bench_c5regen) run bench_c5regen 600 python bench.py --workload c5regen ;;
+    bench_c5regen_digest) run bench_c5regen_digest 400 python bench.py --workload c5regen_digest ;;
+    bench_f1) run bench_f1verify 600 python bench.py --workload f1verify ;;
     bench_c1) run bench_c1 300 python bench.py --workload c1 --steps 2 --warmup 1 ;;
     # the LDS-DMA CRC variants live in the diagnostic build (make -C kraken_amd/csrc diag)
     crc_parity) run crc_parity 600 env KRK_CRC_VARIANT=20 KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py tests/test_gpu_digest_metainfo.py ;;
