@@ -17,6 +17,7 @@ run() {  # run <name> <seconds> <cmd...>
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
 for step in "$@"; do
     case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     all) run pytest_all 1000 $PYT tests -m gpu ;;
     new) run pytest_new 600 $PYT tests/test_gpu_files.py tests/test_gpu_digest_metainfo.py tests/test_gpu_bench_contract.py tests/test_gpu_defaults.py tests/test_gpu_bindings.py tests/test_gpu_engine.py ;;
     gather) run gather_probe 240 tools/micro/gather_probe 8 16 ;;
