@@ -7,9 +7,11 @@
 // a rank's CPU share in copy threads.  Here the blobs' pages are registered with
 // hipHostRegister instead -- no byte is touched on the host -- and each window goes up in
 // ONE gather launch that reads the registered pages over PCIe: one host-DRAM read a byte, by
-// the GPU.  Measured on MI355X (profiles/r05/gather_probe.jsonl): registering 100 MiB blobs
-// runs 34.9 GB/s on one thread at 0.029 CPU-s/GB, against 0.145 CPU-s/GB for the staging
-// copy; the gather moves 55-57 GB/s.
+// the GPU.  Used only when KRK_HOST_GATHER=1 asks for it: measured on MI355X it loses to
+// the staging copy for ordinary 4 KiB-page memory (C2 end to end 28.4 against 53.9 GB/s,
+// profiles/r05/bench_c2.json; registration of fresh pages 20-45 GB/s whatever the thread
+// count, profiles/r05/reg_probe.jsonl), so the default stages pageable blobs and gathers
+// only page-locked ones.
 //
 // Registration runs ahead of the window loop on a few helper threads, segment by segment
 // (<= kRegSeg bytes of page-aligned, merged blob ranges), in the order the window schedule
@@ -80,8 +82,9 @@ class HostRegistry {
         for (size_t i = 0; i < seg_.size(); ++i) order_[i] = (uint32_t)i;
         std::stable_sort(order_.begin(), order_.end(), [&](uint32_t x, uint32_t y) { return seg_[x].first < seg_[y].first; });
         need_count_.assign(windows_ + 1, 0);
-        for (uint32_t i : order_)
-            if (seg_[i].first >= 0) need_count_[seg_[i].first + 1]++;
+        // a segment no window reads (none should exist) sorts first and counts as window 0's,
+        // so "the first k segments are registered" always means window w's are
+        for (uint32_t i : order_) need_count_[std::max(seg_[i].first, 0) + 1]++;
         for (int w = 0; w < windows_; ++w) need_count_[w + 1] += need_count_[w];
         state_ = std::vector<std::atomic<int>>(seg_.size());
         for (auto& s : state_) s.store(kPending);
