@@ -80,7 +80,7 @@ def load_valu(workload):
     (tools/pmc_valu.py -> profiles/r03/valu_<workload>.json); the raw counters stay in
     that file, the derived fractions go into the bench line."""
     d, path = None, None
-    for rnd in ("r04", "r03", "r02"):  # the newest round's passes
+    for rnd in ("r05", "r04", "r03", "r02"):  # the newest round's passes
         path = os.path.join(ROOT, "profiles", rnd, f"valu_{workload}.json")
         try:
             d = json.load(open(path))
@@ -392,10 +392,11 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
 
 def load_traffic(path, workload, n):
     """Per-launch HBM bytes from the PMC passes (tools/pmc_traffic.py): `path` if given, else
-    the newest of profiles/r04/pmc_traffic_<workload>.json, profiles/pmc_traffic_<workload>.json
+    the newest of profiles/r05 and r04/pmc_traffic_<workload>.json, profiles/pmc_traffic_<workload>.json
     and (C2) profiles/pmc_traffic.json -- the first whose workload and blob count match."""
     cands = [path] if path else []
-    cands += [os.path.join(ROOT, "profiles", "r04", f"pmc_traffic_{workload}.json"),
+    cands += [os.path.join(ROOT, "profiles", "r05", f"pmc_traffic_{workload}.json"),
+              os.path.join(ROOT, "profiles", "r04", f"pmc_traffic_{workload}.json"),
               os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json"),
               os.path.join(ROOT, "profiles", "pmc_traffic.json")]
     for c in cands:
@@ -404,8 +405,12 @@ def load_traffic(path, workload, n):
         except (ValueError, OSError):
             continue
         if pm.get("workload") == workload and pm.get("blobs") == n:
+            TRAFFIC_FOUND[workload] = os.path.relpath(c, ROOT)
             return pm.get("bytes_per_launch", {})
     return {}
+
+
+TRAFFIC_FOUND = {}  # workload -> the committed PMC file load_traffic used
 
 
 def run_metainfo(a, D, T, rank, world, res):
@@ -746,7 +751,7 @@ def link_roofline(D, gbps, traffic_workload=None, n=None):
                             "window_bytes": win,
                             "over_algorithmic": {k: round(t[k] / win, 4) for k in ("crc32_pieces", "sha256_multi")
                                                  if k in t},
-                            "source": f"profiles/r04/pmc_traffic_{traffic_workload}.json (FETCH_SIZE/WRITE_SIZE "
+                            "source": f"{TRAFFIC_FOUND.get(traffic_workload)} (FETCH_SIZE/WRITE_SIZE "
                                       "passes, gfx950 correction)"}
     return r
 

@@ -55,6 +55,20 @@ for step in "$@"; do
                   -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
     prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c4_v$v -- python3 bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
+    # round-5 PMC of the production kernels on the current tree (tools/pmc_traffic.py, pmc_valu.py)
+    pmc_c2 | pmc_c4 | pmc_files)
+        case $step in
+        pmc_c2) B="python3 bench.py --steps 1 --warmup 0 --no-e2e --no-cpu-baseline --no-ceiling" ;;
+        pmc_c4) B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-e2e --no-cpu-baseline" ;;
+        pmc_files) B="python3 bench.py --workload files --steps 1 --warmup 0 --cold-gib 0 --no-cpu-baseline" ;;
+        esac
+        X=${step#pmc_}
+        run pmc_${X}_valu 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+            SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv -d gpurun_out/pmc_${X}_valu -- $B
+        run pmc_${X}_wait 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmc_${X}_wait -- $B
+        run pmc_${X}_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_${X}_fetch -- $B
+        run pmc_${X}_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_${X}_write -- $B ;;
     pmc_c4_v16 | pmc_c4_v20 | pmc_c4_v21 | pmc_c4_v22 | pmc_c4_v23)
         v=${step#pmc_c4_v}
         B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
