@@ -56,8 +56,9 @@ for step in "$@"; do
     prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c4_v$v -- python3 bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
     # round-5 PMC of the production kernels on the current tree (tools/pmc_traffic.py, pmc_valu.py)
-    pmc_c2 | pmc_c4 | pmc_files)
+    pmc_c2 | pmc_c4 | pmc_files | pmc_e2e)
         case $step in
+        pmc_e2e) B="python3 bench.py --e2e-only --no-cpu-baseline" ;;
         pmc_c2) B="python3 bench.py --steps 1 --warmup 0 --no-e2e --no-cpu-baseline --no-ceiling" ;;
         pmc_c4) B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-e2e --no-cpu-baseline" ;;
         pmc_files) B="python3 bench.py --workload files --steps 1 --warmup 0 --cold-gib 0 --no-cpu-baseline" ;;
