@@ -29,7 +29,7 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = {"crc_items_kernel": "crc32_pieces", "sha256_ws_kernel": "sha256_multi", "sha256_w8_kernel": "sha256_multi",
+KERNELS = {"crc_items_kernel": "crc32_pieces", "gather_kernel": "host_gather", "sha256_ws_kernel": "sha256_multi", "sha256_w8_kernel": "sha256_multi",
            "hrw_order_kernel": "hrw_order",
            "shard_gather_kernel": "hrw_gather", "synth_fill": "synth_fill"}
 SIMDS = 1024  # 256 CUs x 4 SIMD-32
