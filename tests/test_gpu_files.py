@@ -219,16 +219,53 @@ def c3_law(gpu, orc, tmp_path_factory):
     return lens, srcs, paths, offs, one
 
 
+def _expected_all(lens, srcs, orc):
+    """Every blob's digest and piece sums without hashing 151 GB: blob i is a prefix of source
+    i % 64, so one pass per source gives them all -- SHA-256 (hashlib = crypto/sha256) fed in
+    order of length, a copy finalised at each blob's end; the full pieces' sums are the
+    source's own (the oracle's calcPieceSums); a partial last piece's CRC (zlib = hash/crc32)
+    carried along the blobs whose last piece is the same piece."""
+    import zlib
+    dg = np.zeros((N, 32), dtype=np.uint8)
+    sums = [None] * N
+    for s, x in enumerate(srcs):
+        ids = sorted(range(s, N, SOURCES), key=lambda i: lens[i])
+        full = orc.calc_piece_sums(x[:len(x) // P4 * P4], P4)[1]
+        h, pos = hashlib.sha256(), 0
+        crc, cpos, cpiece = 0, 0, -1
+        for i in ids:
+            L = lens[i]
+            h.update(memoryview(x[pos:L]))
+            pos = L
+            dg[i] = np.frombuffer(h.copy().digest(), dtype=np.uint8)
+            k = L // P4
+            if L % P4:
+                if k != cpiece:
+                    crc, cpos, cpiece = 0, k * P4, k
+                crc = zlib.crc32(memoryview(x[cpos:L]), crc)
+                cpos = L
+                sums[i] = np.concatenate([full[:k], np.array([crc], dtype=np.uint32)])
+            else:
+                sums[i] = np.asarray(full[:k], dtype=np.uint32)
+    return sums, dg
+
+
 def _check_against_one_shot_and_oracle(lens, srcs, offs, one, sums, dg, orc):
     s1, d1 = one
     assert np.array_equal(dg, d1)
     for i in range(N):
         assert np.array_equal(sums[i], s1[int(offs[i]):int(offs[i + 1])]), i
+    # every one of the 16,384 blobs against the reference arithmetic
+    want_sums, want_dg = _expected_all(lens, srcs, orc)
+    bad = [i for i in range(N) if bytes(dg[i]) != bytes(want_dg[i])]
+    assert not bad, bad[:8]
+    bad = [i for i in range(N) if not np.array_equal(sums[i], want_sums[i])]
+    assert not bad, bad[:8]
     L = np.asarray(lens)
     order = np.argsort(-L, kind="stable")
     late = int(order[14336])  # the first blob admitted after the initial 14,336
     partial = int(np.flatnonzero(L % P4)[0])
-    for i in sorted({int(L.argmin()), int(L.argmax()), partial, late}):
+    for i in sorted({int(L.argmin()), int(L.argmax()), partial, late}):  # and a few the direct way
         data = srcs[i % SOURCES][:lens[i]]
         assert bytes(dg[i]) == hashlib.sha256(data.tobytes()).digest(), i
         assert np.array_equal(sums[i], orc.calc_piece_sums(data, P4)[1]), i
