@@ -28,6 +28,7 @@ for step in "$@"; do
     bench_engine_zc) run bench_engine_zc 900 env KRK_ENGINE_SLOT_SRC=zerocopy python bench.py --workload engine ;;
     bench_engine_gather) run bench_engine_gather 900 env KRK_ENGINE_SLOT_SRC=gather python bench.py --workload engine ;;
     diskprobe) run disk_probe 400 bash -c 'd=$(mktemp -d -p .); tools/micro/disk_probe $d 32; rc=$?; rm -rf $d; exit $rc' ;;
+    hostmem) run host_mem_probe 400 tools/micro/host_mem_probe 8 16 ;;
     regprobe) run reg_probe 300 tools/micro/reg_probe 8 ;;
     gather_tests) run pytest_gather 600 $PYT tests/test_gpu_gather.py tests/test_gpu_files.py tests/test_gpu_agent_verify.py tests/test_gpu_bindings.py tests/test_gpu_bench_contract.py ;;
     engine_tests) run pytest_engine 600 $PYT tests/test_gpu_engine.py tests/test_gpu_concurrency.py tests/test_gpu_bindings.py tests/test_gpu_digest_metainfo.py ;;

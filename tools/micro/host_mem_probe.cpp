@@ -122,8 +122,8 @@ int main(int argc, char** argv) {
             if (line.rfind("Mems_allowed_list:", 0) == 0) mems = line.substr(18);
         printf("{\"nodes_online\": \"%s\", \"mems_allowed\": \"%s\"}\n", online.c_str(), mems.c_str());
     }
-    for (const char* kind : {"hipHostMalloc", "malloc", "mmap_thp", "mmap_thp_registered", "mmap_thp_interleave_registered",
-                             "hipHostMalloc_numauser"}) {
+    for (const char* kind : {"hipHostMalloc", "malloc", "malloc_1touch", "mmap_thp", "mmap_thp_registered",
+                             "mmap_thp_interleave_registered", "hipHostMalloc_numauser"}) {
         const long huge0 = anon_huge_kb();
         uint8_t* p = nullptr;
         bool pinned = false, mapped = false;
@@ -134,7 +134,7 @@ int main(int argc, char** argv) {
         } else if (!strcmp(kind, "hipHostMalloc_numauser")) {
             if (hipHostMalloc((void**)&p, n, hipHostMallocNumaUser) != hipSuccess) return 1;
             pinned = true;
-        } else if (!strcmp(kind, "malloc")) {
+        } else if (!strncmp(kind, "malloc", 6)) {
             p = (uint8_t*)malloc(n);
         } else {
             p = (uint8_t*)mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
@@ -147,8 +147,14 @@ int main(int argc, char** argv) {
                 printf("{\"mbind_rc\": %ld, \"errno\": %d}\n", rc, rc ? errno : 0);
             }
         }
-        // first touch on T threads (spans), as a filling receive path would
-        {
+        // first touch on T threads (spans), as a filling receive path would (malloc_1touch: on
+        // this thread alone, as the bench's numpy buffers are)
+        if (!strcmp(kind, "malloc_1touch")) {
+            for (size_t i = 0; i < n; i += 8) {
+                uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+                memcpy(p + i, &z, 8);
+            }
+        } else {
             std::vector<std::thread> th;
             const size_t span = n / T;
             for (int t = 0; t < T; ++t)
@@ -195,8 +201,9 @@ int main(int argc, char** argv) {
         printf("{\"affinity_cpus\": %d, \"cpus_per_node\": [%d,%d,%d,%d]}\n", CPU_COUNT(&cs), per_node[0], per_node[1],
                per_node[2], per_node[3]);
     }
-    for (const char* kind : {"lib_pinned_cpu_filled", "lib_pinned_dma_filled", "lib_pageable", "lib_thp_interleave_pageable",
-                             "lib_thp_local_registered", "lib_thp_local_pageable"}) {
+    for (const char* kind : {"lib_pinned_cpu_filled", "lib_pinned_spread_filled", "lib_pinned_dma_filled", "lib_pageable",
+                             "lib_pageable_spread", "lib_thp_interleave_pageable", "lib_thp_local_registered",
+                             "lib_thp_local_pageable"}) {
         uint8_t* p = nullptr;
         const bool pinned = strncmp(kind, "lib_pinned", 10) == 0;
         const bool thp = strncmp(kind, "lib_thp", 7) == 0;
@@ -214,6 +221,17 @@ int main(int argc, char** argv) {
         }
         if (!strcmp(kind, "lib_pinned_dma_filled")) {
             if (hipMemcpy(p, dev, n, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+        } else if (strstr(kind, "spread")) {  // written by T threads in spans (a receive path's threads)
+            std::vector<std::thread> th;
+            const size_t span = n / T;
+            for (int t = 0; t < T; ++t)
+                th.emplace_back([=] {
+                    for (size_t i = t * span; i < (t + 1) * span; i += 8) {
+                        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+                        memcpy(p + i, &z, 8);
+                    }
+                });
+            for (auto& x : th) x.join();
         } else {
             for (size_t i = 0; i < n; i += 8) {
                 uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
