@@ -279,12 +279,12 @@ int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n_chunks
  * byte crosses PCIe once, window by window, and both kernels run on each window
  * (SHA-256 chained from per-blob midstates, CRC by byte range) while the next window
  * goes up.  How a window goes up: page-locked blobs (krk_host_alloc) by one DMA a chunk
- * (few wide chunks) or one gather launch that reads the caller's pages over PCIe;
- * pageable blobs of a large call (>= 256 MiB) are registered page by page ahead of the
- * windows (hipHostRegister, released as the windows pass) and gathered the same way, so
- * each byte is read from host memory once, by the GPU; otherwise (small calls, pages that
- * cannot be registered) host threads copy them into the library's pinned windows first.
- * sums_host indexed by blobs[i].sums_offset; digests_host n_blobs*32 bytes.  Synchronous. */
+ * (few wide chunks) or one gather launch that reads the caller's pages over PCIe, so each
+ * byte is read from host memory once, by the GPU; pageable blobs are copied by host threads
+ * into the library's pinned windows first (measured faster than registering the caller's
+ * 4 KiB pages for the gather, which KRK_HOST_GATHER=1 still does).  Allocate receive buffers
+ * with krk_host_alloc to get the one-read path.  sums_host indexed by blobs[i].sums_offset;
+ * digests_host n_blobs*32 bytes.  Synchronous. */
 int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_host,
                              uint8_t* digests_host);
 
