@@ -1827,9 +1827,9 @@ def files_cold_leg(a, D, T, rank, world, P):
             legs["gpu_only_live2048"]["max_live"] = D.windows_last_call()["max_live"]
         finally:
             os.environ.pop("KRK_LIVE_CAP", None)
-        # the per-file readahead (staging.hpp par_read; default 2 MiB ahead): off, and 8 MiB
+        # the per-file readahead (staging.hpp par_read; default off): 2 and 8 MiB ahead
         ra_out = []
-        for mb in (0, 8):
+        for mb in (2, 8):
             os.environ["KRK_FILE_READAHEAD_MB"] = str(mb)
             try:
                 ra_out.append(leg(f"gpu_only_readahead{mb}", lambda: D.metainfo_digest_files(paths, lens, P)))

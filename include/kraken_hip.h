@@ -299,9 +299,9 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* 
  * capped by the file descriptors the process may still open (RLIMIT_NOFILE).  With the host
  * offload (KRK_OFFLOAD_AUTO) the planner's files are read, hashed and piece-summed on host
  * threads in one pass each -- unless a sample of the files (mmap + mincore, no reads) finds
- * them mostly outside the page cache: a disk-bound batch stays on the windows.  Page-cache
- * reads run ahead of the windows per file (POSIX_FADV_WILLNEED, KRK_FILE_READAHEAD_MB, default
- * 2).  Synchronous. */
+ * them mostly outside the page cache: a disk-bound batch stays on the windows.
+ * KRK_FILE_READAHEAD_MB=N keeps each file hinted N MiB ahead of its reads
+ * (POSIX_FADV_WILLNEED; off by default).  Synchronous. */
 int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host,
                               uint8_t* digests_host);
 

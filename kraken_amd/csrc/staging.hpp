@@ -299,18 +299,20 @@ struct ReadTask {
     uint64_t flen = 0;                    // the file's length (readahead stops there)
 };
 
-// Per-file readahead of the page-cache reads (KRK_FILE_READAHEAD_MB, default 2; 0 = off).
+// Per-file readahead of the page-cache reads (KRK_FILE_READAHEAD_MB; default 0 = off).
 // A window holds one chunk of every live file -- ~136 KiB each at 3,826 live files -- and the
 // kernel's readahead turns that into ~128 KiB disk requests; the box's disk reads 13.9 GB/s at
 // 128 KiB requests, 18.0 at 1 MiB and 21.9 at 8 MiB (16 threads, tools/micro/disk_probe,
 // profiles/r05/disk_probe.jsonl), and neither more threads nor per-chunk WILLNEED hints
 // move it.  So each file's reads run R bytes ahead of its chunks as POSIX_FADV_WILLNEED in
 // R-sized pieces: one large request a file every R bytes, landing in the page cache while the
-// windows before it are read, and the chunk reads copy from the cache.  Cached files cost a
-// page-cache lookup a hint.
+// windows before it are read, and the chunk reads copy from the cache.  Measured against no
+// hint on four boxes' cold 32 GiB legs (profiles/r05/bench_files*.json): 2 MiB ahead ran
+// 0.91-1.07x, 8 MiB 0.91-1.00x -- no effect beyond the disk's run-to-run noise, so it is off
+// by default and the knob stays for disks where request size is the whole story.
 inline uint64_t file_readahead_bytes() {
     const char* v = getenv("KRK_FILE_READAHEAD_MB");
-    return (v ? strtoull(v, nullptr, 10) : 2) << 20;
+    return (v ? strtoull(v, nullptr, 10) : 0) << 20;
 }
 
 // Returns -1 on success, else the index of the failed task; err = its errno (0 = EOF).
