@@ -480,7 +480,7 @@ def run_metainfo(a, D, T, rank, world, res):
                 "roofline_crc": roof_crc,
                 "kernels": {"crc32_pieces": {"launches": crc_n, "avg_ms": round(crc_avg, 3)},
                             "sha256_multi": {"launches": sha_n, "avg_ms": round(sha_avg, 3)}}})
-    if a.workload in ("c1", "c5regen_digest") and not a.no_offload:
+    if a.workload in ("c1", "c2", "c5regen_digest") and not a.no_offload:
         res["host_offload"] = host_offload_leg(a, D, T, step, lens, world, dg_h, n)
     if a.workload == "c2" and not a.no_e2e:
         res["end_to_end"] = end_to_end(D, T, arena, n, min(a.e2e_mb << 20, lens[0]), P, out, world)
@@ -508,6 +508,7 @@ def host_offload_leg(a, D, T, step, lens, world, dg_h, n):
     batch (C1's one 1 GiB blob, the log-uniform regen batch) gets from the library."""
     thr = host_cores()
     idx, g_s, h_s = D.sha_offload_plan(lens, thr)
+    t_idx, t_start, t_end, t_gpu = D.sha_tail_plan(lens, thr)
     gpu_only = dg_h.copy()  # step() gathers the digests into dg_h
     D.set_sha_host_offload(-1)
     try:
@@ -519,17 +520,27 @@ def host_offload_leg(a, D, T, step, lens, world, dg_h, n):
             step()
         T.barrier()
         el = T.max_over_ranks(time.perf_counter() - t0)
+        tail = D.sha_last_tail()
     finally:
         D.set_sha_host_offload(0)
     total = int(sum(lens))
+    if tail["chains"]:  # the run handed chain tails over (tail_plan beat whole blobs)
+        on_host, host_bytes = tail["chains"], int(total - tail["gpu_prefix_bytes"] -
+                                                  sum(int(lens[i]) for i in set(range(n)) - set(t_idx.tolist())))
+    else:
+        on_host, host_bytes = int(idx.size), int(sum(int(lens[i]) for i in idx))
     return {"value": round(world * total * a.steps / el / 1e9, 3), "unit": "GB/s",
-            "ms_per_step": round(el / a.steps * 1e3, 3), "host_threads": thr, "blobs_on_host": int(idx.size),
-            "bytes_on_host": int(sum(int(lens[i]) for i in idx)), "blobs": n,
-            "model_s": {"gpu": round(g_s, 3), "host": round(h_s, 3)},
+            "ms_per_step": round(el / a.steps * 1e3, 3), "host_threads": thr, "blobs_on_host": on_host,
+            "bytes_on_host": host_bytes, "blobs": n,
+            "model_s": {"gpu": round(g_s, 3), "host": round(h_s, 3), "tail_handoff_end": round(t_end, 3),
+                        "gpu_alone": round(t_gpu, 3)},
+            "tail_handoff": {"chains": tail["chains"], "gpu_prefix_bytes": tail["gpu_prefix_bytes"]},
             "digests_match_gpu_only": bool(np.array_equal(dg_h, gpu_only)),
-            "what": "krk_metainfo_digest_dev with the default offload (AUTO, host cores): the planner's longest "
-                    "blobs hashed on host threads from HBM through pinned double buffers while the GPU hashes "
-                    "the rest and every blob's piece CRCs (DESIGN.md 4.2)"}
+            "what": "krk_metainfo_digest_dev with the default offload (AUTO, host cores): whole blobs hashed on "
+                    "host threads from HBM through pinned double buffers, or -- when the model ends the batch "
+                    "sooner that way -- every chain started on the GPU and the longest chains' tails finished "
+                    "on host threads from the GPU's midstate (tail handoff); the GPU hashes the rest and every "
+                    "blob's piece CRCs (DESIGN.md 4.2)"}
 
 
 def run_regen(a, D, T, rank, world, res):

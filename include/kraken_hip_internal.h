@@ -70,6 +70,17 @@ int krk_windows_last_direct(int* direct_windows);
  * 0 / 1 forces off / on), the caller bytes it registered and the helper threads' seconds
  * spent registering them. */
 int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, double* register_seconds);
+/* The calling thread's last device-resident SHA-256 batch (krk_sha256_dev,
+ * krk_metainfo_digest_dev): chains whose tails host threads finished from the GPU's midstate
+ * (the tail handoff of the host offload; 0 when whole blobs or nothing went to the host) and
+ * the GPU's prefix bytes of those chains.  KRK_SHA_TAIL=0 turns tail handoff off. */
+int krk_sha_last_tail(uint64_t* chains, uint64_t* gpu_prefix_bytes);
+/* Tail handoff plan of the host offload for a device-resident batch (the planner's rates):
+ * chain idx[k] runs its first start[k] bytes on the GPU, the rest on a host thread; *n_out
+ * chains (host_idx / start sized n); *end_s the planned batch end, *gpu_s the GPU alone.
+ * For tests. */
+int krk_sha_tail_plan(const uint64_t* lengths, uint64_t n, int threads, uint32_t* host_idx, uint64_t* start,
+                      uint64_t* n_out, double* end_s, double* gpu_s);
 /* ... and its window loop's wall seconds, split into waiting for a free staging window,
  * filling windows (staging copies or file reads) and enqueueing copies and kernels; for a
  * krk_metainfo_digest_files call under AUTO offload, the page-cache resident share of its

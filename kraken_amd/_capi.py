@@ -132,6 +132,8 @@ def _load() -> C.CDLL:
         "krk_windows_last_direct": (i, [C.POINTER(C.c_int)]),
         "krk_windows_last_gather": (i, [C.POINTER(C.c_int), u64p, f64p]),
         "krk_windows_last_phases": (i, [f64p, f64p, f64p, f64p, f64p]),
+        "krk_sha_last_tail": (i, [u64p, u64p]),
+        "krk_sha_tail_plan": (i, [u64p, C.c_uint64, i, C.POINTER(C.c_uint32), u64p, u64p, f64p, f64p]),
         "krk_set_host_gather": (i, [i]),
         "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_metainfo_digest_chunks_dev_on": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp, vp]),

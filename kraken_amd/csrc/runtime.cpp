@@ -174,21 +174,78 @@ int krk_piece_sums_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_d
     return piece_sums_dev(D, blobs, n_blobs, sums_dev, pick(D, stream));
 }
 
-// The blobs of a device-resident batch the host offload takes (krk_set_sha_host_offload;
-// empty when it is off or would not shorten the batch), and a per-blob mark.
-static std::vector<uint32_t> offload_split(Device* D, const uint64_t* lens, uint64_t n, std::vector<char>& on_host) {
+// The chains of a device-resident batch host threads finish (krk_set_sha_host_offload; empty
+// when it is off or would not shorten the batch), and a per-blob mark: whole blobs
+// (`start` empty: offload_plan), or the tails of chains the GPU starts (tail_plan) when those
+// end the batch sooner -- the model's ends compared, KRK_SHA_TAIL=0 keeps whole blobs only.
+struct HostShare {
+    std::vector<uint32_t> idx;
+    std::vector<uint64_t> start;  // tail handoff: the GPU's prefix of chain idx[k]
+};
+struct TailStats {
+    uint64_t chains = 0, gpu_prefix_bytes = 0;
+};
+static thread_local TailStats t_last_tail;  // krk_sha_last_tail
+static HostShare offload_split(Device* D, const uint64_t* lens, uint64_t n, std::vector<char>& on_host) {
     on_host.assign(n, 0);
+    HostShare hs;
     const int T = offload_threads();
-    if (T <= 0 || n == 0) return {};
-    std::vector<uint32_t> host = offload_plan(lens, n, T, planner_rates(D), nullptr, nullptr);
-    for (uint32_t i : host) on_host[i] = 1;
-    return host;
+    if (T <= 0 || n == 0) return hs;
+    const Rates R = planner_rates(D);
+    double g = 0, h = 0;
+    hs.idx = offload_plan(lens, n, T, R, &g, &h);
+    static const bool tails = !getenv("KRK_SHA_TAIL") || atoi(getenv("KRK_SHA_TAIL")) != 0;
+    if (tails) {
+        const double whole = std::max(g, h);
+        TailPlan tp = tail_plan(lens, n, T, R);
+        if (!tp.idx.empty() && tp.end_s < 0.95 * whole) {
+            hs.idx = std::move(tp.idx);
+            hs.start = std::move(tp.start);
+        }
+    }
+    for (uint32_t i : hs.idx) on_host[i] = 1;
+    t_last_tail = {hs.start.empty() ? 0 : hs.idx.size(), 0};
+    for (uint64_t y : hs.start) t_last_tail.gpu_prefix_bytes += y;
+    return hs;
 }
 
-// Hash the offloaded blobs on host threads (their D2H waits for `ready`) and store the
-// digests into digests_dev on stream s.
-static int offload_run(Device* D, const std::vector<uint32_t>& host, const uint8_t* const* ptrs,
-                       const uint64_t* lens, hipEvent_t ready, uint8_t* digests_dev, hipStream_t s) {
+// The GPU's side of a batch: whole chains, and the prefixes of the chains whose tails host
+// threads finish -- those write their midstates to `note` (page-locked, coherent host memory
+// the kernel stores to over PCIe) instead of a digest.
+static void host_share_jobs(const HostShare& hs, const uint8_t* const* ptrs, std::vector<ShaJob>& jobs) {
+    for (size_t k = 0; k < hs.start.size(); ++k)
+        if (hs.start[k]) {
+            ShaJob j = full_job(ptrs[hs.idx[k]], hs.start[k], hs.idx[k]);
+            j.flags = 0;  // a midstate, not a digest
+            jobs.push_back(j);
+        }
+}
+
+// Page-locked note for the midstates of n chains, every word kTailSentinel; its device
+// address in *dev.
+static int tail_note(uint64_t n, uint32_t** host, uint32_t** dev) {
+    *host = *dev = nullptr;
+    KRK_HIP(hipHostMalloc(reinterpret_cast<void**>(host), std::max<uint64_t>(n, 1) * 32,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    memset(*host, 0xFF, std::max<uint64_t>(n, 1) * 32);
+    static_assert(kTailSentinel == 0xFFFFFFFFu, "the note's fill");
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, *host, 0) != hipSuccess) {
+        hipHostFree(*host);
+        *host = nullptr;
+        KRK_CHECK(false, KRK_EHIP, "sha256 tail handoff: no device address for the midstate note");
+    }
+    *dev = static_cast<uint32_t*>(d);
+    return KRK_OK;
+}
+
+// Hash the host threads' chains (their D2H waits for `ready`; tails wait for their midstates
+// in `note`, written by the launch `gpu_done` follows) and store the digests into digests_dev
+// on stream s.
+static int offload_run(Device* D, const HostShare& hs, const uint8_t* const* ptrs, const uint64_t* lens,
+                       hipEvent_t ready, uint8_t* digests_dev, hipStream_t s, const uint32_t* note = nullptr,
+                       hipEvent_t gpu_done = nullptr) {
+    const std::vector<uint32_t>& host = hs.idx;
     std::vector<const uint8_t*> p(host.size());
     std::vector<uint64_t> l(host.size());
     for (size_t j = 0; j < host.size(); ++j) {
@@ -196,8 +253,54 @@ static int offload_run(Device* D, const std::vector<uint32_t>& host, const uint8
         l[j] = lens[host[j]];
     }
     std::vector<uint8_t> dig(32 * host.size());
-    int r = offload_hash(D, p, l, offload_threads(), ready, dig.data());
+    TailSrc tail{note, host.data(), hs.start.data(), gpu_done};
+    int r = offload_hash(D, p, l, offload_threads(), ready, dig.data(), hs.start.empty() ? nullptr : &tail);
     return r ? r : offload_store(D, host, dig.data(), digests_dev, s);
+}
+
+// A batch's SHA-256 launch on `s` plus its host share: runs the GPU part, the host threads'
+// chains beside it, and returns once the host's digests are queued into digests_dev on
+// `s_out` (with tails: once the launch has ended too, so the note can go).
+static int sha_with_host_share(Device* D, const HostShare& hs, const std::vector<char>& on_host,
+                               const uint8_t* const* ptrs, const uint64_t* lens, uint64_t n, hipEvent_t ready,
+                               uint8_t* digests_dev, hipStream_t s, hipStream_t s_out) {
+    std::vector<ShaJob> jobs;
+    jobs.reserve(n);
+    for (uint64_t i = 0; i < n; ++i)
+        if (!on_host[i]) jobs.push_back(full_job(ptrs[i], lens[i], (uint32_t)i));
+    uint32_t *note = nullptr, *note_dev = nullptr;
+    const bool tails = !hs.start.empty();
+    if (tails) {
+        host_share_jobs(hs, ptrs, jobs);
+        int r = tail_note(n, &note, &note_dev);
+        if (r) return r;
+    }
+    hipEvent_t done = nullptr;
+    int r = KRK_OK;
+    if (tails && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+        set_error(KRK_EHIP, "sha256 tail handoff: event");
+        r = KRK_EHIP;
+    }
+    if (!r) r = run_jobs(D, jobs, digests_dev, note_dev, s);  // the GPU part runs while the host hashes
+    if (!r && tails && hipEventRecord(done, s) != hipSuccess) {
+        set_error(KRK_EHIP, "sha256 tail handoff: event record");
+        r = KRK_EHIP;
+    }
+    if (!r && !hs.idx.empty()) r = offload_run(D, hs, ptrs, lens, ready, digests_dev, s_out, note, done);
+    if (tails) {
+        // the launch wrote the note: it goes only once the launch has ended
+        if (done) hipEventSynchronize(done);
+        else hipStreamSynchronize(s);
+        hipHostFree(note);
+        if (done) hipEventDestroy(done);
+    }
+    return r;
+}
+
+int krk_sha_last_tail(uint64_t* chains, uint64_t* gpu_prefix_bytes) {
+    if (chains) *chains = t_last_tail.chains;
+    if (gpu_prefix_bytes) *gpu_prefix_bytes = t_last_tail.gpu_prefix_bytes;
+    return KRK_OK;
 }
 
 int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint64_t n, uint8_t* digests_dev,
@@ -207,12 +310,13 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
     KRK_CHECK(data_dev && lengths && digests_dev, KRK_EINVAL, "sha256_dev: null argument");
     hipStream_t s = pick(D, stream);
     std::vector<char> on_host;
-    const std::vector<uint32_t> host = offload_split(D, lengths, n, on_host);
-    std::vector<ShaJob> jobs;
-    jobs.reserve(n);
-    for (uint64_t i = 0; i < n; ++i)
-        if (!on_host[i]) jobs.push_back(full_job(data_dev[i], lengths[i], (uint32_t)i));
-    if (host.empty()) return run_jobs(D, jobs, digests_dev, nullptr, s);
+    const HostShare hs = offload_split(D, lengths, n, on_host);
+    if (hs.idx.empty()) {
+        std::vector<ShaJob> jobs;
+        jobs.reserve(n);
+        for (uint64_t i = 0; i < n; ++i) jobs.push_back(full_job(data_dev[i], lengths[i], (uint32_t)i));
+        return run_jobs(D, jobs, digests_dev, nullptr, s);
+    }
     hipEvent_t ready;
     KRK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
     int r = KRK_OK;
@@ -220,8 +324,7 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
         set_error(KRK_EHIP, "sha256_dev: event record failed");
         r = KRK_EHIP;
     }
-    if (!r) r = run_jobs(D, jobs, digests_dev, nullptr, s);  // the GPU part runs while the host hashes
-    if (!r) r = offload_run(D, host, data_dev, lengths, ready, digests_dev, s);
+    if (!r) r = sha_with_host_share(D, hs, on_host, data_dev, lengths, n, ready, digests_dev, s, s);
     hipEventDestroy(ready);
     return r;
 }
@@ -361,19 +464,27 @@ int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* s
         ptrs[i] = blobs[i].data;
     }
     std::vector<char> on_host;
-    const std::vector<uint32_t> host = offload_split(D, lens.data(), n_blobs, on_host);
-    // SHA first: it is the long pole; the CRC kernel fills the rest of the chip.
-    std::vector<ShaJob> jobs;
-    jobs.reserve(n_blobs);
-    for (uint64_t i = 0; i < n_blobs; ++i)
-        if (!on_host[i]) jobs.push_back(full_job(blobs[i].data, blobs[i].length, (uint32_t)i));
-    r = run_jobs(D, jobs, digests_dev, nullptr, D->s_a);
-    if (!r) r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
-    hipEventRecord(j1, D->s_a);
-    hipEventRecord(j2, D->s_b);
-    hipStreamWaitEvent(s, j1, 0);
-    hipStreamWaitEvent(s, j2, 0);
-    if (!r && !host.empty()) r = offload_run(D, host, ptrs.data(), lens.data(), fork, digests_dev, s);
+    const HostShare hs = offload_split(D, lens.data(), n_blobs, on_host);
+    if (hs.idx.empty()) {
+        // SHA first: it is the long pole; the CRC kernel fills the rest of the chip.
+        std::vector<ShaJob> jobs;
+        jobs.reserve(n_blobs);
+        for (uint64_t i = 0; i < n_blobs; ++i) jobs.push_back(full_job(blobs[i].data, blobs[i].length, (uint32_t)i));
+        r = run_jobs(D, jobs, digests_dev, nullptr, D->s_a);
+        if (!r) r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
+        hipEventRecord(j1, D->s_a);
+        hipEventRecord(j2, D->s_b);
+        hipStreamWaitEvent(s, j1, 0);
+        hipStreamWaitEvent(s, j2, 0);
+    } else {
+        // the CRC launch first here: the host share below returns only once the host is done
+        r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
+        hipEventRecord(j2, D->s_b);
+        hipStreamWaitEvent(s, j2, 0);
+        if (!r) r = sha_with_host_share(D, hs, on_host, ptrs.data(), lens.data(), n_blobs, fork, digests_dev, D->s_a, s);
+        hipEventRecord(j1, D->s_a);
+        hipStreamWaitEvent(s, j1, 0);
+    }
     hipEventDestroy(fork);
     hipEventDestroy(j1);
     hipEventDestroy(j2);

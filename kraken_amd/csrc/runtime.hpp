@@ -800,6 +800,26 @@ double engine_gpu_bps(uint64_t m, const Rates& R);
 int64_t digester_crossover(const Rates& R, int threads);
 std::vector<uint32_t> offload_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R, double* gpu_s,
                                    double* host_s, int mode = kOffDevice);
+// Tail handoff of device-resident chains (offload.cpp): chain idx[k] runs its first start[k]
+// bytes on the GPU (0: none) and the rest on a host thread from the GPU's midstate; listed in
+// the order of start (the host threads' queue).  end_s = the planned batch end, gpu_s = the
+// GPU alone; empty when host takeovers would not end the batch sooner.
+struct TailPlan {
+    std::vector<uint32_t> idx;
+    std::vector<uint64_t> start;
+    double gpu_s = 0, end_s = 0;
+};
+TailPlan tail_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R);
+// Where the host threads' chains start (offload_hash): chain j from byte start[j], from the
+// GPU's midstate at note + 8 * slot[j] once the GPU has written it there (all eight words
+// off kTailSentinel, or gpu_done complete), from the IV when start[j] == 0.
+constexpr uint32_t kTailSentinel = 0xFFFFFFFFu;
+struct TailSrc {
+    const volatile uint32_t* note;
+    const uint32_t* slot;
+    const uint64_t* start;
+    hipEvent_t gpu_done;
+};
 void offload_teardown(Device& D);  // krk_shutdown: the offload threads' streams and pinned buffers
 void offload_hash_host(const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
                        uint8_t* out);
@@ -813,7 +833,7 @@ int offload_whole_files(const std::vector<const char*>& paths, const std::vector
                         const std::vector<uint64_t>& plen, const std::vector<uint32_t*>& sums, int threads,
                         uint8_t* out);
 int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::vector<uint64_t>& lens, int threads,
-                 hipEvent_t ready, uint8_t* out);
+                 hipEvent_t ready, uint8_t* out, const TailSrc* tail = nullptr);
 int offload_store(Device* D, const std::vector<uint32_t>& idx, const uint8_t* dig, uint8_t* digests_dev,
                   hipStream_t s);
 

@@ -317,6 +317,27 @@ def set_planner_rates(rates: dict | None):
     check(lib.krk_planner_rates_set(C.byref(r)))
 
 
+def sha_tail_plan(lengths, threads: int):
+    """krk_sha_tail_plan: (chain indices whose tails host threads finish, the GPU's prefix
+    bytes of each, planned end seconds, GPU-alone seconds) -- planner_rates(), no device."""
+    L = np.ascontiguousarray(lengths, dtype=np.uint64)
+    idx = np.zeros(max(L.size, 1), dtype=np.uint32)
+    st = np.zeros(max(L.size, 1), dtype=np.uint64)
+    k, e, g = C.c_uint64(0), C.c_double(0), C.c_double(0)
+    check(lib.krk_sha_tail_plan(L.ctypes.data_as(C.POINTER(C.c_uint64)), L.size, int(threads),
+                                idx.ctypes.data_as(C.POINTER(C.c_uint32)), st.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                C.byref(k), C.byref(e), C.byref(g)))
+    return idx[:k.value].copy(), st[:k.value].copy(), e.value, g.value
+
+
+def sha_last_tail() -> dict:
+    """krk_sha_last_tail: the calling thread's last device-resident SHA-256 batch's tail
+    handoff (chains finished on host threads from the GPU's midstate, the GPU's prefix bytes)."""
+    c, b = C.c_uint64(0), C.c_uint64(0)
+    check(lib.krk_sha_last_tail(C.byref(c), C.byref(b)))
+    return {"chains": c.value, "gpu_prefix_bytes": b.value}
+
+
 def sha_offload_plan(lengths, threads: int, cus: int = 0, mode: int = OFFLOAD_DEVICE):
     """krk_host_offload_plan: (indices of the blobs the host would take, longest first,
     modelled GPU seconds, modelled host seconds) -- no device work (planner_rates(); cus

@@ -635,3 +635,47 @@ def test_digester_crossover_follows_injected_rates():
     finally:
         check(lib.krk_set_digester_host_streams(-1))
         check(lib.krk_planner_rates_set(None))
+
+
+def _replay_tails(lens, idx, start, threads, r, h):
+    """The plan's own schedule replayed: host threads take the chains in the plan's order
+    (ascending GPU prefix), each when it is free AND the GPU has reached the prefix (start /
+    r); the batch ends when the last host tail and the last GPU-only chain end."""
+    import heapq
+    free = [0.0] * threads
+    end = 0.0
+    for i, y in zip(idx, start):
+        t = max(heapq.heappop(free), y / r)
+        done = t + (lens[i] - y) / h
+        heapq.heappush(free, done)
+        end = max(end, done)
+    on_gpu = set(range(len(lens))) - set(int(i) for i in idx)
+    return max([end] + [lens[i] / r for i in on_gpu])
+
+
+def test_sha_tail_plan_follows_rates():
+    """Tail handoff of the host offload (offload.cpp tail_plan): every chain starts on the GPU
+    and host threads finish the tails of the longest from the GPU's midstate.  C2's shape on
+    16 threads at the box's rates (58.5 MB/s a GPU stream, 2.1 GB/s a SHA-NI thread): the batch
+    ends ~1.49 s instead of 1.79; one long chain (C1) goes to the host whole; prefixes are
+    64-byte multiples below each chain's length, listed in ascending order; the plan's replay
+    meets its own end; no host threads, no plan."""
+    from kraken_amd import device as Dv
+    try:
+        _set_rates([58.5e6, 51.7e6, 34.9e6], 2.1e9, 55.9e9)
+        L = [104857600] * 1000
+        idx, start, end_s, gpu_s = Dv.sha_tail_plan(L, 16)
+        assert len(idx) == 1000 and len(set(idx.tolist())) == 1000
+        assert 1.40 < end_s < 1.55 and abs(gpu_s - 104857600 / 58.5e6) < 1e-6, (end_s, gpu_s)
+        assert (start % 64 == 0).all() and (start < 104857600).all() and (np.diff(start.astype(np.int64)) >= 0).all()
+        assert (start[:16] == 0).all() and start[-1] > 0  # the first takeovers are whole blobs
+        assert _replay_tails(L, idx, start, 16, 58.5e6, 2.1e9) <= end_s * 1.001
+        idx, start, end_s, gpu_s = Dv.sha_tail_plan([1 << 30] + [1 << 20] * 5, 16)
+        assert 0 in idx.tolist() and start[idx.tolist().index(0)] == 0 and end_s < 0.6
+        mixed = [(50 + 37 * k % 200) << 20 for k in range(300)]
+        idx, start, end_s, gpu_s = Dv.sha_tail_plan(mixed, 8)
+        assert end_s < gpu_s and _replay_tails(mixed, idx, start, 8, 58.5e6, 2.1e9) <= end_s * 1.001
+        assert all(start[k] < mixed[i] for k, i in enumerate(idx))
+        assert Dv.sha_tail_plan(L, 0)[0].size == 0
+    finally:
+        check(lib.krk_planner_rates_set(None))

@@ -512,6 +512,45 @@ def test_sha_host_offload_bit_exact(gpu, orc, misalign):
         D.set_sha_host_offload(0)
 
 
+@pytest.mark.parametrize("misalign", [0, 3])
+def test_sha_tail_handoff_bit_exact(gpu, orc, misalign):
+    """Tail handoff of the host offload: the GPU runs the first start[k] bytes of a chain and
+    writes its midstate to page-locked host memory, a host thread reads it there and finishes
+    the chain from HBM (prefix lengths are 64-byte multiples; tails end on, around and past
+    the 8 MiB copy-chunk edges).  Rates set so the plan hands tails over whatever the box;
+    digests (krk_sha256_dev, krk_metainfo_digest_dev) equal hashlib, piece sums the oracle."""
+    lens = [(24 << 20) + 13 * k for k in range(40)] + [(8 << 20) + 64, 4096 + 1, 0, 1, 63, 64]
+    ids = list(range(7000, 7000 + len(lens)))
+    P = 1 << 20
+    R = D.planner_rates()
+    rates = dict(R, sha_stream_bps=[50e6, 50e6, 35e6], host_sha_bps=0.2e9, d2h_bps=50e9, h2d_bps=50e9, cus=256)
+    arena = D.BlobArena(lens, P, blob_ids=ids, misalign=misalign)
+    out = D.BatchOutputs(arena)
+    want = [hashlib.sha256(orc.synth(b, L).tobytes()).digest() for b, L in zip(ids, lens)]
+    try:
+        D.set_planner_rates(rates)
+        idx, start, end_s, gpu_s = D.sha_tail_plan(lens, 8)
+        assert idx.size and (start > 0).any() and end_s < 0.95 * gpu_s
+        D.set_sha_host_offload(8)
+        for fn in (D.sha256, D.metainfo_digest):
+            out.digests.from_host(np.zeros(32 * len(lens), dtype=np.uint8))
+            fn(arena, out)
+            D.synchronize()
+            tail = D.sha_last_tail()
+            assert tail["chains"] > 0 and tail["gpu_prefix_bytes"] > 0, (fn.__name__, tail)
+            dg = out.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+            for i in range(len(lens)):
+                assert bytes(dg[i]) == want[i], (fn.__name__, i, lens[i])
+        sums = out.sums.to_host(np.uint32, max(arena.total_pieces, 1))
+        for i, (b, L) in enumerate(zip(ids, lens)):
+            ref = orc.calc_piece_sums(orc.synth(b, L), P)[1]
+            o = int(arena.sums_off[i])
+            assert np.array_equal(sums[o:o + len(ref)], ref), i
+    finally:
+        D.set_sha_host_offload(0)
+        D.set_planner_rates(None)
+
+
 @pytest.mark.parametrize("window_mb", ["1", None])
 def test_sha_host_offload_host_buffers(gpu, orc, window_mb):
     """The host-buffer entry points with the offload on: the longest blobs are worked on
