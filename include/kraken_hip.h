@@ -446,9 +446,14 @@ int krk_event_destroy(void* ev);
  * memory through pinned double buffers while the GPU hashes the rest and every blob's piece
  * CRCs; the digests land in digests_dev as before.  How many go to the host minimises
  * max(GPU time, host time) at the planner's measured rates (krk_planner_rates_get) and is 0
- * unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host, 1,000
- * equal 100 MiB blobs (C2) stay on the GPU.  The call then returns after the host part is
- * hashed (the GPU part stays asynchronous on `stream`).  The host-buffer entry points work
+ * unless that shortens the batch by 10 %: a single 1 GiB blob (C1) goes to the host.  When
+ * whole blobs cannot shorten it -- 1,000 equal 100 MiB blobs (C2) each take the GPU ~1.8 s
+ * wherever the others run -- every chain starts on the GPU and host threads take over the
+ * tails of the longest ones from the GPU's midstate, each as soon as the GPU has reached its
+ * planned split (tail handoff, when the model ends the batch 5 % sooner; KRK_SHA_TAIL=0
+ * off): C2 1.48 s a batch against 1.77.  The call then returns after the host part is
+ * hashed (the GPU part stays asynchronous on `stream`; with tail handoff, once the SHA-256
+ * launch has ended too).  The host-buffer entry points work
  * on their offloaded blobs in place and never upload them: krk_sha256_host hashes them,
  * krk_metainfo_digest_host hashes them AND computes their piece sums (the SHA-256 pass and
  * the CRC pass of a blob are separate host tasks), so the bytes that cross the host link
