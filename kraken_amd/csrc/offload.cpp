@@ -431,6 +431,9 @@ TailPlan tail_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R
         total += (double)lens[i];
     }
     best.gpu_s = gpu_seconds(longest, total, n, R);
+    // only chain-bound batches gain (the GPU's time is its longest chain, not its aggregate
+    // rate), and the plan stays cheap: at most 65,536 chains
+    if (n > (1u << 16) || longest / r < 0.9 * best.gpu_s) return best;
     std::vector<uint32_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
