@@ -75,10 +75,10 @@ int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, dou
  * (the tail handoff of the host offload; 0 when whole blobs or nothing went to the host) and
  * the GPU's prefix bytes of those chains.  KRK_SHA_TAIL=0 turns tail handoff off. */
 int krk_sha_last_tail(uint64_t* chains, uint64_t* gpu_prefix_bytes);
-/* Tail handoff plan of the host offload for a device-resident batch (the planner's rates):
- * chain idx[k] runs its first start[k] bytes on the GPU, the rest on a host thread; *n_out
- * chains (host_idx / start sized n); *end_s the planned batch end, *gpu_s the GPU alone.
- * For tests. */
+/* Tail handoff plan of the host offload for a device-resident batch (the rates
+ * krk_planner_rates_get reports on this thread's device; nominal without one): chain
+ * host_idx[k] runs its first start[k] bytes on the GPU, the rest on a host thread; *n_out
+ * chains (host_idx / start sized n); *end_s the planned batch end, *gpu_s the GPU alone. */
 int krk_sha_tail_plan(const uint64_t* lengths, uint64_t n, int threads, uint32_t* host_idx, uint64_t* start,
                       uint64_t* n_out, double* end_s, double* gpu_s);
 /* ... and its window loop's wall seconds, split into waiting for a free staging window,

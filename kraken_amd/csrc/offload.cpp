@@ -930,7 +930,9 @@ int krk_sha_tail_plan(const uint64_t* lengths, uint64_t n, int threads, uint32_t
                       uint64_t* n_out, double* end_s, double* gpu_s) {
     KRK_CHECK(lengths && host_idx && start && n_out, KRK_EINVAL, "sha_tail_plan: null argument");
     KRK_CHECK(threads >= 0, KRK_EINVAL, "sha_tail_plan: threads < 0");
-    const TailPlan tp = tail_plan(lengths, n, threads, krk::planner_rates(nullptr));
+    int drc = KRK_OK;
+    Device* D = device(&drc);  // none: the override or the nominal rates
+    const TailPlan tp = tail_plan(lengths, n, threads, planner_rates(D));
     *n_out = tp.idx.size();
     for (size_t k = 0; k < tp.idx.size(); ++k) {
         host_idx[k] = tp.idx[k];
