@@ -32,6 +32,7 @@ for step in "$@"; do
     regprobe) run reg_probe 300 tools/micro/reg_probe 8 ;;
     gather_tests) run pytest_gather 600 $PYT tests/test_gpu_gather.py tests/test_gpu_files.py tests/test_gpu_agent_verify.py tests/test_gpu_bindings.py tests/test_gpu_bench_contract.py ;;
     engine_tests) run pytest_engine 600 $PYT tests/test_gpu_engine.py tests/test_gpu_concurrency.py tests/test_gpu_bindings.py tests/test_gpu_digest_metainfo.py ;;
+    tail_trace) run tail_trace 400 env KRK_TRACE=1 python bench.py --no-e2e --no-cpu-baseline ;;
     hyb_sweep) run hyb_sweep 600 env KRK_BENCH_HYBRID=-1,6,8,10,12 python bench.py --e2e-only --no-cpu-baseline ;;
     bench_defaults) run bench_defaults 300 python bench.py --workload defaults ;;
     bench_files) run bench_files 900 python bench.py --workload files --steps 2 --warmup 1 ;;
