@@ -258,44 +258,60 @@ static int offload_run(Device* D, const HostShare& hs, const uint8_t* const* ptr
     return r ? r : offload_store(D, host, dig.data(), digests_dev, s);
 }
 
-// A batch's SHA-256 launch on `s` plus its host share: runs the GPU part, the host threads'
-// chains beside it, and returns once the host's digests are queued into digests_dev on
-// `s_out` (with tails: once the launch has ended too, so the note can go).
-static int sha_with_host_share(Device* D, const HostShare& hs, const std::vector<char>& on_host,
-                               const uint8_t* const* ptrs, const uint64_t* lens, uint64_t n, hipEvent_t ready,
-                               uint8_t* digests_dev, hipStream_t s, hipStream_t s_out) {
-    std::vector<ShaJob> jobs;
-    jobs.reserve(n);
-    for (uint64_t i = 0; i < n; ++i)
-        if (!on_host[i]) jobs.push_back(full_job(ptrs[i], lens[i], (uint32_t)i));
+// A batch's SHA-256 launch plus its host share, in two steps so that other launches (the
+// CRC) can be queued between them: launch() queues the GPU part on `s` (whole chains, and
+// the prefixes of the tails with their midstate note); finish() runs the host threads'
+// chains beside it and returns once their digests are queued into digests_dev on `s_out`
+// (with tails: once the launch has ended too, so the note can go).
+struct ShaHostShare {
+    const HostShare& hs;
     uint32_t *note = nullptr, *note_dev = nullptr;
-    const bool tails = !hs.start.empty();
-    if (tails) {
-        host_share_jobs(hs, ptrs, jobs);
-        int r = tail_note(n, &note, &note_dev);
-        if (r) return r;
-    }
     hipEvent_t done = nullptr;
     int r = KRK_OK;
-    if (tails && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
-        set_error(KRK_EHIP, "sha256 tail handoff: event");
-        r = KRK_EHIP;
-    }
-    if (!r) r = run_jobs(D, jobs, digests_dev, note_dev, s);  // the GPU part runs while the host hashes
-    if (!r && tails && hipEventRecord(done, s) != hipSuccess) {
-        set_error(KRK_EHIP, "sha256 tail handoff: event record");
-        r = KRK_EHIP;
-    }
-    if (!r && !hs.idx.empty()) r = offload_run(D, hs, ptrs, lens, ready, digests_dev, s_out, note, done);
-    if (tails) {
-        // the launch wrote the note: it goes only once the launch has ended
-        if (done) hipEventSynchronize(done);
-        else hipStreamSynchronize(s);
-        hipHostFree(note);
+    explicit ShaHostShare(const HostShare& h) : hs(h) {}
+    ShaHostShare(const ShaHostShare&) = delete;
+    ShaHostShare& operator=(const ShaHostShare&) = delete;
+    ~ShaHostShare() { release(nullptr); }
+    void release(hipStream_t s) {
+        if (note) {  // the launch wrote the note: it goes only once the launch has ended
+            if (done) hipEventSynchronize(done);
+            else if (s) hipStreamSynchronize(s);
+            hipHostFree(note);
+            note = nullptr;
+        }
         if (done) hipEventDestroy(done);
+        done = nullptr;
     }
-    return r;
-}
+    int launch(Device* D, const std::vector<char>& on_host, const uint8_t* const* ptrs, const uint64_t* lens,
+               uint64_t n, uint8_t* digests_dev, hipStream_t s) {
+        std::vector<ShaJob> jobs;
+        jobs.reserve(n);
+        for (uint64_t i = 0; i < n; ++i)
+            if (!on_host[i]) jobs.push_back(full_job(ptrs[i], lens[i], (uint32_t)i));
+        const bool tails = !hs.start.empty();
+        if (tails) {
+            host_share_jobs(hs, ptrs, jobs);
+            if ((r = tail_note(n, &note, &note_dev))) return r;
+            if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+                done = nullptr;
+                set_error(KRK_EHIP, "sha256 tail handoff: event");
+                return r = KRK_EHIP;
+            }
+        }
+        if ((r = run_jobs(D, jobs, digests_dev, note_dev, s))) return r;
+        if (tails && hipEventRecord(done, s) != hipSuccess) {
+            set_error(KRK_EHIP, "sha256 tail handoff: event record");
+            return r = KRK_EHIP;
+        }
+        return r;
+    }
+    int finish(Device* D, const uint8_t* const* ptrs, const uint64_t* lens, hipEvent_t ready, uint8_t* digests_dev,
+               hipStream_t s, hipStream_t s_out) {
+        if (!r && !hs.idx.empty()) r = offload_run(D, hs, ptrs, lens, ready, digests_dev, s_out, note, done);
+        release(s);
+        return r;
+    }
+};
 
 int krk_sha_last_tail(uint64_t* chains, uint64_t* gpu_prefix_bytes) {
     if (chains) *chains = t_last_tail.chains;
@@ -324,7 +340,11 @@ int krk_sha256_dev(const uint8_t* const* data_dev, const uint64_t* lengths, uint
         set_error(KRK_EHIP, "sha256_dev: event record failed");
         r = KRK_EHIP;
     }
-    if (!r) r = sha_with_host_share(D, hs, on_host, data_dev, lengths, n, ready, digests_dev, s, s);
+    if (!r) {
+        ShaHostShare sh(hs);
+        sh.launch(D, on_host, data_dev, lengths, n, digests_dev, s);  // the GPU part runs while the host hashes
+        r = sh.finish(D, data_dev, lengths, ready, digests_dev, s, s);
+    }
     hipEventDestroy(ready);
     return r;
 }
@@ -477,11 +497,15 @@ int krk_metainfo_digest_dev(const krk_blob* blobs, uint64_t n_blobs, uint32_t* s
         hipStreamWaitEvent(s, j1, 0);
         hipStreamWaitEvent(s, j2, 0);
     } else {
-        // the CRC launch first here: the host share below returns only once the host is done
-        r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
+        // SHA first here too (the long pole), then the CRC, then the host share, which
+        // returns once the host is done
+        ShaHostShare sh(hs);
+        r = sh.launch(D, on_host, ptrs.data(), lens.data(), n_blobs, digests_dev, D->s_a);
+        if (!r) r = piece_sums_dev(D, blobs, n_blobs, sums_dev, D->s_b);
         hipEventRecord(j2, D->s_b);
         hipStreamWaitEvent(s, j2, 0);
-        if (!r) r = sha_with_host_share(D, hs, on_host, ptrs.data(), lens.data(), n_blobs, fork, digests_dev, D->s_a, s);
+        const int rf = sh.finish(D, ptrs.data(), lens.data(), fork, digests_dev, D->s_a, s);
+        if (!r) r = rf;
         hipEventRecord(j1, D->s_a);
         hipStreamWaitEvent(s, j1, 0);
     }
