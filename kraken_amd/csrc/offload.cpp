@@ -33,18 +33,16 @@ void host_sha256_blocks(uint32_t h[8], const uint8_t* p, size_t nblocks);
 void host_sha256_final(const uint32_t h[8], uint64_t absorbed, const uint8_t* tail, size_t n, uint8_t out[32]);
 uint32_t host_crc32_update(uint32_t crc, const uint8_t* p, size_t n);
 
-// One host thread, bytes/s: measured once (16 MiB) and derated 5 % for the clock a loaded
-// socket holds -- 16 threads of the C2 tail handoff hashed 2.42 GB/s each against 2.47 for
-// one C1 thread (profiles/r05/c2_tail_handoff_trace.txt, bench_c1.json; 0.85 before round 5
-// under-priced the host by 13 %).  SHA-256 (x86 SHA extensions) and the piece CRC (PCLMUL
-// folding).
+// One host thread, bytes/s: measured once (16 MiB) and derated for the clock a fully
+// loaded socket holds.  SHA-256 (x86 SHA extensions) and the piece CRC (PCLMUL folding).
+constexpr double kHostDerate = 0.85;
 static double time_rate(const std::function<void(const uint8_t*, size_t)>& f) {
     std::vector<uint8_t> buf(16u << 20, 0x5a);
     f(buf.data(), 64 << 10);  // warm
     const auto t0 = std::chrono::steady_clock::now();
     f(buf.data(), buf.size());
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    return 0.95 * buf.size() / std::max(s, 1e-6);
+    return kHostDerate * buf.size() / std::max(s, 1e-6);
 }
 double host_sha_rate() {
     static const double r = time_rate([](const uint8_t* p, size_t n) {
@@ -425,7 +423,12 @@ TailPlan tail_plan(const uint64_t* lens, uint64_t n, int threads, const Rates& R
     TailPlan best;
     if (!n || threads <= 0) return best;
     const double r = R.stream[tier_of(n, R.cus)];
-    const double h = std::min(R.host_sha, R.d2h / threads);
+    // a tail thread runs SHA-NI alone over its two pinned buffers: 16 of them hashed 2.42
+    // GB/s each against 2.47 for one C1 thread (profiles/r05/c2_tail_handoff_trace.txt), so
+    // the rate is derated 2 %, not the 15 % that holds for the host-whole and file modes
+    // (SHA + CRC + copies: the warm files leg lost 58.9 -> 55.0 GB/s when those were priced
+    // at 5 %)
+    const double h = std::min(R.host_sha * (0.98 / kHostDerate), R.d2h / threads);
     if (!(r > 0) || !(h > r)) return best;
     uint64_t longest = 0;
     double total = 0;

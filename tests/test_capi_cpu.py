@@ -656,8 +656,10 @@ def _replay_tails(lens, idx, start, threads, r, h):
 def test_sha_tail_plan_follows_rates():
     """Tail handoff of the host offload (offload.cpp tail_plan): every chain starts on the GPU
     and host threads finish the tails of the longest from the GPU's midstate.  C2's shape on
-    16 threads at the box's rates (58.5 MB/s a GPU stream, 2.1 GB/s a SHA-NI thread): the batch
-    ends ~1.49 s instead of 1.79; one long chain (C1) goes to the host whole; prefixes are
+    16 threads at the box's rates (58.5 MB/s a GPU stream, 2.1 GB/s a SHA-NI thread as the
+    planner reports it -- derated 15 %; a tail thread is priced at 0.98 of the rate measured,
+    2.42 GB/s): the batch ends ~1.43 s instead of 1.79 (measured 1.429); one long chain (C1)
+    goes to the host whole; prefixes are
     64-byte multiples below each chain's length, listed in ascending order; the plan's replay
     meets its own end; no host threads, no plan."""
     from kraken_amd import device as Dv
@@ -666,15 +668,16 @@ def test_sha_tail_plan_follows_rates():
         L = [104857600] * 1000
         idx, start, end_s, gpu_s = Dv.sha_tail_plan(L, 16)
         assert len(idx) == 1000 and len(set(idx.tolist())) == 1000
-        assert 1.40 < end_s < 1.55 and abs(gpu_s - 104857600 / 58.5e6) < 1e-6, (end_s, gpu_s)
+        assert 1.38 < end_s < 1.47 and abs(gpu_s - 104857600 / 58.5e6) < 1e-6, (end_s, gpu_s)
         assert (start % 64 == 0).all() and (start < 104857600).all() and (np.diff(start.astype(np.int64)) >= 0).all()
         assert (start[:16] == 0).all() and start[-1] > 0  # the first takeovers are whole blobs
-        assert _replay_tails(L, idx, start, 16, 58.5e6, 2.1e9) <= end_s * 1.001
+        h = 2.1e9 * 0.98 / 0.85  # a tail thread's rate (offload.cpp tail_plan)
+        assert _replay_tails(L, idx, start, 16, 58.5e6, h) <= end_s * 1.001
         idx, start, end_s, gpu_s = Dv.sha_tail_plan([1 << 30] + [1 << 20] * 5, 16)
         assert 0 in idx.tolist() and start[idx.tolist().index(0)] == 0 and end_s < 0.6
         mixed = [(50 + 37 * k % 200) << 20 for k in range(300)]
         idx, start, end_s, gpu_s = Dv.sha_tail_plan(mixed, 8)
-        assert end_s < gpu_s and _replay_tails(mixed, idx, start, 8, 58.5e6, 2.1e9) <= end_s * 1.001
+        assert end_s < gpu_s and _replay_tails(mixed, idx, start, 8, 58.5e6, h) <= end_s * 1.001
         assert all(start[k] < mixed[i] for k, i in enumerate(idx))
         assert Dv.sha_tail_plan(L, 0)[0].size == 0
     finally:
