@@ -451,7 +451,7 @@ int krk_event_destroy(void* ev);
  * wherever the others run -- every chain starts on the GPU and host threads take over the
  * tails of the longest ones from the GPU's midstate, each as soon as the GPU has reached its
  * planned split (tail handoff, when the model ends the batch 5 % sooner; KRK_SHA_TAIL=0
- * off): C2 1.43 s a batch against 1.77.  The call then returns after the host part is
+ * off): C2 1.42 s a batch against 1.77.  The call then returns after the host part is
  * hashed (the GPU part stays asynchronous on `stream`; with tail handoff, once the SHA-256
  * launch has ended too).  The host-buffer entry points work
  * on their offloaded blobs in place and never upload them: krk_sha256_host hashes them,
