@@ -44,6 +44,7 @@ void set_error(int code, const char* fmt, ...) {
 }
 
 void engine_teardown(Device& D);                 // engine.cpp
+void owner_tables_teardown(Device& D);           // below
 void set_device_set_from_mask(uint64_t mask);    // multidev.cpp
 
 // Everything a device context holds: streams, tables, scratch cache, pinned
@@ -55,6 +56,7 @@ static void teardown_device(Device& D) {
     delete D.staging;  // drains its windows' events
     D.staging = nullptr;
     offload_teardown(D);
+    owner_tables_teardown(D);  // before the scratch cache: the tables' blocks go back to it
     {
         std::lock_guard<std::mutex> g(D.cache.mu);
         for (auto& kv : D.cache.idle) {
@@ -1348,6 +1350,127 @@ static int shard_owner_table(Device* D, const krk_nodes* nodes, const uint8_t* h
                          d_tl, d_tc, s);
 }
 
+// The shard owner tables of the last few memberships a device served (ring.Refresh caches
+// its hrw in the reference, lib/hashring/ring.go:141-165; Locations never recomputes it):
+// keyed by the exact membership bytes (labels, weights, health, MaxReplica).  A table is
+// built once on the caller's stream (ready event); later callers wait for that event and
+// record a per-stream "used" event, and an evicted table's blocks go back to the scratch
+// cache stream-ordered behind every stream that used it.
+namespace krk {
+struct OwnerTable {
+    std::vector<uint8_t> key;
+    int32_t* tl = nullptr;
+    uint8_t* tc = nullptr;
+    hipEvent_t ready = nullptr;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> used;
+    uint64_t stamp = 0;
+};
+struct OwnerTables {
+    std::vector<OwnerTable> e;
+    uint64_t clock = 0;
+};
+}  // namespace krk
+static constexpr size_t kOwnerTables = 8;
+
+static std::vector<uint8_t> owner_key(const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica) {
+    const uint32_t N = nodes->n_nodes;
+    std::vector<uint8_t> k;
+    auto put = [&k](const void* p, size_t n) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        k.insert(k.end(), b, b + n);
+    };
+    put(&N, 4);
+    put(&max_replica, 4);
+    put(nodes->label_off, (N + 1) * 8);
+    put(nodes->labels + nodes->label_off[0], nodes->label_off[N] - nodes->label_off[0]);
+    put(nodes->weights, N * 8);
+    put(healthy, N);
+    return k;
+}
+
+static void owner_release(Device* D, OwnerTable& t, hipStream_t s) {
+    for (auto& u : t.used) {
+        hipStreamWaitEvent(s, u.second, 0);
+        hipEventDestroy(u.second);
+    }
+    if (t.ready) hipEventDestroy(t.ready);
+    if (t.tl) scratch_free(D, t.tl, s);
+    if (t.tc) scratch_free(D, t.tc, s);
+    t = OwnerTable{};
+}
+
+// Device pointers of the owner table of (nodes, healthy, max_replica), usable on stream s
+// once the call returns (s waits for its build); the caller's use is recorded after its
+// launch with owner_used().
+static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica,
+                       uint32_t row_out, int32_t** d_tl, uint8_t** d_tc, size_t* slot, hipStream_t s) {
+    std::vector<uint8_t> key = owner_key(nodes, healthy, max_replica);
+    std::lock_guard<std::mutex> g(D->owners_mu);
+    if (!D->owners) D->owners = new OwnerTables();
+    OwnerTables& C = *D->owners;
+    for (size_t i = 0; i < C.e.size(); ++i)
+        if (C.e[i].key == key) {
+            KRK_HIP(hipStreamWaitEvent(s, C.e[i].ready, 0));
+            C.e[i].stamp = ++C.clock;
+            *d_tl = C.e[i].tl;
+            *d_tc = C.e[i].tc;
+            *slot = i;
+            return KRK_OK;
+        }
+    size_t i = C.e.size();
+    if (i >= kOwnerTables) {  // the least recently used one goes
+        i = 0;
+        for (size_t j = 1; j < C.e.size(); ++j)
+            if (C.e[j].stamp < C.e[i].stamp) i = j;
+        owner_release(D, C.e[i], s);
+    } else {
+        C.e.emplace_back();
+    }
+    OwnerTable& t = C.e[i];
+    int r = shard_owner_table(D, nodes, healthy, max_replica, row_out, &t.tl, &t.tc, s);
+    if (!r && (hipEventCreateWithFlags(&t.ready, hipEventDisableTiming) != hipSuccess ||
+               hipEventRecord(t.ready, s) != hipSuccess)) {
+        set_error(KRK_EHIP, "ring owner table: event");
+        r = KRK_EHIP;
+    }
+    if (r) {
+        owner_release(D, t, s);
+        C.e.erase(C.e.begin() + (long)i);
+        return r;
+    }
+    t.key = std::move(key);
+    t.stamp = ++C.clock;
+    *d_tl = t.tl;
+    *d_tc = t.tc;
+    *slot = i;
+    return KRK_OK;
+}
+
+void krk::owner_tables_teardown(Device& D) {
+    if (!D.owners) return;
+    for (OwnerTable& t : D.owners->e) owner_release(&D, t, D.s_main);
+    hipStreamSynchronize(D.s_main);
+    delete D.owners;
+    D.owners = nullptr;
+}
+
+static void owner_used(Device* D, size_t slot, hipStream_t s) {
+    std::lock_guard<std::mutex> g(D->owners_mu);
+    OwnerTable& t = D->owners->e[slot];
+    for (auto& u : t.used)
+        if (u.first == s) {
+            hipEventRecord(u.second, s);
+            return;
+        }
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, s) == hipSuccess)
+        t.used.push_back({s, ev});
+    else if (ev) {
+        hipEventDestroy(ev);
+        hipStreamSynchronize(s);  // no event to order the release behind: the use is done now
+    }
+}
+
 template <typename T>
 static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
                               const uint8_t* healthy, int32_t max_replica, T* locs_dev, uint8_t* counts_dev,
@@ -1362,7 +1485,8 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
     const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
     int32_t* d_tl = nullptr;
     uint8_t* d_tc = nullptr;
-    int r = shard_owner_table(D, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, s);
+    size_t slot = 0;
+    int r = owner_table(D, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, &slot, s);
     if (!r) {
         hipError_t e = timed(K_GATHER, s, [&] {
             if constexpr (sizeof(T) == 1)
@@ -1370,10 +1494,9 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
             else
                 return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
         });
+        owner_used(D, slot, s);
         if (e != hipSuccess) { set_error(KRK_EHIP, "gather launch: %s", launch_error_text(e)); r = KRK_EHIP; }
     }
-    if (d_tl) scratch_free(D, d_tl, s);
-    if (d_tc) scratch_free(D, d_tc, s);
     return r;
 }
 

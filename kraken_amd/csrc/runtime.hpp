@@ -265,6 +265,7 @@ struct Pipeline;
 struct Engine;
 struct OffloadPool;
 
+struct OwnerTables;  // runtime.cpp
 struct Device {
     // Submission engine (engine.cpp): the batching queues of the streaming
     // Digester / piece-stream / crc32.Update calls, created on first use.
@@ -287,6 +288,10 @@ struct Device {
     uint8_t* shard_bad = nullptr;
     std::once_flag shard_once;
     int shard_rc = 0;
+    // ring.Locations owner tables by membership (runtime.cpp OwnerTables): the reference's
+    // Ring rebuilds its hrw only on Refresh (lib/hashring/ring.go:141-165).
+    OwnerTables* owners = nullptr;
+    std::mutex owners_mu;
     int id = 0;
     int cus = 0;
     hipStream_t s_main = nullptr, s_a = nullptr, s_b = nullptr;

@@ -128,6 +128,43 @@ def test_ring_locations_dev_full_table(gpu, orc):
     assert ring.Locations(d) == [labels[j] for j in locs[0, : counts[0]]]
 
 
+def test_ring_owner_tables_cached_by_membership(gpu, orc):
+    """Owner tables are kept per membership (ring.Refresh semantics, lib/hashring/ring.go:
+    141-165): twelve memberships (more than the eight a device keeps) visited twice in
+    interleaved order -- hits, misses and evictions -- every result against the oracle,
+    including a health flip that keeps the labels and a relabelled node."""
+    rng = np.random.default_rng(0x0C5)
+    n = 4096
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    rings = []
+    for k in range(12):
+        N = [3, 5, 16, 64][k % 4]
+        labels = [f"origin-{i:03d}.kraken.test:{15002 + (k // 4)}" for i in range(N)]
+        healthy = (rng.random(N) < 0.75).astype(np.uint8)
+        rings.append((labels, healthy, 2 + k % 2))
+    labels, healthy, R = rings[0]
+    flipped = healthy.copy()
+    flipped[0] ^= 1
+    rings.append((labels, flipped, R))  # same labels, other health: its own table
+    rings.append((labels[:-1] + ["origin-zzz.kraken.test:15002"], healthy, R))
+    lbuf = D.DeviceBuffer(n * 3)
+    cbuf = D.DeviceBuffer(n)
+    picks = list(range(0, n, 97))
+    for rep in range(2):
+        for labels, healthy, R in (rings if rep == 0 else rings[::-1]):
+            D.ring_locations_u8_dev(dbuf, n, labels, healthy, R, lbuf, cbuf)
+            D.synchronize()
+            locs = lbuf.to_host(np.uint8, n * R).reshape(n, R)
+            counts = cbuf.to_host(np.uint8, n)
+            N = len(labels)
+            for i in picks:
+                key = bytes(digests[i, :2]).hex()
+                want = orc.ring_locations(orc.hrw_ordered(key, labels, [100] * N), healthy, R)
+                assert locs[i, : counts[i]].tolist() == want, (rep, N, R, i)
+
+
 def test_cas_volume_placement(gpu, orc, tmp_path):
     """lib/store/ca_store.go:137-171: weighted HRW over volumes for subdirs "%02X"."""
     from kraken_amd import castore
