@@ -54,6 +54,8 @@ for step in "$@"; do
                   -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
     prof_files) run prof_files 600 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_files -- python3 bench.py --workload files --steps 1 --warmup 1 --cold-gib 0 --no-cpu-baseline ;;
+    prof_tail) run prof_tail 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+                  -d gpurun_out/prof_tail -- python3 bench.py --no-e2e --no-cpu-baseline ;;
     prof_e2e) run prof_e2e 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
                   -d gpurun_out/prof_e2e -- python3 bench.py --e2e-only --no-cpu-baseline ;;
     prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --stats --output-format csv \
