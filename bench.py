@@ -1755,9 +1755,9 @@ def files_cold_leg(a, D, T, rank, world, P):
     page cache.  >= a.cold_gib GiB of DISTINCT files (the C3 length law / 64, every file its
     own synthetic content), fsync'ed, and the page cache dropped for every file before every
     pass (posix_fadvise DONTNEED; the resident share measured by mincore).  Passes: the
-    library's GPU-only path (offload off), its default (AUTO offload), O_DIRECT reads
-    (KRK_FILE_DIRECT=1), fewer live files (KRK_LIVE_CAP=2048), the per-file readahead off and at
-    8 MiB (KRK_FILE_READAHEAD_MB), plain reads of the files on 16 threads (the disk roofline), and the
+    library's GPU-only path (offload off) and its default (AUTO offload) -- both read a cold
+    batch O_DIRECT through Linux AIO by default -- the page-cache reads (KRK_FILE_DIRECT=0),
+    O_DIRECT by synchronous preads (KRK_FILE_AIO=0), fewer live files (KRK_LIVE_CAP=2048), plain reads of the files on 16 threads (the disk roofline), and the
     reference's two reads on the CPU (origin/blobserver/uploader.go:74-94 digest, then
     lib/metainfogen/generator.go:41-58 piece sums): per file back to back (the second read
     from the page cache the first filled, as on an origin with memory to spare) and the two
@@ -1818,40 +1818,41 @@ def files_cold_leg(a, D, T, rank, world, P):
         D.set_sha_host_offload(0)
         s_g, d_g = leg("gpu_only", lambda: D.metainfo_digest_files(paths, lens, P))
         legs["gpu_only"].update({k: v for k, v in D.windows_last_call().items()
-                                 if k in ("windows", "max_live", "phases_s")})
+                                 if k in ("windows", "max_live", "phases_s", "resident_sample", "direct_reads")})
         D.set_sha_host_offload(-1)
         try:
             s_a, d_a = leg("default", lambda: D.metainfo_digest_files(paths, lens, P))
             wl = D.windows_last_call()
-            legs["default"].update({"host_blobs": wl["host_blobs"], "resident_sample": wl["resident_sample"]})
+            legs["default"].update({"host_blobs": wl["host_blobs"], "resident_sample": wl["resident_sample"],
+                                    "direct_reads": wl["direct_reads"]})
         finally:
             D.set_sha_host_offload(0)
-        os.environ["KRK_FILE_DIRECT"] = "1"
+        # the reads' forms: page cache (the default when cached), O_DIRECT by synchronous
+        # preads (the round-4 O_DIRECT path); the default for a cold batch is O_DIRECT through
+        # Linux AIO (gpu_only / default above)
+        os.environ["KRK_FILE_DIRECT"] = "0"
         try:
-            s_d, d_d = leg("o_direct", lambda: D.metainfo_digest_files(paths, lens, P))
+            s_d, d_d = leg("page_cache", lambda: D.metainfo_digest_files(paths, lens, P))
         finally:
             os.environ.pop("KRK_FILE_DIRECT", None)
-        # fewer live files: bigger reads per file per window (512 MiB / live), same GPU path
-        os.environ["KRK_LIVE_CAP"] = "2048"
+        os.environ["KRK_FILE_DIRECT"], os.environ["KRK_FILE_AIO"] = "1", "0"
+        try:
+            s_s, d_s = leg("o_direct_sync_preads", lambda: D.metainfo_digest_files(paths, lens, P))
+        finally:
+            os.environ.pop("KRK_FILE_DIRECT", None)
+            os.environ.pop("KRK_FILE_AIO", None)
+        # fewer live files: bigger reads per file per window (512 MiB / live), page cache
+        os.environ["KRK_LIVE_CAP"], os.environ["KRK_FILE_DIRECT"] = "2048", "0"
         try:
             s_l, d_l = leg("gpu_only_live2048", lambda: D.metainfo_digest_files(paths, lens, P))
             legs["gpu_only_live2048"]["max_live"] = D.windows_last_call()["max_live"]
         finally:
             os.environ.pop("KRK_LIVE_CAP", None)
-        # the per-file readahead (staging.hpp par_read; default off): 2 and 8 MiB ahead
-        ra_out = []
-        for mb in (2, 8):
-            os.environ["KRK_FILE_READAHEAD_MB"] = str(mb)
-            try:
-                ra_out.append(leg(f"gpu_only_readahead{mb}", lambda: D.metainfo_digest_files(paths, lens, P)))
-                legs[f"gpu_only_readahead{mb}"]["phases_s"] = D.windows_last_call()["phases_s"]
-            finally:
-                os.environ.pop("KRK_FILE_READAHEAD_MB", None)
+            os.environ.pop("KRK_FILE_DIRECT", None)
         rate, got = leg("disk_read", lambda: disk_read_rate(paths))
         legs["disk_read"]["what"] = "plain 8 MiB reads of every file on 16 threads, no compute (the disk roofline)"
-        (s_n, d_n), (s_8, d_8) = ra_out
-        same = all(np.array_equal(d_g, y) for y in (d_a, d_d, d_l, d_n, d_8)) and all(
-            all(np.array_equal(x, y) for y in ys) for x, *ys in zip(s_g, s_a, s_d, s_l, s_n, s_8))
+        same = all(np.array_equal(d_g, y) for y in (d_a, d_d, d_l, d_s)) and all(
+            all(np.array_equal(x, y) for y in ys) for x, *ys in zip(s_g, s_a, s_d, s_l, s_s))
         from oracle import oracle as O  # checker and CPU baseline only
         O.build()
         import hashlib

@@ -83,10 +83,11 @@ int krk_sha_tail_plan(const uint64_t* lengths, uint64_t n, int threads, uint32_t
                       uint64_t* n_out, double* end_s, double* gpu_s);
 /* ... and its window loop's wall seconds, split into waiting for a free staging window,
  * filling windows (staging copies or file reads) and enqueueing copies and kernels; for a
- * krk_metainfo_digest_files call under AUTO offload, the page-cache resident share of its
- * sampled files (below 0.5 the batch is treated as disk-bound: no host offload), else -1. */
+ * krk_metainfo_digest_files call, the page-cache resident share of its sampled files (below
+ * 0.5 the batch is disk-bound: no host offload under AUTO, O_DIRECT reads unless
+ * KRK_FILE_DIRECT says otherwise), else -1; and whether it read with O_DIRECT. */
 int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s,
-                            double* resident);
+                            double* resident, int* direct_reads);
 /* The gather of host-buffer calls, process-wide: -1 AUTO (the default: page-locked blobs
  * gathered in wide windows, pageable ones staged -- measured faster), 0 off
  * (stage every window through the pinned host windows), 1 on (pageable blobs registered for

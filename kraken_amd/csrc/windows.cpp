@@ -140,6 +140,7 @@ struct FileFiller : Filler {
     std::vector<int> fd;
     std::vector<char> is_direct;
     std::unique_ptr<std::atomic<uint64_t>[]> ra;  // each file's readahead mark (par_read)
+    AioReader aio;                                  // the O_DIRECT chunks of a window
     FileFiller(const krk_file_blob* f, uint64_t n, bool want_direct)
         : files(f), direct(want_direct), fd(n, -1), is_direct(n, 0), ra(new std::atomic<uint64_t>[n]()) {}
     ~FileFiller() override {
@@ -173,7 +174,8 @@ struct FileFiller : Filler {
             const auto& rt = pass ? odirect : plain;
             if (rt.empty()) continue;
             int e = 0;
-            const long bad = par_read(rt, pass == 1, &e);
+            long bad = pass == 1 && use_aio() ? aio.read(rt, &e) : -2;
+            if (bad == -2) bad = par_read(rt, pass == 1, &e);
             if (bad >= 0) {
                 const char* path = files[rt[bad].blob].path;
                 if (e) set_error(KRK_EIO, "read blob: %s: %s", path, strerror(e));
@@ -263,6 +265,7 @@ struct CallStats {
     // windows from the source (fill: staging copies or file reads), enqueueing copies + kernels
     double loop_s = 0, acquire_s = 0, fill_s = 0, enqueue_s = 0;
     double resident = -1;  // file batches: the page-cache resident share of the sampled files
+    bool direct_reads = false;  // file batches: read with O_DIRECT
 };
 thread_local CallStats t_last_call;
 
@@ -280,6 +283,7 @@ int windows_pass(Device* D, uint64_t n, const uint64_t* lens, const int64_t* ple
     st->max_live = 0;
     st->windows = st->direct_windows = st->gather_windows = 0;
     st->loop_s = st->acquire_s = st->fill_s = st->enqueue_s = 0;
+    st->direct_reads = false;
     if (blobs.empty()) return KRK_OK;
     const size_t W = window_bytes();
     const uint64_t live_cap = std::min<uint64_t>(cap, blobs.size());
@@ -819,15 +823,17 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     KRK_CHECK(hi == lo || sums_host, KRK_EINVAL, "sums_host is NULL");
     // Host offload (AUTO by default): the planner's files are read, hashed and piece-summed
     // by host threads in one pass each and never cross the host link.
-    // Under AUTO, a batch mostly out of the page cache is bound by the disk, wherever its bytes
-    // are hashed: host threads would read the same disk and take CPU from the window readers
-    // (cold 32 GiB leg: AUTO 13.4 GB/s against 14.8 GPU-only, profiles/r05/bench_files.json),
-    // so such a batch stays on the windows.
+    // A batch mostly out of the page cache (the residency sample) is bound by the disk,
+    // wherever its bytes are hashed: under AUTO, host threads would read the same disk and
+    // take CPU from the window readers (cold 32 GiB leg: AUTO 13.4 GB/s against 14.8
+    // GPU-only, profiles/r05/bench_files.json), so such a batch stays on the windows -- and
+    // is read with O_DIRECT (below).
     std::vector<char> on_host(n, 0);
     std::vector<uint32_t> host;
     int off_t = offload_threads(kOffHostWhole);
-    const double resident = off_t > 0 && offload_auto() ? files_resident_fraction(files, n) : -1.0;
-    if (resident >= 0 && resident < 0.5) off_t = 0;
+    const double resident = files_resident_fraction(files, n);
+    const bool cold = resident >= 0 && resident < 0.5;
+    if (cold && offload_auto()) off_t = 0;
     if (off_t > 0) {
         host = offload_plan(lens.data(), n, off_t, planner_rates(D), nullptr, nullptr, kOffHostFiles);
         for (uint32_t i : host) on_host[i] = 1;
@@ -868,7 +874,13 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
         ~ShareGuard() { t_host_share = saved; }
     } share_guard{t_host_share};
     if (!host.empty()) t_host_share = std::max(4, host_threads_for_call() - off_t);
-    const bool direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
+    // O_DIRECT reads (Linux AIO, a window's chunks queued at once): KRK_FILE_DIRECT=1 / 0
+    // force them on / off; by default a cold batch takes them (no page-cache copy, a deep
+    // disk queue from one thread: 16.3 GB/s against 11.7 for 16 threads' page-cache preads
+    // of the same window chunks, profiles/r05/disk_probe_aio.jsonl) and a cached one reads
+    // the page cache.
+    const char* fd_env = getenv("KRK_FILE_DIRECT");
+    const bool direct = fd_env ? atoi(fd_env) > 0 : cold;
     FileFiller filler(files, n, direct);
     CallStats st;
     // at most as many live blobs as this call holds file descriptors (a lease of the
@@ -877,6 +889,7 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, fds.n,
                      o.d_sums, o.d_dig, o.d_state, &st);
     st.resident = resident;
+    st.direct_reads = direct;
     // drain what was queued even after a read error (the windows' kernels read the buffers)
     const bool synced = hipStreamSynchronize(D->s_a) == hipSuccess && hipStreamSynchronize(D->s_b) == hipSuccess &&
                         hipStreamSynchronize(D->s_main) == hipSuccess;
@@ -934,8 +947,9 @@ int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, dou
 }
 
 int krk_windows_last_phases(double* loop_s, double* acquire_s, double* fill_s, double* enqueue_s,
-                            double* resident) {
+                            double* resident, int* direct_reads) {
     if (resident) *resident = t_last_call.resident;
+    if (direct_reads) *direct_reads = t_last_call.direct_reads ? 1 : 0;
     if (loop_s) *loop_s = t_last_call.loop_s;
     if (acquire_s) *acquire_s = t_last_call.acquire_s;
     if (fill_s) *fill_s = t_last_call.fill_s;

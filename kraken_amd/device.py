@@ -446,11 +446,12 @@ def windows_last_call() -> dict:
     check(lib.krk_windows_last_direct(C.byref(d)))
     check(lib.krk_windows_last_gather(C.byref(g), C.byref(rb), C.byref(rs)))
     ph = [C.c_double() for _ in range(5)]
-    check(lib.krk_windows_last_phases(*[C.byref(x) for x in ph]))
+    dr = C.c_int()
+    check(lib.krk_windows_last_phases(*[C.byref(x) for x in ph], C.byref(dr)))
     return {"max_live": m.value, "windows": w.value, "host_blobs": h.value, "direct_windows": d.value,
             "gather_windows": g.value, "registered_bytes": rb.value, "register_s": rs.value,
             "phases_s": dict(zip(("loop", "acquire", "fill", "enqueue"), (round(x.value, 4) for x in ph[:4]))),
-            "resident_sample": round(ph[4].value, 4)}
+            "resident_sample": round(ph[4].value, 4), "direct_reads": bool(dr.value)}
 
 
 def set_host_gather(mode: int):

@@ -38,13 +38,16 @@ def _write(tmp_path, name, data):
 
 
 @pytest.mark.parametrize("P", [1 << 20, 3, 4 << 20])
-@pytest.mark.parametrize("mode", ["gpu", "offload", "cap3"])
+@pytest.mark.parametrize("mode", ["gpu", "offload", "cap3", "direct_aio", "direct_sync"])
 def test_files_edge_lengths_match_oracle(gpu, orc, tmp_path, P, mode, monkeypatch):
     lens = EDGE if P != 3 else [0, 1, 2, 3, 4, 64, 65, 100_001]
     datas = [orc.synth(50 + i, L) for i, L in enumerate(lens)]
     paths = [_write(tmp_path, f"b{i}", d) for i, d in enumerate(datas)]
     if mode == "cap3":
         monkeypatch.setenv("KRK_LIVE_CAP", "3")
+    if mode.startswith("direct"):  # O_DIRECT chunks: Linux AIO (the cold default) or preads
+        monkeypatch.setenv("KRK_FILE_DIRECT", "1")
+        monkeypatch.setenv("KRK_FILE_AIO", "1" if mode == "direct_aio" else "0")
     if mode == "offload":
         D.set_sha_host_offload(8)
         D.set_planner_rates(dict(D.planner_rates(), sha_stream_bps=[1e6, 1e6, 1e6]))  # the host takes files
@@ -61,12 +64,15 @@ def test_files_edge_lengths_match_oracle(gpu, orc, tmp_path, P, mode, monkeypatc
         assert st["host_blobs"] > 0
     if mode == "cap3":
         assert st["max_live"] == 3 and st["windows"] >= len(lens) // 3
+    if mode.startswith("direct"):
+        assert st["direct_reads"], st
 
 
 def test_files_cold_batch_stays_on_windows_under_auto(gpu, orc, tmp_path):
-    """AUTO offload samples the batch's page-cache residency (mmap + mincore): files out of the
-    cache are disk-bound wherever they are hashed, so none go to host threads; the same files
-    cached do (with rates that make the host worth it).  Outputs equal the oracle both ways."""
+    """The batch's page-cache residency is sampled (mmap + mincore): files out of the cache are
+    disk-bound wherever they are hashed, so AUTO sends none to host threads and reads them
+    O_DIRECT through Linux AIO; the same files cached go to host threads (with rates that make
+    the host worth it) and are read from the page cache.  Outputs equal the oracle both ways."""
     lens = [4 << 20] * 6 + [3 << 20, 1]
     datas = [orc.synth(700 + i, L) for i, L in enumerate(lens)]
     paths = [_write(tmp_path, f"c{i}", d) for i, d in enumerate(datas)]
@@ -95,7 +101,8 @@ def test_files_cold_batch_stays_on_windows_under_auto(gpu, orc, tmp_path):
         D.set_sha_host_offload(0)
         D.set_planner_rates(None)
     assert 0 <= cold["resident_sample"] < 0.5 and cold["host_blobs"] == 0, cold
-    assert warm["resident_sample"] >= 0.5 and warm["host_blobs"] > 0, warm
+    assert cold["direct_reads"], cold  # a cold batch reads O_DIRECT (Linux AIO)
+    assert warm["resident_sample"] >= 0.5 and warm["host_blobs"] > 0 and not warm["direct_reads"], warm
     for i, d in enumerate(datas):
         want = hashlib.sha256(d.tobytes()).digest()
         assert bytes(dg_c[i]) == want and bytes(dg_w[i]) == want, i
