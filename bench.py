@@ -1813,12 +1813,16 @@ def files_cold_leg(a, D, T, rank, world, P):
             el = T.max_over_ranks(time.perf_counter() - t0)
             legs[name] = {"GBps": round(world * tot / el / 1e9, 3), "seconds": round(el, 3),
                           "resident_before": round(cold, 4)}
+            if name != "disk_read":  # the window loop's split: fill = the reads
+                wl = D.windows_last_call()
+                legs[name].update({"phases_s": wl["phases_s"], "direct_reads": wl["direct_reads"],
+                                   "fill_GBps": round(tot / max(wl["phases_s"]["fill"], 1e-9) / 1e9, 3)})
             return out
 
         D.set_sha_host_offload(0)
         s_g, d_g = leg("gpu_only", lambda: D.metainfo_digest_files(paths, lens, P))
         legs["gpu_only"].update({k: v for k, v in D.windows_last_call().items()
-                                 if k in ("windows", "max_live", "phases_s", "resident_sample", "direct_reads")})
+                                 if k in ("windows", "max_live", "resident_sample")})
         D.set_sha_host_offload(-1)
         try:
             s_a, d_a = leg("default", lambda: D.metainfo_digest_files(paths, lens, P))
@@ -1854,7 +1858,6 @@ def files_cold_leg(a, D, T, rank, world, P):
         # boxes): the order effect beside the paths' differences
         D.set_sha_host_offload(0)
         s_r, d_r = leg("gpu_only_again", lambda: D.metainfo_digest_files(paths, lens, P))
-        legs["gpu_only_again"]["direct_reads"] = D.windows_last_call()["direct_reads"]
         legs["disk_read"]["what"] = "plain 8 MiB reads of every file on 16 threads, no compute (the disk roofline)"
         same = all(np.array_equal(d_g, y) for y in (d_a, d_d, d_l, d_s, d_r)) and all(
             all(np.array_equal(x, y) for y in ys) for x, *ys in zip(s_g, s_a, s_d, s_l, s_s, s_r))

@@ -213,7 +213,11 @@ inline int lease_staging(Device* D, size_t cap, StagingLease& L) {
             delete D->staging;  // its destructor drains the old windows' events
             D->staging = nullptr;
             auto p = std::make_unique<Pipeline>();
-            int r = p->init(cap);
+            // kept windows grow in 32 MiB steps with 32 MiB of headroom: a batch whose chunk
+            // placement pads a little more (O_DIRECT's 4 KiB places: 512 MiB + 4 KiB x live)
+            // must not re-pin three windows (~0.6 s) after one that padded less
+            constexpr size_t kStep = size_t(32) << 20;
+            int r = p->init(std::min(kKeepMax, (cap + kStep - 1) / kStep * kStep + kStep));
             if (r) return r;
             D->staging = p.release();
         }
