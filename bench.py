@@ -1808,11 +1808,12 @@ def files_cold_leg(a, D, T, rank, world, P):
             drop_cache(paths)
             cold = resident_fraction(paths[::max(1, n // 64)])
             T.barrier()
-            t0 = time.perf_counter()
+            c0, t0 = cpu_seconds(), time.perf_counter()
             out = fn()
             el = T.max_over_ranks(time.perf_counter() - t0)
+            cpu = cpu_seconds() - c0
             legs[name] = {"GBps": round(world * tot / el / 1e9, 3), "seconds": round(el, 3),
-                          "resident_before": round(cold, 4)}
+                          "resident_before": round(cold, 4), "host_cpu_s_per_GB": round(cpu / (tot / 1e9), 4)}
             if name != "disk_read":  # the window loop's split: fill = the reads
                 wl = D.windows_last_call()
                 legs[name].update({"phases_s": wl["phases_s"], "direct_reads": wl["direct_reads"],
