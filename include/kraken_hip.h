@@ -292,16 +292,17 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* 
  * (origin/blobserver/uploader.go:74-94) or the cache-fill digest of CAStore.WriteCacheFile
  * (lib/store/ca_store.go:99-135) fused with the metainfo Generator.Generate computes from the
  * cache file (lib/metainfogen/generator.go:41-58): each file is read ONCE (pread on the host
- * pool into the pinned windows; O_DIRECT with KRK_FILE_DIRECT=1) and that read feeds both
+ * pool into the pinned windows; O_DIRECT for a cold batch, below) and that read feeds both
  * the SHA-256 digest and the piece CRCs -- the reference reads it twice.  files[i].length is
  * the size the caller stat-ed; a shorter file is KRK_EIO "read blob: <path>: unexpected EOF",
  * an unopenable one KRK_EIO "open <path>: <errno text>".  Live blobs per window are also
  * capped by the file descriptors the process may still open (RLIMIT_NOFILE).  With the host
  * offload (KRK_OFFLOAD_AUTO) the planner's files are read, hashed and piece-summed on host
  * threads in one pass each -- unless a sample of the files (mmap + mincore, no reads) finds
- * them mostly outside the page cache: a disk-bound batch stays on the windows.
- * KRK_FILE_READAHEAD_MB=N keeps each file hinted N MiB ahead of its reads
- * (POSIX_FADV_WILLNEED; off by default).  Synchronous. */
+ * them mostly outside the page cache: a disk-bound batch stays on the windows and is read
+ * O_DIRECT through Linux AIO (one thread queues a window's chunks; KRK_FILE_DIRECT=1/0
+ * forces O_DIRECT on/off).  KRK_FILE_READAHEAD_MB=N keeps each file hinted N MiB ahead of
+ * its page-cache reads (POSIX_FADV_WILLNEED; off by default).  Synchronous. */
 int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n_files, uint32_t* sums_host,
                               uint8_t* digests_host);
 
