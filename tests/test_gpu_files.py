@@ -110,7 +110,11 @@ def test_files_cold_batch_stays_on_windows_under_auto(gpu, orc, tmp_path):
         assert np.array_equal(sums_c[i], ref) and np.array_equal(sums_w[i], ref), i
 
 
-def test_files_errors_keep_reference_texts(gpu, orc, tmp_path):
+@pytest.mark.parametrize("mode", ["default", "direct_aio", "direct_sync"])
+def test_files_errors_keep_reference_texts(gpu, orc, tmp_path, mode, monkeypatch):
+    if mode != "default":  # the same texts from the O_DIRECT reads (Linux AIO or preads)
+        monkeypatch.setenv("KRK_FILE_DIRECT", "1")
+        monkeypatch.setenv("KRK_FILE_AIO", "1" if mode == "direct_aio" else "0")
     d = orc.synth(1, 1 << 20)
     p = _write(tmp_path, "short", d)
     with pytest.raises(KrakenError) as e:
