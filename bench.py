@@ -1193,7 +1193,14 @@ def run_pieces(a, D, T, rank, world, res):
         s, off = sums
         cnt = int(off[1] - off[0])
         cb["outputs_match_gpu"] = bool(np.array_equal(s[:cnt], sums_h[:cnt]))
-        cb["sample"] += " (sample blobs: 256 MiB prefixes of the same synthetic blob)"
+        cb["sample"] += (" (sample blobs: 256 MiB prefixes of the same synthetic blob, one a thread: C4's "
+                         "ONE blob would be one goroutine in the reference, see one_goroutine)")
+        # the reference's calcPieceSums over C4's single blob runs on one goroutine
+        # (core/metainfo.go:157-179): one thread over one 256 MiB prefix
+        c1, _, _ = cpu_baseline_metainfo([256 << 20], [ids[0]], P, min(a.cpu_seconds, 3.0), passes=2)
+        cb["one_goroutine"] = {"value": c1["value"], "unit": "GB/s", "cores": 1,
+                               "what": "the reference's calcPieceSums over the one C4 blob: a single "
+                                       "goroutine (one thread, 256 MiB sample)"}
         res["cpu_baseline"] = cb
 
 
