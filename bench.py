@@ -698,6 +698,8 @@ def run_verify(a, D, T, rank, world, res):
                           "what": "the last step's bytes on the GPU (DMA from the pinned pieces) and on host PCLMUL "
                                   "threads; the share is learned from the measured rates of both sides"},
                 "verdicts_match": bool(np.array_equal(got[0], want))})
+    if world == 1 and not a.no_cpu_baseline:
+        res["same_buffer"] = same_buffer_ab(step, [host.ctypes.data + i * P for i in range(n)], [P] * n, expected)
     # the same pieces from pageable memory
     pg = np.empty(n * P, dtype=np.uint8)
     pg[:] = host
@@ -809,7 +811,33 @@ def host_crc_ceiling(D):
             "source": "krk_planner_rates_get (measured on this box at krk_init)"}
 
 
-def c4_end_to_end(D, T, arena, want_sums, P, world):
+def same_buffer_ab(lib_pass, ptrs, lens, want, rounds=3):
+    """The library's host pass and the oracle's per-piece CRC (orc_crc_bufs: the reference's
+    crc32 per piece, every host core taking pieces in turn) over the SAME host bytes,
+    alternated `rounds` times: host-memory bandwidth on these boxes moves by 2x between
+    minutes (placement, the host's other tenants), so a baseline timed on its own sample at
+    another moment is no like-for-like.  Medians; the oracle's sums are checked against
+    `want`."""
+    from oracle import oracle as O  # the CPU baseline leg (test infrastructure)
+    O.build()
+    total = float(sum(int(x) for x in lens))
+    lib_t, orc_t, ok = [], [], True
+    for _ in range(rounds):
+        t0 = time.perf_counter()
+        lib_pass()
+        lib_t.append(time.perf_counter() - t0)
+        t, sums = O.crc_bufs(ptrs, lens, node_cores())
+        orc_t.append(t)
+        ok = ok and bool(np.array_equal(sums, want))
+    med = lambda v: sorted(v)[len(v) // 2]
+    return {"library_GBps": round(total / med(lib_t) / 1e9, 3), "oracle_GBps": round(total / med(orc_t) / 1e9, 3),
+            "library_s": [round(x, 4) for x in lib_t], "oracle_s": [round(x, 4) for x in orc_t],
+            "oracle_threads": node_cores(), "oracle_sums_match": ok,
+            "what": "library pass and oracle pass (crc32 per piece on every host core, oracle/oracle.c orc_crc_bufs) "
+                    f"alternated {rounds}x over the same host buffer; medians"}
+
+
+def c4_end_to_end(D, T, arena, want_sums, P, world, ab=False):
     """C4's blob in HOST memory (VERDICT r03 missing #2): krk_piece_sums_host over the 20 GiB
     blob in a pinned receive buffer (the library splits whole pieces between host PCLMUL
     threads and DMA into the GPU by the measured rates) and in pageable memory (host
@@ -837,6 +865,12 @@ def c4_end_to_end(D, T, arena, want_sums, P, world):
         res[name] = {"value": round(world * Le / el / 1e9, 3), "seconds": round(el, 3),
                      "passes_s": [round(x, 3) for x in ts], "gpu_bytes": g, "host_bytes": h,
                      "sums_match_device_run": bool(np.array_equal(r[0][:k], want_sums[:k]))}
+    if ab:  # rank 0 at N=1: the reference's per-piece CRC over the same pinned bytes, alternated
+        base = pin.a.ctypes.data
+        res["pinned"]["same_buffer"] = same_buffer_ab(lambda: D.piece_sums_host([pin.a], P),
+                                                      [base + i * P for i in range(k)], [P] * k, want_sums[:k])
+        res["pinned"]["same_buffer"]["what"] += (" (generous to the reference: its calcPieceSums is one goroutine "
+                                                 "per blob, cpu_baseline.one_goroutine)")
     res["value"] = res["pinned"]["value"]
     res["what"] = ("the blob in host memory through krk_piece_sums_host (agent verify / Generate over a host "
                    "buffer): `pinned` = a krk_host_alloc receive buffer (host threads + GPU DMA by the measured "
@@ -1186,7 +1220,7 @@ def run_pieces(a, D, T, rank, world, res):
     core._info_hash(P, sums_h[:arena.total_pieces], "0" * 64, lens[0])
     res["info_hash_host_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
     if a.workload == "c4" and not a.no_e2e:
-        res["end_to_end"] = c4_end_to_end(D, T, arena, sums_h, P, world)
+        res["end_to_end"] = c4_end_to_end(D, T, arena, sums_h, P, world, ab=world == 1 and not a.no_cpu_baseline)
     if rank == 0 and not a.no_cpu_baseline:
         m = 2 * node_cores()
         cb, _, sums = cpu_baseline_metainfo([256 << 20] * m, [ids[0]] * m, P, a.cpu_seconds, passes=2)

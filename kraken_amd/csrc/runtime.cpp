@@ -6,6 +6,7 @@
 #include <stdarg.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
+#include <optional>
 #include <unistd.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -615,6 +616,140 @@ struct PieceTask {
     uint64_t out;
 };
 
+// NUMA-aware hand-out of host CRC tasks (runs of ~8 MiB), opt-in: the node of each task's
+// first, middle and last page (move_pages, one call for all of them) and, per claim, the
+// node of the CPU the claiming thread runs on; a thread takes the next task of its own node
+// and steals from the others once its node has none (KRK_CRC_NUMA=1), and with
+// KRK_CRC_NUMA=2, for a batch spread over both sockets' memory, a thread that takes another
+// node's task runs it on that node's CPUs (NodeVisit).  Off by default (0 = one plain
+// cursor): on the GPU boxes' two-socket hosts, four interleaved A/B runs of the three modes
+// (profiles/r05/host_mem_probe_numa.jsonl) moved the spread-buffer case by +33, +8, +14 and
+// -14 % with visits and left every one-node buffer equal or a few % lower -- inside the
+// host's minute-to-minute swing, not a win to ship.
+class NodeTasks {
+  public:
+    // sysfs's CPU lists per node, parsed once: node of each CPU and the CPUs of each node
+    struct Topology {
+        std::vector<int> node_of_cpu = std::vector<int>(CPU_SETSIZE, 0);
+        std::vector<cpu_set_t> cpus;
+        Topology() {
+            for (int nd = 0; nd < 64; ++nd) {
+                FILE* f = fopen(("/sys/devices/system/node/node" + std::to_string(nd) + "/cpulist").c_str(), "r");
+                if (!f) break;
+                char buf[4096] = {0};
+                const size_t got = fread(buf, 1, sizeof buf - 1, f);
+                fclose(f);
+                buf[got] = 0;
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                for (char* q = buf; *q && *q != '\n';) {  // "0-63,128-191"
+                    char* e = nullptr;
+                    const long lo = strtol(q, &e, 10);
+                    if (e == q) break;
+                    long hi = lo;
+                    if (*e == '-') hi = strtol(e + 1, &e, 10);
+                    for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c) {
+                        node_of_cpu[(size_t)c] = nd;
+                        CPU_SET((int)c, &set);
+                    }
+                    q = (*e == ',') ? e + 1 : e;
+                }
+                cpus.push_back(set);
+            }
+        }
+    };
+    static const Topology& topo() {
+        static const Topology t;
+        return t;
+    }
+    static int cpu_node(int cpu) { return cpu >= 0 && cpu < CPU_SETSIZE ? topo().node_of_cpu[(size_t)cpu] : 0; }
+    // the CPUs of node nd (nullptr when sysfs did not list it)
+    static const cpu_set_t* node_cpus(int nd) {
+        return nd >= 0 && (size_t)nd < topo().cpus.size() ? &topo().cpus[(size_t)nd] : nullptr;
+    }
+    // node visits (mode 2) only for a batch spread over nodes: two or more nodes holding at least
+    // an eighth of the tasks each.  A batch on one node keeps its threads spread over both
+    // sockets (moving all of them to the memory's socket measured 10 % slower).
+    bool visits() const {
+        if (mode_ < 2) return false;
+        std::vector<size_t> on(list_.size(), 0);
+        for (int nd : node_)
+            if (nd >= 0) ++on[(size_t)nd];
+        size_t big = 0;
+        for (size_t c : on) big += c * 8 >= node_.size();
+        return big >= 2;
+    }
+    int node_of(size_t task) const { return task < node_.size() ? node_[task] : -1; }
+    // tasks' first, middle and last pages -> per-node lists; a task whose three pages are
+    // not on one node (interleaved memory) is nobody's: it goes on its first page's list and
+    // is never visited.  False when there is one node or the query fails.
+    bool build(const std::vector<const void*>& first, const std::vector<const void*>& mid,
+               const std::vector<const void*>& last) {
+        const char* v = getenv("KRK_CRC_NUMA");
+        mode_ = v ? atoi(v) : 0;
+        const size_t n = first.size();
+        if (mode_ <= 0 || n < 2) return false;
+        std::vector<int> status(3 * n, -1);
+        std::vector<void*> pages(3 * n);
+        auto page = [](const void* q) { return reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(q) & ~uintptr_t(4095)); };
+        for (size_t i = 0; i < n; ++i) {
+            pages[3 * i] = page(first[i]);
+            pages[3 * i + 1] = page(mid[i]);
+            pages[3 * i + 2] = page(last[i]);
+        }
+        if (syscall(SYS_move_pages, 0, (unsigned long)pages.size(), pages.data(), nullptr, status.data(), 0) != 0)
+            return false;
+        int nodes = 0;
+        for (int st : status) nodes = std::max(nodes, st + 1);
+        if (nodes < 2) return false;
+        list_.assign((size_t)nodes, {});
+        node_.assign(n, -1);
+        for (size_t i = 0; i < n; ++i) {
+            const int a = status[3 * i], b = status[3 * i + 1], c = status[3 * i + 2];
+            if (a >= 0 && a == b && b == c) node_[i] = a;
+            list_[(size_t)std::max(0, a)].push_back(i);
+        }
+        next_ = std::vector<std::atomic<size_t>>(list_.size());
+        return true;
+    }
+    // the next task for a thread on the CPU it runs on now (SIZE_MAX: none left)
+    size_t claim() {
+        const int home = std::min<int>((int)list_.size() - 1, cpu_node(sched_getcpu()));
+        for (size_t k = 0; k < list_.size(); ++k) {
+            const size_t nd = ((size_t)home + k) % list_.size();
+            if (next_[nd].load(std::memory_order_relaxed) >= list_[nd].size()) continue;
+            const size_t i = next_[nd].fetch_add(1);
+            if (i < list_[nd].size()) return list_[nd][i];
+        }
+        return SIZE_MAX;
+    }
+
+  private:
+    int mode_ = 0;
+    std::vector<int> node_;
+    std::vector<std::vector<size_t>> list_;
+    std::vector<std::atomic<size_t>> next_;
+};
+
+// Mode 2 of KRK_CRC_NUMA (the default): a thread that takes a task of another node moves to
+// that node's CPUs for the task (within the CPUs it may use) and back afterwards.
+struct NodeVisit {
+    cpu_set_t old;
+    bool moved = false;
+    explicit NodeVisit(int nd) {
+        if (sched_getaffinity(0, sizeof old, &old) != 0) return;
+        const cpu_set_t* on = NodeTasks::node_cpus(nd);
+        if (!on) return;
+        cpu_set_t to;
+        CPU_AND(&to, &old, on);
+        if (CPU_COUNT(&to) == 0) return;
+        moved = sched_setaffinity(0, sizeof to, &to) == 0;
+    }
+    ~NodeVisit() {
+        if (moved) sched_setaffinity(0, sizeof old, &old);
+    }
+};
+
 // The pinned-batch split of each device, learned from earlier calls (per device).
 //  * frac: the balanced GPU share -- where both sides would have ended together at the
 //    rates the last split call measured (-1: none yet; first call: the rates' model, <= 10 %);
@@ -727,7 +862,27 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
                                   : std::max<size_t>(1, (size_t)(task_bytes / std::max(1.0, hbytes_all / host.size())));
     const size_t n_tasks = (host.size() + G - 1) / G;
     left.store(n_tasks);
+    NodeTasks nt;
+    bool numa = false;
+    if (n_tasks >= 2) {
+        std::vector<const void*> first(n_tasks), mid(n_tasks), last(n_tasks);
+        for (size_t t = 0; t < n_tasks; ++t) {
+            const size_t j0 = t * G, j1 = std::min(host.size(), (t + 1) * G) - 1;
+            first[t] = host[j0].p;
+            mid[t] = host[(j0 + j1) / 2].p + host[(j0 + j1) / 2].n / 2;
+            last[t] = host[j1].p + (host[j1].n ? host[j1].n - 1 : 0);
+        }
+        numa = nt.build(first, mid, last);
+    }
+    const bool visits = numa && nt.visits();
     HostBatch hb(n_tasks, gpu.empty() ? TH - 1 : TH, [&](size_t t) {
+        if (numa) {  // every call claims one task: n_tasks calls take them all
+            const size_t k = nt.claim();
+            if (k != SIZE_MAX) t = k;
+        }
+        std::optional<NodeVisit> visit;
+        if (visits && nt.node_of(t) >= 0 && nt.node_of(t) != NodeTasks::cpu_node(sched_getcpu()))
+            visit.emplace(nt.node_of(t));
         for (size_t j = t * G; j < std::min(host.size(), (t + 1) * G); ++j)
             sums_host[host[j].out] = host_crc32_update(0, host[j].p, host[j].n);
         if (left.fetch_sub(1) == 1)  // the last task: the host side's wall time

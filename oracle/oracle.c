@@ -733,6 +733,49 @@ double orc_baseline_run(const uint64_t* blob_idx, const uint64_t* lengths, uint6
     return t1 - t0;
 }
 
+/* The reference's per-piece check over buffers that already sit in memory (the agent's
+ * received pieces, agentstorage/torrent.go:174-199 writePiece: crc32 over the piece, compared
+ * with GetPieceSum) -- the bench's A/B leg that runs over the SAME host bytes the library
+ * verified, interleaved with it, so both see one memory placement and one box state.
+ * n_threads workers take the next piece in turn; 32 KiB PCLMUL chunks as baseline_run.
+ * Returns wall seconds. */
+typedef struct { const uint8_t* const* p; const uint64_t* len; uint64_t n, next; uint32_t* out; pthread_barrier_t bar; } bufs_job;
+static void* bufs_worker(void* a) {
+    bufs_job* J = (bufs_job*)a;
+    pthread_barrier_wait(&J->bar);
+    for (;;) {
+        uint64_t q = __atomic_fetch_add(&J->next, 1, __ATOMIC_RELAXED);
+        if (q >= J->n) break;
+        const uint64_t CH = 32768; /* io.Copy's 32 KiB buffer */
+        uint32_t crc = 0;
+        for (uint64_t o = 0; o < J->len[q]; o += CH) {
+            uint64_t m = J->len[q] - o < CH ? J->len[q] - o : CH;
+            crc = orc_crc32_update_clmul(crc, J->p[q] + o, m);
+        }
+        J->out[q] = crc;
+    }
+    pthread_barrier_wait(&J->bar);
+    return NULL;
+}
+
+double orc_crc_bufs(const uint8_t* const* ptrs, const uint64_t* lens, uint64_t n, int n_threads, uint32_t* out) {
+    if (n_threads < 1) n_threads = 1;
+    bufs_job J;
+    memset(&J, 0, sizeof J);
+    J.p = ptrs; J.len = lens; J.n = n; J.out = out;
+    pthread_barrier_init(&J.bar, NULL, (unsigned)n_threads + 1);
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)n_threads);
+    for (int i = 0; i < n_threads; i++) pthread_create(&th[i], NULL, bufs_worker, &J);
+    double t0 = now_s();
+    pthread_barrier_wait(&J.bar);
+    pthread_barrier_wait(&J.bar);
+    double t1 = now_s();
+    for (int i = 0; i < n_threads; i++) pthread_join(th[i], NULL);
+    pthread_barrier_destroy(&J.bar);
+    free(th);
+    return t1 - t0;
+}
+
 /* Bounded-memory form for samples too large to hold at once (C3's blobs are 100 MiB -
  * 1 GiB): each worker thread owns one buffer, takes the next blob, materialises it
  * (untimed) and times only its two passes.  Returns the summed busy seconds of all

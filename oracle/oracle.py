@@ -56,6 +56,7 @@ def _load() -> C.CDLL:
                                           C.c_uint64, u8p, u32p, u64p]),
         "orc_baseline_files": (C.c_double, [C.POINTER(C.c_char_p), u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
                                             u32p, u64p, u8p]),
+        "orc_crc_bufs": (C.c_double, [C.POINTER(C.c_void_p), u64p, C.c_uint64, C.c_int, u32p]),
         "orc_baseline_run_lazy": (C.c_double, [u64p, u64p, C.c_uint64, C.c_int64, C.c_int, C.c_int,
                                                u8p, u32p, u64p]),
         "orc_baseline_hrw": (C.c_double, [u8p, C.c_uint64, C.c_char_p, u64p, C.c_uint32, u8p,
@@ -267,6 +268,17 @@ def baseline_run_lazy(blob_idx, lengths, piece_length: int, threads: int, passes
     busy = lib().orc_baseline_run_lazy(_ptr(bi, C.c_uint64), _ptr(ln, C.c_uint64), len(bi), piece_length, threads,
                                        passes, _ptr(dg, C.c_uint8), _ptr(sums, C.c_uint32), _ptr(off, C.c_uint64))
     return busy, dg, (sums, off)
+
+
+def crc_bufs(ptrs, lengths, threads: int):
+    """orc_crc_bufs: one CRC-32 per caller buffer (addresses `ptrs`, byte counts `lengths`) on
+    `threads` threads.  Returns (seconds, sums)."""
+    n = len(ptrs)
+    pa = (C.c_void_p * max(n, 1))(*[int(x) for x in ptrs])
+    ln = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+    sums = np.zeros(max(n, 1), dtype=np.uint32)
+    t = lib().orc_crc_bufs(pa, _ptr(ln, C.c_uint64), n, threads, _ptr(sums, C.c_uint32))
+    return t, sums[:n]
 
 
 def baseline_files(paths, lengths, piece_length: int, threads: int, passes: int = 2):

@@ -99,3 +99,43 @@ def test_host_gpu_split_bit_exact(gpu, monkeypatch, frac, pinned):
     for b, s in zip(big, D.piece_sums_host(big, P)):
         want_s = [zlib.crc32(b[k:k + P].tobytes()) for k in range(0, b.size, P)]
         assert [int(x) for x in s] == want_s
+
+
+def _place_stripes(arr, stripe):
+    """Moves the pages of `arr` (page-aligned) to NUMA nodes 0 and 1 in alternating stripes of
+    `stripe` bytes (move_pages(2)); False when the host has one node or the call fails."""
+    import ctypes
+    nodes = [d for d in os.listdir("/sys/devices/system/node") if d.startswith("node")] \
+        if os.path.isdir("/sys/devices/system/node") else []
+    if len(nodes) < 2:
+        return False
+    libc = ctypes.CDLL(None, use_errno=True)
+    n = arr.size // 4096
+    pages = (ctypes.c_void_p * n)(*[arr.ctypes.data + i * 4096 for i in range(n)])
+    dst = (ctypes.c_int * n)(*[(i * 4096 // stripe) & 1 for i in range(n)])
+    status = (ctypes.c_int * n)()
+    return libc.syscall(279, 0, ctypes.c_ulong(n), pages, dst, status, 2) == 0  # SYS_move_pages, MPOL_MF_MOVE
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_host_crc_numa_handout_bit_exact(gpu, monkeypatch, mode):
+    """The host CRC share's NUMA-aware hand-out (KRK_CRC_NUMA: 0 one cursor, 1 per-node
+    claims, 2 per-node claims + node visits, the default) over a buffer whose 8 MiB runs sit
+    on alternating nodes (and on a half-stripe offset, so every task straddles two nodes and
+    is never visited): every task is summed once, the sums are zlib's."""
+    import mmap
+    from kraken_amd import device as D
+    monkeypatch.setenv("KRK_CRC_NUMA", mode)
+    monkeypatch.setenv("KRK_CRC_GPU_FRACTION", "0")  # every byte through the host hand-out
+    P, L = 256 << 10, 192 << 20
+    for shift in (0, 4 << 20):
+        m = mmap.mmap(-1, L)
+        arr = np.frombuffer(m, dtype=np.uint8)
+        arr[:] = np.random.default_rng(7).integers(0, 256, L, dtype=np.uint8)
+        _place_stripes(arr, 8 << 20)
+        blob = arr[shift:]
+        (s,) = D.piece_sums_host([blob], P)
+        want = [zlib.crc32(blob[k:k + P].tobytes()) for k in range(0, blob.size, P)]
+        assert [int(x) for x in s] == want
+        del arr, blob, s
+        m.close()

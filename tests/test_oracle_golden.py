@@ -136,6 +136,17 @@ def test_baseline_runner_outputs(orc):
         assert sums[int(off[i]):int(off[i]) + len(ref)].tolist() == ref.tolist()
 
 
+def test_crc_bufs_matches_zlib(orc):
+    """The same-buffer CPU leg (one CRC per caller buffer, bench f1verify / C4 A/B) is zlib's
+    crc32 of each buffer, empty ones included."""
+    import zlib
+    rng = np.random.default_rng(6)
+    bufs = [rng.integers(0, 256, L, dtype=np.uint8) for L in (0, 1, 32767, 32768, 32769, (1 << 20) + 5)]
+    t, sums = orc.crc_bufs([b.ctypes.data for b in bufs], [b.size for b in bufs], 3)
+    assert t >= 0
+    assert sums.tolist() == [zlib.crc32(b.tobytes()) for b in bufs]
+
+
 def test_baseline_files_matches_zlib(orc, tmp_path):
     """The files CPU baseline (the reference's Generate over cache files: calcPieceSums over
     the file reader in 32 KiB reads) gives zlib's piece sums, and fails on a short file."""
