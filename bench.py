@@ -1397,24 +1397,52 @@ def run_hrw(a, D, T, rank, world, res):
     pin = D.PinnedArray((n, R), np.uint8 if compact else np.int32)  # owner lists gathered to pinned host memory
     locs_h = pin.a
     place = D.ring_locations_u8_dev if compact else D.ring_locations_dev
+    # A step = the placement call, the owner lists' copy into pinned host memory queued
+    # behind it on the same stream, and one wait for that stream (how a caller uses it: the
+    # lists are on the host when the step ends).  Serial: each step's lists on the host
+    # before the next is enqueued.  `back_to_back` then enqueues step k + 1 on the other
+    # stream (its own outputs) before waiting for step k, so the host's enqueue and each
+    # copy overlap the neighbour's kernel (a placement service draining a queue of batches).
+    import ctypes as C
+    streams = [C.c_void_p(), C.c_void_p()]
+    for st in streams:
+        D.check(D.lib.krk_stream_create(C.byref(st)))
+    outs = [(locs, counts, pin), (D.DeviceBuffer(n * R * isz), D.DeviceBuffer(n),
+                                  D.PinnedArray((n, R), np.uint8 if compact else np.int32))]
 
-    def step():
-        place(dbuf, n, labels, healthy, R, locs, counts)
-        D.synchronize()
-        pin.fill_from(locs)
+    def enqueue(k):
+        lo, co, pi = outs[k & 1]
+        place(dbuf, n, labels, healthy, R, lo, co, stream=streams[k & 1])
+        pi.fill_from_async(lo, streams[k & 1])
 
-    for _ in range(a.warmup):
-        step()
+    def run(nsteps, serial):
+        for k in range(nsteps):
+            enqueue(k)
+            if serial:
+                D.check(D.lib.krk_stream_sync(streams[k & 1]))
+            elif k:
+                D.check(D.lib.krk_stream_sync(streams[(k - 1) & 1]))
+        if nsteps:
+            D.check(D.lib.krk_stream_sync(streams[(nsteps - 1) & 1]))
+
+    run(a.warmup, True)
     T.barrier()
     with D.KernelTimer():
         t0 = time.perf_counter()
-        for _ in range(a.steps):
-            step()
+        run(a.steps, True)
         T.barrier()
         t1 = time.perf_counter()
         hn, hms = D.KernelTimer.stats("hrw_order")
         gn, gms = D.KernelTimer.stats("hrw_gather")
     elapsed = T.timed_region(t1 - t0)
+    locs_h = outs[(a.steps - 1) & 1][2].a if a.steps else locs_h
+    want_locs = locs_h.copy()
+    T.barrier()
+    t2 = time.perf_counter()
+    run(a.steps, False)
+    T.barrier()
+    el_b2b = T.max_over_ranks(time.perf_counter() - t2)
+    b2b_ok = all(np.array_equal(outs[i][2].a, want_locs) for i in range(min(2, a.steps)))
     res.update({"metric": "hashring placement digests/s (C5)", "value": round(world * n * a.steps / elapsed, 1),
                 "unit": "digests/s", "steps": a.steps, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "weak", "dtype": "u64+f64",
@@ -1423,7 +1451,11 @@ def run_hrw(a, D, T, rank, world, res):
                            "max_replica": R, "mode": "device-resident (65,536-shard table + gather)",
                            "owner_index_bytes": isz},
                 "kernels": {"hrw_order": {"launches": hn, "avg_ms": round(hms / max(hn, 1), 3)},
-                            "hrw_gather": {"launches": gn, "avg_ms": round(gms / max(gn, 1), 3)}}})
+                            "hrw_gather": {"launches": gn, "avg_ms": round(gms / max(gn, 1), 3)}},
+                "back_to_back": {"value": round(world * n * a.steps / el_b2b, 1), "unit": "digests/s",
+                                 "ms_per_step": round(el_b2b / a.steps * 1e3, 3), "locs_match_serial": b2b_ok,
+                                 "what": "the same steps with step k+1 enqueued on the other stream (its own "
+                                         "outputs) before the host waits for step k"}})
     # Roofline of the per-digest kernel (the gather: HBM-bound, 32-B digest record in,
     # R owner indices + a count out).  The shard-table kernel's work is fixed (65,536
     # ShardIDs x N scores: murmur3 + Go math.Log, VALU/f64-bound, not per-digest).

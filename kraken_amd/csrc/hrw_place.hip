@@ -245,4 +245,95 @@ hipError_t launch_shard_gather_u8(const uint8_t* digests32, uint64_t n, const in
     return launch_gather(digests32, n, table_locs, table_counts, row_out, locs, counts, s);
 }
 
+// One word a ShardID: owners in bytes 0..row_out-1 (0xFF for none), 0xFF up to byte 2,
+// the count in byte 3.
+__global__ void pack_owner_rows_kernel(const int32_t* tl, const uint8_t* tc, uint32_t row_out, uint32_t* packed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 65536u) return;
+    uint32_t w = 0x00FFFFFFu;
+    for (uint32_t q = 0; q < row_out; ++q) {
+        const int32_t v = tl[(uint64_t)i * row_out + q];
+        w = (w & ~(0xFFu << (8 * q))) | ((uint32_t)(v < 0 ? 0xFF : v) << (8 * q));
+    }
+    packed[i] = (w & 0x00FFFFFFu) | ((uint32_t)tc[i] << 24);
+}
+
+hipError_t launch_pack_owner_rows(const int32_t* table_locs, const uint8_t* table_counts, uint32_t row_out,
+                                  uint32_t* packed, hipStream_t s) {
+    if (row_out < 1 || row_out > 3) return hipErrorInvalidValue;
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
+    hipLaunchKernelGGL(pack_owner_rows_kernel, dim3(65536 / 256), dim3(256), 0, s, table_locs, table_counts, row_out,
+                       packed);
+    return hipGetLastError();
+}
+
+// 256 digests a wave.  Loads are wave-contiguous (load k of lane l: digest 64k + l, so one
+// instruction reads 64 consecutive 32-byte records), the ShardID is bytes 0, 1 of the
+// record (one 16-bit load, big-endian), its packed row comes from the L2-resident 256 KiB
+// table, and the rows go through LDS so that each lane then holds four CONSECUTIVE digests'
+// rows: 4 x R owner bytes = R word stores and the four counts = one word store, adjacent
+// lanes writing adjacent words.  A ragged tail writes byte by byte.
+template <int R>
+__global__ void __launch_bounds__(256) shard_gather_packed_kernel(const uint8_t* digests32, uint64_t n,
+                                                                  const uint32_t* packed, uint8_t* locs,
+                                                                  uint8_t* counts) {
+    __shared__ uint32_t rows[4 * 256];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t wbase = ((uint64_t)blockIdx.x * 4 + wv) * 256;
+    uint32_t* x = rows + wv * 256;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t d = wbase + 64 * k + lane;
+        uint32_t shard = 0;
+        if (d < n) {
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(digests32 + 32 * d);
+            shard = ((v & 0xFFu) << 8) | (v >> 8);
+        }
+        x[64 * k + lane] = packed[shard];
+    }
+    __syncthreads();  // every thread reaches it: no early exit above
+    const uint64_t base = wbase + 4 * lane;
+    if (base >= n) return;
+    const uint32_t m = (uint32_t)(n - base < 4 ? n - base : 4);
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = x[4 * lane + k];
+    if (m == 4) {
+        uint32_t* lo = reinterpret_cast<uint32_t*>(locs + base * R);
+        if constexpr (R == 3) {
+            lo[0] = (w[0] & 0xFFFFFFu) | (w[1] << 24);
+            lo[1] = ((w[1] >> 8) & 0xFFFFu) | ((w[2] & 0xFFFFu) << 16);
+            lo[2] = ((w[2] >> 16) & 0xFFu) | ((w[3] & 0xFFFFFFu) << 8);
+        } else if constexpr (R == 2) {
+            lo[0] = (w[0] & 0xFFFFu) | ((w[1] & 0xFFFFu) << 16);
+            lo[1] = (w[2] & 0xFFFFu) | ((w[3] & 0xFFFFu) << 16);
+        } else {
+            lo[0] = (w[0] & 0xFFu) | ((w[1] & 0xFFu) << 8) | ((w[2] & 0xFFu) << 16) | ((w[3] & 0xFFu) << 24);
+        }
+        *reinterpret_cast<uint32_t*>(counts + base) =
+            (w[0] >> 24) | ((w[1] >> 24) << 8) | ((w[2] >> 24) << 16) | ((w[3] >> 24) << 24);
+        return;
+    }
+    for (uint32_t k = 0; k < m; ++k) {
+        for (int q = 0; q < R; ++q) locs[(base + k) * R + q] = (uint8_t)(w[k] >> (8 * q));
+        counts[base + k] = (uint8_t)(w[k] >> 24);
+    }
+}
+
+hipError_t launch_shard_gather_packed(const uint8_t* digests32, uint64_t n, const uint32_t* packed,
+                                      uint32_t row_out, uint8_t* locs, uint8_t* counts, hipStream_t s) {
+    if (!n) return hipSuccess;
+    if (row_out < 1 || row_out > 3 || ((uintptr_t)digests32 & 1) || ((uintptr_t)locs & 3) || ((uintptr_t)counts & 3))
+        return hipErrorInvalidValue;
+    if (const hipError_t p_ = launch_precheck(); p_ != hipSuccess) return p_;
+    const dim3 grid((uint32_t)((n + 1023) / 1024)), block(256);  // 1,024 digests a workgroup
+    if (row_out == 3)
+        hipLaunchKernelGGL(shard_gather_packed_kernel<3>, grid, block, 0, s, digests32, n, packed, locs, counts);
+    else if (row_out == 2)
+        hipLaunchKernelGGL(shard_gather_packed_kernel<2>, grid, block, 0, s, digests32, n, packed, locs, counts);
+    else
+        hipLaunchKernelGGL(shard_gather_packed_kernel<1>, grid, block, 0, s, digests32, n, packed, locs, counts);
+    return hipGetLastError();
+}
+
 }  // namespace krk

@@ -189,6 +189,15 @@ hipError_t launch_shard_gather(const uint8_t* digests32, uint64_t n, const int32
 hipError_t launch_shard_gather_u8(const uint8_t* digests32, uint64_t n, const int32_t* table_locs,
                                   const uint8_t* table_counts, uint32_t row_out, uint8_t* locs,
                                   uint8_t* counts, hipStream_t s);
+// The owner table of a ring of <= 255 nodes with rows of <= 3 owners packed one word a
+// ShardID (owner bytes 0-2, 0xFF padded; the count in byte 3), and the gather over it:
+// wave-contiguous digest loads, one word load a row, rows regrouped through LDS so owner
+// lists and counts go out as whole words.
+// Needs digests32 2-byte aligned and locs / counts 4-byte aligned (the caller checks).
+hipError_t launch_pack_owner_rows(const int32_t* table_locs, const uint8_t* table_counts, uint32_t row_out,
+                                  uint32_t* packed, hipStream_t s);
+hipError_t launch_shard_gather_packed(const uint8_t* digests32, uint64_t n, const uint32_t* packed,
+                                      uint32_t row_out, uint8_t* locs, uint8_t* counts, hipStream_t s);
 
 // ---------------------------------------------------------------- synthetic data
 // One synthetic chunk: bytes [offset, offset + n) of the blob whose stream seed is `seed`.

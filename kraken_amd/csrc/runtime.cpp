@@ -1516,6 +1516,7 @@ struct OwnerTable {
     std::vector<uint8_t> key;
     int32_t* tl = nullptr;
     uint8_t* tc = nullptr;
+    uint32_t* tp = nullptr;  // packed rows (launch_pack_owner_rows) when N <= 255 and row <= 3
     hipEvent_t ready = nullptr;
     std::vector<std::pair<hipStream_t, hipEvent_t>> used;
     uint64_t stamp = 0;
@@ -1551,6 +1552,7 @@ static void owner_release(Device* D, OwnerTable& t, hipStream_t s) {
     if (t.ready) hipEventDestroy(t.ready);
     if (t.tl) scratch_free(D, t.tl, s);
     if (t.tc) scratch_free(D, t.tc, s);
+    if (t.tp) scratch_free(D, t.tp, s);
     t = OwnerTable{};
 }
 
@@ -1558,7 +1560,8 @@ static void owner_release(Device* D, OwnerTable& t, hipStream_t s) {
 // once the call returns (s waits for its build); the caller's use is recorded after its
 // launch with owner_used().
 static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica,
-                       uint32_t row_out, int32_t** d_tl, uint8_t** d_tc, size_t* slot, hipStream_t s) {
+                       uint32_t row_out, int32_t** d_tl, uint8_t** d_tc, uint32_t** d_tp, size_t* slot,
+                       hipStream_t s) {
     std::vector<uint8_t> key = owner_key(nodes, healthy, max_replica);
     std::lock_guard<std::mutex> g(D->owners_mu);
     if (!D->owners) D->owners = new OwnerTables();
@@ -1569,6 +1572,7 @@ static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy
             C.e[i].stamp = ++C.clock;
             *d_tl = C.e[i].tl;
             *d_tc = C.e[i].tc;
+            *d_tp = C.e[i].tp;
             *slot = i;
             return KRK_OK;
         }
@@ -1583,6 +1587,12 @@ static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy
     }
     OwnerTable& t = C.e[i];
     int r = shard_owner_table(D, nodes, healthy, max_replica, row_out, &t.tl, &t.tc, s);
+    if (!r && nodes->n_nodes <= 255 && row_out <= 3 &&
+        (scratch_alloc(D, &t.tp, 65536 * sizeof(uint32_t), s) != hipSuccess ||
+         launch_pack_owner_rows(t.tl, t.tc, row_out, t.tp, s) != hipSuccess)) {
+        set_error(KRK_EHIP, "ring owner table: packed rows");
+        r = KRK_EHIP;
+    }
     if (!r && (hipEventCreateWithFlags(&t.ready, hipEventDisableTiming) != hipSuccess ||
                hipEventRecord(t.ready, s) != hipSuccess)) {
         set_error(KRK_EHIP, "ring owner table: event");
@@ -1597,6 +1607,7 @@ static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy
     t.stamp = ++C.clock;
     *d_tl = t.tl;
     *d_tc = t.tc;
+    *d_tp = t.tp;
     *slot = i;
     return KRK_OK;
 }
@@ -1640,13 +1651,18 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
     const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
     int32_t* d_tl = nullptr;
     uint8_t* d_tc = nullptr;
+    uint32_t* d_tp = nullptr;
     size_t slot = 0;
-    int r = owner_table(D, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, &slot, s);
+    int r = owner_table(D, nodes, healthy, max_replica, row_out, &d_tl, &d_tc, &d_tp, &slot, s);
     if (!r) {
         hipError_t e = timed(K_GATHER, s, [&] {
-            if constexpr (sizeof(T) == 1)
+            if constexpr (sizeof(T) == 1) {
+                // word stores need word-aligned outputs and a 2-byte aligned digest array
+                const bool words = d_tp && !((uintptr_t)digests32_dev & 1) && !((uintptr_t)locs_dev & 3) &&
+                                   !((uintptr_t)counts_dev & 3);
+                if (words) return launch_shard_gather_packed(digests32_dev, n, d_tp, row_out, locs_dev, counts_dev, s);
                 return launch_shard_gather_u8(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
-            else
+            } else
                 return launch_shard_gather(digests32_dev, n, d_tl, d_tc, row_out, locs_dev, counts_dev, s);
         });
         owner_used(D, slot, s);

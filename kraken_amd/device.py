@@ -545,7 +545,23 @@ def synth_fill_chunks(items, variant: int = 0, stream=None):
     check(lib.krk_synth_fill_chunks_dev(arr, len(items), variant, stream))
 
 
+_NODES_CACHE: dict = {}
+
+
 def nodes_struct(labels, weights):
+    """krk_nodes for (labels, weights), kept per membership (the last 16) so a placement
+    call per batch does not re-encode the ring."""
+    key = (tuple(labels), tuple(int(w) for w in weights))
+    hit = _NODES_CACHE.get(key)
+    if hit is not None:
+        return hit
+    if len(_NODES_CACHE) >= 16:
+        _NODES_CACHE.pop(next(iter(_NODES_CACHE)))
+    _NODES_CACHE[key] = hit = _nodes_struct(labels, weights)
+    return hit
+
+
+def _nodes_struct(labels, weights):
     enc = [s.encode() for s in labels]
     blob = b"".join(enc)
     off = np.zeros(len(enc) + 1, dtype=np.uint64)

@@ -216,10 +216,12 @@ def test_ring_locations_u8_dev_equals_int32_path(gpu, orc, n_nodes, max_replica)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("max_replica", [1, 3, 5])
+@pytest.mark.parametrize("max_replica", [1, 2, 3, 5])
 def test_ring_locations_u8_dev_offsets_and_tails(gpu, max_replica):
-    """Compact owner lists at any output address and count (byte stores, tails of every
-    length): every layout gives the int32 path's lists."""
+    """Compact owner lists at any output address and count: word-aligned outputs take the
+    packed-row gather (four digests a thread, word stores, rows of <= 3), others and rows
+    of more owners the byte-store gather; every layout and every tail length gives the
+    int32 path's lists."""
     import ctypes as C
     labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(16)]
     healthy = np.ones(16, dtype=np.uint8)
@@ -235,14 +237,26 @@ def test_ring_locations_u8_dev_offsets_and_tails(gpu, max_replica):
         want = np.where(l32.to_host(np.int32, n * max_replica) < 0, 255,
                         l32.to_host(np.int32, n * max_replica)).astype(np.uint8)
         wc = c32.to_host(np.uint8, n)
-        for shift in (0, 1, 3):
+        for shift, cshift in ((0, 0), (1, 1), (3, 3), (0, 2), (4, 0)):
             lb, cb = D.DeviceBuffer(n * max_replica + 8), D.DeviceBuffer(n + 8)
             s, keep = D.nodes_struct(labels, [100] * 16)
             check(lib.krk_ring_locations_u8_dev(dbuf.ptr, n, C.byref(s), healthy.ctypes.data_as(C.POINTER(C.c_uint8)),
-                                                 max_replica, lb.ptr + shift, cb.ptr + shift, None))
+                                                 max_replica, lb.ptr + shift, cb.ptr + cshift, None))
             D.synchronize()
             assert np.array_equal(lb.to_host(np.uint8, n * max_replica, shift), want), (n, shift)
-            assert np.array_equal(cb.to_host(np.uint8, n, shift), wc), (n, shift)
+            assert np.array_equal(cb.to_host(np.uint8, n, cshift), wc), (n, cshift)
+        # a digest array at an odd address (byte loads) and at a 2-byte one (16-bit loads)
+        for dshift in (1, 2):
+            db2 = D.DeviceBuffer(n * 32 + 4)
+            db2.from_host(np.concatenate([np.zeros(dshift, np.uint8), digests.reshape(-1)]))
+            lb, cb = D.DeviceBuffer(n * max_replica), D.DeviceBuffer(n)
+            s, keep = D.nodes_struct(labels, [100] * 16)
+            check(lib.krk_ring_locations_u8_dev(db2.ptr + dshift, n, C.byref(s),
+                                                 healthy.ctypes.data_as(C.POINTER(C.c_uint8)), max_replica, lb.ptr,
+                                                 cb.ptr, None))
+            D.synchronize()
+            assert np.array_equal(lb.to_host(np.uint8, n * max_replica), want), (n, dshift)
+            assert np.array_equal(cb.to_host(np.uint8, n), wc), (n, dshift)
 
 
 @pytest.mark.gpu

@@ -50,6 +50,8 @@ for step in "$@"; do
     crc_parity22 | crc_parity23) v=${step#crc_parity}
         run crc_parity$v 600 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so $PYT tests/test_gpu_pieces.py tests/test_gpu_full_size.py ;;
     # rocprofv3 summaries (kernel trace + copy trace; PMC passes on their own runs)
+    prof_c5) run prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d gpurun_out/prof_c5 -- python3 bench.py --workload c5 --no-cpu-baseline --no-sweep ;;
     prof_c2) run prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
     prof_files) run prof_files 600 rocprofv3 --kernel-trace --stats --output-format csv \
@@ -61,8 +63,9 @@ for step in "$@"; do
     prof_c4) for v in 16 20 21; do run prof_c4_v$v 300 env KRK_CRC_VARIANT=$v KRK_LIB_PATH=kraken_amd/lib/diag/libkraken_hip.so rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c4_v$v -- python3 bench.py --workload c4 --no-cpu-baseline --no-e2e; done ;;
     # round-5 PMC of the production kernels on the current tree (tools/pmc_traffic.py, pmc_valu.py)
-    pmc_c2 | pmc_c4 | pmc_files | pmc_e2e)
+    pmc_c2 | pmc_c4 | pmc_c5 | pmc_files | pmc_e2e)
         case $step in
+        pmc_c5) B="python3 bench.py --workload c5 --steps 3 --warmup 1 --no-cpu-baseline --no-sweep" ;;
         pmc_e2e) B="python3 bench.py --e2e-only --no-cpu-baseline" ;;
         pmc_c2) B="python3 bench.py --steps 1 --warmup 0 --no-e2e --no-cpu-baseline --no-ceiling" ;;
         pmc_c4) B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-e2e --no-cpu-baseline" ;;

@@ -31,12 +31,13 @@ from collections import defaultdict
 
 KERNELS = {"crc_items_kernel": "crc32_pieces", "gather_kernel": "host_gather", "sha256_ws_kernel": "sha256_multi", "sha256_w8_kernel": "sha256_multi",
            "hrw_order_kernel": "hrw_order",
-           "shard_gather_kernel": "hrw_gather", "synth_fill": "synth_fill"}
+           "shard_gather_kernel": "hrw_gather", "shard_gather_packed_kernel": "hrw_gather",
+           "pack_owner_rows_kernel": "hrw_order", "synth_fill": "synth_fill"}
 SIMDS = 1024  # 256 CUs x 4 SIMD-32
 
 
 def _short(name):
-    for k, v in KERNELS.items():
+    for k, v in sorted(KERNELS.items(), key=lambda kv: -len(kv[0])):  # the longest name first
         if k in name:
             return v
     return None
