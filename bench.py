@@ -1410,10 +1410,14 @@ def run_hrw(a, D, T, rank, world, res):
     outs = [(locs, counts, pin), (D.DeviceBuffer(n * R * isz), D.DeviceBuffer(n),
                                   D.PinnedArray((n, R), np.uint8 if compact else np.int32))]
 
+    enq_s = [0.0]
+
     def enqueue(k):
         lo, co, pi = outs[k & 1]
+        t = time.perf_counter()
         place(dbuf, n, labels, healthy, R, lo, co, stream=streams[k & 1])
         pi.fill_from_async(lo, streams[k & 1])
+        enq_s[0] += time.perf_counter() - t
 
     def run(nsteps, serial):
         for k in range(nsteps):
@@ -1427,6 +1431,7 @@ def run_hrw(a, D, T, rank, world, res):
 
     run(a.warmup, True)
     T.barrier()
+    enq_s[0] = 0.0
     with D.KernelTimer():
         t0 = time.perf_counter()
         run(a.steps, True)
@@ -1435,6 +1440,7 @@ def run_hrw(a, D, T, rank, world, res):
         hn, hms = D.KernelTimer.stats("hrw_order")
         gn, gms = D.KernelTimer.stats("hrw_gather")
     elapsed = T.timed_region(t1 - t0)
+    enqueue_us = enq_s[0] / max(a.steps, 1) * 1e6
     locs_h = outs[(a.steps - 1) & 1][2].a if a.steps else locs_h
     want_locs = locs_h.copy()
     T.barrier()
@@ -1452,6 +1458,7 @@ def run_hrw(a, D, T, rank, world, res):
                            "owner_index_bytes": isz},
                 "kernels": {"hrw_order": {"launches": hn, "avg_ms": round(hms / max(hn, 1), 3)},
                             "hrw_gather": {"launches": gn, "avg_ms": round(gms / max(gn, 1), 3)}},
+                "host_enqueue_us": round(enqueue_us, 1),
                 "back_to_back": {"value": round(world * n * a.steps / el_b2b, 1), "unit": "digests/s",
                                  "ms_per_step": round(el_b2b / a.steps * 1e3, 3), "locs_match_serial": b2b_ok,
                                  "what": "the same steps with step k+1 enqueued on the other stream (its own "
