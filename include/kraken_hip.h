@@ -398,10 +398,13 @@ int krk_ring_locations(const uint8_t* digests32, uint64_t n, const krk_nodes* no
  * entries.  Same semantics as krk_ring_locations. */
 int krk_ring_owner_table(const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica,
                          int32_t* locs_out, uint8_t* counts_out);
-/* Device-resident form (digests/locs/counts are device pointers).  The owner table of a
- * membership (labels, weights, healthy, max_replica) is built on its first call and kept
- * (8 memberships a device, least recently used replaced), as the reference's Ring keeps its
- * hrw until Refresh; later calls only gather. */
+/* Device-resident form (digests in device memory).  The owner table of a membership
+ * (labels, weights, healthy, max_replica) is built on its first call and kept (8
+ * memberships a device, least recently used replaced), as the reference's Ring keeps its
+ * hrw until Refresh; later calls only gather.  locs/counts: device memory, or page-locked
+ * host memory (krk_host_alloc) that the gather writes over PCIe -- the owner lists are on
+ * the host when the stream reaches the call's end, with no copy-back; any other pointer is
+ * KRK_EINVAL. */
 int krk_ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
                            const uint8_t* healthy, int32_t max_replica,
                            int32_t* locs_dev, uint8_t* counts_dev, void* stream);

@@ -1637,6 +1637,23 @@ static void owner_used(Device* D, size_t slot, hipStream_t s) {
     }
 }
 
+// Where the placement kernels may write [p, p + n): device memory, or page-locked host
+// memory the GPU maps at its host address (krk_host_alloc / hipHostMalloc / registered:
+// the gather then writes the owner lists over PCIe and the caller needs no copy-back).
+// Pageable memory, or a mapping at another address, is refused -- the kernel would fault.
+static bool device_writable(const void* p, uint64_t n) {
+    auto ok_at = [](const void* q) {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type == hipMemoryTypeDevice) return true;
+        return a.type == hipMemoryTypeHost && a.devicePointer == q;
+    };
+    return ok_at(p) && (n <= 1 || ok_at(static_cast<const uint8_t*>(p) + n - 1));
+}
+
 template <typename T>
 static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const krk_nodes* nodes,
                               const uint8_t* healthy, int32_t max_replica, T* locs_dev, uint8_t* counts_dev,
@@ -1649,6 +1666,8 @@ static int ring_locations_dev(const uint8_t* digests32_dev, uint64_t n, const kr
     KRK_DEVICE(D);
     hipStream_t s = pick(D, stream);
     const uint32_t row_out = (uint32_t)std::max<int32_t>(1, max_replica);
+    KRK_CHECK(device_writable(locs_dev, n * row_out * sizeof(T)) && device_writable(counts_dev, n), KRK_EINVAL,
+              "ring_locations_dev: locs and counts must be device memory or page-locked host memory");
     int32_t* d_tl = nullptr;
     uint8_t* d_tc = nullptr;
     uint32_t* d_tp = nullptr;

@@ -327,3 +327,49 @@ def test_ring_owner_table_lookup(gpu, orc, n_nodes, max_replica):
     d = core.NewSHA256DigestFromHex(bytes(digests[0]).hex())
     key = d.ShardID()
     assert ring.Locations(d) == [labels[orc.hrw_ordered(key, labels, [100] * n_nodes)[0]]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_replica", [2, 3, 5])
+def test_ring_locations_into_page_locked_host_memory(gpu, max_replica):
+    """locs / counts in page-locked host memory (krk_host_alloc): the gather writes the owner
+    lists there over PCIe -- the same lists as device outputs, word-aligned or not, u8 and
+    int32; pageable host memory is refused (KRK_EINVAL) before any launch."""
+    import ctypes as C
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(16)]
+    healthy = np.ones(16, dtype=np.uint8)
+    healthy[[4, 11]] = 0
+    rng = np.random.default_rng(500 + max_replica)
+    n = 20003
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    l8, c8 = D.DeviceBuffer(n * max_replica), D.DeviceBuffer(n)
+    l32, c32 = D.DeviceBuffer(n * max_replica * 4), D.DeviceBuffer(n)
+    D.ring_locations_u8_dev(dbuf, n, labels, healthy, max_replica, l8, c8)
+    D.ring_locations_dev(dbuf, n, labels, healthy, max_replica, l32, c32)
+    D.synchronize()
+    w8, wc = l8.to_host(np.uint8, n * max_replica), c8.to_host(np.uint8, n)
+    w32 = l32.to_host(np.int32, n * max_replica)
+    pl, pc = D.PinnedArray((n * max_replica + 8,), np.uint8), D.PinnedArray((n + 8,), np.uint8)
+    s, keep = D.nodes_struct(labels, [100] * 16)
+    hp = healthy.ctypes.data_as(C.POINTER(C.c_uint8))
+    for shift in (0, 1, 4):
+        pl.a[:] = 0xAA
+        pc.a[:] = 0xAA
+        check(lib.krk_ring_locations_u8_dev(dbuf.ptr, n, C.byref(s), hp, max_replica, pl.ptr + shift, pc.ptr + shift,
+                                             None))
+        D.synchronize()
+        assert np.array_equal(pl.a[shift:shift + n * max_replica], w8), shift
+        assert np.array_equal(pc.a[shift:shift + n], wc), shift
+        assert (pl.a[:shift] == 0xAA).all() and (pl.a[shift + n * max_replica:] == 0xAA).all()
+    p32 = D.PinnedArray((n * max_replica,), np.int32)
+    pc.a[:] = 0
+    check(lib.krk_ring_locations_dev(dbuf.ptr, n, C.byref(s), hp, max_replica, p32.ptr, pc.ptr, None))
+    D.synchronize()
+    assert np.array_equal(p32.a, w32) and np.array_equal(pc.a[:n], wc)
+    pageable = np.zeros(n * max_replica, dtype=np.uint8)
+    with pytest.raises(Exception, match="page-locked"):
+        check(lib.krk_ring_locations_u8_dev(dbuf.ptr, n, C.byref(s), hp, max_replica,
+                                             pageable.ctypes.data, c8.ptr, None))
+    D.synchronize()
