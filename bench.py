@@ -106,7 +106,9 @@ WORKLOADS = {
                                        "lengths from {0:1MB, 2GB:4MB, 4GB:8MB}"),
     "c5regen_digest": dict(kind="metainfo", desc="C5 regen blobs with the upload digest as well (metainfo + "
                                                  "SHA-256 per blob)"),
-    "f1verify": dict(kind="verify", desc="Agent piece verify (agentstorage.Torrent.writePiece, torrent.go:174-199): "
+    # warmup 3: the host/GPU split's learning calls (window setup, a split sample, a host-only
+    # sample) run before the timed steps, as in a long-running agent
+    "f1verify": dict(kind="verify", steps=5, warmup=3, desc="Agent piece verify (agentstorage.Torrent.writePiece, torrent.go:174-199): "
                                          "4,096 received 4 MiB pieces in pinned host receive buffers checked against "
                                          "GetPieceSum, split between host threads and the GPU; 1 in 64 corrupted"),
     "c4": dict(kind="pieces", steps=20, warmup=2,  # 3.6 ms steps
