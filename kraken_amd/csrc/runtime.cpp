@@ -622,9 +622,9 @@ struct PieceTask {
 // and steals from the others once its node has none (KRK_CRC_NUMA=1), and with
 // KRK_CRC_NUMA=2, for a batch spread over both sockets' memory, a thread that takes another
 // node's task runs it on that node's CPUs (NodeVisit).  Off by default (0 = one plain
-// cursor): on the GPU boxes' two-socket hosts, four interleaved A/B runs of the three modes
-// (profiles/r05/host_mem_probe_numa.jsonl) moved the spread-buffer case by +33, +8, +14 and
-// -14 % with visits and left every one-node buffer equal or a few % lower -- inside the
+// cursor): on the GPU boxes' two-socket hosts, five interleaved A/B runs of the three modes
+// (profiles/r05/host_mem_probe_numa.jsonl) moved the spread-buffer case by +33, +8, +14,
+// -14, +31 % with visits and left every one-node buffer equal or a few % lower -- inside the
 // host's minute-to-minute swing, not a win to ship.
 class NodeTasks {
   public:

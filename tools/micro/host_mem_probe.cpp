@@ -84,6 +84,24 @@ double h2d_rate(const uint8_t* p, size_t n, void* dev, hipStream_t s) {
     }
     return best;
 }
+// The CPUs of NUMA node nd (empty when sysfs does not list it).
+cpu_set_t node_set(int nd) {
+    std::ifstream f("/sys/devices/system/node/node" + std::to_string(nd) + "/cpulist");
+    std::string list;
+    std::getline(f, list);
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    for (size_t q = 0; q < list.size();) {
+        size_t e = list.find(',', q);
+        if (e == std::string::npos) e = list.size();
+        const std::string r = list.substr(q, e - q);
+        const size_t d = r.find('-');
+        const int a = atoi(r.c_str()), b = d == std::string::npos ? a : atoi(r.c_str() + d + 1);
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(c, &cs);
+        q = e + 1;
+    }
+    return cs;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -203,7 +221,7 @@ int main(int argc, char** argv) {
     }
     for (const char* kind : {"lib_pinned_cpu_filled", "lib_pinned_spread_filled", "lib_pinned_dma_filled", "lib_pageable",
                              "lib_pageable_spread", "lib_thp_interleave_pageable", "lib_thp_local_registered",
-                             "lib_thp_local_pageable"}) {
+                             "lib_thp_local_pageable", "lib_thp_nodespread_registered", "lib_thp_nodespread_pageable"}) {
         uint8_t* p = nullptr;
         const bool pinned = strncmp(kind, "lib_pinned", 10) == 0;
         const bool thp = strncmp(kind, "lib_thp", 7) == 0;
@@ -221,6 +239,19 @@ int main(int argc, char** argv) {
         }
         if (!strcmp(kind, "lib_pinned_dma_filled")) {
             if (hipMemcpy(p, dev, n, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+        } else if (strstr(kind, "nodespread")) {  // T spans first-touched by threads on alternating nodes
+            std::vector<std::thread> th;
+            const size_t span = n / T;
+            for (int t = 0; t < T; ++t)
+                th.emplace_back([=] {
+                    cpu_set_t cs = node_set(t & 1);
+                    if (CPU_COUNT(&cs)) sched_setaffinity(0, sizeof cs, &cs);
+                    for (size_t i = t * span; i < (t + 1) * span; i += 8) {
+                        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+                        memcpy(p + i, &z, 8);
+                    }
+                });
+            for (auto& x : th) x.join();
         } else if (strstr(kind, "spread")) {  // written by T threads in spans (a receive path's threads)
             std::vector<std::thread> th;
             const size_t span = n / T;
@@ -238,8 +269,8 @@ int main(int argc, char** argv) {
                 memcpy(p + i, &z, 8);
             }
         }
-        if (!strcmp(kind, "lib_thp_local_registered") && hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess)
-            return 1;
+        const bool reg = thp && strstr(kind, "_registered");
+        if (reg && hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) return 1;
         const uint64_t P = 256 << 10, np = n / P;
         std::vector<uint32_t> sums(np);
         krk_blob b{p, n, (int64_t)P, 0};
@@ -267,7 +298,7 @@ int main(int argc, char** argv) {
         fflush(stdout);
         if (pinned) krk_host_free(p);
         else if (thp) {
-            if (!strcmp(kind, "lib_thp_local_registered")) hipHostUnregister(p);
+            if (reg) hipHostUnregister(p);
             munmap(p, n);
         } else free(p);
     }
