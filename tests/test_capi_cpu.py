@@ -209,13 +209,30 @@ def test_host_crossover_primitives_match_hashlib_zlib():
         assert c.value == zlib.crc32(d, seed), n
 
 
+def test_host_crc_folding_paths_match_zlib():
+    """The host CRC's folding loops -- AVX-512 VPCLMULQDQ (256 bytes an iteration, then 64-byte
+    and 16-byte folds) where this CPU has it, the 128-bit PCLMUL loop otherwise -- at every
+    length around their block edges and at unaligned addresses, against zlib."""
+    import zlib
+    rng = np.random.default_rng(12)
+    buf = rng.integers(0, 256, (1 << 20) + 64, dtype=np.uint8)
+    lens = [n for b in (64, 256, 512, 768, 4096) for n in range(b - 17, b + 18)]
+    lens += [int(x) for x in rng.integers(0, 1 << 20, 64)]
+    c = C.c_uint32()
+    for n in lens:
+        for off in (0, 3, 40):
+            seed = int(rng.integers(0, 2 ** 32))
+            check(lib.krk_host_crc32_update(seed, buf.ctypes.data + off, n, C.byref(c)))
+            assert c.value == zlib.crc32(buf[off:off + n].tobytes(), seed), (n, off)
+
+
 _HOST_SCRIPT = """
 import sys, ctypes as C, numpy as np
 sys.path.insert(0, sys.argv[1])
 from kraken_amd._capi import lib
 rng = np.random.default_rng(5)
 out = []
-for n in [0, 1, 63, 64, 65, 127, 128, 1000, 4096, 100000]:
+for n in [0, 1, 63, 64, 65, 127, 128, 1000, 4096, 100003]:
     d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
     o = (C.c_uint8 * 32)(); c = C.c_uint32()
     lib.krk_host_sha256(d, n, o); lib.krk_host_crc32_update(7, d, n, C.byref(c))
@@ -225,16 +242,18 @@ print(" ".join(out))
 
 
 def test_host_crossover_ni_matches_portable(tmp_path):
-    """SHA-NI / PCLMULQDQ routines (when this CPU has them) equal the portable ones."""
+    """SHA-NI / PCLMULQDQ / VPCLMULQDQ routines (when this CPU has them) equal the portable
+    ones (KRK_HOST_CRC_AVX512=0: the 128-bit PCLMUL loop)."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     f = tmp_path / "h.py"
     f.write_text(_HOST_SCRIPT)
     runs = [subprocess.run([sys.executable, str(f), root], capture_output=True, text=True,
-                           env={**os.environ, "KRK_HOST_PORTABLE": v}) for v in ("0", "1")]
+                           env={**os.environ, "KRK_HOST_PORTABLE": v, "KRK_HOST_CRC_AVX512": a})
+            for v, a in (("0", "1"), ("1", "1"), ("0", "0"))]
     assert all(r.returncode == 0 for r in runs), [r.stderr for r in runs]
-    assert runs[0].stdout == runs[1].stdout and len(runs[0].stdout.split()) == 10
+    assert runs[0].stdout == runs[1].stdout == runs[2].stdout and len(runs[0].stdout.split()) == 10
 
 
 def test_host_placements_work_without_a_device():
