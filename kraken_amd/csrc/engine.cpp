@@ -1485,7 +1485,17 @@ void stream_host_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
         bool ends_piece;
         uint32_t c;
     };
-    const uint64_t span = std::max<uint64_t>(256u << 10, ((n / (uint64_t)(idle + 1)) + 63) & ~uint64_t(63));
+    // A span should outlast a pool thread's wake-up: at least ~40 us of one thread's CRC
+    // (256 KiB on the 128-bit PCLMUL loop, ~1.7 MiB on AVX-512 VPCLMULQDQ, where 256 KiB spans
+    // took ~6 us each and the caller finished its own before the helpers woke).
+    // KRK_STREAM_SPAN_KB overrides it (A/B).
+    static const uint64_t min_span = [] {
+        const char* v = getenv("KRK_STREAM_SPAN_KB");
+        if (v) return std::max<uint64_t>(64, strtoull(v, nullptr, 10)) << 10;
+        const uint64_t b = (uint64_t)(host_crc_rate() * 40e-6);
+        return std::max<uint64_t>(256u << 10, (b + 65535) & ~uint64_t(65535));
+    }();
+    const uint64_t span = std::max<uint64_t>(min_span, ((n / (uint64_t)(idle + 1)) + 63) & ~uint64_t(63));
     std::vector<Span> sp;
     for (uint64_t in = s->in_piece, o = 0; o < n;) {
         const uint64_t take = std::min<uint64_t>(n - o, s->P - in);
