@@ -696,6 +696,13 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         r = KRK_EHIP;
     }
     const bool bounce = filler.reg != nullptr;
+    // The registry's helper threads may still be registering caller ranges (pages that can
+    // hold the output arrays or the bounce buffer): stop them and unregister before any
+    // copy-out -- every gather has drained with the streams above.
+    if (filler.reg) {
+        filler.reg->finish(filler.gather_stream);
+        filler.reg.reset();
+    }
     if (!r) r = copy_out(digests_host, o.d_dig, n * 32, bounce, "digest");
     if (!r && hi > lo) r = copy_out(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, bounce, "sums");
     if (host_th.joinable()) host_th.join();
