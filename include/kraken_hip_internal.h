@@ -70,6 +70,10 @@ int krk_windows_last_direct(int* direct_windows);
  * 0 / 1 forces off / on), the caller bytes it registered and the helper threads' seconds
  * spent registering them. */
 int krk_windows_last_gather(int* gather_windows, uint64_t* registered_bytes, double* register_seconds);
+/* ... and how many of the caller ranges it registered for the gather were still registered
+ * when its results were copied out (0: every host-buffer call releases them first; a copy
+ * into a page the call holds registered is refused). */
+int krk_windows_last_copyout(uint64_t* live_registered);
 /* The calling thread's last device-resident SHA-256 batch (krk_sha256_dev,
  * krk_metainfo_digest_dev): chains whose tails host threads finished from the GPU's midstate
  * (the tail handoff of the host offload; 0 when whole blobs or nothing went to the host) and

@@ -130,6 +130,7 @@ def _load() -> C.CDLL:
         "krk_window_stream_cap": (i, [u64p]),
         "krk_windows_last_call": (i, [u64p, C.POINTER(C.c_int), u64p]),
         "krk_windows_last_direct": (i, [C.POINTER(C.c_int)]),
+        "krk_windows_last_copyout": (i, [u64p]),
         "krk_windows_last_gather": (i, [C.POINTER(C.c_int), u64p, f64p]),
         "krk_windows_last_phases": (i, [f64p, f64p, f64p, f64p, f64p, C.POINTER(C.c_int)]),
         "krk_sha_last_tail": (i, [u64p, u64p]),

@@ -33,6 +33,14 @@
 
 namespace krk {
 
+// The HIP calls the registry makes, swappable so that the schedule and the page accounting
+// run on a CPU with a recording stand-in (tests/native/registry_race.cpp under TSan/ASan).
+struct RegBackend {
+    hipError_t (*reg)(void* p, size_t n, unsigned flags) = hipHostRegister;
+    hipError_t (*unreg)(void* p) = hipHostUnregister;
+    hipError_t (*dev_ptr)(void** d, void* p, unsigned flags) = hipHostGetDevicePointer;
+};
+
 class HostRegistry {
   public:
     static constexpr uint64_t kPage = 4096;
@@ -40,7 +48,8 @@ class HostRegistry {
     static constexpr int kRegAhead = 6;               // windows registered ahead of the loop
 
     // [a, b) ranges of the blobs the windows will read (any alignment, may overlap)
-    explicit HostRegistry(std::vector<std::pair<uintptr_t, uintptr_t>> ranges) {
+    explicit HostRegistry(std::vector<std::pair<uintptr_t, uintptr_t>> ranges, RegBackend be = RegBackend())
+        : be_(be) {
         for (auto& r : ranges) {
             r.first &= ~(kPage - 1);
             r.second = (r.second + kPage - 1) & ~(kPage - 1);
@@ -116,7 +125,7 @@ class HostRegistry {
         for (size_t q = retired_; q < prefix_; ++q) {
             const uint32_t i = order_[q];
             if (state_[i].load() == kRegistered && seg_[i].last <= w) {
-                hipHostUnregister(reinterpret_cast<void*>(seg_[i].a));
+                be_.unreg(reinterpret_cast<void*>(seg_[i].a));
                 state_[i].store(kReleased);
             }
         }
@@ -136,9 +145,27 @@ class HostRegistry {
         if (s) hipStreamSynchronize(s);
         for (size_t i = 0; i < state_.size(); ++i)
             if (state_[i].load() == kRegistered) {
-                hipHostUnregister(reinterpret_cast<void*>(seg_[i].a));
+                be_.unreg(reinterpret_cast<void*>(seg_[i].a));
                 state_[i].store(kReleased);
             }
+    }
+
+    // Segments registered now (0 once finish() has returned): every host-buffer entry point
+    // reports this at its copy-out (krk_windows_last_copyout).
+    uint64_t live_segments() const {
+        uint64_t k = 0;
+        for (const auto& s : state_) k += s.load() == kRegistered;
+        return k;
+    }
+    // Whether [p, p + n) touches a page of a segment registered now: a HIP copy whose
+    // destination starts in a registered page and runs past it is refused, so no copy-out
+    // may target one.
+    bool overlaps_live(const void* p, uint64_t n) const {
+        if (!n) return false;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(kPage - 1), b = reinterpret_cast<uintptr_t>(p) + n;
+        for (size_t i = 0; i < seg_.size(); ++i)
+            if (state_[i].load() == kRegistered && seg_[i].a < b && a < seg_[i].b) return true;
+        return false;
     }
 
     uint64_t registered_bytes() const { return reg_bytes_.load(); }
@@ -151,6 +178,7 @@ class HostRegistry {
         uintptr_t a, b;
         int first = -1, last = -1;  // windows that first / last read the segment
     };
+    RegBackend be_;
     std::vector<Seg> seg_;
     std::vector<uint32_t> order_;       // registration order (first-need window)
     std::vector<size_t> need_count_;    // need_count_[w + 1]: segments windows 0..w need
@@ -182,12 +210,12 @@ class HostRegistry {
             const Seg& s = seg_[order_[q]];
             const auto t0 = std::chrono::steady_clock::now();
             void* p = reinterpret_cast<void*>(s.a);
-            hipError_t e = hipHostRegister(p, s.b - s.a, hipHostRegisterMapped);
+            hipError_t e = be_.reg(p, s.b - s.a, hipHostRegisterMapped);
             bool ok = e == hipSuccess;
             if (ok) {
                 void* d = nullptr;  // the gather reads the host address itself
-                ok = hipHostGetDevicePointer(&d, p, 0) == hipSuccess && d == p;
-                if (!ok) hipHostUnregister(p);
+                ok = be_.dev_ptr(&d, p, 0) == hipSuccess && d == p;
+                if (!ok) be_.unreg(p);
             } else {
                 (void)hipGetLastError();  // a refused range: staged instead, not an error of the call
             }

@@ -541,9 +541,9 @@ static int piece_sums_host_gpu(Device* D, const krk_blob* blobs, uint64_t n_blob
     ItemBuilder B;
     int k = 0;
     uint64_t bi = 0, boff = 0;
-    uint64_t first = 0;
-    while (first < n_blobs && !blobs[first].length) ++first;
-    const bool gather_ok = direct && first < n_blobs && mapped_at_host_address(blobs[first].data);
+    bool gather_ok = direct;  // every blob read at its host address
+    MappedAtHost mapped;
+    for (uint64_t i = 0; gather_ok && i < n_blobs; ++i) gather_ok = mapped(blobs[i].data, blobs[i].length);
     while (!r && bi < n_blobs) {
         r = pl.acquire(k);
         if (r) break;
@@ -1520,6 +1520,7 @@ struct OwnerTable {
     hipEvent_t ready = nullptr;
     std::vector<std::pair<hipStream_t, hipEvent_t>> used;
     uint64_t stamp = 0;
+    int inflight = 0;  // callers between owner_table() and owner_used(): not evictable
 };
 struct OwnerTables {
     std::vector<OwnerTable> e;
@@ -1553,12 +1554,17 @@ static void owner_release(Device* D, OwnerTable& t, hipStream_t s) {
     if (t.tl) scratch_free(D, t.tl, s);
     if (t.tc) scratch_free(D, t.tc, s);
     if (t.tp) scratch_free(D, t.tp, s);
+    const int inflight = t.inflight;
     t = OwnerTable{};
+    t.inflight = inflight;
 }
 
 // Device pointers of the owner table of (nodes, healthy, max_replica), usable on stream s
 // once the call returns (s waits for its build); the caller's use is recorded after its
-// launch with owner_used().
+// launch with owner_used(), which every successful call must be followed by.  Slots are
+// stable: a failed build leaves its slot empty instead of erasing it, and a slot
+// with a caller between the two calls is never evicted (the cache grows past kOwnerTables
+// rather than release a table a launch is about to read).
 static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy, int32_t max_replica,
                        uint32_t row_out, int32_t** d_tl, uint8_t** d_tc, uint32_t** d_tp, size_t* slot,
                        hipStream_t s) {
@@ -1570,6 +1576,7 @@ static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy
         if (C.e[i].key == key) {
             KRK_HIP(hipStreamWaitEvent(s, C.e[i].ready, 0));
             C.e[i].stamp = ++C.clock;
+            C.e[i].inflight++;
             *d_tl = C.e[i].tl;
             *d_tc = C.e[i].tc;
             *d_tp = C.e[i].tp;
@@ -1577,14 +1584,17 @@ static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy
             return KRK_OK;
         }
     size_t i = C.e.size();
-    if (i >= kOwnerTables) {  // the least recently used one goes
-        i = 0;
-        for (size_t j = 1; j < C.e.size(); ++j)
-            if (C.e[j].stamp < C.e[i].stamp) i = j;
-        owner_release(D, C.e[i], s);
-    } else {
-        C.e.emplace_back();
+    for (size_t j = 0; j < C.e.size(); ++j)  // an empty slot (a failed build) first
+        if (C.e[j].key.empty() && !C.e[j].inflight) {
+            i = j;
+            break;
+        }
+    if (i == C.e.size() && C.e.size() >= kOwnerTables) {  // else the least recently used idle one goes
+        for (size_t j = 0; j < C.e.size(); ++j)
+            if (!C.e[j].inflight && (i == C.e.size() || C.e[j].stamp < C.e[i].stamp)) i = j;
+        if (i < C.e.size()) owner_release(D, C.e[i], s);
     }
+    if (i == C.e.size()) C.e.emplace_back();
     OwnerTable& t = C.e[i];
     int r = shard_owner_table(D, nodes, healthy, max_replica, row_out, &t.tl, &t.tc, s);
     if (!r && nodes->n_nodes <= 255 && row_out <= 3 &&
@@ -1599,12 +1609,12 @@ static int owner_table(Device* D, const krk_nodes* nodes, const uint8_t* healthy
         r = KRK_EHIP;
     }
     if (r) {
-        owner_release(D, t, s);
-        C.e.erase(C.e.begin() + (long)i);
+        owner_release(D, t, s);  // the slot stays, empty (key cleared), for the next build
         return r;
     }
     t.key = std::move(key);
     t.stamp = ++C.clock;
+    t.inflight++;
     *d_tl = t.tl;
     *d_tc = t.tc;
     *d_tp = t.tp;
@@ -1623,6 +1633,7 @@ void krk::owner_tables_teardown(Device& D) {
 static void owner_used(Device* D, size_t slot, hipStream_t s) {
     std::lock_guard<std::mutex> g(D->owners_mu);
     OwnerTable& t = D->owners->e[slot];
+    t.inflight--;
     for (auto& u : t.used)
         if (u.first == s) {
             hipEventRecord(u.second, s);
@@ -1648,7 +1659,10 @@ static bool device_writable(const void* p, uint64_t n) {
             (void)hipGetLastError();
             return false;
         }
-        if (a.type == hipMemoryTypeDevice) return true;
+        // device memory, managed / unified memory, or page-locked host memory
+        // the GPU maps at its host address
+        if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.type == hipMemoryTypeUnified)
+            return true;
         return a.type == hipMemoryTypeHost && a.devicePointer == q;
     };
     return ok_at(p) && (n <= 1 || ok_at(static_cast<const uint8_t*>(p) + n - 1));
@@ -1811,6 +1825,16 @@ bool lib_pinned_range(const void* p, uint64_t n) {
     if (it == g_host_ranges.begin()) return false;
     --it;
     return a >= it->first && a + n <= it->first + it->second;
+}
+bool lib_pinned_block(const void* p, uint64_t n, uintptr_t* base) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(g_host_mu);
+    auto it = g_host_ranges.upper_bound(a);
+    if (it == g_host_ranges.begin()) return false;
+    --it;
+    if (a < it->first || a + n > it->first + it->second) return false;
+    *base = it->first;
+    return true;
 }
 }  // namespace krk
 }

@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <cstring>
+#include <unordered_map>
 
 #include "runtime.hpp"
 
@@ -259,6 +260,30 @@ inline bool mapped_at_host_address(const void* p) {
     }
     return a.devicePointer == p;
 }
+
+// The live krk_host_alloc block holding [p, p + n): its base in *base (runtime.cpp).
+bool lib_pinned_block(const void* p, uint64_t n, uintptr_t* base);
+
+// Whether the gather may read EVERY blob of a batch at its host address (the
+// first blob alone was checked, and a batch mixing krk_host_alloc blocks with other
+// page-locked mappings whose device address differs would have faulted the gather).  A
+// krk_host_alloc block is queried once per call; other memory at both ends of each blob.
+class MappedAtHost {
+  public:
+    bool operator()(const void* p, uint64_t n) {
+        if (!n) return true;
+        uintptr_t base = 0;
+        if (lib_pinned_block(p, n, &base)) {
+            auto it = blocks_.find(base);
+            if (it == blocks_.end()) it = blocks_.emplace(base, mapped_at_host_address(reinterpret_cast<void*>(base))).first;
+            return it->second;
+        }
+        return mapped_at_host_address(p) && (n == 1 || mapped_at_host_address(static_cast<const uint8_t*>(p) + n - 1));
+    }
+
+  private:
+    std::unordered_map<uintptr_t, bool> blocks_;
+};
 
 // Host -> pinned staging copies of one window, split over the calling thread and the host
 // pool's idle threads (one host thread's memcpy is well below the PCIe rate).

@@ -266,6 +266,7 @@ struct CallStats {
     double loop_s = 0, acquire_s = 0, fill_s = 0, enqueue_s = 0;
     double resident = -1;  // file batches: the page-cache resident share of the sampled files
     bool direct_reads = false;  // file batches: read with O_DIRECT
+    uint64_t live_at_copyout = 0;  // registry segments still registered when the results were copied out
 };
 thread_local CallStats t_last_call;
 
@@ -516,7 +517,10 @@ void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std
         if (f.pinned && !host_pinned(blobs[i].data, blobs[i].length)) f.pinned = false;
     }
     if (first == n) return;
-    f.mapped = f.pinned && gm != 0 && mapped_at_host_address(blobs[first].data);
+    f.mapped = f.pinned && gm != 0;  // every windowed blob at its host address
+    MappedAtHost at_host;
+    for (uint64_t i = first; f.mapped && i < n; ++i)
+        if (!on_host[i]) f.mapped = at_host(blobs[i].data, blobs[i].length);
     if (!f.pinned && gm == 1) {
         std::vector<std::pair<uintptr_t, uintptr_t>> ranges;
         for (uint64_t i = 0; i < n; ++i)
@@ -529,19 +533,26 @@ void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std
     }
 }
 
-// A call's results to the caller's host memory.  `bounce`: through a private pageable
-// buffer -- the call registered pages of the caller's memory (KRK_HOST_GATHER=1), and a
-// HIP copy whose destination starts in a registered page and runs past it is refused.
-int copy_out(void* dst, const void* src_dev, size_t n, bool bounce, const char* what) {
+// Every host-buffer entry point, once its streams have drained and before any copy-out: the
+// registry's helpers stopped and every caller range it registered released.  A HIP copy whose
+// destination starts in a registered page and runs past it is refused ("copy-out failed:
+// invalid argument"): the registry rounds each blob out to whole pages,
+// so with the last windows' segments still registered an output array -- or any heap buffer
+// -- sharing a page with a small blob was such a destination.  The count left registered is
+// kept for krk_windows_last_copyout (0 by construction).
+void release_caller_pages(MemFiller& f, CallStats* st) {
+    if (!f.reg) return;
+    f.reg->finish(f.gather_stream);
+    st->live_at_copyout = f.reg->live_segments();
+}
+
+// A call's results to the caller's host memory, refused (not attempted) while the call still
+// holds a registration touching the destination's pages.
+int copy_out(void* dst, const void* src_dev, size_t n, const HostRegistry* reg, const char* what) {
     if (!n) return KRK_OK;
-    hipError_t e;
-    if (bounce) {
-        std::vector<uint8_t> b(n);
-        e = hipMemcpy(b.data(), src_dev, n, hipMemcpyDeviceToHost);
-        if (e == hipSuccess) memcpy(dst, b.data(), n);
-    } else {
-        e = hipMemcpy(dst, src_dev, n, hipMemcpyDeviceToHost);
-    }
+    KRK_CHECK(!reg || !reg->overlaps_live(dst, n), KRK_EINVAL,
+              "%s copy-out: destination shares a page the call still holds registered", what);
+    const hipError_t e = hipMemcpy(dst, src_dev, n, hipMemcpyDeviceToHost);
     KRK_CHECK(e == hipSuccess, KRK_EHIP, "%s copy-out failed: %s", what, hipGetErrorString(e));
     return KRK_OK;
 }
@@ -695,16 +706,9 @@ int krk_metainfo_digest_host(const krk_blob* blobs, uint64_t n, uint32_t* sums_h
         set_error(KRK_EHIP, "metainfo_digest_host: sync failed");
         r = KRK_EHIP;
     }
-    const bool bounce = filler.reg != nullptr;
-    // The registry's helper threads may still be registering caller ranges (pages that can
-    // hold the output arrays or the bounce buffer): stop them and unregister before any
-    // copy-out -- every gather has drained with the streams above.
-    if (filler.reg) {
-        filler.reg->finish(filler.gather_stream);
-        filler.reg.reset();
-    }
-    if (!r) r = copy_out(digests_host, o.d_dig, n * 32, bounce, "digest");
-    if (!r && hi > lo) r = copy_out(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, bounce, "sums");
+    release_caller_pages(filler, &st);
+    if (!r) r = copy_out(digests_host, o.d_dig, n * 32, filler.reg.get(), "digest");
+    if (!r && hi > lo) r = copy_out(sums_host + lo, o.d_sums + lo, (hi - lo) * 4, filler.reg.get(), "sums");
     if (host_th.joinable()) host_th.join();
     for (size_t q = 0; !r && q < host.size(); ++q) {
         memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
@@ -773,7 +777,8 @@ int krk_sha256_host(const uint8_t* const* data_host, const uint64_t* lengths, ui
         set_error(KRK_EHIP, "sha256_host: sync failed");
         r = KRK_EHIP;
     }
-    if (!r) r = copy_out(digests_host, d_dig, n * 32, filler.reg != nullptr, "digest");
+    release_caller_pages(filler, &st);
+    if (!r) r = copy_out(digests_host, d_dig, n * 32, filler.reg.get(), "digest");
     if (host_th.joinable()) host_th.join();
     for (size_t q = 0; !r && q < host.size(); ++q) memcpy(digests_host + 32 * (size_t)host[q], &host_dig[32 * q], 32);
     st.host_blobs = host.size();
@@ -931,6 +936,12 @@ int krk_windows_last_call(uint64_t* max_live, int* windows, uint64_t* host_blobs
     if (max_live) *max_live = t_last_call.max_live;
     if (windows) *windows = t_last_call.windows;
     if (host_blobs) *host_blobs = t_last_call.host_blobs;
+    return KRK_OK;
+}
+
+int krk_windows_last_copyout(uint64_t* live_registered) {
+    KRK_CHECK(live_registered, KRK_EINVAL, "live_registered is NULL");
+    *live_registered = t_last_call.live_at_copyout;
     return KRK_OK;
 }
 

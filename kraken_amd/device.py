@@ -448,7 +448,9 @@ def windows_last_call() -> dict:
     ph = [C.c_double() for _ in range(5)]
     dr = C.c_int()
     check(lib.krk_windows_last_phases(*[C.byref(x) for x in ph], C.byref(dr)))
-    return {"max_live": m.value, "windows": w.value, "host_blobs": h.value, "direct_windows": d.value,
+    lc = C.c_uint64()
+    check(lib.krk_windows_last_copyout(C.byref(lc)))
+    return {"live_registered_at_copyout": lc.value, "max_live": m.value, "windows": w.value, "host_blobs": h.value, "direct_windows": d.value,
             "gather_windows": g.value, "registered_bytes": rb.value, "register_s": rs.value,
             "phases_s": dict(zip(("loop", "acquire", "fill", "enqueue"), (round(x.value, 4) for x in ph[:4]))),
             "resident_sample": round(ph[4].value, 4), "direct_reads": bool(dr.value)}

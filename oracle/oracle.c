@@ -567,6 +567,28 @@ uint32_t orc_ring_locations(const int32_t* order, uint32_t n_nodes, const uint8_
     return k;
 }
 
+/* Every ShardID's ring.Locations (lib/hashring/ring.go:96-118 over rendezvous.go:207-217):
+ * key = 4 lowercase hex digits "%04x" of shard (core/digest.go ShardID = hex[:4]); the full
+ * HRW order, then the replica filter -- 65,536 rows of row_out (>= 1) owners, -1 padded,
+ * counts[shard] owners each.  A plain loop over orc_hrw_ordered + orc_ring_locations: the
+ * exhaustive checker of the device owner table (tests/test_gpu_hrw.py). */
+void orc_ring_owner_table(const char* labels, const uint64_t* label_off, const int64_t* weights,
+                          uint32_t n_nodes, const uint8_t* healthy, int32_t max_replica, uint32_t row_out,
+                          int32_t* locs, uint8_t* counts) {
+    int32_t* order = (int32_t*)malloc(sizeof(int32_t) * (n_nodes ? n_nodes : 1));
+    int32_t* out = (int32_t*)malloc(sizeof(int32_t) * (n_nodes ? n_nodes : 1));
+    static const char hx[] = "0123456789abcdef";
+    for (uint32_t shard = 0; shard < 65536; shard++) {
+        char key[4] = {hx[(shard >> 12) & 15], hx[(shard >> 8) & 15], hx[(shard >> 4) & 15], hx[shard & 15]};
+        orc_hrw_ordered(key, 4, labels, label_off, weights, n_nodes, n_nodes, order, NULL);
+        uint32_t k = orc_ring_locations(order, n_nodes, healthy, max_replica, out);
+        counts[shard] = (uint8_t)k;
+        for (uint32_t r = 0; r < row_out; r++) locs[(uint64_t)shard * row_out + r] = r < k ? out[r] : -1;
+    }
+    free(order);
+    free(out);
+}
+
 /* pieceLengthConfig.get -- lib/metainfogen/config.go:71-80 (ranges sorted asc). */
 int64_t orc_piece_length_for_size(const int64_t* thresholds, const int64_t* lengths,
                                   uint32_t n, int64_t size) {

@@ -79,6 +79,11 @@ int orc_hrw_ordered(const char* key_hex, uint64_t key_len, const char* labels,
 uint32_t orc_ring_locations(const int32_t* order, uint32_t n_nodes, const uint8_t* healthy,
                             int32_t max_replica, int32_t* out);
 
+/* Every ShardID's Locations: 65,536 rows of row_out owners (-1 padded) + counts. */
+void orc_ring_owner_table(const char* labels, const uint64_t* label_off, const int64_t* weights,
+                          uint32_t n_nodes, const uint8_t* healthy, int32_t max_replica, uint32_t row_out,
+                          int32_t* locs, uint8_t* counts);
+
 /* ---- lib/metainfogen/config.go:71-80 ---- */
 int64_t orc_piece_length_for_size(const int64_t* thresholds, const int64_t* lengths,
                                   uint32_t n, int64_t size);

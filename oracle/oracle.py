@@ -49,6 +49,8 @@ def _load() -> C.CDLL:
         "orc_hrw_ordered": (C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, u64p, i64p, C.c_uint32,
                                       C.c_uint32, i32p, f64p]),
         "orc_ring_locations": (C.c_uint32, [i32p, C.c_uint32, u8p, C.c_int32, i32p]),
+        "orc_ring_owner_table": (None, [C.c_char_p, u64p, i64p, C.c_uint32, u8p, C.c_int32, C.c_uint32, i32p,
+                                        u8p]),
         "orc_piece_length_for_size": (C.c_int64, [i64p, i64p, C.c_uint32, C.c_int64]),
         "orc_blob_seed": (C.c_uint64, [C.c_uint64]),
         "orc_synth_fill": (None, [C.c_uint64, C.c_uint64, u8p, C.c_uint64, C.c_int]),
@@ -211,6 +213,19 @@ def ring_locations(order, healthy, max_replica: int):
     k = lib().orc_ring_locations(_ptr(o, C.c_int32), len(order), _ptr(h, C.c_uint8), max_replica,
                                  _ptr(out, C.c_int32))
     return out[:k].tolist()
+
+
+def ring_owner_table(labels, weights, healthy, max_replica: int):
+    """Every ShardID's Locations (65,536 rows, -1 padded to max(1, max_replica)) and counts."""
+    blob, off = _labels(labels)
+    w = np.ascontiguousarray(np.asarray(weights, dtype=np.int64))
+    h = np.ascontiguousarray(np.asarray(healthy, dtype=np.uint8))
+    row = max(1, int(max_replica))
+    locs = np.zeros((65536, row), dtype=np.int32)
+    counts = np.zeros(65536, dtype=np.uint8)
+    lib().orc_ring_owner_table(blob, _ptr(off, C.c_uint64), _ptr(w, C.c_int64), len(labels), _ptr(h, C.c_uint8),
+                               int(max_replica), row, _ptr(locs, C.c_int32), _ptr(counts, C.c_uint8))
+    return locs, counts
 
 
 def piece_length_for_size(ranges: dict, size: int) -> int:

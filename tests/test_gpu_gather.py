@@ -133,3 +133,114 @@ def test_gather_default_large_pageable_and_pinned_wide(gpu, orc):
     got = D.piece_sums_host(pd, 1 << 16)
     for i in range(0, 200, 23):
         assert np.array_equal(got[i], orc.calc_piece_sums(pd[i], 1 << 16)[1]), i
+
+
+def test_copyout_shares_page_with_registered_blob(gpu, orc):
+    """under the gather of pageable blobs (KRK_HOST_GATHER=1), a tiny
+    blob and the call's output arrays carved from ONE 4 KiB page of one page-aligned
+    buffer, for both host-buffer entry points (krk_metainfo_digest_host, krk_sha256_host).
+    The registry rounds the blob out to that whole page, so the outputs sit in a page the
+    call registered: every call must release its registrations before the copy-out
+    (windows.cpp release_caller_pages), report none live at it, and be bit-exact."""
+    import ctypes as C
+    import mmap
+
+    PAGE = 4096
+    m = mmap.mmap(-1, 64 * PAGE)
+    buf = np.frombuffer(m, dtype=np.uint8)
+    assert buf.ctypes.data % PAGE == 0
+    P = 1 << 12
+    lens = [200, 3 * PAGE + 17, 20 * PAGE + 5, 1, 0, 9 * PAGE]
+    blobs, o = [], PAGE  # page 0 holds the tiny blob and the outputs; the rest follow it
+    for L in lens[1:]:
+        blobs.append(buf[o:o + L])
+        o += L + 3
+    tiny = buf[64:64 + lens[0]]
+    datas = [tiny] + blobs
+    for k, d in enumerate(datas):
+        d[:] = orc.synth(7000 + k, d.size)
+    n = len(datas)
+    counts = [int(D.lib.krk_num_pieces(int(d.size), P)) for d in datas]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(counts)
+    dg_off, sums_off = 1024, 2048  # both inside page 0, after the tiny blob
+    assert dg_off >= 64 + lens[0] and sums_off >= dg_off + 32 * n and sums_off + 4 * int(offs[-1]) <= PAGE
+    dg = buf[dg_off:dg_off + 32 * n]
+    sums = buf[sums_off:sums_off + 4 * int(offs[-1])].view(np.uint32)
+    arr = (D.krk_blob * n)()
+    for i, d in enumerate(datas):
+        arr[i] = D.krk_blob(d.ctypes.data if d.size else None, int(d.size), P, int(offs[i]))
+    D.set_sha_host_offload(0)
+    D.set_host_gather(1)
+    try:
+        for rep in range(3):
+            dg[:] = 0
+            sums[:] = 0
+            D.check(D.lib.krk_metainfo_digest_host(arr, n, sums.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                   dg.ctypes.data_as(C.POINTER(C.c_uint8))))
+            st = D.windows_last_call()
+            assert st["gather_windows"] == st["windows"] > 0 and st["registered_bytes"] > 0, st
+            assert st["live_registered_at_copyout"] == 0, st
+            for i, d in enumerate(datas):
+                b = d.tobytes()
+                assert bytes(dg[32 * i:32 * i + 32]) == hashlib.sha256(b).digest(), (rep, i)
+                ref = orc.calc_piece_sums(np.frombuffer(b, np.uint8), P)[1]
+                assert np.array_equal(sums[int(offs[i]):int(offs[i + 1])], ref), (rep, i)
+            # the Digester batch: its digests into the same page as the tiny blob
+            ptrs = (C.c_void_p * n)(*[d.ctypes.data if d.size else None for d in datas])
+            L = np.array([d.size for d in datas], np.uint64)
+            dg[:] = 0
+            D.check(D.lib.krk_sha256_host(ptrs, L.ctypes.data_as(C.POINTER(C.c_uint64)), n,
+                                          dg.ctypes.data_as(C.POINTER(C.c_uint8))))
+            st = D.windows_last_call()
+            assert st["gather_windows"] == st["windows"] > 0 and st["live_registered_at_copyout"] == 0, st
+            for i, d in enumerate(datas):
+                assert bytes(dg[32 * i:32 * i + 32]) == hashlib.sha256(d.tobytes()).digest(), (rep, i)
+    finally:
+        D.set_host_gather(-1)
+        D.set_sha_host_offload(-1)
+
+
+def test_gather_mixed_pinned_mappings(gpu, orc):
+    """a batch mixing krk_host_alloc blobs with page-locked memory the caller
+    registered itself (hipHostRegister) -- the gather reads every blob at its host address,
+    so every blob's mapping is checked before a window is gathered (staging.hpp MappedAtHost),
+    not the first blob's alone.  Windows of more than 64 chunks (the gather's domain);
+    bit-exact whichever path each window takes."""
+    import ctypes as C
+    import mmap
+
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+    hip.hipHostUnregister.argtypes = [C.c_void_p]
+    m = mmap.mmap(-1, 32 << 20)
+    buf = np.frombuffer(m, dtype=np.uint8)
+    assert hip.hipHostRegister(buf.ctypes.data, buf.size, 0) == 0
+    try:
+        pins, datas, o = [], [], 0
+        for i in range(160):
+            L = 70_001 + 37 * i
+            if i % 2:
+                pa = D.PinnedArray((L,), np.uint8)
+                pa.a[:] = orc.synth(9000 + i, L)
+                pins.append(pa)
+                datas.append(pa.a)
+            else:
+                v = buf[o + (i % 13):o + (i % 13) + L]
+                v[:] = orc.synth(9000 + i, L)
+                datas.append(v)
+                o += L + 64
+        D.set_sha_host_offload(0)
+        sums, dg = D.metainfo_digest_host(datas, 1 << 16)
+        st = D.windows_last_call()
+        assert st["windows"] > 0 and st["registered_bytes"] == 0, st
+        for i in range(0, len(datas), 7):
+            assert bytes(dg[i]) == hashlib.sha256(datas[i].tobytes()).digest(), i
+            assert np.array_equal(sums[i], orc.calc_piece_sums(datas[i], 1 << 16)[1]), i
+        got = D.piece_sums_host(datas, 1 << 16)
+        for i in range(0, len(datas), 9):
+            assert np.array_equal(got[i], orc.calc_piece_sums(datas[i], 1 << 16)[1]), i
+        print("mixed mappings:", st)
+    finally:
+        D.set_sha_host_offload(-1)
+        hip.hipHostUnregister(buf.ctypes.data)

@@ -373,3 +373,76 @@ def test_ring_locations_into_page_locked_host_memory(gpu, max_replica):
         check(lib.krk_ring_locations_u8_dev(dbuf.ptr, n, C.byref(s), hp, max_replica,
                                              pageable.ctypes.data, c8.ptr, None))
     D.synchronize()
+
+
+@pytest.mark.parametrize("n_nodes", [3, 5, 16, 64])
+def test_owner_table_every_row_matches_oracle(gpu, orc, n_nodes):
+    """the WHOLE C5 output space.  With equal weights Locations depends
+    on the digest only through its 2-byte ShardID (lib/hashring/ring.go:96-118 over
+    lib/hrw/rendezvous.go:207-217), so the 65,536-row owner table is every result a ring can
+    give.  For MaxReplica in {2, 3} and healthy in {all, a seeded 75 %, none}: every row of
+    the device table (krk_ring_owner_table) equals the oracle's (orc_ring_owner_table) --
+    owners, -1 padding and counts -- and 1M random digests gathered on the device (int32 and
+    u8 / packed-row paths) equal the oracle table's row of their ShardID.  No row is sampled."""
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(n_nodes)]
+    rng = np.random.default_rng(0xC5 + n_nodes)
+    n = 1 << 20
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    shard = (digests[:, 0].astype(np.int64) << 8) | digests[:, 1]
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    h75 = (rng.random(n_nodes) < 0.75).astype(np.uint8)
+    h75[rng.integers(0, n_nodes)] = 1
+    for max_replica in (2, 3):
+        for healthy in (np.ones(n_nodes, np.uint8), h75, np.zeros(n_nodes, np.uint8)):
+            want_l, want_c = orc.ring_owner_table(labels, [100] * n_nodes, healthy, max_replica)
+            ring = hashring.Ring(labels, [l for l, h in zip(labels, healthy) if h], max_replica)
+            ring.Refresh()
+            got_l, got_c = ring._table
+            bad = np.nonzero((got_l != want_l).any(axis=1) | (got_c != want_c))[0]
+            assert bad.size == 0, (max_replica, healthy.tolist(), bad[:8], got_l[bad[:4]], want_l[bad[:4]])
+            if not healthy.any() or healthy.all() and max_replica == 3:
+                continue  # the gather legs below: one healthy set per replica count is enough
+            l32, c32 = D.DeviceBuffer(n * max_replica * 4), D.DeviceBuffer(n)
+            l8, c8 = D.DeviceBuffer(n * max_replica), D.DeviceBuffer(n)
+            D.ring_locations_dev(dbuf, n, labels, healthy, max_replica, l32, c32)
+            D.ring_locations_u8_dev(dbuf, n, labels, healthy, max_replica, l8, c8)
+            D.synchronize()
+            a32 = l32.to_host(np.int32, n * max_replica).reshape(n, max_replica)
+            assert np.array_equal(a32, want_l[shard]), (max_replica, healthy.tolist())
+            assert np.array_equal(c32.to_host(np.uint8, n), want_c[shard])
+            a8 = l8.to_host(np.uint8, n * max_replica).reshape(n, max_replica)
+            assert np.array_equal(a8, np.where(want_l < 0, 255, want_l).astype(np.uint8)[shard])
+            assert np.array_equal(c8.to_host(np.uint8, n), want_c[shard])
+
+
+def test_ring_locations_into_managed_memory(gpu):
+    """outputs in managed memory (hipMallocManaged) are device-writable -- the
+    placement kernels write them like device memory -- and give the device outputs' lists."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMallocManaged.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
+    hip.hipFree.argtypes = [C.c_void_p]
+    labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(16)]
+    healthy = np.ones(16, dtype=np.uint8)
+    n, R = 10007, 3
+    rng = np.random.default_rng(42)
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    l8, c8 = D.DeviceBuffer(n * R), D.DeviceBuffer(n)
+    D.ring_locations_u8_dev(dbuf, n, labels, healthy, R, l8, c8)
+    D.synchronize()
+    ml, mc = C.c_void_p(), C.c_void_p()
+    assert hip.hipMallocManaged(C.byref(ml), n * R, 1) == 0 and hip.hipMallocManaged(C.byref(mc), n, 1) == 0
+    try:
+        s, keep = D.nodes_struct(labels, [100] * 16)
+        check(lib.krk_ring_locations_u8_dev(dbuf.ptr, n, C.byref(s), healthy.ctypes.data_as(C.POINTER(C.c_uint8)), R,
+                                             ml.value, mc.value, None))
+        D.synchronize()
+        got_l = np.ctypeslib.as_array((C.c_uint8 * (n * R)).from_address(ml.value)).copy()
+        got_c = np.ctypeslib.as_array((C.c_uint8 * n).from_address(mc.value)).copy()
+        assert np.array_equal(got_l, l8.to_host(np.uint8, n * R)) and np.array_equal(got_c, c8.to_host(np.uint8, n))
+    finally:
+        hip.hipFree(ml)
+        hip.hipFree(mc)

@@ -186,3 +186,25 @@ def test_baseline_files_matches_zlib(orc, tmp_path):
     _, sums2, _, dg = orc.baseline_files(paths, [len(x) for x in datas], P, 2, passes=3)
     assert np.array_equal(sums2, sums)
     assert [bytes(d) for d in dg] == [hashlib.sha256(x).digest() for x in datas]
+
+
+def test_oracle_owner_table_is_the_per_key_oracle():
+    """orc_ring_owner_table (the exhaustive checker of the device owner tables) is the
+    per-key restatement looped over all 65,536 ShardIDs: rows sampled against
+    orc_hrw_ordered + orc_ring_locations, and SURVEY.md 8(c)'s sanity vector (labels
+    dummy-origin-master0{1,2,3}-zone2:80: e3b0 -> 03, 02, 01; 0000 and ffff -> 01, 03, 02)."""
+    import numpy as np
+
+    from oracle import oracle as O
+    labels = [f"dummy-origin-master0{i}-zone2:80" for i in (1, 2, 3)]
+    locs, counts = O.ring_owner_table(labels, [100] * 3, np.ones(3, np.uint8), 3)
+    assert locs[0xE3B0].tolist() == [2, 1, 0] and locs[0].tolist() == [0, 2, 1] and locs[0xFFFF].tolist() == [0, 2, 1]
+    assert (counts == 3).all()
+    rng = np.random.default_rng(5)
+    for N, R in ((5, 2), (16, 3)):
+        labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(N)]
+        healthy = (rng.random(N) < 0.75).astype(np.uint8)
+        locs, counts = O.ring_owner_table(labels, [100] * N, healthy, R)
+        for shard in list(range(0, 65536, 1021)) + [65535]:
+            ref = O.ring_locations(O.hrw_ordered(f"{shard:04x}", labels, [100] * N), healthy, R)
+            assert locs[shard, :counts[shard]].tolist() == ref and (locs[shard, counts[shard]:] == -1).all()
