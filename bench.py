@@ -1335,6 +1335,8 @@ def run_chunked(a, D, T, rank, world, res):
     wr.close()
     if a.host_lane:
         res["host_offload"] = run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums)
+    if a.tail_handoff:
+        res["tail_handoff"] = run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums)
     if not a.no_e2e:
         res["end_to_end"] = c3_end_to_end(D, T, world, rank)
 
@@ -1377,6 +1379,49 @@ def run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums):
     out.update({"value": round(total_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el * 1e3, 3),
                 "host_bytes": int(sum(lens[i] for i in wr.lane_blobs)), "lane_s": round(wr.lane_seconds, 3),
                 "windows": len(wr.wins),
+                "matches_gpu_only": bool(np.array_equal(dg2, dg) and np.array_equal(s2, sums))})
+    return out
+
+
+def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
+    """C3 with the tail handoff (kraken_amd.windowed.TailHandoffRun): every chain starts in
+    the windows (the threads start on the longest ones whole) and host threads steal the
+    chains with the most bytes left at window boundaries, from the midstates in HBM; the
+    stolen chains' remaining piece CRCs stay on the GPU.  GPU + host throughput, reported
+    beside the GPU-only value (never as it), with the same policy modelled on the planner's
+    rates (windowed.simulate_tail_handoff) and the outputs compared with the GPU-only run's."""
+    from kraken_amd.windowed import TAIL_CHUNK, TailHandoffRun, simulate_tail_handoff, window_stream_cap
+    threads = max(1, host_cores() - 1)  # one core stays with the window loop
+    cap = len(lens) if a.no_admission else (a.live_cap or window_stream_cap(D, len(lens)))
+    live = min(cap, len(lens))
+    # windows of <= 4 MiB a live chain (a ~70 ms SHA launch at eight lanes): a chain is handed
+    # over at a window boundary, so short windows keep the threads from waiting on one
+    W = int(min(a.window_gib << 30, live * TAIL_CHUNK))
+    rates = D.planner_rates()
+    model = simulate_tail_handoff(lens, W, cap, threads, rates, max_chunk=TAIL_CHUNK)
+    out = {"threads": threads, "window_bytes": W, "live_cap": int(cap),
+           "model": {"end_s": round(model["end_s"], 3), "gpu_windows_end_s": round(model["gpu_end_s"], 3),
+                     "host_bytes": int(model["host_bytes"]), "takeovers": int(model["takeovers"]),
+                     "value_GBps": round(total_bytes / model["end_s"] / 1e9, 3),
+                     "thread_rate_GBps": round(model["thread_rate_Bps"] / 1e9, 3)},
+           "planner_rates": {"sha_stream_MBps": [round(x / 1e6, 2) for x in rates["sha_stream_bps"]],
+                             "host_sha_GBps_per_thread": round(rates["host_sha_bps"] / 1e9, 3),
+                             "d2h_GBps": round(rates["d2h_bps"] / 1e9, 2), "source": rates["source"]},
+           "what": "GPU + host: host threads (SHA-NI) steal the chains with the most bytes left at window "
+                   "boundaries from the windows' midstates in HBM; piece CRCs all on the GPU"}
+    tr = TailHandoffRun(D, ids, lens, P, W, threads, cap=cap if (a.no_admission or a.live_cap) else None,
+                        device=a.device)
+    T.barrier()
+    t0 = time.perf_counter()
+    tr.run()
+    T.barrier()
+    el = T.max_over_ranks(time.perf_counter() - t0)
+    n = len(lens)
+    dg2 = tr.cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
+    s2 = tr.cb.sums.to_host(np.uint32, max(tr.cb.total_pieces, 1))
+    tr.close()
+    out.update({"value": round(total_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el * 1e3, 3),
+                "measured_over_model": round(el / model["end_s"], 4), **tr.stats,
                 "matches_gpu_only": bool(np.array_equal(dg2, dg) and np.array_equal(s2, sums))})
     return out
 
@@ -2213,6 +2258,9 @@ def main():
                     help="C3: also run the batch with the host lane (the longest blobs hashed on host threads "
                          "while the windows run the rest), reported as host_offload beside the GPU-only value")
     ap.add_argument("--host-lane-k", type=int, default=-1, help="C3: blobs the host lane takes (-1 = the planner's)")
+    ap.add_argument("--tail-handoff", action="store_true",
+                    help="C3: also run the batch with the tail handoff (host threads steal the chains with the most "
+                         "bytes left at window boundaries), reported as tail_handoff beside the GPU-only value")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
     ap.add_argument("--regen-serial", action="store_true",
                     help="c5regen: piece sums then InfoHashes (no krk_metainfo_batch_dev pipelining)")

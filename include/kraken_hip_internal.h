@@ -51,7 +51,24 @@ int krk_window_sched_new(const uint64_t* lengths, uint64_t n, uint64_t window_by
                          krk_window_sched** out);
 int krk_window_sched_next(krk_window_sched* s, uint32_t* blobs, uint64_t* offsets, uint64_t* lengths, uint64_t cap,
                           uint64_t* n_out);
+/* Take blob `blob` out of the schedule (a host thread continues its chain: the windowed tail
+ * handoff); *offset = the bytes the windows gave it (0 if it was still waiting).  A live
+ * blob's place goes to the next waiting blob at the next window.  KRK_EINVAL if it is
+ * neither live nor waiting. */
+int krk_window_sched_drop(krk_window_sched* s, uint32_t blob, uint64_t* offset);
+/* At most max_chunk bytes (>= 64) a chunk from the next window on: windows stay short once
+ * few blobs are live. */
+int krk_window_sched_set_chunk_cap(krk_window_sched* s, uint64_t max_chunk);
 void krk_window_sched_free(krk_window_sched* s);
+/* The piece CRCs of device chunks without SHA-256 (XOR-accumulated into sums_dev like a
+ * window's): the tails of chains a host thread hashes.  Asynchronous on `stream`. */
+int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, void* stream);
+/* Continue one SHA-256 chain on the calling thread from n device bytes at data_dev (after
+ * the work queued on `stream`): state8 holds the midstate after `absorbed` bytes (a multiple
+ * of 64) and is updated; final != 0 pads and writes the digest to digest32 (n may then be
+ * any length).  Read through pinned double buffers, x86 SHA extensions.  Synchronous. */
+int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uint8_t* data_dev, uint64_t n,
+                                  int final, uint8_t* digest32, void* stream);
 /* The live-stream cap of the windows on the calling thread's device: 7/8 of the largest
  * stream count whose SHA-256 launch runs more than one lane a stream (14,336 on 256 CUs),
  * so each window's CRC launch has the CUs the SHA workgroups leave free.  KRK_LIVE_CAP

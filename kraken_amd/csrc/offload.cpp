@@ -676,6 +676,74 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     return KRK_OK;
 }
 
+// One chain continued on the calling thread from device bytes (krk_sha256_resume_dev_on_host):
+// a worker (two pinned buffers + streams) of the device's pool, D2H double-buffered in
+// kOffChunk pieces, SHA-NI over each while the next comes down.
+static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uint8_t* src, uint64_t L, bool final,
+                          uint8_t* digest, hipEvent_t ready) {
+    OffloadPool& P = *pool_of(D);
+    std::vector<Worker> set;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        for (auto& fs : P.free_sets)  // a set with a spare worker: take one
+            if (!fs.empty()) {
+                set.push_back(fs.back());
+                fs.pop_back();
+                break;
+            }
+    }
+    if (set.empty()) {
+        Worker w;
+        for (int b = 0; b < 2; ++b) {
+            if (hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking) != hipSuccess ||
+                hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault) != hipSuccess) {
+                for (int c = 0; c <= b; ++c) {
+                    if (w.s[c]) hipStreamDestroy(w.s[c]);
+                    if (w.buf[c]) hipHostFree(w.buf[c]);
+                }
+                KRK_CHECK(false, KRK_ENOMEM, "sha256 resume: pinned buffers / streams");
+            }
+        }
+        set.push_back(w);
+    }
+    struct Return {
+        OffloadPool& P;
+        std::vector<Worker>& set;
+        ~Return() {
+            std::lock_guard<std::mutex> g(P.mu);
+            P.free_sets.push_back(std::move(set));
+        }
+    } give_back{P, set};
+    Worker& W = set[0];
+    KRK_HIP(hipEventSynchronize(ready));
+    const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
+    auto issue = [&](uint64_t c) {
+        const uint64_t o = c * kOffChunk, m = std::min(kOffChunk, L - o);
+        return m == 0 || hipMemcpyAsync(W.buf[c & 1], src + o, m, hipMemcpyDeviceToHost, W.s[c & 1]) == hipSuccess;
+    };
+    bool ok = issue(0);
+    for (uint64_t c = 0; ok && c < nch; ++c) {
+        if (c + 1 < nch) ok = issue(c + 1);
+        if (!ok || hipStreamSynchronize(W.s[c & 1]) != hipSuccess) {
+            ok = false;
+            break;
+        }
+        const uint64_t m = std::min(kOffChunk, L - c * kOffChunk);
+        if (c + 1 < nch || !final) {
+            host_sha256_blocks(h, W.buf[c & 1], m / 64);
+            absorbed += m;
+        } else {
+            host_sha256_final(h, absorbed, W.buf[c & 1], m, digest);
+        }
+    }
+    if (!ok) {
+        hipStreamSynchronize(W.s[0]);
+        hipStreamSynchronize(W.s[1]);
+    }
+    KRK_CHECK(ok, KRK_EHIP, "sha256 resume: device-to-host copy failed");
+    return KRK_OK;
+}
+
 void offload_teardown(Device& D) {  // krk_shutdown: no offload phase is running (contract)
     OffloadPool* P = D.offload;
     if (!P) return;
@@ -930,6 +998,26 @@ int krk_planner_rates_set(const krk_planner_rates* in) {
     g_rates_override = R;
     g_rates_set = true;
     return KRK_OK;
+}
+
+int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uint8_t* data_dev, uint64_t n,
+                                  int final, uint8_t* digest32, void* stream) {
+    KRK_CHECK(state8, KRK_EINVAL, "sha256_resume: state is NULL");
+    KRK_CHECK(n == 0 || data_dev, KRK_EINVAL, "sha256_resume: data is NULL");
+    KRK_CHECK(absorbed % 64 == 0, KRK_EINVAL, "sha256_resume: absorbed bytes not a multiple of 64");
+    KRK_CHECK(final || n % 64 == 0, KRK_EINVAL, "sha256_resume: a non-final run must be whole 64-byte blocks");
+    KRK_CHECK(!final || digest32, KRK_EINVAL, "sha256_resume: digest is NULL");
+    KRK_DEVICE(D);
+    hipEvent_t ready;
+    KRK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    int r = KRK_OK;
+    if (hipEventRecord(ready, pick(D, stream)) != hipSuccess) {
+        set_error(KRK_EHIP, "sha256_resume: event record failed");
+        r = KRK_EHIP;
+    }
+    if (!r) r = resume_on_host(D, state8, absorbed, data_dev, n, final != 0, digest32, ready);
+    hipEventDestroy(ready);
+    return r;
 }
 
 int krk_sha_tail_plan(const uint64_t* lengths, uint64_t n, int threads, uint32_t* host_idx, uint64_t* start,

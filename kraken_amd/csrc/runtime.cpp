@@ -1210,6 +1210,24 @@ int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n, uint3
                        static_cast<hipStream_t>(sha_stream));
 }
 
+// The piece CRCs of device chunks alone (no SHA-256): the tail bytes of chains whose
+// SHA-256 a host thread finishes (the windowed tail handoff, kraken_amd/windowed.py) still
+// get their piece sums on the GPU, XOR-accumulated like a window's.
+int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, void* stream) {
+    KRK_DEVICE(D);
+    int r = validate_chunks(chunks, n);
+    if (r || !n) return r;
+    KRK_CHECK(sums_dev, KRK_EINVAL, "chunks_crc_dev: sums_dev is NULL");
+    ItemBuilder B;
+    CrcBatch items;
+    for (uint64_t i = 0; i < n; ++i)
+        if (chunks[i].length)
+            B.add(items, reinterpret_cast<uint64_t>(chunks[i].data), chunks[i].offset,
+                  chunks[i].offset + chunks[i].length, chunks[i].blob_length, (uint64_t)chunks[i].piece_length,
+                  chunks[i].sums_offset);
+    return run_items(D, items, sums_dev, pick(D, stream));
+}
+
 // krk_metainfo_digest_host: windows.cpp
 
 int krk_verify_pieces_dev(const krk_blob* blob, const uint32_t* expected_host, uint8_t* ok_out_host, void* stream) {

@@ -49,7 +49,7 @@ class WindowSched {
         while (live_.size() < cap_ && q_ < queue_.size()) live_.push_back({queue_[q_++], 0});
         if (live_.empty()) return false;
         max_live_ = std::max<uint64_t>(max_live_, live_.size());
-        const uint64_t c = std::max(align_, W_ / live_.size() / align_ * align_);
+        const uint64_t c = std::max(align_, std::min(max_chunk_, W_ / live_.size()) / align_ * align_);
         size_t keep = 0;
         for (size_t k = 0; k < live_.size(); ++k) {
             auto [b, pos] = live_[k];
@@ -62,6 +62,27 @@ class WindowSched {
         return true;
     }
     uint64_t max_live() const { return max_live_; }
+    // At most `c` bytes a chunk (rounded down to the alignment): the windows stay short once
+    // few blobs are live (the tail handoff hands chains over at window boundaries).
+    void set_max_chunk(uint64_t c) { max_chunk_ = std::max<uint64_t>(c, 1); }
+    // Take blob b out of the schedule (its chain continues elsewhere): a live blob's slot goes
+    // to the next waiting blob at the next window; a waiting one is never admitted.  *done:
+    // the bytes the windows gave it (0 for a waiting blob).
+    bool drop(uint32_t b, uint64_t* done) {
+        for (size_t k = 0; k < live_.size(); ++k)
+            if (live_[k].first == b) {
+                *done = live_[k].second;
+                live_.erase(live_.begin() + (long)k);
+                return true;
+            }
+        for (size_t k = q_; k < queue_.size(); ++k)
+            if (queue_[k] == b) {
+                *done = 0;
+                queue_.erase(queue_.begin() + (long)k);
+                return true;
+            }
+        return false;
+    }
 
   private:
     const uint64_t* L_;
@@ -70,6 +91,7 @@ class WindowSched {
     size_t q_ = 0;
     std::vector<std::pair<uint32_t, uint64_t>> live_;  // blob, bytes done
     uint64_t max_live_ = 0;
+    uint64_t max_chunk_ = UINT64_MAX;
 };
 
 // Live streams per window on device D: 7/8 of the largest stream count whose SHA-256 launch
@@ -631,6 +653,18 @@ int krk_window_sched_next(krk_window_sched* w, uint32_t* blobs, uint64_t* offset
         if (offsets) offsets[k] = w->win[k].off;
         if (lengths) lengths[k] = w->win[k].len;
     }
+    return KRK_OK;
+}
+
+int krk_window_sched_drop(krk_window_sched* w, uint32_t blob, uint64_t* offset) {
+    KRK_CHECK(w && offset, KRK_EINVAL, "window_sched_drop: null argument");
+    KRK_CHECK(w->s->drop(blob, offset), KRK_EINVAL, "window_sched_drop: blob %u is neither live nor waiting", blob);
+    return KRK_OK;
+}
+
+int krk_window_sched_set_chunk_cap(krk_window_sched* w, uint64_t max_chunk) {
+    KRK_CHECK(w && max_chunk >= 64, KRK_EINVAL, "window_sched_set_chunk_cap: null schedule or cap < 64");
+    w->s->set_max_chunk(max_chunk);
     return KRK_OK;
 }
 

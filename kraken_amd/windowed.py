@@ -327,3 +327,403 @@ class WindowedRun:
             self.close()
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------------------------------
+# Tail handoff of the windowed chains.  A windowed batch whose longest
+# chain outlasts the GPU's aggregate work -- every shard of an 8-GPU C3, whose 1.07 GB blob
+# takes ~18 s at ~58 MB/s a stream while the shard's 1.47 TB would take ~2 s -- ends when
+# that chain ends.  Host threads (SHA-NI, ~2.3 GB/s, 40x a GPU stream) steal chains instead:
+# at each window boundary every thread that will be free before the next window ends takes
+# the chain with the most bytes left (earliest deadline first, as offload.cpp tail_plan does
+# for batches in HBM), from the midstate the windows keep in HBM (ChunkedBatch.state); the
+# chain leaves the window schedule (krk_window_sched_drop), its remaining bytes are
+# generated on the device in 64 MiB pieces, their piece CRCs run on the GPU
+# (krk_chunks_crc_dev, XOR-accumulated into the same sums), and the thread hashes them out
+# of HBM (krk_sha256_resume_dev_on_host).  The threads start on the longest chains whole.
+# The same policy is simulated on the planner's rates (simulate_tail_handoff): the bench
+# reports that model beside the measured run.
+
+_IV = np.array([0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19],
+               dtype=np.uint32)
+TAIL_PIECE = 64 << 20  # device bytes a tail thread generates, CRCs and hashes at a time
+# Window chunk cap of the tail handoff: ~70 ms of a chain at eight lanes a window, so a
+# chain is handed over within a short window of a thread becoming free, however few chains
+# are left live (modelled on rank 0's shard of an 8-GPU C3: 1/2/4/8 MiB end at 11.7 / 11.7
+# / 12.0 / 12.7 s with 0.5 ms a launch, 12.7 / 12.2 / 12.3 / 12.9 s with 3 ms).
+TAIL_CHUNK = 4 << 20
+
+
+def tail_thread_rate(rates, threads):
+    """One tail thread's bytes/s: its SHA-NI rate (the planner's figure is derated 15 % for a
+    loaded socket; a tail thread alone on its buffers loses ~2 %, offload.cpp tail_plan),
+    capped by its share of the device-to-host copy rate."""
+    return min(rates["host_sha_bps"] * (0.98 / 0.85), rates["d2h_bps"] / max(1, int(threads)))
+
+
+class _Sched:
+    """krk_window_sched over a subset of the batch (indices into the full batch)."""
+
+    def __init__(self, lens, idx, W, cap, max_chunk=0):
+        from ._capi import check, lib
+        self.check, self.lib = check, lib
+        self.idx = np.asarray(idx, dtype=np.int64)
+        self.pos = {}
+        L = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64)[self.idx])
+        self.cap = max(1, min(int(cap), max(1, L.size)))
+        self.h = C.c_void_p()
+        if L.size:
+            check(lib.krk_window_sched_new(L.ctypes.data_as(C.POINTER(C.c_uint64)), L.size, int(W), self.cap,
+                                           C.byref(self.h)))
+            if max_chunk:
+                check(lib.krk_window_sched_set_chunk_cap(self.h, int(max_chunk)))
+        self.sub = {int(b): k for k, b in enumerate(self.idx)}
+        self._b = np.zeros(self.cap, dtype=np.uint32)
+        self._o = np.zeros(self.cap, dtype=np.uint64)
+        self._t = np.zeros(self.cap, dtype=np.uint64)
+
+    def next(self):
+        if not self.h.value:
+            return None
+        k = C.c_uint64(0)
+        self.check(self.lib.krk_window_sched_next(self.h, self._b.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                  self._o.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                                  self._t.ctypes.data_as(C.POINTER(C.c_uint64)), self.cap,
+                                                  C.byref(k)))
+        m = k.value
+        if not m:
+            return None
+        return self.idx[self._b[:m].astype(np.int64)], self._o[:m].copy(), self._t[:m].copy()
+
+    def drop(self, b):
+        off = C.c_uint64(0)
+        self.check(self.lib.krk_window_sched_drop(self.h, self.sub[int(b)], C.byref(off)))
+        return off.value
+
+    def close(self):
+        if self.h.value:
+            self.lib.krk_window_sched_free(self.h)
+            self.h = C.c_void_p()
+
+
+class TailPolicy:
+    """Which chains the host threads take, and when (shared by the run and its model).
+    A chain is a candidate while it has more bytes left than the window after the queued one
+    would give it; candidates go longest-remaining first.  Waiting (not yet admitted) blobs
+    are candidates too, with all their bytes left."""
+
+    def __init__(self, lens, threads):
+        self.L = np.asarray(lens, dtype=np.int64)
+        self.H = max(1, int(threads))
+        self.pos = np.zeros(self.L.size, dtype=np.int64)  # bytes the windows queued so far
+        self.on_gpu = np.ones(self.L.size, dtype=bool)    # not (yet) taken by a host thread
+
+    def initial(self):
+        """The chains the threads take whole before the first window (the H longest)."""
+        k = min(self.H, self.L.size)
+        first = np.argsort(-self.L, kind="stable")[:k]
+        self.on_gpu[first] = False
+        return [int(b) for b in first]
+
+    def queued(self, blobs, offs, takes):
+        self.pos[blobs] = (offs + takes).astype(np.int64)
+
+    def pick(self, n, min_left):
+        """Up to n chains for threads about to be free, most bytes left first; min_left: a
+        chain the next window would finish anyway stays on the GPU."""
+        if n <= 0:
+            return []
+        left = np.where(self.on_gpu, self.L - self.pos, -1)
+        if n < left.size:
+            cand = np.argpartition(-left, n)[:n]
+        else:
+            cand = np.arange(left.size)
+        cand = cand[np.argsort(-left[cand], kind="stable")]
+        out = [int(b) for b in cand if left[b] > min_left]
+        self.on_gpu[out] = False
+        return out
+
+
+def simulate_tail_handoff(lens, W, cap, threads, rates, launch_s=0.0005, max_chunk=0):
+    """The tail handoff on the planner's rates, window by window, with the policy the run uses:
+    window k lasts its largest chunk over the per-stream rate of its live count's tier plus a
+    launch; at the start of window k (the end of k-1) every thread free before window k+1
+    would end takes a chain, whose midstate is ready when window k ends.  Returns the
+    modelled end (s), the GPU windows' end, the host bytes and the takeovers."""
+    L = np.asarray(lens, dtype=np.int64)
+    H = max(1, int(threads))
+    h = tail_thread_rate(rates, H)
+    pol = TailPolicy(L, H)
+    first = pol.initial()
+    free = [float(L[b]) / h for b in first] + [0.0] * (H - len(first))
+    host_bytes = int(L[first].sum())
+    takes = 0
+    sched = _Sched(L, np.nonzero(pol.on_gpu)[0], W, cap, max_chunk)
+    t = 0.0  # end of the previous window = start of this one
+    try:
+        win = sched.next()
+        while win is not None:
+            blobs, offs, tk = win
+            pol.queued(blobs, offs, tk)
+            dur = float(tk.max()) / stream_rate(rates, blobs.size) + launch_s
+            end_k = t + dur
+            horizon = end_k + dur  # window k+1 modelled like k
+            ready = [i for i in range(H) if free[i] <= horizon]
+            chosen = pol.pick(len(ready), stream_rate(rates, blobs.size) * dur)
+            ready.sort(key=lambda i: free[i])
+            for i, b in zip(ready, chosen):
+                y = sched.drop(b)
+                start = max(free[i], end_k if y else free[i])
+                free[i] = start + float(L[b] - y) / h
+                host_bytes += int(L[b] - y)
+                takes += 1
+            t = end_k
+            win = sched.next()
+    finally:
+        sched.close()
+    return {"end_s": max([t] + free), "gpu_end_s": t, "host_bytes": host_bytes, "takeovers": takes + len(first),
+            "thread_rate_Bps": h}
+
+
+class TailHandoffRun:
+    """A windowed batch (the WindowedRun layout: synthetic blobs generated window by window on
+    the device, two device windows, one ChunkedBatch) with the tail handoff: `threads` host
+    threads steal chains at window boundaries (TailPolicy).  After run(): cb.sums / cb.digests
+    hold every blob's piece sums and digest (device); `stats` the run's takeovers and timing."""
+
+    def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK):
+        self.D = D
+        self.ids = np.asarray(ids, dtype=np.uint64)
+        self.lens = np.asarray(lens, dtype=np.int64)
+        self.P = P
+        self.W = int(W)
+        self.H = max(1, int(threads))
+        self.device = device
+        self.max_chunk = int(max_chunk)
+        n = self.lens.size
+        self.cap = window_stream_cap(D, n) if cap is None else int(cap)
+        self.rates = D.planner_rates()
+        self.h = tail_thread_rate(self.rates, self.H)
+        wb = self.W + 16 * max(min(self.cap, n), 1)
+        self.bufs = [D.DeviceBuffer(wb), D.DeviceBuffer(wb)]
+        self.cb = D.ChunkedBatch(self.lens, P)
+        self.tbuf = [[D.DeviceBuffer(TAIL_PIECE), D.DeviceBuffer(TAIL_PIECE)] for _ in range(self.H)]
+        self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
+        D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
+        # the windows' SHA-256 launches on hardware queues of their own (high priority): the
+        # threads' copies and generator / CRC launches must not queue behind a window's launch
+        D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
+        self.t_s = []
+        for _ in range(self.H):
+            self.t_s.append(C.c_void_p())
+            D.check(D.lib.krk_stream_create(C.byref(self.t_s[-1])))
+        self.stats = {}
+
+    # ---- one thread's chains
+    def _job(self, i, b, y, ev, dig):
+        """Chain b from byte y: its remaining bytes generated on the device piece by piece,
+        their CRCs queued on the GPU, SHA-256 continued on this thread from the midstate the
+        windows left in HBM (window event `ev`), or from the IV when y == 0."""
+        D = self.D
+        s = self.t_s[i]
+        L = int(self.lens[b])
+        rest = L - y
+        nch = max(1, -(-rest // TAIL_PIECE))
+        soff = int(self.cb.sums_off[b])
+
+        def queue(c):
+            o = y + c * TAIL_PIECE
+            m = min(TAIL_PIECE, L - o)
+            if m <= 0:
+                return
+            ptr = np.array([self.tbuf[i][c & 1].ptr], dtype=np.uint64)
+            D.synth_fill_chunk_arrays(self.ids[b:b + 1], ptr, np.array([o], np.uint64), np.array([m], np.uint64),
+                                      stream=s)
+            arr = D.chunk_array(ptr, np.array([o], np.uint64), np.array([m], np.uint64), np.uint64(L),
+                                np.int64(self.cb.piece_lengths[b]), np.uint64(soff), np.uint64(b))
+            D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), 1, self.cb.sums.ptr, s))
+
+        queue(0)
+        h = _IV.copy()
+        if y:
+            D.check(D.lib.krk_event_sync(ev))  # the window that last advanced chain b is done
+            D.check(D.lib.krk_memcpy_d2h(h.ctypes.data_as(C.c_void_p), C.c_void_p(self.cb.state.ptr + 32 * b), 32))
+        out = np.zeros(32, dtype=np.uint8)
+        for c in range(nch):
+            if c + 1 < nch:
+                queue(c + 1)
+            o = y + c * TAIL_PIECE
+            m = min(TAIL_PIECE, L - o)
+            D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), o,
+                                                        C.c_void_p(self.tbuf[i][c & 1].ptr), m, int(c + 1 == nch),
+                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), s))
+            with self._mu:
+                self._left[i] -= m
+                self._t_last[i] = self._clock()
+        dig[b] = out
+
+    def _worker(self, i, err, dig):
+        import time
+        try:
+            self.D.set_device(self.device)
+            while True:
+                with self._cv:
+                    while not self._jobs[i] and not self._done:
+                        self._cv.wait()
+                    if not self._jobs[i]:
+                        return
+                    b, y, ev = self._jobs[i][0]
+                t0 = time.perf_counter()
+                self._job(i, b, y, ev, dig)
+                with self._cv:
+                    self._jobs[i].pop(0)
+                    self._busy_s[i] += time.perf_counter() - t0
+                    self._cv.notify_all()
+        except BaseException as e:  # re-raised on the caller's thread
+            err.append(e)
+            with self._cv:
+                self._done = True
+                self._cv.notify_all()
+
+    def _free_at(self, i, now):
+        """When thread i is expected to be done with its queued chains (measured progress)."""
+        return (self._t_last[i] if self._jobs[i] else now) + max(0, self._left[i]) / self.h
+
+    def run(self):
+        import threading
+        import time
+        D = self.D
+        n = self.lens.size
+        self._clock = time.perf_counter
+        self._mu = threading.Lock()
+        self._cv = threading.Condition(self._mu)
+        self._jobs = [[] for _ in range(self.H)]
+        self._left = [0] * self.H
+        self._t_last = [0.0] * self.H
+        self._busy_s = [0.0] * self.H
+        self._done = False
+        dig = np.zeros((n, 32), dtype=np.uint8)
+        err = []
+        pol = TailPolicy(self.lens, self.H)
+        host_blobs = set()
+        host_bytes = 0
+        t0 = self._clock()
+        with self._cv:
+            for i, b in enumerate(pol.initial()):
+                self._jobs[i].append((b, 0, None))
+                self._left[i] = int(self.lens[b])
+                self._t_last[i] = t0
+                host_blobs.add(b)
+                host_bytes += int(self.lens[b])
+        workers = [threading.Thread(target=self._worker, args=(i, err, dig), name=f"krk-tail-{i}")
+                   for i in range(self.H)]
+        for w in workers:
+            w.start()
+        sched = _Sched(self.lens, np.nonzero(pol.on_gpu)[0], self.W, self.cap, self.max_chunk)
+        evs = []
+        takes, resumed, wait_win_s = 0, 0, 0.0
+        scale = 1.0  # measured / modelled window time (EMA)
+        try:
+            win = sched.next()
+            k = 0
+            items = self._items(win, 0) if win is not None else None
+            if items is not None:
+                self._gen(items)
+            t_prev_end = self._clock()
+            self._last_model = 1.0
+            while win is not None and not err:
+                blobs, offs, tk = win
+                pol.queued(blobs, offs, tk)
+                self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s)
+                ev = C.c_void_p()
+                D.check(D.lib.krk_event_create(C.byref(ev)))
+                D.check(D.lib.krk_event_record(ev, self.run_s))
+                evs.append(ev)
+                model = float(tk.max()) / stream_rate(self.rates, blobs.size) + 0.0005
+                if k:
+                    tw = self._clock()
+                    D.check(D.lib.krk_event_sync(evs[k - 1]))
+                    now = self._clock()
+                    wait_win_s += now - tw
+                    scale = 0.7 * scale + 0.3 * max(0.2, min(5.0, (now - t_prev_end) / max(self._last_model, 1e-6)))
+                    t_prev_end = now
+                now = self._clock()
+                self._last_model = model
+                end_k = now + model * scale
+                horizon = end_k + model * scale  # window k+1 modelled like k
+                with self._cv:  # threads with at most their current chain, free before k+1 ends
+                    ready = [i for i in range(self.H) if len(self._jobs[i]) <= 1 and self._free_at(i, now) <= horizon]
+                    ready.sort(key=lambda i: self._free_at(i, now))
+                chosen = pol.pick(len(ready), stream_rate(self.rates, blobs.size) * model)
+                with self._cv:
+                    for i, b in zip(ready, chosen):
+                        y = sched.drop(b)
+                        if not self._jobs[i]:
+                            self._t_last[i] = now
+                        self._jobs[i].append((b, y, ev if y else None))
+                        self._left[i] += int(self.lens[b]) - y
+                        host_blobs.add(b)
+                        host_bytes += int(self.lens[b]) - y
+                        takes += 1
+                        resumed += y > 0
+                    self._cv.notify_all()
+                win = sched.next()
+                k += 1
+                if win is not None:
+                    items = self._items(win, k)
+                    self._gen(items)
+            if evs:
+                D.check(D.lib.krk_stream_sync(self.run_s))
+            gpu_end = self._clock() - t0
+        finally:
+            with self._cv:
+                self._done = True
+                self._cv.notify_all()
+            for w in workers:
+                w.join()
+            sched.close()
+        if err:
+            for e in evs:
+                D.lib.krk_event_destroy(e)
+            raise err[0]
+        for s in self.t_s:  # the tails' CRCs
+            D.check(D.lib.krk_stream_sync(s))
+        for e in evs:
+            D.lib.krk_event_destroy(e)
+        for b in sorted(host_blobs):
+            row = np.ascontiguousarray(dig[b])
+            D.check(D.lib.krk_memcpy_h2d(C.c_void_p(self.cb.digests.ptr + 32 * int(b)),
+                                         row.ctypes.data_as(C.c_void_p), 32))
+        self.stats = {"windows": len(evs), "gpu_windows_end_s": round(gpu_end, 3),
+                      "takeovers": takes, "resumed_from_midstate": resumed, "host_chains": len(host_blobs),
+                      "host_bytes": host_bytes,
+                      "thread_busy_s": [round(x, 3) for x in self._busy_s],
+                      "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
+
+    def _items(self, win, k):
+        blobs, offs, take = win
+        dev = np.zeros(take.size, dtype=np.uint64)
+        dev[1:] = np.cumsum((take + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]
+        dev += np.uint64(self.bufs[k & 1].ptr)
+        return blobs, dev, offs, take
+
+    def _gen(self, items):
+        blobs, dev, offs, take = items
+        self.D.synth_fill_chunk_arrays(self.ids[blobs], dev, offs, take, stream=self.gen_s)
+        self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
+
+    def close(self):
+        for b in self.bufs + [x for pair in self.tbuf for x in pair]:
+            b.free()
+        self.bufs, self.tbuf = [], []
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s:
+            if s.value:
+                self.D.lib.krk_stream_destroy(s)
+        self.gen_s, self.run_s, self.sha_s, self.t_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

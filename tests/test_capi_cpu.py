@@ -701,3 +701,67 @@ def test_sha_tail_plan_follows_rates():
         assert Dv.sha_tail_plan(L, 0)[0].size == 0
     finally:
         check(lib.krk_planner_rates_set(None))
+
+
+def test_window_sched_drop_and_chunk_cap():
+    """The tail handoff's schedule hooks (no device): krk_window_sched_drop takes a live blob
+    out (its offset = the bytes the windows gave it; its place goes to the next waiting
+    blob) or a waiting one (offset 0, never admitted); krk_window_sched_set_chunk_cap bounds
+    every later chunk.  Every other blob still gets every byte once, in order."""
+    lens = np.array([9000, 7000, 5000, 3000, 1000], dtype=np.uint64)
+    h = C.c_void_p()
+    check(lib.krk_window_sched_new(lens.ctypes.data_as(C.POINTER(C.c_uint64)), 5, 4096, 2, C.byref(h)))
+    b, o, t = np.zeros(8, np.uint32), np.zeros(8, np.uint64), np.zeros(8, np.uint64)
+    k = C.c_uint64()
+
+    def nxt():
+        check(lib.krk_window_sched_next(h, b.ctypes.data_as(C.POINTER(C.c_uint32)), o.ctypes.data_as(
+            C.POINTER(C.c_uint64)), t.ctypes.data_as(C.POINTER(C.c_uint64)), 8, C.byref(k)))
+        return [(int(b[j]), int(o[j]), int(t[j])) for j in range(k.value)]
+
+    try:
+        w0 = nxt()
+        assert [x[0] for x in w0] == [0, 1] and all(x[2] == 2048 for x in w0)  # longest first, 4096 / 2 live
+        off = C.c_uint64()
+        check(lib.krk_window_sched_drop(h, 0, C.byref(off)))
+        assert off.value == 2048
+        check(lib.krk_window_sched_drop(h, 3, C.byref(off)))  # still waiting
+        assert off.value == 0
+        with pytest.raises(RuntimeError, match="neither live nor waiting"):
+            check(lib.krk_window_sched_drop(h, 3, C.byref(off)))
+        check(lib.krk_window_sched_set_chunk_cap(h, 640))
+        pos = {1: 2048, 2: 0, 4: 0}
+        seen = set()
+        while True:
+            w = nxt()
+            if not w:
+                break
+            for blob, offs, take in w:
+                assert blob in pos and offs == pos[blob] and take <= 640, (blob, offs, take)
+                pos[blob] += take
+                seen.add(blob)
+        assert pos == {1: 7000, 2: 5000, 4: 1000} and seen == {1, 2, 4}
+    finally:
+        lib.krk_window_sched_free(h)
+
+
+def test_tail_handoff_model_accounts_every_byte():
+    """windowed.simulate_tail_handoff (no device; the planner's rates injected): the policy
+    the GPU run uses, on rank 0's LPT shard of an 8-GPU C3 scaled down 64x.  The threads'
+    bytes plus the windows' bytes are the batch; the modelled end beats the GPU alone (the
+    longest chain at the eight-lane rate) and is no earlier than the work allows (launches
+    priced at 0 s at this scale)."""
+    from kraken_amd.shard import lpt_shard
+    from kraken_amd.windowed import c3_lengths, simulate_tail_handoff
+    L = c3_lengths(20000, scale=64)
+    lens = [L[i] for i in lpt_shard(L, 8)[0]]
+    rates = {"sha_stream_bps": [58.5e6, 52.3e6, 35.2e6], "d2h_bps": 56e9, "h2d_bps": 56e9, "host_sha_bps": 2.1e9,
+             "host_crc_bps": 17e9, "host_copy_bps": 30e9, "cus": 256, "source": 2}
+    m = simulate_tail_handoff(lens, len(lens) * (64 << 10), len(lens), 15, rates, launch_s=0.0, max_chunk=64 << 10)
+    gpu_only = max(lens) / 58.5e6
+    assert m["end_s"] < 0.8 * gpu_only, (m, gpu_only)
+    total = sum(lens)
+    assert 0 < m["host_bytes"] < total
+    # no faster than all of it on the host threads plus every GPU stream at once
+    assert m["end_s"] >= total / (15 * m["thread_rate_Bps"] + len(lens) * 58.5e6)
+    assert m["takeovers"] >= 15

@@ -80,3 +80,60 @@ def test_window_plan_covers_c3_law_once():
         assert ((take % 64 == 0) | (offs + take == np.asarray(lens, dtype=np.uint64)[blobs])).all()
         pos[blobs] += take
     assert np.array_equal(pos, np.asarray(lens, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("cap,threads", [(None, 3), (200, 4)])
+def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads):
+    """the windowed batch with the tail handoff (windowed.TailHandoffRun):
+    host threads start on the longest chains whole, then steal the chains with the most bytes
+    left at window boundaries -- live chains from the midstate the windows left in HBM, and
+    (cap=200) blobs still waiting for admission from the IV -- while their remaining piece
+    CRCs run on the GPU beside the windows'.  1 MiB window chunks: hundreds of windows and
+    takeovers.  Every blob equals the one-shot device path; sampled blobs the oracle."""
+    from kraken_amd.windowed import TailHandoffRun
+    lens, ids, dg1, sums1, offs1, counts1 = one_shot
+    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20)
+    tr.run()
+    st = tr.stats
+    cb = tr.cb
+    dg = cb.digests.to_host(np.uint8, 32 * N).reshape(-1, 32)
+    sums = cb.sums.to_host(np.uint32, cb.total_pieces)
+    tr.close()
+    print(st)
+    assert st["takeovers"] > threads and st["resumed_from_midstate"] > 0 and st["windows"] > 50, st
+    assert 0 < st["host_bytes"] < int(np.sum(lens)), st
+    bad = [i for i in range(N) if bytes(dg[i]) != bytes(dg1[i])]
+    assert not bad, (len(bad), bad[:10])
+    for i in range(N):
+        a, b = int(cb.sums_off[i]), int(offs1[i])
+        assert np.array_equal(sums[a:a + int(counts1[i])], sums1[b:b + int(counts1[i])]), i
+    L = np.asarray(lens)
+    for i in sorted({int(L.argmin()), int(L.argmax()), 7, 777}):
+        data = orc.synth(ids[i], lens[i])
+        assert bytes(dg[i]) == hashlib.sha256(data.tobytes()).digest(), i
+        a = int(cb.sums_off[i])
+        assert np.array_equal(sums[a:a + int(counts1[i])], orc.calc_piece_sums(data, P)[1]), i
+
+
+def test_sha256_resume_from_device_bytes(gpu, orc):
+    """krk_sha256_resume_dev_on_host: one chain continued on the calling thread from device
+    bytes, in runs of whole blocks then a final run of any length (0, 1, 55, 56, 64, 8 MiB +
+    3 ...), equals hashlib over the whole blob."""
+    import ctypes as C
+    from kraken_amd.windowed import _IV
+    for L, cuts in ((0, []), (1, []), (55, []), (64, [64]), (130, [64]), ((8 << 20) + 3, [1 << 20, 3 << 20]),
+                    ((17 << 20) + 64, [64, (16 << 20) + 64])):
+        data = orc.synth(4242 + L, L)
+        buf = D.DeviceBuffer(max(L, 1))
+        if L:
+            buf.from_host(data)
+        h = _IV.copy()
+        out = np.zeros(32, np.uint8)
+        prev = 0
+        for c in cuts + [L]:
+            D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), prev,
+                                                        C.c_void_p(buf.ptr + prev), c - prev, int(c == L),
+                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), None))
+            prev = c
+        assert bytes(out) == hashlib.sha256(data.tobytes()).digest(), L
+        buf.free()
