@@ -60,8 +60,8 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
-size_t env_size(const char* k, size_t dflt) {
-    const char* v = getenv(k);
+// a knob's value (KRK_OP_ENV / KRK_AB_ENV, knobs.hpp) as a positive size, else dflt
+size_t env_size(const char* v, size_t dflt) {
     if (!v || !*v) return dflt;
     const unsigned long long x = strtoull(v, nullptr, 10);
     return x ? (size_t)x : dflt;
@@ -652,7 +652,7 @@ void launch_batch(Engine* E, Queue* Q, Inflight* f, bool sha) {
                 std::chrono::duration<double, std::milli>(f->t_launch.time_since_epoch()).count(), f->batch.size(),
                 f->reason, f->depth, f->left_queued, (long long)f->missing, f->est);
     if (!sha && ++E->crc_launches == E->fail_crc_at) {
-        set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (KRK_ENGINE_FAIL_CRC_LAUNCH)",
+        set_error(KRK_EHIP, "engine: injected failure of CRC launch %llu (fault injection, diag build)",
                   (unsigned long long)E->crc_launches);
         f->rc = KRK_EHIP;
     } else {
@@ -796,26 +796,27 @@ int engine_start(Engine* E) {
     // launch behind for good, so the launch should be short; 256 concurrent digesters from
     // native threads, same box, interleaved (tests/native/digesters.cpp): 2 MiB slots with 4
     // in flight 8.8-12.6 GB/s, 512 KiB with 8 in flight 11.1-14.2 GB/s (zero-copy).
-    const size_t slot = getenv("KRK_SLOT_KB") ? (env_size("KRK_SLOT_KB", 512) << 10)
-                                              : getenv("KRK_SLOT_MB") ? (env_size("KRK_SLOT_MB", 2) << 20) : (512u << 10);
+    const size_t slot = KRK_AB_ENV("KRK_SLOT_KB")   ? (env_size(KRK_AB_ENV("KRK_SLOT_KB"), 512) << 10)
+                        : KRK_AB_ENV("KRK_SLOT_MB") ? (env_size(KRK_AB_ENV("KRK_SLOT_MB"), 2) << 20)
+                                                    : (512u << 10);
     // KRK_SLOT_NUMA: "gpu" = the device's NUMA node, N = node N, unset = no binding
     int numa = -1;
-    if (const char* nm = getenv("KRK_SLOT_NUMA")) numa = strcmp(nm, "gpu") == 0 ? device_numa_node(E->dev) : atoi(nm);
-    E->pool.init((slot + 63) & ~size_t(63), env_size("KRK_SLOT_POOL_MB", 4096) << 20, numa);
-    g_owner_inflight = std::max<size_t>(2, env_size("KRK_OWNER_INFLIGHT", 8));
-    g_inflight = (int)std::min<size_t>(kMaxInflight, std::max<size_t>(1, env_size("KRK_ENGINE_INFLIGHT", 3)));
-    E->coalesce_us = env_size("KRK_SHA_COALESCE_US", 30000);
+    if (const char* nm = KRK_AB_ENV("KRK_SLOT_NUMA")) numa = strcmp(nm, "gpu") == 0 ? device_numa_node(E->dev) : atoi(nm);
+    E->pool.init((slot + 63) & ~size_t(63), env_size(KRK_OP_ENV("KRK_SLOT_POOL_MB"), 4096) << 20, numa);
+    g_owner_inflight = std::max<size_t>(2, env_size(KRK_AB_ENV("KRK_OWNER_INFLIGHT"), 8));
+    g_inflight = (int)std::min<size_t>(kMaxInflight, std::max<size_t>(1, env_size(KRK_AB_ENV("KRK_ENGINE_INFLIGHT"), 3)));
+    E->coalesce_us = env_size(KRK_AB_ENV("KRK_SHA_COALESCE_US"), 30000);
     // 10 ms: 256 writers starting together reach their first full slot over 5-25 ms on a
     // CPU-quota box; with 3 ms a third of the rounds launched before all were in and ran 3-4
     // launches more (profiles/r03/engine_quiet_ab.jsonl: median 13.94 -> 14.16 GB/s, every
     // round 33 launches).  A GPU Digester carries >= 512 KiB a request, ~9 ms of a stream.
-    E->quiet_us = env_size("KRK_SHA_QUIET_US", 10000);
-    E->fail_crc_at = env_size("KRK_ENGINE_FAIL_CRC_LAUNCH", 0);
-    E->trace = env_size("KRK_ENGINE_TRACE", 0) != 0;
-    if (const char* z = getenv("KRK_SHA_ZERO_COPY")) E->src = atoi(z) ? kSrcZeroCopy : kSrcDma;  // round-4 knob
-    if (const char* m = getenv("KRK_ENGINE_SLOT_SRC"))
+    E->quiet_us = env_size(KRK_AB_ENV("KRK_SHA_QUIET_US"), 10000);
+    E->fail_crc_at = env_size(KRK_AB_ENV("KRK_ENGINE_FAIL_CRC_LAUNCH"), 0);
+    E->trace = env_size(KRK_OP_ENV("KRK_ENGINE_TRACE"), 0) != 0;
+    if (const char* z = KRK_AB_ENV("KRK_SHA_ZERO_COPY")) E->src = atoi(z) ? kSrcZeroCopy : kSrcDma;  // round-4 knob
+    if (const char* m = KRK_AB_ENV("KRK_ENGINE_SLOT_SRC"))
         E->src = !strcmp(m, "gather") ? kSrcGather : !strcmp(m, "dma") ? kSrcDma : kSrcZeroCopy;
-    if (const char* c = getenv("KRK_ENGINE_CALLER_RUNS")) E->caller_runs = atoi(c) != 0;
+    if (const char* c = KRK_AB_ENV("KRK_ENGINE_CALLER_RUNS")) E->caller_runs = atoi(c) != 0;
     KRK_HIP(hipMalloc(&E->d_state, 32ull * kStateRows));
     KRK_HIP(hipMalloc(&E->d_digest, 32ull * kStateRows));
     KRK_HIP(hipStreamCreateWithFlags(&E->s_copy, hipStreamNonBlocking));
@@ -1021,7 +1022,7 @@ int64_t host_stream_limit() {
     const int64_t v = g_host_streams.load(std::memory_order_relaxed);
     if (v >= 0) return v;
     static const int64_t env = [] {
-        const char* e = getenv("KRK_DIGESTER_HOST_STREAMS");
+        const char* e = KRK_OP_ENV("KRK_DIGESTER_HOST_STREAMS");
         return e && *e ? std::max<int64_t>(0, strtoll(e, nullptr, 10)) : int64_t(-1);
     }();
     if (env >= 0) return env;
@@ -1341,7 +1342,7 @@ std::atomic<int> g_crc_placement{KRK_PLACE_AUTO};  // krk_set_crc_placement / KR
 int crc_placement_setting() {
     static std::once_flag once;
     std::call_once(once, [] {
-        if (const char* e = getenv("KRK_CRC_PLACEMENT")) {
+        if (const char* e = KRK_OP_ENV("KRK_CRC_PLACEMENT")) {
             const int v = atoi(e);
             if (v >= KRK_PLACE_AUTO && v <= KRK_PLACE_GPU) g_crc_placement.store(v);
         }
@@ -1490,7 +1491,7 @@ void stream_host_update(krk_piece_stream* s, const uint8_t* buf, uint64_t n) {
     // took ~6 us each and the caller finished its own before the helpers woke).
     // KRK_STREAM_SPAN_KB overrides it (A/B).
     static const uint64_t min_span = [] {
-        const char* v = getenv("KRK_STREAM_SPAN_KB");
+        const char* v = KRK_AB_ENV("KRK_STREAM_SPAN_KB");
         if (v) return std::max<uint64_t>(64, strtoull(v, nullptr, 10)) << 10;
         const uint64_t b = (uint64_t)(host_crc_rate() * 40e-6);
         return std::max<uint64_t>(256u << 10, (b + 65535) & ~uint64_t(65535));
@@ -1636,7 +1637,7 @@ int krk_crc32_update_on(int placement, uint32_t crc, const uint8_t* data, uint64
     KRK_CHECK(n == 0 || data, KRK_EINVAL, "data is NULL");
     KRK_CHECK(placement >= KRK_PLACE_AUTO && placement <= KRK_PLACE_GPU, KRK_EINVAL, "unknown placement %d",
               placement);
-    static const size_t host_max = env_size("KRK_CRC_HOST_MAX", 64 << 10);
+    static const size_t host_max = env_size(KRK_OP_ENV("KRK_CRC_HOST_MAX"), 64 << 10);
     int rc = KRK_OK;
     const int where = (placement == KRK_PLACE_AUTO && n <= host_max) ? KRK_PLACE_HOST
                                                                       : resolve_placement(placement, &rc);

@@ -14,6 +14,8 @@
 #include <utility>
 #include <vector>
 
+#include "knobs.hpp"
+
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
@@ -101,7 +103,7 @@ static bool have_sha_ni() {
 // KRK_SHA1_PORTABLE=1 forces the portable compressor (tests compare both).
 static void sha1_blocks(uint32_t h[5], const uint8_t* p, size_t nblocks) {
 #if defined(__x86_64__)
-    static const bool portable = getenv("KRK_SHA1_PORTABLE") && atoi(getenv("KRK_SHA1_PORTABLE")) > 0;
+    static const bool portable = KRK_AB_ENV("KRK_SHA1_PORTABLE") && atoi(KRK_AB_ENV("KRK_SHA1_PORTABLE")) > 0;
     if (!portable && have_sha_ni()) return sha1_blocks_ni(h, p, nblocks);
 #endif
     sha1_blocks_portable(h, p, nblocks);
@@ -209,7 +211,7 @@ __attribute__((target("sha,sse4.1"))) static void sha256_blocks_ni(uint32_t h[8]
 
 // KRK_HOST_PORTABLE=1 forces the portable SHA-256 / CRC-32 routines (tests compare).
 static bool host_portable() {
-    static const bool p = getenv("KRK_HOST_PORTABLE") && atoi(getenv("KRK_HOST_PORTABLE")) > 0;
+    static const bool p = KRK_AB_ENV("KRK_HOST_PORTABLE") && atoi(KRK_AB_ENV("KRK_HOST_PORTABLE")) > 0;
     return p;
 }
 
@@ -343,7 +345,7 @@ __attribute__((target("avx512f,avx512bw,vpclmulqdq,pclmul,sse4.1"))) static uint
 
 static bool have_vclmul() {
     static const bool ok = [] {
-        const char* v = getenv("KRK_HOST_CRC_AVX512");  // 0: the 128-bit loop (A/B)
+        const char* v = KRK_AB_ENV("KRK_HOST_CRC_AVX512");  // 0: the 128-bit loop (A/B)
         if (v && v[0] == '0') return false;
         return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
                __builtin_cpu_supports("vpclmulqdq") && __builtin_cpu_supports("pclmul");

@@ -509,8 +509,7 @@ static int node_cpu_count() {
     return c;
 }
 
-static int env_pos(const char* k) {
-    const char* e = getenv(k);
+static int env_pos(const char* e) {
     return e && atoi(e) > 0 ? atoi(e) : 0;
 }
 
@@ -529,10 +528,10 @@ struct CpuBudget {
 static const CpuBudget& cpu_budget() {
     static const CpuBudget b = [] {
         const int node = node_cpu_count();
-        if (int x = env_pos("KRK_HOST_CPUS")) return CpuBudget{x, node, "KRK_HOST_CPUS"};
-        if (int w = env_pos("LOCAL_WORLD_SIZE"); w > 1)
+        if (int x = env_pos(KRK_OP_ENV("KRK_HOST_CPUS"))) return CpuBudget{x, node, "KRK_HOST_CPUS"};
+        if (int w = env_pos(getenv("LOCAL_WORLD_SIZE")); w > 1)
             return CpuBudget{std::max(1, node / w), node, "node/LOCAL_WORLD_SIZE"};
-        if (int o = env_pos("OMP_NUM_THREADS"); o > 0 && o < node)
+        if (int o = env_pos(getenv("OMP_NUM_THREADS")); o > 0 && o < node)
             return CpuBudget{o, node, "OMP_NUM_THREADS"};
         return CpuBudget{node, node, "node"};
     }();
@@ -587,7 +586,7 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     }
     std::atomic<size_t> next{0};
     std::atomic<int> err{0};
-    static const bool trace = getenv("KRK_TRACE") && atoi(getenv("KRK_TRACE")) > 0;
+    static const bool trace = KRK_OP_ENV("KRK_TRACE") && atoi(KRK_OP_ENV("KRK_TRACE")) > 0;
     std::vector<double> t_wait(T, 0.0), t_hash(T, 0.0);
     const auto t_start = std::chrono::steady_clock::now();
     auto secs = [](std::chrono::steady_clock::time_point a) {

@@ -125,7 +125,7 @@ int krk_init(uint64_t dev_mask) {
         if (!D) r = rc;
         // the planners' rates, measured now while the library has no work on the device
         // (a first use under load would fix a contended split for the process)
-        else if (!getenv("KRK_NO_CALIBRATE")) r = calibrate_device(D);
+        else if (!KRK_OP_ENV("KRK_NO_CALIBRATE")) r = calibrate_device(D);
     }
     for (int i = n; i < 64 && !r; ++i)
         if ((dev_mask >> i) & 1) {
@@ -197,7 +197,7 @@ static HostShare offload_split(Device* D, const uint64_t* lens, uint64_t n, std:
     const Rates R = planner_rates(D);
     double g = 0, h = 0;
     hs.idx = offload_plan(lens, n, T, R, &g, &h);
-    static const bool tails = !getenv("KRK_SHA_TAIL") || atoi(getenv("KRK_SHA_TAIL")) != 0;
+    static const bool tails = !KRK_AB_ENV("KRK_SHA_TAIL") || atoi(KRK_AB_ENV("KRK_SHA_TAIL")) != 0;
     if (tails) {
         const double whole = std::max(g, h);
         TailPlan tp = tail_plan(lens, n, T, R);
@@ -398,7 +398,7 @@ int krk_metainfo_batch_dev(const krk_blob* blobs, uint64_t n_blobs, const char* 
     // with eight (each launch's ramp and tail cost more than the InfoHash overlap buys) and
     // 9.70-10.07 with one (profiles/r03/regen_groups_ab.txt).
     static const uint64_t kGroups = [] {
-        const char* g = getenv("KRK_REGEN_GROUPS");
+        const char* g = KRK_AB_ENV("KRK_REGEN_GROUPS");
         return (uint64_t)std::max(1, g ? atoi(g) : 4);
     }();
     const uint64_t G = std::min<uint64_t>(n_blobs, kGroups);
@@ -407,7 +407,7 @@ int krk_metainfo_batch_dev(const krk_blob* blobs, uint64_t n_blobs, const char* 
     // equal groups), the others sharing the rest equally.  C5 regen 5.10-5.24 TB/s with equal
     // groups, 5.44-5.58 with a 4 % tail, 5.35-5.41 with 2 % (profiles/r03/regen_tail_ab.txt).
     static const double kTail = [] {
-        const char* t = getenv("KRK_REGEN_TAIL");
+        const char* t = KRK_AB_ENV("KRK_REGEN_TAIL");
         return t ? atof(t) : 0.04;
     }();
     const double tail = (kTail > 0 && kTail < 1 && G > 1) ? kTail : 1.0 / (double)G;
@@ -685,7 +685,7 @@ class NodeTasks {
     // is never visited.  False when there is one node or the query fails.
     bool build(const std::vector<const void*>& first, const std::vector<const void*>& mid,
                const std::vector<const void*>& last) {
-        const char* v = getenv("KRK_CRC_NUMA");
+        const char* v = KRK_AB_ENV("KRK_CRC_NUMA");
         mode_ = v ? atoi(v) : 0;
         const size_t n = first.size();
         if (mode_ <= 0 || n < 2) return false;
@@ -792,7 +792,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
         bytes += (double)blobs[i].length;
         if (all_pinned && blobs[i].length && !host_pinned(blobs[i].data, blobs[i].length)) all_pinned = false;
     }
-    const char* forced = getenv("KRK_CRC_GPU_FRACTION");
+    const char* forced = KRK_OP_ENV("KRK_CRC_GPU_FRACTION");
     // Pageable batches stay on the host threads and need no device; pinned (or forced) ones
     // split by the device's rates.
     Device* D = nullptr;
@@ -855,7 +855,7 @@ int krk_piece_sums_host(const krk_blob* blobs, uint64_t n_blobs, uint32_t* sums_
     // bytes, which the hardware prefetchers follow (256 KiB tasks handed out one at a time ran
     // C4's host side ~30 % below contiguous spans, profiles/r04/host_mem_probe_lib.jsonl).
     static const double task_bytes = [] {  // KRK_CRC_TASK_KB overrides the run length (A/B)
-        const char* v = getenv("KRK_CRC_TASK_KB");
+        const char* v = KRK_AB_ENV("KRK_CRC_TASK_KB");
         return v ? atof(v) * 1024.0 : double(8u << 20);
     }();
     const size_t G = host.empty() ? 1
@@ -1033,7 +1033,7 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
     t_split_host = where == KRK_PLACE_GPU ? 0 : bytes;
     if (where != KRK_PLACE_GPU) return piece_sums_files_host(files, n, sums_host);
     KRK_DEVICE(D);
-    const bool want_direct = getenv("KRK_FILE_DIRECT") && atoi(getenv("KRK_FILE_DIRECT")) > 0;
+    const bool want_direct = KRK_OP_ENV("KRK_FILE_DIRECT") && atoi(KRK_OP_ENV("KRK_FILE_DIRECT")) > 0;
     uint32_t* d_sums = nullptr;
     DevMem mem;
     KRK_HIP(mem.alloc(&d_sums, hi * 4));

@@ -21,6 +21,7 @@
 #include "../../include/kraken_hip_internal.h"
 #include "crc_math.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 
 namespace krk {
 
@@ -348,7 +349,7 @@ inline int init_device(Device& D, int id) {
     // Launch variant, read once per device context (crc32_pieces.hip: 16 = byte-addressable
     // tables with the work queue, the default; 7 = the same with a static item stride; 8,
     // 14, 15, 17 = measured alternatives; the rest only in the KRK_DIAG build).
-    const char* v = getenv("KRK_CRC_VARIANT");
+    const char* v = KRK_AB_ENV("KRK_CRC_VARIANT");
     const int want = v ? atoi(v) : 16;
     D.crc_variant = crc_variant_valid(want) ? want : 16;
     return KRK_OK;

@@ -24,6 +24,7 @@
 
 #include "../../include/kraken_hip_internal.h"
 #include "kernels.hpp"
+#include "knobs.hpp"
 #include "device_util.hpp"
 
 namespace krk {
@@ -1253,7 +1254,7 @@ static std::atomic<int> g_sha_plan{-1};
 static int sha_plan() {
     int p = g_sha_plan.load(std::memory_order_relaxed);
     if (p >= 0) return p;
-    const char* e = getenv("KRK_SHA_PLAN");
+    const char* e = KRK_AB_ENV("KRK_SHA_PLAN");  // krk_set_sha_plan is the run-time setter
     int want = e ? atoi(e) : KRK_SHA_PLAN_AUTO;
     if (!sha_plan_valid(want)) want = KRK_SHA_PLAN_AUTO;
     int expect = -1;

@@ -70,7 +70,7 @@ struct CopyTask {
 constexpr int kMaxWindows = 4;
 inline int staging_windows() {
     static const int n = [] {
-        const char* v = getenv("KRK_STAGING_WINDOWS");
+        const char* v = KRK_OP_ENV("KRK_STAGING_WINDOWS");
         const int x = v ? atoi(v) : 3;
         return std::min(kMaxWindows, std::max(2, x));
     }();
@@ -178,7 +178,7 @@ struct Pipeline {
 
 // KRK_TRACE=1: host-side phase times of the windowed host paths, to stderr.
 inline bool trace_on() {
-    static const bool on = getenv("KRK_TRACE") && atoi(getenv("KRK_TRACE")) > 0;
+    static const bool on = KRK_OP_ENV("KRK_TRACE") && atoi(KRK_OP_ENV("KRK_TRACE")) > 0;
     return on;
 }
 inline double wall_s() {
@@ -186,7 +186,7 @@ inline double wall_s() {
 }
 
 inline size_t window_bytes() {
-    const char* v = getenv("KRK_WINDOW_MB");
+    const char* v = KRK_OP_ENV("KRK_WINDOW_MB");
     size_t mb = v ? strtoull(v, nullptr, 10) : 512;
     if (mb < 1) mb = 1;
     return mb << 20;
@@ -290,7 +290,7 @@ class MappedAtHost {
 // KRK_COPY_THREADS overrides the split.
 
 inline unsigned copy_threads() {
-    const char* v = getenv("KRK_COPY_THREADS");
+    const char* v = KRK_AB_ENV("KRK_COPY_THREADS");
     if (v) return std::max(1u, (unsigned)strtoul(v, nullptr, 10));
     return std::max(1u, std::min(16u, (unsigned)host_threads_for_call()));
 }
@@ -343,7 +343,7 @@ struct ReadTask {
 // 0.91-1.07x, 8 MiB 0.91-1.00x -- no effect beyond the disk's run-to-run noise, so it is off
 // by default and the knob stays for disks where request size is the whole story.
 inline uint64_t file_readahead_bytes() {
-    const char* v = getenv("KRK_FILE_READAHEAD_MB");
+    const char* v = KRK_AB_ENV("KRK_FILE_READAHEAD_MB");
     return (v ? strtoull(v, nullptr, 10) : 0) << 20;
 }
 
@@ -411,7 +411,7 @@ inline long par_read(const std::vector<ReadTask>& tasks, bool direct, int* err) 
 // success, else the index of a failed task with *err its errno (0 = unexpected EOF);
 // -2 when AIO is unavailable (the caller reads synchronously).
 inline bool use_aio() {  // KRK_FILE_AIO=0: O_DIRECT chunks by synchronous preads (A/B)
-    const char* v = getenv("KRK_FILE_AIO");
+    const char* v = KRK_OP_ENV("KRK_FILE_AIO");
     return !(v && v[0] == '0');
 }
 // AIO contexts are kept for the process and reused: io_destroy waits out an RCU grace

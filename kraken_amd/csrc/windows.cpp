@@ -246,7 +246,7 @@ class FdPool {
 
   private:
     static uint64_t initial_budget() {
-        if (const char* e = getenv("KRK_FD_BUDGET"))  // tests: a small budget without touching the rlimit
+        if (const char* e = KRK_OP_ENV("KRK_FD_BUDGET"))  // tests: a small budget without touching the rlimit
             if (strtoull(e, nullptr, 10) > 0) return strtoull(e, nullptr, 10);
         struct rlimit rl {};
         if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return uint64_t(1) << 20;
@@ -519,7 +519,7 @@ std::atomic<int> g_host_gather{-2};  // -2: not read yet; krk_set_host_gather
 int host_gather_mode() {
     int m = g_host_gather.load(std::memory_order_relaxed);
     if (m != -2) return m;
-    const char* e = getenv("KRK_HOST_GATHER");
+    const char* e = KRK_OP_ENV("KRK_HOST_GATHER");
     int expect = -2;
     g_host_gather.compare_exchange_strong(expect, e ? (atoi(e) > 0 ? 1 : 0) : -1);
     return g_host_gather.load();
@@ -529,7 +529,7 @@ int host_gather_mode() {
 // pageable ones registered for the gather (KRK_HOST_GATHER) or staged.
 void setup_mem_filler(MemFiller& f, const krk_blob* blobs, uint64_t n, const std::vector<char>& on_host, Device* D) {
     // KRK_PINNED_DIRECT=0 stages pinned sources too (A/B)
-    static const bool allow_direct = !getenv("KRK_PINNED_DIRECT") || atoi(getenv("KRK_PINNED_DIRECT")) != 0;
+    static const bool allow_direct = !KRK_AB_ENV("KRK_PINNED_DIRECT") || atoi(KRK_AB_ENV("KRK_PINNED_DIRECT")) != 0;
     const int gm = host_gather_mode();
     f.pinned = allow_direct;
     uint64_t first = n;
@@ -581,7 +581,7 @@ int copy_out(void* dst, const void* src_dev, size_t n, const HostRegistry* reg, 
 
 // KRK_LIVE_CAP: overrides the window's live-stream cap (tests, sweeps).
 uint64_t live_cap_for(Device* D) {
-    const char* e = getenv("KRK_LIVE_CAP");
+    const char* e = KRK_OP_ENV("KRK_LIVE_CAP");
     const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
     return v ? v : window_stream_cap(D);
 }
@@ -925,7 +925,7 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     // disk queue from one thread: 16.3 GB/s against 11.7 for 16 threads' page-cache preads
     // of the same window chunks, profiles/r05/disk_probe_aio.jsonl) and a cached one reads
     // the page cache.
-    const char* fd_env = getenv("KRK_FILE_DIRECT");
+    const char* fd_env = KRK_OP_ENV("KRK_FILE_DIRECT");
     const bool direct = fd_env ? atoi(fd_env) > 0 : cold;
     FileFiller filler(files, n, direct);
     CallStats st;

@@ -43,3 +43,13 @@ def _gpu_session_settings(request):
     names itself."""
     if request.node.get_closest_marker("gpu"):
         request.getfixturevalue("gpu")
+
+
+def diag_lib() -> str:
+    """The diag build of the library (`make diag`: reads the A/B switches of knobs.hpp, which
+    the production library does not), built here if missing (build() ships it prebuilt)."""
+    import subprocess
+    path = os.path.join(ROOT, "kraken_amd", "lib", "diag", "libkraken_hip.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-j", "8", "-C", os.path.join(ROOT, "kraken_amd", "csrc"), "diag"])
+    return path

@@ -147,14 +147,17 @@ print(" ".join(out))
 
 
 def test_info_hash_sha_ni_matches_portable_sha1(tmp_path):
-    """The SHA-NI compressor (when this CPU has it) and the portable one agree."""
+    """The SHA-NI compressor (when this CPU has it) and the portable one agree: the production
+    library against the diag build with KRK_SHA1_PORTABLE=1 (an A/B switch production does
+    not read, knobs.hpp)."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     f = tmp_path / "ih.py"
     f.write_text(_IH_SCRIPT)
-    runs = [subprocess.run([sys.executable, str(f), root], capture_output=True, text=True,
-                           env={**os.environ, "KRK_SHA1_PORTABLE": v}) for v in ("0", "1")]
+    from tests.conftest import diag_lib
+    runs = [subprocess.run([sys.executable, str(f), root], capture_output=True, text=True, env=env)
+            for env in (dict(os.environ), {**os.environ, "KRK_SHA1_PORTABLE": "1", "KRK_LIB_PATH": diag_lib()})]
     assert all(r.returncode == 0 for r in runs), [r.stderr for r in runs]
     assert runs[0].stdout == runs[1].stdout and len(runs[0].stdout.split()) == 43
 
@@ -243,15 +246,18 @@ print(" ".join(out))
 
 def test_host_crossover_ni_matches_portable(tmp_path):
     """SHA-NI / PCLMULQDQ / VPCLMULQDQ routines (when this CPU has them) equal the portable
-    ones (KRK_HOST_CRC_AVX512=0: the 128-bit PCLMUL loop)."""
+    ones (KRK_HOST_CRC_AVX512=0: the 128-bit PCLMUL loop): the production library against the
+    diag build with those A/B switches set (production does not read them, knobs.hpp)."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     f = tmp_path / "h.py"
     f.write_text(_HOST_SCRIPT)
+    from tests.conftest import diag_lib
     runs = [subprocess.run([sys.executable, str(f), root], capture_output=True, text=True,
-                           env={**os.environ, "KRK_HOST_PORTABLE": v, "KRK_HOST_CRC_AVX512": a})
-            for v, a in (("0", "1"), ("1", "1"), ("0", "0"))]
+                           env={**os.environ, **extra})
+            for extra in ({}, {"KRK_LIB_PATH": diag_lib(), "KRK_HOST_PORTABLE": "1", "KRK_HOST_CRC_AVX512": "1"},
+                          {"KRK_LIB_PATH": diag_lib(), "KRK_HOST_PORTABLE": "0", "KRK_HOST_CRC_AVX512": "0"})]
     assert all(r.returncode == 0 for r in runs), [r.stderr for r in runs]
     assert runs[0].stdout == runs[1].stdout == runs[2].stdout and len(runs[0].stdout.split()) == 10
 
@@ -765,3 +771,34 @@ def test_tail_handoff_model_accounts_every_byte():
     # no faster than all of it on the host threads plus every GPU stream at once
     assert m["end_s"] >= total / (15 * m["thread_rate_Bps"] + len(lens) * 58.5e6)
     assert m["takeovers"] >= 15
+
+
+def test_production_library_reads_only_the_operator_knobs():
+    """the production library's environment is INTEGRATION.md's operator
+    table, exactly -- every KRK_* name in its strings is in the table and every table entry is
+    one it reads; the A/B switches of measurement sessions (knobs.hpp KRK_AB_ENV) are read by
+    the diag build only.  Every library source reads its environment through knobs.hpp."""
+    import glob
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    a = doc.index("## Operator knobs")
+    b = doc.find("\n## ", a + 1)
+    table = set()
+    for line in doc[a:b if b > 0 else None].splitlines():
+        if line.startswith("| `KRK_"):
+            table |= set(re.findall(r"`(KRK_[A-Z0-9_]+)`", line.split("|")[1]))
+    blob = open(_capi.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"KRK_[A-Z0-9_]+", blob))
+    read = {n.decode() for n in names}
+    assert read == table, ("read, not in the table", sorted(read - table), "table, not read", sorted(table - read))
+    src = ""
+    for p in glob.glob(os.path.join(root, "kraken_amd", "csrc", "*.[ch]*")):
+        if not p.endswith("knobs.hpp"):
+            src += open(p).read()
+    bare = re.findall(r'getenv\("(KRK_[A-Z0-9_]+)"\)', src)
+    assert not bare, f"KRK_* read outside knobs.hpp: {sorted(set(bare))}"
+    op = set(re.findall(r'KRK_OP_ENV\("(KRK_[A-Z0-9_]+)"\)', src))
+    ab = set(re.findall(r'KRK_AB_ENV\("(KRK_[A-Z0-9_]+)"\)', src))
+    assert op == table and not op & ab, (sorted(op ^ table), sorted(op & ab))

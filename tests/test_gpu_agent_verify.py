@@ -117,25 +117,42 @@ def _place_stripes(arr, stripe):
     return libc.syscall(279, 0, ctypes.c_ulong(n), pages, dst, status, 2) == 0  # SYS_move_pages, MPOL_MF_MOVE
 
 
+_NUMA_SCRIPT = r"""
+import mmap, sys, zlib
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from tests.test_gpu_agent_verify import _place_stripes
+from kraken_amd import device as D
+D.set_device(0)
+P, L = 256 << 10, 192 << 20
+for shift in (0, 4 << 20):
+    m = mmap.mmap(-1, L)
+    arr = np.frombuffer(m, dtype=np.uint8)
+    arr[:] = np.random.default_rng(7).integers(0, 256, L, dtype=np.uint8)
+    _place_stripes(arr, 8 << 20)
+    blob = arr[shift:]
+    (s,) = D.piece_sums_host([blob], P)
+    want = [zlib.crc32(blob[k:k + P].tobytes()) for k in range(0, blob.size, P)]
+    assert [int(x) for x in s] == want, shift
+    del arr, blob, s
+    m.close()
+print("ok")
+"""
+
+
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
-def test_host_crc_numa_handout_bit_exact(gpu, monkeypatch, mode):
-    """The host CRC share's NUMA-aware hand-out (KRK_CRC_NUMA: 0 one cursor, 1 per-node
-    claims, 2 per-node claims + node visits, the default) over a buffer whose 8 MiB runs sit
-    on alternating nodes (and on a half-stripe offset, so every task straddles two nodes and
-    is never visited): every task is summed once, the sums are zlib's."""
-    import mmap
-    from kraken_amd import device as D
-    monkeypatch.setenv("KRK_CRC_NUMA", mode)
-    monkeypatch.setenv("KRK_CRC_GPU_FRACTION", "0")  # every byte through the host hand-out
-    P, L = 256 << 10, 192 << 20
-    for shift in (0, 4 << 20):
-        m = mmap.mmap(-1, L)
-        arr = np.frombuffer(m, dtype=np.uint8)
-        arr[:] = np.random.default_rng(7).integers(0, 256, L, dtype=np.uint8)
-        _place_stripes(arr, 8 << 20)
-        blob = arr[shift:]
-        (s,) = D.piece_sums_host([blob], P)
-        want = [zlib.crc32(blob[k:k + P].tobytes()) for k in range(0, blob.size, P)]
-        assert [int(x) for x in s] == want
-        del arr, blob, s
-        m.close()
+def test_host_crc_numa_handout_bit_exact(gpu, mode):
+    """The host CRC share's NUMA-aware hand-out (KRK_CRC_NUMA: 0 one cursor, the default; 1
+    per-node claims; 2 per-node claims + node visits) over a buffer whose 8 MiB runs sit on
+    alternating nodes (and on a half-stripe offset, so every task straddles two nodes and is
+    never visited): every task is summed once, the sums are zlib's.  KRK_CRC_NUMA is an A/B
+    switch (knobs.hpp): the diag build reads it, once a process, so each mode runs in a fresh
+    process on that build."""
+    import subprocess
+    import sys
+    from tests.conftest import ROOT, diag_lib
+    env = dict(os.environ, KRK_CRC_NUMA=mode, KRK_CRC_GPU_FRACTION="0",  # every byte through the host hand-out
+               KRK_LIB_PATH=diag_lib())
+    r = subprocess.run([sys.executable, "-c", _NUMA_SCRIPT, ROOT], capture_output=True, text=True, timeout=240,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-3000:]

@@ -343,7 +343,10 @@ def test_piece_stream_failure_mid_stream(gpu):
     (fault injected: the 2nd CRC launch of the engine) poisons the stream -- its later
     portions are not folded into sums the failed request never wrote -- and the error
     comes back from update/end; the engine serves later calls correctly."""
-    out = _run_script(_FAIL_SCRIPT, {"KRK_ENGINE_FAIL_CRC_LAUNCH": "2", "KRK_CRC_HOST_MAX": "1"})
+    from tests.conftest import diag_lib
+    # fault injection is an A/B hook: the diag build reads it (knobs.hpp), production does not
+    out = _run_script(_FAIL_SCRIPT, {"KRK_ENGINE_FAIL_CRC_LAUNCH": "2", "KRK_CRC_HOST_MAX": "1",
+                                     "KRK_LIB_PATH": diag_lib()})
     rc, msg, ok = [x.strip() for x in out.strip().splitlines()[-1].split("|")]
     assert int(rc) != 0 and "injected failure" in msg, out
     assert ok == "True"
