@@ -121,7 +121,7 @@ def test_sha256_resume_from_device_bytes(gpu, orc):
     3 ...), equals hashlib over the whole blob."""
     import ctypes as C
     from kraken_amd.windowed import _IV
-    for L, cuts in ((0, []), (1, []), (55, []), (64, [64]), (130, [64]), ((8 << 20) + 3, [1 << 20, 3 << 20]),
+    for L, cuts in ((0, []), (1, []), (55, []), (64, []), (128, [64]), (130, [64]), ((8 << 20) + 3, [1 << 20, 3 << 20]),
                     ((17 << 20) + 64, [64, (16 << 20) + 64])):
         data = orc.synth(4242 + L, L)
         buf = D.DeviceBuffer(max(L, 1))
