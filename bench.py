@@ -348,15 +348,17 @@ def roofline_obj(kernel, gbps, avg_ms, bytes_launch, traffic):
 
 
 def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
-    """sha256_multi is bound by per-stream VALU issue, not HBM: one sequential
-    Merkle-Damgard chain per blob.  peak = streams x the ISA per-stream ceiling; the
-    HBM fraction is kept beside it."""
+    """sha256_multi against the HBM roofline the contract prices every kernel on (peak = the
+    8 TB/s spec, frac = achieved / peak: ~0.007, VERDICT r05 weak #2 -- the headline shows
+    it).  What actually bounds it is per-stream VALU issue (one sequential Merkle-Damgard
+    chain per blob): `issue_bound` / `valu` give the streams x ISA per-stream ceiling and the
+    fraction of it, beside the HBM one."""
     lanes = D.sha_lanes_per_stream(n)
     per_stream = max(lens) / (avg_ms / 1e3) / 1e6
-    roof = {"kernel": "sha256_multi", "bound": "valu", "achieved": round(gbps, 4),
-            "peak": None, "unit": "GB/s", "frac": None, "traffic": traffic, "avg_launch_ms": round(avg_ms, 3),
-            "algorithmic_bytes_per_launch": bytes_launch,
-            "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5)}}
+    roof = {"kernel": "sha256_multi", "bound": "hbm", "achieved": round(gbps, 4),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 5), "traffic": traffic,
+            "avg_launch_ms": round(avg_ms, 3), "algorithmic_bytes_per_launch": bytes_launch,
+            "valu": {"peak": None, "unit": "GB/s", "frac": None}}
     if traffic is not None:
         roof["traffic_source"] = TRAFFIC_SOURCE
     ib = {"achieved_per_stream_MBps": round(per_stream, 2), "streams": n, "lanes_per_stream": lanes}
@@ -372,7 +374,8 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
                                           "cycles per VALU for a lone wave (MI355X_MICROARCH.md:489) at the "
                                           "shader clock measured beside a SHA launch (krk_device_clock_mhz)")})
             peak = n * ceil / 1e3
-            roof.update({"peak": round(peak, 4), "frac": round(gbps / peak, 4)})
+            roof["valu"] = {"peak": round(peak, 4), "unit": "GB/s", "frac": round(gbps / peak, 4),
+                            "what": "streams x the ISA per-stream ceiling (issue_bound)"}
             import sha_isa
             fc = sha_isa.fetch_ceiling_mbps(isa, mhz)
             ib["fetch_bound"] = {"code_bytes_per_block": isa["code_bytes_per_block"],
@@ -385,10 +388,11 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
             ib["ceiling_error"] = isa.get("error")
     roof["issue_bound"] = ib
     waves = -(-n // (64 // lanes)) if lanes in (2, 8) else -(-n // 64)
-    roof["note"] = (f"bound 'valu': SHA-256 is one sequential Merkle-Damgard chain per blob ({lanes} lane(s) each "
-                    f"here), so the kernel is bound by the per-stream VALU issue of its consumer waves ({waves} of the "
-                    f"chip's 1,024 SIMDs for {n:,} streams), not by HBM; peak = streams x ISA per-stream ceiling, "
-                    "hbm.frac beside it; fetch_bound = the same loop priced by its code bytes (DESIGN.md 4.2)")
+    roof["note"] = (f"peak/frac: the HBM roofline (8 TB/s spec). SHA-256 is one sequential Merkle-Damgard chain per "
+                    f"blob ({lanes} lane(s) each here), so the kernel is bound by the per-stream VALU issue of its "
+                    f"consumer waves ({waves} of the chip's 1,024 SIMDs for {n:,} streams), far below HBM: valu.frac = "
+                    "achieved / (streams x ISA per-stream ceiling); fetch_bound = the same loop priced by its code "
+                    "bytes (DESIGN.md 4.2)")
     return roof
 
 
@@ -1306,12 +1310,10 @@ def run_chunked(a, D, T, rank, world, res):
     if sha_n:
         gbps = bytes_rank / (sha_ms / 1e3) / 1e9
         roof = roofline_obj("sha256_multi", gbps, sha_ms / sha_n, bytes_rank / sha_n, None)
-        roof.update({"bound": "valu", "hbm": {"peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                              "frac": round(gbps / HBM_PEAK_GBPS, 5)}})
+        roof["chain"] = {"peak": None, "frac": None}
         # The chain bound: no schedule finishes before the longest blob's chain, which runs
         # at the per-stream ISA ceiling of the plan the first (largest) window takes.
         lanes = D.sha_lanes_per_stream(int(min(wr.cap, n)))
-        roof.update({"peak": None, "frac": None})
         if lanes in (2, 8) and not a.no_ceiling:
             import ctypes as C
             import sha_isa
@@ -1321,16 +1323,17 @@ def run_chunked(a, D, T, rank, world, res):
                 D.check(D.lib.krk_device_clock_mhz(None, C.byref(mhz)))
                 ceil = sha_isa.ceiling_mbps(isa, mhz.value)
                 peak = bytes_rank / (max(lens) / (ceil * 1e6)) / 1e9
-                roof.update({"peak": round(peak, 2), "frac": round(gbps / peak, 4),
-                             "chain_bound": {"longest_blob": max(lens), "lanes_per_stream": lanes,
+                roof["chain"] = {"peak": round(peak, 2), "frac": round(gbps / peak, 4)}
+                roof.update({"chain_bound": {"longest_blob": max(lens), "lanes_per_stream": lanes,
                                              "ceiling_per_stream_MBps": round(ceil, 2),
                                              "clock_mhz": round(mhz.value, 1),
                                              "source": "tools/sha_isa.py VALU per block x 4 cycles, idle clock"}})
             except Exception as e:  # tools missing on the box: report, never guess
                 roof["ceiling_error"] = f"{type(e).__name__}: {e}"
-        roof["note"] = ("bound 'valu' (DESIGN.md 4.2): achieved = SHA bytes / summed SHA launch time; peak = the "
-                        "bytes over the longest blob's chain at the per-stream ISA ceiling (no schedule beats it); "
-                        "the windows shrink as blobs finish, so late launches carry few streams")
+        roof["note"] = ("peak/frac: the HBM roofline (8 TB/s spec); achieved = SHA bytes / summed SHA launch time. "
+                        "What bounds it is VALU issue along the longest chain (DESIGN.md 4.2): chain.peak = the bytes "
+                        "over the longest blob's chain at the per-stream ISA ceiling (no schedule beats it); the "
+                        "windows shrink as blobs finish, so late launches carry few streams")
         res["roofline"] = roof
     dg = cb.digests.to_host(np.uint8, 32 * n).reshape(-1, 32)
     sums = cb.sums.to_host(np.uint32, max(cb.total_pieces, 1))
