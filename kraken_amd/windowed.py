@@ -544,20 +544,34 @@ class TailHandoffRun:
                                 np.int64(self.cb.piece_lengths[b]), np.uint64(soff), np.uint64(b))
             D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), 1, self.cb.sums.ptr, s))
 
+        clk = self._clock
+        tq = clk()
         queue(0)
+        ph = self._phase[i]
+        ph["queue"] += clk() - tq
         h = _IV.copy()
         if y:
+            tw = clk()
             D.check(D.lib.krk_event_sync(ev))  # the window that last advanced chain b is done
             D.check(D.lib.krk_memcpy_d2h(h.ctypes.data_as(C.c_void_p), C.c_void_p(self.cb.state.ptr + 32 * b), 32))
+            ph["midstate"] += clk() - tw
         out = np.zeros(32, dtype=np.uint8)
         for c in range(nch):
+            tq = clk()
             if c + 1 < nch:
                 queue(c + 1)
+            t1 = clk()
+            D.check(D.lib.krk_stream_sync(s))  # this piece generated (and the next queued behind it)
+            t2 = clk()
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
             D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), o,
                                                         C.c_void_p(self.tbuf[i][c & 1].ptr), m, int(c + 1 == nch),
                                                         out.ctypes.data_as(C.POINTER(C.c_uint8)), s))
+            t3 = clk()
+            ph["queue"] += t1 - tq
+            ph["device"] += t2 - t1
+            ph["hash"] += t3 - t2
             with self._mu:
                 self._left[i] -= m
                 self._t_last[i] = self._clock()
@@ -602,6 +616,7 @@ class TailHandoffRun:
         self._left = [0] * self.H
         self._t_last = [0.0] * self.H
         self._busy_s = [0.0] * self.H
+        self._phase = [{"queue": 0.0, "midstate": 0.0, "device": 0.0, "hash": 0.0} for _ in range(self.H)]
         self._done = False
         dig = np.zeros((n, 32), dtype=np.uint8)
         err = []
@@ -699,6 +714,7 @@ class TailHandoffRun:
                       "takeovers": takes, "resumed_from_midstate": resumed, "host_chains": len(host_blobs),
                       "host_bytes": host_bytes,
                       "thread_busy_s": [round(x, 3) for x in self._busy_s],
+                      "thread_phases_s": {k: round(sum(p[k] for p in self._phase), 3) for k in self._phase[0]},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
 
     def _items(self, win, k):
