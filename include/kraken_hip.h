@@ -267,7 +267,8 @@ typedef struct krk_chunk {
 int krk_metainfo_digest_chunks_dev(const krk_chunk* chunks, uint64_t n_chunks, uint32_t* state_dev,
                                    uint32_t* sums_dev, uint8_t* digests_dev, void* stream);
 /* The same with the SHA-256 launch on `sha_stream` (NULL: the library's own), forked from
- * and joined back into `stream` like the default.  A caller that runs D2H copies beside
+ * and joined back into `stream` like the default; with a sha_stream the piece CRCs run on
+ * `stream` itself (no barrier of the step on the library's streams).  A caller that runs D2H copies beside
  * the windows (the C3 host lane, kraken_amd/windowed.py) passes a stream of another
  * priority (krk_stream_create_prio): streams of one priority share the device's few
  * hardware queues, and a copy queued behind a window's ~0.6 s SHA-256 launch on a shared

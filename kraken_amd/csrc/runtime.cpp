@@ -1150,10 +1150,15 @@ static int validate_chunks(const krk_chunk* c, uint64_t n) {
     return KRK_OK;
 }
 
-// One window step over device chunks: SHA jobs on D->s_a, CRC items on D->s_b,
-// both forked from and joined back into s.
+// One window step over device chunks: SHA jobs on D->s_a, CRC items on D->s_b, both
+// forked from and joined back into s.  With the caller's SHA stream `ks`, the CRC items run
+// on s itself: a caller that keeps its window streams at high priority (the C3 tail
+// handoff, kraken_amd/windowed.py) then leaves no fork / join barrier of a window on the
+// library's normal-priority streams, whose hardware queues its copy threads share -- a
+// barrier waiting for a window's ~70 ms SHA launch blocks every packet behind it there.
 static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
                        uint8_t* digests_dev, hipStream_t s, ItemBuilder& B, hipStream_t ks = nullptr) {
+    const hipStream_t kc = ks ? s : D->s_b;
     if (!ks) ks = D->s_a;
     std::vector<ShaJob> jobs(n);
     CrcBatch items;
@@ -1176,13 +1181,15 @@ static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* stat
     KRK_HIP(hipEventCreateWithFlags(&j2, hipEventDisableTiming));
     KRK_HIP(hipEventRecord(fork, s));
     KRK_HIP(hipStreamWaitEvent(ks, fork, 0));
-    KRK_HIP(hipStreamWaitEvent(D->s_b, fork, 0));
+    if (kc != s) KRK_HIP(hipStreamWaitEvent(kc, fork, 0));
     int r = run_jobs(D, jobs, digests_dev, state_dev, ks);
-    if (!r) r = run_items(D, items, sums_dev, D->s_b);
+    if (!r) r = run_items(D, items, sums_dev, kc);
     hipEventRecord(j1, ks);
-    hipEventRecord(j2, D->s_b);
     hipStreamWaitEvent(s, j1, 0);
-    hipStreamWaitEvent(s, j2, 0);
+    if (kc != s) {
+        hipEventRecord(j2, kc);
+        hipStreamWaitEvent(s, j2, 0);
+    }
     hipEventDestroy(fork);
     hipEventDestroy(j1);
     hipEventDestroy(j2);

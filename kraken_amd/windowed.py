@@ -509,10 +509,12 @@ class TailHandoffRun:
         self.cb = D.ChunkedBatch(self.lens, P)
         self.tbuf = [[D.DeviceBuffer(TAIL_PIECE), D.DeviceBuffer(TAIL_PIECE)] for _ in range(self.H)]
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        D.check(D.lib.krk_stream_create(C.byref(self.run_s)))
+        # the windows' streams at high priority, i.e. on hardware queues of their own: a
+        # window's SHA-256 launch, its CRC (on run_s beside it) and the barrier joining them
+        # stay off the normal-priority queues the threads' generator / CRC launches and copies
+        # share, where a packet behind such a barrier waits for the whole window
+        D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
-        # the windows' SHA-256 launches on hardware queues of their own (high priority): the
-        # threads' copies and generator / CRC launches must not queue behind a window's launch
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
         self.t_s = []
         for _ in range(self.H):
