@@ -516,10 +516,15 @@ class TailHandoffRun:
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
-        self.t_s = []
-        for _ in range(self.H):
+        self.t_s, self.t_idle, self.t_ev = [], [], []
+        for _ in range(self.H):  # a thread's generator / CRC stream, an idle one, two events
             self.t_s.append(C.c_void_p())
             D.check(D.lib.krk_stream_create(C.byref(self.t_s[-1])))
+            self.t_idle.append(C.c_void_p())
+            D.check(D.lib.krk_stream_create(C.byref(self.t_idle[-1])))
+            self.t_ev.append([C.c_void_p(), C.c_void_p()])
+            for e in self.t_ev[-1]:
+                D.check(D.lib.krk_event_create(C.byref(e)))
         self.stats = {}
 
     # ---- one thread's chains
@@ -534,14 +539,19 @@ class TailHandoffRun:
         nch = max(1, -(-rest // TAIL_PIECE))
         soff = int(self.cb.sums_off[b])
 
+        evg = self.t_ev[i]
+
         def queue(c):
+            """Piece c generated into buffer c & 1 (event evg[c & 1] after it), then its CRCs."""
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
             if m <= 0:
+                D.check(D.lib.krk_event_record(evg[c & 1], s))
                 return
             ptr = np.array([self.tbuf[i][c & 1].ptr], dtype=np.uint64)
             D.synth_fill_chunk_arrays(self.ids[b:b + 1], ptr, np.array([o], np.uint64), np.array([m], np.uint64),
                                       stream=s)
+            D.check(D.lib.krk_event_record(evg[c & 1], s))
             arr = D.chunk_array(ptr, np.array([o], np.uint64), np.array([m], np.uint64), np.uint64(L),
                                 np.int64(self.cb.piece_lengths[b]), np.uint64(soff), np.uint64(b))
             D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), 1, self.cb.sums.ptr, s))
@@ -563,13 +573,14 @@ class TailHandoffRun:
             if c + 1 < nch:
                 queue(c + 1)
             t1 = clk()
-            D.check(D.lib.krk_stream_sync(s))  # this piece generated (and the next queued behind it)
+            D.check(D.lib.krk_event_sync(evg[c & 1]))  # piece c generated; c + 1 (and c's CRCs) run meanwhile
             t2 = clk()
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
+            # ordered by the event above, not by a stream: the call waits for nothing else
             D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), o,
                                                         C.c_void_p(self.tbuf[i][c & 1].ptr), m, int(c + 1 == nch),
-                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), s))
+                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), self.t_idle[i]))
             t3 = clk()
             ph["queue"] += t1 - tq
             ph["device"] += t2 - t1
@@ -735,10 +746,15 @@ class TailHandoffRun:
         for b in self.bufs + [x for pair in self.tbuf for x in pair]:
             b.free()
         self.bufs, self.tbuf = [], []
-        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s:
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s + self.t_idle:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s, self.run_s, self.sha_s, self.t_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), []
+        for pair in self.t_ev:
+            for e in pair:
+                if e.value:
+                    self.D.lib.krk_event_destroy(e)
+        self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self.t_s, self.t_idle, self.t_ev = [], [], []
 
     def __del__(self):
         try:
