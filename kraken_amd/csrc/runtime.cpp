@@ -1996,6 +1996,12 @@ int krk_event_record(void* ev, void* stream) {
     KRK_HIP(hipEventRecord(static_cast<hipEvent_t>(ev), pick(D, stream)));
     return KRK_OK;
 }
+int krk_stream_wait_event(void* stream, void* ev) {
+    KRK_CHECK(ev, KRK_EINVAL, "event is NULL");
+    KRK_DEVICE(D);
+    KRK_HIP(hipStreamWaitEvent(pick(D, stream), static_cast<hipEvent_t>(ev), 0));
+    return KRK_OK;
+}
 int krk_event_sync(void* ev) {
     KRK_CHECK(ev, KRK_EINVAL, "event is NULL");
     KRK_HIP(hipEventSynchronize(static_cast<hipEvent_t>(ev)));

@@ -352,6 +352,7 @@ TAIL_PIECE = 64 << 20  # device bytes a tail thread generates, CRCs and hashes a
 # are left live (modelled on rank 0's shard of an 8-GPU C3: 1/2/4/8 MiB end at 11.7 / 11.7
 # / 12.0 / 12.7 s with 0.5 ms a launch, 12.7 / 12.2 / 12.3 / 12.9 s with 3 ms).
 TAIL_CHUNK = 4 << 20
+TAIL_RING = 6  # device pieces a tail thread keeps in flight (generated / hashed / waiting for their CRC)
 
 
 def tail_thread_rate(rates, threads):
@@ -507,7 +508,7 @@ class TailHandoffRun:
         wb = self.W + 16 * max(min(self.cap, n), 1)
         self.bufs = [D.DeviceBuffer(wb), D.DeviceBuffer(wb)]
         self.cb = D.ChunkedBatch(self.lens, P)
-        self.tbuf = [[D.DeviceBuffer(TAIL_PIECE), D.DeviceBuffer(TAIL_PIECE)] for _ in range(self.H)]
+        self.tbuf = [[D.DeviceBuffer(TAIL_PIECE) for _ in range(TAIL_RING)] for _ in range(self.H)]
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
         # the windows' streams at high priority, i.e. on hardware queues of their own: a
         # window's SHA-256 launch, its CRC (on run_s beside it) and the barrier joining them
@@ -516,15 +517,15 @@ class TailHandoffRun:
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
-        self.t_s, self.t_idle, self.t_ev = [], [], []
-        for _ in range(self.H):  # a thread's generator / CRC stream, an idle one, two events
-            self.t_s.append(C.c_void_p())
-            D.check(D.lib.krk_stream_create(C.byref(self.t_s[-1])))
-            self.t_idle.append(C.c_void_p())
-            D.check(D.lib.krk_stream_create(C.byref(self.t_idle[-1])))
-            self.t_ev.append([C.c_void_p(), C.c_void_p()])
-            for e in self.t_ev[-1]:
+        self.t_s, self.t_crc, self.t_idle, self.t_ev = [], [], [], []
+        for _ in range(self.H):  # a thread's generator, CRC and idle streams; an event pair per ring slot
+            for lst in (self.t_s, self.t_crc, self.t_idle):
+                lst.append(C.c_void_p())
+                D.check(D.lib.krk_stream_create(C.byref(lst[-1])))
+            ev = ([C.c_void_p() for _ in range(TAIL_RING)], [C.c_void_p() for _ in range(TAIL_RING)])
+            for e in ev[0] + ev[1]:
                 D.check(D.lib.krk_event_create(C.byref(e)))
+            self.t_ev.append(ev)
         self.stats = {}
 
     # ---- one thread's chains
@@ -533,28 +534,40 @@ class TailHandoffRun:
         their CRCs queued on the GPU, SHA-256 continued on this thread from the midstate the
         windows left in HBM (window event `ev`), or from the IV when y == 0."""
         D = self.D
-        s = self.t_s[i]
         L = int(self.lens[b])
         rest = L - y
         nch = max(1, -(-rest // TAIL_PIECE))
         soff = int(self.cb.sums_off[b])
 
-        evg = self.t_ev[i]
+        gen_s, crc_s, bufs = self.t_s[i], self.t_crc[i], self.tbuf[i]
+        evg, evc = self.t_ev[i]
+        R = len(bufs)
+        base = self._seq[i]  # the thread's pieces so far: the ring runs on across its chains
+        self._seq[i] += nch
 
         def queue(c):
-            """Piece c generated into buffer c & 1 (event evg[c & 1] after it), then its CRCs."""
+            """Piece c generated into ring slot c % R (event evg after it) on the thread's generator
+            stream; its CRCs on the thread's CRC stream once generated.  The CRC launch (144 KiB of
+            LDS a workgroup) waits for a CU the window's SHA-256 workgroups leave free -- often the
+            window's end -- so it runs on a stream of its own and the generator only waits for the
+            CRC of the piece R back, whose slot it refills."""
+            k = (base + c) % R
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
-            if m <= 0:
-                D.check(D.lib.krk_event_record(evg[c & 1], s))
-                return
-            ptr = np.array([self.tbuf[i][c & 1].ptr], dtype=np.uint64)
-            D.synth_fill_chunk_arrays(self.ids[b:b + 1], ptr, np.array([o], np.uint64), np.array([m], np.uint64),
-                                      stream=s)
-            D.check(D.lib.krk_event_record(evg[c & 1], s))
-            arr = D.chunk_array(ptr, np.array([o], np.uint64), np.array([m], np.uint64), np.uint64(L),
-                                np.int64(self.cb.piece_lengths[b]), np.uint64(soff), np.uint64(b))
-            D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), 1, self.cb.sums.ptr, s))
+            if base + c >= R:
+                D.check(D.lib.krk_stream_wait_event(gen_s, evc[k]))
+            if m > 0:
+                ptr = np.array([bufs[k].ptr], dtype=np.uint64)
+                D.synth_fill_chunk_arrays(self.ids[b:b + 1], ptr, np.array([o], np.uint64), np.array([m], np.uint64),
+                                          stream=gen_s)
+            D.check(D.lib.krk_event_record(evg[k], gen_s))
+            if m > 0:
+                D.check(D.lib.krk_stream_wait_event(crc_s, evg[k]))
+                arr = D.chunk_array(ptr, np.array([o], np.uint64), np.array([m], np.uint64), np.uint64(L),
+                                    np.int64(self.cb.piece_lengths[b]), np.uint64(soff), np.uint64(b))
+                D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), 1, self.cb.sums.ptr,
+                                                 crc_s))
+            D.check(D.lib.krk_event_record(evc[k], crc_s))
 
         clk = self._clock
         tq = clk()
@@ -573,13 +586,13 @@ class TailHandoffRun:
             if c + 1 < nch:
                 queue(c + 1)
             t1 = clk()
-            D.check(D.lib.krk_event_sync(evg[c & 1]))  # piece c generated; c + 1 (and c's CRCs) run meanwhile
+            D.check(D.lib.krk_event_sync(evg[(base + c) % R]))  # piece c generated; c + 1 and the CRCs run meanwhile
             t2 = clk()
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
             # ordered by the event above, not by a stream: the call waits for nothing else
             D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), o,
-                                                        C.c_void_p(self.tbuf[i][c & 1].ptr), m, int(c + 1 == nch),
+                                                        C.c_void_p(bufs[(base + c) % R].ptr), m, int(c + 1 == nch),
                                                         out.ctypes.data_as(C.POINTER(C.c_uint8)), self.t_idle[i]))
             t3 = clk()
             ph["queue"] += t1 - tq
@@ -630,6 +643,7 @@ class TailHandoffRun:
         self._t_last = [0.0] * self.H
         self._busy_s = [0.0] * self.H
         self._phase = [{"queue": 0.0, "midstate": 0.0, "device": 0.0, "hash": 0.0} for _ in range(self.H)]
+        self._seq = [0] * self.H
         self._done = False
         dig = np.zeros((n, 32), dtype=np.uint8)
         err = []
@@ -715,7 +729,7 @@ class TailHandoffRun:
             for e in evs:
                 D.lib.krk_event_destroy(e)
             raise err[0]
-        for s in self.t_s:  # the tails' CRCs
+        for s in self.t_crc:  # the tails' CRCs
             D.check(D.lib.krk_stream_sync(s))
         for e in evs:
             D.lib.krk_event_destroy(e)
@@ -746,15 +760,15 @@ class TailHandoffRun:
         for b in self.bufs + [x for pair in self.tbuf for x in pair]:
             b.free()
         self.bufs, self.tbuf = [], []
-        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s + self.t_idle:
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s + self.t_crc + self.t_idle:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        for pair in self.t_ev:
-            for e in pair:
+        for evg, evc in self.t_ev:
+            for e in evg + evc:
                 if e.value:
                     self.D.lib.krk_event_destroy(e)
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        self.t_s, self.t_idle, self.t_ev = [], [], []
+        self.t_s, self.t_crc, self.t_idle, self.t_ev = [], [], [], []
 
     def __del__(self):
         try:
