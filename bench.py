@@ -1274,6 +1274,13 @@ def run_chunked(a, D, T, rank, world, res):
     shard_world = a.emulate_world or world
     ids, lens, P = workload_blobs(a.workload, rank, shard_world, a.blobs)
     n = len(lens)
+    if a.c3_tail_only:  # a measurement run of the tail handoff alone (no value line)
+        res.update({"metric": "C3 tail handoff only (measurement run)", "value": None, "unit": "GB/s",
+                    "config": {"workload": WORKLOADS["c3"]["desc"], "blobs_this_rank": n,
+                               "emulated_world": shard_world}})
+        res["tail_handoff"] = run_tail_handoff(a, D, T, ids, lens, P, int(sum(c3_lengths(a.blobs or 20000))),
+                                               None, None)
+        return
     wr = WindowedRun(D, ids, lens, P, a.window_gib << 30,
                      cap=n if a.no_admission else (a.live_cap or None))
     T.barrier()
@@ -1412,7 +1419,7 @@ def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
     beside the GPU-only value (never as it), with the same policy modelled on the planner's
     rates (windowed.simulate_tail_handoff) and the outputs compared with the GPU-only run's."""
     from kraken_amd.windowed import TAIL_CHUNK, TailHandoffRun, simulate_tail_handoff, window_stream_cap
-    threads = max(1, host_cores() - 1)  # one core stays with the window loop
+    threads = a.tail_threads or max(1, host_cores() - 1)  # one core stays with the window loop
     cap = len(lens) if a.no_admission else (a.live_cap or window_stream_cap(D, len(lens)))
     live = min(cap, len(lens))
     # windows of <= 4 MiB a live chain (a ~70 ms SHA launch at eight lanes): a chain is handed
@@ -1443,7 +1450,8 @@ def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
     tr.close()
     out.update({"value": round(total_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el * 1e3, 3),
                 "measured_over_model": round(el / model["end_s"], 4), **tr.stats,
-                "matches_gpu_only": bool(np.array_equal(dg2, dg) and np.array_equal(s2, sums))})
+                **({"matches_gpu_only": bool(np.array_equal(dg2, dg) and np.array_equal(s2, sums))}
+                   if dg is not None else {})})
     return out
 
 
@@ -2282,6 +2290,9 @@ def main():
     ap.add_argument("--tail-handoff", action="store_true",
                     help="C3: also run the batch with the tail handoff (host threads steal the chains with the most "
                          "bytes left at window boundaries), reported as tail_handoff beside the GPU-only value")
+    ap.add_argument("--tail-threads", type=int, default=0, help="C3 tail handoff: host threads (0 = the CPU budget - 1)")
+    ap.add_argument("--c3-tail-only", action="store_true",
+                    help="C3: skip the GPU-only windows (measurement runs of the tail handoff; no value line)")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")
     ap.add_argument("--regen-serial", action="store_true",
                     help="c5regen: piece sums then InfoHashes (no krk_metainfo_batch_dev pipelining)")

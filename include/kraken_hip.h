@@ -442,7 +442,8 @@ int krk_stream_create_prio(int priority, void** out);
 int krk_stream_destroy(void* s);
 int krk_stream_sync(void* s);
 /* Events (a window loop waits for ONE earlier window's kernels while the next
- * window's are already queued behind them on the same stream). */
+ * window's are already queued behind them on the same stream).  No timing; a thread in
+ * krk_event_sync sleeps until the event completes rather than spinning a core. */
 int krk_event_create(void** out);
 int krk_event_record(void* ev, void* stream);
 int krk_event_sync(void* ev);

@@ -1986,7 +1986,9 @@ int krk_event_create(void** out) {
     KRK_DEVICE(D);
     (void)D;
     hipEvent_t e;
-    KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // blocking sync: a host thread waiting for a window (tens of ms) sleeps instead of
+    // spinning a core of the process's CPU budget, which its hash threads need
+    KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     *out = e;
     return KRK_OK;
 }
