@@ -68,6 +68,9 @@ int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, 
  * of 64) and is updated by a non-final run (n whole blocks); final != 0 pads and writes the
  * digest to digest32 instead (n any length).  Read through pinned double buffers, x86 SHA
  * extensions.  Synchronous. */
+/* The calling thread's cumulative seconds in krk_sha256_resume_dev_on_host waiting for its
+ * device-to-host copies and hashing. */
+int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s);
 /* Work queued on `stream` after the call waits for event `ev` (hipStreamWaitEvent). */
 int krk_stream_wait_event(void* stream, void* ev);
 int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uint8_t* data_dev, uint64_t n,

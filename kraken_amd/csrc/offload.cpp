@@ -675,6 +675,10 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
     return KRK_OK;
 }
 
+// The calling thread's seconds in krk_sha256_resume_dev_on_host waiting for device-to-host
+// copies and hashing (krk_sha256_resume_stats).
+static thread_local double t_resume_wait = 0, t_resume_hash = 0;
+
 // One chain continued on the calling thread from device bytes (krk_sha256_resume_dev_on_host):
 // a worker (two pinned buffers + streams) of the device's pool, D2H double-buffered in
 // kOffChunk pieces, SHA-NI over each while the next comes down.
@@ -723,10 +727,12 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
     bool ok = issue(0);
     for (uint64_t c = 0; ok && c < nch; ++c) {
         if (c + 1 < nch) ok = issue(c + 1);
+        const auto tw = std::chrono::steady_clock::now();
         if (!ok || hipStreamSynchronize(W.s[c & 1]) != hipSuccess) {
             ok = false;
             break;
         }
+        const auto th = std::chrono::steady_clock::now();
         const uint64_t m = std::min(kOffChunk, L - c * kOffChunk);
         if (c + 1 < nch || !final) {
             host_sha256_blocks(h, W.buf[c & 1], m / 64);
@@ -734,6 +740,8 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
         } else {
             host_sha256_final(h, absorbed, W.buf[c & 1], m, digest);
         }
+        t_resume_wait += std::chrono::duration<double>(th - tw).count();
+        t_resume_hash += std::chrono::duration<double>(std::chrono::steady_clock::now() - th).count();
     }
     if (!ok) {
         hipStreamSynchronize(W.s[0]);
@@ -1017,6 +1025,12 @@ int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uin
     if (!r) r = resume_on_host(D, state8, absorbed, data_dev, n, final != 0, digest32, ready);
     hipEventDestroy(ready);
     return r;
+}
+
+int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s) {
+    if (copy_wait_s) *copy_wait_s = t_resume_wait;
+    if (hash_s) *hash_s = t_resume_hash;
+    return KRK_OK;
 }
 
 int krk_sha_tail_plan(const uint64_t* lengths, uint64_t n, int threads, uint32_t* host_idx, uint64_t* start,

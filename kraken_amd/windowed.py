@@ -607,11 +607,18 @@ class TailHandoffRun:
         import time
         try:
             self.D.set_device(self.device)
+            w, hh = C.c_double(), C.c_double()
+            self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
+            self._phase[i]["copy_wait0"], self._phase[i]["sha0"] = w.value, hh.value
             while True:
                 with self._cv:
                     while not self._jobs[i] and not self._done:
                         self._cv.wait()
                     if not self._jobs[i]:
+                        w, hh = C.c_double(), C.c_double()
+                        self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
+                        self._phase[i]["copy_wait"] = w.value - self._phase[i].get("copy_wait0", 0.0)
+                        self._phase[i]["sha"] = hh.value - self._phase[i].get("sha0", 0.0)
                         return
                     b, y, ev = self._jobs[i][0]
                 t0 = time.perf_counter()
@@ -620,6 +627,7 @@ class TailHandoffRun:
                     self._jobs[i].pop(0)
                     self._busy_s[i] += time.perf_counter() - t0
                     self._cv.notify_all()
+            # (returns above when the run is done)
         except BaseException as e:  # re-raised on the caller's thread
             err.append(e)
             with self._cv:
@@ -741,7 +749,8 @@ class TailHandoffRun:
                       "takeovers": takes, "resumed_from_midstate": resumed, "host_chains": len(host_blobs),
                       "host_bytes": host_bytes,
                       "thread_busy_s": [round(x, 3) for x in self._busy_s],
-                      "thread_phases_s": {k: round(sum(p[k] for p in self._phase), 3) for k in self._phase[0]},
+                      "thread_phases_s": {k: round(sum(p.get(k, 0.0) for p in self._phase), 3)
+                                          for k in ("queue", "midstate", "device", "hash", "copy_wait", "sha")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
 
     def _items(self, win, k):
