@@ -490,7 +490,16 @@ class TailHandoffRun:
     """A windowed batch (the WindowedRun layout: synthetic blobs generated window by window on
     the device, two device windows, one ChunkedBatch) with the tail handoff: `threads` host
     threads steal chains at window boundaries (TailPolicy).  After run(): cb.sums / cb.digests
-    hold every blob's piece sums and digest (device); `stats` the run's takeovers and timing."""
+    hold every blob's piece sums and digest (device); `stats` the run's takeovers and timing.
+
+    Queues: the window loop's step and SHA-256 streams are high priority (hardware queues of
+    their own) and the normal-priority streams carry only generator launches and copies.  A packet that cannot start
+    blocks every later packet of its hardware queue, and the normal-priority streams share four
+    of them (GPU_MAX_HW_QUEUES): a barrier waiting for a window's ~70 ms SHA-256 launch, or a
+    CRC launch whose 144 KiB-LDS workgroups find no CU the window's SHA workgroups leave room
+    on, would hold every thread's copies behind it.  So the tail pieces' CRCs go into the
+    window stream (the loop queues the pieces generated since the last window after each
+    window's step), and a ring slot is refilled only after the window that CRC'd it."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK):
         self.D = D
@@ -510,69 +519,67 @@ class TailHandoffRun:
         self.cb = D.ChunkedBatch(self.lens, P)
         self.tbuf = [[D.DeviceBuffer(TAIL_PIECE) for _ in range(TAIL_RING)] for _ in range(self.H)]
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        # the windows' streams at high priority, i.e. on hardware queues of their own: a
-        # window's SHA-256 launch, its CRC (on run_s beside it) and the barrier joining them
-        # stay off the normal-priority queues the threads' generator / CRC launches and copies
-        # share, where a packet behind such a barrier waits for the whole window
+        # the window generator stays at normal priority: its launches need no LDS (never blocked
+        # behind the SHA workgroups) and the host waits for each, so it puts no barrier in a queue
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
-        self.t_s, self.t_crc, self.t_idle, self.t_ev = [], [], [], []
-        for _ in range(self.H):  # a thread's generator, CRC and idle streams; an event pair per ring slot
-            for lst in (self.t_s, self.t_crc, self.t_idle):
+        self.t_s, self.t_idle, self.t_ev = [], [], []
+        for _ in range(self.H):  # a thread's generator and idle streams; an event per ring slot
+            for lst in (self.t_s, self.t_idle):
                 lst.append(C.c_void_p())
                 D.check(D.lib.krk_stream_create(C.byref(lst[-1])))
-            ev = ([C.c_void_p() for _ in range(TAIL_RING)], [C.c_void_p() for _ in range(TAIL_RING)])
-            for e in ev[0] + ev[1]:
+            ev = [C.c_void_p() for _ in range(TAIL_RING)]
+            for e in ev:
                 D.check(D.lib.krk_event_create(C.byref(e)))
             self.t_ev.append(ev)
         self.stats = {}
 
     # ---- one thread's chains
+    def _slot(self, i, k):
+        """Ring slot k of thread i is free to refill: its last piece's CRC has run (the window
+        event the loop recorded after queueing it), or it never held one."""
+        with self._cv:
+            while self._slot_ev[i][k] is False and not self._abort:
+                self._cv.wait()
+            ev = self._slot_ev[i][k]
+            self._slot_ev[i][k] = None
+        if ev:
+            self.D.check(self.D.lib.krk_event_sync(ev))
+
     def _job(self, i, b, y, ev, dig):
-        """Chain b from byte y: its remaining bytes generated on the device piece by piece,
-        their CRCs queued on the GPU, SHA-256 continued on this thread from the midstate the
+        """Chain b from byte y: its remaining bytes generated on the device piece by piece (their
+        CRCs queued by the window loop), SHA-256 continued on this thread from the midstate the
         windows left in HBM (window event `ev`), or from the IV when y == 0."""
         D = self.D
         L = int(self.lens[b])
-        rest = L - y
-        nch = max(1, -(-rest // TAIL_PIECE))
-        soff = int(self.cb.sums_off[b])
-
-        gen_s, crc_s, bufs = self.t_s[i], self.t_crc[i], self.tbuf[i]
-        evg, evc = self.t_ev[i]
+        nch = max(1, -(-(L - y) // TAIL_PIECE))
+        gen_s, bufs, evg = self.t_s[i], self.tbuf[i], self.t_ev[i]
         R = len(bufs)
         base = self._seq[i]  # the thread's pieces so far: the ring runs on across its chains
         self._seq[i] += nch
+        ph = self._phase[i]
+        clk = self._clock
 
         def queue(c):
-            """Piece c generated into ring slot c % R (event evg after it) on the thread's generator
-            stream; its CRCs on the thread's CRC stream once generated.  The CRC launch (144 KiB of
-            LDS a workgroup) waits for a CU the window's SHA-256 workgroups leave free -- often the
-            window's end -- so it runs on a stream of its own and the generator only waits for the
-            CRC of the piece R back, whose slot it refills."""
             k = (base + c) % R
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
-            if base + c >= R:
-                D.check(D.lib.krk_stream_wait_event(gen_s, evc[k]))
+            tw = clk()
+            self._slot(i, k)
+            ph["ring"] += clk() - tw
             if m > 0:
                 ptr = np.array([bufs[k].ptr], dtype=np.uint64)
                 D.synth_fill_chunk_arrays(self.ids[b:b + 1], ptr, np.array([o], np.uint64), np.array([m], np.uint64),
                                           stream=gen_s)
             D.check(D.lib.krk_event_record(evg[k], gen_s))
-            if m > 0:
-                D.check(D.lib.krk_stream_wait_event(crc_s, evg[k]))
-                arr = D.chunk_array(ptr, np.array([o], np.uint64), np.array([m], np.uint64), np.uint64(L),
-                                    np.int64(self.cb.piece_lengths[b]), np.uint64(soff), np.uint64(b))
-                D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), 1, self.cb.sums.ptr,
-                                                 crc_s))
-            D.check(D.lib.krk_event_record(evc[k], crc_s))
+            with self._cv:
+                if m > 0:  # its CRCs go with the next window
+                    self._slot_ev[i][k] = False
+                    self._pending.append((i, k, bufs[k].ptr, o, m, b))
 
-        clk = self._clock
         tq = clk()
         queue(0)
-        ph = self._phase[i]
         ph["queue"] += clk() - tq
         h = _IV.copy()
         if y:
@@ -586,7 +593,7 @@ class TailHandoffRun:
             if c + 1 < nch:
                 queue(c + 1)
             t1 = clk()
-            D.check(D.lib.krk_event_sync(evg[(base + c) % R]))  # piece c generated; c + 1 and the CRCs run meanwhile
+            D.check(D.lib.krk_event_sync(evg[(base + c) % R]))  # piece c generated
             t2 = clk()
             o = y + c * TAIL_PIECE
             m = min(TAIL_PIECE, L - o)
@@ -600,7 +607,8 @@ class TailHandoffRun:
             ph["hash"] += t3 - t2
             with self._mu:
                 self._left[i] -= m
-                self._t_last[i] = self._clock()
+                self._t_last[i] = clk()
+                self._done_bytes[i] += m
         dig[b] = out
 
     def _worker(self, i, err, dig):
@@ -609,17 +617,13 @@ class TailHandoffRun:
             self.D.set_device(self.device)
             w, hh = C.c_double(), C.c_double()
             self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
-            self._phase[i]["copy_wait0"], self._phase[i]["sha0"] = w.value, hh.value
+            w0, h0 = w.value, hh.value
             while True:
                 with self._cv:
-                    while not self._jobs[i] and not self._done:
+                    while not self._jobs[i] and not self._done and not self._abort:
                         self._cv.wait()
-                    if not self._jobs[i]:
-                        w, hh = C.c_double(), C.c_double()
-                        self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
-                        self._phase[i]["copy_wait"] = w.value - self._phase[i].get("copy_wait0", 0.0)
-                        self._phase[i]["sha"] = hh.value - self._phase[i].get("sha0", 0.0)
-                        return
+                    if not self._jobs[i] or self._abort:
+                        break
                     b, y, ev = self._jobs[i][0]
                 t0 = time.perf_counter()
                 self._job(i, b, y, ev, dig)
@@ -627,16 +631,50 @@ class TailHandoffRun:
                     self._jobs[i].pop(0)
                     self._busy_s[i] += time.perf_counter() - t0
                     self._cv.notify_all()
-            # (returns above when the run is done)
+            self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
+            self._phase[i]["copy_wait"] = w.value - w0
+            self._phase[i]["sha"] = hh.value - h0
         except BaseException as e:  # re-raised on the caller's thread
             err.append(e)
             with self._cv:
-                self._done = True
+                self._abort = True
+                self._cv.notify_all()
+        finally:
+            with self._cv:
+                self._alive -= 1
                 self._cv.notify_all()
 
     def _free_at(self, i, now):
-        """When thread i is expected to be done with its queued chains (measured progress)."""
-        return (self._t_last[i] if self._jobs[i] else now) + max(0, self._left[i]) / self.h
+        """When thread i is expected to be done with its queued chains, at its measured rate."""
+        rate = self._done_bytes[i] / self._busy_s[i] if self._busy_s[i] > 0.5 else self.h
+        return (self._t_last[i] if self._jobs[i] else now) + max(0, self._left[i]) / max(rate, 1e6)
+
+    def _flush_crcs(self, stream):
+        """Queue on `stream` the CRCs of the tail pieces generated since the last flush (each
+        after its generator event); returns the ring slots they hold."""
+        D = self.D
+        with self._cv:
+            take, self._pending = self._pending, []
+        if not take:
+            return take
+        for i, k, _, _, _, _ in take:
+            D.check(D.lib.krk_stream_wait_event(stream, self.t_ev[i][k]))
+        ptr = np.array([t[2] for t in take], dtype=np.uint64)
+        off = np.array([t[3] for t in take], dtype=np.uint64)
+        ln = np.array([t[4] for t in take], dtype=np.uint64)
+        bl = np.array([t[5] for t in take], dtype=np.int64)
+        arr = D.chunk_array(ptr, off, ln, self.cb.lengths[bl], self.cb.piece_lengths[bl], self.cb.sums_off[bl],
+                            bl.astype(np.uint64))
+        D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), len(take), self.cb.sums.ptr,
+                                         stream))
+        self._tail_crc_pieces += len(take)
+        return take
+
+    def _release(self, take, ev):
+        with self._cv:
+            for i, k, _, _, _, _ in take:
+                self._slot_ev[i][k] = ev
+            self._cv.notify_all()
 
     def run(self):
         import threading
@@ -650,9 +688,15 @@ class TailHandoffRun:
         self._left = [0] * self.H
         self._t_last = [0.0] * self.H
         self._busy_s = [0.0] * self.H
-        self._phase = [{"queue": 0.0, "midstate": 0.0, "device": 0.0, "hash": 0.0} for _ in range(self.H)]
+        self._done_bytes = [0] * self.H
+        self._phase = [{"queue": 0.0, "ring": 0.0, "midstate": 0.0, "device": 0.0, "hash": 0.0}
+                       for _ in range(self.H)]
         self._seq = [0] * self.H
-        self._done = False
+        self._slot_ev = [[None] * TAIL_RING for _ in range(self.H)]  # None free, False CRC pending, event
+        self._pending = []
+        self._tail_crc_pieces = 0
+        self._done = self._abort = False
+        self._alive = self.H
         dig = np.zeros((n, 32), dtype=np.uint8)
         err = []
         pol = TailPolicy(self.lens, self.H)
@@ -672,8 +716,16 @@ class TailHandoffRun:
             w.start()
         sched = _Sched(self.lens, np.nonzero(pol.on_gpu)[0], self.W, self.cap, self.max_chunk)
         evs = []
+
+        def new_event():
+            e = C.c_void_p()
+            D.check(D.lib.krk_event_create(C.byref(e)))
+            evs.append(e)
+            return e
+
         takes, resumed, wait_win_s = 0, 0, 0.0
         scale = 1.0  # measured / modelled window time (EMA)
+        gpu_end = 0.0
         try:
             win = sched.next()
             k = 0
@@ -681,25 +733,27 @@ class TailHandoffRun:
             if items is not None:
                 self._gen(items)
             t_prev_end = self._clock()
-            self._last_model = 1.0
+            last_model = 1.0
+            wev = []  # the windows' events
             while win is not None and not err:
                 blobs, offs, tk = win
                 pol.queued(blobs, offs, tk)
                 self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s)
-                ev = C.c_void_p()
-                D.check(D.lib.krk_event_create(C.byref(ev)))
+                take = self._flush_crcs(self.run_s)
+                ev = new_event()
                 D.check(D.lib.krk_event_record(ev, self.run_s))
-                evs.append(ev)
+                wev.append(ev)
+                self._release(take, ev)
                 model = float(tk.max()) / stream_rate(self.rates, blobs.size) + 0.0005
                 if k:
                     tw = self._clock()
-                    D.check(D.lib.krk_event_sync(evs[k - 1]))
+                    D.check(D.lib.krk_event_sync(wev[k - 1]))
                     now = self._clock()
                     wait_win_s += now - tw
-                    scale = 0.7 * scale + 0.3 * max(0.2, min(5.0, (now - t_prev_end) / max(self._last_model, 1e-6)))
+                    scale = 0.7 * scale + 0.3 * max(0.2, min(5.0, (now - t_prev_end) / max(last_model, 1e-6)))
                     t_prev_end = now
                 now = self._clock()
-                self._last_model = model
+                last_model = model
                 end_k = now + model * scale
                 horizon = end_k + model * scale  # window k+1 modelled like k
                 with self._cv:  # threads with at most their current chain, free before k+1 ends
@@ -723,34 +777,54 @@ class TailHandoffRun:
                 if win is not None:
                     items = self._items(win, k)
                     self._gen(items)
-            if evs:
+            if wev:
                 D.check(D.lib.krk_stream_sync(self.run_s))
             gpu_end = self._clock() - t0
+            with self._cv:
+                self._done = True
+                self._cv.notify_all()
+            # the windows are done: the threads' remaining pieces' CRCs, flushed as they come
+            while not err:
+                with self._cv:
+                    if self._alive == 0 and not self._pending:
+                        break
+                    if not self._pending:
+                        self._cv.wait(0.01)
+                take = self._flush_crcs(self.run_s)
+                if take:
+                    ev = new_event()
+                    D.check(D.lib.krk_event_record(ev, self.run_s))
+                    self._release(take, ev)
         finally:
             with self._cv:
                 self._done = True
+                if err:
+                    self._abort = True
                 self._cv.notify_all()
             for w in workers:
                 w.join()
             sched.close()
-        if err:
+        try:
+            if err:
+                raise err[0]
+            D.check(D.lib.krk_stream_sync(self.run_s))  # the last tail CRCs
+            for b in sorted(host_blobs):
+                row = np.ascontiguousarray(dig[b])
+                D.check(D.lib.krk_memcpy_h2d(C.c_void_p(self.cb.digests.ptr + 32 * int(b)),
+                                             row.ctypes.data_as(C.c_void_p), 32))
+        finally:
+            D.lib.krk_stream_sync(self.run_s)
             for e in evs:
                 D.lib.krk_event_destroy(e)
-            raise err[0]
-        for s in self.t_crc:  # the tails' CRCs
-            D.check(D.lib.krk_stream_sync(s))
-        for e in evs:
-            D.lib.krk_event_destroy(e)
-        for b in sorted(host_blobs):
-            row = np.ascontiguousarray(dig[b])
-            D.check(D.lib.krk_memcpy_h2d(C.c_void_p(self.cb.digests.ptr + 32 * int(b)),
-                                         row.ctypes.data_as(C.c_void_p), 32))
-        self.stats = {"windows": len(evs), "gpu_windows_end_s": round(gpu_end, 3),
+        self.stats = {"windows": len(wev), "gpu_windows_end_s": round(gpu_end, 3),
                       "takeovers": takes, "resumed_from_midstate": resumed, "host_chains": len(host_blobs),
-                      "host_bytes": host_bytes,
+                      "host_bytes": host_bytes, "tail_crc_pieces": self._tail_crc_pieces,
                       "thread_busy_s": [round(x, 3) for x in self._busy_s],
+                      "thread_GBps": [round(self._done_bytes[i] / max(self._busy_s[i], 1e-9) / 1e9, 3)
+                                      for i in range(self.H)],
                       "thread_phases_s": {k: round(sum(p.get(k, 0.0) for p in self._phase), 3)
-                                          for k in ("queue", "midstate", "device", "hash", "copy_wait", "sha")},
+                                          for k in ("queue", "ring", "midstate", "device", "hash", "copy_wait",
+                                                    "sha")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
 
     def _items(self, win, k):
@@ -766,18 +840,18 @@ class TailHandoffRun:
         self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
 
     def close(self):
-        for b in self.bufs + [x for pair in self.tbuf for x in pair]:
+        for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
         self.bufs, self.tbuf = [], []
-        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s + self.t_crc + self.t_idle:
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s + self.t_idle:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        for evg, evc in self.t_ev:
-            for e in evg + evc:
+        for ring in self.t_ev:
+            for e in ring:
                 if e.value:
                     self.D.lib.krk_event_destroy(e)
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        self.t_s, self.t_crc, self.t_idle, self.t_ev = [], [], [], []
+        self.t_s, self.t_idle, self.t_ev = [], [], []
 
     def __del__(self):
         try:
