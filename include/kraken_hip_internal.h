@@ -61,7 +61,8 @@ int krk_window_sched_drop(krk_window_sched* s, uint32_t blob, uint64_t* offset);
 int krk_window_sched_set_chunk_cap(krk_window_sched* s, uint64_t max_chunk);
 void krk_window_sched_free(krk_window_sched* s);
 /* The piece CRCs of device chunks without SHA-256 (XOR-accumulated into sums_dev like a
- * window's): the tails of chains a host thread hashes.  Asynchronous on `stream`. */
+ * window's; several chunks of one blob allowed): the tails of chains a host thread hashes.
+ * Asynchronous on `stream`. */
 int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, void* stream);
 /* Continue one SHA-256 chain on the calling thread from n device bytes at data_dev (after
  * the work queued on `stream`): state8 holds the midstate after `absorbed` bytes (a multiple

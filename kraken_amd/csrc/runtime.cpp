@@ -1128,12 +1128,14 @@ int krk_piece_sums_files(const krk_file_blob* files, uint64_t n, uint32_t* sums_
     return r;
 }
 
-static int validate_chunks(const krk_chunk* c, uint64_t n) {
+// crc_only: chunks of one blob may repeat (their CRCs XOR into the sums independently); a
+// SHA-256 step takes at most one chunk a blob slot (one midstate each).
+static int validate_chunks(const krk_chunk* c, uint64_t n, bool crc_only = false) {
     KRK_CHECK(n == 0 || c, KRK_EINVAL, "chunks is NULL");
     std::unordered_map<uint64_t, uint64_t> seen;
     seen.reserve(n);
     for (uint64_t i = 0; i < n; ++i) {
-        KRK_CHECK(seen.emplace(c[i].blob, i).second, KRK_EINVAL, "blob slot %llu appears twice in one call",
+        KRK_CHECK(crc_only || seen.emplace(c[i].blob, i).second, KRK_EINVAL, "blob slot %llu appears twice in one call",
                   (unsigned long long)c[i].blob);
         KRK_CHECK(c[i].piece_length > 0, KRK_EINVAL, "piece length must be positive");
         KRK_CHECK(c[i].length == 0 || c[i].data, KRK_EINVAL, "chunk %llu: data is NULL", (unsigned long long)i);
@@ -1222,7 +1224,7 @@ int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n, uint3
 // get their piece sums on the GPU, XOR-accumulated like a window's.
 int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, void* stream) {
     KRK_DEVICE(D);
-    int r = validate_chunks(chunks, n);
+    int r = validate_chunks(chunks, n, /*crc_only=*/true);
     if (r || !n) return r;
     KRK_CHECK(sums_dev, KRK_EINVAL, "chunks_crc_dev: sums_dev is NULL");
     ItemBuilder B;

@@ -501,7 +501,7 @@ class TailHandoffRun:
     window stream (the loop queues the pieces generated since the last window after each
     window's step), and a ring slot is refilled only after the window that CRC'd it."""
 
-    def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK):
+    def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -510,6 +510,8 @@ class TailHandoffRun:
         self.H = max(1, int(threads))
         self.device = device
         self.max_chunk = int(max_chunk)
+        self.piece = int(piece)  # a multiple of 64
+        assert self.piece > 0 and self.piece % 64 == 0, piece
         n = self.lens.size
         self.cap = window_stream_cap(D, n) if cap is None else int(cap)
         self.rates = D.planner_rates()
@@ -517,7 +519,7 @@ class TailHandoffRun:
         wb = self.W + 16 * max(min(self.cap, n), 1)
         self.bufs = [D.DeviceBuffer(wb), D.DeviceBuffer(wb)]
         self.cb = D.ChunkedBatch(self.lens, P)
-        self.tbuf = [[D.DeviceBuffer(TAIL_PIECE) for _ in range(TAIL_RING)] for _ in range(self.H)]
+        self.tbuf = [[D.DeviceBuffer(self.piece) for _ in range(TAIL_RING)] for _ in range(self.H)]
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
         # the window generator stays at normal priority: its launches need no LDS (never blocked
         # behind the SHA workgroups) and the host waits for each, so it puts no barrier in a queue
@@ -553,7 +555,7 @@ class TailHandoffRun:
         windows left in HBM (window event `ev`), or from the IV when y == 0."""
         D = self.D
         L = int(self.lens[b])
-        nch = max(1, -(-(L - y) // TAIL_PIECE))
+        nch = max(1, -(-(L - y) // self.piece))
         gen_s, bufs, evg = self.t_s[i], self.tbuf[i], self.t_ev[i]
         R = len(bufs)
         base = self._seq[i]  # the thread's pieces so far: the ring runs on across its chains
@@ -563,8 +565,8 @@ class TailHandoffRun:
 
         def queue(c):
             k = (base + c) % R
-            o = y + c * TAIL_PIECE
-            m = min(TAIL_PIECE, L - o)
+            o = y + c * self.piece
+            m = min(self.piece, L - o)
             tw = clk()
             self._slot(i, k)
             ph["ring"] += clk() - tw
@@ -595,8 +597,8 @@ class TailHandoffRun:
             t1 = clk()
             D.check(D.lib.krk_event_sync(evg[(base + c) % R]))  # piece c generated
             t2 = clk()
-            o = y + c * TAIL_PIECE
-            m = min(TAIL_PIECE, L - o)
+            o = y + c * self.piece
+            m = min(self.piece, L - o)
             # ordered by the event above, not by a stream: the call waits for nothing else
             D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), o,
                                                         C.c_void_p(bufs[(base + c) % R].ptr), m, int(c + 1 == nch),
@@ -795,6 +797,11 @@ class TailHandoffRun:
                     ev = new_event()
                     D.check(D.lib.krk_event_record(ev, self.run_s))
                     self._release(take, ev)
+        except BaseException:  # the loop failed: the threads must not wait for it
+            with self._cv:
+                self._abort = True
+                self._cv.notify_all()
+            raise
         finally:
             with self._cv:
                 self._done = True

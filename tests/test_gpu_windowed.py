@@ -82,17 +82,19 @@ def test_window_plan_covers_c3_law_once():
     assert np.array_equal(pos, np.asarray(lens, dtype=np.uint64))
 
 
-@pytest.mark.parametrize("cap,threads", [(None, 3), (200, 4)])
-def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads):
+@pytest.mark.parametrize("cap,threads,piece", [(None, 3, 64 << 20), (200, 4, 64 << 20), (None, 5, 1 << 20)])
+def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, piece):
     """the windowed batch with the tail handoff (windowed.TailHandoffRun):
     host threads start on the longest chains whole, then steal the chains with the most bytes
     left at window boundaries -- live chains from the midstate the windows left in HBM, and
     (cap=200) blobs still waiting for admission from the IV -- while their remaining piece
     CRCs run on the GPU beside the windows'.  1 MiB window chunks: hundreds of windows and
-    takeovers.  Every blob equals the one-shot device path; sampled blobs the oracle."""
+    takeovers.  piece=1 MiB: a thread's chain spans many device pieces, so its ring of six
+    slots wraps inside one chain and one window's CRC flush carries several pieces of one
+    blob.  Every blob equals the one-shot device path; sampled blobs the oracle."""
     from kraken_amd.windowed import TailHandoffRun
     lens, ids, dg1, sums1, offs1, counts1 = one_shot
-    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20)
+    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20, piece=piece)
     tr.run()
     st = tr.stats
     cb = tr.cb
@@ -102,6 +104,7 @@ def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads):
     print(st)
     assert st["takeovers"] > threads and st["resumed_from_midstate"] > 0 and st["windows"] > 50, st
     assert 0 < st["host_bytes"] < int(np.sum(lens)), st
+    assert st["tail_crc_pieces"] >= st["host_chains"], st
     bad = [i for i in range(N) if bytes(dg[i]) != bytes(dg1[i])]
     assert not bad, (len(bad), bad[:10])
     for i in range(N):
