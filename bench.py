@@ -1437,8 +1437,10 @@ def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
                              "d2h_GBps": round(rates["d2h_bps"] / 1e9, 2), "source": rates["source"]},
            "what": "GPU + host: host threads (SHA-NI) steal the chains with the most bytes left at window "
                    "boundaries from the windows' midstates in HBM; piece CRCs all on the GPU"}
+    from kraken_amd.windowed import TAIL_PIECE, TAIL_RING
     tr = TailHandoffRun(D, ids, lens, P, W, threads, cap=cap if (a.no_admission or a.live_cap) else None,
-                        device=a.device)
+                        device=a.device, piece=(a.tail_piece_mib << 20) if a.tail_piece_mib else TAIL_PIECE,
+                        ring=a.tail_ring or TAIL_RING)
     T.barrier()
     t0 = time.perf_counter()
     tr.run()
@@ -2291,6 +2293,8 @@ def main():
                     help="C3: also run the batch with the tail handoff (host threads steal the chains with the most "
                          "bytes left at window boundaries), reported as tail_handoff beside the GPU-only value")
     ap.add_argument("--tail-threads", type=int, default=0, help="C3 tail handoff: host threads (0 = the CPU budget - 1)")
+    ap.add_argument("--tail-ring", type=int, default=0, help="C3 tail handoff: device pieces a thread keeps in flight")
+    ap.add_argument("--tail-piece-mib", type=int, default=0, help="C3 tail handoff: MiB a device piece")
     ap.add_argument("--c3-tail-only", action="store_true",
                     help="C3: skip the GPU-only windows (measurement runs of the tail handoff; no value line)")
     ap.add_argument("--hrw-int32", action="store_true", help="C5: int32 owner indices even for <= 255 nodes")

@@ -501,7 +501,8 @@ class TailHandoffRun:
     window stream (the loop queues the pieces generated since the last window after each
     window's step), and a ring slot is refilled only after the window that CRC'd it."""
 
-    def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE):
+    def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
+                 ring=TAIL_RING):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -519,7 +520,8 @@ class TailHandoffRun:
         wb = self.W + 16 * max(min(self.cap, n), 1)
         self.bufs = [D.DeviceBuffer(wb), D.DeviceBuffer(wb)]
         self.cb = D.ChunkedBatch(self.lens, P)
-        self.tbuf = [[D.DeviceBuffer(self.piece) for _ in range(TAIL_RING)] for _ in range(self.H)]
+        self.ring = max(2, int(ring))
+        self.tbuf = [[D.DeviceBuffer(self.piece) for _ in range(self.ring)] for _ in range(self.H)]
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
         # the window generator stays at normal priority: its launches need no LDS (never blocked
         # behind the SHA workgroups) and the host waits for each, so it puts no barrier in a queue
@@ -531,7 +533,7 @@ class TailHandoffRun:
             for lst in (self.t_s, self.t_idle):
                 lst.append(C.c_void_p())
                 D.check(D.lib.krk_stream_create(C.byref(lst[-1])))
-            ev = [C.c_void_p() for _ in range(TAIL_RING)]
+            ev = [C.c_void_p() for _ in range(self.ring)]
             for e in ev:
                 D.check(D.lib.krk_event_create(C.byref(e)))
             self.t_ev.append(ev)
@@ -694,7 +696,7 @@ class TailHandoffRun:
         self._phase = [{"queue": 0.0, "ring": 0.0, "midstate": 0.0, "device": 0.0, "hash": 0.0}
                        for _ in range(self.H)]
         self._seq = [0] * self.H
-        self._slot_ev = [[None] * TAIL_RING for _ in range(self.H)]  # None free, False CRC pending, event
+        self._slot_ev = [[None] * self.ring for _ in range(self.H)]  # None free, False CRC pending, event
         self._pending = []
         self._tail_crc_pieces = 0
         self._done = self._abort = False
