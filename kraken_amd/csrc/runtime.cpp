@@ -2000,6 +2000,15 @@ int krk_event_record(void* ev, void* stream) {
     KRK_HIP(hipEventRecord(static_cast<hipEvent_t>(ev), pick(D, stream)));
     return KRK_OK;
 }
+int krk_event_create_polling(void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    hipEvent_t e;
+    KRK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = e;
+    return KRK_OK;
+}
 int krk_stream_wait_event(void* stream, void* ev) {
     KRK_CHECK(ev, KRK_EINVAL, "event is NULL");
     KRK_DEVICE(D);

@@ -534,8 +534,8 @@ class TailHandoffRun:
                 lst.append(C.c_void_p())
                 D.check(D.lib.krk_stream_create(C.byref(lst[-1])))
             ev = [C.c_void_p() for _ in range(self.ring)]
-            for e in ev:
-                D.check(D.lib.krk_event_create(C.byref(e)))
+            for e in ev:  # a piece's generator launch takes microseconds: polled, not slept on
+                D.check(D.lib.krk_event_create_polling(C.byref(e)))
             self.t_ev.append(ev)
         self.stats = {}
 
