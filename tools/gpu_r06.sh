@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-6 GPU steps: gpurun --timeout T -- 'bash tools/gpu_r06.sh <step>...'
+# Each step runs under its own time limit; a step that ends in a fault, abort, crash or
+# time limit (rc >= 2 other than pytest's 1 = test failures) ends the script: nothing more
+# runs on the GPU in that call.
+mkdir -p gpurun_out
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -3 "gpurun_out/$name.log"
+    if [ $rc -ge 2 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+C3T="python -u bench.py --workload c3 --emulate-world 8 --c3-tail-only --no-e2e --no-cpu-baseline"
+for step in "$@"; do
+    case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    all) run pytest_all 1100 $PYT tests -m gpu ;;
+    windowed) run pytest_windowed 400 $PYT tests/test_gpu_windowed.py ;;
+    bench) run bench_c2 300 python bench.py ;;
+    c3w8) run bench_c3_w8 600 python -u bench.py --workload c3 --emulate-world 8 --tail-handoff --host-lane --no-e2e ;;
+    c3w8_tail) run bench_c3_w8_tail 200 $C3T ;;
+    c3w4_tail) run bench_c3_w4_tail 200 python -u bench.py --workload c3 --emulate-world 4 --c3-tail-only --no-e2e --no-cpu-baseline ;;
+    c3w2_tail) run bench_c3_w2_tail 200 python -u bench.py --workload c3 --emulate-world 2 --c3-tail-only --no-e2e --no-cpu-baseline ;;
+    c3) run bench_c3 900 python -u bench.py --workload c3 --tail-handoff ;;
+    tail_sweep) for cfg in "6 64" "12 64" "16 32"; do set -- $cfg
+                    run c3_tail_r$1_p$2 200 $C3T --tail-ring $1 --tail-piece-mib $2; done ;;
+    tail_probe) run tail_probe 200 python -u tools/tail_probe.py 15 ;;
+    prof_c3w8) run prof_c3w8 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d gpurun_out/prof_c3w8 -- python3 bench.py --workload c3 --emulate-world 8 --no-e2e --no-cpu-baseline --no-ceiling ;;
+    prof_c3) run prof_c3 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d gpurun_out/prof_c3 -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
+    # PMC passes of C3's windows (N=1), each pass its own run (counter limits per block)
+    pmc_c3_valu) run pmc_c3_valu 400 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES \
+                  SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv \
+                  -d gpurun_out/pmc_c3_valu -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
+    pmc_c3_wait) run pmc_c3_wait 400 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY \
+                  SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv \
+                  -d gpurun_out/pmc_c3_wait -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
+    pmc_c3_hbm) run pmc_c3_hbm 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
+                  -d gpurun_out/pmc_c3_hbm -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
