@@ -172,6 +172,7 @@ def _load() -> C.CDLL:
         "krk_event_record": (i, [vp, vp]),
         "krk_stream_wait_event": (i, [vp, vp]),
         "krk_event_create_polling": (i, [C.POINTER(vp)]),
+        "krk_event_query": (i, [vp, C.POINTER(C.c_int)]),
         "krk_sha256_resume_stats": (i, [f64p, f64p]),
         "krk_event_sync": (i, [vp]),
         "krk_event_destroy": (i, [vp]),

@@ -2000,6 +2000,14 @@ int krk_event_record(void* ev, void* stream) {
     KRK_HIP(hipEventRecord(static_cast<hipEvent_t>(ev), pick(D, stream)));
     return KRK_OK;
 }
+int krk_event_query(void* ev, int* done) {
+    KRK_CHECK(ev && done, KRK_EINVAL, "event_query: null argument");
+    const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(ev));
+    KRK_CHECK(e == hipSuccess || e == hipErrorNotReady, KRK_EHIP, "event query: %s", hipGetErrorString(e));
+    if (e == hipErrorNotReady) (void)hipGetLastError();
+    *done = e == hipSuccess;
+    return KRK_OK;
+}
 int krk_event_create_polling(void** out) {
     KRK_CHECK(out, KRK_EINVAL, "out is NULL");
     KRK_DEVICE(D);

@@ -352,7 +352,7 @@ TAIL_PIECE = 64 << 20  # device bytes a tail thread generates, CRCs and hashes a
 # are left live (modelled on rank 0's shard of an 8-GPU C3: 1/2/4/8 MiB end at 11.7 / 11.7
 # / 12.0 / 12.7 s with 0.5 ms a launch, 12.7 / 12.2 / 12.3 / 12.9 s with 3 ms).
 TAIL_CHUNK = 4 << 20
-TAIL_RING = 6  # device pieces a tail thread keeps in flight (generated / hashed / waiting for their CRC)
+TAIL_RING = 8  # device slots a tail thread's pieces cycle through (generated / hashed / waiting for their CRC)
 
 
 def tail_thread_rate(rates, threads):
@@ -492,14 +492,17 @@ class TailHandoffRun:
     threads steal chains at window boundaries (TailPolicy).  After run(): cb.sums / cb.digests
     hold every blob's piece sums and digest (device); `stats` the run's takeovers and timing.
 
-    Queues: the window loop's step and SHA-256 streams are high priority (hardware queues of
-    their own) and the normal-priority streams carry only generator launches and copies.  A packet that cannot start
-    blocks every later packet of its hardware queue, and the normal-priority streams share four
-    of them (GPU_MAX_HW_QUEUES): a barrier waiting for a window's ~70 ms SHA-256 launch, or a
-    CRC launch whose 144 KiB-LDS workgroups find no CU the window's SHA workgroups leave room
-    on, would hold every thread's copies behind it.  So the tail pieces' CRCs go into the
-    window stream (the loop queues the pieces generated since the last window after each
-    window's step), and a ring slot is refilled only after the window that CRC'd it."""
+    Who does what.  The window loop (the calling thread) owns every device launch: the
+    windows, and the stolen chains' remaining bytes, generated piece by piece (64 MiB) into
+    each thread's ring of device slots on the window generator's stream as slots come free;
+    the pieces' CRCs are queued into the window stream after each window's step.  The host
+    threads only copy pieces down and hash them (krk_sha256_resume_dev_on_host), in order,
+    from the chain's midstate.  Queues: a packet that cannot start blocks every later packet
+    of its hardware queue, and normal-priority streams share four of them (GPU_MAX_HW_QUEUES;
+    16 or 32 measured slower, profiles/r06): so the windows' step and SHA-256 streams are high
+    priority, the CRC launches (144 KiB-LDS workgroups, which wait for CUs the window's SHA
+    workgroups leave room on) go only there, and the normal queues carry the threads' copies
+    and the generator's launches (no LDS, never blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
                  ring=TAIL_RING):
@@ -523,68 +526,25 @@ class TailHandoffRun:
         self.ring = max(2, int(ring))
         self.tbuf = [[D.DeviceBuffer(self.piece) for _ in range(self.ring)] for _ in range(self.H)]
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        # the window generator stays at normal priority: its launches need no LDS (never blocked
-        # behind the SHA workgroups) and the host waits for each, so it puts no barrier in a queue
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
-        self.t_s, self.t_idle, self.t_ev = [], [], []
-        for _ in range(self.H):  # a thread's generator and idle streams; an event per ring slot
-            for lst in (self.t_s, self.t_idle):
-                lst.append(C.c_void_p())
-                D.check(D.lib.krk_stream_create(C.byref(lst[-1])))
-            ev = [C.c_void_p() for _ in range(self.ring)]
-            for e in ev:  # a piece's generator launch takes microseconds: polled, not slept on
-                D.check(D.lib.krk_event_create_polling(C.byref(e)))
-            self.t_ev.append(ev)
+        self.t_idle = []
+        for _ in range(self.H):  # the stream a thread's copies are ordered after (nothing queued on it)
+            self.t_idle.append(C.c_void_p())
+            D.check(D.lib.krk_stream_create(C.byref(self.t_idle[-1])))
         self.stats = {}
 
-    # ---- one thread's chains
-    def _slot(self, i, k):
-        """Ring slot k of thread i is free to refill: its last piece's CRC has run (the window
-        event the loop recorded after queueing it), or it never held one."""
-        with self._cv:
-            while self._slot_ev[i][k] is False and not self._abort:
-                self._cv.wait()
-            ev = self._slot_ev[i][k]
-            self._slot_ev[i][k] = None
-        if ev:
-            self.D.check(self.D.lib.krk_event_sync(ev))
-
+    # ---- the host threads: copy and hash
     def _job(self, i, b, y, ev, dig):
-        """Chain b from byte y: its remaining bytes generated on the device piece by piece (their
-        CRCs queued by the window loop), SHA-256 continued on this thread from the midstate the
-        windows left in HBM (window event `ev`), or from the IV when y == 0."""
+        """Chain b from byte y: its pieces as the loop generates them into this thread's ring,
+        SHA-256 continued from the midstate the windows left in HBM (window event `ev`), or
+        from the IV when y == 0."""
         D = self.D
         L = int(self.lens[b])
         nch = max(1, -(-(L - y) // self.piece))
-        gen_s, bufs, evg = self.t_s[i], self.tbuf[i], self.t_ev[i]
-        R = len(bufs)
-        base = self._seq[i]  # the thread's pieces so far: the ring runs on across its chains
-        self._seq[i] += nch
         ph = self._phase[i]
         clk = self._clock
-
-        def queue(c):
-            k = (base + c) % R
-            o = y + c * self.piece
-            m = min(self.piece, L - o)
-            tw = clk()
-            self._slot(i, k)
-            ph["ring"] += clk() - tw
-            if m > 0:
-                ptr = np.array([bufs[k].ptr], dtype=np.uint64)
-                D.synth_fill_chunk_arrays(self.ids[b:b + 1], ptr, np.array([o], np.uint64), np.array([m], np.uint64),
-                                          stream=gen_s)
-            D.check(D.lib.krk_event_record(evg[k], gen_s))
-            with self._cv:
-                if m > 0:  # its CRCs go with the next window
-                    self._slot_ev[i][k] = False
-                    self._pending.append((i, k, bufs[k].ptr, o, m, b))
-
-        tq = clk()
-        queue(0)
-        ph["queue"] += clk() - tq
         h = _IV.copy()
         if y:
             tw = clk()
@@ -593,26 +553,27 @@ class TailHandoffRun:
             ph["midstate"] += clk() - tw
         out = np.zeros(32, dtype=np.uint8)
         for c in range(nch):
-            tq = clk()
-            if c + 1 < nch:
-                queue(c + 1)
             t1 = clk()
-            D.check(D.lib.krk_event_sync(evg[(base + c) % R]))  # piece c generated
+            with self._cv:  # the next piece of this thread, generated by the loop
+                while not self._ready[i] and not self._abort:
+                    self._cv.wait()
+                if self._abort:
+                    return
+                k, pb, po, pm = self._ready[i].pop(0)
+            assert pb == b and po == y + c * self.piece, (pb, po, b, y, c)
             t2 = clk()
-            o = y + c * self.piece
-            m = min(self.piece, L - o)
-            # ordered by the event above, not by a stream: the call waits for nothing else
-            D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), o,
-                                                        C.c_void_p(bufs[(base + c) % R].ptr), m, int(c + 1 == nch),
+            D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
+                                                        C.c_void_p(self.tbuf[i][k].ptr), pm, int(c + 1 == nch),
                                                         out.ctypes.data_as(C.POINTER(C.c_uint8)), self.t_idle[i]))
             t3 = clk()
-            ph["queue"] += t1 - tq
             ph["device"] += t2 - t1
             ph["hash"] += t3 - t2
-            with self._mu:
-                self._left[i] -= m
-                self._t_last[i] = clk()
-                self._done_bytes[i] += m
+            with self._cv:
+                self._slot_used[i][k] = False  # copied down: the loop may refill it once its CRC ran
+                self._left[i] -= pm
+                self._t_last[i] = t3
+                self._done_bytes[i] += pm
+                self._cv.notify_all()
         dig[b] = out
 
     def _worker(self, i, err, dig):
@@ -653,32 +614,89 @@ class TailHandoffRun:
         rate = self._done_bytes[i] / self._busy_s[i] if self._busy_s[i] > 0.5 else self.h
         return (self._t_last[i] if self._jobs[i] else now) + max(0, self._left[i]) / max(rate, 1e6)
 
+    # ---- the loop's side: generate pieces into free slots, queue their CRCs
+    def _assign(self, i, b, y, ev):
+        """Chain b from byte y becomes thread i's next job (caller holds the lock)."""
+        self._jobs[i].append((b, y, ev))
+        L = int(self.lens[b])
+        for o in range(y, max(L, y + 1), self.piece):
+            self._to_gen[i].append((b, o, min(self.piece, L - o)))
+        self._left[i] += L - y
+
+    def _service(self):
+        """Every free ring slot (copied down and its CRC done) refilled with its thread's next
+        piece: generated on the generator stream, waited for, handed to the thread; their CRCs
+        go with the next flush.  Returns the pieces generated."""
+        D = self.D
+        gen = []
+        with self._cv:
+            for i in range(self.H):
+                while self._to_gen[i]:
+                    k = self._next_slot[i]
+                    if self._slot_used[i][k]:
+                        break
+                    ev = self._slot_crc[i][k]
+                    if ev is not None:
+                        done = C.c_int(0)
+                        D.check(D.lib.krk_event_query(ev, C.byref(done)))
+                        if not done.value:
+                            break
+                        self._slot_crc[i][k] = None
+                    b, o, m = self._to_gen[i].pop(0)
+                    self._slot_used[i][k] = True
+                    self._next_slot[i] = (k + 1) % self.ring
+                    gen.append((i, k, b, o, m))
+        if not gen:
+            return gen
+        live = [g for g in gen if g[4] > 0]
+        if live:
+            ptr = np.array([self.tbuf[i][k].ptr for i, k, _, _, _ in live], dtype=np.uint64)
+            bl = np.array([b for _, _, b, _, _ in live], dtype=np.int64)
+            D.synth_fill_chunk_arrays(self.ids[bl], ptr, np.array([g[3] for g in live], np.uint64),
+                                      np.array([g[4] for g in live], np.uint64), stream=self.gen_s)
+            D.check(D.lib.krk_stream_sync(self.gen_s))
+        with self._cv:
+            for i, k, b, o, m in gen:
+                self._ready[i].append((k, b, o, m))
+                if m > 0:
+                    self._pending.append((i, k, b, o, m))
+            self._cv.notify_all()
+        self._tail_pieces += len(gen)
+        return gen
+
     def _flush_crcs(self, stream):
-        """Queue on `stream` the CRCs of the tail pieces generated since the last flush (each
-        after its generator event); returns the ring slots they hold."""
+        """Queue on `stream` the CRCs of the pieces generated since the last flush; returns
+        them (their slots are held until the event recorded after this)."""
         D = self.D
         with self._cv:
             take, self._pending = self._pending, []
         if not take:
             return take
-        for i, k, _, _, _, _ in take:
-            D.check(D.lib.krk_stream_wait_event(stream, self.t_ev[i][k]))
-        ptr = np.array([t[2] for t in take], dtype=np.uint64)
-        off = np.array([t[3] for t in take], dtype=np.uint64)
-        ln = np.array([t[4] for t in take], dtype=np.uint64)
-        bl = np.array([t[5] for t in take], dtype=np.int64)
-        arr = D.chunk_array(ptr, off, ln, self.cb.lengths[bl], self.cb.piece_lengths[bl], self.cb.sums_off[bl],
+        ptr = np.array([self.tbuf[i][k].ptr for i, k, _, _, _ in take], dtype=np.uint64)
+        bl = np.array([b for _, _, b, _, _ in take], dtype=np.int64)
+        arr = D.chunk_array(ptr, np.array([t[3] for t in take], np.uint64), np.array([t[4] for t in take], np.uint64),
+                            self.cb.lengths[bl], self.cb.piece_lengths[bl], self.cb.sums_off[bl],
                             bl.astype(np.uint64))
         D.check(D.lib.krk_chunks_crc_dev(arr.ctypes.data_as(C.POINTER(D.krk_chunk)), len(take), self.cb.sums.ptr,
                                          stream))
-        self._tail_crc_pieces += len(take)
         return take
 
     def _release(self, take, ev):
         with self._cv:
-            for i, k, _, _, _, _ in take:
-                self._slot_ev[i][k] = ev
-            self._cv.notify_all()
+            for i, k, _, _, _ in take:
+                self._slot_crc[i][k] = ev
+
+    def _wait_window(self, ev):
+        """Until window event `ev` completes, keep the threads' rings full."""
+        D = self.D
+        done = C.c_int(0)
+        while True:
+            D.check(D.lib.krk_event_query(ev, C.byref(done)))
+            if done.value:
+                return
+            if not self._service():
+                with self._cv:
+                    self._cv.wait(0.002)
 
     def run(self):
         import threading
@@ -688,34 +706,36 @@ class TailHandoffRun:
         self._clock = time.perf_counter
         self._mu = threading.Lock()
         self._cv = threading.Condition(self._mu)
-        self._jobs = [[] for _ in range(self.H)]
-        self._left = [0] * self.H
-        self._t_last = [0.0] * self.H
-        self._busy_s = [0.0] * self.H
-        self._done_bytes = [0] * self.H
-        self._phase = [{"queue": 0.0, "ring": 0.0, "midstate": 0.0, "device": 0.0, "hash": 0.0}
-                       for _ in range(self.H)]
-        self._seq = [0] * self.H
-        self._slot_ev = [[None] * self.ring for _ in range(self.H)]  # None free, False CRC pending, event
+        H, R = self.H, self.ring
+        self._jobs = [[] for _ in range(H)]
+        self._to_gen = [[] for _ in range(H)]   # pieces the loop still has to generate, in order
+        self._ready = [[] for _ in range(H)]    # generated pieces a thread may copy and hash, in order
+        self._slot_used = [[False] * R for _ in range(H)]
+        self._slot_crc = [[None] * R for _ in range(H)]  # the event after the slot's last CRC
+        self._next_slot = [0] * H
         self._pending = []
-        self._tail_crc_pieces = 0
+        self._left = [0] * H
+        self._t_last = [0.0] * H
+        self._busy_s = [0.0] * H
+        self._done_bytes = [0] * H
+        self._phase = [{"midstate": 0.0, "device": 0.0, "hash": 0.0} for _ in range(H)]
+        self._tail_pieces = 0
         self._done = self._abort = False
-        self._alive = self.H
+        self._alive = H
         dig = np.zeros((n, 32), dtype=np.uint8)
         err = []
-        pol = TailPolicy(self.lens, self.H)
+        pol = TailPolicy(self.lens, H)
         host_blobs = set()
         host_bytes = 0
         t0 = self._clock()
         with self._cv:
             for i, b in enumerate(pol.initial()):
-                self._jobs[i].append((b, 0, None))
-                self._left[i] = int(self.lens[b])
+                self._assign(i, b, 0, None)
                 self._t_last[i] = t0
                 host_blobs.add(b)
                 host_bytes += int(self.lens[b])
         workers = [threading.Thread(target=self._worker, args=(i, err, dig), name=f"krk-tail-{i}")
-                   for i in range(self.H)]
+                   for i in range(H)]
         for w in workers:
             w.start()
         sched = _Sched(self.lens, np.nonzero(pol.on_gpu)[0], self.W, self.cap, self.max_chunk)
@@ -730,7 +750,9 @@ class TailHandoffRun:
         takes, resumed, wait_win_s = 0, 0, 0.0
         scale = 1.0  # measured / modelled window time (EMA)
         gpu_end = 0.0
+        wev = []  # the windows' events
         try:
+            self._service()
             win = sched.next()
             k = 0
             items = self._items(win, 0) if win is not None else None
@@ -738,7 +760,6 @@ class TailHandoffRun:
                 self._gen(items)
             t_prev_end = self._clock()
             last_model = 1.0
-            wev = []  # the windows' events
             while win is not None and not err:
                 blobs, offs, tk = win
                 pol.queued(blobs, offs, tk)
@@ -751,7 +772,7 @@ class TailHandoffRun:
                 model = float(tk.max()) / stream_rate(self.rates, blobs.size) + 0.0005
                 if k:
                     tw = self._clock()
-                    D.check(D.lib.krk_event_sync(wev[k - 1]))
+                    self._wait_window(wev[k - 1])
                     now = self._clock()
                     wait_win_s += now - tw
                     scale = 0.7 * scale + 0.3 * max(0.2, min(5.0, (now - t_prev_end) / max(last_model, 1e-6)))
@@ -761,7 +782,7 @@ class TailHandoffRun:
                 end_k = now + model * scale
                 horizon = end_k + model * scale  # window k+1 modelled like k
                 with self._cv:  # threads with at most their current chain, free before k+1 ends
-                    ready = [i for i in range(self.H) if len(self._jobs[i]) <= 1 and self._free_at(i, now) <= horizon]
+                    ready = [i for i in range(H) if len(self._jobs[i]) <= 1 and self._free_at(i, now) <= horizon]
                     ready.sort(key=lambda i: self._free_at(i, now))
                 chosen = pol.pick(len(ready), stream_rate(self.rates, blobs.size) * model)
                 with self._cv:
@@ -769,36 +790,42 @@ class TailHandoffRun:
                         y = sched.drop(b)
                         if not self._jobs[i]:
                             self._t_last[i] = now
-                        self._jobs[i].append((b, y, ev if y else None))
-                        self._left[i] += int(self.lens[b]) - y
+                        self._assign(i, b, y, ev if y else None)
                         host_blobs.add(b)
                         host_bytes += int(self.lens[b]) - y
                         takes += 1
                         resumed += y > 0
                     self._cv.notify_all()
+                self._service()
                 win = sched.next()
                 k += 1
                 if win is not None:
                     items = self._items(win, k)
                     self._gen(items)
             if wev:
-                D.check(D.lib.krk_stream_sync(self.run_s))
+                self._wait_window(wev[-1])
             gpu_end = self._clock() - t0
             with self._cv:
                 self._done = True
                 self._cv.notify_all()
-            # the windows are done: the threads' remaining pieces' CRCs, flushed as they come
+            # the windows are done: keep the rings full and the pieces' CRCs flushed
             while not err:
                 with self._cv:
-                    if self._alive == 0 and not self._pending:
+                    if self._alive == 0:
                         break
-                    if not self._pending:
-                        self._cv.wait(0.01)
+                self._service()
                 take = self._flush_crcs(self.run_s)
                 if take:
                     ev = new_event()
                     D.check(D.lib.krk_event_record(ev, self.run_s))
                     self._release(take, ev)
+                with self._cv:
+                    self._cv.wait(0.002)
+            take = self._flush_crcs(self.run_s)  # the last pieces (every thread is done)
+            if take:
+                ev = new_event()
+                D.check(D.lib.krk_event_record(ev, self.run_s))
+                self._release(take, ev)
         except BaseException:  # the loop failed: the threads must not wait for it
             with self._cv:
                 self._abort = True
@@ -827,13 +854,12 @@ class TailHandoffRun:
                 D.lib.krk_event_destroy(e)
         self.stats = {"windows": len(wev), "gpu_windows_end_s": round(gpu_end, 3),
                       "takeovers": takes, "resumed_from_midstate": resumed, "host_chains": len(host_blobs),
-                      "host_bytes": host_bytes, "tail_crc_pieces": self._tail_crc_pieces,
+                      "host_bytes": host_bytes, "tail_pieces": self._tail_pieces,
                       "thread_busy_s": [round(x, 3) for x in self._busy_s],
                       "thread_GBps": [round(self._done_bytes[i] / max(self._busy_s[i], 1e-9) / 1e9, 3)
-                                      for i in range(self.H)],
+                                      for i in range(H)],
                       "thread_phases_s": {k: round(sum(p.get(k, 0.0) for p in self._phase), 3)
-                                          for k in ("queue", "ring", "midstate", "device", "hash", "copy_wait",
-                                                    "sha")},
+                                          for k in ("midstate", "device", "hash", "copy_wait", "sha")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
 
     def _items(self, win, k):
@@ -852,15 +878,11 @@ class TailHandoffRun:
         for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
         self.bufs, self.tbuf = [], []
-        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_s + self.t_idle:
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_idle:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        for ring in self.t_ev:
-            for e in ring:
-                if e.value:
-                    self.D.lib.krk_event_destroy(e)
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        self.t_s, self.t_idle, self.t_ev = [], [], []
+        self.t_idle = []
 
     def __del__(self):
         try:

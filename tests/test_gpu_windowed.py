@@ -104,7 +104,7 @@ def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, p
     print(st)
     assert st["takeovers"] > threads and st["resumed_from_midstate"] > 0 and st["windows"] > 50, st
     assert 0 < st["host_bytes"] < int(np.sum(lens)), st
-    assert st["tail_crc_pieces"] >= st["host_chains"], st
+    assert st["tail_pieces"] >= st["host_chains"], st
     bad = [i for i in range(N) if bytes(dg[i]) != bytes(dg1[i])]
     assert not bad, (len(bad), bad[:10])
     for i in range(N):
