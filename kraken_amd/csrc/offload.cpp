@@ -125,9 +125,20 @@ struct CalBufs {
 // Per device: host threads + pinned double buffers of the offload phases, and the planner
 // calibration (measured once per device and process, or again on krk_planner_calibrate).
 struct Worker;
+// A resumer (krk_sha256_resume_dev_on_host): one copy stream, kResumeBufs pinned buffers and
+// their events -- copies run up to kResumeBufs - 1 pieces ahead of the hash, so a copy held
+// back a few ms behind another stream's packet in a shared hardware queue does not stall it.
+constexpr int kResumeBufs = 4;
+struct Resumer {
+    hipStream_t s = nullptr;
+    uint8_t* buf[kResumeBufs] = {};
+    hipEvent_t ev[kResumeBufs] = {};
+};
+
 struct OffloadPool {
     std::mutex mu;
     std::vector<std::vector<Worker>> free_sets;
+    std::vector<Resumer> free_resumers;
     std::mutex cal_mu;  // one calibration of this device at a time
     CalBufs cal;
     bool measured = false;
@@ -680,73 +691,72 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
 static thread_local double t_resume_wait = 0, t_resume_hash = 0;
 
 // One chain continued on the calling thread from device bytes (krk_sha256_resume_dev_on_host):
-// a worker (two pinned buffers + streams) of the device's pool, D2H double-buffered in
-// kOffChunk pieces, SHA-NI over each while the next comes down.
+// a resumer of the device's pool, the D2H copies kResumeBufs - 1 kOffChunk pieces ahead of
+// SHA-NI over each.
 static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uint8_t* src, uint64_t L, bool final,
                           uint8_t* digest, hipEvent_t ready) {
     OffloadPool& P = *pool_of(D);
-    std::vector<Worker> set;
+    Resumer R;
     {
         std::lock_guard<std::mutex> g(P.mu);
-        for (auto& fs : P.free_sets)  // a set with a spare worker: take one
-            if (!fs.empty()) {
-                set.push_back(fs.back());
-                fs.pop_back();
-                break;
-            }
-    }
-    if (set.empty()) {
-        Worker w;
-        for (int b = 0; b < 2; ++b) {
-            if (hipStreamCreateWithFlags(&w.s[b], hipStreamNonBlocking) != hipSuccess ||
-                hipHostMalloc(reinterpret_cast<void**>(&w.buf[b]), kOffChunk, hipHostMallocDefault) != hipSuccess) {
-                for (int c = 0; c <= b; ++c) {
-                    if (w.s[c]) hipStreamDestroy(w.s[c]);
-                    if (w.buf[c]) hipHostFree(w.buf[c]);
-                }
-                KRK_CHECK(false, KRK_ENOMEM, "sha256 resume: pinned buffers / streams");
-            }
+        if (!P.free_resumers.empty()) {
+            R = P.free_resumers.back();
+            P.free_resumers.pop_back();
         }
-        set.push_back(w);
+    }
+    if (!R.s) {
+        bool ok = hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking) == hipSuccess;
+        for (int b = 0; ok && b < kResumeBufs; ++b)
+            ok = hipHostMalloc(reinterpret_cast<void**>(&R.buf[b]), kOffChunk, hipHostMallocDefault) == hipSuccess &&
+                 hipEventCreateWithFlags(&R.ev[b], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            if (R.s) hipStreamDestroy(R.s);
+            for (int b = 0; b < kResumeBufs; ++b) {
+                if (R.buf[b]) hipHostFree(R.buf[b]);
+                if (R.ev[b]) hipEventDestroy(R.ev[b]);
+            }
+            KRK_CHECK(false, KRK_ENOMEM, "sha256 resume: pinned buffers / stream");
+        }
     }
     struct Return {
         OffloadPool& P;
-        std::vector<Worker>& set;
+        Resumer& R;
         ~Return() {
             std::lock_guard<std::mutex> g(P.mu);
-            P.free_sets.push_back(std::move(set));
+            P.free_resumers.push_back(R);
         }
-    } give_back{P, set};
-    Worker& W = set[0];
+    } give_back{P, R};
     KRK_HIP(hipEventSynchronize(ready));
     const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
     auto issue = [&](uint64_t c) {
         const uint64_t o = c * kOffChunk, m = std::min(kOffChunk, L - o);
-        return m == 0 || hipMemcpyAsync(W.buf[c & 1], src + o, m, hipMemcpyDeviceToHost, W.s[c & 1]) == hipSuccess;
+        const int b = (int)(c % kResumeBufs);
+        return (m == 0 || hipMemcpyAsync(R.buf[b], src + o, m, hipMemcpyDeviceToHost, R.s) == hipSuccess) &&
+               hipEventRecord(R.ev[b], R.s) == hipSuccess;
     };
-    bool ok = issue(0);
+    bool ok = true;
+    uint64_t issued = 0;
+    for (; ok && issued < std::min<uint64_t>(nch, kResumeBufs - 1); ++issued) ok = issue(issued);
     for (uint64_t c = 0; ok && c < nch; ++c) {
-        if (c + 1 < nch) ok = issue(c + 1);
+        if (issued < nch) ok = issue(issued++);  // into the buffer hashed at c - 1
         const auto tw = std::chrono::steady_clock::now();
-        if (!ok || hipStreamSynchronize(W.s[c & 1]) != hipSuccess) {
+        if (!ok || hipEventSynchronize(R.ev[c % kResumeBufs]) != hipSuccess) {
             ok = false;
             break;
         }
         const auto th = std::chrono::steady_clock::now();
         const uint64_t m = std::min(kOffChunk, L - c * kOffChunk);
+        const uint8_t* p = R.buf[c % kResumeBufs];
         if (c + 1 < nch || !final) {
-            host_sha256_blocks(h, W.buf[c & 1], m / 64);
+            host_sha256_blocks(h, p, m / 64);
             absorbed += m;
         } else {
-            host_sha256_final(h, absorbed, W.buf[c & 1], m, digest);
+            host_sha256_final(h, absorbed, p, m, digest);
         }
         t_resume_wait += std::chrono::duration<double>(th - tw).count();
         t_resume_hash += std::chrono::duration<double>(std::chrono::steady_clock::now() - th).count();
     }
-    if (!ok) {
-        hipStreamSynchronize(W.s[0]);
-        hipStreamSynchronize(W.s[1]);
-    }
+    if (!ok) hipStreamSynchronize(R.s);  // leave no copy in flight into the buffers
     KRK_CHECK(ok, KRK_EHIP, "sha256 resume: device-to-host copy failed");
     return KRK_OK;
 }
@@ -760,6 +770,13 @@ void offload_teardown(Device& D) {  // krk_shutdown: no offload phase is running
                 if (w.s[b]) hipStreamSynchronize(w.s[b]), hipStreamDestroy(w.s[b]);
                 if (w.buf[b]) hipHostFree(w.buf[b]);
             }
+    for (Resumer& r : P->free_resumers) {
+        if (r.s) hipStreamSynchronize(r.s), hipStreamDestroy(r.s);
+        for (int b = 0; b < kResumeBufs; ++b) {
+            if (r.buf[b]) hipHostFree(r.buf[b]);
+            if (r.ev[b]) hipEventDestroy(r.ev[b]);
+        }
+    }
     CalBufs& c = P->cal;
     if (c.s) hipStreamSynchronize(c.s), hipStreamDestroy(c.s);
     for (void* p : {(void*)c.d_in, (void*)c.d_state, (void*)c.d_dig, (void*)c.d_jobs, (void*)c.d_copy})

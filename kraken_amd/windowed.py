@@ -352,6 +352,11 @@ TAIL_PIECE = 64 << 20  # device bytes a tail thread generates, CRCs and hashes a
 # are left live (modelled on rank 0's shard of an 8-GPU C3: 1/2/4/8 MiB end at 11.7 / 11.7
 # / 12.0 / 12.7 s with 0.5 ms a launch, 12.7 / 12.2 / 12.3 / 12.9 s with 3 ms).
 TAIL_CHUNK = 4 << 20
+# A thread gets its next chain while it is expected to be free within this many windows
+# after the queued one ends: a chain handed over early idles on the GPU side (r/h ~ 2.4 % of
+# the idle time in extra host bytes), a thread that finishes before the window holding its
+# next chain's midstate ends waits for it (all of that time lost).
+TAIL_HORIZON = 2.5
 TAIL_RING = 8  # device slots a tail thread's pieces cycle through (generated / hashed / waiting for their CRC)
 
 
@@ -448,8 +453,8 @@ class TailPolicy:
 def simulate_tail_handoff(lens, W, cap, threads, rates, launch_s=0.0005, max_chunk=0):
     """The tail handoff on the planner's rates, window by window, with the policy the run uses:
     window k lasts its largest chunk over the per-stream rate of its live count's tier plus a
-    launch; at the start of window k (the end of k-1) every thread free before window k+1
-    would end takes a chain, whose midstate is ready when window k ends.  Returns the
+    launch; at the start of window k (the end of k-1) every thread free within TAIL_HORIZON
+    windows after window k takes a chain, whose midstate is ready when window k ends.  Returns the
     modelled end (s), the GPU windows' end, the host bytes and the takeovers."""
     L = np.asarray(lens, dtype=np.int64)
     H = max(1, int(threads))
@@ -468,7 +473,7 @@ def simulate_tail_handoff(lens, W, cap, threads, rates, launch_s=0.0005, max_chu
             pol.queued(blobs, offs, tk)
             dur = float(tk.max()) / stream_rate(rates, blobs.size) + launch_s
             end_k = t + dur
-            horizon = end_k + dur  # window k+1 modelled like k
+            horizon = end_k + TAIL_HORIZON * dur  # later windows modelled like k
             ready = [i for i in range(H) if free[i] <= horizon]
             chosen = pol.pick(len(ready), stream_rate(rates, blobs.size) * dur)
             ready.sort(key=lambda i: free[i])
@@ -780,7 +785,7 @@ class TailHandoffRun:
                 now = self._clock()
                 last_model = model
                 end_k = now + model * scale
-                horizon = end_k + model * scale  # window k+1 modelled like k
+                horizon = end_k + TAIL_HORIZON * model * scale  # later windows modelled like k
                 with self._cv:  # threads with at most their current chain, free before k+1 ends
                     ready = [i for i in range(H) if len(self._jobs[i]) <= 1 and self._free_at(i, now) <= horizon]
                     ready.sort(key=lambda i: self._free_at(i, now))
