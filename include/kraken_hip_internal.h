@@ -72,6 +72,8 @@ int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, 
 /* The calling thread's cumulative seconds in krk_sha256_resume_dev_on_host waiting for its
  * device-to-host copies and hashing. */
 int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s);
+/* ... and in enqueueing its copies and waiting for the caller's stream. */
+int krk_sha256_resume_stats2(double* issue_s, double* ready_s);
 /* *done = 1 once event `ev` has completed, else 0 (no wait). */
 int krk_event_query(void* ev, int* done);
 /* An event whose krk_event_sync polls instead of sleeping: for waits of microseconds (a

@@ -174,6 +174,7 @@ def _load() -> C.CDLL:
         "krk_event_create_polling": (i, [C.POINTER(vp)]),
         "krk_event_query": (i, [vp, C.POINTER(C.c_int)]),
         "krk_sha256_resume_stats": (i, [f64p, f64p]),
+        "krk_sha256_resume_stats2": (i, [f64p, f64p]),
         "krk_event_sync": (i, [vp]),
         "krk_event_destroy": (i, [vp]),
         "krk_set_sha_host_offload": (i, [i]),

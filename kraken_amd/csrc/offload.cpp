@@ -688,7 +688,7 @@ int offload_hash(Device* D, const std::vector<const uint8_t*>& ptrs, const std::
 
 // The calling thread's seconds in krk_sha256_resume_dev_on_host waiting for device-to-host
 // copies and hashing (krk_sha256_resume_stats).
-static thread_local double t_resume_wait = 0, t_resume_hash = 0;
+static thread_local double t_resume_wait = 0, t_resume_hash = 0, t_resume_issue = 0, t_resume_ready = 0;
 
 // One chain continued on the calling thread from device bytes (krk_sha256_resume_dev_on_host):
 // a resumer of the device's pool, the D2H copies kResumeBufs - 1 kOffChunk pieces ahead of
@@ -726,13 +726,18 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
             P.free_resumers.push_back(R);
         }
     } give_back{P, R};
+    const auto tr = std::chrono::steady_clock::now();
     KRK_HIP(hipEventSynchronize(ready));
+    t_resume_ready += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
     const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
     auto issue = [&](uint64_t c) {
+        const auto ti = std::chrono::steady_clock::now();
         const uint64_t o = c * kOffChunk, m = std::min(kOffChunk, L - o);
         const int b = (int)(c % kResumeBufs);
-        return (m == 0 || hipMemcpyAsync(R.buf[b], src + o, m, hipMemcpyDeviceToHost, R.s) == hipSuccess) &&
-               hipEventRecord(R.ev[b], R.s) == hipSuccess;
+        const bool ok = (m == 0 || hipMemcpyAsync(R.buf[b], src + o, m, hipMemcpyDeviceToHost, R.s) == hipSuccess) &&
+                        hipEventRecord(R.ev[b], R.s) == hipSuccess;
+        t_resume_issue += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti).count();
+        return ok;
     };
     bool ok = true;
     uint64_t issued = 0;
@@ -1047,6 +1052,11 @@ int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uin
 int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s) {
     if (copy_wait_s) *copy_wait_s = t_resume_wait;
     if (hash_s) *hash_s = t_resume_hash;
+    return KRK_OK;
+}
+int krk_sha256_resume_stats2(double* issue_s, double* ready_s) {
+    if (issue_s) *issue_s = t_resume_issue;
+    if (ready_s) *ready_s = t_resume_ready;
     return KRK_OK;
 }
 

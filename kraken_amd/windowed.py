@@ -585,9 +585,10 @@ class TailHandoffRun:
         import time
         try:
             self.D.set_device(self.device)
-            w, hh = C.c_double(), C.c_double()
+            w, hh, iss, rdy = C.c_double(), C.c_double(), C.c_double(), C.c_double()
             self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
-            w0, h0 = w.value, hh.value
+            self.D.check(self.D.lib.krk_sha256_resume_stats2(C.byref(iss), C.byref(rdy)))
+            w0, h0, i0, r0 = w.value, hh.value, iss.value, rdy.value
             while True:
                 with self._cv:
                     while not self._jobs[i] and not self._done and not self._abort:
@@ -602,8 +603,11 @@ class TailHandoffRun:
                     self._busy_s[i] += time.perf_counter() - t0
                     self._cv.notify_all()
             self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
+            self.D.check(self.D.lib.krk_sha256_resume_stats2(C.byref(iss), C.byref(rdy)))
             self._phase[i]["copy_wait"] = w.value - w0
             self._phase[i]["sha"] = hh.value - h0
+            self._phase[i]["copy_issue"] = iss.value - i0
+            self._phase[i]["ready_wait"] = rdy.value - r0
         except BaseException as e:  # re-raised on the caller's thread
             err.append(e)
             with self._cv:
@@ -864,7 +868,8 @@ class TailHandoffRun:
                       "thread_GBps": [round(self._done_bytes[i] / max(self._busy_s[i], 1e-9) / 1e9, 3)
                                       for i in range(H)],
                       "thread_phases_s": {k: round(sum(p.get(k, 0.0) for p in self._phase), 3)
-                                          for k in ("midstate", "device", "hash", "copy_wait", "sha")},
+                                          for k in ("midstate", "device", "hash", "copy_wait", "sha", "copy_issue",
+                                                    "ready_wait")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
 
     def _items(self, win, k):
