@@ -65,7 +65,7 @@ void krk_window_sched_free(krk_window_sched* s);
  * Asynchronous on `stream`. */
 int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, void* stream);
 /* Continue one SHA-256 chain on the calling thread from n device bytes at data_dev (after
- * the work queued on `stream`): state8 holds the midstate after `absorbed` bytes (a multiple
+ * the work queued on `stream`; NULL: the bytes are ready now, nothing is waited for): state8 holds the midstate after `absorbed` bytes (a multiple
  * of 64) and is updated by a non-final run (n whole blocks); final != 0 pads and writes the
  * digest to digest32 instead (n any length).  Read through pinned double buffers, x86 SHA
  * extensions.  Synchronous. */

@@ -726,9 +726,11 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
             P.free_resumers.push_back(R);
         }
     } give_back{P, R};
-    const auto tr = std::chrono::steady_clock::now();
-    KRK_HIP(hipEventSynchronize(ready));
-    t_resume_ready += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
+    if (ready) {
+        const auto tr = std::chrono::steady_clock::now();
+        KRK_HIP(hipEventSynchronize(ready));
+        t_resume_ready += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
+    }
     const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
     auto issue = [&](uint64_t c) {
         const auto ti = std::chrono::steady_clock::now();
@@ -1037,10 +1039,13 @@ int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uin
     KRK_CHECK(final || n % 64 == 0, KRK_EINVAL, "sha256_resume: a non-final run must be whole 64-byte blocks");
     KRK_CHECK(!final || digest32, KRK_EINVAL, "sha256_resume: digest is NULL");
     KRK_DEVICE(D);
+    if (!stream)  // the caller has waited for the bytes: an event on an idle stream would still
+                  // queue behind other streams' packets in its shared hardware queue (ms each)
+        return resume_on_host(D, state8, absorbed, data_dev, n, final != 0, digest32, nullptr);
     hipEvent_t ready;
     KRK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
     int r = KRK_OK;
-    if (hipEventRecord(ready, pick(D, stream)) != hipSuccess) {
+    if (hipEventRecord(ready, static_cast<hipStream_t>(stream)) != hipSuccess) {
         set_error(KRK_EHIP, "sha256_resume: event record failed");
         r = KRK_EHIP;
     }

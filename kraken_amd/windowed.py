@@ -534,10 +534,6 @@ class TailHandoffRun:
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
-        self.t_idle = []
-        for _ in range(self.H):  # the stream a thread's copies are ordered after (nothing queued on it)
-            self.t_idle.append(C.c_void_p())
-            D.check(D.lib.krk_stream_create(C.byref(self.t_idle[-1])))
         self.stats = {}
 
     # ---- the host threads: copy and hash
@@ -569,7 +565,7 @@ class TailHandoffRun:
             t2 = clk()
             D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
                                                         C.c_void_p(self.tbuf[i][k].ptr), pm, int(c + 1 == nch),
-                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), self.t_idle[i]))
+                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), None))
             t3 = clk()
             ph["device"] += t2 - t1
             ph["hash"] += t3 - t2
@@ -888,11 +884,10 @@ class TailHandoffRun:
         for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
         self.bufs, self.tbuf = [], []
-        for s in [self.gen_s, self.run_s, self.sha_s] + self.t_idle:
+        for s in [self.gen_s, self.run_s, self.sha_s]:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
         self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        self.t_idle = []
 
     def __del__(self):
         try:

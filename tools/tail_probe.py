@@ -34,7 +34,7 @@ def threads_rate(T, secs, bufs, idle):
         while time.perf_counter() < stop:
             o = off % BUF
             D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), off,
-                                                        C.c_void_p(bufs[i].ptr + o), RUN, 0, None, idle[i]))
+                                                        C.c_void_p(bufs[i].ptr + o), RUN, 0, None, None))
             off += RUN
             done[i] += RUN
 
