@@ -129,6 +129,7 @@ struct Worker;
 // their events -- copies run up to kResumeBufs - 1 pieces ahead of the hash, so a copy held
 // back a few ms behind another stream's packet in a shared hardware queue does not stall it.
 constexpr int kResumeBufs = 4;
+constexpr uint64_t kResumeChunk = 16ull << 20;  // a copy: fewer, longer copies through the shared queues
 struct Resumer {
     hipStream_t s = nullptr;
     uint8_t* buf[kResumeBufs] = {};
@@ -707,7 +708,7 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
     if (!R.s) {
         bool ok = hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking) == hipSuccess;
         for (int b = 0; ok && b < kResumeBufs; ++b)
-            ok = hipHostMalloc(reinterpret_cast<void**>(&R.buf[b]), kOffChunk, hipHostMallocDefault) == hipSuccess &&
+            ok = hipHostMalloc(reinterpret_cast<void**>(&R.buf[b]), kResumeChunk, hipHostMallocDefault) == hipSuccess &&
                  hipEventCreateWithFlags(&R.ev[b], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             if (R.s) hipStreamDestroy(R.s);
@@ -731,10 +732,10 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
         KRK_HIP(hipEventSynchronize(ready));
         t_resume_ready += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
     }
-    const uint64_t nch = std::max<uint64_t>(1, (L + kOffChunk - 1) / kOffChunk);
+    const uint64_t nch = std::max<uint64_t>(1, (L + kResumeChunk - 1) / kResumeChunk);
     auto issue = [&](uint64_t c) {
         const auto ti = std::chrono::steady_clock::now();
-        const uint64_t o = c * kOffChunk, m = std::min(kOffChunk, L - o);
+        const uint64_t o = c * kResumeChunk, m = std::min(kResumeChunk, L - o);
         const int b = (int)(c % kResumeBufs);
         const bool ok = (m == 0 || hipMemcpyAsync(R.buf[b], src + o, m, hipMemcpyDeviceToHost, R.s) == hipSuccess) &&
                         hipEventRecord(R.ev[b], R.s) == hipSuccess;
@@ -752,7 +753,7 @@ static int resume_on_host(Device* D, uint32_t h[8], uint64_t absorbed, const uin
             break;
         }
         const auto th = std::chrono::steady_clock::now();
-        const uint64_t m = std::min(kOffChunk, L - c * kOffChunk);
+        const uint64_t m = std::min(kResumeChunk, L - c * kResumeChunk);
         const uint8_t* p = R.buf[c % kResumeBufs];
         if (c + 1 < nch || !final) {
             host_sha256_blocks(h, p, m / 64);
