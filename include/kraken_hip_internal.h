@@ -60,6 +60,12 @@ int krk_window_sched_drop(krk_window_sched* s, uint32_t blob, uint64_t* offset);
  * few blobs are live. */
 int krk_window_sched_set_chunk_cap(krk_window_sched* s, uint64_t max_chunk);
 void krk_window_sched_free(krk_window_sched* s);
+/* krk_metainfo_digest_chunks_dev_on with the piece CRCs queued on `stream` only after the
+ * SHA-256 launch on sha_stream has ended (no CRC waiting for CUs at the head of a
+ * high-priority queue while the SHA launch holds them: that keeps the dispatcher from every
+ * normal-priority queue, device-to-host copies included).  The C3 tail handoff's window step. */
+int krk_metainfo_digest_chunks_dev_after(const krk_chunk* chunks, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
+                                         uint8_t* digests_dev, void* stream, void* sha_stream);
 /* The piece CRCs of device chunks without SHA-256 (XOR-accumulated into sums_dev like a
  * window's; several chunks of one blob allowed): the tails of chains a host thread hashes.
  * Asynchronous on `stream`. */

@@ -142,6 +142,7 @@ def _load() -> C.CDLL:
         "krk_set_host_gather": (i, [i]),
         "krk_metainfo_digest_chunks_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp]),
         "krk_metainfo_digest_chunks_dev_on": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp, vp]),
+        "krk_metainfo_digest_chunks_dev_after": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp, vp, vp, vp]),
         "krk_info_hash": (i, [C.c_int64, u32p, C.c_uint64, C.c_char_p, C.c_uint64, C.c_int64, u8p]),
         "krk_info_hash_batch": (i, [C.POINTER(C.c_int64), u32p, u64p, u64p, C.c_char_p, u64p, C.POINTER(C.c_int64),
                                     C.c_uint64, u8p]),

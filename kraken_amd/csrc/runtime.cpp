@@ -1158,8 +1158,15 @@ static int validate_chunks(const krk_chunk* c, uint64_t n, bool crc_only = false
 // handoff, kraken_amd/windowed.py) then leaves no fork / join barrier of a window on the
 // library's normal-priority streams, whose hardware queues its copy threads share -- a
 // barrier waiting for a window's ~70 ms SHA launch blocks every packet behind it there.
+//
+// crc_after_sha (with ks): the CRC items are queued on s only once the SHA-256 launch has
+// ended.  A launch on a high-priority queue whose workgroups wait for CUs (the CRC's 144 KiB
+// of LDS, with a window's SHA workgroups holding every CU) keeps the dispatcher from the
+// normal-priority queues meanwhile: device-to-host copies of other streams stall for the
+// whole window (tools/tail_probe.py, profiles/r06/tail_probe.jsonl: 36 -> 0.18 GB/s).
 static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
-                       uint8_t* digests_dev, hipStream_t s, ItemBuilder& B, hipStream_t ks = nullptr) {
+                       uint8_t* digests_dev, hipStream_t s, ItemBuilder& B, hipStream_t ks = nullptr,
+                       bool crc_after_sha = false) {
     const hipStream_t kc = ks ? s : D->s_b;
     if (!ks) ks = D->s_a;
     std::vector<ShaJob> jobs(n);
@@ -1185,12 +1192,17 @@ static int chunks_step(Device* D, const krk_chunk* c, uint64_t n, uint32_t* stat
     KRK_HIP(hipStreamWaitEvent(ks, fork, 0));
     if (kc != s) KRK_HIP(hipStreamWaitEvent(kc, fork, 0));
     int r = run_jobs(D, jobs, digests_dev, state_dev, ks);
-    if (!r) r = run_items(D, items, sums_dev, kc);
     hipEventRecord(j1, ks);
-    hipStreamWaitEvent(s, j1, 0);
-    if (kc != s) {
-        hipEventRecord(j2, kc);
-        hipStreamWaitEvent(s, j2, 0);
+    if (crc_after_sha && kc == s) {
+        hipStreamWaitEvent(s, j1, 0);
+        if (!r) r = run_items(D, items, sums_dev, kc);
+    } else {
+        if (!r) r = run_items(D, items, sums_dev, kc);
+        hipStreamWaitEvent(s, j1, 0);
+        if (kc != s) {
+            hipEventRecord(j2, kc);
+            hipStreamWaitEvent(s, j2, 0);
+        }
     }
     hipEventDestroy(fork);
     hipEventDestroy(j1);
@@ -1217,6 +1229,17 @@ int krk_metainfo_digest_chunks_dev_on(const krk_chunk* chunks, uint64_t n, uint3
     ItemBuilder B;
     return chunks_step(D, chunks, n, state_dev, sums_dev, digests_dev, pick(D, stream), B,
                        static_cast<hipStream_t>(sha_stream));
+}
+
+int krk_metainfo_digest_chunks_dev_after(const krk_chunk* chunks, uint64_t n, uint32_t* state_dev, uint32_t* sums_dev,
+                                         uint8_t* digests_dev, void* stream, void* sha_stream) {
+    KRK_DEVICE(D);
+    int r = validate_chunks(chunks, n);
+    if (r || !n) return r;
+    KRK_CHECK(state_dev && sums_dev && digests_dev && sha_stream, KRK_EINVAL, "chunks_dev_after: null argument");
+    ItemBuilder B;
+    return chunks_step(D, chunks, n, state_dev, sums_dev, digests_dev, pick(D, stream), B,
+                       static_cast<hipStream_t>(sha_stream), /*crc_after_sha=*/true);
 }
 
 // The piece CRCs of device chunks alone (no SHA-256): the tail bytes of chains whose

@@ -498,13 +498,15 @@ class ChunkedBatch:
         self.sums.zero()
         self.digests = DeviceBuffer(max(n, 1) * 32)
 
-    def step_arrays(self, blob_idx, ptrs, offsets, lengths, stream=None, sha_stream=None):
+    def step_arrays(self, blob_idx, ptrs, offsets, lengths, stream=None, sha_stream=None, crc_after_sha=False):
         """step() from numpy arrays (one window of thousands of chunks, no Python loop);
-        sha_stream: the SHA-256 launch's stream (krk_metainfo_digest_chunks_dev_on)."""
+        sha_stream: the SHA-256 launch's stream (krk_metainfo_digest_chunks_dev_on);
+        crc_after_sha: the CRCs on `stream` once that launch has ended (_after)."""
         arr = chunk_array(ptrs, offsets, lengths, self.lengths[blob_idx], self.piece_lengths[blob_idx],
                           self.sums_off[blob_idx], blob_idx)
-        check(lib.krk_metainfo_digest_chunks_dev_on(arr.ctypes.data_as(C.POINTER(krk_chunk)), len(arr), self.state.ptr,
-                                                    self.sums.ptr, self.digests.ptr, stream, sha_stream))
+        fn = lib.krk_metainfo_digest_chunks_dev_after if crc_after_sha else lib.krk_metainfo_digest_chunks_dev_on
+        check(fn(arr.ctypes.data_as(C.POINTER(krk_chunk)), len(arr), self.state.ptr, self.sums.ptr, self.digests.ptr,
+                 stream, sha_stream))
 
     def step(self, items, stream=None):
         """items: [(blob index, device address of the chunk, offset, length)]."""

@@ -768,7 +768,8 @@ class TailHandoffRun:
             while win is not None and not err:
                 blobs, offs, tk = win
                 pol.queued(blobs, offs, tk)
-                self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s)
+                self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s,
+                                    crc_after_sha=True)
                 take = self._flush_crcs(self.run_s)
                 ev = new_event()
                 D.check(D.lib.krk_event_record(ev, self.run_s))
