@@ -615,8 +615,11 @@ class TailHandoffRun:
                 self._cv.notify_all()
 
     def _free_at(self, i, now):
-        """When thread i is expected to be done with its queued chains, at its measured rate."""
-        rate = self._done_bytes[i] / self._busy_s[i] if self._busy_s[i] > 0.5 else self.h
+        """When thread i is expected to be done with its queued chains, at the rate its pieces
+        have been copied and hashed so far (not counting its waits for midstates: a thread
+        predicted late gets its next chain late and then waits for it)."""
+        t = self._phase[i]["hash"]
+        rate = self._done_bytes[i] / t if t > 0.3 else self.h
         return (self._t_last[i] if self._jobs[i] else now) + max(0, self._left[i]) / max(rate, 1e6)
 
     # ---- the loop's side: generate pieces into free slots, queue their CRCs
