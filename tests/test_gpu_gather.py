@@ -210,7 +210,7 @@ def test_gather_mixed_pinned_mappings(gpu, orc):
     import ctypes as C
     import mmap
 
-    hip = C.CDLL("libamdhip64.so")
+    hip = C.CDLL(D.lib._name)  # the HIP runtime the library itself links (not another copy in the process)
     hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
     hip.hipHostUnregister.argtypes = [C.c_void_p]
     m = mmap.mmap(-1, 32 << 20)

@@ -420,7 +420,7 @@ def test_ring_locations_into_managed_memory(gpu):
     """outputs in managed memory (hipMallocManaged) are device-writable -- the
     placement kernels write them like device memory -- and give the device outputs' lists."""
     import ctypes as C
-    hip = C.CDLL("libamdhip64.so")
+    hip = C.CDLL(D.lib._name)  # the HIP runtime the library itself links (not another copy in the process)
     hip.hipMallocManaged.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
     hip.hipFree.argtypes = [C.c_void_p]
     labels = [f"origin-{i:03d}.kraken.test:15002" for i in range(16)]
