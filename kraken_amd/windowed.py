@@ -457,12 +457,14 @@ def simulate_tail_handoff(lens, W, cap, threads, rates, launch_s=0.0005, max_chu
     windows after window k takes a chain, whose midstate is ready when window k ends.  Returns the
     modelled end (s), the GPU windows' end, the host bytes and the takeovers."""
     L = np.asarray(lens, dtype=np.int64)
-    H = max(1, int(threads))
-    h = tail_thread_rate(rates, H)
-    pol = TailPolicy(L, H)
-    first = pol.initial()
+    H = max(0, int(threads))  # 0: the windows alone (the GPU-only model)
+    h = tail_thread_rate(rates, max(H, 1))
+    pol = TailPolicy(L, max(H, 1))
+    first = pol.initial() if H else []
+    if not H:
+        pol.on_gpu[:] = True
     free = [float(L[b]) / h for b in first] + [0.0] * (H - len(first))
-    host_bytes = int(L[first].sum())
+    host_bytes = int(L[first].sum()) if H else 0
     takes = 0
     sched = _Sched(L, np.nonzero(pol.on_gpu)[0], W, cap, max_chunk)
     t = 0.0  # end of the previous window = start of this one

@@ -24,8 +24,8 @@ for step in "$@"; do
     bench) run bench_c2 300 python bench.py ;;
     c3w8) run bench_c3_w8 600 python -u bench.py --workload c3 --emulate-world 8 --tail-handoff --host-lane --no-e2e ;;
     c3w8_tail) run bench_c3_w8_tail 200 $C3T ;;
-    c3w4_tail) run bench_c3_w4_tail 200 python -u bench.py --workload c3 --emulate-world 4 --c3-tail-only --no-e2e --no-cpu-baseline ;;
-    c3w2_tail) run bench_c3_w2_tail 200 python -u bench.py --workload c3 --emulate-world 2 --c3-tail-only --no-e2e --no-cpu-baseline ;;
+    c3w4) run bench_c3_w4 400 python -u bench.py --workload c3 --emulate-world 4 --tail-handoff --no-e2e --no-cpu-baseline ;;
+    c3w2) run bench_c3_w2 400 python -u bench.py --workload c3 --emulate-world 2 --tail-handoff --no-e2e --no-cpu-baseline ;;
     c3) run bench_c3 900 python -u bench.py --workload c3 --tail-handoff ;;
     tail_sweep) for cfg in "6 64" "12 64" "16 32"; do set -- $cfg
                     run c3_tail_r$1_p$2 200 $C3T --tail-ring $1 --tail-piece-mib $2; done ;;
