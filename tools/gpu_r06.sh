@@ -31,7 +31,7 @@ for step in "$@"; do
                     run c3_tail_r$1_p$2 200 $C3T --tail-ring $1 --tail-piece-mib $2; done ;;
     tail_probe) run tail_probe 200 python -u tools/tail_probe.py 15 ;;
     prof_c3w8) run prof_c3w8 400 rocprofv3 --kernel-trace --stats --output-format csv \
-                  -d gpurun_out/prof_c3w8 -- python3 bench.py --workload c3 --emulate-world 8 --no-e2e --no-cpu-baseline --no-ceiling ;;
+                  -d gpurun_out/prof_c3w8 -- python3 bench.py --workload c3 --emulate-world 8 --tail-handoff --no-e2e --no-cpu-baseline --no-ceiling ;;
     prof_c3) run prof_c3 400 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c3 -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
     # PMC passes of C3's windows (N=1), each pass its own run (counter limits per block)
