@@ -43,6 +43,15 @@ for step in "$@"; do
                   -d gpurun_out/pmc_c3_wait -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
     pmc_c3_hbm) run pmc_c3_hbm 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
                   -d gpurun_out/pmc_c3_hbm -- python3 bench.py --workload c3 --no-e2e --no-cpu-baseline --no-ceiling ;;
+    # the two-lane plan alone: 14,336 streams of 16 MiB in one device-resident launch (C3's
+    # live count), plain and under the PMC pass the C3 windows got
+    small2l) run bench_small2l 300 python -u bench.py --workload small --blobs 14336 --no-e2e --no-cpu-baseline --no-offload ;;
+    pmc_small2l) run pmc_small2l 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES \
+                  SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv \
+                  -d gpurun_out/pmc_small2l -- python3 bench.py --workload small --blobs 14336 --no-e2e --no-cpu-baseline --no-ceiling --no-offload --steps 1 --warmup 1 ;;
+    pmc_small2l_wait) run pmc_small2l_wait 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY \
+                  SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv \
+                  -d gpurun_out/pmc_small2l_wait -- python3 bench.py --workload small --blobs 14336 --no-e2e --no-cpu-baseline --no-ceiling --no-offload --steps 1 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
