@@ -52,6 +52,13 @@ for step in "$@"; do
     pmc_small2l_wait) run pmc_small2l_wait 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY \
                   SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv \
                   -d gpurun_out/pmc_small2l_wait -- python3 bench.py --workload small --blobs 14336 --no-e2e --no-cpu-baseline --no-ceiling --no-offload --steps 1 --warmup 1 ;;
+    bench_f1) run bench_f1verify 600 python -u bench.py --workload f1verify ;;
+    bench_c4) run bench_c4 600 python -u bench.py --workload c4 ;;
+    bench_files) run bench_files 900 python -u bench.py --workload files --steps 2 --warmup 1 ;;
+    bench_c5) run bench_c5 300 python -u bench.py --workload c5 ;;
+    bench_c5regen) run bench_c5regen 600 python -u bench.py --workload c5regen ;;
+    bench_c1) run bench_c1 300 python -u bench.py --workload c1 --steps 2 --warmup 1 ;;
+    bench_defaults) run bench_defaults 300 python -u bench.py --workload defaults ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
