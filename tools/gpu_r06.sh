@@ -59,6 +59,8 @@ for step in "$@"; do
     bench_c5regen) run bench_c5regen 600 python -u bench.py --workload c5regen ;;
     bench_c1) run bench_c1 300 python -u bench.py --workload c1 --steps 2 --warmup 1 ;;
     bench_defaults) run bench_defaults 300 python -u bench.py --workload defaults ;;
+    prof_c2) run prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
