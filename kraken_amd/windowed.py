@@ -493,6 +493,9 @@ def simulate_tail_handoff(lens, W, cap, threads, rates, launch_s=0.0005, max_chu
             "thread_rate_Bps": h}
 
 
+_CRC_UNQUEUED = object()  # a ring slot whose piece's CRC has not been flushed to the device yet
+
+
 class TailHandoffRun:
     """A windowed batch (the WindowedRun layout: synthetic blobs generated window by window on
     the device, two device windows, one ChunkedBatch) with the tail handoff: `threads` host
@@ -634,7 +637,7 @@ class TailHandoffRun:
         self._left[i] += L - y
 
     def _service(self):
-        """Every free ring slot (copied down and its CRC done) refilled with its thread's next
+        """Every free ring slot (copied down, its CRC queued and done) refilled with its thread's next
         piece: generated on the generator stream, waited for, handed to the thread; their CRCs
         go with the next flush.  Returns the pieces generated."""
         D = self.D
@@ -646,6 +649,8 @@ class TailHandoffRun:
                     if self._slot_used[i][k]:
                         break
                     ev = self._slot_crc[i][k]
+                    if ev is _CRC_UNQUEUED:  # its piece's CRC is not even queued yet
+                        break
                     if ev is not None:
                         done = C.c_int(0)
                         D.check(D.lib.krk_event_query(ev, C.byref(done)))
@@ -654,6 +659,7 @@ class TailHandoffRun:
                         self._slot_crc[i][k] = None
                     b, o, m = self._to_gen[i].pop(0)
                     self._slot_used[i][k] = True
+                    self._slot_crc[i][k] = _CRC_UNQUEUED if m > 0 else None  # until _release
                     self._next_slot[i] = (k + 1) % self.ring
                     gen.append((i, k, b, o, m))
         if not gen:

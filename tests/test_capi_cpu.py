@@ -773,6 +773,64 @@ def test_tail_handoff_model_accounts_every_byte():
     assert m["takeovers"] >= 15
 
 
+def test_tail_ring_slot_held_until_its_crc_is_queued():
+    """TailHandoffRun's ring (no device: a stand-in records every generation into a slot).  A
+    thread may copy a piece down and free its slot before the loop has flushed that piece's
+    CRC; the slot must not be regenerated until the CRC is queued and its event done -- the
+    round-6 GPU failure was a 1 MiB-piece run whose ring wrapped inside one window wait and
+    overwrote pieces whose CRCs had not run (wrong sums, right digests)."""
+    import threading
+    from kraken_amd import windowed as WN
+
+    class Buf:
+        def __init__(self, p):
+            self.ptr = p
+
+    class Lib:
+        def __init__(self):
+            self.done = {}
+
+        def krk_event_query(self, ev, out):
+            out._obj.value = int(self.done.get(ev.value, 0))
+            return 0
+
+        def krk_stream_sync(self, s):
+            return 0
+
+    class FakeD:
+        def __init__(self):
+            self.lib = Lib()
+            self.fills = []
+
+        def check(self, rc):
+            assert rc == 0
+
+        def synth_fill_chunk_arrays(self, ids, ptr, off, n, stream=None):
+            self.fills.extend(int(p) for p in ptr)
+
+    D = FakeD()
+    r = WN.TailHandoffRun.__new__(WN.TailHandoffRun)
+    r.D, r.H, r.ring, r.piece = D, 1, 2, 64
+    r.ids = np.arange(4, dtype=np.uint64)
+    r.gen_s = C.c_void_p()
+    r.tbuf = [[Buf(0x1000), Buf(0x2000)]]
+    r._cv = threading.Condition(threading.Lock())
+    r._to_gen = [[(0, o, 64) for o in range(0, 6 * 64, 64)]]
+    r._ready, r._pending, r._tail_pieces = [[]], [], 0
+    r._slot_used, r._slot_crc, r._next_slot = [[False, False]], [[None, None]], [0]
+    assert len(r._service()) == 2  # both slots filled
+    r._ready[0].clear()
+    r._slot_used[0] = [False, False]  # the thread copied both down ...
+    assert r._service() == [] and D.fills == [0x1000, 0x2000]  # ... but no CRC is queued yet
+    take = r._pending[:]
+    r._pending.clear()  # what _flush_crcs does, then _release with the event after it
+    ev = C.c_void_p(77)
+    r._release(take, ev)
+    assert r._service() == []  # queued, not done
+    D.lib.done[77] = 1
+    assert len(r._service()) == 2 and D.fills[2:] == [0x1000, 0x2000]
+
+
 def test_production_library_reads_only_the_operator_knobs():
     """the production library's environment is INTEGRATION.md's operator
     table, exactly -- every KRK_* name in its strings is in the table and every table entry is

@@ -82,19 +82,22 @@ def test_window_plan_covers_c3_law_once():
     assert np.array_equal(pos, np.asarray(lens, dtype=np.uint64))
 
 
-@pytest.mark.parametrize("cap,threads,piece", [(None, 3, 64 << 20), (200, 4, 64 << 20), (None, 5, 1 << 20)])
-def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, piece):
+@pytest.mark.parametrize("cap,threads,piece,ring", [(None, 3, 64 << 20, 8), (200, 4, 64 << 20, 8), (None, 5, 1 << 20, 8),
+                                                    (None, 5, 1 << 20, 2)])
+def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, piece, ring):
     """the windowed batch with the tail handoff (windowed.TailHandoffRun):
     host threads start on the longest chains whole, then steal the chains with the most bytes
     left at window boundaries -- live chains from the midstate the windows left in HBM, and
     (cap=200) blobs still waiting for admission from the IV -- while their remaining piece
     CRCs run on the GPU beside the windows'.  1 MiB window chunks: hundreds of windows and
-    takeovers.  piece=1 MiB: a thread's chain spans many device pieces, so its ring of six
-    slots wraps inside one chain and one window's CRC flush carries several pieces of one
-    blob.  Every blob equals the one-shot device path; sampled blobs the oracle."""
+    takeovers.  piece=1 MiB: a thread's chain spans many device pieces, so its ring wraps
+    inside one chain and one window's CRC flush carries several pieces of one blob; ring=2
+    wraps inside one window wait, where a slot a thread has copied down may not be refilled
+    before its piece's CRC is queued (a round-6 failure: right digests, wrong sums).  Every
+    blob equals the one-shot device path; sampled blobs the oracle."""
     from kraken_amd.windowed import TailHandoffRun
     lens, ids, dg1, sums1, offs1, counts1 = one_shot
-    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20, piece=piece)
+    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20, piece=piece, ring=ring)
     tr.run()
     st = tr.stats
     cb = tr.cb
