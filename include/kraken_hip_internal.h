@@ -70,13 +70,8 @@ int krk_metainfo_digest_chunks_dev_after(const krk_chunk* chunks, uint64_t n, ui
  * window's; several chunks of one blob allowed): the tails of chains a host thread hashes.
  * Asynchronous on `stream`. */
 int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, void* stream);
-/* Continue one SHA-256 chain on the calling thread from n device bytes at data_dev (after
- * the work queued on `stream`; NULL: the bytes are ready now, nothing is waited for): state8 holds the midstate after `absorbed` bytes (a multiple
- * of 64) and is updated by a non-final run (n whole blocks); final != 0 pads and writes the
- * digest to digest32 instead (n any length).  Read through pinned double buffers, x86 SHA
- * extensions.  Synchronous. */
 /* The calling thread's cumulative seconds in krk_sha256_resume_dev_on_host waiting for its
- * device-to-host copies and hashing. */
+ * device-to-host copies and hashing (krk_sha256_resume_host's hashing counts too). */
 int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s);
 /* ... and in enqueueing its copies and waiting for the caller's stream. */
 int krk_sha256_resume_stats2(double* issue_s, double* ready_s);
@@ -87,8 +82,18 @@ int krk_event_query(void* ev, int* done);
 int krk_event_create_polling(void** out);
 /* Work queued on `stream` after the call waits for event `ev` (hipStreamWaitEvent). */
 int krk_stream_wait_event(void* stream, void* ev);
+/* Continue one SHA-256 chain on the calling thread from n device bytes at data_dev (after
+ * the work queued on `stream`; NULL: the bytes are ready now, nothing is waited for): state8
+ * holds the midstate after `absorbed` bytes (a multiple of 64) and is updated by a non-final
+ * run (n whole blocks); final != 0 pads and writes the digest to digest32 instead (n any
+ * length).  Read through pinned buffers (copies three ahead), x86 SHA extensions.
+ * Synchronous. */
 int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uint8_t* data_dev, uint64_t n,
                                   int final, uint8_t* digest32, void* stream);
+/* The same continuation over n bytes already in host memory (a device-to-host copy the
+ * caller queued and waited for): no device call. */
+int krk_sha256_resume_host(uint32_t* state8, uint64_t absorbed, const uint8_t* data_host, uint64_t n, int final,
+                           uint8_t* digest32);
 /* The live-stream cap of the windows on the calling thread's device: 7/8 of the largest
  * stream count whose SHA-256 launch runs more than one lane a stream (14,336 on 256 CUs),
  * so each window's CRC launch has the CUs the SHA workgroups leave free.  KRK_LIVE_CAP

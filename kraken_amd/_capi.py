@@ -131,6 +131,7 @@ def _load() -> C.CDLL:
         "krk_window_sched_set_chunk_cap": (i, [vp, C.c_uint64]),
         "krk_chunks_crc_dev": (i, [C.POINTER(krk_chunk), C.c_uint64, vp, vp]),
         "krk_sha256_resume_dev_on_host": (i, [u32p, C.c_uint64, vp, C.c_uint64, i, u8p, vp]),
+        "krk_sha256_resume_host": (i, [u32p, C.c_uint64, vp, C.c_uint64, i, u8p]),
         "krk_window_stream_cap": (i, [u64p]),
         "krk_windows_last_call": (i, [u64p, C.POINTER(C.c_int), u64p]),
         "krk_windows_last_direct": (i, [C.POINTER(C.c_int)]),

@@ -1055,6 +1055,22 @@ int krk_sha256_resume_dev_on_host(uint32_t* state8, uint64_t absorbed, const uin
     return r;
 }
 
+int krk_sha256_resume_host(uint32_t* state8, uint64_t absorbed, const uint8_t* data_host, uint64_t n, int final,
+                           uint8_t* digest32) {
+    KRK_CHECK(state8, KRK_EINVAL, "sha256_resume: state is NULL");
+    KRK_CHECK(n == 0 || data_host, KRK_EINVAL, "sha256_resume: data is NULL");
+    KRK_CHECK(absorbed % 64 == 0, KRK_EINVAL, "sha256_resume: absorbed bytes not a multiple of 64");
+    KRK_CHECK(final || n % 64 == 0, KRK_EINVAL, "sha256_resume: a non-final run must be whole 64-byte blocks");
+    KRK_CHECK(!final || digest32, KRK_EINVAL, "sha256_resume: digest is NULL");
+    const auto t = std::chrono::steady_clock::now();
+    if (!final)
+        host_sha256_blocks(state8, data_host, n / 64);
+    else
+        host_sha256_final(state8, absorbed, data_host, n, digest32);
+    t_resume_hash += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+    return KRK_OK;
+}
+
 int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s) {
     if (copy_wait_s) *copy_wait_s = t_resume_wait;
     if (hash_s) *hash_s = t_resume_hash;

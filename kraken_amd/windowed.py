@@ -515,7 +515,7 @@ class TailHandoffRun:
     and the generator's launches (no LDS, never blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
-                 ring=TAIL_RING):
+                 ring=TAIL_RING, loop_copies=True):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -539,6 +539,22 @@ class TailHandoffRun:
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
+        # loop_copies: the loop also copies each generated piece down (one stream, whole
+        # pieces) into a pinned twin of its slot, and the threads only hash host memory;
+        # otherwise each thread copies its pieces itself (8 MiB copies on a stream of its own)
+        self.loop_copies = bool(loop_copies)
+        self.copy_s = C.c_void_p()
+        self.hbuf, self.slot_ev = [], []
+        if self.loop_copies:
+            D.check(D.lib.krk_stream_create(C.byref(self.copy_s)))
+            self.hbuf = [[D.PinnedArray((self.piece,), np.uint8) for _ in range(self.ring)] for _ in range(self.H)]
+            for _ in range(self.H):
+                row = []
+                for _ in range(self.ring):
+                    e = C.c_void_p()
+                    D.check(D.lib.krk_event_create_polling(C.byref(e)))
+                    row.append(e)
+                self.slot_ev.append(row)
         self.stats = {}
 
     # ---- the host threads: copy and hash
@@ -568,9 +584,18 @@ class TailHandoffRun:
                 k, pb, po, pm = self._ready[i].pop(0)
             assert pb == b and po == y + c * self.piece, (pb, po, b, y, c)
             t2 = clk()
-            D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
-                                                        C.c_void_p(self.tbuf[i][k].ptr), pm, int(c + 1 == nch),
-                                                        out.ctypes.data_as(C.POINTER(C.c_uint8)), None))
+            if self.loop_copies:
+                if pm:
+                    D.check(D.lib.krk_event_sync(self.slot_ev[i][k]))  # the loop's copy of the piece
+                t2b = clk()
+                ph["copy_wait"] = ph.get("copy_wait", 0.0) + t2b - t2
+                D.check(D.lib.krk_sha256_resume_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
+                                                     C.c_void_p(self.hbuf[i][k].ptr), pm, int(c + 1 == nch),
+                                                     out.ctypes.data_as(C.POINTER(C.c_uint8))))
+            else:
+                D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
+                                                            C.c_void_p(self.tbuf[i][k].ptr), pm, int(c + 1 == nch),
+                                                            out.ctypes.data_as(C.POINTER(C.c_uint8)), None))
             t3 = clk()
             ph["device"] += t2 - t1
             ph["hash"] += t3 - t2
@@ -605,7 +630,7 @@ class TailHandoffRun:
                     self._cv.notify_all()
             self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
             self.D.check(self.D.lib.krk_sha256_resume_stats2(C.byref(iss), C.byref(rdy)))
-            self._phase[i]["copy_wait"] = w.value - w0
+            self._phase[i]["copy_wait"] = self._phase[i].get("copy_wait", 0.0) + w.value - w0
             self._phase[i]["sha"] = hh.value - h0
             self._phase[i]["copy_issue"] = iss.value - i0
             self._phase[i]["ready_wait"] = rdy.value - r0
@@ -671,6 +696,11 @@ class TailHandoffRun:
             D.synth_fill_chunk_arrays(self.ids[bl], ptr, np.array([g[3] for g in live], np.uint64),
                                       np.array([g[4] for g in live], np.uint64), stream=self.gen_s)
             D.check(D.lib.krk_stream_sync(self.gen_s))
+            if self.loop_copies:  # each piece down into its slot's pinned twin, then its event
+                for i, k, _, _, m in live:
+                    D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
+                                                       C.c_void_p(self.tbuf[i][k].ptr), m, self.copy_s))
+                    D.check(D.lib.krk_event_record(self.slot_ev[i][k], self.copy_s))
         with self._cv:
             for i, k, b, o, m in gen:
                 self._ready[i].append((k, b, o, m))
@@ -893,13 +923,18 @@ class TailHandoffRun:
         self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
 
     def close(self):
+        if self.copy_s.value:
+            self.D.lib.krk_stream_sync(self.copy_s)
         for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
-        self.bufs, self.tbuf = [], []
-        for s in [self.gen_s, self.run_s, self.sha_s]:
+        self.bufs, self.tbuf, self.hbuf = [], [], []
+        for e in [e for row in self.slot_ev for e in row]:
+            self.D.lib.krk_event_destroy(e)
+        self.slot_ev = []
+        for s in [self.gen_s, self.run_s, self.sha_s, self.copy_s]:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s, self.run_s, self.sha_s = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self.gen_s, self.run_s, self.sha_s, self.copy_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
 
     def __del__(self):
         try:

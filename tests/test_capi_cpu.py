@@ -810,7 +810,7 @@ def test_tail_ring_slot_held_until_its_crc_is_queued():
 
     D = FakeD()
     r = WN.TailHandoffRun.__new__(WN.TailHandoffRun)
-    r.D, r.H, r.ring, r.piece = D, 1, 2, 64
+    r.D, r.H, r.ring, r.piece, r.loop_copies = D, 1, 2, 64, False
     r.ids = np.arange(4, dtype=np.uint64)
     r.gen_s = C.c_void_p()
     r.tbuf = [[Buf(0x1000), Buf(0x2000)]]
