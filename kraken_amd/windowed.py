@@ -542,6 +542,10 @@ class TailHandoffRun:
         # loop_copies: the loop also copies each generated piece down (one stream, whole
         # pieces) into a pinned twin of its slot, and the threads only hash host memory;
         # otherwise each thread copies its pieces itself (8 MiB copies on a stream of its own)
+        # every window's midstates, copied down after its step on the window stream: a stolen
+        # chain's midstate is read here once the window's event is done (a synchronous copy
+        # would queue behind other streams' packets in a shared hardware queue)
+        self.state_host = D.PinnedArray((n, 8), np.uint32)
         self.loop_copies = bool(loop_copies)
         self.copy_s = C.c_void_p()
         self.hbuf, self.slot_ev = [], []
@@ -571,7 +575,7 @@ class TailHandoffRun:
         if y:
             tw = clk()
             D.check(D.lib.krk_event_sync(ev))  # the window that last advanced chain b is done
-            D.check(D.lib.krk_memcpy_d2h(h.ctypes.data_as(C.c_void_p), C.c_void_p(self.cb.state.ptr + 32 * b), 32))
+            h = self.state_host.a[b].copy()  # copied down before that window's event
             ph["midstate"] += clk() - tw
         out = np.zeros(32, dtype=np.uint8)
         for c in range(nch):
@@ -812,6 +816,8 @@ class TailHandoffRun:
                 self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s,
                                     crc_after_sha=True)
                 take = self._flush_crcs(self.run_s)
+                D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.state_host.ptr), C.c_void_p(self.cb.state.ptr),
+                                                   32 * n, self.run_s))
                 ev = new_event()
                 D.check(D.lib.krk_event_record(ev, self.run_s))
                 wev.append(ev)
