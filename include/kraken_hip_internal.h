@@ -75,6 +75,11 @@ int krk_chunks_crc_dev(const krk_chunk* chunks, uint64_t n, uint32_t* sums_dev, 
 int krk_sha256_resume_stats(double* copy_wait_s, double* hash_s);
 /* ... and in enqueueing its copies and waiting for the caller's stream. */
 int krk_sha256_resume_stats2(double* issue_s, double* ready_s);
+/* Page-locked host memory from the HIP runtime's own allocator (hipHostMalloc), which places
+ * it on the NUMA node nearest the calling thread's device: targets of device-to-host copies
+ * (krk_host_alloc's pages land on the allocating thread's node; 53 vs 56 GB/s measured,
+ * tools/pinned_d2h_probe.py).  Freed by krk_host_free. */
+int krk_host_alloc_dma(uint64_t bytes, void** out);
 /* *done = 1 once event `ev` has completed, else 0 (no wait). */
 int krk_event_query(void* ev, int* done);
 /* An event whose krk_event_sync polls instead of sleeping: for waits of microseconds (a

@@ -160,6 +160,7 @@ def _load() -> C.CDLL:
         "krk_dev_alloc": (i, [C.c_uint64, C.POINTER(vp)]),
         "krk_dev_free": (i, [vp]),
         "krk_host_alloc": (i, [C.c_uint64, C.POINTER(vp)]),
+        "krk_host_alloc_dma": (i, [C.c_uint64, C.POINTER(vp)]),
         "krk_host_free": (i, [vp]),
         "krk_memcpy_h2d": (i, [vp, vp, C.c_uint64]),
         "krk_memcpy_d2h": (i, [vp, vp, C.c_uint64]),

@@ -1916,6 +1916,17 @@ int krk_host_alloc(uint64_t bytes, void** out) {
     g_host_ranges[reinterpret_cast<uintptr_t>(*out)] = bytes ? bytes : 1;
     return KRK_OK;
 }
+int krk_host_alloc_dma(uint64_t bytes, void** out) {
+    KRK_CHECK(out, KRK_EINVAL, "out is NULL");
+    KRK_DEVICE(D);
+    (void)D;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    KRK_CHECK(e == hipSuccess, KRK_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
+              hipGetErrorString(e));
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host_ranges[reinterpret_cast<uintptr_t>(*out)] = bytes ? bytes : 1;
+    return KRK_OK;
+}
 int krk_host_free(void* p) {
     size_t len = 0;
     {

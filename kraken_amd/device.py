@@ -50,10 +50,12 @@ class PinnedArray:
     """A numpy view of library-allocated pinned host memory (krk_host_alloc):
     device results land here at PCIe rate instead of through a pageable bounce."""
 
-    def __init__(self, shape, dtype):
+    def __init__(self, shape, dtype, dma_target=False):
+        """dma_target: the HIP runtime's allocator (krk_host_alloc_dma: the device's NUMA
+        node) for buffers the device copies into."""
         self.array_nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
         p = C.c_void_p()
-        check(lib.krk_host_alloc(max(self.array_nbytes, 1), C.byref(p)))
+        check((lib.krk_host_alloc_dma if dma_target else lib.krk_host_alloc)(max(self.array_nbytes, 1), C.byref(p)))
         self.ptr = p.value
         buf = (C.c_uint8 * max(self.array_nbytes, 1)).from_address(self.ptr)
         self.a = np.frombuffer(buf, dtype=np.uint8, count=self.array_nbytes).view(dtype).reshape(shape)

@@ -515,7 +515,7 @@ class TailHandoffRun:
     and the generator's launches (no LDS, never blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
-                 ring=TAIL_RING, loop_copies=True):
+                 ring=TAIL_RING, loop_copies=True, copy_streams=1):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -545,13 +545,17 @@ class TailHandoffRun:
         # every window's midstates, copied down after its step on the window stream: a stolen
         # chain's midstate is read here once the window's event is done (a synchronous copy
         # would queue behind other streams' packets in a shared hardware queue)
-        self.state_host = D.PinnedArray((n, 8), np.uint32)
+        self.state_host = D.PinnedArray((n, 8), np.uint32, dma_target=True)
         self.loop_copies = bool(loop_copies)
-        self.copy_s = C.c_void_p()
+        self.copy_s = []
         self.hbuf, self.slot_ev = [], []
         if self.loop_copies:
-            D.check(D.lib.krk_stream_create(C.byref(self.copy_s)))
-            self.hbuf = [[D.PinnedArray((self.piece,), np.uint8) for _ in range(self.ring)] for _ in range(self.H)]
+            for _ in range(max(1, int(copy_streams))):  # threads spread over them (i % count)
+                cs = C.c_void_p()
+                D.check(D.lib.krk_stream_create(C.byref(cs)))
+                self.copy_s.append(cs)
+            self.hbuf = [[D.PinnedArray((self.piece,), np.uint8, dma_target=True) for _ in range(self.ring)]
+                         for _ in range(self.H)]
             for _ in range(self.H):
                 row = []
                 for _ in range(self.ring):
@@ -703,8 +707,9 @@ class TailHandoffRun:
             if self.loop_copies:  # each piece down into its slot's pinned twin, then its event
                 for i, k, _, _, m in live:
                     D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
-                                                       C.c_void_p(self.tbuf[i][k].ptr), m, self.copy_s))
-                    D.check(D.lib.krk_event_record(self.slot_ev[i][k], self.copy_s))
+                                                       C.c_void_p(self.tbuf[i][k].ptr), m,
+                                                       self.copy_s[i % len(self.copy_s)]))
+                    D.check(D.lib.krk_event_record(self.slot_ev[i][k], self.copy_s[i % len(self.copy_s)]))
         with self._cv:
             for i, k, b, o, m in gen:
                 self._ready[i].append((k, b, o, m))
@@ -929,18 +934,18 @@ class TailHandoffRun:
         self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
 
     def close(self):
-        if self.copy_s.value:
-            self.D.lib.krk_stream_sync(self.copy_s)
+        for cs in self.copy_s:
+            self.D.lib.krk_stream_sync(cs)
         for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
         self.bufs, self.tbuf, self.hbuf = [], [], []
         for e in [e for row in self.slot_ev for e in row]:
             self.D.lib.krk_event_destroy(e)
         self.slot_ev = []
-        for s in [self.gen_s, self.run_s, self.sha_s, self.copy_s]:
+        for s in [self.gen_s, self.run_s, self.sha_s] + self.copy_s:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s, self.run_s, self.sha_s, self.copy_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self.gen_s, self.run_s, self.sha_s, self.copy_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), []
 
     def __del__(self):
         try:
