@@ -563,6 +563,19 @@ class TailHandoffRun:
                     D.check(D.lib.krk_event_create_polling(C.byref(e)))
                     row.append(e)
                 self.slot_ev.append(row)
+            # every twin written once by DMA before the run (a page's first device write runs at
+            # about half the rate: 30 vs 56 GB/s measured), then the twins' copy rate, a record
+            # beside the run's copy waits
+            import time
+            for rep in range(2):
+                t0 = time.perf_counter()
+                for i in range(self.H):
+                    for k in range(self.ring):
+                        D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
+                                                           C.c_void_p(self.tbuf[i][k].ptr), self.piece,
+                                                           self.copy_s[0]))
+                D.check(D.lib.krk_stream_sync(self.copy_s[0]))
+                self.twin_GBps = self.H * self.ring * self.piece / (time.perf_counter() - t0) / 1e9
         self.stats = {}
 
     # ---- the host threads: copy and hash
@@ -919,7 +932,8 @@ class TailHandoffRun:
                       "thread_phases_s": {k: round(sum(p.get(k, 0.0) for p in self._phase), 3)
                                           for k in ("midstate", "device", "hash", "copy_wait", "sha", "copy_issue",
                                                     "ready_wait")},
-                      "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3)}
+                      "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3),
+                      **({"twin_copy_GBps_before_run": round(self.twin_GBps, 2)} if self.loop_copies else {})}
 
     def _items(self, win, k):
         blobs, offs, take = win

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 from kraken_amd import device as D  # noqa: E402
 
 PIECE = 64 << 20
-NBUF = 8
+NBUF = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 libc = C.CDLL(None, use_errno=True)
 
 
@@ -59,8 +59,13 @@ def main():
     cases["hipHostMalloc"] = hm
     for name, ptrs in cases.items():
         nodes = [numa_node(p) for p in ptrs]
-        print(json.dumps({"case": name, "GBps": round(rate(ptrs, src, s), 2), "numa_nodes": nodes,
-                          "cpu": os.sched_getaffinity(0).__len__()}), flush=True)
+        per = [round(rate([p], src, s, reps=2), 1) for p in ptrs]  # each buffer alone
+        print(json.dumps({"case": name, "buffers": len(ptrs), "GBps": round(rate(ptrs, src, s, reps=2), 2),
+                          "numa_nodes": {str(n): nodes.count(n) for n in sorted(set(nodes), key=str)},
+                          "per_buffer_GBps_min_median_max": [min(per), sorted(per)[len(per) // 2], max(per)],
+                          "slow_buffers_below_40": sum(x < 40 for x in per),
+                          "slow_by_node": {str(n): sum(1 for x, m in zip(per, nodes) if x < 40 and m == n)
+                                           for n in sorted(set(nodes), key=str)}}), flush=True)
 
 
 if __name__ == "__main__":
