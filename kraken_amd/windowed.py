@@ -515,7 +515,7 @@ class TailHandoffRun:
     and the generator's launches (no LDS, never blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
-                 ring=TAIL_RING, loop_copies=True, copy_streams=1):
+                 ring=TAIL_RING, loop_copies=True, copy_streams=1, crc_after_sha=True):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -546,6 +546,7 @@ class TailHandoffRun:
         # chain's midstate is read here once the window's event is done (a synchronous copy
         # would queue behind other streams' packets in a shared hardware queue)
         self.state_host = D.PinnedArray((n, 8), np.uint32, dma_target=True)
+        self.crc_after_sha = bool(crc_after_sha)  # False: a window's CRC beside its SHA launch (A/B)
         self.loop_copies = bool(loop_copies)
         self.copy_s = []
         self.hbuf, self.slot_ev = [], []
@@ -832,7 +833,7 @@ class TailHandoffRun:
                 blobs, offs, tk = win
                 pol.queued(blobs, offs, tk)
                 self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s,
-                                    crc_after_sha=True)
+                                    crc_after_sha=self.crc_after_sha)
                 take = self._flush_crcs(self.run_s)
                 D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.state_host.ptr), C.c_void_p(self.cb.state.ptr),
                                                    32 * n, self.run_s))
