@@ -12,7 +12,8 @@ everything in seconds: sampled oracle checks plus size-independent properties.
 * C3 (configs[2]'s blob law, unscaled): 256 seeded blobs of 100 MiB - 1 GiB (151.7 GB,
   the bench's CPU-baseline sample, its longest 1.07 GB) through the production window
   machinery (kraken_amd.windowed.WindowedRun, 48 GiB windows), every digest and piece sum
-  against the oracle.
+  against the oracle; and rank 0's whole 8-GPU shard (2,500 blobs, 1.47 TB) through the
+  GPU-only windows and the tail handoff, all digests and sums equal between the two.
 * C4 (configs[3]: one 20 GiB blob, 256 KiB pieces): sampled pieces against the
   oracle (content regenerated at the piece's offset), and CRC linearity -- the
   81,920 piece sums combined with crc(A||B) = shift(crc(A), |B|) ^ crc(B) equal the
@@ -182,3 +183,46 @@ def test_c4_full_size_sampled_and_linear(gpu, orc):
     check(lib.krk_piece_sums_dev(one, 1, s1.ptr, None))
     D.synchronize()
     assert int(s1.to_host(np.uint32, 1)[0]) == _combine(sums, P)
+
+
+def test_c3_shard_tail_handoff_whole_shard_equals_windows(gpu, orc):
+    """C3's multi-GPU config at full size (C3 checked on 256 of 20,000
+    blobs): rank 0's LPT shard of an 8-GPU run, 2,500 unscaled blobs (1.47 TB, longest
+    1.07 GB), through the GPU-only windows and through the tail handoff (host threads
+    finishing ~400 GB of chains on SHA-NI from the windows' midstates, the loop's copies and
+    the GPU's CRCs of the stolen pieces).  Every one of the 2,500 digests and ~350,000 piece
+    sums must agree between the two -- different work on different processors over the same
+    bytes -- and the shard's shortest and longest blobs match the oracle."""
+    from kraken_amd.shard import lpt_shard
+    from kraken_amd.windowed import TAIL_CHUNK, TailHandoffRun, WindowedRun, c3_lengths
+    lens_all = c3_lengths(20000)
+    mine = lpt_shard(lens_all, 8)[0]
+    ids = [(2 << 40) + int(i) for i in mine]
+    lens = [int(lens_all[i]) for i in mine]
+    P = 4 << 20
+    assert len(lens) == 2500 and max(lens) > 1_070_000_000
+    wr = WindowedRun(D, ids, lens, P, 10 << 30)
+    try:
+        wr.run()
+        dg = wr.cb.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+        sums = wr.cb.sums.to_host(np.uint32, wr.cb.total_pieces)
+        offs = wr.cb.sums_off.copy()
+    finally:
+        wr.close()
+    tr = TailHandoffRun(D, ids, lens, P, min(10 << 30, len(lens) * TAIL_CHUNK), 15)
+    try:
+        tr.run()
+        dg2 = tr.cb.digests.to_host(np.uint8, 32 * len(lens)).reshape(-1, 32)
+        sums2 = tr.cb.sums.to_host(np.uint32, tr.cb.total_pieces)
+        st = tr.stats
+    finally:
+        tr.close()
+    assert st["host_bytes"] > 100e9 and st["resumed_from_midstate"] > 100, st
+    assert np.array_equal(dg2, dg)
+    assert np.array_equal(sums2, sums)
+    for k in (int(np.argmin(lens)), int(np.argmax(lens))):
+        data = orc.synth(ids[k], lens[k])
+        assert bytes(dg[k]) == hashlib.sha256(data).digest(), k
+        a = int(offs[k])
+        want = orc.calc_piece_sums(data, P)[1]
+        assert np.array_equal(sums[a:a + len(want)], want), k
