@@ -493,6 +493,18 @@ def simulate_tail_handoff(lens, W, cap, threads, rates, launch_s=0.0005, max_chu
             "thread_rate_Bps": h}
 
 
+def _wait_summary(ws):
+    """The tail threads' midstate waits: how many, how many found the window already done,
+    wait and assignment-to-start percentiles (ms)."""
+    if not ws:
+        return {"n": 0}
+    w = np.array([x[0] for x in ws]) * 1e3
+    a = np.array([x[2] for x in ws]) * 1e3
+    return {"n": len(ws), "window_already_done": int(sum(x[1] for x in ws)), "over_5ms": int((w > 5).sum()),
+            "wait_ms_p50_p90_max": [round(float(np.percentile(w, q)), 2) for q in (50, 90, 100)],
+            "since_assigned_ms_p10_p50_p90": [round(float(np.percentile(a, q)), 1) for q in (10, 50, 90)]}
+
+
 _CRC_UNQUEUED = object()  # a ring slot whose piece's CRC has not been flushed to the device yet
 
 
@@ -545,7 +557,7 @@ class TailHandoffRun:
         # every window's midstates, copied down after its step on the window stream: a stolen
         # chain's midstate is read here once the window's event is done (a synchronous copy
         # would queue behind other streams' packets in a shared hardware queue)
-        self.state_host = D.PinnedArray((n, 8), np.uint32, dma_target=True)
+        self.state_host = [D.PinnedArray((n, 8), np.uint32, dma_target=True) for _ in range(2)]  # window k: k & 1
         self.crc_after_sha = bool(crc_after_sha)  # False: a window's CRC beside its SHA launch (A/B)
         self.loop_copies = bool(loop_copies)
         self.copy_s = []
@@ -580,21 +592,32 @@ class TailHandoffRun:
         self.stats = {}
 
     # ---- the host threads: copy and hash
-    def _job(self, i, b, y, ev, dig):
+    def _job(self, i, b, y, win, h0, dig):
         """Chain b from byte y: its pieces as the loop generates them into this thread's ring,
-        SHA-256 continued from the midstate the windows left in HBM (window event `ev`), or
-        from the IV when y == 0."""
+        SHA-256 continued from `h0` (a midstate the loop read at hand-over), else from the
+        midstate window `win` left (mirrored to host memory; the loop announces each window's
+        end in _win_done, so a worker makes no HIP call to learn it), or from the IV when
+        y == 0."""
         D = self.D
         L = int(self.lens[b])
         nch = max(1, -(-(L - y) // self.piece))
         ph = self._phase[i]
         clk = self._clock
         h = _IV.copy()
-        if y:
+        if h0 is not None:
+            h = h0
+        elif y:
             tw = clk()
-            D.check(D.lib.krk_event_sync(ev))  # the window that last advanced chain b is done
-            h = self.state_host.a[b].copy()  # copied down before that window's event
-            ph["midstate"] += clk() - tw
+            with self._cv:
+                done = self._win_done >= win
+                while self._win_done < win and not self._abort:  # the window that last advanced b
+                    self._cv.wait()
+                if self._abort:
+                    return
+            h = self.state_host[win & 1].a[b].copy()  # copied down before that window's event
+            dt = clk() - tw
+            ph["midstate"] += dt
+            self._mwaits[i].append((dt, done, tw - self._t_assigned.get((i, b), tw)))
         out = np.zeros(32, dtype=np.uint8)
         for c in range(nch):
             t1 = clk()
@@ -643,9 +666,9 @@ class TailHandoffRun:
                         self._cv.wait()
                     if not self._jobs[i] or self._abort:
                         break
-                    b, y, ev = self._jobs[i][0]
+                    b, y, win, hm = self._jobs[i][0]
                 t0 = time.perf_counter()
-                self._job(i, b, y, ev, dig)
+                self._job(i, b, y, win, hm, dig)
                 with self._cv:
                     self._jobs[i].pop(0)
                     self._busy_s[i] += time.perf_counter() - t0
@@ -675,12 +698,17 @@ class TailHandoffRun:
         return (self._t_last[i] if self._jobs[i] else now) + max(0, self._left[i]) / max(rate, 1e6)
 
     # ---- the loop's side: generate pieces into free slots, queue their CRCs
-    def _assign(self, i, b, y, ev):
-        """Chain b from byte y becomes thread i's next job (caller holds the lock)."""
-        self._jobs[i].append((b, y, ev))
+    def _assign(self, i, b, y, win, h0=None, crc_from=None):
+        """Chain b from byte y (its midstate after window `win`, or h0) becomes thread i's
+        next job (caller holds the lock).  Its pieces' CRCs cover bytes from crc_from (y
+        unless a window already summed [y, crc_from))."""
+        self._jobs[i].append((b, y, win, h0))
+        self._t_assigned[(i, b)] = self._clock()
         L = int(self.lens[b])
+        cf = y if crc_from is None else int(crc_from)
         for o in range(y, max(L, y + 1), self.piece):
-            self._to_gen[i].append((b, o, min(self.piece, L - o)))
+            m = min(self.piece, L - o)
+            self._to_gen[i].append((b, o, m, min(m, max(0, cf - o))))
         self._left[i] += L - y
 
     def _service(self):
@@ -704,31 +732,31 @@ class TailHandoffRun:
                         if not done.value:
                             break
                         self._slot_crc[i][k] = None
-                    b, o, m = self._to_gen[i].pop(0)
+                    b, o, m, c0 = self._to_gen[i].pop(0)
                     self._slot_used[i][k] = True
-                    self._slot_crc[i][k] = _CRC_UNQUEUED if m > 0 else None  # until _release
+                    self._slot_crc[i][k] = _CRC_UNQUEUED if m > c0 else None  # until _release
                     self._next_slot[i] = (k + 1) % self.ring
-                    gen.append((i, k, b, o, m))
+                    gen.append((i, k, b, o, m, c0))
         if not gen:
             return gen
         live = [g for g in gen if g[4] > 0]
         if live:
-            ptr = np.array([self.tbuf[i][k].ptr for i, k, _, _, _ in live], dtype=np.uint64)
-            bl = np.array([b for _, _, b, _, _ in live], dtype=np.int64)
+            ptr = np.array([self.tbuf[i][k].ptr for i, k, _, _, _, _ in live], dtype=np.uint64)
+            bl = np.array([g[2] for g in live], dtype=np.int64)
             D.synth_fill_chunk_arrays(self.ids[bl], ptr, np.array([g[3] for g in live], np.uint64),
                                       np.array([g[4] for g in live], np.uint64), stream=self.gen_s)
             D.check(D.lib.krk_stream_sync(self.gen_s))
             if self.loop_copies:  # each piece down into its slot's pinned twin, then its event
-                for i, k, _, _, m in live:
+                for i, k, _, _, m, _ in live:
                     D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
                                                        C.c_void_p(self.tbuf[i][k].ptr), m,
                                                        self.copy_s[i % len(self.copy_s)]))
                     D.check(D.lib.krk_event_record(self.slot_ev[i][k], self.copy_s[i % len(self.copy_s)]))
         with self._cv:
-            for i, k, b, o, m in gen:
+            for i, k, b, o, m, c0 in gen:
                 self._ready[i].append((k, b, o, m))
-                if m > 0:
-                    self._pending.append((i, k, b, o, m))
+                if m > c0:  # the CRC of its bytes from c0 on
+                    self._pending.append((i, k, b, o + c0, m - c0, c0))
             self._cv.notify_all()
         self._tail_pieces += len(gen)
         return gen
@@ -741,8 +769,8 @@ class TailHandoffRun:
             take, self._pending = self._pending, []
         if not take:
             return take
-        ptr = np.array([self.tbuf[i][k].ptr for i, k, _, _, _ in take], dtype=np.uint64)
-        bl = np.array([b for _, _, b, _, _ in take], dtype=np.int64)
+        ptr = np.array([self.tbuf[i][k].ptr + c0 for i, k, _, _, _, c0 in take], dtype=np.uint64)
+        bl = np.array([t[2] for t in take], dtype=np.int64)
         arr = D.chunk_array(ptr, np.array([t[3] for t in take], np.uint64), np.array([t[4] for t in take], np.uint64),
                             self.cb.lengths[bl], self.cb.piece_lengths[bl], self.cb.sums_off[bl],
                             bl.astype(np.uint64))
@@ -752,8 +780,8 @@ class TailHandoffRun:
 
     def _release(self, take, ev):
         with self._cv:
-            for i, k, _, _, _ in take:
-                self._slot_crc[i][k] = ev
+            for t in take:
+                self._slot_crc[t[0]][t[1]] = ev
 
     def _wait_window(self, ev):
         """Until window event `ev` completes, keep the threads' rings full."""
@@ -788,8 +816,11 @@ class TailHandoffRun:
         self._busy_s = [0.0] * H
         self._done_bytes = [0] * H
         self._phase = [{"midstate": 0.0, "device": 0.0, "hash": 0.0} for _ in range(H)]
+        self._mwaits = [[] for _ in range(H)]  # (wait s, event already done, s since assignment)
+        self._t_assigned = {}
         self._tail_pieces = 0
         self._done = self._abort = False
+        self._win_done = -1  # the last window the loop has seen end
         self._alive = H
         dig = np.zeros((n, 32), dtype=np.uint8)
         err = []
@@ -816,7 +847,7 @@ class TailHandoffRun:
             evs.append(e)
             return e
 
-        takes, resumed, wait_win_s = 0, 0, 0.0
+        takes, resumed, early, wait_win_s = 0, 0, 0, 0.0
         scale = 1.0  # measured / modelled window time (EMA)
         gpu_end = 0.0
         wev = []  # the windows' events
@@ -835,7 +866,7 @@ class TailHandoffRun:
                 self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s,
                                     crc_after_sha=self.crc_after_sha)
                 take = self._flush_crcs(self.run_s)
-                D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.state_host.ptr), C.c_void_p(self.cb.state.ptr),
+                D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.state_host[k & 1].ptr), C.c_void_p(self.cb.state.ptr),
                                                    32 * n, self.run_s))
                 ev = new_event()
                 D.check(D.lib.krk_event_record(ev, self.run_s))
@@ -845,6 +876,9 @@ class TailHandoffRun:
                 if k:
                     tw = self._clock()
                     self._wait_window(wev[k - 1])
+                    with self._cv:
+                        self._win_done = k - 1
+                        self._cv.notify_all()
                     now = self._clock()
                     wait_win_s += now - tw
                     scale = 0.7 * scale + 0.3 * max(0.2, min(5.0, (now - t_prev_end) / max(last_model, 1e-6)))
@@ -856,17 +890,30 @@ class TailHandoffRun:
                 with self._cv:  # threads with at most their current chain, free before k+1 ends
                     ready = [i for i in range(H) if len(self._jobs[i]) <= 1 and self._free_at(i, now) <= horizon]
                     ready.sort(key=lambda i: self._free_at(i, now))
+                    before_k = {i: self._free_at(i, now) < end_k for i in ready}
                 chosen = pol.pick(len(ready), stream_rate(self.rates, blobs.size) * model)
                 with self._cv:
                     for i, b in zip(ready, chosen):
                         y = sched.drop(b)
                         if not self._jobs[i]:
                             self._t_last[i] = now
-                        self._assign(i, b, y, ev if y else None)
+                        if y and before_k[i]:
+                            # free before window k ends: start from the midstate window k-1 left
+                            # (done, mirrored, read now), hashing window k's chunk of b again on
+                            # the host; the window keeps that chunk's CRC, the thread's pieces
+                            # sum from y on
+                            j = np.flatnonzero(blobs == b)
+                            yp = int(offs[j[0]]) if j.size else y
+                            h0 = self.state_host[(k - 1) & 1].a[b].copy() if yp else _IV.copy()
+                            self._assign(i, b, yp, -1, h0=h0, crc_from=y)
+                            early += 1
+                        else:
+                            yp = y
+                            self._assign(i, b, y, k if y else -1)
                         host_blobs.add(b)
-                        host_bytes += int(self.lens[b]) - y
+                        host_bytes += int(self.lens[b]) - yp
                         takes += 1
-                        resumed += y > 0
+                        resumed += yp > 0
                     self._cv.notify_all()
                 self._service()
                 win = sched.next()
@@ -876,6 +923,9 @@ class TailHandoffRun:
                     self._gen(items)
             if wev:
                 self._wait_window(wev[-1])
+                with self._cv:
+                    self._win_done = len(wev) - 1
+                    self._cv.notify_all()
             gpu_end = self._clock() - t0
             with self._cv:
                 self._done = True
@@ -925,7 +975,8 @@ class TailHandoffRun:
             for e in evs:
                 D.lib.krk_event_destroy(e)
         self.stats = {"windows": len(wev), "gpu_windows_end_s": round(gpu_end, 3),
-                      "takeovers": takes, "resumed_from_midstate": resumed, "host_chains": len(host_blobs),
+                      "takeovers": takes, "resumed_from_midstate": resumed, "from_previous_window": early,
+                      "host_chains": len(host_blobs),
                       "host_bytes": host_bytes, "tail_pieces": self._tail_pieces,
                       "thread_busy_s": [round(x, 3) for x in self._busy_s],
                       "thread_GBps": [round(self._done_bytes[i] / max(self._busy_s[i], 1e-9) / 1e9, 3)
@@ -934,6 +985,7 @@ class TailHandoffRun:
                                           for k in ("midstate", "device", "hash", "copy_wait", "sha", "copy_issue",
                                                     "ready_wait")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3),
+                      "midstate_waits": _wait_summary([w for ws in self._mwaits for w in ws]),
                       **({"twin_copy_GBps_before_run": round(self.twin_GBps, 2)} if self.loop_copies else {})}
 
     def _items(self, win, k):

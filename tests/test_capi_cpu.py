@@ -815,7 +815,7 @@ def test_tail_ring_slot_held_until_its_crc_is_queued():
     r.gen_s = C.c_void_p()
     r.tbuf = [[Buf(0x1000), Buf(0x2000)]]
     r._cv = threading.Condition(threading.Lock())
-    r._to_gen = [[(0, o, 64) for o in range(0, 6 * 64, 64)]]
+    r._to_gen = [[(0, o, 64, 0) for o in range(0, 6 * 64, 64)]]
     r._ready, r._pending, r._tail_pieces = [[]], [], 0
     r._slot_used, r._slot_crc, r._next_slot = [[False, False]], [[None, None]], [0]
     assert len(r._service()) == 2  # both slots filled
