@@ -1451,8 +1451,7 @@ def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
     from kraken_amd.windowed import TAIL_PIECE, TAIL_RING
     tr = TailHandoffRun(D, ids, lens, P, W, threads, cap=cap if (a.no_admission or a.live_cap) else None,
                         device=a.device, piece=(a.tail_piece_mib << 20) if a.tail_piece_mib else TAIL_PIECE,
-                        ring=a.tail_ring or TAIL_RING, loop_copies=not a.tail_thread_copies,
-                        copy_streams=a.tail_copy_streams, crc_after_sha=not a.tail_crc_beside_sha)
+                        ring=a.tail_ring or TAIL_RING, crc_after_sha=not a.tail_crc_beside_sha)
     T.barrier()
     t0 = time.perf_counter()
     tr.run()
@@ -2306,12 +2305,8 @@ def main():
                          "bytes left at window boundaries), reported as tail_handoff beside the GPU-only value")
     ap.add_argument("--tail-threads", type=int, default=0, help="C3 tail handoff: host threads (0 = the CPU budget - 1)")
     ap.add_argument("--tail-ring", type=int, default=0, help="C3 tail handoff: device pieces a thread keeps in flight")
-    ap.add_argument("--tail-copy-streams", type=int, default=1, help="C3 tail handoff: the loop's copy streams")
     ap.add_argument("--tail-crc-beside-sha", action="store_true",
                     help="C3 tail handoff: each window's CRC launch beside its SHA launch (A/B; default after it)")
-    ap.add_argument("--tail-thread-copies", action="store_true",
-                    help="C3 tail handoff: each thread copies its pieces down itself (A/B; default: the window "
-                         "loop copies whole pieces on one stream)")
     ap.add_argument("--tail-piece-mib", type=int, default=0, help="C3 tail handoff: MiB a device piece")
     ap.add_argument("--c3-tail-only", action="store_true",
                     help="C3: skip the GPU-only windows (measurement runs of the tail handoff; no value line)")

@@ -514,20 +514,22 @@ class TailHandoffRun:
     threads steal chains at window boundaries (TailPolicy).  After run(): cb.sums / cb.digests
     hold every blob's piece sums and digest (device); `stats` the run's takeovers and timing.
 
-    Who does what.  The window loop (the calling thread) owns every device launch: the
+    Who does what.  The window loop (the calling thread) owns every device call: the
     windows, and the stolen chains' remaining bytes, generated piece by piece (64 MiB) into
-    each thread's ring of device slots on the window generator's stream as slots come free;
-    the pieces' CRCs are queued into the window stream after each window's step.  The host
-    threads only copy pieces down and hash them (krk_sha256_resume_dev_on_host), in order,
-    from the chain's midstate.  Queues: a packet that cannot start blocks every later packet
-    of its hardware queue, and normal-priority streams share four of them (GPU_MAX_HW_QUEUES;
-    16 or 32 measured slower, profiles/r06): so the windows' step and SHA-256 streams are high
-    priority, the CRC launches (144 KiB-LDS workgroups, which wait for CUs the window's SHA
-    workgroups leave room on) go only there, and the normal queues carry the threads' copies
-    and the generator's launches (no LDS, never blocked, waited for by the host)."""
+    each thread's ring of device slots on the window generator's stream as slots come free
+    and copied down, whole, on one copy stream into a pinned twin of the slot; the pieces'
+    CRCs are queued into the window stream after each window's step; each window's midstates
+    are mirrored to host memory.  The host threads only wait for their pieces' copies and hash
+    them (krk_sha256_resume_host), in order, from the chain's midstate.  Queues: a packet that
+    cannot start blocks every later packet of its hardware queue, and normal-priority streams
+    share four of them (GPU_MAX_HW_QUEUES; 16 or 32 measured slower, profiles/r06): so the
+    windows' step and SHA-256 streams are high priority, the CRC launches (144 KiB-LDS
+    workgroups, which wait for CUs the window's SHA workgroups leave room on) go only there,
+    and the normal queues carry the copies and the generator's launches (no LDS, never
+    blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
-                 ring=TAIL_RING, loop_copies=True, copy_streams=1, crc_after_sha=True):
+                 ring=TAIL_RING, crc_after_sha=True):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -551,44 +553,38 @@ class TailHandoffRun:
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.run_s)))
         D.check(D.lib.krk_stream_create(C.byref(self.gen_s)))
         D.check(D.lib.krk_stream_create_prio(-1, C.byref(self.sha_s)))
-        # loop_copies: the loop also copies each generated piece down (one stream, whole
-        # pieces) into a pinned twin of its slot, and the threads only hash host memory;
-        # otherwise each thread copies its pieces itself (8 MiB copies on a stream of its own)
-        # every window's midstates, copied down after its step on the window stream: a stolen
-        # chain's midstate is read here once the window's event is done (a synchronous copy
-        # would queue behind other streams' packets in a shared hardware queue)
-        self.state_host = [D.PinnedArray((n, 8), np.uint32, dma_target=True) for _ in range(2)]  # window k: k & 1
+        # every window's midstates, copied down after its step on the window stream (window k
+        # into mirror k & 1): a stolen chain's midstate is read there once the window is done
+        # (a synchronous copy would queue behind other streams' packets in a shared hardware
+        # queue)
+        self.state_host = [D.PinnedArray((n, 8), np.uint32, dma_target=True) for _ in range(2)]
         self.crc_after_sha = bool(crc_after_sha)  # False: a window's CRC beside its SHA launch (A/B)
-        self.loop_copies = bool(loop_copies)
-        self.copy_s = []
-        self.hbuf, self.slot_ev = [], []
-        if self.loop_copies:
-            for _ in range(max(1, int(copy_streams))):  # threads spread over them (i % count)
-                cs = C.c_void_p()
-                D.check(D.lib.krk_stream_create(C.byref(cs)))
-                self.copy_s.append(cs)
-            self.hbuf = [[D.PinnedArray((self.piece,), np.uint8, dma_target=True) for _ in range(self.ring)]
-                         for _ in range(self.H)]
-            for _ in range(self.H):
-                row = []
-                for _ in range(self.ring):
-                    e = C.c_void_p()
-                    D.check(D.lib.krk_event_create_polling(C.byref(e)))
-                    row.append(e)
-                self.slot_ev.append(row)
-            # every twin written once by DMA before the run (a page's first device write runs at
-            # about half the rate: 30 vs 56 GB/s measured), then the twins' copy rate, a record
-            # beside the run's copy waits
-            import time
-            for rep in range(2):
-                t0 = time.perf_counter()
-                for i in range(self.H):
-                    for k in range(self.ring):
-                        D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
-                                                           C.c_void_p(self.tbuf[i][k].ptr), self.piece,
-                                                           self.copy_s[0]))
-                D.check(D.lib.krk_stream_sync(self.copy_s[0]))
-                self.twin_GBps = self.H * self.ring * self.piece / (time.perf_counter() - t0) / 1e9
+        # the loop copies each generated piece down, whole, on one stream into a pinned twin of
+        # its slot (an event a slot); the threads only hash host memory
+        self.copy_s = C.c_void_p()
+        D.check(D.lib.krk_stream_create(C.byref(self.copy_s)))
+        self.hbuf = [[D.PinnedArray((self.piece,), np.uint8, dma_target=True) for _ in range(self.ring)]
+                     for _ in range(self.H)]
+        self.slot_ev = []
+        for _ in range(self.H):
+            row = []
+            for _ in range(self.ring):
+                e = C.c_void_p()
+                D.check(D.lib.krk_event_create_polling(C.byref(e)))
+                row.append(e)
+            self.slot_ev.append(row)
+        # every twin written once by DMA before the run (a page's first device write runs at
+        # about half the rate: 30 vs 56 GB/s measured), then the twins' copy rate, a record
+        # beside the run's copy waits
+        import time
+        for _ in range(2):
+            t0 = time.perf_counter()
+            for i in range(self.H):
+                for k in range(self.ring):
+                    D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
+                                                       C.c_void_p(self.tbuf[i][k].ptr), self.piece, self.copy_s))
+            D.check(D.lib.krk_stream_sync(self.copy_s))
+            self.twin_GBps = self.H * self.ring * self.piece / (time.perf_counter() - t0) / 1e9
         self.stats = {}
 
     # ---- the host threads: copy and hash
@@ -629,18 +625,12 @@ class TailHandoffRun:
                 k, pb, po, pm = self._ready[i].pop(0)
             assert pb == b and po == y + c * self.piece, (pb, po, b, y, c)
             t2 = clk()
-            if self.loop_copies:
-                if pm:
-                    D.check(D.lib.krk_event_sync(self.slot_ev[i][k]))  # the loop's copy of the piece
-                t2b = clk()
-                ph["copy_wait"] = ph.get("copy_wait", 0.0) + t2b - t2
-                D.check(D.lib.krk_sha256_resume_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
-                                                     C.c_void_p(self.hbuf[i][k].ptr), pm, int(c + 1 == nch),
-                                                     out.ctypes.data_as(C.POINTER(C.c_uint8))))
-            else:
-                D.check(D.lib.krk_sha256_resume_dev_on_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
-                                                            C.c_void_p(self.tbuf[i][k].ptr), pm, int(c + 1 == nch),
-                                                            out.ctypes.data_as(C.POINTER(C.c_uint8)), None))
+            if pm:
+                D.check(D.lib.krk_event_sync(self.slot_ev[i][k]))  # the loop's copy of the piece
+            ph["copy_wait"] += clk() - t2
+            D.check(D.lib.krk_sha256_resume_host(h.ctypes.data_as(C.POINTER(C.c_uint32)), po,
+                                                 C.c_void_p(self.hbuf[i][k].ptr), pm, int(c + 1 == nch),
+                                                 out.ctypes.data_as(C.POINTER(C.c_uint8))))
             t3 = clk()
             ph["device"] += t2 - t1
             ph["hash"] += t3 - t2
@@ -656,10 +646,9 @@ class TailHandoffRun:
         import time
         try:
             self.D.set_device(self.device)
-            w, hh, iss, rdy = C.c_double(), C.c_double(), C.c_double(), C.c_double()
+            w, hh = C.c_double(), C.c_double()
             self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
-            self.D.check(self.D.lib.krk_sha256_resume_stats2(C.byref(iss), C.byref(rdy)))
-            w0, h0, i0, r0 = w.value, hh.value, iss.value, rdy.value
+            h0 = hh.value  # this thread's SHA-NI seconds so far
             while True:
                 with self._cv:
                     while not self._jobs[i] and not self._done and not self._abort:
@@ -674,11 +663,7 @@ class TailHandoffRun:
                     self._busy_s[i] += time.perf_counter() - t0
                     self._cv.notify_all()
             self.D.check(self.D.lib.krk_sha256_resume_stats(C.byref(w), C.byref(hh)))
-            self.D.check(self.D.lib.krk_sha256_resume_stats2(C.byref(iss), C.byref(rdy)))
-            self._phase[i]["copy_wait"] = self._phase[i].get("copy_wait", 0.0) + w.value - w0
             self._phase[i]["sha"] = hh.value - h0
-            self._phase[i]["copy_issue"] = iss.value - i0
-            self._phase[i]["ready_wait"] = rdy.value - r0
         except BaseException as e:  # re-raised on the caller's thread
             err.append(e)
             with self._cv:
@@ -746,12 +731,10 @@ class TailHandoffRun:
             D.synth_fill_chunk_arrays(self.ids[bl], ptr, np.array([g[3] for g in live], np.uint64),
                                       np.array([g[4] for g in live], np.uint64), stream=self.gen_s)
             D.check(D.lib.krk_stream_sync(self.gen_s))
-            if self.loop_copies:  # each piece down into its slot's pinned twin, then its event
-                for i, k, _, _, m, _ in live:
-                    D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr),
-                                                       C.c_void_p(self.tbuf[i][k].ptr), m,
-                                                       self.copy_s[i % len(self.copy_s)]))
-                    D.check(D.lib.krk_event_record(self.slot_ev[i][k], self.copy_s[i % len(self.copy_s)]))
+            for i, k, _, _, m, _ in live:  # each piece down into its slot's pinned twin, then its event
+                D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr), C.c_void_p(self.tbuf[i][k].ptr),
+                                                   m, self.copy_s))
+                D.check(D.lib.krk_event_record(self.slot_ev[i][k], self.copy_s))
         with self._cv:
             for i, k, b, o, m, c0 in gen:
                 self._ready[i].append((k, b, o, m))
@@ -815,7 +798,7 @@ class TailHandoffRun:
         self._t_last = [0.0] * H
         self._busy_s = [0.0] * H
         self._done_bytes = [0] * H
-        self._phase = [{"midstate": 0.0, "device": 0.0, "hash": 0.0} for _ in range(H)]
+        self._phase = [{"midstate": 0.0, "device": 0.0, "hash": 0.0, "copy_wait": 0.0} for _ in range(H)]
         self._mwaits = [[] for _ in range(H)]  # (wait s, event already done, s since assignment)
         self._t_assigned = {}
         self._tail_pieces = 0
@@ -982,11 +965,10 @@ class TailHandoffRun:
                       "thread_GBps": [round(self._done_bytes[i] / max(self._busy_s[i], 1e-9) / 1e9, 3)
                                       for i in range(H)],
                       "thread_phases_s": {k: round(sum(p.get(k, 0.0) for p in self._phase), 3)
-                                          for k in ("midstate", "device", "hash", "copy_wait", "sha", "copy_issue",
-                                                    "ready_wait")},
+                                          for k in ("midstate", "device", "hash", "copy_wait", "sha")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3),
                       "midstate_waits": _wait_summary([w for ws in self._mwaits for w in ws]),
-                      **({"twin_copy_GBps_before_run": round(self.twin_GBps, 2)} if self.loop_copies else {})}
+                      "twin_copy_GBps_before_run": round(self.twin_GBps, 2)}
 
     def _items(self, win, k):
         blobs, offs, take = win
@@ -1001,18 +983,18 @@ class TailHandoffRun:
         self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
 
     def close(self):
-        for cs in self.copy_s:
-            self.D.lib.krk_stream_sync(cs)
+        if self.copy_s.value:
+            self.D.lib.krk_stream_sync(self.copy_s)
         for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
         self.bufs, self.tbuf, self.hbuf = [], [], []
         for e in [e for row in self.slot_ev for e in row]:
             self.D.lib.krk_event_destroy(e)
         self.slot_ev = []
-        for s in [self.gen_s, self.run_s, self.sha_s] + self.copy_s:
+        for s in [self.gen_s, self.run_s, self.sha_s, self.copy_s]:
             if s.value:
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s, self.run_s, self.sha_s, self.copy_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), []
+        self.gen_s, self.run_s, self.sha_s, self.copy_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
 
     def __del__(self):
         try:

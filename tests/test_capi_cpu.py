@@ -797,6 +797,12 @@ def test_tail_ring_slot_held_until_its_crc_is_queued():
         def krk_stream_sync(self, s):
             return 0
 
+        def krk_memcpy_d2h_async(self, dst, src, n, s):
+            return 0
+
+        def krk_event_record(self, ev, s):
+            return 0
+
     class FakeD:
         def __init__(self):
             self.lib = Lib()
@@ -810,7 +816,8 @@ def test_tail_ring_slot_held_until_its_crc_is_queued():
 
     D = FakeD()
     r = WN.TailHandoffRun.__new__(WN.TailHandoffRun)
-    r.D, r.H, r.ring, r.piece, r.loop_copies = D, 1, 2, 64, False
+    r.D, r.H, r.ring, r.piece = D, 1, 2, 64
+    r.hbuf, r.slot_ev, r.copy_s = [[Buf(0x9000), Buf(0xA000)]], [[C.c_void_p(1), C.c_void_p(2)]], C.c_void_p()
     r.ids = np.arange(4, dtype=np.uint64)
     r.gen_s = C.c_void_p()
     r.tbuf = [[Buf(0x1000), Buf(0x2000)]]

@@ -29,7 +29,6 @@ for step in "$@"; do
     c3) run bench_c3 900 python -u bench.py --workload c3 --tail-handoff ;;
     tail_sweep) for cfg in ${TAIL_SWEEP:-6x64 12x64 16x32}; do set -- ${cfg/x/ }
                     run c3_tail_r$1_p$2 200 $C3T --tail-ring $1 --tail-piece-mib $2; done ;;
-    c3w8_tail_ab) run c3_tail_loopcopy 200 $C3T && run c3_tail_threadcopy 200 $C3T --tail-thread-copies ;;
     tail_probe) run tail_probe 200 python -u tools/tail_probe.py 15 ;;
     prof_c3w8) run prof_c3w8 400 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d gpurun_out/prof_c3w8 -- python3 bench.py --workload c3 --emulate-world 8 --tail-handoff --no-e2e --no-cpu-baseline --no-ceiling ;;
