@@ -529,7 +529,7 @@ class TailHandoffRun:
     blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
-                 ring=TAIL_RING, crc_after_sha=True):
+                 ring=TAIL_RING, crc_after_sha=True, from_previous="auto"):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -559,6 +559,10 @@ class TailHandoffRun:
         # queue)
         self.state_host = [D.PinnedArray((n, 8), np.uint32, dma_target=True) for _ in range(2)]
         self.crc_after_sha = bool(crc_after_sha)  # False: a window's CRC beside its SHA launch (A/B)
+        # "auto": a thread predicted free before the queued window ends takes its chain from the
+        # previous window's midstate; "always" / "never": every takeover does / none does (tests)
+        assert from_previous in ("auto", "always", "never"), from_previous
+        self.from_previous = from_previous
         # the loop copies each generated piece down, whole, on one stream into a pinned twin of
         # its slot (an event a slot); the threads only hash host memory
         self.copy_s = C.c_void_p()
@@ -873,7 +877,8 @@ class TailHandoffRun:
                 with self._cv:  # threads with at most their current chain, free before k+1 ends
                     ready = [i for i in range(H) if len(self._jobs[i]) <= 1 and self._free_at(i, now) <= horizon]
                     ready.sort(key=lambda i: self._free_at(i, now))
-                    before_k = {i: self._free_at(i, now) < end_k for i in ready}
+                    before_k = {i: (self.from_previous == "always" or
+                                    (self.from_previous == "auto" and self._free_at(i, now) < end_k)) for i in ready}
                 chosen = pol.pick(len(ready), stream_rate(self.rates, blobs.size) * model)
                 with self._cv:
                     for i, b in zip(ready, chosen):

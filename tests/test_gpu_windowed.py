@@ -82,9 +82,10 @@ def test_window_plan_covers_c3_law_once():
     assert np.array_equal(pos, np.asarray(lens, dtype=np.uint64))
 
 
-@pytest.mark.parametrize("cap,threads,piece,ring", [(None, 3, 64 << 20, 8), (200, 4, 64 << 20, 8), (None, 5, 1 << 20, 8),
-                                                    (None, 5, 1 << 20, 2)])
-def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, piece, ring):
+@pytest.mark.parametrize("cap,threads,piece,ring,prev", [(None, 3, 64 << 20, 8, "auto"), (200, 4, 64 << 20, 8, "never"),
+                                                         (None, 5, 1 << 20, 8, "always"), (None, 5, 1 << 20, 2, "auto"),
+                                                         (200, 4, 64 << 20, 8, "always")])
+def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, piece, ring, prev):
     """the windowed batch with the tail handoff (windowed.TailHandoffRun):
     host threads start on the longest chains whole, then steal the chains with the most bytes
     left at window boundaries -- live chains from the midstate the windows left in HBM, and
@@ -93,11 +94,15 @@ def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, p
     takeovers.  piece=1 MiB: a thread's chain spans many device pieces, so its ring wraps
     inside one chain and one window's CRC flush carries several pieces of one blob; ring=2
     wraps inside one window wait, where a slot a thread has copied down may not be refilled
-    before its piece's CRC is queued (a round-6 failure: right digests, wrong sums).  Every
-    blob equals the one-shot device path; sampled blobs the oracle."""
+    before its piece's CRC is queued (a round-6 failure: right digests, wrong sums).
+    prev="always": every chain changes hands from the midstate the PREVIOUS window left, the
+    thread hashing the queued window's chunk again while the window keeps that chunk's CRC
+    (its pieces sum from the window's end on); "never": always from the queued window's.
+    Every blob equals the one-shot device path; sampled blobs the oracle."""
     from kraken_amd.windowed import TailHandoffRun
     lens, ids, dg1, sums1, offs1, counts1 = one_shot
-    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20, piece=piece, ring=ring)
+    tr = TailHandoffRun(D, ids, lens, P, 200 << 20, threads, cap=cap, max_chunk=1 << 20, piece=piece, ring=ring,
+                        from_previous=prev)
     tr.run()
     st = tr.stats
     cb = tr.cb
@@ -108,6 +113,10 @@ def test_tail_handoff_matches_one_shot_and_oracle(one_shot, orc, cap, threads, p
     assert st["takeovers"] > threads and st["resumed_from_midstate"] > 0 and st["windows"] > 50, st
     assert 0 < st["host_bytes"] < int(np.sum(lens)), st
     assert st["tail_pieces"] >= st["host_chains"], st
+    if prev == "never":
+        assert st["from_previous_window"] == 0, st
+    if prev == "always":
+        assert st["from_previous_window"] >= st["resumed_from_midstate"] > 0, st
     bad = [i for i in range(N) if bytes(dg[i]) != bytes(dg1[i])]
     assert not bad, (len(bad), bad[:10])
     for i in range(N):
