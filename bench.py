@@ -2088,6 +2088,19 @@ def files_cold_leg(a, D, T, rank, world, P):
         finally:
             os.environ.pop("KRK_LIVE_CAP", None)
             os.environ.pop("KRK_FILE_DIRECT", None)
+        # fewer live files read O_DIRECT: larger disk requests (a window holds one chunk of
+        # every live file; 512 MiB / live a chunk)
+        for cap in (a.cold_live_caps or []):
+            os.environ["KRK_LIVE_CAP"], os.environ["KRK_FILE_DIRECT"] = str(cap), "1"
+            try:
+                nm = f"gpu_only_live{cap}_direct"
+                s_x, d_x = leg(nm, lambda: D.metainfo_digest_files(paths, lens, P))
+                legs[nm]["max_live"] = D.windows_last_call()["max_live"]
+                legs[nm]["outputs_equal_gpu_only"] = bool(np.array_equal(d_x, d_g) and all(
+                    np.array_equal(x, y) for x, y in zip(s_x, s_g)))
+            finally:
+                os.environ.pop("KRK_LIVE_CAP", None)
+                os.environ.pop("KRK_FILE_DIRECT", None)
         rate, got = leg("disk_read", lambda: disk_read_rate(paths))
         # the first leg again, last (the first pass after writing the files runs slow on some
         # boxes): the order effect beside the paths' differences
@@ -2304,6 +2317,8 @@ def main():
                     help="C3: also run the batch with the tail handoff (host threads steal the chains with the most "
                          "bytes left at window boundaries), reported as tail_handoff beside the GPU-only value")
     ap.add_argument("--tail-threads", type=int, default=0, help="C3 tail handoff: host threads (0 = the CPU budget - 1)")
+    ap.add_argument("--cold-live-caps", type=int, nargs="*", default=None,
+                    help="files workload: extra cold legs read O_DIRECT with these live-file caps")
     ap.add_argument("--tail-ring", type=int, default=0, help="C3 tail handoff: device pieces a thread keeps in flight")
     ap.add_argument("--tail-crc-beside-sha", action="store_true",
                     help="C3 tail handoff: each window's CRC launch beside its SHA launch (A/B; default after it)")

@@ -586,6 +586,21 @@ uint64_t live_cap_for(Device* D) {
     return v ? v : window_stream_cap(D);
 }
 
+// A file batch read O_DIRECT (cold: bound by the disk) needs no more live files than it takes
+// the windows' SHA-256 streams to outrun the host link -- h2d over the eight-lane per-stream
+// rate, ~970 on MI355X, rounded up to 64: every live file beyond that only shrinks each
+// file's chunk of a window, and so the disk's requests.  Cold 32 GiB leg on one box
+// (profiles/r06/bench_files_live.json): 3,734 live 12.4 GB/s, 2,048 14.7, 1,024 15.2, 512
+// 15.2, 256 13.5 (the streams bind there), the reference's two reads 14.3.  KRK_LIVE_CAP wins.
+uint64_t direct_live_cap(Device* D) {
+    if (KRK_OP_ENV("KRK_LIVE_CAP")) return live_cap_for(D);
+    const Rates R = planner_rates(D);
+    const double per_stream = R.stream[0] > 0 ? R.stream[0] : 58e6;
+    const double link = R.h2d > 0 ? R.h2d : 56e9;
+    const uint64_t need = (uint64_t)(link / per_stream) + 1;
+    return std::min(live_cap_for(D), std::max<uint64_t>(256, (need + 63) / 64 * 64));
+}
+
 
 }  // namespace
 
@@ -931,7 +946,7 @@ int krk_metainfo_digest_files(const krk_file_blob* files, uint64_t n, uint32_t* 
     CallStats st;
     // at most as many live blobs as this call holds file descriptors (a lease of the
     // process's budget, shared with every other file batch running now)
-    FdLease fds(std::min<uint64_t>(live_cap_for(D), n));
+    FdLease fds(std::min<uint64_t>(direct ? direct_live_cap(D) : live_cap_for(D), n));
     r = windows_pass(D, n, lens.data(), plens.data(), soff.data(), on_host, filler, direct ? 4096 : 64, fds.n,
                      o.d_sums, o.d_dig, o.d_state, &st);
     st.resident = resident;
