@@ -68,6 +68,36 @@ def test_files_edge_lengths_match_oracle(gpu, orc, tmp_path, P, mode, monkeypatc
         assert st["direct_reads"], st
 
 
+def test_direct_batch_live_files_match_the_link(gpu, orc, tmp_path, monkeypatch):
+    """Round 6: a batch read O_DIRECT keeps at most as many files live as it takes the windows'
+    streams to outrun the host link (h2d / the eight-lane per-stream rate, rounded up to 64,
+    at least 256) -- larger disk requests for cold batches.  With injected rates (30 GB/s,
+    60 MB/s a stream) that is 512 of 1,300 files; KRK_LIVE_CAP still wins; every output equals
+    hashlib / the oracle."""
+    rng = np.random.default_rng(77)
+    lens = [int(x) for x in rng.integers(1, 40_000, 1300)]
+    src = orc.synth(4242, max(lens))
+    paths = [_write(tmp_path, f"d{i}", src[:L]) for i, L in enumerate(lens)]
+    monkeypatch.setenv("KRK_FILE_DIRECT", "1")
+    D.set_planner_rates(dict(D.planner_rates(), h2d_bps=30e9, sha_stream_bps=[60e6, 50e6, 35e6]))
+    try:
+        D.set_sha_host_offload(0)
+        sums, dg = D.metainfo_digest_files(paths, lens, 1 << 14)
+        st = D.windows_last_call()
+        monkeypatch.setenv("KRK_LIVE_CAP", "700")
+        sums2, dg2 = D.metainfo_digest_files(paths, lens, 1 << 14)
+        st2 = D.windows_last_call()
+    finally:
+        D.set_planner_rates(None)
+    assert st["direct_reads"] and st["max_live"] == 512, st
+    assert st2["max_live"] == 700, st2
+    for i in range(0, len(lens), 37):
+        d = src[:lens[i]]
+        assert bytes(dg[i]) == hashlib.sha256(d.tobytes()).digest(), i
+        assert np.array_equal(sums[i], orc.calc_piece_sums(d, 1 << 14)[1]), i
+    assert np.array_equal(dg2, dg) and all(np.array_equal(a, b) for a, b in zip(sums, sums2))
+
+
 def test_files_cold_batch_stays_on_windows_under_auto(gpu, orc, tmp_path):
     """The batch's page-cache residency is sampled (mmap + mincore): files out of the cache are
     disk-bound wherever they are hashed, so AUTO sends none to host threads and reads them
