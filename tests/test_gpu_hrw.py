@@ -165,6 +165,56 @@ def test_ring_owner_tables_cached_by_membership(gpu, orc):
                 assert locs[i, : counts[i]].tolist() == want, (rep, N, R, i)
 
 
+def test_ring_owner_tables_concurrent_callers_with_evictions(gpu):
+    """ADVICE r05 (owner-table slots): eight threads place digests over twelve memberships at
+    once (more than the eight tables a device keeps), so tables are built, used and evicted
+    while other callers' launches still read theirs.  A table in use is never evicted and a
+    failed or replaced build never moves another caller's slot: every thread's owner lists
+    equal the serial run's for that membership, every time."""
+    import threading
+    rng = np.random.default_rng(0xC0C5)
+    n = 8192
+    digests = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    dbuf = D.DeviceBuffer(n * 32)
+    dbuf.from_host(digests.reshape(-1))
+    rings = []
+    for k in range(12):
+        N = [3, 5, 16, 64][k % 4]
+        labels = [f"origin-{i:03d}.kraken.test:{16002 + k}" for i in range(N)]
+        rings.append((labels, (rng.random(N) < 0.8).astype(np.uint8), 2 + k % 2))
+    want = []
+    lb, cb = D.DeviceBuffer(n * 3), D.DeviceBuffer(n)
+    for labels, healthy, R in rings:  # serial
+        D.ring_locations_u8_dev(dbuf, n, labels, healthy, R, lb, cb)
+        D.synchronize()
+        want.append((lb.to_host(np.uint8, n * R).copy(), cb.to_host(np.uint8, n).copy()))
+    errors = []
+
+    def caller(t):
+        try:
+            D.set_device(0)
+            r = np.random.default_rng(t)
+            mlb, mcb = D.DeviceBuffer(n * 3), D.DeviceBuffer(n)
+            for _ in range(30):
+                k = int(r.integers(0, len(rings)))
+                labels, healthy, R = rings[k]
+                D.ring_locations_u8_dev(dbuf, n, labels, healthy, R, mlb, mcb)
+                D.synchronize()
+                got = (mlb.to_host(np.uint8, n * R), mcb.to_host(np.uint8, n))
+                if not (np.array_equal(got[0], want[k][0]) and np.array_equal(got[1], want[k][1])):
+                    errors.append((t, k))
+        except Exception as e:  # surfaced below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=caller, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th)
+    assert not errors, errors[:5]
+
+
 def test_cas_volume_placement(gpu, orc, tmp_path):
     """lib/store/ca_store.go:137-171: weighted HRW over volumes for subdirs "%02X"."""
     from kraken_amd import castore
