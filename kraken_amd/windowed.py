@@ -358,6 +358,7 @@ TAIL_CHUNK = 4 << 20
 # next chain's midstate ends waits for it (all of that time lost).
 TAIL_HORIZON = 2.5
 TAIL_RING = 8  # device slots a tail thread's pieces cycle through (generated / hashed / waiting for their CRC)
+TAIL_FIRST_PIECE = 8 << 20  # a stolen chain's first piece (a multiple of 64)
 
 
 def tail_thread_rate(rates, threads):
@@ -600,7 +601,8 @@ class TailHandoffRun:
         y == 0."""
         D = self.D
         L = int(self.lens[b])
-        nch = max(1, -(-(L - y) // self.piece))
+        pieces = self._pieces(y, L)
+        nch = len(pieces)
         ph = self._phase[i]
         clk = self._clock
         h = _IV.copy()
@@ -627,7 +629,7 @@ class TailHandoffRun:
                 if self._abort:
                     return
                 k, pb, po, pm = self._ready[i].pop(0)
-            assert pb == b and po == y + c * self.piece, (pb, po, b, y, c)
+            assert pb == b and (po, pm) == pieces[c], (pb, po, pm, b, y, c)
             t2 = clk()
             if pm:
                 D.check(D.lib.krk_event_sync(self.slot_ev[i][k]))  # the loop's copy of the piece
@@ -695,10 +697,22 @@ class TailHandoffRun:
         self._t_assigned[(i, b)] = self._clock()
         L = int(self.lens[b])
         cf = y if crc_from is None else int(crc_from)
-        for o in range(y, max(L, y + 1), self.piece):
-            m = min(self.piece, L - o)
+        # the first piece small (a thread starts hashing after one short copy, not behind a
+        # burst of whole-piece copies at a window boundary), the rest whole pieces
+        for o, m in self._pieces(y, L):
             self._to_gen[i].append((b, o, m, min(m, max(0, cf - o))))
         self._left[i] += L - y
+
+    def _pieces(self, y, L):
+        """A chain's bytes [y, L) as the pieces its thread hashes: a short first one, then
+        whole pieces; one empty piece when y == L."""
+        out, o = [], y
+        while True:
+            m = min(TAIL_FIRST_PIECE if o == y else self.piece, self.piece, L - o)
+            out.append((o, m))
+            o += m
+            if o >= L:
+                return out
 
     def _service(self):
         """Every free ring slot (copied down, its CRC queued and done) refilled with its thread's next
