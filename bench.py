@@ -1464,7 +1464,7 @@ def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
     from kraken_amd.windowed import TAIL_PIECE, TAIL_RING
     tr = TailHandoffRun(D, ids, lens, P, W, threads, cap=cap if (a.no_admission or a.live_cap) else None,
                         device=a.device, piece=(a.tail_piece_mib << 20) if a.tail_piece_mib else TAIL_PIECE,
-                        ring=a.tail_ring or TAIL_RING, crc_after_sha=not a.tail_crc_beside_sha)
+                        ring=a.tail_ring or TAIL_RING, crc_after_sha=False if a.tail_crc_beside_sha else None)
     T.barrier()
     t0 = time.perf_counter()
     tr.run()
@@ -2334,7 +2334,8 @@ def main():
                     help="files workload: extra cold legs read O_DIRECT with these live-file caps")
     ap.add_argument("--tail-ring", type=int, default=0, help="C3 tail handoff: device pieces a thread keeps in flight")
     ap.add_argument("--tail-crc-beside-sha", action="store_true",
-                    help="C3 tail handoff: each window's CRC launch beside its SHA launch (A/B; default after it)")
+                    help="C3 tail handoff: each window's CRC launch beside its SHA launch (A/B; default: beside "
+                         "only when the windows are full)")
     ap.add_argument("--tail-piece-mib", type=int, default=0, help="C3 tail handoff: MiB a device piece")
     ap.add_argument("--c3-tail-only", action="store_true",
                     help="C3: skip the GPU-only windows (measurement runs of the tail handoff; no value line)")

@@ -530,7 +530,7 @@ class TailHandoffRun:
     blocked, waited for by the host)."""
 
     def __init__(self, D, ids, lens, P, W, threads, cap=None, device=0, max_chunk=TAIL_CHUNK, piece=TAIL_PIECE,
-                 ring=TAIL_RING, crc_after_sha=True, from_previous="auto"):
+                 ring=TAIL_RING, crc_after_sha=None, from_previous="auto"):
         self.D = D
         self.ids = np.asarray(ids, dtype=np.uint64)
         self.lens = np.asarray(lens, dtype=np.int64)
@@ -559,7 +559,13 @@ class TailHandoffRun:
         # (a synchronous copy would queue behind other streams' packets in a shared hardware
         # queue)
         self.state_host = [D.PinnedArray((n, 8), np.uint32, dma_target=True) for _ in range(2)]
-        self.crc_after_sha = bool(crc_after_sha)  # False: a window's CRC beside its SHA launch (A/B)
+        # a window's CRC after its SHA launch, or beside it when the windows are full (every
+        # stream the cap allows live: throughput-bound windows, where a serialised CRC costs
+        # ~13 %; measured beside / after: 1 GPU 537 / 503, 2 GPUs 615 / 586-613, 4 GPUs
+        # 720-740 / 746-762, 8 GPUs 946 / 933-954 GB/s, profiles/r06/c3_tail_crc_placement_ab.jsonl)
+        if crc_after_sha is None:
+            crc_after_sha = min(self.cap, n) < window_stream_cap(D, 1 << 62)  # the device's cap
+        self.crc_after_sha = bool(crc_after_sha)
         # "auto": a thread predicted free before the queued window ends takes its chain from the
         # previous window's midstate; "always" / "never": every takeover does / none does (tests)
         assert from_previous in ("auto", "always", "never"), from_previous
@@ -568,6 +574,17 @@ class TailHandoffRun:
         # its slot (an event a slot); the threads only hash host memory
         self.copy_s = C.c_void_p()
         D.check(D.lib.krk_stream_create(C.byref(self.copy_s)))
+        # the stolen chains' pieces are generated on a stream of their own (the loop waits for
+        # them), the windows' bytes on gen_s behind an event the loop polls while it keeps the
+        # threads' rings full (a blocking wait there left the rings unserviced for most of each
+        # window: 10.5 of 12.5 s on the 8-GPU shard, 19.2 of 21.7 at N=1)
+        self.piece_s = C.c_void_p()
+        D.check(D.lib.krk_stream_create(C.byref(self.piece_s)))
+        self.gen_ev = []
+        for _ in range(2):
+            e = C.c_void_p()
+            D.check(D.lib.krk_event_create_polling(C.byref(e)))
+            self.gen_ev.append(e)
         self.hbuf = [[D.PinnedArray((self.piece,), np.uint8, dma_target=True) for _ in range(self.ring)]
                      for _ in range(self.H)]
         self.slot_ev = []
@@ -746,9 +763,11 @@ class TailHandoffRun:
         if live:
             ptr = np.array([self.tbuf[i][k].ptr for i, k, _, _, _, _ in live], dtype=np.uint64)
             bl = np.array([g[2] for g in live], dtype=np.int64)
+            tg = self._clock()
             D.synth_fill_chunk_arrays(self.ids[bl], ptr, np.array([g[3] for g in live], np.uint64),
-                                      np.array([g[4] for g in live], np.uint64), stream=self.gen_s)
-            D.check(D.lib.krk_stream_sync(self.gen_s))
+                                      np.array([g[4] for g in live], np.uint64), stream=self.piece_s)
+            D.check(D.lib.krk_stream_sync(self.piece_s))
+            self._gen_wait[0] += self._clock() - tg
             for i, k, _, _, m, _ in live:  # each piece down into its slot's pinned twin, then its event
                 D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(self.hbuf[i][k].ptr), C.c_void_p(self.tbuf[i][k].ptr),
                                                    m, self.copy_s))
@@ -820,6 +839,7 @@ class TailHandoffRun:
         self._mwaits = [[] for _ in range(H)]  # (wait s, event already done, s since assignment)
         self._t_assigned = {}
         self._tail_pieces = 0
+        self._gen_wait = [0.0, 0.0]  # the loop's seconds generating: tail pieces, windows
         self._done = self._abort = False
         self._win_done = -1  # the last window the loop has seen end
         self._alive = H
@@ -858,11 +878,14 @@ class TailHandoffRun:
             k = 0
             items = self._items(win, 0) if win is not None else None
             if items is not None:
-                self._gen(items)
+                self._gen(items, 0)
             t_prev_end = self._clock()
             last_model = 1.0
             while win is not None and not err:
                 blobs, offs, tk = win
+                tg = self._clock()
+                self._wait_window(self.gen_ev[k & 1])  # window k's bytes
+                self._gen_wait[1] += self._clock() - tg
                 pol.queued(blobs, offs, tk)
                 self.cb.step_arrays(items[0], items[1], items[2], items[3], stream=self.run_s, sha_stream=self.sha_s,
                                     crc_after_sha=self.crc_after_sha)
@@ -922,7 +945,7 @@ class TailHandoffRun:
                 k += 1
                 if win is not None:
                     items = self._items(win, k)
-                    self._gen(items)
+                    self._gen(items, k)
             if wev:
                 self._wait_window(wev[-1])
                 with self._cv:
@@ -987,7 +1010,9 @@ class TailHandoffRun:
                                           for k in ("midstate", "device", "hash", "copy_wait", "sha")},
                       "loop_wait_s": round(wait_win_s, 3), "window_time_scale": round(scale, 3),
                       "midstate_waits": _wait_summary([w for ws in self._mwaits for w in ws]),
-                      "twin_copy_GBps_before_run": round(self.twin_GBps, 2)}
+                      "twin_copy_GBps_before_run": round(self.twin_GBps, 2), "crc_after_sha": self.crc_after_sha,
+                      "loop_generate_s": {"tail_pieces": round(self._gen_wait[0], 3),
+                                          "windows": round(self._gen_wait[1], 3)}}
 
     def _items(self, win, k):
         blobs, offs, take = win
@@ -996,24 +1021,31 @@ class TailHandoffRun:
         dev += np.uint64(self.bufs[k & 1].ptr)
         return blobs, dev, offs, take
 
-    def _gen(self, items):
+    def _gen(self, items, k):
+        """Window k's bytes generated on gen_s; gen_ev[k & 1] marks them done."""
         blobs, dev, offs, take = items
         self.D.synth_fill_chunk_arrays(self.ids[blobs], dev, offs, take, stream=self.gen_s)
-        self.D.check(self.D.lib.krk_stream_sync(self.gen_s))
+        self.D.check(self.D.lib.krk_event_record(self.gen_ev[k & 1], self.gen_s))
 
     def close(self):
-        if self.copy_s.value:
-            self.D.lib.krk_stream_sync(self.copy_s)
+        for s in [self.gen_s, self.run_s, self.sha_s, self.copy_s, self.piece_s]:  # nothing in flight
+            if s.value:
+                self.D.lib.krk_stream_sync(s)
         for b in self.bufs + [x for ring in self.tbuf for x in ring]:
             b.free()
         self.bufs, self.tbuf, self.hbuf = [], [], []
         for e in [e for row in self.slot_ev for e in row]:
             self.D.lib.krk_event_destroy(e)
         self.slot_ev = []
-        for s in [self.gen_s, self.run_s, self.sha_s, self.copy_s]:
+        for s in [self.gen_s, self.run_s, self.sha_s, self.copy_s, self.piece_s]:
             if s.value:
+                self.D.lib.krk_stream_sync(s)
                 self.D.lib.krk_stream_destroy(s)
-        self.gen_s, self.run_s, self.sha_s, self.copy_s = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        for e in self.gen_ev:
+            self.D.lib.krk_event_destroy(e)
+        self.gen_ev = []
+        self.gen_s, self.run_s, self.sha_s, self.copy_s, self.piece_s = (C.c_void_p(), C.c_void_p(), C.c_void_p(),
+                                                                          C.c_void_p(), C.c_void_p())
 
     def __del__(self):
         try:

@@ -816,8 +816,10 @@ def test_tail_ring_slot_held_until_its_crc_is_queued():
 
     D = FakeD()
     r = WN.TailHandoffRun.__new__(WN.TailHandoffRun)
-    r.D, r.H, r.ring, r.piece = D, 1, 2, 64
+    import time
+    r.D, r.H, r.ring, r.piece, r._clock, r._gen_wait = D, 1, 2, 64, time.perf_counter, [0.0, 0.0]
     r.hbuf, r.slot_ev, r.copy_s = [[Buf(0x9000), Buf(0xA000)]], [[C.c_void_p(1), C.c_void_p(2)]], C.c_void_p()
+    r.piece_s = C.c_void_p()
     r.ids = np.arange(4, dtype=np.uint64)
     r.gen_s = C.c_void_p()
     r.tbuf = [[Buf(0x1000), Buf(0x2000)]]
