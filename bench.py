@@ -1385,6 +1385,36 @@ def run_chunked(a, D, T, rank, world, res):
         res["end_to_end"] = c3_end_to_end(D, T, world, rank)
 
 
+_SETTLE = {}
+
+
+def settle_dma(D, max_s=15.0):
+    """Wait until device-to-host copies run at the calibrated rate again before a leg starts.
+    After a leg frees tens of GB of device memory, D2H copies run at half rate (30.3 against
+    56.5 GB/s) for ~4 s and then jump back (profiles/r06/d2h_after_lane_timeline.json) -- the
+    copy engines busy with something of the driver's after the free; a leg that started
+    inside that window lost 7-20 % (c3_w8_leg_order.jsonl).  Returns the seconds waited."""
+    import ctypes as C
+    if not _SETTLE:
+        _SETTLE["src"] = D.DeviceBuffer(64 << 20)
+        _SETTLE["dst"] = [D.PinnedArray((64 << 20,), np.uint8) for _ in range(4)]
+        s = C.c_void_p()
+        D.check(D.lib.krk_stream_create(C.byref(s)))
+        _SETTLE["s"] = s
+    want = 0.85 * D.planner_rates()["d2h_bps"]
+    t0 = time.perf_counter()
+    while True:
+        t1 = time.perf_counter()
+        for b in _SETTLE["dst"]:
+            D.check(D.lib.krk_memcpy_d2h_async(C.c_void_p(b.ptr), C.c_void_p(_SETTLE["src"].ptr), 64 << 20,
+                                               _SETTLE["s"]))
+        D.check(D.lib.krk_stream_sync(_SETTLE["s"]))
+        r = 4 * (64 << 20) / (time.perf_counter() - t1)
+        if r >= want or time.perf_counter() - t0 > max_s:
+            return round(time.perf_counter() - t0, 3)
+        time.sleep(0.1)
+
+
 def run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums):
     """C3 with the host lane (kraken_amd.windowed): the K longest blobs of the shard are
     generated into a device buffer of their own, their piece CRCs run on the GPU and their
@@ -1411,6 +1441,7 @@ def run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums):
         return out
     wr = WindowedRun(D, ids, lens, P, W, cap=cap if (a.no_admission or a.live_cap) else None,
                      host_lane=(k, threads), device=a.device)
+    out["settle_s"] = settle_dma(D)
     T.barrier()
     t0 = time.perf_counter()
     wr.run()
@@ -1465,6 +1496,7 @@ def run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums):
     tr = TailHandoffRun(D, ids, lens, P, W, threads, cap=cap if (a.no_admission or a.live_cap) else None,
                         device=a.device, piece=(a.tail_piece_mib << 20) if a.tail_piece_mib else TAIL_PIECE,
                         ring=a.tail_ring or TAIL_RING, crc_after_sha=False if a.tail_crc_beside_sha else None)
+    out["settle_s"] = settle_dma(D)
     T.barrier()
     t0 = time.perf_counter()
     tr.run()
