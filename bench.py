@@ -1374,13 +1374,14 @@ def run_chunked(a, D, T, rank, world, res):
             ok = ok and np.array_equal(sums[o:o + cnt], rs[ro:ro + cnt])
         res["spot_check_matches_one_shot"] = bool(ok)
     wr.close()
-    # the tail handoff before the host lane: after the lane's leg (its host threads' pinned
-    # double buffers and copy streams) the handoff's piece copies wait 16-26 s instead of 1-6
-    # (profiles/r06/c3_w8_leg_order.jsonl; the cause is not isolated)
-    if a.tail_handoff:
-        res["tail_handoff"] = run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums)
+    # the host lane before the tail handoff: the lane loses 15-35 % when it runs second in a
+    # process (cause not isolated, profiles/r06/c3_w8_leg_order.jsonl); the handoff lost its
+    # 7-20 % second only to the copy engines' half-rate window after the lane freed its
+    # memory, which settle_dma now waits out
     if a.host_lane:
         res["host_offload"] = run_host_lane(a, D, T, ids, lens, P, total_bytes, dg, sums)
+    if a.tail_handoff:
+        res["tail_handoff"] = run_tail_handoff(a, D, T, ids, lens, P, total_bytes, dg, sums)
     if not a.no_e2e:
         res["end_to_end"] = c3_end_to_end(D, T, world, rank)
 
