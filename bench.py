@@ -80,7 +80,7 @@ def load_valu(workload):
     (tools/pmc_valu.py -> profiles/r03/valu_<workload>.json); the raw counters stay in
     that file, the derived fractions go into the bench line."""
     d, path = None, None
-    for rnd in ("r05", "r04", "r03", "r02"):  # the newest round's passes
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):  # the newest round's passes
         path = os.path.join(ROOT, "profiles", rnd, f"valu_{workload}.json")
         try:
             d = json.load(open(path))
@@ -398,10 +398,11 @@ def sha_roofline(a, D, n, lens, gbps, avg_ms, bytes_launch, traffic, launch):
 
 def load_traffic(path, workload, n):
     """Per-launch HBM bytes from the PMC passes (tools/pmc_traffic.py): `path` if given, else
-    the newest of profiles/r05 and r04/pmc_traffic_<workload>.json, profiles/pmc_traffic_<workload>.json
+    the newest of profiles/r06, r05 and r04/pmc_traffic_<workload>.json, profiles/pmc_traffic_<workload>.json
     and (C2) profiles/pmc_traffic.json -- the first whose workload and blob count match."""
     cands = [path] if path else []
-    cands += [os.path.join(ROOT, "profiles", "r05", f"pmc_traffic_{workload}.json"),
+    cands += [os.path.join(ROOT, "profiles", "r06", f"pmc_traffic_{workload}.json"),
+              os.path.join(ROOT, "profiles", "r05", f"pmc_traffic_{workload}.json"),
               os.path.join(ROOT, "profiles", "r04", f"pmc_traffic_{workload}.json"),
               os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json"),
               os.path.join(ROOT, "profiles", "pmc_traffic.json")]

@@ -60,7 +60,21 @@ for step in "$@"; do
     bench_c1) run bench_c1 300 python -u bench.py --workload c1 --steps 2 --warmup 1 ;;
     bench_defaults) run bench_defaults 300 python -u bench.py --workload defaults ;;
     prof_c2) run prof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv \
-                  -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline ;;
+                  -d gpurun_out/prof_c2 -- python3 bench.py --no-e2e --no-cpu-baseline --no-offload ;;
+    # final-tree PMC of the production kernels (tools/pmc_traffic.py, pmc_valu.py), each pass its own run
+    pmc_c2 | pmc_c4 | pmc_e2e)
+        case $step in
+        pmc_e2e) B="python3 bench.py --e2e-only --no-cpu-baseline" ;;
+        pmc_c2) B="python3 bench.py --steps 1 --warmup 0 --no-e2e --no-cpu-baseline --no-ceiling --no-offload" ;;
+        pmc_c4) B="python3 bench.py --workload c4 --steps 3 --warmup 1 --no-e2e --no-cpu-baseline" ;;
+        esac
+        X=${step#pmc_}
+        run pmc_${X}_valu 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+            SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS --output-format csv -d gpurun_out/pmc_${X}_valu -- $B
+        run pmc_${X}_wait 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d gpurun_out/pmc_${X}_wait -- $B
+        run pmc_${X}_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_${X}_fetch -- $B
+        run pmc_${X}_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_${X}_write -- $B ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -60,17 +60,22 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--blobs", type=int, default=1000)
     ap.add_argument("--algorithmic-bytes", type=float, default=1000 * 104857600.0)
+    ap.add_argument("--pick", default="median", choices=["median", "max"],
+                    help="a kernel's dispatches: the median, or the largest (the workload's own launch "
+                         "when the run has shorter ones of the same kernel)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                    "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     fetch = read_counter(a.fetch, "FETCH_SIZE")
     write = read_counter(a.write, "WRITE_SIZE")
     res = {"workload": a.workload, "blobs": a.blobs, "algorithmic_bytes_per_launch": a.algorithmic_bytes,
+           "dispatch": a.pick,
            "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
            "bytes_per_launch": {}, "raw": {}}
     for k in sorted(set(fetch) | set(write)):
-        f = statistics.median(fetch[k]) if fetch.get(k) else 0.0
-        w = statistics.median(write[k]) if write.get(k) else 0.0
+        agg = max if a.pick == "max" else statistics.median
+        f = agg(fetch[k]) if fetch.get(k) else 0.0
+        w = agg(write[k]) if write.get(k) else 0.0
         b = 2 * f * 1024 + w * 1024
         res["bytes_per_launch"][k] = b
         res["raw"][k] = {"FETCH_SIZE_KiB_median": f, "WRITE_SIZE_KiB_median": w,

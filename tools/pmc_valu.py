@@ -43,23 +43,38 @@ def _short(name):
     return None
 
 
-def read_dir(d):
-    """({kernel: {counter: total}}, {kernel: [dispatches, total ns]})"""
-    ctr = defaultdict(lambda: defaultdict(float))
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                k = _short(row.get("Kernel_Name", ""))
-                if k:
-                    ctr[k][row["Counter_Name"]] += float(row["Counter_Value"])
-    tim = defaultdict(lambda: [0, 0])
+def read_dir(d, longest=False):
+    """({kernel: {counter: total}}, {kernel: [dispatches, total ns]}); longest: only each
+    kernel's longest dispatch (the workload's own launch when the run has shorter ones of the
+    same kernel: calibration, a host-offload leg's prefixes)."""
+    dur = {}  # dispatch id -> (kernel, ns)
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = _short(row.get("Kernel_Name", ""))
                 if k:
-                    tim[k][0] += 1
-                    tim[k][1] += int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                    dur[row.get("Dispatch_Id") or row.get("Correlation_Id")] = (
+                        k, int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    keep = None
+    if longest:
+        best = {}
+        for did, (k, ns) in dur.items():
+            if k not in best or ns > best[k][1]:
+                best[k] = (did, ns)
+        keep = {did for did, _ in best.values()}
+    ctr = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = _short(row.get("Kernel_Name", ""))
+                did = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                if k and (keep is None or did in keep):
+                    ctr[k][row["Counter_Name"]] += float(row["Counter_Value"])
+    tim = defaultdict(lambda: [0, 0])
+    for did, (k, ns) in dur.items():
+        if keep is None or did in keep:
+            tim[k][0] += 1
+            tim[k][1] += ns
     return ctr, tim
 
 
@@ -90,13 +105,14 @@ def main():
     ap.add_argument("--mode", default="device_resident", choices=["device_resident", "end_to_end"])
     ap.add_argument("--what", default="")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--longest", action="store_true", help="only each kernel's longest dispatch")
     a = ap.parse_args()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = a.out or os.path.join(root, "profiles", "r02", f"valu_{a.workload}.json")
     ctr = defaultdict(dict)
     tim = {}
     for d in a.dirs:
-        c, t = read_dir(d)
+        c, t = read_dir(d, a.longest)
         for k, v in c.items():
             ctr[k].update(v)
         for k, v in t.items():
