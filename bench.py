@@ -1286,12 +1286,15 @@ def run_chunked(a, D, T, rank, world, res):
     # share nothing, so a W-GPU run takes as long as its slowest shard; rank 0 holds the
     # longest blob, whose chain bounds every shard).
     shard_world = a.emulate_world or world
-    ids, lens, P = workload_blobs(a.workload, rank, shard_world, a.blobs)
+    shard_rank = rank if a.emulate_rank is None else a.emulate_rank  # --emulate-rank: another rank's shard
+    assert 0 <= shard_rank < shard_world, (shard_rank, shard_world)
+    ids, lens, P = workload_blobs(a.workload, shard_rank, shard_world, a.blobs)
     n = len(lens)
     if a.c3_tail_only:  # a measurement run of the tail handoff alone (no value line)
         res.update({"metric": "C3 tail handoff only (measurement run)", "value": None, "unit": "GB/s",
                     "config": {"workload": WORKLOADS["c3"]["desc"], "blobs_this_rank": n,
-                               "emulated_world": shard_world}})
+                               "emulated_world": shard_world, "emulated_rank": shard_rank,
+                               "longest_blob": int(max(lens))}})
         res["tail_handoff"] = run_tail_handoff(a, D, T, ids, lens, P, int(sum(c3_lengths(a.blobs or 20000))),
                                                None, None)
         return
@@ -1319,9 +1322,11 @@ def run_chunked(a, D, T, rank, world, res):
                            "windows": len(wr.wins), "window_bytes": wr.W, "live_cap": int(wr.cap), "piece_length": P,
                            "longest_blob": max(lens), "parallelism": f"LPT blob shard x{shard_world}, no collective",
                            **({"emulated_world": shard_world,
-                               "emulation": f"rank {rank}'s shard of a {shard_world}-GPU run on one GPU; value = all "
-                                            f"{shard_world} shards' bytes / this shard's time (it holds the longest "
-                                            f"blob)"} if a.emulate_world else {})},
+                               "emulated_rank": shard_rank,
+                               "emulation": f"rank {shard_rank}'s shard of a {shard_world}-GPU run on one GPU; value = "
+                                            f"all {shard_world} shards' bytes / this shard's time"
+                                            + (" (it holds the longest blob)" if shard_rank == 0 else "")}
+                             if a.emulate_world else {})},
                 "kernels": {"sha256_multi": {"launches": sha_n, "total_ms": round(sha_ms, 1)},
                             "crc32_pieces": {"launches": crc_n, "total_ms": round(crc_ms, 1)},
                             "synth_fill": {"launches": gen_n, "total_ms": round(gen_ms, 1)}},
@@ -2354,6 +2359,9 @@ def main():
     ap.add_argument("--live-cap", type=int, default=0, help="C3: live streams per window (0 = the planner's)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="C3: run rank 0's LPT shard of an N-GPU run on this GPU (no collective exists to emulate)")
+    ap.add_argument("--emulate-rank", type=int, default=None,
+                    help="C3 with --emulate-world: run this rank's shard instead of rank 0's (every shard in turn "
+                         "gives the emulated job's max over ranks)")
     ap.add_argument("--no-admission", action="store_true",
                     help="C3: all blobs live from window 0 (no longest-first admission under the two-lane cap)")
     ap.add_argument("--host-lane", action="store_true",
